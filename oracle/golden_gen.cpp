@@ -1,0 +1,263 @@
+// golden_gen.cpp -- TEST INFRASTRUCTURE.  Runs the synthetic workload (tonk_amd/csrc/workload.h)
+// against the REFERENCE codec compiled from /root/reference (oracle/_ref/libsiamese_ref.so) and
+//   * writes the per-stream transcript (tests/golden fixtures), or
+//   * times the reference CPU path over many streams on host threads (bench.py cpu_baseline).
+//
+// Only siamese.h API calls are made; nothing of the reference is copied.  Every recovered
+// packet is also checked against the true payload so a fixture can never pin a wrong decode.
+//
+// usage: golden_gen transcript <out.txt> key=value...
+//        golden_gen time threads=T streams=S key=value...
+#include "siamese.h"
+
+#include "../tonk_amd/csrc/workload.h"
+#include "transcript.h"
+
+#include <chrono>
+#include <thread>
+#include <atomic>
+#include <memory>
+#include <stdlib.h>
+#include <string.h>
+
+using namespace tamd::wl;
+
+struct RefBackend {
+    struct RecRef { std::vector<uint8_t> bytes; };
+    struct DecRef { std::vector<std::vector<uint8_t>> data; };
+
+    const Params& p;
+    SiameseEncoder enc = nullptr;
+    SiameseDecoder dec = nullptr;
+    std::vector<uint8_t> payloads;   // all payloads, pregenerated (index * stride)
+    std::vector<uint32_t> lens;
+    uint32_t stride = 0;
+    uint64_t bad_recoveries = 0;
+
+    explicit RefBackend(const Params& prm) : p(prm) {
+        enc = siamese_encoder_create();
+        dec = siamese_decoder_create();
+        stride = prm.payload_max;
+        payloads.resize((size_t)stride * prm.n_originals);
+        lens.resize(prm.n_originals);
+        for (uint32_t i = 0; i < prm.n_originals; ++i) {
+            lens[i] = payload_length(prm, i);
+            payload_bytes(prm, i, payloads.data() + (size_t)i * stride, lens[i]);
+        }
+    }
+    ~RefBackend() {
+        siamese_encoder_free(enc);
+        siamese_decoder_free(dec);
+    }
+    const uint8_t* pay(uint32_t i) const { return payloads.data() + (size_t)i * stride; }
+
+    int enc_add(uint32_t index, uint32_t len, uint32_t* col) {
+        SiameseOriginalPacket o;
+        o.PacketNum = 0;
+        o.Data = pay(index);
+        o.DataBytes = len;
+        const int rc = siamese_encoder_add(enc, &o);
+        *col = o.PacketNum;
+        return rc;
+    }
+    int enc_encode(RecRef& r) {
+        SiameseRecoveryPacket rp;
+        rp.Data = nullptr;
+        rp.DataBytes = 0;
+        const int rc = siamese_encode(enc, &rp);
+        if (rc == 0) r.bytes.assign(rp.Data, rp.Data + rp.DataBytes);
+        return rc;
+    }
+    int enc_ack(const uint8_t* buf, uint32_t n, uint32_t* next) {
+        return siamese_encoder_ack(enc, buf, n, next);
+    }
+    int dec_add_original(uint32_t col, uint32_t index, uint32_t len) {
+        SiameseOriginalPacket o;
+        o.PacketNum = col;
+        o.Data = pay(index);
+        o.DataBytes = len;
+        return siamese_decoder_add_original(dec, &o);
+    }
+    int dec_add_recovery(const RecRef& r) {
+        SiameseRecoveryPacket rp;
+        rp.Data = r.bytes.data();
+        rp.DataBytes = (unsigned)r.bytes.size();
+        return siamese_decoder_add_recovery(dec, &rp);
+    }
+    int dec_is_ready() { return siamese_decoder_is_ready(dec); }
+    int dec_decode(std::vector<uint32_t>& nums, DecRef& out) {
+        SiameseOriginalPacket* pk = nullptr;
+        unsigned count = 0;
+        const int rc = siamese_decode(dec, &pk, &count);
+        if (rc == 0) {
+            for (unsigned k = 0; k < count; ++k) {
+                nums.push_back(pk[k].PacketNum);
+                out.data.emplace_back(pk[k].Data, pk[k].Data + pk[k].DataBytes);
+                const uint32_t idx = pk[k].PacketNum;
+                if (idx >= p.n_originals || lens[idx] != pk[k].DataBytes ||
+                    memcmp(pay(idx), pk[k].Data, pk[k].DataBytes) != 0)
+                    ++bad_recoveries;
+            }
+        }
+        return rc;
+    }
+    int dec_ack(uint8_t* buf, uint32_t limit, uint32_t* used) {
+        return siamese_decoder_ack(dec, buf, limit, used);
+    }
+    void stats(uint64_t e[9], uint64_t d[11]) {
+        siamese_encoder_stats(enc, e, 9);
+        siamese_decoder_stats(dec, d, 11);
+    }
+};
+
+struct RefTranscript {
+    TextSink t;
+    bool enabled = true;
+    void on_encode(int rc, const RefBackend::RecRef& r) {
+        if (!enabled) return;
+        if (rc != 0) { t.put("E %d\n", rc); return; }
+        RecoveryMetadataView m;
+        decode_footer(r.bytes, m);
+        t.put("E 0 %zu %u %u %u %u %016llx\n", r.bytes.size(), m.row, m.cs, m.sc, m.ldpc,
+              (unsigned long long)fnv1a(r.bytes.data(), r.bytes.size()));
+    }
+    void on_decode(int rc, const std::vector<uint32_t>& nums, const RefBackend::DecRef& d) {
+        if (!enabled) return;
+        t.put("D %d %zu", rc, nums.size());
+        for (size_t k = 0; k < nums.size(); ++k)
+            t.put(" %u:%zu:%016llx", nums[k], d.data[k].size(),
+                  (unsigned long long)fnv1a(d.data[k].data(), d.data[k].size()));
+        t.put("\n");
+    }
+    void on_ack(int rd, const uint8_t* buf, uint32_t used, int re, uint32_t next) {
+        if (!enabled) return;
+        t.put("K %d %u %016llx %d %u\n", rd, used, (unsigned long long)fnv1a(buf, used), re, next);
+    }
+    void on_event(char kind, int rc, uint32_t a, uint32_t b) {
+        if (!enabled) return;
+        if (rc != 0) t.put("%c %d %u %u\n", kind, rc, a, b);
+    }
+    void on_stats(const uint64_t e[9], const uint64_t d[11]) {
+        if (enabled) fmt_stats(t, e, d);
+    }
+
+    struct RecoveryMetadataView { unsigned row = 0, cs = 0, sc = 0, ldpc = 0; };
+    // Footer parse (SiameseSerializers.h:759-800), restated for transcript labelling only.
+    static void decode_footer(const std::vector<uint8_t>& b, RecoveryMetadataView& m) {
+        size_t n = b.size();
+        auto cnt = [&](unsigned& v) {
+            const uint8_t x = b[n - 1];
+            if ((x & 0x80) == 0) { v = x; n -= 1; }
+            else { v = (((unsigned)x << 8) | b[n - 2]) & 0x7fff; n -= 2; }
+        };
+        auto pnum = [&](unsigned& v) {
+            const uint8_t x = b[n - 1];
+            const unsigned k = x >> 6;
+            if (k <= 1) { v = x; n -= 1; }
+            else if (k == 2) { v = (((unsigned)x << 8) | b[n - 2]) & 0x3fff; n -= 2; }
+            else { v = (((unsigned)x << 16) | ((unsigned)b[n - 2] << 8) | b[n - 3]) & 0x3fffff; n -= 3; }
+        };
+        cnt(m.sc); m.sc += 1;
+        pnum(m.cs);
+        if (m.sc <= 1) { m.ldpc = 1; m.row = 0; }
+        else { cnt(m.ldpc); m.row = b[n - 1]; }
+    }
+};
+
+static bool parse_kv(Params& p, int& threads, int& streams, const char* kv) {
+    const char* eq = strchr(kv, '=');
+    if (!eq) return false;
+    std::string k(kv, eq - kv);
+    const unsigned long long v = strtoull(eq + 1, nullptr, 0);
+    if (k == "stream") p.stream_id = (uint32_t)v;
+    else if (k == "n") p.n_originals = (uint32_t)v;
+    else if (k == "pmin") p.payload_min = (uint32_t)v;
+    else if (k == "pmax") p.payload_max = (uint32_t)v;
+    else if (k == "loss") p.loss_thresh = (uint32_t)v;
+    else if (k == "ge") p.ge_enable = (uint32_t)v;
+    else if (k == "gb") p.gb_thresh = (uint32_t)v;
+    else if (k == "bg") p.bg_thresh = (uint32_t)v;
+    else if (k == "lossrec") p.loss_on_recovery = (uint32_t)v;
+    else if (k == "fec") p.fec_rate_q16 = (uint32_t)v;
+    else if (k == "ack") p.ack_every = (uint32_t)v;
+    else if (k == "ackbytes") p.ack_bytes = (uint32_t)v;
+    else if (k == "arq") p.arq_lag = (uint32_t)v;
+    else if (k == "flush") p.flush_max = (uint32_t)v;
+    else if (k == "seed_data") p.seed_data = v;
+    else if (k == "seed_loss") p.seed_loss = v;
+    else if (k == "threads") threads = (int)v;
+    else if (k == "streams") streams = (int)v;
+    else return false;
+    return true;
+}
+
+int main(int argc, char** argv) {
+    if (argc < 2) {
+        fprintf(stderr, "usage: %s transcript <out> k=v... | time k=v...\n", argv[0]);
+        return 2;
+    }
+    if (siamese_init() != 0) { fprintf(stderr, "siamese_init failed\n"); return 3; }
+    Params base;
+    int threads = 1, streams = 1;
+    const bool timing = strcmp(argv[1], "time") == 0;
+    const int first_kv = timing ? 2 : 3;
+    for (int i = first_kv; i < argc; ++i) {
+        if (!parse_kv(base, threads, streams, argv[i])) { fprintf(stderr, "bad arg %s\n", argv[i]); return 2; }
+    }
+
+    if (!timing) {
+        RefBackend be(base);
+        RefTranscript tr;
+        Summary s = run_stream(base, be, tr);
+        FILE* f = fopen(argv[2], "wb");
+        if (!f) return 4;
+        fwrite(tr.t.text.data(), 1, tr.t.text.size(), f);
+        fprintf(f, "Z originals=%llu lost=%llu recoveries=%llu lostrec=%llu recovered=%llu arq=%llu "
+                   "acks=%llu decodes=%llu flush=%llu missing=%llu bad=%llu\n",
+                (unsigned long long)s.originals, (unsigned long long)s.lost_originals,
+                (unsigned long long)s.recoveries, (unsigned long long)s.lost_recoveries,
+                (unsigned long long)s.recovered, (unsigned long long)s.arq_redelivered,
+                (unsigned long long)s.acks, (unsigned long long)s.decode_calls,
+                (unsigned long long)s.flush_encodes, (unsigned long long)s.missing_at_end,
+                (unsigned long long)be.bad_recoveries);
+        fclose(f);
+        return be.bad_recoveries ? 5 : 0;
+    }
+
+    // Timing: `streams` independent streams (stream id s uses seeds 1000+s / 2000+s) spread
+    // over `threads` host threads; payload generation happens before the clock starts.
+    std::atomic<int> next{0};
+    std::atomic<unsigned long long> bytes{0}, bad{0};
+    std::vector<std::thread> pool;
+    std::vector<std::unique_ptr<RefBackend>> bes(streams);
+    std::vector<Params> ps(streams, base);
+    for (int s = 0; s < streams; ++s) {
+        ps[s].stream_id = base.stream_id + s;
+        ps[s].seed_data = 1000 + ps[s].stream_id;
+        ps[s].seed_loss = 2000 + ps[s].stream_id;
+        bes[s].reset(new RefBackend(ps[s]));
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int t = 0; t < threads; ++t) {
+        pool.emplace_back([&]() {
+            for (;;) {
+                const int s = next++;
+                if (s >= streams) break;
+                RefTranscript tr;
+                tr.enabled = false;
+                run_stream(ps[s], *bes[s], tr);
+                unsigned long long b = 0;
+                for (uint32_t i = 0; i < ps[s].n_originals; ++i) b += bes[s]->lens[i];
+                bytes += b;
+                bad += bes[s]->bad_recoveries;
+            }
+        });
+    }
+    for (auto& th : pool) th.join();
+    const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    printf("{\"seconds\": %.6f, \"payload_bytes\": %llu, \"gib_per_s\": %.6f, \"threads\": %d, "
+           "\"streams\": %d, \"bad\": %llu}\n",
+           sec, (unsigned long long)bytes.load(), bytes.load() / sec / (1024.0 * 1024 * 1024),
+           threads, streams, (unsigned long long)bad.load());
+    return bad.load() ? 5 : 0;
+}

@@ -1,0 +1,282 @@
+// cp_harness.cpp -- TEST ONLY.  Drives the MI355X engine's host control plane (encoder.cpp,
+// decoder.cpp, engine.cpp) through the synthetic workload with NO GPU: the device programs the
+// control plane emits are executed by the oracle's CPU interpreter (oracle/siamese_oracle.c)
+// over a host copy of the arena, and the run writes the same transcript as
+// oracle/golden_gen.cpp does for the reference codec.  Used by tests/test_control_plane.py to
+// pin the control plane (every decision and every recovery/recovered byte) on CPU-only hosts.
+//
+// usage: cp_harness <out.txt> mode=sync|batch batch=K key=value...
+#include "../../tonk_amd/csrc/encoder.h"
+#include "../../tonk_amd/csrc/decoder.h"
+#include "../../tonk_amd/csrc/workload.h"
+#include "../../oracle/transcript.h"
+#include "../../oracle/siamese_oracle.h"
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <string>
+
+using namespace tamd;
+using namespace tamd::wl;
+
+static uint64_t g_arena_bytes = 512ull << 20;
+
+struct Harness {
+    Params p;
+    Context ctx;
+    std::vector<uint8_t> arena;
+    Encoder* enc = nullptr;
+    Decoder* dec = nullptr;
+    uint32_t row_bytes = 0;
+    bool sync = true;
+    uint32_t batch = 0;
+    TextSink out;
+    uint64_t programs = 0, ops = 0, levels = 0, instrs = 0;
+    std::string error;
+
+    // transcript entries waiting for their rows to be computed
+    struct PendEnc { RowId row; uint32_t total; RecoveryMeta meta; size_t pos; };
+    struct PendDec { RowId row; uint32_t upper; size_t pos; };
+    std::vector<PendEnc> pend_enc;
+    std::vector<std::vector<PendDec>> pend_dec;  // per decode line
+    std::vector<size_t> pend_dec_pos;
+    std::vector<std::string> lines;  // transcript lines, some filled after execution
+
+    explicit Harness(const Params& prm) : p(prm) {
+        row_bytes = ((p.payload_max + 4 + 8 + 63) / 64) * 64;
+        ctx.rows.init(g_arena_bytes);
+        arena.assign(g_arena_bytes, 0);
+        enc = new Encoder(&ctx, row_bytes);
+        dec = new Decoder(&ctx, row_bytes);
+    }
+    ~Harness() {
+        delete enc;
+        delete dec;
+    }
+
+    uint8_t* at(RowId r) { return arena.data() + (size_t)ctx.rows.offset(r) * TAMD_ROW_UNIT; }
+
+    RowId write_original(uint32_t index, uint32_t len, uint32_t* framed, uint32_t* header) {
+        uint8_t hdr[4];
+        const uint32_t hb = put_length_header(len, hdr);
+        const RowId r = ctx.alloc(hb + len);
+        if (r == kNoRow) return r;
+        uint8_t* d = at(r);
+        memset(d, 0, ctx.rows.cap_bytes(r));
+        memcpy(d, hdr, hb);
+        payload_bytes(p, index, d + hb, len);
+        *framed = hb + len;
+        *header = hb;
+        return r;
+    }
+
+    void flush() {
+        ctx.prepare_flush();
+        const auto& ops_v = ctx.pb.ops();
+        const auto& lv = ctx.pb.op_levels();
+        const uint32_t maxl = ctx.pb.max_level();
+        std::vector<uint32_t> sorted;
+        sorted.reserve(ops_v.size() * 4);
+        for (uint32_t l = 1; l <= maxl; ++l)
+            for (size_t i = 0; i < ops_v.size(); ++i)
+                if (lv[i] == l) {
+                    const tamd_op& o = ops_v[i];
+                    sorted.push_back(o.first); sorted.push_back(o.count);
+                    sorted.push_back(o.span); sorted.push_back(o.tag);
+                }
+        if (!ops_v.empty()) {
+            const int rc = oracle_run_program(arena.data(), arena.size(), sorted.data(),
+                                              (unsigned)(sorted.size() / 4),
+                                              (const uint32_t*)ctx.pb.instrs().data(),
+                                              (unsigned)ctx.pb.instrs().size());
+            if (rc != 0 && error.empty()) error = "oracle_run_program failed rc=" + std::to_string(rc);
+            ++programs;
+            ops += ops_v.size();
+            instrs += ctx.pb.instrs().size();
+            levels += maxl;
+        }
+        resolve();
+        const uint64_t done = ctx.epoch;
+        ctx.finish_flush();
+        ctx.rows.release_up_to(done);
+    }
+
+    void resolve() {
+        char buf[256];
+        for (const PendEnc& e : pend_enc) {
+            const uint8_t* d = at(e.row);
+            snprintf(buf, sizeof(buf), "E 0 %u %u %u %u %u %016llx", e.total, e.meta.Row, e.meta.ColumnStart,
+                     e.meta.SumCount, e.meta.LDPCCount, (unsigned long long)fnv1a(d, e.total));
+            lines[e.pos] = buf;
+        }
+        pend_enc.clear();
+        for (size_t k = 0; k < pend_dec.size(); ++k) {
+            std::string& ln = lines[pend_dec_pos[k]];
+            for (const PendDec& dd : pend_dec[k]) {
+                const uint8_t* d = at(dd.row);
+                unsigned len = 0;
+                const int hb = get_length_header(d, dd.upper, len);
+                uint32_t packet = 0;
+                if (hb < 1 || len + hb > dd.upper) { if (error.empty()) error = "bad recovered header"; continue; }
+                (void)packet;
+                snprintf(buf, sizeof(buf), ":%u:%016llx", len, (unsigned long long)fnv1a(d + hb, len));
+                // placeholder "#" marks where the length/hash go
+                const size_t at_pos = ln.find('#');
+                if (at_pos != std::string::npos) ln.replace(at_pos, 1, buf);
+            }
+        }
+        pend_dec.clear();
+        pend_dec_pos.clear();
+    }
+
+    // ---- backend interface for run_stream ----
+    struct RecRef { RecoveryOut out; };
+    struct DecRef { };
+
+    int enc_add(uint32_t index, uint32_t len, uint32_t* col) {
+        uint32_t framed = 0, header = 0;
+        const RowId r = write_original(index, len, &framed, &header);
+        if (r == kNoRow) { error = "arena full"; return 5; }
+        const Result rc = enc->add(r, framed, header, len, nullptr, col);
+        if (rc != kSuccess) ctx.rows.free_deferred(r);
+        if (batch && (index + 1) % batch == 0) flush();
+        return rc;
+    }
+    int enc_encode(RecRef& r) {
+        if (undelivered != kNoRow) ctx.rows.free_deferred(undelivered);  // it was lost
+        const Result rc = enc->encode(r.out);
+        undelivered = rc == kSuccess ? r.out.row : kNoRow;
+        return rc;
+    }
+    int enc_ack(const uint8_t* buf, uint32_t n, uint32_t* next) { return enc->acknowledge(buf, n, next); }
+    int dec_add_original(uint32_t col, uint32_t index, uint32_t len) {
+        uint32_t framed = 0, header = 0;
+        const RowId r = write_original(index, len, &framed, &header);
+        if (r == kNoRow) { error = "arena full"; return 5; }
+        bool took = false;
+        const Result rc = dec->add_original(col, r, framed, header, len, nullptr, &took);
+        if (!took) ctx.rows.free_deferred(r);
+        return rc;
+    }
+    RowId undelivered = kNoRow;  // last encoder output not (yet) handed to the decoder
+
+    int dec_add_recovery(const RecRef& r) {
+        bool took = false;
+        // Footer parsing reads only the footer bytes at the end of the packet, which the
+        // encoder produced on the host; the data bytes in front of it are not needed.
+        uint8_t tail[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        const uint32_t tl = r.out.total() < 8 ? r.out.total() : 8;
+        memcpy(tail + tl - r.out.footer_len, r.out.footer, r.out.footer_len);
+        undelivered = kNoRow;
+        const Result rc = dec->add_recovery(r.out.row, r.out.total(), tail, nullptr, &took);
+        if (!took) ctx.rows.free_deferred(r.out.row);
+        return rc;
+    }
+    int dec_is_ready() { return dec->is_ready(); }
+    int dec_decode(std::vector<uint32_t>& nums, DecRef&) {
+        std::vector<RecoveredPacket*> got;
+        const Result rc = dec->decode(got);
+        if (rc == kSuccess) {
+            pend_dec.emplace_back();
+            for (RecoveredPacket* rp : got) {
+                nums.push_back(rp->packet_num);
+                pend_dec.back().push_back(PendDec{rp->row, rp->framed_upper, 0});
+            }
+        }
+        return rc;
+    }
+    int dec_ack(uint8_t* buf, uint32_t limit, uint32_t* used) { return dec->ack(buf, limit, used); }
+    void stats(uint64_t e[9], uint64_t d[11]) { enc->stats(e, 9); dec->stats(d, 11); }
+
+    // ---- transcript interface ----
+    void on_encode(int rc, const RecRef& r) {
+        if (rc != 0) { lines.push_back("E " + std::to_string(rc)); return; }
+        pend_enc.push_back(PendEnc{r.out.row, r.out.total(), r.out.meta, lines.size()});
+        lines.push_back("E ?");
+        if (sync) flush();
+    }
+    void on_decode(int rc, const std::vector<uint32_t>& nums, const DecRef&) {
+        std::string ln = "D " + std::to_string(rc) + " " + std::to_string(nums.size());
+        for (uint32_t n : nums) ln += " " + std::to_string(n) + "#";
+        if (rc == 0) pend_dec_pos.push_back(lines.size());
+        lines.push_back(ln);
+        if (sync) flush();
+    }
+    void on_ack(int rd, const uint8_t* buf, uint32_t used, int re, uint32_t next) {
+        char b[128];
+        snprintf(b, sizeof(b), "K %d %u %016llx %d %u", rd, used, (unsigned long long)fnv1a(buf, used), re, next);
+        lines.push_back(b);
+    }
+    void on_event(char kind, int rc, uint32_t a, uint32_t b) {
+        if (rc == 0) return;
+        char t[64];
+        snprintf(t, sizeof(t), "%c %d %u %u", kind, rc, a, b);
+        lines.push_back(t);
+    }
+    void on_stats(const uint64_t e[9], const uint64_t d[11]) {
+        flush();
+        TextSink t;
+        fmt_stats(t, e, d);
+        std::string s = t.text;
+        if (!s.empty() && s.back() == '\n') s.pop_back();
+        lines.push_back(s);
+    }
+};
+
+int main(int argc, char** argv) {
+    if (argc < 2) { fprintf(stderr, "usage: cp_harness <out> k=v...\n"); return 2; }
+    if (!gf_init()) { fprintf(stderr, "gf_init failed\n"); return 3; }
+    if (oracle_self_test() != 0) { fprintf(stderr, "oracle self test failed\n"); return 3; }
+    Params p;
+    bool sync = true;
+    uint32_t batch = 0;
+    for (int i = 2; i < argc; ++i) {
+        const char* eq = strchr(argv[i], '=');
+        if (!eq) return 2;
+        std::string k(argv[i], eq - argv[i]);
+        const char* vs = eq + 1;
+        const unsigned long long v = strtoull(vs, nullptr, 0);
+        if (k == "mode") sync = strcmp(vs, "sync") == 0;
+        else if (k == "batch") batch = (uint32_t)v;
+        else if (k == "arena_mb") g_arena_bytes = v << 20;
+        else if (k == "n") p.n_originals = (uint32_t)v;
+        else if (k == "pmin") p.payload_min = (uint32_t)v;
+        else if (k == "pmax") p.payload_max = (uint32_t)v;
+        else if (k == "loss") p.loss_thresh = (uint32_t)v;
+        else if (k == "ge") p.ge_enable = (uint32_t)v;
+        else if (k == "gb") p.gb_thresh = (uint32_t)v;
+        else if (k == "bg") p.bg_thresh = (uint32_t)v;
+        else if (k == "lossrec") p.loss_on_recovery = (uint32_t)v;
+        else if (k == "fec") p.fec_rate_q16 = (uint32_t)v;
+        else if (k == "ack") p.ack_every = (uint32_t)v;
+        else if (k == "ackbytes") p.ack_bytes = (uint32_t)v;
+        else if (k == "arq") p.arq_lag = (uint32_t)v;
+        else if (k == "flush") p.flush_max = (uint32_t)v;
+        else if (k == "seed_data") p.seed_data = v;
+        else if (k == "seed_loss") p.seed_loss = v;
+        else if (k == "stream") p.stream_id = (uint32_t)v;
+        else { fprintf(stderr, "bad key %s\n", k.c_str()); return 2; }
+    }
+    Harness h(p);
+    h.sync = sync;
+    h.batch = sync ? 0 : (batch ? batch : 1u << 30);
+    Summary s = run_stream(p, h, h);
+    h.flush();
+    FILE* f = fopen(argv[1], "wb");
+    if (!f) return 4;
+    for (const std::string& l : h.lines) fprintf(f, "%s\n", l.c_str());
+    fprintf(f, "Z originals=%llu lost=%llu recoveries=%llu lostrec=%llu recovered=%llu arq=%llu "
+               "acks=%llu decodes=%llu flush=%llu missing=%llu bad=0\n",
+            (unsigned long long)s.originals, (unsigned long long)s.lost_originals,
+            (unsigned long long)s.recoveries, (unsigned long long)s.lost_recoveries,
+            (unsigned long long)s.recovered, (unsigned long long)s.arq_redelivered,
+            (unsigned long long)s.acks, (unsigned long long)s.decode_calls,
+            (unsigned long long)s.flush_encodes, (unsigned long long)s.missing_at_end);
+    fclose(f);
+    fprintf(stderr, "programs=%llu ops=%llu instrs=%llu levels=%llu live_rows=%zu\n",
+            (unsigned long long)h.programs, (unsigned long long)h.ops, (unsigned long long)h.instrs,
+            (unsigned long long)h.levels, h.ctx.rows.live_rows());
+    if (!h.error.empty()) { fprintf(stderr, "error: %s\n", h.error.c_str()); return 6; }
+    return 0;
+}

@@ -1,0 +1,1103 @@
+// decoder.cpp -- Siamese decoder control plane.  Each function names the reference routine it
+// restates (SiameseDecoder.cpp line numbers); byte work becomes symbolic terms (engine.h).
+#include "decoder.h"
+
+#include <string.h>
+
+namespace tamd {
+
+static inline uint32_t popcount64(uint64_t x) { return (uint32_t)__builtin_popcountll(x); }
+
+// CustomBitSet<64> helpers (PacketAllocator.h:243-346)
+static inline uint32_t bits_popcount(uint64_t w, uint32_t start, uint32_t end) {
+    if (start >= end) return 0;
+    const uint32_t n = end - start;
+    const uint64_t mask = n >= 64 ? ~0ull : ((1ull << n) - 1);
+    return popcount64((w >> start) & mask);
+}
+static inline uint32_t bits_first_clear(uint64_t w, uint32_t start) {
+    const uint64_t v = (~w) >> start;
+    if (start >= 64 || v == 0) return 64;
+    return start + (uint32_t)__builtin_ctzll(v);
+}
+static inline uint32_t bits_first_set(uint64_t w, uint32_t start) {
+    const uint64_t v = w >> start;
+    if (start >= 64 || v == 0) return 64;
+    return start + (uint32_t)__builtin_ctzll(v);
+}
+
+Decoder::Decoder(Context* ctx, uint32_t row_bytes, HostRelease release, void* user)
+    : ctx_(ctx), row_bytes_(row_bytes), release_(release), user_(user) {
+    ctx_->attach(this);
+}
+
+Decoder::~Decoder() {
+    for (Subwindow* s : subs_) {
+        for (unsigned i = 0; i < kSubwindow; ++i) drop_original(s->orig[i]);
+        delete s;
+    }
+    subs_.clear();
+    Recovery* r = head_;
+    while (r) { Recovery* n = r->next; free_recovery(r); r = n; }
+    for (Recovery* g : graveyard_) delete g;
+    graveyard_.clear();
+    for (unsigned l = 0; l < kLanes; ++l)
+        for (unsigned s = 0; s < kSums; ++s) lanes_[l][s].chain.release(ctx_->rows);
+    for (RecoveredPacket& p : recovered_) if (p.host && release_) { release_(p.host, user_); p.host = nullptr; }
+    ctx_->detach(this);
+}
+
+void Decoder::pre_flush() {
+    for (unsigned l = 0; l < kLanes; ++l)
+        for (unsigned s = 0; s < kSums; ++s) lanes_[l][s].chain.flush(ctx_->rows, ctx_->pb, ctx_->ex, row_bytes_);
+}
+
+void Decoder::drop_original(StoredOriginal& o) {
+    if (o.row != kNoRow) ctx_->rows.free_deferred(o.row);
+    if (o.host && release_) release_(o.host, user_);
+    o = StoredOriginal();
+}
+
+void Decoder::free_recovery(Recovery* r) {
+    if (r->row != kNoRow) ctx_->rows.free_deferred(r->row);
+    r->row = kNoRow;
+    graveyard_.push_back(r);
+}
+
+void Decoder::read_original(const StoredOriginal& o, uint32_t len, uint8_t coef, Sym& out) const {
+    ctx_->ex.append(ctx_->rows, o.row, len, coef, out);
+}
+
+// ============================================================================================
+// Window (SiameseDecoder.cpp:1260-1536)
+// ============================================================================================
+
+// DecoderPacketWindow::MarkGotColumn (:1260-1277)
+bool Decoder::mark_got(uint32_t column) {
+    const uint32_t e = to_element(column);
+    if (invalid_element(e)) { disabled_ = true; return false; }
+    Subwindow* s = subs_[e / kSubwindow];
+    s->got_count++;
+    s->got |= 1ull << (e % kSubwindow);
+    return e == next_expected_;
+}
+
+// RangeLostPackets (:1279-1323)
+uint32_t Decoder::range_lost(uint32_t start, uint32_t end) {
+    if (start >= end) return 0;
+    uint32_t lost = 0;
+    uint32_t sub = start / kSubwindow;
+    const uint32_t bit = start % kSubwindow;
+    if (bit > 0) {
+        uint32_t bit_end = bit + end - start;
+        if (bit_end > kSubwindow) bit_end = kSubwindow;
+        lost += (bit_end - bit) - bits_popcount(subs_[sub]->got, bit, bit_end);
+        ++sub;
+    }
+    const uint32_t sub_end = end / kSubwindow;
+    for (uint32_t i = sub; i < sub_end; ++i) lost += kSubwindow - subs_[i]->got_count;
+    if (sub_end >= sub) {
+        const uint32_t last_bits = end - sub_end * kSubwindow;
+        if (last_bits > 0) lost += last_bits - bits_popcount(subs_[sub_end]->got, 0, last_bits);
+    }
+    return lost;
+}
+
+// FindNextLostElement (:1325-1370)
+uint32_t Decoder::find_next_lost(uint32_t start) {
+    if (start >= count_) return count_;
+    const uint32_t sub_end = (count_ + kSubwindow - 1) / kSubwindow;
+    uint32_t sub = start / kSubwindow, bit = start % kSubwindow;
+    while (sub < sub_end) {
+        if (subs_[sub]->got_count < kSubwindow) {
+            bit = bits_first_clear(subs_[sub]->got, bit);
+            if (bit < kSubwindow) {
+                uint32_t e = sub * kSubwindow + bit;
+                if (e > count_) e = count_;
+                return e;
+            }
+        }
+        bit = 0;
+        ++sub;
+    }
+    return count_;
+}
+
+// FindNextGotElement (:1372-1417)
+uint32_t Decoder::find_next_got(uint32_t start) {
+    if (start >= count_) return count_;
+    const uint32_t sub_end = (count_ + kSubwindow - 1) / kSubwindow;
+    uint32_t sub = start / kSubwindow, bit = start % kSubwindow;
+    while (sub < sub_end) {
+        if (subs_[sub]->got_count > 0) {
+            bit = bits_first_set(subs_[sub]->got, bit);
+            if (bit < kSubwindow) {
+                uint32_t e = sub * kSubwindow + bit;
+                if (e > count_) e = count_;
+                return e;
+            }
+        }
+        bit = 0;
+        ++sub;
+    }
+    return count_;
+}
+
+// IterateNextExpectedElement (:1419-1434)
+void Decoder::iterate_next_expected(uint32_t start) {
+    if (next_expected_ >= count_) return;
+    next_expected_ = find_next_lost(start);
+}
+
+// GrowWindow (:1436-1465)
+bool Decoder::grow_window(uint32_t end) {
+    const uint32_t needed = (end + kLanes + kSubwindow - 1) / kSubwindow;
+    while (subs_.size() < needed) subs_.push_back(new Subwindow());
+    if (end > count_) count_ = end;
+    return true;
+}
+
+// DecoderPacketWindow::AddOriginal (:1467-1536)
+Result Decoder::add_original(uint32_t packet_num, RowId row, uint32_t framed_bytes, uint32_t header_bytes,
+                             uint32_t payload_bytes, void* host, bool* took) {
+    *took = false;
+    if (disabled_) return kDisabled;
+    const uint32_t e = to_element(packet_num);
+    if (col_delta_negative(e)) {
+        stats_[6]++;
+        return kDuplicateData;
+    }
+    grow_window(e + 1);
+    Subwindow* s = subs_[e / kSubwindow];
+    const uint32_t bit = e % kSubwindow;
+    StoredOriginal& o = s->orig[bit];
+    if (o.bytes > 0) {
+        stats_[6]++;
+        return kDuplicateData;
+    }
+    drop_original(o);
+    o.row = row;
+    o.bytes = framed_bytes;
+    o.column = packet_num;
+    o.header_bytes = header_bytes;
+    o.host = host;
+    *took = true;
+    s->got_count++;
+    s->got |= 1ull << bit;
+
+    if (e == next_expected_) {
+        iterate_next_expected(e + 1);
+        list_delete_before(next_expected_);
+    }
+    if (e >= cr_.element_start && e < cr_.next_check_start) checked_reset();
+
+    stats_[0]++;
+    stats_[1] += payload_bytes;
+    return kSuccess;
+}
+
+// PlugSumHoles (:1538-1602)
+bool Decoder::plug_sum_holes(uint32_t element_start) {
+    for (uint32_t column : recovered_columns_) {
+        const uint32_t e = to_element(column);
+        if (invalid_element(e)) continue;
+        const uint32_t lane = column % kLanes;
+        const uint32_t lane_start = next_lane_element(element_start, lane);
+        for (unsigned s = 0; s < kSums; ++s) {
+            LaneSum& sum = lanes_[lane][s];
+            if (e >= lane_start && e < sum.element_end) {
+                const StoredOriginal& o = elem(e);
+                if (o.bytes <= 0) return false;
+                if (o.bytes > sum.chain.bytes) sum.chain.grow(o.bytes);
+                uint8_t cx = 1;
+                if (s > 0) {
+                    cx = column_value(column);
+                    if (s == 2) cx = gf_sqr(cx);
+                }
+                sum.chain.accumulate(ctx_->rows, o.row, o.bytes, cx);
+            }
+        }
+    }
+    recovered_columns_.clear();
+    return true;
+}
+
+// ResetSums (:1604-1627)
+void Decoder::reset_sums(uint32_t element_start) {
+    for (unsigned l = 0; l < kLanes; ++l) {
+        const uint32_t ls = next_lane_element(element_start, l);
+        for (unsigned s = 0; s < kSums; ++s) {
+            LaneSum& sum = lanes_[l][s];
+            sum.element_start = ls;
+            sum.element_end = ls;
+            sum.chain.reset(ctx_->rows);
+        }
+    }
+    recovered_columns_.clear();
+}
+
+// StartSums (:1629-1678)
+bool Decoder::start_sums(uint32_t element_start, uint32_t buffer_bytes) {
+    for (unsigned l = 0; l < kLanes; ++l) {
+        const uint32_t ls = next_lane_element(element_start, l);
+        for (unsigned s = 0; s < kSums; ++s) {
+            LaneSum& sum = lanes_[l][s];
+            if (sum.chain.bytes == 0) {
+                sum.element_end = ls;
+            } else if (sum.element_start != ls) {
+                sum.element_end = ls;
+                sum.chain.reset(ctx_->rows);
+            }
+            sum.element_start = ls;
+            sum.chain.grow(buffer_bytes);
+        }
+    }
+    if (!recovered_columns_.empty() && !plug_sum_holes(element_start)) return false;
+    return true;
+}
+
+// DecoderPacketWindow::GetSum (:1680-1739)
+Chain& Decoder::get_sum(uint32_t lane, uint32_t sum_index, uint32_t element_end) {
+    LaneSum& sum = lanes_[lane][sum_index];
+    uint32_t e = sum.element_end;
+    if (e >= element_end) return sum.chain;
+    do {
+        const StoredOriginal& o = elem(e);
+        if (o.bytes > 0) {
+            if (o.bytes > sum.chain.bytes) sum.chain.grow(o.bytes);
+            uint8_t cx = 1;
+            if (sum_index > 0) {
+                cx = column_value(o.column);
+                if (sum_index == 2) cx = gf_sqr(cx);
+            }
+            sum.chain.accumulate(ctx_->rows, o.row, o.bytes, cx);
+        }
+        e += kLanes;
+    } while (e < element_end);
+    sum.element_end = e;
+    return sum.chain;
+}
+
+// DecoderPacketWindow::RemoveElements (:1778-2033)
+void Decoder::remove_elements() {
+    if (next_expected_ < kRemoveThreshold) return;
+
+    uint32_t first_kept = 0, target_start = 0, target_count = 0, initial_bytes = 0;
+    bool seen_sum = false;
+    const Recovery* r = head_;
+    if (!r) {
+        const RecoveryMeta m = last_meta_;
+        const uint32_t end = to_element(m.ColumnStart + m.SumCount);
+        if (col_delta_negative(end) || end < m.LDPCCount) { disabled_ = true; return; }
+        first_kept = end - m.LDPCCount;
+        target_start = m.ColumnStart;
+        target_count = m.SumCount;
+        initial_bytes = last_bytes_;
+        if (m.SumCount > kCauchyThreshold) seen_sum = true;
+    } else {
+        first_kept = r->element_start;
+        initial_bytes = r->bytes;
+        for (;;) {
+            const uint32_t sc = r->meta.SumCount, cs = r->meta.ColumnStart;
+            if (sc > kCauchyThreshold) {
+                if (!seen_sum) {
+                    target_start = cs;
+                    target_count = sc;
+                    seen_sum = true;
+                } else if (cs != target_start || sc < target_count) {
+                    const uint32_t fse = to_element(cs);
+                    if (invalid_element(fse)) { disabled_ = true; return; }
+                    if (first_kept > fse) first_kept = fse;
+                }
+            }
+            r = r->next;
+            if (!r) break;
+            if (first_kept > r->element_start) first_kept = r->element_start;
+            if (initial_bytes < r->bytes) initial_bytes = r->bytes;
+        }
+    }
+    if (first_kept < kRemoveThreshold) return;
+
+    const uint32_t first_kept_sub = first_kept / kSubwindow;
+    const uint32_t removed = first_kept_sub * kSubwindow;
+
+    if (seen_sum) {
+        uint32_t sum_elem = to_element(target_start);
+        if (sum_column_start_ != target_start || sum_column_count_ > target_count) {
+            if (invalid_element(sum_elem)) { disabled_ = true; return; }
+            reset_sums(sum_elem);
+            sum_column_start_ = target_start;
+            sum_column_count_ = target_count;
+        } else {
+            if (invalid_element(sum_elem)) sum_elem = 0;
+            if (!start_sums(sum_elem, initial_bytes)) { disabled_ = true; return; }
+        }
+        for (unsigned l = 0; l < kLanes; ++l) {
+            for (unsigned s = 0; s < kSums; ++s) {
+                get_sum(l, s, removed);
+                LaneSum& sum = lanes_[l][s];
+                if (sum.element_start >= removed) sum.element_start -= removed;
+                else sum.element_start = l;
+                sum.element_end -= removed;
+            }
+        }
+    } else {
+        sum_column_count_ = 0;
+    }
+
+    for (uint32_t i = 0; i < first_kept_sub; ++i) {
+        Subwindow* s = subs_[i];
+        for (unsigned k = 0; k < kSubwindow; ++k) drop_original(s->orig[k]);
+        s->got = 0;
+        s->got_count = 0;
+    }
+    std::vector<Subwindow*> moved(subs_.begin(), subs_.begin() + first_kept_sub);
+    subs_.erase(subs_.begin(), subs_.begin() + first_kept_sub);
+    subs_.insert(subs_.end(), moved.begin(), moved.end());
+
+    count_ -= removed;
+    column_start_ = to_column(removed);
+    next_expected_ -= removed;
+
+    for (Recovery* q = head_; q; q = q->next) {
+        q->element_end -= removed;
+        q->element_start -= removed;
+    }
+    checked_decrement(removed);
+    prev_next_check_start_ = prev_next_check_start_ > removed ? prev_next_check_start_ - removed : 0;
+}
+
+// ============================================================================================
+// Recovery list and checked region (:2537-2666)
+// ============================================================================================
+
+// RecoveryPacketList::Insert (:2567-2635)
+void Decoder::list_insert(Recovery* rec, bool out_of_order) {
+    Recovery* prev = tail_;
+    Recovery* next = nullptr;
+    const uint32_t rs = rec->meta.ColumnStart, re = rec->element_end;
+    for (; prev; next = prev, prev = prev->prev) {
+        const uint32_t ps = prev->meta.ColumnStart, pe = prev->element_end;
+        if (re >= pe) {
+            if (re > pe) break;
+            if (col_delta_negative(col_sub(rs, ps))) break;
+        }
+    }
+    rec->next = next;
+    rec->prev = prev;
+    if (prev) prev->next = rec; else head_ = rec;
+    if (next) next->prev = rec; else tail_ = rec;
+    if (!prev || next) checked_reset();
+    ++recovery_count_;
+    if (!out_of_order) {
+        last_meta_ = rec->meta;
+        last_bytes_ = rec->bytes;
+    }
+}
+
+// RecoveryPacketList::DeletePacketsBefore (:2637-2666)
+void Decoder::list_delete_before(uint32_t element) {
+    Recovery* r = head_;
+    uint32_t deleted = 0;
+    while (r) {
+        if (r->element_end > element) break;
+        Recovery* n = r->next;
+        free_recovery(r);
+        ++deleted;
+        r = n;
+    }
+    head_ = r;
+    if (r) {
+        r->prev = nullptr;
+        recovery_count_ -= deleted;
+    } else {
+        tail_ = nullptr;
+        recovery_count_ = 0;
+    }
+}
+
+// CheckedRegionState::Reset (:2537-2548)
+void Decoder::checked_reset() {
+    cr_ = Checked();
+    matrix_reset();
+    for (Recovery* r : graveyard_) delete r;
+    graveyard_.clear();
+}
+
+// CheckedRegionState::DecrementElementCounters (:2550-2561)
+void Decoder::checked_decrement(uint32_t n) {
+    if (cr_.element_start < n || cr_.next_check_start < n) {
+        checked_reset();
+        return;
+    }
+    cr_.element_start -= n;
+    cr_.next_check_start -= n;
+}
+
+// ============================================================================================
+// Recovery matrix (:2039-2531)
+// ============================================================================================
+
+// RecoveryMatrixState::Reset (:2039-2049)
+void Decoder::matrix_reset() {
+    mcols_.clear();
+    mrows_.clear();
+    pivots_.clear();
+    mat_rows_ = mat_cols_ = 0;
+    prev_next_check_start_ = 0;
+    ge_resume_pivot_ = 0;
+}
+
+// GrowingAlignedByteMatrix::Initialize / Resize (SiameseCommon.cpp:51-117).  Elements of the
+// old matrix keep their values; the rest are written by generate_matrix before use.
+bool Decoder::matrix_resize(uint32_t rows, uint32_t cols, bool keep) {
+    if (keep && rows <= mat_alloc_rows_ && cols <= mat_stride_) {
+        mat_rows_ = rows;
+        mat_cols_ = cols;
+        return true;
+    }
+    const uint32_t arows = rows + 4;
+    const uint32_t acols = (cols + 4 + 31) & ~31u;
+    std::vector<uint8_t> m((size_t)arows * acols, 0);
+    if (keep && mat_cols_ > 0) {
+        const uint32_t copy = mat_cols_ < cols ? mat_cols_ : cols;
+        for (uint32_t i = 0; i < mat_rows_; ++i)
+            memcpy(&m[(size_t)i * acols], &mat_[(size_t)i * mat_stride_], copy);
+    }
+    mat_.swap(m);
+    mat_alloc_rows_ = arows;
+    mat_stride_ = acols;
+    mat_rows_ = rows;
+    mat_cols_ = cols;
+    return true;
+}
+
+// RecoveryMatrixState::PopulateColumns (:2059-2130)
+void Decoder::populate_columns(uint32_t old_cols, uint32_t new_cols) {
+    if (old_cols >= new_cols) return;
+    mcols_.resize(new_cols);
+    uint32_t start = prev_next_check_start_;
+    prev_next_check_start_ = cr_.next_check_start;
+    const uint32_t end = cr_.next_check_start;
+    if (start < cr_.element_start) start = cr_.element_start;
+    const uint32_t sub_end = (end + kSubwindow - 1) / kSubwindow;
+    uint32_t sub = start / kSubwindow, bit = start % kSubwindow, column = old_cols;
+    while (sub < sub_end) {
+        Subwindow* s = subs_[sub];
+        if (s->got_count < kSubwindow) {
+            do {
+                bit = bits_first_clear(s->got, bit);
+                if (bit >= kSubwindow) break;
+                const uint32_t e = sub * kSubwindow + bit;
+                MatCol& c = mcols_[column];
+                c.column = to_column(e);
+                c.orig = &s->orig[bit];
+                c.cx = column_value(c.column);
+                c.orig->column = column;  // lost slot remembers its matrix column
+                if (++column >= new_cols) return;
+            } while (++bit < kSubwindow);
+        }
+        bit = 0;
+        ++sub;
+    }
+    disabled_ = true;  // should never get here
+}
+
+// RecoveryMatrixState::PopulateRows (:2132-2155)
+void Decoder::populate_rows(uint32_t old_rows, uint32_t new_rows) {
+    if (old_rows >= new_rows) return;
+    mrows_.resize(new_rows);
+    Recovery* r = old_rows > 0 ? mrows_[old_rows - 1].rec->next : cr_.first;
+    for (uint32_t i = old_rows; i < new_rows; ++i, r = r->next) {
+        mrows_[i].rec = r;
+        mrows_[i].used = false;
+        mrows_[i].mcols = r->lost_count;
+    }
+}
+
+// RecoveryMatrixState::GenerateMatrix (:2157-2383)
+bool Decoder::generate_matrix() {
+    const uint32_t columns = cr_.lost_count;
+    const uint32_t rows = cr_.recovery_count;
+    uint32_t old_rows = (uint32_t)mrows_.size();
+    uint32_t old_cols = (uint32_t)mcols_.size();
+    if (rows < old_rows || columns < old_cols) {
+        matrix_reset();
+        old_rows = old_cols = 0;
+    }
+    matrix_resize(rows, columns, old_rows != 0);
+    populate_columns(old_cols, columns);
+    populate_rows(old_rows, rows);
+    if (disabled_) return false;
+
+    const uint32_t start_row = columns <= old_cols ? old_rows : 0;
+    for (uint32_t i = start_row; i < rows; ++i) {
+        Recovery* rec = mrows_[i].rec;
+        const RecoveryMeta m = rec->meta;
+        const uint32_t start_col = i < old_rows ? old_cols : 0;
+        if (m.SumCount <= kCauchyThreshold) {
+            for (uint32_t j = start_col; j < columns; ++j) {
+                const uint32_t column = mcols_[j].column;
+                const uint32_t e = col_sub(column, m.ColumnStart);
+                if (e >= m.SumCount) {
+                    for (; j < columns; ++j) mat(i, j) = 0;
+                    break;
+                }
+                mat(i, j) = m.Row == 0 ? 1 : cauchy_element(m.Row - 1, column % kCauchyMaxColumns);
+            }
+            continue;
+        }
+        const uint8_t rx = row_value(m.Row);
+        for (uint32_t j = start_col; j < columns; ++j) {
+            const uint32_t column = mcols_[j].column;
+            const uint32_t e = col_sub(column, m.ColumnStart);
+            if (e >= m.SumCount) {
+                for (; j < columns; ++j) mat(i, j) = 0;
+                break;
+            }
+            const uint8_t cx = mcols_[j].cx, cx2 = gf_sqr(cx);
+            const unsigned op = row_opcode(column % kLanes, m.Row);
+            uint8_t v = 0;
+            if (op & 1) v ^= 1;
+            if (op & 2) v ^= cx;
+            if (op & 4) v ^= cx2;
+            if (op & 8) v ^= rx;
+            if (op & 16) v ^= gf_mul(cx, rx);
+            if (op & 32) v ^= gf_mul(cx2, rx);
+            mat(i, j) = v;
+        }
+        Pcg32 prng;
+        prng.seed(m.Row, m.LDPCCount);
+        const uint32_t es = rec->element_start;
+        const uint32_t pairs = (m.LDPCCount + kPairRate - 1) / kPairRate;
+        for (uint32_t k = 0; k < pairs; ++k) {
+            const uint32_t e1 = es + prng.next() % m.LDPCCount;
+            const StoredOriginal& o1 = elem(e1);
+            if (o1.bytes <= 0) {
+                const uint32_t mc = o1.column;
+                if (mc >= columns) { disabled_ = true; return false; }
+                if (mc >= start_col) mat(i, mc) ^= 1;
+            }
+            const uint32_t erx = es + prng.next() % m.LDPCCount;
+            const StoredOriginal& orx = elem(erx);
+            if (orx.bytes <= 0) {
+                const uint32_t mc = orx.column;
+                if (mc >= columns) { disabled_ = true; return false; }
+                if (mc >= start_col) mat(i, mc) ^= rx;
+            }
+        }
+    }
+    pivots_.resize(rows);
+    for (uint32_t i = old_rows; i < rows; ++i) pivots_[i] = i;
+    if (ge_resume_pivot_ > 0) resume_ge(old_rows, rows);
+    return true;
+}
+
+// RecoveryMatrixState::EliminateRow / MulAddRows (SiameseDecoder.h:504-541)
+bool Decoder::eliminate_row(uint32_t ge_row, uint32_t rem_row, uint32_t pivot_i, uint32_t column_end, uint8_t val_i) {
+    uint8_t* rem = &mat_[(size_t)rem_row * mat_stride_];
+    const uint8_t* ge = &mat_[(size_t)ge_row * mat_stride_];
+    const uint8_t val_j = rem[pivot_i];
+    if (val_j == 0) return false;
+    const uint8_t y = gf_div(val_j, val_i);
+    rem[pivot_i] = y;
+    const uint8_t* ymul = g_gf.mul[y];
+    for (uint32_t c = pivot_i + 1; c < column_end; ++c) rem[c] ^= ymul[ge[c]];
+    return true;
+}
+
+// RecoveryMatrixState::ResumeGE (:2385-2421)
+void Decoder::resume_ge(uint32_t old_rows, uint32_t rows) {
+    if (old_rows >= rows) return;
+    for (uint32_t pi = 0; pi < ge_resume_pivot_; ++pi) {
+        const uint32_t ri = pivots_[pi];
+        const uint8_t val_i = mat(ri, pi);
+        const uint32_t pcc = mrows_[ri].mcols;
+        for (uint32_t nr = old_rows; nr < rows; ++nr) {
+            if (eliminate_row(ri, nr, pi, pcc, val_i)) {
+                if (mrows_[nr].mcols < pcc) mrows_[nr].mcols = pcc;
+            }
+        }
+    }
+}
+
+// RecoveryMatrixState::GaussianElimination (:2423-2465)
+bool Decoder::gaussian_elimination() {
+    if (ge_resume_pivot_ > 0) return pivoted_ge(ge_resume_pivot_);
+    const uint32_t columns = mat_cols_, rows = mat_rows_;
+    for (uint32_t pi = 0; pi < columns; ++pi) {
+        const uint8_t val_i = mat(pi, pi);
+        if (val_i == 0) return pivoted_ge(pi);
+        mrows_[pi].used = true;
+        const uint32_t pcc = mrows_[pi].mcols;
+        for (uint32_t pj = pi + 1; pj < rows; ++pj) eliminate_row(pi, pj, pi, pcc, val_i);
+    }
+    return true;
+}
+
+// RecoveryMatrixState::PivotedGaussianElimination (:2467-2531)
+bool Decoder::pivoted_ge(uint32_t pivot_i) {
+    const uint32_t columns = mat_cols_, rows = mat_rows_;
+    uint32_t pj = pivot_i + 1;
+    bool resume = true;
+    for (; pivot_i < columns; ++pivot_i) {
+        if (!resume) pj = pivot_i;
+        resume = false;
+        bool found = false;
+        for (; pj < rows; ++pj) {
+            const uint32_t rj = pivots_[pj];
+            const uint8_t val_i = mat(rj, pivot_i);
+            if (val_i == 0) continue;
+            if (pivot_i != pj) std::swap(pivots_[pivot_i], pivots_[pj]);
+            mrows_[rj].used = true;
+            const uint32_t pcc = mrows_[rj].mcols;
+            if (pivot_i >= columns - 1) return true;
+            for (uint32_t pk = pivot_i + 1; pk < rows; ++pk) {
+                const uint32_t rk = pivots_[pk];
+                if (eliminate_row(rj, rk, pivot_i, pcc, val_i)) {
+                    if (mrows_[rk].mcols < pcc) mrows_[rk].mcols = pcc;
+                }
+            }
+            found = true;
+            break;
+        }
+        if (!found) {
+            ge_resume_pivot_ = pivot_i;
+            return false;
+        }
+    }
+    return true;
+}
+
+// ============================================================================================
+// Decoder (SiameseDecoder.cpp:71-811)
+// ============================================================================================
+
+// Decoder::AddRecovery (:257-451)
+Result Decoder::add_recovery(RowId row, uint32_t total_bytes, const uint8_t* tail, const uint8_t* host,
+                             bool* took) {
+    *took = false;
+    if (disabled_) return kDisabled;
+    RecoveryMeta m;
+    const uint32_t tl = total_bytes < 8 ? total_bytes : 8;
+    const int footer = get_recovery_footer(tail, tl, m);
+    if (footer < 0) { disabled_ = true; return kDisabled; }
+
+    stats_[2]++;
+    stats_[3] += total_bytes;
+
+    const bool out_of_order = col_delta_negative(m.ColumnStart + m.SumCount - latest_column_);
+    if (!out_of_order) latest_column_ = (m.ColumnStart + m.SumCount) % kColumnPeriod;
+
+    uint32_t es, ee;
+    if (count_ <= 0) {
+        if (out_of_order) { stats_[9]++; return kSuccess; }
+        column_start_ = m.ColumnStart;
+        grow_window(m.SumCount);
+        ee = m.SumCount;
+        es = ee - m.LDPCCount;
+    } else {
+        ee = to_element(m.ColumnStart + m.SumCount);
+        if (col_delta_negative(ee)) { stats_[9]++; return kSuccess; }
+        if (ee < m.LDPCCount) { stats_[9]++; return kSuccess; }
+        es = ee - m.LDPCCount;
+        if (ee <= next_expected_) {
+            if (out_of_order) { stats_[9]++; return kSuccess; }
+            if (es >= kRemoveThreshold) {
+                last_meta_ = m;
+                last_bytes_ = total_bytes - (uint32_t)footer;
+                remove_elements();
+            }
+            stats_[9]++;
+            return kSuccess;
+        }
+        if (m.SumCount > kCauchyThreshold) {
+            if (sum_column_count_ == 0 || sum_column_start_ != m.ColumnStart) {
+                if (invalid_element(to_element(m.ColumnStart))) { stats_[9]++; return kSuccess; }
+            }
+        }
+        grow_window(ee);
+    }
+
+    if (m.SumCount == 1) {
+        if (!add_single_recovery(row, total_bytes - (uint32_t)footer, host, m, took)) {
+            disabled_ = true;
+            return kDisabled;
+        }
+        return kSuccess;
+    }
+
+    Recovery* r = new Recovery();
+    r->bytes = total_bytes - (uint32_t)footer;
+    r->row = row;
+    *took = true;
+    r->buf.push_back(Term{row, r->bytes, 1});
+    r->meta = m;
+    r->element_start = es;
+    r->element_end = ee;
+    list_insert(r, out_of_order);
+    if (es >= kRemoveThreshold) remove_elements();
+    return kSuccess;
+}
+
+// Decoder::AddSingleRecovery (:453-539).  The packet data is the framed original itself, so
+// the window slot takes the packet row (its first `data_bytes` bytes) without a copy.
+bool Decoder::add_single_recovery(RowId row, uint32_t data_bytes, const uint8_t* host,
+                                  const RecoveryMeta& m, bool* took) {
+    const uint32_t e = to_element(m.ColumnStart);
+    if (invalid_element(e)) return false;
+    StoredOriginal& o = elem(e);
+    if (o.bytes != 0) return true;
+
+    uint32_t header = 0, payload = 0;
+    if (host) {
+        unsigned len = 0;
+        const int hb = get_length_header(host, data_bytes, len);
+        if (hb < 1 || len == 0 || len + (unsigned)hb != data_bytes) return false;
+        header = (uint32_t)hb;
+        payload = len;
+    }
+    drop_original(o);
+    o.row = row;
+    o.bytes = data_bytes;
+    o.column = m.ColumnStart;
+    o.header_bytes = header;
+    *took = true;
+
+    if (!has_recovered_) {
+        has_recovered_ = true;
+        recovered_.clear();
+    }
+    RecoveredPacket rp;
+    rp.packet_num = m.ColumnStart;
+    rp.row = row;
+    rp.framed_upper = data_bytes;
+    rp.header_bytes = header;
+    rp.data_bytes = payload;
+    recovered_.push_back(rp);
+    recovered_columns_.push_back(m.ColumnStart);
+
+    if (e >= cr_.element_start && e < cr_.next_check_start) checked_reset();
+
+    if (mark_got(m.ColumnStart)) {
+        iterate_next_expected(e + 1);
+        list_delete_before(next_expected_);
+        if (cr_.next_check_start >= kRemoveThreshold) remove_elements();
+    }
+    return true;
+}
+
+// Decoder::CheckRecoveryPossible (:541-628)
+bool Decoder::check_recovery_possible() {
+    if (disabled_) return false;
+    Recovery* r;
+    uint32_t next_check, rcount, lost;
+    if (!cr_.last) {
+        r = head_;
+        if (!r) return false;
+        cr_.first = r;
+        cr_.element_start = r->element_start;
+        rcount = 1;
+        next_check = r->element_end;
+        lost = range_lost(r->element_start, next_check);
+        cr_.solve_failed = false;
+        r->lost_count = lost;
+    } else {
+        rcount = cr_.recovery_count;
+        lost = cr_.lost_count;
+        if (rcount >= lost && !cr_.solve_failed) return lost <= kMaxLossRecovery;
+        r = cr_.last;
+        next_check = cr_.next_check_start;
+    }
+    while ((rcount < lost || cr_.solve_failed) && r->next) {
+        r = r->next;
+        ++rcount;
+        uint32_t ee = r->element_end;
+        if (ee < next_check) ee = next_check;
+        lost += range_lost(next_check, ee);
+        next_check = ee;
+        r->lost_count = lost;
+        cr_.solve_failed = false;
+    }
+    cr_.last = r;
+    cr_.recovery_count = rcount;
+    cr_.lost_count = lost;
+    cr_.next_check_start = next_check;
+    if (lost > kMaxLossRecovery) return false;
+    return rcount >= lost && !cr_.solve_failed;
+}
+
+Result Decoder::is_ready() {
+    if (has_recovered_ || check_recovery_possible()) return kSuccess;
+    return kNeedMoreData;
+}
+
+// Decoder::Decode (:630-727)
+Result Decoder::decode(std::vector<RecoveredPacket*>& out) {
+    if (disabled_) return kDisabled;
+    if (has_recovered_) {
+        has_recovered_ = false;
+        for (RecoveredPacket& p : recovered_) out.push_back(&p);
+        return kSuccess;
+    }
+    if (!check_recovery_possible()) return kNeedMoreData;
+
+    Recovery* r = cr_.last;
+    uint32_t next_check = cr_.next_check_start, rcount = cr_.recovery_count, lost = cr_.lost_count;
+    for (;;) {
+        if (rcount >= lost) {
+            const Result res = decode_checked_region();
+            if (res == kSuccess) {
+                for (RecoveredPacket& p : recovered_) out.push_back(&p);
+                return kSuccess;
+            }
+            if (res != kNeedMoreData) return res;
+        }
+        if (!r->next) break;
+        r = r->next;
+        ++rcount;
+        uint32_t ee = r->element_end;
+        if (ee < next_check) ee = next_check;
+        lost += range_lost(next_check, ee);
+        r->lost_count = lost;
+        next_check = ee;
+    }
+    cr_.last = r;
+    cr_.next_check_start = next_check;
+    cr_.recovery_count = rcount;
+    cr_.lost_count = lost;
+    return kNeedMoreData;
+}
+
+// Decoder::DecodeCheckedRegion (:729-810)
+Result Decoder::decode_checked_region() {
+    if (!generate_matrix()) { disabled_ = true; return kDisabled; }
+    if (!gaussian_elimination()) {
+        cr_.solve_failed = true;
+        stats_[8]++;
+        return kNeedMoreData;
+    }
+    if (!eliminate_original_data()) { disabled_ = true; return kDisabled; }
+    if (!multiply_lower_triangle()) { disabled_ = true; return kDisabled; }
+    const Result res = back_substitution();
+    checked_reset();
+    return res;
+}
+
+// Decoder::EliminateOriginalData (:812-1063)
+bool Decoder::eliminate_original_data() {
+    const uint32_t rows = cr_.recovery_count;
+    for (uint32_t ri = 0; ri < rows; ++ri) {
+        if (!mrows_[ri].used) continue;
+        Recovery* rec = mrows_[ri].rec;
+        const RecoveryMeta m = rec->meta;
+        const uint32_t es = rec->element_start, ee = rec->element_end;
+        Sym& buf = rec->buf;
+
+        if (m.SumCount <= kCauchyThreshold) {
+            for (uint32_t j = es; j < ee; ++j) {
+                const StoredOriginal& o = elem(j);
+                uint32_t add = o.bytes;
+                if (add > 0) {
+                    if (add > rec->bytes) add = rec->bytes;
+                    const uint8_t y = m.Row == 0 ? 1 : cauchy_element(m.Row - 1, o.column % kCauchyMaxColumns);
+                    read_original(o, add, y, buf);
+                }
+            }
+        } else {
+            const uint32_t rbytes = rec->bytes;
+            Sym prod;
+            uint32_t sum_elem = to_element(m.ColumnStart);
+            if (m.ColumnStart != sum_column_start_ || m.SumCount < sum_column_count_) {
+                if (invalid_element(sum_elem)) return false;
+                reset_sums(sum_elem);
+                sum_column_start_ = m.ColumnStart;
+            } else {
+                if (invalid_element(sum_elem)) sum_elem = 0;
+                if (!start_sums(sum_elem, rbytes)) return false;
+            }
+            sum_column_count_ = m.SumCount;
+
+            for (unsigned l = 0; l < kLanes; ++l) {
+                const unsigned op = row_opcode(l, m.Row);
+                for (unsigned s = 0; s < kSums; ++s) {
+                    if (op & (1u << s)) {
+                        Chain& c = get_sum(l, s, ee);
+                        const uint32_t n = c.bytes < rbytes ? c.bytes : rbytes;
+                        if (n) c.read(ctx_->rows, ctx_->ex, buf, n, 1);
+                    }
+                }
+                for (unsigned s = 0; s < kSums; ++s) {
+                    if (op & (1u << (s + 3))) {
+                        Chain& c = get_sum(l, s, ee);
+                        const uint32_t n = c.bytes < rbytes ? c.bytes : rbytes;
+                        if (n) c.read(ctx_->rows, ctx_->ex, prod, n, 1);
+                    }
+                }
+            }
+            Pcg32 prng;
+            prng.seed(m.Row, m.LDPCCount);
+            const uint32_t pairs = (m.LDPCCount + kPairRate - 1) / kPairRate;
+            for (uint32_t i = 0; i < pairs; ++i) {
+                const uint32_t e1 = es + prng.next() % m.LDPCCount;
+                const StoredOriginal& o1 = elem(e1);
+                if (o1.bytes > 0) read_original(o1, o1.bytes < rbytes ? o1.bytes : rbytes, 1, buf);
+                const uint32_t erx = es + prng.next() % m.LDPCCount;
+                const StoredOriginal& orx = elem(erx);
+                if (orx.bytes > 0) read_original(orx, orx.bytes < rbytes ? orx.bytes : rbytes, 1, prod);
+            }
+            sym_add(buf, prod, rbytes, row_value(m.Row));
+        }
+        if (ctx_->oom) return false;
+        // Fold everything already in memory into one partial row so the triangular solve and
+        // any later reader in this program touch one row instead of the whole elimination.
+        sym_clip(buf, rec->bytes);
+        const RowId p = fold_low_levels(ctx_->rows, ctx_->pb, buf, 3, rec->bytes, row_bytes_);
+        if (p != kNoRow) ctx_->temps.push_back(p);
+    }
+    return !disabled_ && !ctx_->oom;
+}
+
+// Decoder::MultiplyLowerTriangle (:1065-1104)
+bool Decoder::multiply_lower_triangle() {
+    const uint32_t columns = cr_.lost_count;
+    for (uint32_t ci = 0; ci + 1 < columns; ++ci) {
+        Recovery* ri = mrows_[pivots_[ci]].rec;
+        sym_merge(ri->buf);  // row ci is final from here on; keep sources compact
+        const uint32_t src_bytes = ri->bytes;
+        for (uint32_t cj = ci + 1; cj < columns; ++cj) {
+            const uint32_t rj_index = pivots_[cj];
+            const uint8_t y = mat(rj_index, ci);
+            if (y == 0) continue;
+            Recovery* rj = mrows_[rj_index].rec;
+            if (rj->bytes < src_bytes) rj->bytes = src_bytes;  // GrowZeroPadded
+            sym_add(rj->buf, ri->buf, src_bytes, y);
+        }
+    }
+    for (uint32_t ci = 0; ci < columns; ++ci) sym_merge(mrows_[pivots_[ci]].rec->buf);
+    return true;
+}
+
+// Decoder::BackSubstitution (:1106-1238).  The recovered length is data dependent (the framed
+// header inside the recovered bytes); the symbolic solve uses the recovery row length, which
+// only adds zero bytes, and the exact length is read back with the data.
+Result Decoder::back_substitution() {
+    const uint32_t columns = cr_.lost_count;
+    recovered_.assign(columns, RecoveredPacket());
+    bool iterate = false;
+    for (int ci = (int)columns - 1; ci >= 0; --ci) {
+        const uint32_t ri = pivots_[ci];
+        StoredOriginal* o = mcols_[ci].orig;
+        Recovery* rec = mrows_[ri].rec;
+        const uint8_t y = mat(ri, (uint32_t)ci);
+        if (y == 0) { disabled_ = true; return kDisabled; }
+        const uint8_t inv_y = gf_inv(y);
+        const uint32_t bytes = rec->bytes;
+
+        Sym value;
+        sym_add(value, rec->buf, bytes, inv_y);
+        sym_merge(value);
+        const RowId out_row = ctx_->alloc(bytes);
+        if (out_row == kNoRow) { disabled_ = true; return kDisabled; }
+        ctx_->pb.combine(out_row, value.data(), value.size(), bytes);
+        ctx_->ex.set(out_row, value);
+
+        drop_original(*o);
+        o->row = out_row;
+        o->bytes = bytes;
+        o->column = mcols_[ci].column;
+        o->header_bytes = 0;
+        rec->buf.clear();
+        rec->bytes = 0;
+
+        RecoveredPacket& rp = recovered_[ci];
+        rp.packet_num = o->column;
+        rp.row = out_row;
+        rp.framed_upper = bytes;
+        recovered_columns_.push_back(o->column);
+        iterate |= mark_got(o->column);
+
+        for (uint32_t cj = 0; cj < (uint32_t)ci; ++cj) {
+            const uint32_t pj = pivots_[cj];
+            const uint8_t x = mat(pj, (uint32_t)ci);
+            if (x == 0) continue;
+            Recovery* bj = mrows_[pj].rec;
+            uint32_t add = bytes;
+            if (add > bj->bytes) add = bj->bytes;
+            sym_add(bj->buf, value, add, x);
+        }
+    }
+    if (!iterate) { disabled_ = true; return kDisabled; }
+    iterate_next_expected(cr_.next_check_start);
+    list_delete_before(next_expected_);
+    if (cr_.next_check_start >= kRemoveThreshold) remove_elements();
+    stats_[7]++;
+    return kSuccess;
+}
+
+void Decoder::set_recovered_length(uint32_t packet_num, uint32_t framed_bytes, uint32_t header_bytes, void* host) {
+    const uint32_t e = to_element(packet_num);
+    if (invalid_element(e)) { if (host && release_) release_(host, user_); return; }
+    StoredOriginal& o = elem(e);
+    if (o.column != packet_num || o.bytes == 0) { if (host && release_) release_(host, user_); return; }
+    o.bytes = framed_bytes;
+    o.header_bytes = header_bytes;
+    if (o.host && release_) release_(o.host, user_);
+    o.host = host;
+}
+
+// Decoder::Get (:71-123)
+Result Decoder::get(uint32_t packet_num, StoredOriginal** out) {
+    *out = nullptr;
+    if (disabled_) return kDisabled;
+    const uint32_t e = to_element(packet_num);
+    if (invalid_element(e)) return kNeedMoreData;
+    StoredOriginal& o = elem(e);
+    if (o.bytes <= 0) return kNeedMoreData;
+    *out = &o;
+    return kSuccess;
+}
+
+// Decoder::GenerateAcknowledgement (:125-255)
+Result Decoder::ack(uint8_t* buffer, uint32_t limit, uint32_t* used) {
+    if (disabled_) return kDisabled;
+    const uint32_t wc = count_;
+    if (wc == 0) { *used = 0; return kNeedMoreData; }
+    uint8_t* start = buffer;
+    const uint32_t nee = next_expected_;
+    const uint32_t hb = put_pnum_header(to_column(nee), buffer);
+    buffer += hb;
+    limit -= hb;
+    if (invalid_element(nee)) {
+        *used = (uint32_t)(buffer - start);
+        stats_[4]++;
+        stats_[5] += *used;
+        return kSuccess;
+    }
+    uint32_t off = nee;
+    while (limit >= kMaxLossRangeBytes) {
+        const uint32_t rs = find_next_lost(off);
+        if (rs >= wc) {
+            if (wc >= off) buffer += put_nack_range(wc - off, 0, buffer);
+            break;
+        }
+        const uint32_t re = find_next_got(rs + 1);
+        const uint32_t n = put_nack_range(rs - off, re - rs - 1, buffer);
+        off = re + 1;
+        buffer += n;
+        limit -= n;
+    }
+    *used = (uint32_t)(buffer - start);
+    stats_[4]++;
+    stats_[5] += *used;
+    return kSuccess;
+}
+
+// Decoder::GetStatistics (:1240-1254)
+void Decoder::stats(uint64_t* out, unsigned n) {
+    if (n > 11) n = 11;
+    stats_[10] = ctx_->rows.bytes_in_use();
+    for (unsigned i = 0; i < n; ++i) out[i] = stats_[i];
+}
+
+} // namespace tamd

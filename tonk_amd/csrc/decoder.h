@@ -1,0 +1,180 @@
+// decoder.h -- Siamese decoder control plane (restates SiameseDecoder.h/.cpp of the reference).
+//
+// Window of received originals with per-subwindow got-bitmaps, sorted recovery-packet list,
+// checked region, recovery-matrix generation, incremental Gaussian elimination with pivoting,
+// running-sum elimination of received data, lower-triangle and back substitution, NACK ack
+// generation and window removal -- all decisions identical to the reference.  The bulk row
+// operations are symbolic (engine.h): after a successful solve each recovered original is one
+// combine op over "partial" rows (received recovery rows with the known data eliminated).
+#pragma once
+
+#include "encoder.h"
+
+#include <stdint.h>
+#include <vector>
+
+namespace tamd {
+
+struct RecoveredPacket {
+    uint32_t packet_num = 0;
+    RowId row = kNoRow;          // framed row (varint len || payload) in the arena
+    uint32_t framed_upper = 0;   // bytes the row may hold (exact once the length is read back)
+    void* host = nullptr;        // C-ABI: host copy filled after readback
+    uint32_t data_bytes = 0;     // payload length (valid after readback)
+    uint32_t header_bytes = 0;
+};
+
+class Decoder : public FlushClient {
+public:
+    Decoder(Context* ctx, uint32_t row_bytes, HostRelease release = nullptr, void* user = nullptr);
+    ~Decoder();
+
+    // siamese_decoder_add_original: `row` holds the framed original; ownership passes to the
+    // decoder on success only (on DuplicateData the caller keeps it).
+    Result add_original(uint32_t packet_num, RowId row, uint32_t framed_bytes, uint32_t header_bytes,
+                        uint32_t payload_bytes, void* host, bool* took_ownership);
+    // siamese_decoder_add_recovery: `row` holds the packet (data || footer), `tail` the last
+    // min(total, 8) bytes of the packet (footer parsing), `host` the whole packet if available.
+    // Ownership of `row` passes to the decoder when *took_ownership is set.
+    Result add_recovery(RowId row, uint32_t total_bytes, const uint8_t* tail, const uint8_t* host,
+                        bool* took_ownership);
+    Result is_ready();
+    // siamese_decode: recovered packets are appended to `out` (increasing packet number).
+    Result decode(std::vector<RecoveredPacket*>& out);
+    Result get(uint32_t packet_num, StoredOriginal** out);
+    Result ack(uint8_t* buffer, uint32_t limit, uint32_t* used);
+    void stats(uint64_t* out, unsigned n);
+
+    bool disabled() const { return disabled_; }
+    void set_disabled() { disabled_ = true; }
+
+    // Recovered packets of the latest successful decode (for readback by the C-ABI layer).
+    std::vector<RecoveredPacket>& recovered() { return recovered_; }
+    // After readback: the exact framed length of a recovered original.
+    void set_recovered_length(uint32_t packet_num, uint32_t framed_bytes, uint32_t header_bytes, void* host);
+
+    void pre_flush() override;
+    void post_flush() override {}
+
+private:
+    struct Subwindow {
+        StoredOriginal orig[kSubwindow];
+        uint64_t got = 0;
+        uint32_t got_count = 0;
+    };
+    struct Recovery {
+        Recovery* next = nullptr;
+        Recovery* prev = nullptr;
+        RecoveryMeta meta;
+        uint32_t element_start = 0, element_end = 0, lost_count = 0;
+        RowId row = kNoRow;   // the received packet (owned)
+        Sym buf;              // Buffer contents (symbolic)
+        uint32_t bytes = 0;   // Buffer.Bytes
+    };
+    struct LaneSum {
+        uint32_t element_start = 0, element_end = 0;
+        Chain chain;
+    };
+    struct MatRow { Recovery* rec = nullptr; bool used = false; uint32_t mcols = 0; };
+    struct MatCol { StoredOriginal* orig = nullptr; uint32_t column = 0; uint8_t cx = 0; };
+
+    Context* ctx_;
+    uint32_t row_bytes_;
+    HostRelease release_;
+    void* user_;
+    uint64_t stats_[11] = {0};
+    bool disabled_ = false;
+
+    // ---- DecoderPacketWindow (SiameseDecoder.h:288-419) ----
+    uint32_t count_ = 0, column_start_ = 0, next_expected_ = 0;
+    std::vector<Subwindow*> subs_;
+    LaneSum lanes_[kLanes][kSums];
+    uint32_t sum_column_start_ = 0, sum_column_count_ = 0;
+    std::vector<RecoveredPacket> recovered_;
+    bool has_recovered_ = false;
+    std::vector<uint32_t> recovered_columns_;
+
+    // ---- RecoveryPacketList ----
+    Recovery* head_ = nullptr;
+    Recovery* tail_ = nullptr;
+    // Deleted packets stay readable until the checked region and matrix forget them: the
+    // reference frees them into its pool allocator, where stale pointers still read the old
+    // fields (RecoveryPacketList::DeletePacketsBefore, SiameseDecoder.cpp:2637-2666).
+    std::vector<Recovery*> graveyard_;
+    uint32_t recovery_count_ = 0;
+    RecoveryMeta last_meta_;
+    uint32_t last_bytes_ = 0;
+
+    // ---- CheckedRegionState ----
+    struct Checked {
+        uint32_t element_start = 0, next_check_start = 0, recovery_count = 0, lost_count = 0;
+        Recovery* first = nullptr;
+        Recovery* last = nullptr;
+        bool solve_failed = false;
+    } cr_;
+
+    // ---- RecoveryMatrixState ----
+    std::vector<MatRow> mrows_;
+    std::vector<MatCol> mcols_;
+    uint32_t prev_next_check_start_ = 0;
+    std::vector<uint8_t> mat_;
+    uint32_t mat_rows_ = 0, mat_cols_ = 0, mat_stride_ = 0, mat_alloc_rows_ = 0;
+    std::vector<uint32_t> pivots_;
+    uint32_t ge_resume_pivot_ = 0;
+
+    uint32_t latest_column_ = 0;
+
+    // helpers
+    uint32_t to_element(uint32_t column) const { return col_sub(column, column_start_); }
+    uint32_t to_column(uint32_t element) const { return col_add(element, column_start_); }
+    bool invalid_element(uint32_t e) const { return e >= count_; }
+    StoredOriginal& elem(uint32_t e) { return subs_[e / kSubwindow]->orig[e % kSubwindow]; }
+    uint32_t next_lane_element(uint32_t element, uint32_t lane) const {
+        uint32_t n = element - (element % kLanes) + lane;
+        if (n < element) n += kLanes;
+        return n;
+    }
+    uint8_t& mat(uint32_t r, uint32_t c) { return mat_[(size_t)r * mat_stride_ + c]; }
+
+    // window
+    bool mark_got(uint32_t column);
+    uint32_t range_lost(uint32_t start, uint32_t end);
+    uint32_t find_next_lost(uint32_t start);
+    uint32_t find_next_got(uint32_t start);
+    void iterate_next_expected(uint32_t start);
+    bool grow_window(uint32_t end);
+    Chain& get_sum(uint32_t lane, uint32_t sum, uint32_t element_end);
+    bool start_sums(uint32_t element_start, uint32_t buffer_bytes);
+    void reset_sums(uint32_t element_start);
+    bool plug_sum_holes(uint32_t element_start);
+    void remove_elements();
+    void drop_original(StoredOriginal& o);
+    void read_original(const StoredOriginal& o, uint32_t len, uint8_t coef, Sym& out) const;
+
+    // recovery list / checked region / matrix
+    void list_insert(Recovery* r, bool out_of_order);
+    void list_delete_before(uint32_t element);
+    void free_recovery(Recovery* r);
+    void checked_reset();
+    void checked_decrement(uint32_t n);
+    void matrix_reset();
+    void populate_columns(uint32_t old_cols, uint32_t new_cols);
+    void populate_rows(uint32_t old_rows, uint32_t new_rows);
+    bool generate_matrix();
+    bool matrix_resize(uint32_t rows, uint32_t cols, bool keep);
+    void resume_ge(uint32_t old_rows, uint32_t rows);
+    bool gaussian_elimination();
+    bool pivoted_ge(uint32_t pivot_i);
+    bool eliminate_row(uint32_t ge_row, uint32_t rem_row, uint32_t pivot_i, uint32_t column_end, uint8_t val_i);
+
+    // solve
+    bool add_single_recovery(RowId row, uint32_t data_bytes, const uint8_t* host,
+                             const RecoveryMeta& m, bool* took);
+    bool check_recovery_possible();
+    Result decode_checked_region();
+    bool eliminate_original_data();
+    bool multiply_lower_triangle();
+    Result back_substitution();
+};
+
+} // namespace tamd

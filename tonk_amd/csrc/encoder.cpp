@@ -1,0 +1,560 @@
+// encoder.cpp -- Siamese encoder control plane.  Each function names the reference routine it
+// restates (SiameseEncoder.cpp line numbers); byte work becomes symbolic terms (engine.h).
+#include "encoder.h"
+
+#include <chrono>
+#include <string.h>
+
+namespace tamd {
+
+uint64_t time_msec() {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::milliseconds>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+Encoder::Encoder(Context* ctx, uint32_t row_bytes, HostRelease release, void* user)
+    : ctx_(ctx), row_bytes_(row_bytes), release_(release), user_(user) {
+    // ClearWindow (SiameseEncoder.cpp:64-83)
+    for (unsigned l = 0; l < kLanes; ++l)
+        for (unsigned s = 0; s < kSums; ++s) lanes_[l].next_element[s] = l;
+    ctx_->attach(this);
+}
+
+Encoder::~Encoder() {
+    for (size_t i = 0; i < win_.size(); ++i) drop_original(win_[i]);
+    win_.clear();
+    for (unsigned l = 0; l < kLanes; ++l)
+        for (unsigned s = 0; s < kSums; ++s) lanes_[l].sum[s].release(ctx_->rows);
+    ctx_->detach(this);
+}
+
+void Encoder::drop_original(StoredOriginal& o) {
+    if (o.row != kNoRow) ctx_->rows.free_deferred(o.row);
+    if (o.host && release_) release_(o.host, user_);
+    o = StoredOriginal();
+}
+
+void Encoder::pre_flush() {
+    for (unsigned l = 0; l < kLanes; ++l)
+        for (unsigned s = 0; s < kSums; ++s) lanes_[l].sum[s].flush(ctx_->rows, ctx_->pb, ctx_->ex, row_bytes_);
+}
+
+// EncoderPacketWindow::Add (SiameseEncoder.cpp:85-161)
+Result Encoder::add(RowId row, uint32_t framed_bytes, uint32_t header_bytes, uint32_t payload_bytes,
+                    void* host, uint32_t* packet_num) {
+    if (disabled_) return kDisabled;
+    if (remaining_slots() <= 0) return kMaxPacketsReached;
+
+    const uint32_t column = next_column_;
+    uint32_t element = count_;
+    *packet_num = column;
+
+    if (count_ > 0) {
+        ++count_;
+    } else {
+        element = column % kLanes;
+        start_new_window(column);
+    }
+    // Elements below `element` in a fresh window are never read (placeholders).
+    while (win_.size() < element) win_.push_back(StoredOriginal());
+    StoredOriginal o;
+    o.row = row;
+    o.bytes = framed_bytes;
+    o.column = column;
+    o.header_bytes = header_bytes;
+    o.send_msec = (uint32_t)time_msec();
+    o.host = host;
+    if (win_.size() == element) win_.push_back(o);
+    else { drop_original(win_[element]); win_[element] = o; }
+
+    next_column_ = col_inc(next_column_);
+
+    Lane& lane = lanes_[column % kLanes];
+    if (lane.longest < framed_bytes) lane.longest = framed_bytes;
+    if (longest_ < framed_bytes) longest_ = framed_bytes;
+
+    stats_[0]++;
+    stats_[1] += payload_bytes;
+    return kSuccess;
+}
+
+// EncoderPacketWindow::StartNewWindow (SiameseEncoder.cpp:163-181)
+void Encoder::start_new_window(uint32_t column) {
+    // Everything from the previous window is unreachable once Count reached zero.
+    for (size_t i = 0; i < win_.size(); ++i) drop_original(win_[i]);
+    win_.clear();
+    const uint32_t element = column % kLanes;
+    column_start_ = column - element;
+    sum_start_ = element;
+    sum_end_ = element;
+    first_unremoved_ = element;
+    count_ = element + 1;
+    longest_ = 0;
+    for (unsigned l = 0; l < kLanes; ++l) lanes_[l].longest = 0;
+}
+
+// EncoderPacketWindow::RemoveBefore (SiameseEncoder.cpp:183-216)
+void Encoder::remove_before(uint32_t first_kept_column) {
+    if (disabled_) return;
+    const uint32_t e = to_element(first_kept_column);
+    if (e >= count_) {
+        if (!col_delta_negative(e)) count_ = 0;  // removed everything
+    } else if (first_unremoved_ < e) {
+        first_unremoved_ = e;
+    }
+}
+
+// EncoderPacketWindow::ResetSums (SiameseEncoder.cpp:218-237)
+void Encoder::reset_sums(uint32_t element_start) {
+    for (unsigned l = 0; l < kLanes; ++l) {
+        const uint32_t next = next_lane_element(element_start, l);
+        for (unsigned s = 0; s < kSums; ++s) {
+            lanes_[l].next_element[s] = next;
+            lanes_[l].sum[s].reset(ctx_->rows);
+        }
+    }
+    sum_start_ = element_start;
+    sum_end_ = element_start;
+    sum_column_start_ = to_column(element_start);
+    sum_erased_ = 0;
+}
+
+// EncoderPacketWindow::RemoveElements (SiameseEncoder.cpp:239-357)
+void Encoder::remove_elements() {
+    const uint32_t first_kept_sub = first_unremoved_ / kSubwindow;
+    const uint32_t removed = first_kept_sub * kSubwindow;
+
+    if (sum_end_ > sum_start_) {
+        for (unsigned l = 0; l < kLanes; ++l) {
+            for (unsigned s = 0; s < kSums; ++s) {
+                get_sum(l, s, removed);
+                lanes_[l].next_element[s] -= removed;
+            }
+        }
+        if (removed > sum_start_) sum_erased_ += removed - sum_start_;
+        sum_end_ = sum_end_ > removed ? sum_end_ - removed : 0;
+        sum_start_ = sum_start_ > removed ? sum_start_ - removed : 0;
+    }
+
+    for (uint32_t i = 0; i < removed && i < win_.size(); ++i) drop_original(win_[i]);
+    win_.pop_front(removed);
+    count_ -= removed;
+    column_start_ = to_column(removed);
+    first_unremoved_ -= removed;
+
+    uint32_t longest = 0, lane_longest[kLanes] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (uint32_t i = first_unremoved_; i < count_; ++i) {
+        const uint32_t b = win_[i].bytes;
+        if (longest < b) longest = b;
+        if (lane_longest[i % kLanes] < b) lane_longest[i % kLanes] = b;
+    }
+    longest_ = longest;
+    for (unsigned l = 0; l < kLanes; ++l) lanes_[l].longest = lane_longest[l];
+
+    if (sum_end_ <= sum_start_) reset_sums(first_unremoved_);
+}
+
+// EncoderPacketWindow::GetSum (SiameseEncoder.cpp:359-418)
+Chain& Encoder::get_sum(uint32_t lane_index, uint32_t sum_index, uint32_t element_end) {
+    Lane& lane = lanes_[lane_index];
+    Chain& sum = lane.sum[sum_index];
+    uint32_t element = lane.next_element[sum_index];
+    if (element < element_end) {
+        if (lane.longest > 0) sum.grow(lane.longest);
+        do {
+            const StoredOriginal& o = win_[element];
+            const uint32_t add = o.bytes;
+            sum.grow(add);
+            uint8_t cx = 1;
+            if (sum_index > 0) {
+                cx = column_value(o.column);
+                if (sum_index == 2) cx = gf_sqr(cx);
+            }
+            sum.accumulate(ctx_->rows, o.row, add, cx);
+            element += kLanes;
+        } while (element < element_end);
+        lane.next_element[sum_index] = element;
+    }
+    return sum;
+}
+
+// ---- acknowledgements (SiameseEncoder.cpp:514-800) ----
+
+bool Encoder::on_ack_data(const uint8_t* data, uint32_t bytes) {
+    unsigned next = 0;
+    const int hb = get_pnum_header(data, (int)bytes, next);
+    if (hb < 1) return false;
+    data += hb;
+    bytes -= (uint32_t)hb;
+
+    if (col_delta_negative(col_sub(next, ack_.next_expected))) return true;  // out of order
+
+    if (ack_.next_expected == next && ack_.have_data && bytes == ack_.data_bytes &&
+        (bytes == 0 || memcmp(data, ack_.data.data(), bytes) == 0))
+        return true;  // duplicate
+
+    ack_.next_expected = next;
+    ack_.offset = 0;
+    ack_.loss_column = next;
+    ack_.loss_count = 0;
+    ack_.data_bytes = bytes;
+    if (bytes > 0) {
+        ack_.data.assign(data, data + bytes);
+        ack_.data.resize((size_t)bytes + 8, 0);
+        ack_.have_data = true;
+        if (!decode_next_range()) return false;
+    }
+    update_rto();
+    remove_before(ack_.next_expected);
+    return true;
+}
+
+// WindowedMinMax<.., WindowedMaxCompare>::Update (SiameseTools.h:184-235)
+void Encoder::rtt_update(uint32_t value, uint64_t now, uint64_t window) {
+    auto* s = ack_.max_rtt;
+    auto expired = [&](int i, uint64_t w) { return (uint64_t)(now - s[i].ts) > w; };
+    if (s[0].value == 0 || value >= s[0].value || expired(2, window)) {
+        s[0].value = s[1].value = s[2].value = value;
+        s[0].ts = s[1].ts = s[2].ts = now;
+        return;
+    }
+    if (value >= s[1].value) { s[1].value = s[2].value = value; s[1].ts = s[2].ts = now; }
+    else if (value >= s[2].value) { s[2].value = value; s[2].ts = now; }
+    if (expired(0, window)) {
+        if (expired(1, window)) { s[0] = s[2]; s[1].value = value; s[1].ts = now; }
+        else { s[0] = s[1]; s[1] = s[2]; }
+        s[2].value = value;
+        s[2].ts = now;
+        return;
+    }
+    if (s[1].value == s[0].value && expired(1, window / 4)) {
+        s[1].value = s[2].value = value;
+        s[1].ts = s[2].ts = now;
+        return;
+    }
+    if (s[2].value == s[1].value && expired(2, window / 2)) { s[2].value = value; s[2].ts = now; }
+}
+
+// EncoderAcknowledgementState::UpdateRTO (SiameseEncoder.cpp:584-723)
+void Encoder::update_rto() {
+    const uint32_t window_count = count_;
+    uint32_t first_loss = to_element(ack_.next_expected);
+    if (first_loss >= window_count) return;
+
+    const uint64_t now64 = time_msec();
+    const uint32_t now = (uint32_t)now64;
+    uint32_t longest = 0;
+
+    uint32_t element = to_element(ack_.next_rto_column);
+    if (element >= window_count) element = first_unremoved_;
+
+    for (; element < first_loss; ++element) {
+        const int32_t d = (int32_t)(now - win_[element].send_msec);
+        if ((uint32_t)d > longest && d > 0) longest = (uint32_t)d;
+    }
+
+    uint32_t remaining = ack_.data_bytes;
+    const uint8_t* data = ack_.data.data();
+    while (remaining > 0) {
+        unsigned rel = 0, lossM1 = 0;
+        const int n = get_nack_range(data, remaining + 8, rel, lossM1);
+        if (n < 0 || n > (int)remaining) return;
+        data += n;
+        remaining -= (uint32_t)n;
+        if (element + 1 < first_loss) element = first_loss - 1;
+        first_loss += rel;
+        for (; element < first_loss; ++element) {
+            if (element >= window_count) return;
+            const int32_t d = (int32_t)(now - win_[element].send_msec);
+            if ((uint32_t)d > longest && d > 0) longest = (uint32_t)d;
+        }
+        first_loss += lossM1 + 2;
+    }
+    ack_.next_rto_column = to_column(element);
+    if (longest <= 0) return;
+
+    uint64_t window = (uint64_t)ack_.rto_msec * 2;
+    if (window < 100) window = 100;
+    else if (window > 4000) window = 4000;
+    rtt_update(longest, now64, window);
+    ack_.rto_msec = (ack_.max_rtt[0].value * 3) / 2;
+    if (ack_.rto_msec < 20) ack_.rto_msec = 20;
+}
+
+// EncoderAcknowledgementState::DecodeNextRange (SiameseEncoder.cpp:725-755)
+bool Encoder::decode_next_range() {
+    if (ack_.offset >= ack_.data_bytes) return false;
+    unsigned rel = 0, lossM1 = 0;
+    const int n = get_nack_range(ack_.data.data() + ack_.offset, ack_.data_bytes + 8 - ack_.offset, rel, lossM1);
+    if (n < 0) return false;
+    ack_.offset += (uint32_t)n;
+    if (ack_.offset > ack_.data_bytes) return false;
+    ack_.loss_column = col_add(ack_.loss_column, rel);
+    ack_.loss_count = lossM1 + 1;
+    return true;
+}
+
+// GetNextLossColumn (SiameseEncoder.cpp:757-777)
+bool Encoder::next_loss_column(uint32_t& column) {
+    if (ack_.loss_count <= 0) {
+        ack_.loss_column = col_inc(ack_.loss_column);
+        if (!decode_next_range()) return false;
+    }
+    column = ack_.loss_column;
+    ack_.loss_column = col_inc(ack_.loss_column);
+    --ack_.loss_count;
+    return true;
+}
+
+// RestartLossIterator (SiameseEncoder.cpp:779-788)
+void Encoder::restart_loss_iterator() {
+    ack_.offset = 0;
+    ack_.loss_column = ack_.next_expected;
+    ack_.loss_count = 0;
+    decode_next_range();
+}
+
+// Encoder::Acknowledge (SiameseEncoder.cpp:814-833)
+Result Encoder::acknowledge(const uint8_t* data, uint32_t bytes, uint32_t* next_expected) {
+    if (disabled_) return kDisabled;
+    if (!on_ack_data(data, bytes)) return kInvalidInput;
+    *next_expected = ack_.next_expected;
+    stats_[6]++;
+    stats_[7] += bytes;
+    return kSuccess;
+}
+
+Result Encoder::attempt_retransmit(const StoredOriginal* o, const StoredOriginal** out) {
+    if (o->header_bytes == 0 || o->bytes <= o->header_bytes) { disabled_ = true; return kDisabled; }
+    *out = o;
+    stats_[4]++;
+    stats_[5] += o->bytes - o->header_bytes;
+    return kSuccess;
+}
+
+// Encoder::Retransmit (SiameseEncoder.cpp:877-1044)
+Result Encoder::retransmit(const StoredOriginal** out) {
+    *out = nullptr;
+    if (disabled_) return kDisabled;
+    if (unacked() == 0) {
+        ack_.found_oldest = false;
+        return kNeedMoreData;
+    }
+    const uint32_t first = col_sub(ack_.next_expected, column_start_);
+    const uint32_t count = count_;
+    if (col_delta_negative(first) || first < first_unremoved_ || first >= count) return kNeedMoreData;
+
+    const uint32_t now = (uint32_t)time_msec();
+    const uint32_t rto = ack_.rto_msec;
+
+    if (ack_.found_oldest) {
+        const uint32_t e = col_sub(ack_.oldest_column, column_start_);
+        if (!col_delta_negative(e) && e >= first && e < count) {
+            StoredOriginal& o = win_[e];
+            if ((uint32_t)(now - o.send_msec) < rto) return kNeedMoreData;
+            o.send_msec = now;
+            ack_.found_oldest = false;
+            return attempt_retransmit(&o, out);
+        }
+        ack_.found_oldest = false;
+    }
+
+    uint32_t nack_element = first;
+    StoredOriginal* oldest = &win_[nack_element];
+    uint32_t oldest_msec = oldest->send_msec;
+    if ((uint32_t)(now - oldest_msec) >= rto) {
+        oldest->send_msec = now;
+        return attempt_retransmit(oldest, out);
+    }
+
+    if (ack_.data_bytes > 0) {
+        restart_loss_iterator();
+        uint32_t column = 0;
+        while (next_loss_column(column)) {
+            nack_element = to_element(column);
+            if (nack_element >= count) break;
+            StoredOriginal& o = win_[nack_element];
+            const uint32_t last = o.send_msec;
+            if ((uint32_t)(now - last) >= rto) {
+                o.send_msec = now;
+                return attempt_retransmit(&o, out);
+            }
+            if ((int32_t)(oldest_msec - last) > 0) { oldest = &o; oldest_msec = last; }
+        }
+    }
+
+    for (uint32_t e = nack_element + 1; e < count; ++e) {
+        StoredOriginal& o = win_[e];
+        const uint32_t last = o.send_msec;
+        if ((uint32_t)(now - last) >= rto) {
+            o.send_msec = now;
+            return attempt_retransmit(&o, out);
+        }
+        if ((int32_t)(oldest_msec - last) > 0) { oldest = &o; oldest_msec = last; }
+    }
+    ack_.found_oldest = true;
+    ack_.oldest_column = oldest->column;
+    return kNeedMoreData;
+}
+
+// Encoder::Get (SiameseEncoder.cpp:1256-1294)
+Result Encoder::get(uint32_t packet_num, const StoredOriginal** out) {
+    *out = nullptr;
+    if (disabled_) return kDisabled;
+    const uint32_t e = to_element(packet_num);
+    if (e >= count_) return kNeedMoreData;
+    const StoredOriginal& o = win_[e];
+    if (o.bytes == 0) return kNeedMoreData;
+    if (o.header_bytes == 0 || o.bytes <= o.header_bytes) { disabled_ = true; return kDisabled; }
+    *out = &o;
+    return kSuccess;
+}
+
+// ---- recovery generation ----
+
+Result Encoder::emit(const Sym& terms_in, uint32_t len, const RecoveryMeta& meta, RecoveryOut& out) {
+    Sym terms = terms_in;
+    sym_merge(terms);
+    out.meta = meta;
+    out.footer_len = put_recovery_footer(meta, out.footer);
+    out.data_len = len;
+    out.row = ctx_->alloc(len + out.footer_len);
+    if (out.row == kNoRow) { disabled_ = true; return kDisabled; }
+    ctx_->pb.combine(out.row, terms.data(), terms.size(), len, out.footer, out.footer_len);
+    stats_[2]++;
+    stats_[3] += out.total();
+    return kSuccess;
+}
+
+// Encoder::GenerateSinglePacket (SiameseEncoder.cpp:1296-1329)
+Result Encoder::generate_single(RecoveryOut& out) {
+    const StoredOriginal& o = win_[first_unremoved_];
+    RecoveryMeta m;
+    m.SumCount = 1;
+    m.LDPCCount = 1;
+    m.ColumnStart = o.column;
+    m.Row = 0;
+    Sym t;
+    t.push_back(Term{o.row, o.bytes, 1});
+    return emit(t, o.bytes, m, out);
+}
+
+// Encoder::GenerateCauchyPacket (SiameseEncoder.cpp:1334-1441)
+Result Encoder::generate_cauchy(RecoveryOut& out) {
+    const uint32_t first = first_unremoved_;
+    RecoveryMeta m;
+    m.SumCount = unacked();
+    m.LDPCCount = m.SumCount;
+    m.ColumnStart = to_column(first);
+    uint32_t used = 0;
+    Sym t;
+    t.reserve(count_ - first);
+
+    const uint32_t next_parity = to_element(next_parity_column_);
+    if (next_parity <= first || col_delta_negative(next_parity)) {
+        next_parity_column_ = col_add(m.ColumnStart, m.SumCount);
+        m.Row = 0;
+        for (uint32_t e = first; e < count_; ++e) {
+            const StoredOriginal& o = win_[e];
+            t.push_back(Term{o.row, o.bytes, 1});
+            if (used < o.bytes) used = o.bytes;
+        }
+    } else {
+        const uint32_t crow = next_cauchy_row_;
+        m.Row = crow + 1;
+        if (++next_cauchy_row_ >= kCauchyMaxRows) next_cauchy_row_ = 0;
+        uint32_t ccol = m.ColumnStart % kCauchyMaxColumns;
+        for (uint32_t e = first; e < count_; ++e) {
+            const StoredOriginal& o = win_[e];
+            t.push_back(Term{o.row, o.bytes, cauchy_element(crow, ccol)});
+            if (used < o.bytes) used = o.bytes;
+            ccol = (ccol + 1) % kCauchyMaxColumns;
+        }
+    }
+    return emit(t, used, m, out);
+}
+
+// Encoder::AddDenseColumns (SiameseEncoder.cpp:1046-1098)
+void Encoder::add_dense(uint32_t row, uint32_t recovery_bytes, Sym& rec, Sym& prod) {
+    for (unsigned l = 0; l < kLanes; ++l) {
+        const unsigned op = row_opcode(l, row);
+        for (unsigned s = 0; s < kSums; ++s) {
+            if (op & (1u << s)) {
+                Chain& c = get_sum(l, s, count_);
+                const uint32_t n = c.bytes < recovery_bytes ? c.bytes : recovery_bytes;
+                if (n) c.read(ctx_->rows, ctx_->ex, rec, n, 1);
+            }
+        }
+        for (unsigned s = 0; s < kSums; ++s) {
+            if (op & (1u << (s + 3))) {
+                Chain& c = get_sum(l, s, count_);
+                const uint32_t n = c.bytes < recovery_bytes ? c.bytes : recovery_bytes;
+                if (n) c.read(ctx_->rows, ctx_->ex, prod, n, 1);
+            }
+        }
+    }
+    sum_end_ = count_;
+}
+
+// Encoder::AddLightColumns (SiameseEncoder.cpp:1100-1144)
+void Encoder::add_light(uint32_t row, Sym& rec, Sym& prod) {
+    const uint32_t start = first_unremoved_;
+    const uint32_t count = sum_end_ - start;
+    Pcg32 prng;
+    prng.seed(row, count);
+    const uint32_t pairs = (count + kPairRate - 1) / kPairRate;
+    for (uint32_t i = 0; i < pairs; ++i) {
+        const uint32_t e1 = start + prng.next() % count;
+        const uint32_t erx = start + prng.next() % count;
+        const StoredOriginal& o1 = win_[e1];
+        const StoredOriginal& orx = win_[erx];
+        rec.push_back(Term{o1.row, o1.bytes, 1});
+        prod.push_back(Term{orx.row, orx.bytes, 1});
+    }
+}
+
+// Encoder::Encode (SiameseEncoder.cpp:1146-1254)
+Result Encoder::encode(RecoveryOut& out) {
+    out = RecoveryOut();
+    if (disabled_) return kDisabled;
+    if (count_ <= 0) return kNeedMoreData;
+    if (first_unremoved_ >= kRemoveThreshold) remove_elements();
+
+    const uint32_t un = unacked();
+    if (un == 1) return generate_single(out);
+
+    const uint32_t ub = count_ - sum_start_ + sum_erased_;
+    if (sum_end_ <= sum_start_ || ub >= kMaxPackets) {
+        if (un <= kCauchyThreshold) return generate_cauchy(out);
+        reset_sums(first_unremoved_);
+    } else if (un <= kSumResetThreshold || ub <= kCauchyThreshold) {
+        sum_end_ = sum_start_;
+        return generate_cauchy(out);
+    }
+
+    const uint32_t row = next_row_;
+    if (++next_row_ >= kRowPeriod) next_row_ = 0;
+
+    const uint32_t recovery_bytes = longest_;
+    Sym rec, prod;
+    add_dense(row, recovery_bytes, rec, prod);
+    add_light(row, rec, prod);
+    sym_add(rec, prod, recovery_bytes, row_value(row));
+
+    RecoveryMeta m;
+    m.SumCount = sum_end_ - sum_start_ + sum_erased_;
+    m.LDPCCount = un;
+    m.ColumnStart = sum_column_start_;
+    m.Row = row;
+    sym_clip(rec, recovery_bytes);
+    return emit(rec, recovery_bytes, m, out);
+}
+
+// Encoder::GetStatistics (SiameseEncoder.cpp:1445-1457)
+void Encoder::stats(uint64_t* out, unsigned n) {
+    if (n > 9) n = 9;
+    stats_[8] = ctx_->rows.bytes_in_use();
+    for (unsigned i = 0; i < n; ++i) out[i] = stats_[i];
+}
+
+} // namespace tamd

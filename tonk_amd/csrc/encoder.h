@@ -1,0 +1,138 @@
+// encoder.h -- Siamese encoder control plane (restates SiameseEncoder.h/.cpp of the reference).
+//
+// State machine identical to the reference: packet window in element order (element % 8 ==
+// column % 8), 8 lanes x 3 lazily accumulated running sums, Cauchy/parity rows while few
+// packets are in flight and Siamese rows (dense sums + LDPC pairs + RX product) otherwise,
+// acknowledgement ingest with NACK-range RTO estimation and retransmit selection.  The only
+// difference is that recovery bytes are not computed here: each recovery packet becomes one
+// combine op (plus running-sum scans) in the context's device program.
+#pragma once
+
+#include "engine.h"
+#include "ring.h"
+#include "serial.h"
+
+#include <stdint.h>
+
+namespace tamd {
+
+enum Result {  // siamese.h SiameseResult values
+    kSuccess = 0, kInvalidInput = 1, kNeedMoreData = 2, kMaxPacketsReached = 3,
+    kDuplicateData = 4, kDisabled = 5
+};
+
+struct RecoveryOut {
+    RowId row = kNoRow;       // device row: data (data_len bytes) then the footer
+    uint32_t data_len = 0;
+    uint32_t footer_len = 0;
+    uint8_t footer[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    RecoveryMeta meta;
+    uint32_t total() const { return data_len + footer_len; }
+};
+
+// An original packet as the codec stores it: a device row holding varint(len) || payload.
+struct StoredOriginal {
+    RowId row = kNoRow;
+    uint32_t bytes = 0;         // framed bytes (Buffer.Bytes)
+    uint32_t column = 0;
+    uint32_t header_bytes = 0;
+    uint32_t send_msec = 0;     // encoder only (retransmit timing)
+    void* host = nullptr;       // optional host mirror (C-ABI: siamese_encoder_get/retransmit)
+};
+
+typedef void (*HostRelease)(void* host, void* user);
+
+class Encoder : public FlushClient {
+public:
+    Encoder(Context* ctx, uint32_t row_bytes, HostRelease release = nullptr, void* user = nullptr);
+    ~Encoder();
+
+    unsigned remaining_slots() const { return kMaxPackets - count_; }
+
+    // siamese_encoder_add: the caller provides the framed row already written to the arena.
+    // Ownership of `row` (and `host`) passes to the encoder on success.
+    Result add(RowId row, uint32_t framed_bytes, uint32_t header_bytes, uint32_t payload_bytes,
+               void* host, uint32_t* packet_num);
+    Result get(uint32_t packet_num, const StoredOriginal** out);
+    void remove_before(uint32_t first_kept_column);
+    Result acknowledge(const uint8_t* data, uint32_t bytes, uint32_t* next_expected);
+    Result retransmit(const StoredOriginal** out);
+    // siamese_encode.  On success `out.row` is owned by the caller (free it with
+    // ctx->rows.free_deferred once nothing reads it).
+    Result encode(RecoveryOut& out);
+    void stats(uint64_t* out, unsigned n);
+
+    bool disabled() const { return disabled_; }
+    uint64_t stat(unsigned i) const { return stats_[i]; }
+
+    // FlushClient
+    void pre_flush() override;
+    void post_flush() override {}
+
+private:
+    Context* ctx_;
+    uint32_t row_bytes_;
+    HostRelease release_;
+    void* user_;
+    uint64_t stats_[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    bool disabled_ = false;
+
+    // ---- EncoderPacketWindow (SiameseEncoder.h:104-232) ----
+    Ring<StoredOriginal> win_;
+    uint32_t next_column_ = 0, count_ = 0, column_start_ = 0, longest_ = 0;
+    uint32_t first_unremoved_ = 0;
+    uint32_t sum_start_ = 0, sum_end_ = 0, sum_column_start_ = 0, sum_erased_ = 0;
+    struct Lane {
+        uint32_t next_element[kSums];
+        Chain sum[kSums];
+        uint32_t longest = 0;
+    } lanes_[kLanes];
+
+    // ---- acknowledgement state (SiameseEncoder.h:239-327) ----
+    struct Ack {
+        std::vector<uint8_t> data;   // NACK bytes + 8 zero guard bytes
+        bool have_data = false;      // reference: Data != nullptr
+        uint32_t data_bytes = 0, offset = 0, loss_column = 0, loss_count = 0;
+        uint32_t next_expected = 0, next_rto_column = 0;
+        bool found_oldest = false;
+        uint32_t oldest_column = 0;
+        uint32_t rto_msec = 500;
+        struct Sample { uint32_t value; uint64_t ts; } max_rtt[3] = {{0, 0}, {0, 0}, {0, 0}};
+    } ack_;
+
+    uint32_t next_row_ = 0, next_parity_column_ = 0, next_cauchy_row_ = 0;
+
+    uint32_t to_element(uint32_t column) const { return col_sub(column, column_start_); }
+    uint32_t to_column(uint32_t element) const { return col_add(element, column_start_); }
+    uint32_t unacked() const { return count_ - first_unremoved_; }
+    StoredOriginal& elem(uint32_t e) { return win_[e]; }
+    uint32_t next_lane_element(uint32_t element, uint32_t lane) const {
+        uint32_t n = element - (element % kLanes) + lane;
+        if (n < element) n += kLanes;
+        return n;
+    }
+
+    void drop_original(StoredOriginal& o);
+    void start_new_window(uint32_t column);
+    void reset_sums(uint32_t element_start);
+    void remove_elements();
+    Chain& get_sum(uint32_t lane, uint32_t sum, uint32_t element_end);
+
+    bool decode_next_range();
+    bool next_loss_column(uint32_t& column);
+    void restart_loss_iterator();
+    bool on_ack_data(const uint8_t* data, uint32_t bytes);
+    void update_rto();
+    void rtt_update(uint32_t value, uint64_t now, uint64_t window);
+    Result attempt_retransmit(const StoredOriginal* o, const StoredOriginal** out);
+
+    Result generate_single(RecoveryOut& out);
+    Result generate_cauchy(RecoveryOut& out);
+    void add_dense(uint32_t row, uint32_t recovery_bytes, Sym& rec, Sym& prod);
+    void add_light(uint32_t row, Sym& rec, Sym& prod);
+    Result emit(const Sym& terms, uint32_t len, const RecoveryMeta& meta, RecoveryOut& out);
+};
+
+uint64_t time_msec();
+
+} // namespace tamd

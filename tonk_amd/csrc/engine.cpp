@@ -1,0 +1,389 @@
+// engine.cpp -- see engine.h.
+#include "engine.h"
+
+#include <string.h>
+
+namespace tamd {
+
+// ---------------------------------------------------------------------------------------------
+// RowTable
+// ---------------------------------------------------------------------------------------------
+static const uint32_t kSmallClasses = 256;  // rows up to 16 KB use exact-size free lists
+
+void RowTable::init(uint64_t arena_bytes) {
+    const uint64_t units = arena_bytes / TAMD_ROW_UNIT;
+    total_units_ = units > 0xfffffff0ull ? 0xfffffff0u : (uint32_t)units;
+    bump_ = 0;
+    used_units_ = 0;
+    live_ = 0;
+    meta_.clear();
+    free_handles_.clear();
+    free_offsets_.assign(kSmallClasses + 1, std::vector<uint32_t>());
+    free_big_.clear();
+    pending_.clear();
+    unsealed_.clear();
+}
+
+RowId RowTable::alloc(uint32_t bytes) {
+    uint32_t units = (bytes + TAMD_ROW_UNIT - 1) / TAMD_ROW_UNIT;
+    if (units == 0) units = 1;
+    uint32_t off = 0xffffffffu;
+    if (units <= kSmallClasses && !free_offsets_[units].empty()) {
+        off = free_offsets_[units].back();
+        free_offsets_[units].pop_back();
+    } else if (units > kSmallClasses) {
+        for (size_t i = 0; i < free_big_.size(); ++i) {
+            if (free_big_[i].second == units) {
+                off = free_big_[i].first;
+                free_big_[i] = free_big_.back();
+                free_big_.pop_back();
+                break;
+            }
+        }
+    }
+    if (off == 0xffffffffu) {
+        if ((uint64_t)bump_ + units > total_units_) return kNoRow;
+        off = bump_;
+        bump_ += units;
+    }
+    RowId h;
+    if (!free_handles_.empty()) {
+        h = free_handles_.back();
+        free_handles_.pop_back();
+    } else {
+        h = (RowId)meta_.size();
+        meta_.push_back(Meta());
+    }
+    meta_[h].off = off;
+    meta_[h].units = units;
+    meta_[h].level = 0;
+    used_units_ += units;
+    ++live_;
+    return h;
+}
+
+void RowTable::release(RowId r) {
+    const Meta& m = meta_[r];
+    if (m.units <= kSmallClasses) free_offsets_[m.units].push_back(m.off);
+    else free_big_.push_back(std::make_pair(m.off, m.units));
+    used_units_ -= m.units;
+    --live_;
+    free_handles_.push_back(r);
+}
+
+void RowTable::free_deferred(RowId r) {
+    if (r != kNoRow) unsealed_.push_back(r);
+}
+
+void RowTable::seal_epoch(uint64_t epoch) {
+    for (RowId r : unsealed_) pending_.push_back(Pending{epoch, r});
+    unsealed_.clear();
+}
+
+void RowTable::release_up_to(uint64_t completed) {
+    size_t k = 0;
+    for (size_t i = 0; i < pending_.size(); ++i) {
+        if (pending_[i].epoch <= completed) release(pending_[i].row);
+        else pending_[k++] = pending_[i];
+    }
+    pending_.resize(k);
+}
+
+// ---------------------------------------------------------------------------------------------
+// ProgramBuilder
+// ---------------------------------------------------------------------------------------------
+void ProgramBuilder::clear() {
+    ops_.clear();
+    instrs_.clear();
+    levels_.clear();
+    written_.clear();
+    max_level_ = 0;
+    acc_bytes_ = store_bytes_ = 0;
+}
+
+void ProgramBuilder::begin_op() {
+    cur_first_ = (uint32_t)instrs_.size();
+    cur_span_ = 0;
+    cur_level_in_ = 0;
+    cur_written_begin_ = written_.size();
+}
+
+void ProgramBuilder::op_acc(RowId src, uint8_t coef, uint32_t len) {
+    if (!coef || !len) return;
+    tamd_instr in;
+    in.w0 = tamd_w0(TAMD_I_ACC, coef);
+    in.row = rows_->offset(src);
+    in.len = len;
+    in.cap = 0;
+    instrs_.push_back(in);
+    if (len > cur_span_) cur_span_ = len;
+    const uint32_t l = rows_->level(src);
+    if (l > cur_level_in_) cur_level_in_ = l;
+    acc_bytes_ += len;
+}
+
+static void push_store(std::vector<tamd_instr>& v, uint32_t off, uint32_t len, uint32_t cap,
+                       const uint8_t* footer, uint32_t flen) {
+    tamd_instr s;
+    s.w0 = tamd_w0(TAMD_I_STORE, flen);
+    s.row = off;
+    s.len = len;
+    s.cap = cap;
+    v.push_back(s);
+    tamd_instr f;
+    uint8_t fb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (flen) memcpy(fb, footer, flen);
+    f.w0 = tamd_w0(TAMD_I_FOOTER, 0);
+    memcpy(&f.row, fb, 4);
+    memcpy(&f.len, fb + 4, 4);
+    f.cap = 0;
+    v.push_back(f);
+}
+
+void ProgramBuilder::op_store(RowId dst, uint32_t len) {
+    const uint32_t cap = rows_->cap_bytes(dst);
+    push_store(instrs_, rows_->offset(dst), len, cap, nullptr, 0);
+    if (cap > cur_span_) cur_span_ = cap;
+    written_.push_back(dst);
+    store_bytes_ += len;
+}
+
+uint32_t ProgramBuilder::end_op(uint32_t min_level) {
+    uint32_t level = cur_level_in_ + 1;
+    if (level < min_level) level = min_level;
+    tamd_op op;
+    op.first = cur_first_;
+    op.count = (uint32_t)instrs_.size() - cur_first_;
+    op.span = (cur_span_ + 7u) & ~7u;
+    op.tag = level;
+    ops_.push_back(op);
+    levels_.push_back(level);
+    for (size_t i = cur_written_begin_; i < written_.size(); ++i) rows_->set_level(written_[i], level);
+    if (level > max_level_) max_level_ = level;
+    return level;
+}
+
+uint32_t ProgramBuilder::combine(RowId dst, const Term* terms, size_t n, uint32_t len,
+                                 const uint8_t* footer, uint32_t footer_len) {
+    begin_op();
+    for (size_t i = 0; i < n; ++i) op_acc(terms[i].row, terms[i].coef, terms[i].len);
+    const uint32_t cap = rows_->cap_bytes(dst);
+    push_store(instrs_, rows_->offset(dst), len, cap, footer, footer_len);
+    if (cap > cur_span_) cur_span_ = cap;
+    if (len > cur_span_) cur_span_ = len;
+    written_.push_back(dst);
+    store_bytes_ += len + footer_len;
+    return end_op(1);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Term lists
+// ---------------------------------------------------------------------------------------------
+void sym_merge(Sym& s) {
+    if (s.size() < 2) return;
+    std::sort(s.begin(), s.end(), [](const Term& a, const Term& b) {
+        return a.row != b.row ? a.row < b.row : a.len < b.len;
+    });
+    size_t k = 0;
+    for (size_t i = 0; i < s.size();) {
+        Term t = s[i];
+        size_t j = i + 1;
+        while (j < s.size() && s[j].row == t.row && s[j].len == t.len) { t.coef ^= s[j].coef; ++j; }
+        if (t.coef) s[k++] = t;
+        i = j;
+    }
+    s.resize(k);
+}
+
+// ---------------------------------------------------------------------------------------------
+// ExpansionTable
+// ---------------------------------------------------------------------------------------------
+void ExpansionTable::set(RowId r, const Sym& s) {
+    if (r >= index_.size()) index_.resize((size_t)r + 1, -1);
+    if (index_[r] >= 0) { pool_[index_[r]] = s; return; }
+    index_[r] = (int32_t)pool_.size();
+    pool_.push_back(s);
+    used_.push_back(r);
+}
+
+void ExpansionTable::clear() {
+    for (RowId r : used_) index_[r] = -1;
+    used_.clear();
+    pool_.clear();
+}
+
+void ExpansionTable::append(const RowTable& rows, RowId r, uint32_t len, uint8_t coef, Sym& out) const {
+    if (!coef || !len) return;
+    if (rows.level(r) == 0 || !has(r)) {
+        out.push_back(Term{r, len, coef});
+        return;
+    }
+    sym_add(out, get(r), len, coef);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Chain
+// ---------------------------------------------------------------------------------------------
+void Chain::reset(RowTable& rows) {
+    if (!snaps_.empty()) {
+        Closed c;
+        c.base = base_;
+        c.content = content_;
+        c.terms.swap(terms_);
+        c.snaps.swap(snaps_);
+        closed_.push_back(std::move(c));
+    } else {
+        rows.free_deferred(base_);
+    }
+    base_ = kNoRow;
+    terms_.clear();
+    snaps_.clear();
+    dyn_.clear();
+    content_ = 0;
+    bytes = 0;
+}
+
+void Chain::accumulate(RowTable& rows, RowId row, uint32_t len, uint8_t coef) {
+    if (!coef || !len) return;
+    if (len > content_) content_ = len;
+    if (rows.level(row) == 0) terms_.push_back(Term{row, len, coef});
+    else dyn_.push_back(DynContribution{row, len, coef});
+}
+
+void Chain::read(RowTable& rows, const ExpansionTable& ex, Sym& out, uint32_t limit, uint8_t coef) {
+    if (!coef || !limit) return;
+    const uint32_t clip = content_ < limit ? content_ : limit;
+    if (!terms_.empty()) {
+        RowId snap;
+        if (!snaps_.empty() && snaps_.back().after == terms_.size()) {
+            snap = snaps_.back().row;
+        } else {
+            snap = rows.alloc(content_);
+            if (snap == kNoRow) return;  // caller checks arena exhaustion via RowTable
+            rows.set_level(snap, 1);
+            snaps_.push_back(Snap{snap, (uint32_t)terms_.size()});
+        }
+        if (clip) out.push_back(Term{snap, clip, coef});
+    } else if (base_ != kNoRow && clip) {
+        out.push_back(Term{base_, clip, coef});
+    }
+    for (const DynContribution& d : dyn_) {
+        const uint32_t l = d.len < limit ? d.len : limit;
+        ex.append(rows, d.row, l, gf_mul(d.coef, coef), out);
+    }
+}
+
+void Chain::emit_scan(RowTable& rows, ProgramBuilder& pb, RowId base, uint32_t content,
+                      const std::vector<Term>& terms, const std::vector<Snap>& snaps,
+                      RowId final_row) {
+    (void)content;
+    pb.begin_op();
+    uint32_t cur = 0;
+    if (base != kNoRow) {
+        pb.op_acc(base, 1, rows.cap_bytes(base));
+    }
+    size_t si = 0;
+    for (size_t i = 0; i <= terms.size(); ++i) {
+        while (si < snaps.size() && snaps[si].after == i) {
+            pb.op_store(snaps[si].row, rows.cap_bytes(snaps[si].row));
+            ++si;
+        }
+        if (i == terms.size()) break;
+        pb.op_acc(terms[i].row, terms[i].coef, terms[i].len);
+        if (terms[i].len > cur) cur = terms[i].len;
+    }
+    if (final_row != kNoRow) pb.op_store(final_row, rows.cap_bytes(final_row));
+    pb.end_op(1);
+}
+
+void Chain::flush(RowTable& rows, ProgramBuilder& pb, const ExpansionTable& ex, uint32_t row_bytes) {
+    (void)row_bytes;
+    for (Closed& c : closed_) {
+        emit_scan(rows, pb, c.base, c.content, c.terms, c.snaps, kNoRow);
+        rows.free_deferred(c.base);
+        for (const Snap& s : c.snaps) rows.free_deferred(s.row);
+    }
+    closed_.clear();
+
+    if (terms_.empty() && dyn_.empty()) {
+        // Nothing accumulated since the last flush: snapshots (if any) alias the base.
+        snaps_.clear();
+        return;
+    }
+
+    RowId state = base_;  // row that holds the static value after the scan
+    bool state_is_new = false;
+    if (!terms_.empty()) {
+        RowId final_row = kNoRow;
+        if (!snaps_.empty() && snaps_.back().after == terms_.size()) {
+            state = snaps_.back().row;
+        } else {
+            final_row = rows.alloc(content_);
+            state = final_row;
+        }
+        emit_scan(rows, pb, base_, content_, terms_, snaps_, final_row);
+        for (const Snap& s : snaps_)
+            if (s.row != state) rows.free_deferred(s.row);
+        state_is_new = true;
+    }
+
+    if (!dyn_.empty()) {
+        // Fold contributions of rows produced by this program into the carried value.
+        Sym t;
+        if (state != kNoRow) t.push_back(Term{state, rows.cap_bytes(state), 1});
+        for (const DynContribution& d : dyn_) ex.append(rows, d.row, d.len, d.coef, t);
+        sym_merge(t);
+        const RowId carry = rows.alloc(content_);
+        pb.combine(carry, t.data(), t.size(), content_);
+        if (state_is_new) rows.free_deferred(state);
+        if (base_ != kNoRow) rows.free_deferred(base_);
+        base_ = carry;
+    } else {
+        if (base_ != kNoRow && base_ != state) rows.free_deferred(base_);
+        base_ = state;
+    }
+    terms_.clear();
+    snaps_.clear();
+    dyn_.clear();
+}
+
+void Chain::release(RowTable& rows) {
+    for (Closed& c : closed_) {
+        rows.free_deferred(c.base);
+        for (const Snap& s : c.snaps) rows.free_deferred(s.row);
+    }
+    closed_.clear();
+    for (const Snap& s : snaps_) rows.free_deferred(s.row);
+    rows.free_deferred(base_);
+    base_ = kNoRow;
+    terms_.clear();
+    snaps_.clear();
+    dyn_.clear();
+    content_ = bytes = 0;
+}
+
+// ---------------------------------------------------------------------------------------------
+RowId fold_low_levels(RowTable& rows, ProgramBuilder& pb, Sym& s, uint32_t keep_level,
+                      uint32_t len, uint32_t row_bytes) {
+    (void)row_bytes;
+    Sym low, high;
+    for (const Term& t : s) {
+        if (rows.level(t.row) < keep_level) low.push_back(t);
+        else high.push_back(t);
+    }
+    sym_merge(low);
+    if (low.empty()) { s.swap(high); return kNoRow; }
+    if (low.size() == 1 && low[0].coef == 1) {
+        high.push_back(low[0]);
+        s.swap(high);
+        return kNoRow;
+    }
+    const RowId r = rows.alloc(len);
+    if (r == kNoRow) return kNoRow;
+    pb.combine(r, low.data(), low.size(), len);
+    high.push_back(Term{r, len, 1});
+    s.swap(high);
+    return r;
+}
+
+} // namespace tamd

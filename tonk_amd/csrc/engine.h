@@ -1,0 +1,289 @@
+// engine.h -- symbolic GF(2^8) row algebra and device-program builder.
+//
+// The control plane (encoder.cpp / decoder.cpp) restates the reference state machines exactly,
+// but every byte buffer of the reference (original packets, running sums, recovery packets,
+// the product workspace, the decoder's recovery rows) is replaced by a symbolic value:
+//
+//     value = XOR over terms of  coef * row[0:len]      (rows zero-padded beyond their data)
+//
+// where `row` is a row of the device arena (HBM).  Every reference gf256_add_mem /
+// gf256_muladd_mem / gf256_mul_mem call becomes a term-list operation on the host, and the
+// values are only *materialized* (an op in the device program) when a result must exist in
+// memory: a recovery packet, a recovered original, a running-sum snapshot, or a decoder
+// elimination ("partial") row.  Because GF(2^8) arithmetic is exact, associative and
+// commutative, the device reproduces the reference bytes exactly no matter how the terms are
+// grouped or ordered.
+//
+// Running sums (SiameseEncoder.cpp:359-418, SiameseDecoder.cpp:1538-1739) are Chains: an
+// in-order list of accumulated terms with snapshot points, executed on the device as ONE scan
+// op per chain per flush (one wave walks the chain for its byte slice and stores a snapshot row
+// at each point), so long sums cost one read per accumulated row, not one per recovery.
+//
+// Levels: a row written by an op in the pending program has level >= 1; ops run level by level
+// (one launch per level), so an op only reads rows of lower levels.  Materialization policies
+// keep the level count small and independent of the number of solves in a flush.
+#pragma once
+
+#include "program.h"
+#include "gf256.h"
+
+#include <stdint.h>
+#include <vector>
+#include <algorithm>
+
+namespace tamd {
+
+using RowId = uint32_t;  // handle into RowTable (not an arena offset)
+static const RowId kNoRow = 0xffffffffu;
+
+struct Term {
+    RowId row;
+    uint32_t len;
+    uint8_t coef;
+};
+
+// A symbolic buffer.  `terms` may contain duplicates; they are merged when materialized.
+typedef std::vector<Term> Sym;
+
+// ---------------------------------------------------------------------------------------------
+// Arena bookkeeping: rows are contiguous ranges of 64-byte units in one device allocation.
+// ---------------------------------------------------------------------------------------------
+class RowTable {
+public:
+    void init(uint64_t arena_bytes);
+    uint64_t arena_bytes() const { return (uint64_t)total_units_ * TAMD_ROW_UNIT; }
+
+    // Allocate a row with capacity >= bytes (rounded up to 64 B).  Returns kNoRow when full.
+    RowId alloc(uint32_t bytes);
+    // Release a row.  The memory is not reused until release_deferred() (called by the owner
+    // once every program that may still read the row has completed on the device).
+    void free_deferred(RowId r);
+    // Make rows freed since the previous call reusable.  `epoch` must be the flush epoch whose
+    // device work has completed.
+    void release_up_to(uint64_t completed_epoch);
+    void seal_epoch(uint64_t epoch);  // rows freed so far belong to `epoch`
+
+    uint32_t offset(RowId r) const { return meta_[r].off; }          // in 64-B units
+    uint32_t cap_bytes(RowId r) const { return meta_[r].units * TAMD_ROW_UNIT; }
+    uint32_t level(RowId r) const { return meta_[r].level; }
+    void set_level(RowId r, uint32_t l) { meta_[r].level = l; }
+    size_t live_rows() const { return live_; }
+    uint64_t bytes_in_use() const { return (uint64_t)used_units_ * TAMD_ROW_UNIT; }
+
+private:
+    struct Meta { uint32_t off, units, level, pad; };
+    std::vector<Meta> meta_;
+    std::vector<RowId> free_handles_;
+    std::vector<std::vector<uint32_t>> free_offsets_;  // by size in units (small sizes)
+    std::vector<std::pair<uint32_t, uint32_t>> free_big_; // (off, units) for large rows
+    struct Pending { uint64_t epoch; RowId row; };
+    std::vector<Pending> pending_;
+    std::vector<RowId> unsealed_;
+    uint32_t total_units_ = 0, bump_ = 0;
+    uint64_t used_units_ = 0;
+    size_t live_ = 0;
+    void release(RowId r);
+};
+
+// ---------------------------------------------------------------------------------------------
+// Device program under construction.
+// ---------------------------------------------------------------------------------------------
+class ProgramBuilder {
+public:
+    explicit ProgramBuilder(RowTable* rows) : rows_(rows) {}
+
+    // Emit `dst[0:len] = sum terms`, followed by `footer` (<= 8 bytes) and zero fill to the
+    // row capacity.  Assigns and returns the op's level (also recorded on dst).
+    uint32_t combine(RowId dst, const Term* terms, size_t n, uint32_t len,
+                     const uint8_t* footer = nullptr, uint32_t footer_len = 0);
+
+    // Raw op construction for scans: begin, add ACC/STORE instructions, end.
+    void begin_op();
+    void op_acc(RowId src, uint8_t coef, uint32_t len);
+    void op_store(RowId dst, uint32_t len);
+    uint32_t end_op(uint32_t min_level = 1);  // returns level; rows stored get that level
+
+    bool empty() const { return ops_.empty(); }
+    void clear();
+    uint32_t max_level() const { return max_level_; }
+
+    const std::vector<tamd_op>& ops() const { return ops_; }
+    const std::vector<tamd_instr>& instrs() const { return instrs_; }
+    const std::vector<uint32_t>& op_levels() const { return levels_; }
+    const std::vector<RowId>& written_rows() const { return written_; }
+
+    uint64_t acc_bytes() const { return acc_bytes_; }       // sum of ACC lengths (op-trace)
+    uint64_t store_bytes() const { return store_bytes_; }
+
+private:
+    RowTable* rows_;
+    std::vector<tamd_op> ops_;
+    std::vector<tamd_instr> instrs_;
+    std::vector<uint32_t> levels_;
+    std::vector<RowId> written_;
+    uint32_t max_level_ = 0;
+    // op under construction
+    uint32_t cur_first_ = 0, cur_span_ = 0, cur_level_in_ = 0;
+    size_t cur_written_begin_ = 0;
+    uint64_t acc_bytes_ = 0, store_bytes_ = 0;
+};
+
+// ---------------------------------------------------------------------------------------------
+// Term-list helpers (all lengths clip like the reference's byte counts).
+// ---------------------------------------------------------------------------------------------
+inline void sym_add(Sym& dst, const Term* src, size_t n, uint32_t limit, uint8_t coef = 1) {
+    if (coef == 0) return;
+    for (size_t i = 0; i < n; ++i) {
+        Term t = src[i];
+        if (t.len > limit) t.len = limit;
+        if (t.len == 0) continue;
+        t.coef = coef == 1 ? t.coef : gf_mul(t.coef, coef);
+        if (t.coef) dst.push_back(t);
+    }
+}
+inline void sym_add(Sym& dst, const Sym& src, uint32_t limit, uint8_t coef = 1) {
+    sym_add(dst, src.data(), src.size(), limit, coef);
+}
+inline void sym_scale(Sym& s, uint8_t coef) {
+    if (coef == 1) return;
+    size_t k = 0;
+    for (size_t i = 0; i < s.size(); ++i) {
+        Term t = s[i];
+        t.coef = gf_mul(t.coef, coef);
+        if (t.coef) s[k++] = t;
+    }
+    s.resize(k);
+}
+inline void sym_clip(Sym& s, uint32_t limit) {
+    size_t k = 0;
+    for (size_t i = 0; i < s.size(); ++i) {
+        Term t = s[i];
+        if (t.len > limit) t.len = limit;
+        if (t.len) s[k++] = t;
+    }
+    s.resize(k);
+}
+// Merge duplicate (row, len) terms, dropping cancelled ones.  Order is not significant.
+void sym_merge(Sym& s);
+
+// ---------------------------------------------------------------------------------------------
+// Running sum (one lane x one sum index) as a chain.
+// ---------------------------------------------------------------------------------------------
+struct DynContribution {
+    RowId row;      // row holding (or that will hold) the contributed data (level > 0)
+    uint32_t len;
+    uint8_t coef;
+};
+
+class ExpansionTable;  // rows produced in the pending program -> their symbolic content
+
+class Chain {
+public:
+    uint32_t bytes = 0;  // logical length, GrowingAlignedDataBuffer::Bytes semantics
+
+    bool empty() const { return base_ == kNoRow && terms_.empty() && dyn_.empty(); }
+    // Reference "Bytes = 0": the contents restart from zero.
+    void reset(RowTable& rows);
+    // GrowZeroPadded: only the logical length changes (data beyond is zero by construction).
+    void grow(uint32_t b) { if (b > bytes) bytes = b; }
+    // sum ^= coef * data  (data = row, possibly produced in the pending program)
+    void accumulate(RowTable& rows, RowId row, uint32_t len, uint8_t coef);
+    // Append the current value, clipped to `limit` bytes and scaled by `coef`, to `out`.
+    void read(RowTable& rows, const ExpansionTable& ex, Sym& out, uint32_t limit, uint8_t coef);
+    // Emit the chain's scan (and fix-up) ops for the pending program and rebase the chain.
+    void flush(RowTable& rows, ProgramBuilder& pb, const ExpansionTable& ex, uint32_t row_bytes);
+    // Drop everything (codec destruction).
+    void release(RowTable& rows);
+
+private:
+    struct Snap { RowId row; uint32_t after; };
+    RowId base_ = kNoRow;        // carry row from a previous flush (level 0)
+    uint32_t content_ = 0;       // bytes the accumulated content may occupy
+    std::vector<Term> terms_;    // level-0 terms accumulated since base_
+    std::vector<Snap> snaps_;
+    std::vector<DynContribution> dyn_;  // contributions from rows produced in this program
+    // closed epochs (reset while the program was pending) still owe their snapshots
+    struct Closed { RowId base; uint32_t content; std::vector<Term> terms; std::vector<Snap> snaps; };
+    std::vector<Closed> closed_;
+    static void emit_scan(RowTable& rows, ProgramBuilder& pb, RowId base, uint32_t content,
+                          const std::vector<Term>& terms, const std::vector<Snap>& snaps,
+                          RowId final_row);
+};
+
+// Symbolic content of rows written by the pending program, so readers in the same flush can
+// use the content's terms instead of the row itself (which would add a level).
+class ExpansionTable {
+public:
+    void set(RowId r, const Sym& s);
+    bool has(RowId r) const { return r < index_.size() && index_[r] >= 0; }
+    const Sym& get(RowId r) const { return pool_[index_[r]]; }
+    void clear();
+    // Append `coef * content(r)[0:len]` to out: the row itself when it is already in memory
+    // (level 0), otherwise its expansion.
+    void append(const RowTable& rows, RowId r, uint32_t len, uint8_t coef, Sym& out) const;
+
+private:
+    std::vector<int32_t> index_;
+    std::vector<Sym> pool_;
+    std::vector<RowId> used_;
+};
+
+// Split a symbolic value: fold every term whose row level is below `keep_level` into a new
+// row (a "partial", materialized by one combine op) and keep the rest symbolic.  Returns the
+// new row or kNoRow when nothing was folded.
+RowId fold_low_levels(RowTable& rows, ProgramBuilder& pb, Sym& s, uint32_t keep_level,
+                      uint32_t len, uint32_t row_bytes);
+
+// ---------------------------------------------------------------------------------------------
+// Context: one arena range + one pending program.  Codecs attached to a context contribute to
+// the same program; a flush hands the program to the executor and rebases every codec.
+// ---------------------------------------------------------------------------------------------
+class FlushClient {
+public:
+    virtual ~FlushClient() {}
+    virtual void pre_flush() = 0;   // emit pending scans (running sums) into the program
+    virtual void post_flush() = 0;  // drop per-program symbolic state
+};
+
+struct Context {
+    RowTable rows;
+    ProgramBuilder pb{&rows};
+    ExpansionTable ex;
+    std::vector<RowId> temps;          // rows only read inside the pending program
+    std::vector<FlushClient*> clients;
+    uint64_t epoch = 1;                // id of the pending program
+    uint64_t arena_base_units = 0;     // offset of this context's range in the device arena
+    bool oom = false;                  // arena exhausted (codecs go to Disabled)
+
+    RowId alloc(uint32_t bytes) {
+        const RowId r = rows.alloc(bytes);
+        if (r == kNoRow) oom = true;
+        return r;
+    }
+    RowId alloc_temp(uint32_t bytes) {
+        const RowId r = alloc(bytes);
+        if (r != kNoRow) temps.push_back(r);
+        return r;
+    }
+    void attach(FlushClient* c) { clients.push_back(c); }
+    void detach(FlushClient* c) {
+        clients.erase(std::remove(clients.begin(), clients.end(), c), clients.end());
+    }
+    // Close the pending program: scans emitted, temps released after `epoch` completes.  The
+    // caller then executes pb's ops and calls finish_flush().
+    void prepare_flush() {
+        for (FlushClient* c : clients) c->pre_flush();
+    }
+    void finish_flush() {
+        for (RowId r : pb.written_rows()) rows.set_level(r, 0);
+        for (RowId r : temps) rows.free_deferred(r);
+        temps.clear();
+        ex.clear();
+        for (FlushClient* c : clients) c->post_flush();
+        rows.seal_epoch(epoch);
+        ++epoch;
+        pb.clear();
+    }
+};
+
+} // namespace tamd

@@ -1,0 +1,45 @@
+// program.h -- the device program format shared by the host control plane (emitter), the HIP
+// executor (kernels.hip) and the test-only CPU interpreter (oracle/siamese_oracle.c).
+//
+// A program is a flat list of independent ops.  Each op owns an accumulator the width of its
+// span and runs its instruction list in order:
+//
+//   ACC   (row, coef, len)             acc[j] ^= coef * row[j]          for j < len
+//   STORE (row, len, footer, cap)      row[j] = acc[j]                  for j < len
+//                                      row[j] = footer[j - len]         for len <= j < len + F
+//                                      row[j] = 0                       for len + F <= j < cap
+//   CLEAR                              acc = 0
+//
+// Rows are addressed in 64-byte units from the arena base.  Byte positions are independent in
+// GF(2^8) arithmetic, so an op is split into byte slices that the device runs in parallel with
+// no synchronisation.  Ops in one launch never read a row another op of the same launch writes
+// (the host orders dependent ops into later launches: "levels").
+#pragma once
+#include <stdint.h>
+
+#define TAMD_ROW_UNIT 64u
+
+enum tamd_instr_kind {
+    TAMD_I_ACC    = 1,
+    TAMD_I_STORE  = 2,
+    TAMD_I_FOOTER = 3,  // payload word that always follows a STORE
+    TAMD_I_CLEAR  = 4,
+};
+
+// 16-byte instruction word.
+typedef struct tamd_instr {
+    uint32_t w0;   // kind | (coef or footer_len) << 8
+    uint32_t row;  // row offset in TAMD_ROW_UNIT units (ACC/STORE); footer bytes 0..3 (FOOTER)
+    uint32_t len;  // byte length (ACC/STORE);                      footer bytes 4..7 (FOOTER)
+    uint32_t cap;  // zero-fill end (STORE)
+} tamd_instr;
+
+// 16-byte op header.
+typedef struct tamd_op {
+    uint32_t first;  // index of first instruction
+    uint32_t count;  // instruction count
+    uint32_t span;   // bytes covered by the op's accumulator
+    uint32_t tag;    // free for the host (stream id / level), ignored by the executor
+} tamd_op;
+
+static inline uint32_t tamd_w0(uint32_t kind, uint32_t arg) { return kind | (arg << 8); }

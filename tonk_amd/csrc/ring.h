@@ -1,0 +1,40 @@
+// ring.h -- random-access window with cheap removal from the front (window elements).
+#pragma once
+#include <stddef.h>
+#include <vector>
+
+namespace tamd {
+
+template <class T>
+class Ring {
+public:
+    size_t size() const { return n_; }
+    T& operator[](size_t i) { return buf_[(head_ + i) & mask_]; }
+    const T& operator[](size_t i) const { return buf_[(head_ + i) & mask_]; }
+    void push_back(const T& v) {
+        if (n_ == buf_.size()) grow();
+        buf_[(head_ + n_) & mask_] = v;
+        ++n_;
+    }
+    void pop_front(size_t k) {
+        if (k > n_) k = n_;
+        for (size_t i = 0; i < k; ++i) buf_[(head_ + i) & mask_] = T();
+        head_ = (head_ + k) & mask_;
+        n_ -= k;
+    }
+    void clear() { pop_front(n_); head_ = 0; }
+
+private:
+    std::vector<T> buf_;
+    size_t head_ = 0, n_ = 0, mask_ = 0;
+    void grow() {
+        const size_t cap = buf_.empty() ? 64 : buf_.size() * 2;
+        std::vector<T> nb(cap);
+        for (size_t i = 0; i < n_; ++i) nb[i] = (*this)[i];
+        buf_.swap(nb);
+        head_ = 0;
+        mask_ = cap - 1;
+    }
+};
+
+} // namespace tamd

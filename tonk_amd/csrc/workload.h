@@ -1,0 +1,233 @@
+// workload.h -- the synthetic Siamese FEC workload.
+//
+// One "stream" is one connection: an encoder and a decoder joined by a lossy channel.  The
+// driver feeds originals, emits recovery packets at rate f with a token bucket (Tonk's rule,
+// TonkineseBandwidth.cpp:248-293), drops packets with a seeded loss process, exchanges
+// acknowledgements every A originals, re-delivers originals still missing after an ARQ lag,
+// and finally flushes recovery packets until every original is received or recovered.
+//
+// The driver is a template over a codec backend so that the SAME event sequence runs against
+//   * the reference codec (oracle/_ref, golden fixtures and the CPU baseline),
+//   * the MI355X engine through the siamese.h C-ABI, and
+//   * the MI355X engine's batched device-resident session (bench).
+// All decisions use integer arithmetic so every compiler produces the same sequence.
+#pragma once
+
+#include <stdint.h>
+#include <string.h>
+#include <vector>
+#include <string>
+#include <algorithm>
+
+namespace tamd {
+namespace wl {
+
+// PCG32 (same generator the codec uses for LDPC columns, SiameseTools.h:79-101).
+struct Pcg {
+    uint64_t state = 0, inc = 0;
+    void seed(uint64_t y, uint64_t x) {
+        state = 0;
+        inc = (y << 1u) | 1u;
+        next();
+        state += x;
+        next();
+    }
+    uint32_t next() {
+        const uint64_t old = state;
+        state = old * 6364136223846793005ULL + inc;
+        const uint32_t xs = (uint32_t)(((old >> 18) ^ old) >> 27);
+        const uint32_t rot = (uint32_t)(old >> 59);
+        return (xs >> rot) | (xs << ((uint32_t)(-(int32_t)rot) & 31u));
+    }
+};
+
+struct Params {
+    uint32_t stream_id = 0;
+    uint32_t n_originals = 256;
+    uint32_t payload_min = 1300, payload_max = 1300;
+    // Loss process over send events (originals and, if enabled, recovery packets).
+    // Uniform: lost iff draw < loss_thresh.  Gilbert-Elliott (ge_enable): the state flips
+    // good->bad with probability gb_thresh/2^32 and bad->good with bg_thresh/2^32 before
+    // each event; a packet is lost iff the state is bad.
+    uint32_t loss_thresh = 0;
+    uint32_t ge_enable = 0, gb_thresh = 0, bg_thresh = 0;
+    uint32_t loss_on_recovery = 1;
+    // Recovery rate in 1/65536 units per original (Tonk: f = max(2p, 1%)).
+    uint32_t fec_rate_q16 = 655;
+    uint32_t ack_every = 0;    // 0: no acknowledgements
+    uint32_t ack_bytes = 256;  // decoder ack buffer size (>= SIAMESE_ACK_MIN_BYTES)
+    uint32_t arq_lag = 0;      // 0: no ARQ
+    uint32_t flush_max = 4096; // cap on end-of-stream recovery packets
+    uint64_t seed_data = 1000, seed_loss = 2000;
+};
+
+// Payload bytes of original i (index within the stream).  Length and contents come from a
+// PCG stream seeded with (seed_data, i) so any packet can be regenerated independently (the
+// device generator in the bench uses the same definition).
+inline uint32_t payload_length(const Params& p, uint32_t i) {
+    if (p.payload_min == p.payload_max) return p.payload_min;
+    Pcg g;
+    g.seed(p.seed_data ^ 0x5bd1e995u, i);
+    return p.payload_min + g.next() % (p.payload_max - p.payload_min + 1);
+}
+
+inline void payload_bytes(const Params& p, uint32_t i, uint8_t* out, uint32_t len) {
+    Pcg g;
+    g.seed(p.seed_data, i);
+    uint32_t k = 0;
+    for (; k + 4 <= len; k += 4) {
+        const uint32_t w = g.next();
+        memcpy(out + k, &w, 4);
+    }
+    if (k < len) {
+        const uint32_t w = g.next();
+        memcpy(out + k, &w, len - k);
+    }
+}
+
+// FNV-1a 64-bit, used for transcript digests.
+inline uint64_t fnv1a(const uint8_t* d, size_t n, uint64_t h = 1469598103934665603ULL) {
+    for (size_t i = 0; i < n; ++i) { h ^= d[i]; h *= 1099511628211ULL; }
+    return h;
+}
+
+struct LossChannel {
+    Pcg rng;
+    bool bad = false;
+    const Params* p = nullptr;
+    void init(const Params& prm) { p = &prm; rng.seed(prm.seed_loss, 0); bad = false; }
+    bool lost() {
+        const uint32_t u = rng.next();
+        if (!p->ge_enable) return u < p->loss_thresh;
+        if (bad) { if (u < p->bg_thresh) bad = false; }
+        else     { if (u < p->gb_thresh) bad = true; }
+        return bad;
+    }
+};
+
+// Counters every backend reports identically.
+struct Summary {
+    uint64_t originals = 0, lost_originals = 0, recoveries = 0, lost_recoveries = 0;
+    uint64_t recovered = 0, arq_redelivered = 0, acks = 0, decode_calls = 0, flush_encodes = 0;
+    uint64_t missing_at_end = 0;
+};
+
+// Backend concept (all methods return siamese.h result codes, 0 = success):
+//   int  enc_add(uint32_t index, uint32_t len, uint32_t* packetNumOut)
+//   int  enc_encode(RecRef& out)              -- out describes the recovery packet
+//   int  enc_ack(const uint8_t* buf, uint32_t n, uint32_t* nextExpected)
+//   int  dec_add_original(uint32_t packetNum, uint32_t index, uint32_t len)
+//   int  dec_add_recovery(const RecRef& r)
+//   int  dec_is_ready()
+//   int  dec_decode(std::vector<uint32_t>& packetNums, DecRef& out)
+//   int  dec_ack(uint8_t* buf, uint32_t limit, uint32_t* used)
+//   void stats(uint64_t enc[9], uint64_t dec[11])
+// Transcript concept:
+//   on_encode(int rc, const RecRef&), on_decode(int rc, nums, const DecRef&), on_ack(...),
+//   on_event(char kind, int rc, uint32_t a, uint32_t b)
+template <class Backend, class Transcript>
+Summary run_stream(const Params& p, Backend& be, Transcript& tr) {
+    Summary s;
+    LossChannel ch;
+    ch.init(p);
+    std::vector<uint8_t> have(p.n_originals, 0);      // received or recovered at the decoder
+    std::vector<uint32_t> colOf(p.n_originals, 0);    // packet number assigned by the encoder
+    std::vector<uint32_t> pendingArq;                 // indices of lost originals
+    size_t arqHead = 0;
+    uint32_t tokens = 0;
+    std::vector<uint32_t> nums;
+
+    // Column -> index map (packet numbers are assigned sequentially from 0 by the encoder).
+    auto decode_loop = [&]() {
+        while (be.dec_is_ready() == 0) {
+            nums.clear();
+            typename Backend::DecRef dref;
+            const int rc = be.dec_decode(nums, dref);
+            ++s.decode_calls;
+            tr.on_decode(rc, nums, dref);
+            if (rc != 0) break;
+            for (uint32_t c : nums) {
+                if (c < p.n_originals && !have[c]) { have[c] = 1; ++s.recovered; }
+            }
+            if (nums.empty()) break;
+        }
+    };
+
+    auto send_recovery = [&](bool lossy) {
+        typename Backend::RecRef r;
+        const int rc = be.enc_encode(r);
+        tr.on_encode(rc, r);
+        if (rc != 0) return;
+        ++s.recoveries;
+        if (lossy && p.loss_on_recovery && ch.lost()) { ++s.lost_recoveries; return; }
+        const int rr = be.dec_add_recovery(r);
+        tr.on_event('R', rr, 0, 0);
+        decode_loop();
+    };
+
+    for (uint32_t i = 0; i < p.n_originals; ++i) {
+        const uint32_t len = payload_length(p, i);
+        uint32_t col = 0;
+        const int ra = be.enc_add(i, len, &col);
+        tr.on_event('a', ra, i, col);
+        colOf[i] = col;
+        ++s.originals;
+        if (ch.lost()) {
+            ++s.lost_originals;
+            pendingArq.push_back(i);
+        } else {
+            const int ro = be.dec_add_original(col, i, len);
+            tr.on_event('O', ro, col, 0);
+            if (!have[i]) have[i] = 1;
+            decode_loop();
+        }
+
+        tokens += p.fec_rate_q16;
+        while (tokens >= 65536u) {
+            tokens -= 65536u;
+            send_recovery(true);
+        }
+
+        if (p.ack_every && (i + 1) % p.ack_every == 0) {
+            std::vector<uint8_t> buf(p.ack_bytes);
+            uint32_t used = 0;
+            const int rd = be.dec_ack(buf.data(), p.ack_bytes, &used);
+            uint32_t next = 0;
+            int re = -1;
+            if (rd == 0 && used > 0) re = be.enc_ack(buf.data(), used, &next);
+            tr.on_ack(rd, buf.data(), used, re, next);
+            ++s.acks;
+        }
+
+        if (p.arq_lag) {
+            while (arqHead < pendingArq.size() && i - pendingArq[arqHead] >= p.arq_lag) {
+                const uint32_t j = pendingArq[arqHead++];
+                if (!have[j]) {
+                    const int ro = be.dec_add_original(colOf[j], j, payload_length(p, j));
+                    tr.on_event('X', ro, colOf[j], 0);
+                    have[j] = 1;
+                    ++s.arq_redelivered;
+                    decode_loop();
+                }
+            }
+        }
+    }
+
+    // End-of-stream flush: lossless recovery packets until the decoder has everything.
+    for (uint32_t k = 0; k < p.flush_max; ++k) {
+        bool complete = true;
+        for (uint32_t i = 0; i < p.n_originals; ++i) if (!have[i]) { complete = false; break; }
+        if (complete) break;
+        ++s.flush_encodes;
+        send_recovery(false);
+    }
+    for (uint32_t i = 0; i < p.n_originals; ++i) if (!have[i]) ++s.missing_at_end;
+
+    uint64_t es[9] = {0}, ds[11] = {0};
+    be.stats(es, ds);
+    tr.on_stats(es, ds);
+    return s;
+}
+
+} // namespace wl
+} // namespace tamd
