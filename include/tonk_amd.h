@@ -1,0 +1,63 @@
+/*
+    tonk_amd.h -- additive batched API of the MI355X Siamese engine (not part of siamese.h).
+
+    A session runs many independent connection streams (encoder + decoder + lossy channel per
+    stream, tonk_amd/csrc/workload.h) whose packets live in HBM.  Host worker threads run the
+    codec control planes; every step's byte work is one merged device program executed level
+    by level on the GPU while the host builds the next step.  This is the device-resident path
+    the benchmark measures; the siamese.h ABI is the drop-in path.
+*/
+#ifndef TONK_AMD_H
+#define TONK_AMD_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct tamd_session_params {
+    uint32_t device;
+    uint32_t n_streams;        /* streams on this device */
+    uint32_t stream_base;      /* global id of the first stream (seeds 1000+id / 2000+id) */
+    uint32_t n_threads;        /* host worker threads */
+    uint32_t n_originals;      /* originals per stream for the whole session */
+    uint32_t payload_min, payload_max;
+    uint32_t loss_thresh, ge_enable, gb_thresh, bg_thresh, loss_on_recovery;
+    uint32_t fec_rate_q16, ack_every, ack_bytes, arq_lag, flush_max;
+    uint32_t record;           /* 1: keep per-stream transcripts (parity checks, not timed) */
+    uint64_t arena_bytes;
+} tamd_session_params;
+
+/* Summary counters (tamd_session_summary indices). */
+enum {
+    TAMD_SUM_ORIGINALS, TAMD_SUM_LOST_ORIGINALS, TAMD_SUM_RECOVERIES, TAMD_SUM_LOST_RECOVERIES,
+    TAMD_SUM_RECOVERED, TAMD_SUM_ARQ, TAMD_SUM_MISSING_AT_END, TAMD_SUM_PAYLOAD_BYTES,
+    TAMD_SUM_ALG_BYTES,        /* algorithmic HBM bytes (SURVEY.md s8(d) B_alg) */
+    TAMD_SUM_ACC_BYTES,        /* bytes read by ACC instructions (op-trace diagnostic) */
+    TAMD_SUM_STORE_BYTES,      /* bytes written by STORE instructions */
+    TAMD_SUM_PROGRAMS, TAMD_SUM_LAUNCHES, TAMD_SUM_OPS, TAMD_SUM_INSTRS, TAMD_SUM_UPLOAD_BYTES,
+    TAMD_SUM_DISABLED_CODECS,
+    TAMD_SUM_COUNT
+};
+
+void* tamd_session_create(const tamd_session_params* p, char* err, size_t err_len);
+int   tamd_session_generate(void* s);                 /* write all input rows in HBM (untimed) */
+int   tamd_session_step(void* s, uint32_t originals); /* host work + enqueue; device is async */
+int   tamd_session_wait(void* s);                     /* wait for every enqueued program */
+int   tamd_session_finish(void* s);                   /* end-of-stream flush, then wait */
+int   tamd_session_summary(void* s, uint64_t* out, unsigned n);
+void  tamd_session_set_timing(void* s, int on);       /* HIP events around every launch */
+double tamd_session_kernel_ms(void* s, uint64_t* launches);
+/* Transcript of one stream in the oracle's text format (record mode). Returns bytes needed. */
+size_t tamd_session_transcript(void* s, uint32_t stream, char* buf, size_t cap);
+void  tamd_session_destroy(void* s);
+
+/* Device self test: v_perm GF(2^8) multiply against the host tables (all 65536 products). */
+int   tamd_device_selftest(uint32_t device, char* err, size_t err_len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,96 @@
+#!/usr/bin/env python3
+"""TEST INFRASTRUCTURE: generate tests/golden fixtures from the REFERENCE codec.
+
+Runs oracle/_ref/golden_gen (our workload driver linked against the reference Siamese codec
+compiled from /root/reference by oracle/Makefile) for every scenario below and writes
+
+  tests/golden/<name>.txt.gz     full transcript (every recovery packet digest, every decode,
+                                 every ack, final stats) for small/medium scenarios
+  tests/golden/scenarios.json    parameters + sha256 of each transcript (+ summary line)
+
+The reference also memcmp-checks every recovered packet against the true payload while it
+runs (golden_gen exits non-zero otherwise), so no fixture can pin a wrong decode.
+
+usage: python oracle/gen_golden.py [--bench-streams 64 --bench-originals 49152]
+"""
+from __future__ import annotations
+
+import argparse
+import gzip
+import hashlib
+import json
+import os
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, ROOT)
+from tonk_amd import WorkloadParams  # noqa: E402  (parameter helpers only)
+
+GEN = os.path.join(HERE, "_ref", "golden_gen")
+OUT = os.path.join(ROOT, "tests", "golden")
+
+
+def scenarios():
+    """name -> (WorkloadParams, stream id, store full transcript?)"""
+    s = {}
+    s["c1_256_p3"] = (WorkloadParams(n=256, loss=0.03, ack=0), 0, True)                      # config 1
+    s["c2_4096_p1_ack64"] = (WorkloadParams(n=4096, loss=0.01, ack=64), 0, True)             # config 2
+    s["c2_4096_p1_noack"] = (WorkloadParams(n=4096, loss=0.01, ack=0), 0, True)              # config 2 stress
+    for sid in (0, 1, 63):
+        s[f"c3_4096_p2_ack64_s{sid}"] = (WorkloadParams(n=4096, loss=0.02, ack=64), sid, True)  # config 3
+    s["c4_4096_p1_ack64_s511"] = (WorkloadParams(n=4096, loss=0.01, ack=64), 511, True)     # config 4
+    s["c5_65536_ge5_b4"] = (WorkloadParams(n=65536, loss=0.05, burst=4, fec=0.10, ack=256, arq=2048), 0, True)
+    s["var_1_1500_p2_ack32"] = (WorkloadParams(n=2000, payload=1, payload_max=1500, loss=0.02, ack=32), 0, True)
+    s["tiny_1_20_p5_ack16"] = (WorkloadParams(n=3000, payload=1, payload_max=20, loss=0.05, ack=16), 0, True)
+    s["big_9000_p3_ack64"] = (WorkloadParams(n=1500, payload=9000, loss=0.03, ack=64), 0, True)
+    s["hiloss_p20_arq"] = (WorkloadParams(n=3000, loss=0.20, ack=64, arq=500), 0, True)
+    s["norecloss_p5_arq"] = (WorkloadParams(n=3000, loss=0.05, ack=0, arq=300, loss_on_recovery=False), 0, True)
+    s["single_p0"] = (WorkloadParams(n=200, loss=0.0, ack=1), 0, True)
+    s["burst8_p5"] = (WorkloadParams(n=8192, loss=0.05, burst=8, fec=0.10, ack=128, arq=1024), 0, True)
+    return s
+
+
+def run(wp: WorkloadParams, sid: int) -> str:
+    args = [GEN, "transcript", "/dev/stdout"] + wp.args() + [f"seed_data={1000 + sid}", f"seed_loss={2000 + sid}"]
+    r = subprocess.run(args, capture_output=True, check=True)
+    return r.stdout.decode()
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--bench-streams", type=int, default=64)
+    ap.add_argument("--bench-originals", type=int, default=12 * 4096)
+    a = ap.parse_args()
+    if not os.path.exists(GEN):
+        print("build the reference first: make -C oracle", file=sys.stderr)
+        return 2
+    os.makedirs(OUT, exist_ok=True)
+    index = {"generator": "oracle/_ref/golden_gen (reference codec from /root/reference)", "scenarios": {}}
+    for name, (wp, sid, full) in scenarios().items():
+        text = run(wp, sid)
+        digest = hashlib.sha256(text.encode()).hexdigest()
+        index["scenarios"][name] = {"args": wp.args(), "stream": sid, "sha256": digest,
+                                    "lines": text.count("\n"), "summary": text.strip().splitlines()[-1],
+                                    "file": f"{name}.txt.gz" if full else None}
+        if full:
+            with gzip.open(os.path.join(OUT, f"{name}.txt.gz"), "wt") as f:
+                f.write(text)
+        print(f"{name}: {index['scenarios'][name]['lines']} lines {digest[:16]}")
+
+    # Bench configuration (bench.py default): per-stream transcript digests for streams 0..S-1.
+    wp = WorkloadParams(n=a.bench_originals, loss=0.01, ack=64)
+    bench = {"args": wp.args(), "streams": {}}
+    for sid in range(a.bench_streams):
+        text = run(wp, sid)
+        bench["streams"][str(sid)] = {"sha256": hashlib.sha256(text.encode()).hexdigest(),
+                                      "summary": text.strip().splitlines()[-1]}
+    index["bench"] = bench
+    with open(os.path.join(OUT, "scenarios.json"), "w") as f:
+        json.dump(index, f, indent=1, sort_keys=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -84,6 +84,7 @@ struct RefBackend {
         rp.DataBytes = (unsigned)r.bytes.size();
         return siamese_decoder_add_recovery(dec, &rp);
     }
+    void recovery_lost(const RecRef&) {}
     int dec_is_ready() { return siamese_decoder_is_ready(dec); }
     int dec_decode(std::vector<uint32_t>& nums, DecRef& out) {
         SiameseOriginalPacket* pk = nullptr;

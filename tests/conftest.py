@@ -1,0 +1,62 @@
+"""Shared test setup.
+
+Markers: ``gpu`` tests need an MI355X (run by the driver with ``-m gpu`` on a GPU box); every
+other test runs on a CPU-only host in a few minutes.
+"""
+from __future__ import annotations
+
+import gzip
+import hashlib
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+NATIVE = os.path.join(ROOT, "tests", "native")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")
+
+
+def _make(path: str, *targets: str) -> None:
+    subprocess.run(["make", "-C", path, "-j8", *targets], check=True, stdout=subprocess.DEVNULL)
+
+
+@pytest.fixture(scope="session")
+def oracle_lib():
+    """The plain-C oracle (oracle/liboracle.so), built on demand."""
+    import ctypes
+    _make(os.path.join(ROOT, "oracle"), "liboracle.so")
+    L = ctypes.CDLL(os.path.join(ROOT, "oracle", "liboracle.so"))
+    assert L.oracle_self_test() == 0
+    return L
+
+
+@pytest.fixture(scope="session")
+def golden_index():
+    with open(os.path.join(GOLDEN, "scenarios.json")) as f:
+        return json.load(f)
+
+
+def golden_text(name: str) -> str:
+    with gzip.open(os.path.join(GOLDEN, f"{name}.txt.gz"), "rt") as f:
+        return f.read()
+
+
+def sha256(text: str) -> str:
+    return hashlib.sha256(text.encode()).hexdigest()
+
+
+def first_diff(a: str, b: str) -> str:
+    la, lb = a.splitlines(), b.splitlines()
+    for i, (x, y) in enumerate(zip(la, lb)):
+        if x != y:
+            return f"line {i + 1}: expected {x!r} got {y!r}"
+    return f"length differs: expected {len(la)} lines got {len(lb)}"

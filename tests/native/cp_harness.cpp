@@ -143,12 +143,7 @@ struct Harness {
         if (batch && (index + 1) % batch == 0) flush();
         return rc;
     }
-    int enc_encode(RecRef& r) {
-        if (undelivered != kNoRow) ctx.rows.free_deferred(undelivered);  // it was lost
-        const Result rc = enc->encode(r.out);
-        undelivered = rc == kSuccess ? r.out.row : kNoRow;
-        return rc;
-    }
+    int enc_encode(RecRef& r) { return enc->encode(r.out); }
     int enc_ack(const uint8_t* buf, uint32_t n, uint32_t* next) { return enc->acknowledge(buf, n, next); }
     int dec_add_original(uint32_t col, uint32_t index, uint32_t len) {
         uint32_t framed = 0, header = 0;
@@ -159,7 +154,7 @@ struct Harness {
         if (!took) ctx.rows.free_deferred(r);
         return rc;
     }
-    RowId undelivered = kNoRow;  // last encoder output not (yet) handed to the decoder
+    void recovery_lost(const RecRef& r) { ctx.rows.free_deferred(r.out.row); }
 
     int dec_add_recovery(const RecRef& r) {
         bool took = false;
@@ -168,7 +163,6 @@ struct Harness {
         uint8_t tail[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         const uint32_t tl = r.out.total() < 8 ? r.out.total() : 8;
         memcpy(tail + tl - r.out.footer_len, r.out.footer, r.out.footer_len);
-        undelivered = kNoRow;
         const Result rc = dec->add_recovery(r.out.row, r.out.total(), tail, nullptr, &took);
         if (!took) ctx.rows.free_deferred(r.out.row);
         return rc;

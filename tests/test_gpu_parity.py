@@ -1,0 +1,115 @@
+"""GPU parity tests (MI355X): the HIP path must reproduce the reference codec bit for bit.
+
+Every scenario's transcript -- the digest of every recovery packet (data + footer), every
+decode result with the digest of each recovered payload, every acknowledgement, the final
+stats -- is compared with the golden transcript produced by the REFERENCE codec
+(tests/golden, oracle/gen_golden.py).  Two device paths are checked:
+
+* the siamese.h C-ABI (drop-in path): oracle/golden_gen.cpp's driver linked against
+  libtonk_amd.so instead of the reference library (tests/native/_build/capi_gen);
+* the batched device-resident session (bench path) in record mode.
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+
+import pytest
+
+from conftest import NATIVE, ROOT, first_diff, golden_text, sha256
+
+pytestmark = pytest.mark.gpu
+
+SCEN_CAPI = ["c1_256_p3", "c2_4096_p1_ack64", "c2_4096_p1_noack", "c3_4096_p2_ack64_s0",
+             "var_1_1500_p2_ack32", "tiny_1_20_p5_ack16", "big_9000_p3_ack64", "hiloss_p20_arq",
+             "norecloss_p5_arq", "single_p0", "burst8_p5", "c5_65536_ge5_b4"]
+SCEN_SESSION = ["c1_256_p3", "c2_4096_p1_ack64", "c2_4096_p1_noack", "c3_4096_p2_ack64_s1",
+                "c3_4096_p2_ack64_s63", "c4_4096_p1_ack64_s511", "var_1_1500_p2_ack32",
+                "tiny_1_20_p5_ack16", "big_9000_p3_ack64", "hiloss_p20_arq", "single_p0",
+                "burst8_p5", "c5_65536_ge5_b4"]
+
+
+def _args(golden_index, name):
+    sc = golden_index["scenarios"][name]
+    sid = sc["stream"]
+    return sc["args"] + [f"seed_data={1000 + sid}", f"seed_loss={2000 + sid}"], sid
+
+
+def test_device_gf_selftest():
+    import tonk_amd
+    tonk_amd.device_selftest(0)
+
+
+@pytest.mark.parametrize("name", SCEN_CAPI)
+def test_capi_matches_reference(golden_index, name):
+    exe = os.path.join(NATIVE, "_build", "capi_gen")
+    assert os.path.exists(exe), "build tests/native first (make -C tests/native)"
+    args, _ = _args(golden_index, name)
+    out = subprocess.run([exe, "transcript", "/dev/stdout"] + args, capture_output=True, timeout=600)
+    assert out.returncode == 0, out.stderr.decode()[-2000:]
+    got = out.stdout.decode()
+    want = golden_text(name)
+    assert got == want, first_diff(want, got)
+
+
+def _session_transcript(golden_index, name, threads=1):
+    import tonk_amd
+    sc = golden_index["scenarios"][name]
+    kv = dict(a.split("=") for a in sc["args"])
+    wp = tonk_amd.WorkloadParams()
+    for k in tonk_amd.WorkloadParams.KEYS:
+        setattr(wp, k, int(kv[k]))
+    s = tonk_amd.Session(wp, n_streams=1, stream_base=sc["stream"], threads=threads,
+                         arena_bytes=1 << 30, record=True)
+    try:
+        s.generate()
+        n = wp.n
+        step = 1000
+        done = 0
+        while done < n:
+            s.step(min(step, n - done))
+            done += step
+        s.finish()
+        return s.transcript(0), s.summary()
+    finally:
+        s.close()
+
+
+@pytest.mark.parametrize("name", SCEN_SESSION)
+def test_session_matches_reference(golden_index, name):
+    got, summ = _session_transcript(golden_index, name)
+    want = golden_text(name)
+    want = "\n".join(l for l in want.splitlines() if not l.startswith("Z ")) + "\n"
+    assert got == want, first_diff(want, got)
+    assert summ["missing_at_end"] == 0
+    assert summ["disabled_codecs"] == 0
+
+
+def test_session_bench_config_streams(golden_index):
+    """Bench configuration (64 streams x 49152 originals, 1% loss, ack 64): every stream's full
+    transcript digest equals the reference's, with 16 host threads as in the bench."""
+    import tonk_amd
+    b = golden_index["bench"]
+    kv = dict(a.split("=") for a in b["args"])
+    wp = tonk_amd.WorkloadParams()
+    for k in tonk_amd.WorkloadParams.KEYS:
+        setattr(wp, k, int(kv[k]))
+    n_streams = len(b["streams"])
+    s = tonk_amd.Session(wp, n_streams=n_streams, stream_base=0, threads=16, arena_bytes=24 << 30, record=True)
+    try:
+        s.generate()
+        for _ in range(wp.n // 4096):
+            s.step(4096)
+        s.finish()
+        bad = []
+        for sid in range(n_streams):
+            t = s.transcript(sid)
+            want = b["streams"][str(sid)]
+            # the golden digest covers the transcript plus its Z summary line
+            if sha256(t + want["summary"] + "\n") != want["sha256"]:
+                bad.append(sid)
+        assert not bad, f"streams differing from the reference: {bad}"
+        summ = s.summary()
+        assert summ["missing_at_end"] == 0 and summ["disabled_codecs"] == 0
+    finally:
+        s.close()

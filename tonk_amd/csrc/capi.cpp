@@ -1,0 +1,393 @@
+// capi.cpp -- the siamese.h C ABI over the MI355X engine (drop-in for the reference siamese.cpp).
+//
+// Argument validation and result codes follow siamese.cpp:43-299 exactly.  Data crosses the
+// device boundary where the API forces it:
+//   encoder_add / decoder_add_original / decoder_add_recovery : H2D of the packet into a row
+//   siamese_encode                                            : run program, D2H recovery row
+//   siamese_decode                                            : run program, D2H recovered rows
+// Host mirrors of originals back siamese_encoder_get/retransmit and siamese_decoder_get.
+#define SIAMESE_BUILDING 1
+#include "../../include/siamese.h"
+
+#include "decoder.h"
+#include "device.h"
+
+#include <mutex>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+using namespace tamd;
+
+namespace {
+
+struct Runtime {
+    std::mutex mu;
+    Device dev;
+    Context ctx;
+    bool ok = false;
+};
+
+Runtime* g_rt = nullptr;
+std::mutex g_init_mu;
+
+void release_host(void* host, void*) { free(host); }
+
+struct CEncoder {
+    Encoder* enc = nullptr;
+    std::vector<uint8_t> recovery;
+};
+
+struct CDecoder {
+    Decoder* dec = nullptr;
+    std::vector<SiameseOriginalPacket> out;
+};
+
+uint64_t row_byte_offset(RowId r) { return (uint64_t)g_rt->ctx.rows.offset(r) * TAMD_ROW_UNIT; }
+
+// Runs the pending program and waits for it (caller holds the lock).
+void flush_locked() {
+    Context& ctx = g_rt->ctx;
+    ctx.prepare_flush();
+    if (!ctx.pb.empty()) g_rt->dev.run(&ctx);
+    const uint64_t done = ctx.epoch;
+    g_rt->dev.synchronize();
+    ctx.finish_flush();
+    ctx.rows.release_up_to(done);
+}
+
+// varint(len) || payload into a malloc'd host buffer and a device row.
+bool store_framed(const unsigned char* data, unsigned len, uint8_t** host_out, RowId* row_out,
+                  uint32_t* framed_out, uint32_t* header_out) {
+    uint8_t hdr[4];
+    const uint32_t hb = put_length_header(len, hdr);
+    const uint32_t framed = hb + len;
+    uint8_t* host = (uint8_t*)malloc(framed);
+    if (!host) return false;
+    memcpy(host, hdr, hb);
+    memcpy(host + hb, data, len);
+    const RowId row = g_rt->ctx.alloc(framed);
+    if (row == kNoRow) { free(host); return false; }
+    g_rt->dev.upload(row_byte_offset(row), host, framed);
+    *host_out = host;
+    *row_out = row;
+    *framed_out = framed;
+    *header_out = hb;
+    return true;
+}
+
+} // namespace
+
+extern "C" {
+
+SIAMESE_EXPORT int siamese_init_(int version) {
+    if (version != SIAMESE_VERSION) return Siamese_Disabled;
+    std::lock_guard<std::mutex> lk(g_init_mu);
+    if (g_rt) return g_rt->ok ? Siamese_Success : Siamese_Disabled;
+    g_rt = new Runtime();
+    if (!gf_init()) return Siamese_Disabled;
+    int device = 0;
+    if (const char* d = getenv("TONK_AMD_DEVICE")) device = atoi(d);
+    uint64_t arena_mb = 2048;
+    if (const char* a = getenv("TONK_AMD_ARENA_MB")) arena_mb = strtoull(a, nullptr, 10);
+    if (!g_rt->dev.init(device, arena_mb << 20)) {
+        fprintf(stderr, "%s\n", g_rt->dev.error().c_str());
+        return Siamese_Disabled;
+    }
+    if (!g_rt->dev.gf_selftest()) {
+        fprintf(stderr, "tonk_amd: device GF(256) self test failed\n");
+        return Siamese_Disabled;
+    }
+    g_rt->ctx.rows.init(g_rt->dev.arena_bytes(), 0);
+    g_rt->ok = true;
+    return Siamese_Success;
+}
+
+// ---------------------------------------------------------------------------- Encoder API
+
+SIAMESE_EXPORT SiameseEncoder siamese_encoder_create() {
+    if (!g_rt || !g_rt->ok) return nullptr;
+    std::lock_guard<std::mutex> lk(g_rt->mu);
+    CEncoder* e = new (std::nothrow) CEncoder();
+    if (!e) return nullptr;
+    e->enc = new Encoder(&g_rt->ctx, 0, release_host, nullptr);
+    return reinterpret_cast<SiameseEncoder>(e);
+}
+
+SIAMESE_EXPORT void siamese_encoder_free(SiameseEncoder encoder_t) {
+    CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
+    if (!e) return;
+    std::lock_guard<std::mutex> lk(g_rt->mu);
+    delete e->enc;
+    delete e;
+}
+
+SIAMESE_EXPORT SiameseResult siamese_encoder_is_ready(SiameseEncoder encoder_t) {
+    CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
+    if (!e) return Siamese_InvalidInput;
+    std::lock_guard<std::mutex> lk(g_rt->mu);
+    if (e->enc->remaining_slots() <= 2) return Siamese_MaxPacketsReached;
+    return Siamese_Success;
+}
+
+SIAMESE_EXPORT SiameseResult siamese_encoder_add(SiameseEncoder encoder_t, SiameseOriginalPacket* packet) {
+    CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
+    if (!e || !packet || !packet->Data || packet->DataBytes <= 0 || packet->DataBytes > SIAMESE_MAX_PACKET_BYTES)
+        return Siamese_InvalidInput;
+    std::lock_guard<std::mutex> lk(g_rt->mu);
+    if (e->enc->disabled()) return Siamese_Disabled;
+    if (e->enc->remaining_slots() <= 0) return Siamese_MaxPacketsReached;
+    uint8_t* host = nullptr;
+    RowId row = kNoRow;
+    uint32_t framed = 0, hb = 0;
+    if (!store_framed(packet->Data, packet->DataBytes, &host, &row, &framed, &hb)) return Siamese_Disabled;
+    uint32_t pn = 0;
+    const Result r = e->enc->add(row, framed, hb, packet->DataBytes, host, &pn);
+    if (r != kSuccess) {
+        g_rt->ctx.rows.free_deferred(row);
+        free(host);
+        return (SiameseResult)r;
+    }
+    packet->PacketNum = pn;
+    return Siamese_Success;
+}
+
+SIAMESE_EXPORT SiameseResult siamese_encoder_get(SiameseEncoder encoder_t, SiameseOriginalPacket* packet) {
+    CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
+    if (!e || !packet || packet->PacketNum > SIAMESE_PACKET_NUM_MAX) return Siamese_InvalidInput;
+    std::lock_guard<std::mutex> lk(g_rt->mu);
+    const StoredOriginal* o = nullptr;
+    const Result r = e->enc->get(packet->PacketNum, &o);
+    if (r != kSuccess) {
+        packet->Data = nullptr;
+        packet->DataBytes = 0;
+        return (SiameseResult)r;
+    }
+    packet->Data = (const unsigned char*)o->host + o->header_bytes;
+    packet->DataBytes = o->bytes - o->header_bytes;
+    return Siamese_Success;
+}
+
+SIAMESE_EXPORT SiameseResult siamese_encoder_remove_before(SiameseEncoder encoder_t, unsigned packetNum) {
+    CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
+    if (!e || packetNum > SIAMESE_PACKET_NUM_MAX) return Siamese_InvalidInput;
+    std::lock_guard<std::mutex> lk(g_rt->mu);
+    e->enc->remove_before(packetNum);
+    return Siamese_Success;
+}
+
+SIAMESE_EXPORT SiameseResult siamese_encoder_ack(SiameseEncoder encoder_t, const void* buffer, unsigned bytes,
+                                                 unsigned* nextExpectedPacketNum) {
+    CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
+    if (!e || !buffer || bytes < 1 || !nextExpectedPacketNum) return Siamese_InvalidInput;
+    std::lock_guard<std::mutex> lk(g_rt->mu);
+    uint32_t next = 0;
+    const Result r = e->enc->acknowledge((const uint8_t*)buffer, bytes, &next);
+    if (r == kSuccess) *nextExpectedPacketNum = next;
+    return (SiameseResult)r;
+}
+
+SIAMESE_EXPORT SiameseResult siamese_encoder_retransmit(SiameseEncoder encoder_t, SiameseOriginalPacket* original) {
+    CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
+    if (!e || !original) return Siamese_InvalidInput;
+    std::lock_guard<std::mutex> lk(g_rt->mu);
+    original->Data = nullptr;
+    original->DataBytes = 0;
+    const StoredOriginal* o = nullptr;
+    const Result r = e->enc->retransmit(&o);
+    if (r != kSuccess) return (SiameseResult)r;
+    original->PacketNum = o->column;
+    original->Data = (const unsigned char*)o->host + o->header_bytes;
+    original->DataBytes = o->bytes - o->header_bytes;
+    return Siamese_Success;
+}
+
+SIAMESE_EXPORT SiameseResult siamese_encode(SiameseEncoder encoder_t, SiameseRecoveryPacket* recovery) {
+    CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
+    if (!e || !recovery) return Siamese_InvalidInput;
+    std::lock_guard<std::mutex> lk(g_rt->mu);
+    RecoveryOut out;
+    const Result r = e->enc->encode(out);
+    if (r != kSuccess) {
+        if (r == kNeedMoreData) recovery->DataBytes = 0;
+        return (SiameseResult)r;
+    }
+    flush_locked();
+    e->recovery.resize(out.total());
+    g_rt->dev.download(e->recovery.data(), row_byte_offset(out.row), out.total());
+    g_rt->ctx.rows.free_deferred(out.row);
+    recovery->Data = e->recovery.data();
+    recovery->DataBytes = out.total();
+    return Siamese_Success;
+}
+
+SIAMESE_EXPORT SiameseResult siamese_encoder_stats(SiameseEncoder encoder_t, uint64_t* statsOut, unsigned statsCount) {
+    CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
+    if (!e || !statsOut || statsCount <= 0) return Siamese_InvalidInput;
+    std::lock_guard<std::mutex> lk(g_rt->mu);
+    e->enc->stats(statsOut, statsCount);
+    return Siamese_Success;
+}
+
+// ---------------------------------------------------------------------------- Decoder API
+
+SIAMESE_EXPORT SiameseDecoder siamese_decoder_create() {
+    if (!g_rt || !g_rt->ok) return nullptr;
+    std::lock_guard<std::mutex> lk(g_rt->mu);
+    CDecoder* d = new (std::nothrow) CDecoder();
+    if (!d) return nullptr;
+    d->dec = new Decoder(&g_rt->ctx, 0, release_host, nullptr);
+    return reinterpret_cast<SiameseDecoder>(d);
+}
+
+SIAMESE_EXPORT void siamese_decoder_free(SiameseDecoder decoder_t) {
+    CDecoder* d = reinterpret_cast<CDecoder*>(decoder_t);
+    if (!d) return;
+    std::lock_guard<std::mutex> lk(g_rt->mu);
+    delete d->dec;
+    delete d;
+}
+
+SIAMESE_EXPORT SiameseResult siamese_decoder_add_original(SiameseDecoder decoder_t, const SiameseOriginalPacket* packet) {
+    CDecoder* d = reinterpret_cast<CDecoder*>(decoder_t);
+    if (!d || !packet || packet->DataBytes <= 0 || packet->DataBytes > SIAMESE_MAX_PACKET_BYTES ||
+        packet->PacketNum > SIAMESE_PACKET_NUM_MAX)
+        return Siamese_InvalidInput;
+    if (!packet->Data) return Siamese_InvalidInput;
+    std::lock_guard<std::mutex> lk(g_rt->mu);
+    if (d->dec->disabled()) return Siamese_Disabled;
+    uint8_t* host = nullptr;
+    RowId row = kNoRow;
+    uint32_t framed = 0, hb = 0;
+    if (!store_framed(packet->Data, packet->DataBytes, &host, &row, &framed, &hb)) {
+        d->dec->set_disabled();
+        return Siamese_Disabled;
+    }
+    bool took = false;
+    const Result r = d->dec->add_original(packet->PacketNum, row, framed, hb, packet->DataBytes, host, &took);
+    if (!took) {
+        g_rt->ctx.rows.free_deferred(row);
+        free(host);
+    }
+    return (SiameseResult)r;
+}
+
+SIAMESE_EXPORT SiameseResult siamese_decoder_add_recovery(SiameseDecoder decoder_t, const SiameseRecoveryPacket* packet) {
+    CDecoder* d = reinterpret_cast<CDecoder*>(decoder_t);
+    if (!d || !packet || !packet->Data || packet->DataBytes <= 0 || packet->DataBytes > SIAMESE_MAX_PACKET_BYTES)
+        return Siamese_InvalidInput;
+    std::lock_guard<std::mutex> lk(g_rt->mu);
+    if (d->dec->disabled()) return Siamese_Disabled;
+    const uint32_t total = packet->DataBytes;
+    const RowId row = g_rt->ctx.alloc(total);
+    if (row == kNoRow) { d->dec->set_disabled(); return Siamese_Disabled; }
+    g_rt->dev.upload(row_byte_offset(row), packet->Data, total);
+    const uint32_t tl = total < 8 ? total : 8;
+    bool took = false;
+    const Result r = d->dec->add_recovery(row, total, packet->Data + total - tl, packet->Data, &took);
+    if (!took) g_rt->ctx.rows.free_deferred(row);
+    return (SiameseResult)r;
+}
+
+SIAMESE_EXPORT SiameseResult siamese_decoder_get(SiameseDecoder decoder_t, SiameseOriginalPacket* packet) {
+    CDecoder* d = reinterpret_cast<CDecoder*>(decoder_t);
+    if (!d || !packet || packet->PacketNum > SIAMESE_PACKET_NUM_MAX) return Siamese_InvalidInput;
+    std::lock_guard<std::mutex> lk(g_rt->mu);
+    StoredOriginal* o = nullptr;
+    const Result r = d->dec->get(packet->PacketNum, &o);
+    if (r != kSuccess) {
+        packet->Data = nullptr;
+        packet->DataBytes = 0;
+        return (SiameseResult)r;
+    }
+    if (!o->host) {  // recovered data not read back yet
+        flush_locked();
+        uint8_t* host = (uint8_t*)malloc(o->bytes);
+        if (!host) return Siamese_Disabled;
+        g_rt->dev.download(host, row_byte_offset(o->row), o->bytes);
+        unsigned len = 0;
+        const int hb = get_length_header(host, o->bytes, len);
+        if (hb < 1 || len == 0 || (uint32_t)hb + len > o->bytes) { free(host); d->dec->set_disabled(); return Siamese_Disabled; }
+        o->host = host;
+        o->header_bytes = (uint32_t)hb;
+        o->bytes = (uint32_t)hb + len;
+    }
+    packet->Data = (const unsigned char*)o->host + o->header_bytes;
+    packet->DataBytes = o->bytes - o->header_bytes;
+    return Siamese_Success;
+}
+
+SIAMESE_EXPORT SiameseResult siamese_decoder_is_ready(SiameseDecoder decoder_t) {
+    CDecoder* d = reinterpret_cast<CDecoder*>(decoder_t);
+    if (!d) return Siamese_InvalidInput;
+    std::lock_guard<std::mutex> lk(g_rt->mu);
+    return (SiameseResult)d->dec->is_ready();
+}
+
+SIAMESE_EXPORT SiameseResult siamese_decode(SiameseDecoder decoder_t, SiameseOriginalPacket** packetsPtrOut,
+                                            unsigned* countOut) {
+    CDecoder* d = reinterpret_cast<CDecoder*>(decoder_t);
+    if (!d || (!packetsPtrOut != !countOut)) return Siamese_InvalidInput;
+    std::lock_guard<std::mutex> lk(g_rt->mu);
+    if (packetsPtrOut) {
+        *packetsPtrOut = nullptr;
+        *countOut = 0;
+    }
+    std::vector<RecoveredPacket*> got;
+    const Result r = d->dec->decode(got);
+    if (r != kSuccess) return (SiameseResult)r;
+    flush_locked();
+    d->out.clear();
+    for (RecoveredPacket* rp : got) {
+        StoredOriginal* o = nullptr;
+        if (d->dec->get(rp->packet_num, &o) != kSuccess || !o) { d->dec->set_disabled(); return Siamese_Disabled; }
+        if (!o->host) {
+            const uint32_t upper = rp->framed_upper;
+            uint8_t* host = (uint8_t*)malloc(upper ? upper : 1);
+            if (!host) { d->dec->set_disabled(); return Siamese_Disabled; }
+            g_rt->dev.download(host, row_byte_offset(rp->row), upper);
+            unsigned len = 0;
+            const int hb = get_length_header(host, upper, len);
+            // BackSubstitution's length check (SiameseDecoder.cpp:1139-1154).
+            if (hb < 1 || len == 0 || (uint32_t)hb + len > upper) {
+                free(host);
+                d->dec->set_disabled();
+                return Siamese_Disabled;
+            }
+            o->host = host;
+            o->header_bytes = (uint32_t)hb;
+            o->bytes = (uint32_t)hb + len;
+        }
+        SiameseOriginalPacket p;
+        p.PacketNum = rp->packet_num;
+        p.Data = (const unsigned char*)o->host + o->header_bytes;
+        p.DataBytes = o->bytes - o->header_bytes;
+        d->out.push_back(p);
+    }
+    if (packetsPtrOut) {
+        *packetsPtrOut = d->out.empty() ? nullptr : d->out.data();
+        *countOut = (unsigned)d->out.size();
+    }
+    return Siamese_Success;
+}
+
+SIAMESE_EXPORT SiameseResult siamese_decoder_ack(SiameseDecoder decoder_t, void* buffer, unsigned byteLimit,
+                                                 unsigned* usedBytes) {
+    CDecoder* d = reinterpret_cast<CDecoder*>(decoder_t);
+    if (!d || !buffer || !usedBytes || byteLimit < SIAMESE_ACK_MIN_BYTES) return Siamese_InvalidInput;
+    std::lock_guard<std::mutex> lk(g_rt->mu);
+    uint32_t used = 0;
+    const Result r = d->dec->ack((uint8_t*)buffer, byteLimit, &used);
+    *usedBytes = used;
+    return (SiameseResult)r;
+}
+
+SIAMESE_EXPORT SiameseResult siamese_decoder_stats(SiameseDecoder decoder_t, uint64_t* statsOut, unsigned statsCount) {
+    CDecoder* d = reinterpret_cast<CDecoder*>(decoder_t);
+    if (!d || !statsOut || statsCount <= 0) return Siamese_InvalidInput;
+    std::lock_guard<std::mutex> lk(g_rt->mu);
+    d->dec->stats(statsOut, statsCount);
+    return Siamese_Success;
+}
+
+} // extern "C"

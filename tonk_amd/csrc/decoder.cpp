@@ -41,9 +41,9 @@ Decoder::~Decoder() {
     while (r) { Recovery* n = r->next; free_recovery(r); r = n; }
     for (Recovery* g : graveyard_) delete g;
     graveyard_.clear();
+    pre_flush();  // snapshots already referenced by the pending program must still be written
     for (unsigned l = 0; l < kLanes; ++l)
         for (unsigned s = 0; s < kSums; ++s) lanes_[l][s].chain.release(ctx_->rows);
-    for (RecoveredPacket& p : recovered_) if (p.host && release_) { release_(p.host, user_); p.host = nullptr; }
     ctx_->detach(this);
 }
 

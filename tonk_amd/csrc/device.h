@@ -1,0 +1,86 @@
+// device.h -- HIP runtime of the engine: device arena, GF tables, program upload and
+// level-by-level execution on one HIP stream.  All byte work of the codec runs here.
+#pragma once
+
+#include "engine.h"
+
+#include <stdint.h>
+#include <vector>
+#include <string>
+
+namespace tamd {
+
+struct DeviceStats {
+    uint64_t programs = 0, launches = 0, ops = 0, items = 0, instrs = 0;
+    uint64_t upload_bytes = 0;
+    uint64_t acc_bytes = 0, store_bytes = 0;  // op-trace bytes of all programs run
+    double kernel_ms = 0;  // sum of tamd_exec durations (when timing is enabled)
+    uint64_t timed_launches = 0;
+};
+
+class Device {
+public:
+    ~Device();
+    // Opens `device`, allocates the arena and uploads the GF tables.  Returns false (with a
+    // message in error()) when no usable gfx950 device is present: the engine has no CPU path.
+    bool init(int device, uint64_t arena_bytes);
+    const std::string& error() const { return error_; }
+    uint64_t arena_bytes() const { return arena_bytes_; }
+    uint8_t* arena() const { return arena_; }
+    void* stream() const { return stream_; }
+
+    // Enqueue the pending programs of `ctxs` as one merged program (asynchronous).  Returns the
+    // completion ticket (monotonic); call completed() / wait() with it.
+    uint64_t run(Context* const* ctxs, size_t n);
+    uint64_t run(Context* ctx) { return run(&ctx, 1); }
+    bool completed(uint64_t ticket);
+    void wait(uint64_t ticket);
+    void synchronize();
+
+    // Host <-> arena copies (stream ordered).  upload() copies `src` into a pinned staging
+    // buffer first so the caller may reuse it immediately.
+    void upload(uint64_t arena_offset, const void* src, size_t n);
+    void download(void* dst, uint64_t arena_offset, size_t n);  // synchronous
+
+    // Bench helpers (kernels.hip).
+    struct GenDesc { uint32_t row, index, len, pad; uint64_t seed; };
+    void generate_rows(const std::vector<GenDesc>& d, uint32_t row_cap);
+    struct DigestDesc { uint32_t row, skip, len, pad; };
+    void digest_rows(const std::vector<DigestDesc>& d, std::vector<uint64_t>& out);
+    bool gf_selftest();  // device v_perm multiply vs host tables, all 65536 products
+
+    // Kernel timing with HIP events around every tamd_exec launch (on the launch stream).
+    void set_timing(bool on) { timing_ = on; }
+    DeviceStats& stats() { return stats_; }
+    void collect_timing();  // adds pending event pairs into stats().kernel_ms
+
+private:
+    std::string error_;
+    int device_ = -1;
+    uint8_t* arena_ = nullptr;
+    uint64_t arena_bytes_ = 0;
+    uint32_t* d_gf_ = nullptr;
+    void* stream_ = nullptr;
+    // program staging: pinned host buffers and device buffers, double buffered
+    struct Slot {
+        uint8_t* host = nullptr;
+        uint8_t* dev = nullptr;
+        size_t cap = 0;
+        void* done = nullptr;  // hipEvent_t
+        uint64_t ticket = 0;
+    };
+    Slot slots_[2];
+    int next_slot_ = 0;
+    uint64_t ticket_ = 0, completed_ = 0;
+    std::vector<void*> ticket_events_;
+    // upload staging
+    uint8_t* up_host_ = nullptr;
+    size_t up_cap_ = 0, up_used_ = 0;
+    void* up_event_ = nullptr;
+    bool timing_ = false;
+    std::vector<std::pair<void*, void*>> timing_events_;
+    DeviceStats stats_;
+    bool ensure_slot(Slot& s, size_t bytes);
+};
+
+} // namespace tamd

@@ -21,6 +21,7 @@ Encoder::Encoder(Context* ctx, uint32_t row_bytes, HostRelease release, void* us
 }
 
 Encoder::~Encoder() {
+    pre_flush();  // snapshots already referenced by the pending program must still be written
     for (size_t i = 0; i < win_.size(); ++i) drop_original(win_[i]);
     win_.clear();
     for (unsigned l = 0; l < kLanes; ++l)

@@ -10,7 +10,8 @@ namespace tamd {
 // ---------------------------------------------------------------------------------------------
 static const uint32_t kSmallClasses = 256;  // rows up to 16 KB use exact-size free lists
 
-void RowTable::init(uint64_t arena_bytes) {
+void RowTable::init(uint64_t arena_bytes, uint64_t base_units) {
+    base_ = base_units;
     const uint64_t units = arena_bytes / TAMD_ROW_UNIT;
     total_units_ = units > 0xfffffff0ull ? 0xfffffff0u : (uint32_t)units;
     bump_ = 0;

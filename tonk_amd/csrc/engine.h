@@ -50,8 +50,10 @@ typedef std::vector<Term> Sym;
 // ---------------------------------------------------------------------------------------------
 class RowTable {
 public:
-    void init(uint64_t arena_bytes);
+    // Manage `bytes` of the device arena starting at 64-byte unit `base_units`.
+    void init(uint64_t bytes, uint64_t base_units = 0);
     uint64_t arena_bytes() const { return (uint64_t)total_units_ * TAMD_ROW_UNIT; }
+    uint64_t base_units() const { return base_; }
 
     // Allocate a row with capacity >= bytes (rounded up to 64 B).  Returns kNoRow when full.
     RowId alloc(uint32_t bytes);
@@ -63,7 +65,7 @@ public:
     void release_up_to(uint64_t completed_epoch);
     void seal_epoch(uint64_t epoch);  // rows freed so far belong to `epoch`
 
-    uint32_t offset(RowId r) const { return meta_[r].off; }          // in 64-B units
+    uint32_t offset(RowId r) const { return (uint32_t)(base_ + meta_[r].off); }  // 64-B units
     uint32_t cap_bytes(RowId r) const { return meta_[r].units * TAMD_ROW_UNIT; }
     uint32_t level(RowId r) const { return meta_[r].level; }
     void set_level(RowId r, uint32_t l) { meta_[r].level = l; }
@@ -80,6 +82,7 @@ private:
     std::vector<Pending> pending_;
     std::vector<RowId> unsealed_;
     uint32_t total_units_ = 0, bump_ = 0;
+    uint64_t base_ = 0;
     uint64_t used_units_ = 0;
     size_t live_ = 0;
     void release(RowId r);

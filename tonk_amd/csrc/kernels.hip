@@ -1,0 +1,177 @@
+// kernels.hip -- CDNA4 (gfx950) kernels of the Siamese engine.
+//
+// tamd_exec runs one level of a device program (program.h).  Work item = (op, 512-byte slice):
+// one 64-lane wave owns 8 bytes per lane of one op's accumulator and walks the op's
+// instruction list (wave-uniform, scalar loads).  GF(2^8) byte multiplication by the
+// instruction's coefficient uses three 8-entry product tables per coefficient staged in LDS
+// and v_perm_b32 byte lookups (x*c = T0[x&7] ^ T1[(x>>3)&7] ^ T2[x>>6]), so a muladd costs
+// ~11 VALU ops per dword and no divergent LDS gathers.  Coefficient 1 is a plain XOR.
+// No MFMA: this is GF(2^8) table/XOR work.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "program.h"
+
+#define TAMD_WAVES_PER_WG 4
+#define TAMD_LANE_BYTES 8
+#define TAMD_SLICE_BYTES (64 * TAMD_LANE_BYTES)
+
+typedef unsigned long long u64;
+
+__device__ __forceinline__ uint32_t gf_mul4(uint32_t x, uint32_t t0lo, uint32_t t0hi, uint32_t t1lo,
+                                            uint32_t t1hi, uint32_t t2lo, uint32_t t2hi) {
+    const uint32_t s0 = x & 0x07070707u;
+    const uint32_t s1 = (x >> 3) & 0x07070707u;
+    const uint32_t s2 = (x >> 6) & 0x03030303u;
+    return __builtin_amdgcn_perm(t0hi, t0lo, s0) ^ __builtin_amdgcn_perm(t1hi, t1lo, s1) ^
+           __builtin_amdgcn_perm(t2hi, t2lo, s2);
+}
+
+__device__ __forceinline__ u64 byte_mask(uint32_t nbytes) {  // low `nbytes` bytes set (nbytes < 8)
+    return (1ull << (8u * nbytes)) - 1ull;
+}
+
+__device__ __forceinline__ uint32_t uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+extern "C" __global__ void __launch_bounds__(256)
+tamd_exec(const tamd_op* __restrict__ ops, const tamd_instr* __restrict__ instrs,
+          const uint2* __restrict__ items, uint32_t n_items, uint8_t* __restrict__ arena,
+          const uint32_t* __restrict__ gf_perm) {
+    __shared__ uint32_t lds_perm[256 * 8];
+    for (uint32_t i = threadIdx.x; i < 256 * 8; i += blockDim.x) lds_perm[i] = gf_perm[i];
+    __syncthreads();
+
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = uniform(threadIdx.x >> 6);
+    const uint32_t stride = gridDim.x * TAMD_WAVES_PER_WG;
+
+    for (uint32_t it = blockIdx.x * TAMD_WAVES_PER_WG + wave; it < n_items; it += stride) {
+        const uint2 item = items[it];
+        const tamd_op op = ops[uniform(item.x)];
+        const uint32_t o = uniform(item.y) * TAMD_SLICE_BYTES + lane * TAMD_LANE_BYTES;
+        u64 acc = 0;
+        const uint32_t end = op.first + op.count;
+        for (uint32_t k = op.first; k < end; ++k) {
+            const tamd_instr in = instrs[k];
+            const uint32_t kind = in.w0 & 0xffu;
+            if (kind == TAMD_I_ACC) {
+                const uint32_t len = in.len;
+                if (o < len) {
+                    const u64* src = (const u64*)(arena + (size_t)in.row * TAMD_ROW_UNIT + o);
+                    u64 v = *src;
+                    if (o + 8u > len) v &= byte_mask(len - o);
+                    const uint32_t coef = (in.w0 >> 8) & 0xffu;
+                    if (coef != 1u) {
+                        const uint32_t* t = &lds_perm[coef * 8u];
+                        const uint32_t t0lo = t[0], t0hi = t[1], t1lo = t[2], t1hi = t[3], t2lo = t[4], t2hi = t[5];
+                        const uint32_t lo = gf_mul4((uint32_t)v, t0lo, t0hi, t1lo, t1hi, t2lo, t2hi);
+                        const uint32_t hi = gf_mul4((uint32_t)(v >> 32), t0lo, t0hi, t1lo, t1hi, t2lo, t2hi);
+                        v = ((u64)hi << 32) | lo;
+                    }
+                    acc ^= v;
+                }
+            } else if (kind == TAMD_I_STORE) {
+                const tamd_instr f = instrs[k + 1];
+                ++k;
+                const uint32_t len = in.len, cap = in.cap;
+                if (o < cap) {
+                    const u64 footer = ((u64)f.len << 32) | f.row;
+                    u64 keep;
+                    if (o + 8u <= len) keep = ~0ull;
+                    else if (o >= len) keep = 0;
+                    else keep = byte_mask(len - o);
+                    u64 fpart = 0;
+                    if (o >= len) {
+                        const uint32_t sh = o - len;
+                        if (sh < 8u) fpart = footer >> (8u * sh);
+                    } else {
+                        const uint32_t sh = len - o;
+                        if (sh < 8u) fpart = footer << (8u * sh);
+                    }
+                    *(u64*)(arena + (size_t)in.row * TAMD_ROW_UNIT + o) = (acc & keep) | fpart;
+                }
+            } else if (kind == TAMD_I_CLEAR) {
+                acc = 0;
+            }
+        }
+    }
+}
+
+// GF self test: out[y * 256 + x] = x * y through the same v_perm path the executor uses.
+extern "C" __global__ void tamd_gf_selftest(const uint32_t* __restrict__ gf_perm, uint8_t* __restrict__ out) {
+    const uint32_t y = blockIdx.x;
+    const uint32_t x4 = threadIdx.x;  // 64 threads x 4 bytes
+    const uint32_t* t = &gf_perm[y * 8u];
+    const uint32_t xs = (x4 * 4u) | ((x4 * 4u + 1u) << 8) | ((x4 * 4u + 2u) << 16) | ((x4 * 4u + 3u) << 24);
+    const uint32_t r = gf_mul4(xs, t[0], t[1], t[2], t[3], t[4], t[5]);
+    *(uint32_t*)(out + y * 256u + x4 * 4u) = r;
+}
+
+// PCG32 (SiameseTools.h:79-101), used to generate the synthetic payloads on the device.
+struct DevPcg {
+    u64 state, inc;
+    __device__ void seed(u64 y, u64 x) {
+        state = 0;
+        inc = (y << 1u) | 1u;
+        next();
+        state += x;
+        next();
+    }
+    __device__ uint32_t next() {
+        const u64 old = state;
+        state = old * 6364136223846793005ULL + inc;
+        const uint32_t xs = (uint32_t)(((old >> 18) ^ old) >> 27);
+        const uint32_t rot = (uint32_t)(old >> 59);
+        return (xs >> rot) | (xs << ((uint32_t)(-(int32_t)rot) & 31u));
+    }
+};
+
+// Synthetic input rows (tonk_amd/csrc/workload.h payload_bytes): for each descriptor
+// {row offset (64-B units), packet index, payload length, row capacity, seed_data}, write
+// varint(len) || PCG bytes and zero-fill to the capacity.  One thread per packet (setup only).
+struct GenDesc { uint32_t row, index, len, cap; u64 seed; };
+
+extern "C" __global__ void tamd_gen_rows(const GenDesc* __restrict__ d, uint32_t n, uint8_t* __restrict__ arena,
+                                          uint32_t row_cap) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const GenDesc g = d[i];
+    uint8_t* dst = arena + (size_t)g.row * TAMD_ROW_UNIT;
+    uint8_t hdr[4];
+    uint32_t hb;
+    const uint32_t len = g.len;
+    if (len <= 0x7f) { hdr[0] = (uint8_t)len; hb = 1; }
+    else if (len <= 0x3fff) { hdr[0] = (uint8_t)(0x80 | (len >> 8)); hdr[1] = (uint8_t)len; hb = 2; }
+    else if (len <= 0x1fffff) { hdr[0] = (uint8_t)(0xC0 | (len >> 16)); hdr[1] = (uint8_t)(len >> 8); hdr[2] = (uint8_t)len; hb = 3; }
+    else { hdr[0] = (uint8_t)(0xE0 | (len >> 24)); hdr[1] = (uint8_t)(len >> 16); hdr[2] = (uint8_t)(len >> 8); hdr[3] = (uint8_t)len; hb = 4; }
+    for (uint32_t k = 0; k < hb; ++k) dst[k] = hdr[k];
+    DevPcg p;
+    p.seed(g.seed, g.index);
+    uint32_t k = 0;
+    for (; k + 4 <= len; k += 4) {
+        const uint32_t w = p.next();
+        dst[hb + k] = (uint8_t)w; dst[hb + k + 1] = (uint8_t)(w >> 8);
+        dst[hb + k + 2] = (uint8_t)(w >> 16); dst[hb + k + 3] = (uint8_t)(w >> 24);
+    }
+    if (k < len) {
+        const uint32_t w = p.next();
+        for (uint32_t b = 0; k + b < len; ++b) dst[hb + k + b] = (uint8_t)(w >> (8 * b));
+    }
+    const uint32_t cap = g.cap < row_cap ? g.cap : row_cap;
+    for (uint32_t z = hb + len; z < cap; ++z) dst[z] = 0;
+}
+
+// Digest of rows (FNV-1a 64 over `len` bytes starting `skip` bytes into the row): one thread
+// per row, for output verification after a timed run (not on the timed path).
+struct DigestDesc { uint32_t row, skip, len, pad; };
+
+extern "C" __global__ void tamd_digest_rows(const DigestDesc* __restrict__ d, uint32_t n,
+                                             const uint8_t* __restrict__ arena, u64* __restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const DigestDesc g = d[i];
+    const uint8_t* p = arena + (size_t)g.row * TAMD_ROW_UNIT + g.skip;
+    u64 h = 1469598103934665603ULL;
+    for (uint32_t k = 0; k < g.len; ++k) { h ^= p[k]; h *= 1099511628211ULL; }
+    out[i] = h;
+}

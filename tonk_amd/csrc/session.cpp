@@ -1,0 +1,467 @@
+// session.cpp -- batched device-resident runner (include/tonk_amd.h).
+//
+// Streams are partitioned over host worker threads.  Each worker owns one Context (a disjoint
+// range of the HBM arena and its own pending program) and the encoder/decoder/channel of its
+// streams.  A step: every worker advances its streams by N originals (control planes emit
+// symbolic ops), then the main thread merges all workers' programs into one and enqueues it
+// level by level on the device stream.  The host then starts the next step while the device
+// executes; rows freed during a step are reused only once that step's program has completed.
+#include "../../include/tonk_amd.h"
+
+#include "decoder.h"
+#include "device.h"
+#include "workload.h"
+
+#include <condition_variable>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <stdio.h>
+#include <string.h>
+
+using namespace tamd;
+
+namespace {
+
+struct Stream;
+
+// Transcript in the oracle's format; digests of device rows are filled after each program.
+struct SessTranscript {
+    bool on = false;
+    std::vector<std::string> lines;
+    struct PendEnc { RowId row; uint32_t total; RecoveryMeta meta; size_t pos; };
+    struct PendDec { RowId row; uint32_t upper; size_t pos; };
+    std::vector<PendEnc> pend_enc;
+    std::vector<PendDec> pend_dec;
+};
+
+struct Stream {
+    wl::Params p;
+    Context* ctx = nullptr;
+    std::unique_ptr<Encoder> enc;
+    std::unique_ptr<Decoder> dec;
+    std::vector<RowId> enc_rows, dec_rows;
+    std::vector<uint32_t> framed;
+    std::vector<uint8_t> dec_row_used;
+    SessTranscript tr;
+    uint64_t alg_bytes = 0, payload_bytes = 0;
+
+    // ---- workload backend ----
+    struct RecRef { RecoveryOut out; };
+    struct DecRef {};
+
+    int enc_add(uint32_t index, uint32_t len, uint32_t* col) {
+        const uint32_t hb = length_header_bytes(len);
+        const Result r = enc->add(enc_rows[index], hb + len, hb, len, nullptr, col);
+        if (r == kSuccess) {
+            enc_rows[index] = kNoRow;  // owned by the encoder now
+            alg_bytes += hb + len;
+            payload_bytes += len;
+        }
+        return r;
+    }
+    int enc_encode(RecRef& r) {
+        const Result rc = enc->encode(r.out);
+        if (rc == kSuccess) alg_bytes += r.out.total();
+        return rc;
+    }
+    int enc_ack(const uint8_t* buf, uint32_t n, uint32_t* next) { return enc->acknowledge(buf, n, next); }
+    int dec_add_original(uint32_t col, uint32_t index, uint32_t len) {
+        const uint32_t hb = length_header_bytes(len);
+        const RowId row = dec_rows[index];
+        if (row == kNoRow) return kInvalidInput;
+        bool took = false;
+        const Result r = dec->add_original(col, row, hb + len, hb, len, nullptr, &took);
+        dec_rows[index] = kNoRow;
+        if (!took) ctx->rows.free_deferred(row);
+        alg_bytes += hb + len;
+        return r;
+    }
+    void recovery_lost(const RecRef& r) { ctx->rows.free_deferred(r.out.row); }
+    int dec_add_recovery(const RecRef& r) {
+        uint8_t tail[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        const uint32_t tl = r.out.total() < 8 ? r.out.total() : 8;
+        memcpy(tail + tl - r.out.footer_len, r.out.footer, r.out.footer_len);
+        bool took = false;
+        const Result rc = dec->add_recovery(r.out.row, r.out.total(), tail, nullptr, &took);
+        if (!took) ctx->rows.free_deferred(r.out.row);
+        alg_bytes += r.out.total();
+        return rc;
+    }
+    int dec_is_ready() { return dec->is_ready(); }
+    std::vector<RecoveredPacket*> got_;
+    int dec_decode(std::vector<uint32_t>& nums, DecRef&) {
+        got_.clear();
+        const Result rc = dec->decode(got_);
+        if (rc == kSuccess) {
+            for (RecoveredPacket* rp : got_) {
+                nums.push_back(rp->packet_num);
+                alg_bytes += rp->framed_upper;
+                if (tr.on) tr.pend_dec.push_back(SessTranscript::PendDec{rp->row, rp->framed_upper, tr.lines.size()});
+            }
+        }
+        return rc;
+    }
+    int dec_ack(uint8_t* buf, uint32_t limit, uint32_t* used) { return dec->ack(buf, limit, used); }
+    void stats(uint64_t e[9], uint64_t d[11]) { enc->stats(e, 9); dec->stats(d, 11); }
+
+    // ---- transcript ----
+    void on_encode(int rc, const RecRef& r) {
+        if (!tr.on) return;
+        if (rc != 0) { tr.lines.push_back("E " + std::to_string(rc)); return; }
+        tr.pend_enc.push_back(SessTranscript::PendEnc{r.out.row, r.out.total(), r.out.meta, tr.lines.size()});
+        tr.lines.push_back("E ?");
+    }
+    void on_decode(int rc, const std::vector<uint32_t>& nums, const DecRef&) {
+        if (!tr.on) return;
+        std::string ln = "D " + std::to_string(rc) + " " + std::to_string(nums.size());
+        for (uint32_t n : nums) ln += " " + std::to_string(n) + "#";
+        // pend_dec entries were pushed with pos = lines.size() before this line is appended
+        tr.lines.push_back(ln);
+    }
+    void on_ack(int rd, const uint8_t* buf, uint32_t used, int re, uint32_t next) {
+        if (!tr.on) return;
+        char b[128];
+        snprintf(b, sizeof(b), "K %d %u %016llx %d %u", rd, used, (unsigned long long)wl::fnv1a(buf, used), re, next);
+        tr.lines.push_back(b);
+    }
+    void on_event(char kind, int rc, uint32_t a, uint32_t b) {
+        if (!tr.on || rc == 0) return;
+        char t[64];
+        snprintf(t, sizeof(t), "%c %d %u %u", kind, rc, a, b);
+        tr.lines.push_back(t);
+    }
+    void on_stats(const uint64_t e[9], const uint64_t d[11]) {
+        if (!tr.on) return;
+        std::string s = "S";
+        for (int i = 0; i < 8; ++i) s += " " + std::to_string(e[i]);
+        s += " |";
+        for (int i = 0; i < 10; ++i) s += " " + std::to_string(d[i]);
+        tr.lines.push_back(s);
+    }
+
+    std::unique_ptr<wl::Runner<Stream, Stream>> runner;
+};
+
+struct Worker {
+    Context ctx;
+    std::vector<Stream*> streams;
+};
+
+struct Session {
+    tamd_session_params prm;
+    Device dev;
+    std::vector<std::unique_ptr<Worker>> workers;
+    std::vector<std::unique_ptr<Stream>> streams;
+    std::vector<std::pair<uint64_t, uint64_t>> epoch_ticket;  // (epoch, ticket) awaiting release
+    uint64_t last_ticket = 0;
+    uint32_t row_cap = 0;
+    bool finished = false;
+    std::string error;
+
+    // worker pool
+    std::vector<std::thread> threads;
+    std::mutex mu;
+    std::condition_variable cv_start, cv_done;
+    std::function<void(Worker&)> job;
+    uint64_t job_gen = 0;
+    size_t job_left = 0;
+    bool quit = false;
+
+    ~Session() {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            quit = true;
+            ++job_gen;
+        }
+        cv_start.notify_all();
+        for (auto& t : threads) t.join();
+        dev.synchronize();
+        for (auto& s : streams) {
+            s->runner.reset();
+            s->enc.reset();
+            s->dec.reset();
+        }
+    }
+
+    void pool_loop(size_t wi) {
+        uint64_t seen = 0;
+        for (;;) {
+            std::function<void(Worker&)> f;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv_start.wait(lk, [&] { return job_gen != seen; });
+                seen = job_gen;
+                if (quit) return;
+                f = job;
+            }
+            f(*workers[wi]);
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                if (--job_left == 0) cv_done.notify_all();
+            }
+        }
+    }
+
+    void run_all(const std::function<void(Worker&)>& f) {
+        if (threads.empty()) {
+            for (auto& w : workers) f(*w);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            job = f;
+            job_left = workers.size();
+            ++job_gen;
+        }
+        cv_start.notify_all();
+        std::unique_lock<std::mutex> lk(mu);
+        cv_done.wait(lk, [&] { return job_left == 0; });
+    }
+
+    void release_completed() {
+        size_t k = 0;
+        for (size_t i = 0; i < epoch_ticket.size(); ++i) {
+            if (dev.completed(epoch_ticket[i].second)) {
+                for (auto& w : workers) w->ctx.rows.release_up_to(epoch_ticket[i].first);
+            } else {
+                epoch_ticket[k++] = epoch_ticket[i];
+            }
+        }
+        epoch_ticket.resize(k);
+    }
+
+    // Merge every worker's pending program, enqueue it, close the epoch.
+    void flush_all() {
+        std::vector<Context*> ctxs;
+        for (auto& w : workers) ctxs.push_back(&w->ctx);
+        last_ticket = dev.run(ctxs.data(), ctxs.size());
+        const uint64_t epoch = workers.empty() ? 0 : workers[0]->ctx.epoch;
+        for (auto& w : workers) w->ctx.finish_flush();
+        epoch_ticket.push_back(std::make_pair(epoch, last_ticket));
+        if (prm.record) resolve_transcripts();
+    }
+
+    void resolve_transcripts() {
+        dev.synchronize();
+        std::vector<uint8_t> buf;
+        for (auto& sp : streams) {
+            Stream& s = *sp;
+            char line[256];
+            for (auto& e : s.tr.pend_enc) {
+                buf.resize(e.total);
+                dev.download(buf.data(), (uint64_t)s.ctx->rows.offset(e.row) * TAMD_ROW_UNIT, e.total);
+                snprintf(line, sizeof(line), "E 0 %u %u %u %u %u %016llx", e.total, e.meta.Row, e.meta.ColumnStart,
+                         e.meta.SumCount, e.meta.LDPCCount, (unsigned long long)wl::fnv1a(buf.data(), e.total));
+                s.tr.lines[e.pos] = line;
+            }
+            s.tr.pend_enc.clear();
+            for (auto& d : s.tr.pend_dec) {
+                buf.resize(d.upper);
+                dev.download(buf.data(), (uint64_t)s.ctx->rows.offset(d.row) * TAMD_ROW_UNIT, d.upper);
+                unsigned len = 0;
+                const int hb = get_length_header(buf.data(), d.upper, len);
+                std::string& ln = s.tr.lines[d.pos];
+                if (hb < 1 || len + (unsigned)hb > d.upper) {
+                    error = "recovered row with a corrupt length header";
+                    continue;
+                }
+                snprintf(line, sizeof(line), ":%u:%016llx", len, (unsigned long long)wl::fnv1a(buf.data() + hb, len));
+                const size_t at = ln.find('#');
+                if (at != std::string::npos) ln.replace(at, 1, line);
+            }
+            s.tr.pend_dec.clear();
+        }
+    }
+};
+
+} // namespace
+
+extern "C" {
+
+void* tamd_session_create(const tamd_session_params* p, char* err, size_t err_len) {
+    auto fail = [&](const std::string& m) -> void* {
+        if (err && err_len) snprintf(err, err_len, "%s", m.c_str());
+        return nullptr;
+    };
+    if (!p || p->n_streams == 0) return fail("bad parameters");
+    if (!gf_init()) return fail("gf self test failed");
+    std::unique_ptr<Session> s(new Session());
+    s->prm = *p;
+    if (!s->dev.init((int)p->device, p->arena_bytes)) return fail(s->dev.error());
+    if (!s->dev.gf_selftest()) return fail("device GF(256) self test failed");
+
+    const uint32_t nthreads = p->n_threads ? (p->n_threads < p->n_streams ? p->n_threads : p->n_streams) : 1;
+    const uint64_t range = (s->dev.arena_bytes() / nthreads) & ~(uint64_t)(TAMD_ROW_UNIT - 1);
+    for (uint32_t t = 0; t < nthreads; ++t) {
+        std::unique_ptr<Worker> w(new Worker());
+        w->ctx.rows.init(range, (range / TAMD_ROW_UNIT) * t);
+        s->workers.push_back(std::move(w));
+    }
+    s->row_cap = ((p->payload_max + 4 + 63) / 64) * 64;
+    for (uint32_t i = 0; i < p->n_streams; ++i) {
+        std::unique_ptr<Stream> st(new Stream());
+        Worker& w = *s->workers[i % nthreads];
+        st->ctx = &w.ctx;
+        wl::Params& q = st->p;
+        q.stream_id = p->stream_base + i;
+        q.n_originals = p->n_originals;
+        q.payload_min = p->payload_min;
+        q.payload_max = p->payload_max;
+        q.loss_thresh = p->loss_thresh;
+        q.ge_enable = p->ge_enable;
+        q.gb_thresh = p->gb_thresh;
+        q.bg_thresh = p->bg_thresh;
+        q.loss_on_recovery = p->loss_on_recovery;
+        q.fec_rate_q16 = p->fec_rate_q16;
+        q.ack_every = p->ack_every;
+        q.ack_bytes = p->ack_bytes ? p->ack_bytes : 256;
+        q.arq_lag = p->arq_lag;
+        q.flush_max = p->flush_max;
+        q.seed_data = 1000 + q.stream_id;
+        q.seed_loss = 2000 + q.stream_id;
+        st->enc.reset(new Encoder(&w.ctx, s->row_cap));
+        st->dec.reset(new Decoder(&w.ctx, s->row_cap));
+        st->tr.on = p->record != 0;
+        w.streams.push_back(st.get());
+        s->streams.push_back(std::move(st));
+    }
+    for (auto& sp : s->streams) sp->runner.reset(new wl::Runner<Stream, Stream>(sp->p, *sp, *sp));
+    if (nthreads > 1) {
+        Session* raw = s.get();
+        for (uint32_t t = 0; t < nthreads; ++t) raw->threads.emplace_back([raw, t] { raw->pool_loop(t); });
+    }
+    return s.release();
+}
+
+int tamd_session_generate(void* sp) {
+    Session* s = (Session*)sp;
+    std::vector<Device::GenDesc> d;
+    for (auto& stp : s->streams) {
+        Stream& st = *stp;
+        const uint32_t n = st.p.n_originals;
+        st.enc_rows.assign(n, kNoRow);
+        st.dec_rows.assign(n, kNoRow);
+        for (uint32_t i = 0; i < n; ++i) {
+            const uint32_t len = wl::payload_length(st.p, i);
+            const uint32_t framed = length_header_bytes(len) + len;
+            for (int side = 0; side < 2; ++side) {
+                const RowId r = st.ctx->alloc(framed);
+                if (r == kNoRow) { s->error = "arena too small for the session inputs"; return -1; }
+                (side ? st.dec_rows : st.enc_rows)[i] = r;
+                Device::GenDesc g;
+                g.row = st.ctx->rows.offset(r);
+                g.index = i;
+                g.len = len;
+                g.pad = st.ctx->rows.cap_bytes(r);
+                g.seed = st.p.seed_data;
+                d.push_back(g);
+            }
+        }
+    }
+    s->dev.generate_rows(d, s->row_cap);
+    return s->dev.error().empty() ? 0 : -2;
+}
+
+int tamd_session_step(void* sp, uint32_t originals) {
+    Session* s = (Session*)sp;
+    s->release_completed();
+    s->run_all([originals](Worker& w) {
+        for (Stream* st : w.streams) st->runner->advance(originals);
+        w.ctx.prepare_flush();
+    });
+    s->flush_all();
+    for (auto& w : s->workers) if (w->ctx.oom) { s->error = "arena exhausted"; return -1; }
+    return s->error.empty() ? 0 : -1;
+}
+
+int tamd_session_wait(void* sp) {
+    Session* s = (Session*)sp;
+    s->dev.synchronize();
+    s->release_completed();
+    return s->dev.error().empty() && s->error.empty() ? 0 : -1;
+}
+
+int tamd_session_finish(void* sp) {
+    Session* s = (Session*)sp;
+    if (!s->finished) {
+        s->release_completed();
+        s->run_all([](Worker& w) {
+            for (Stream* st : w.streams) st->runner->finish();
+            w.ctx.prepare_flush();
+        });
+        s->flush_all();
+        s->finished = true;
+    }
+    return tamd_session_wait(sp);
+}
+
+int tamd_session_summary(void* sp, uint64_t* out, unsigned n) {
+    Session* s = (Session*)sp;
+    uint64_t v[TAMD_SUM_COUNT] = {0};
+    for (auto& stp : s->streams) {
+        const wl::Summary& q = stp->runner->summary();
+        v[TAMD_SUM_ORIGINALS] += q.originals;
+        v[TAMD_SUM_LOST_ORIGINALS] += q.lost_originals;
+        v[TAMD_SUM_RECOVERIES] += q.recoveries;
+        v[TAMD_SUM_LOST_RECOVERIES] += q.lost_recoveries;
+        v[TAMD_SUM_RECOVERED] += q.recovered;
+        v[TAMD_SUM_ARQ] += q.arq_redelivered;
+        v[TAMD_SUM_MISSING_AT_END] += q.missing_at_end;
+        v[TAMD_SUM_PAYLOAD_BYTES] += stp->payload_bytes;
+        v[TAMD_SUM_ALG_BYTES] += stp->alg_bytes;
+        v[TAMD_SUM_DISABLED_CODECS] += (stp->enc->disabled() ? 1 : 0) + (stp->dec->disabled() ? 1 : 0);
+    }
+    const DeviceStats& ds = s->dev.stats();
+    v[TAMD_SUM_PROGRAMS] = ds.programs;
+    v[TAMD_SUM_LAUNCHES] = ds.launches;
+    v[TAMD_SUM_OPS] = ds.ops;
+    v[TAMD_SUM_INSTRS] = ds.instrs;
+    v[TAMD_SUM_UPLOAD_BYTES] = ds.upload_bytes;
+    v[TAMD_SUM_ACC_BYTES] = ds.acc_bytes;
+    v[TAMD_SUM_STORE_BYTES] = ds.store_bytes;
+    if (n > TAMD_SUM_COUNT) n = TAMD_SUM_COUNT;
+    for (unsigned i = 0; i < n; ++i) out[i] = v[i];
+    return s->error.empty() ? 0 : -1;
+}
+
+void tamd_session_set_timing(void* sp, int on) { ((Session*)sp)->dev.set_timing(on != 0); }
+
+double tamd_session_kernel_ms(void* sp, uint64_t* launches) {
+    Session* s = (Session*)sp;
+    s->dev.collect_timing();
+    if (launches) *launches = s->dev.stats().timed_launches;
+    return s->dev.stats().kernel_ms;
+}
+
+size_t tamd_session_transcript(void* sp, uint32_t stream, char* buf, size_t cap) {
+    Session* s = (Session*)sp;
+    if (stream >= s->streams.size()) return 0;
+    std::string all;
+    for (const std::string& l : s->streams[stream]->tr.lines) { all += l; all += '\n'; }
+    if (buf && cap) {
+        const size_t n = all.size() < cap - 1 ? all.size() : cap - 1;
+        memcpy(buf, all.data(), n);
+        buf[n] = 0;
+    }
+    return all.size() + 1;
+}
+
+void tamd_session_destroy(void* sp) { delete (Session*)sp; }
+
+int tamd_device_selftest(uint32_t device, char* err, size_t err_len) {
+    Device d;
+    if (!d.init((int)device, 1 << 20)) {
+        if (err && err_len) snprintf(err, err_len, "%s", d.error().c_str());
+        return -1;
+    }
+    if (!d.gf_selftest()) {
+        if (err && err_len) snprintf(err, err_len, "v_perm GF(256) multiply mismatch");
+        return -2;
+    }
+    return 0;
+}
+
+} // extern "C"

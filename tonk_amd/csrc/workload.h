@@ -63,7 +63,7 @@ struct Params {
 
 // Payload bytes of original i (index within the stream).  Length and contents come from a
 // PCG stream seeded with (seed_data, i) so any packet can be regenerated independently (the
-// device generator in the bench uses the same definition).
+// device generator in the bench uses the same definition, kernels.hip tamd_gen_rows).
 inline uint32_t payload_length(const Params& p, uint32_t i) {
     if (p.payload_min == p.payload_max) return p.payload_min;
     Pcg g;
@@ -113,120 +113,152 @@ struct Summary {
 };
 
 // Backend concept (all methods return siamese.h result codes, 0 = success):
+//   typedef RecRef, DecRef
 //   int  enc_add(uint32_t index, uint32_t len, uint32_t* packetNumOut)
 //   int  enc_encode(RecRef& out)              -- out describes the recovery packet
 //   int  enc_ack(const uint8_t* buf, uint32_t n, uint32_t* nextExpected)
 //   int  dec_add_original(uint32_t packetNum, uint32_t index, uint32_t len)
 //   int  dec_add_recovery(const RecRef& r)
+//   void recovery_lost(const RecRef& r)       -- the channel dropped the packet
 //   int  dec_is_ready()
 //   int  dec_decode(std::vector<uint32_t>& packetNums, DecRef& out)
 //   int  dec_ack(uint8_t* buf, uint32_t limit, uint32_t* used)
 //   void stats(uint64_t enc[9], uint64_t dec[11])
 // Transcript concept:
 //   on_encode(int rc, const RecRef&), on_decode(int rc, nums, const DecRef&), on_ack(...),
-//   on_event(char kind, int rc, uint32_t a, uint32_t b)
+//   on_event(char kind, int rc, uint32_t a, uint32_t b), on_stats(enc, dec)
 template <class Backend, class Transcript>
-Summary run_stream(const Params& p, Backend& be, Transcript& tr) {
-    Summary s;
-    LossChannel ch;
-    ch.init(p);
-    std::vector<uint8_t> have(p.n_originals, 0);      // received or recovered at the decoder
-    std::vector<uint32_t> colOf(p.n_originals, 0);    // packet number assigned by the encoder
-    std::vector<uint32_t> pendingArq;                 // indices of lost originals
-    size_t arqHead = 0;
-    uint32_t tokens = 0;
-    std::vector<uint32_t> nums;
+class Runner {
+public:
+    Runner(const Params& p, Backend& be, Transcript& tr) : p_(p), be_(be), tr_(tr) {
+        ch_.init(p_);
+        have_.assign(p_.n_originals, 0);
+        col_of_.assign(p_.n_originals, 0);
+    }
 
-    // Column -> index map (packet numbers are assigned sequentially from 0 by the encoder).
-    auto decode_loop = [&]() {
-        while (be.dec_is_ready() == 0) {
-            nums.clear();
-            typename Backend::DecRef dref;
-            const int rc = be.dec_decode(nums, dref);
-            ++s.decode_calls;
-            tr.on_decode(rc, nums, dref);
-            if (rc != 0) break;
-            for (uint32_t c : nums) {
-                if (c < p.n_originals && !have[c]) { have[c] = 1; ++s.recovered; }
-            }
-            if (nums.empty()) break;
+    uint32_t position() const { return next_; }
+    const Summary& summary() const { return s_; }
+
+    // Feed the next `n` originals (and everything they trigger).
+    void advance(uint32_t n) {
+        const uint32_t end = std::min(p_.n_originals, next_ + n);
+        for (; next_ < end; ++next_) one(next_);
+    }
+
+    // End of stream: lossless recovery packets until the decoder has everything, then stats.
+    void finish() {
+        advance(p_.n_originals);
+        for (uint32_t k = 0; k < p_.flush_max; ++k) {
+            bool complete = true;
+            for (uint32_t i = 0; i < p_.n_originals; ++i) if (!have_[i]) { complete = false; break; }
+            if (complete) break;
+            ++s_.flush_encodes;
+            send_recovery(false);
         }
-    };
+        for (uint32_t i = 0; i < p_.n_originals; ++i) if (!have_[i]) ++s_.missing_at_end;
+        uint64_t es[9] = {0}, ds[11] = {0};
+        be_.stats(es, ds);
+        tr_.on_stats(es, ds);
+    }
 
-    auto send_recovery = [&](bool lossy) {
+private:
+    const Params& p_;
+    Backend& be_;
+    Transcript& tr_;
+    Summary s_;
+    LossChannel ch_;
+    std::vector<uint8_t> have_;
+    std::vector<uint32_t> col_of_, pending_arq_;
+    size_t arq_head_ = 0;
+    uint32_t tokens_ = 0, next_ = 0;
+    std::vector<uint32_t> nums_;
+
+    void decode_loop() {
+        while (be_.dec_is_ready() == 0) {
+            nums_.clear();
+            typename Backend::DecRef dref;
+            const int rc = be_.dec_decode(nums_, dref);
+            ++s_.decode_calls;
+            tr_.on_decode(rc, nums_, dref);
+            if (rc != 0) break;
+            for (uint32_t c : nums_) {
+                if (c < p_.n_originals && !have_[c]) { have_[c] = 1; ++s_.recovered; }
+            }
+            if (nums_.empty()) break;
+        }
+    }
+
+    void send_recovery(bool lossy) {
         typename Backend::RecRef r;
-        const int rc = be.enc_encode(r);
-        tr.on_encode(rc, r);
+        const int rc = be_.enc_encode(r);
+        tr_.on_encode(rc, r);
         if (rc != 0) return;
-        ++s.recoveries;
-        if (lossy && p.loss_on_recovery && ch.lost()) { ++s.lost_recoveries; return; }
-        const int rr = be.dec_add_recovery(r);
-        tr.on_event('R', rr, 0, 0);
+        ++s_.recoveries;
+        if (lossy && p_.loss_on_recovery && ch_.lost()) {
+            ++s_.lost_recoveries;
+            be_.recovery_lost(r);
+            return;
+        }
+        const int rr = be_.dec_add_recovery(r);
+        tr_.on_event('R', rr, 0, 0);
         decode_loop();
-    };
+    }
 
-    for (uint32_t i = 0; i < p.n_originals; ++i) {
-        const uint32_t len = payload_length(p, i);
+    void one(uint32_t i) {
+        const uint32_t len = payload_length(p_, i);
         uint32_t col = 0;
-        const int ra = be.enc_add(i, len, &col);
-        tr.on_event('a', ra, i, col);
-        colOf[i] = col;
-        ++s.originals;
-        if (ch.lost()) {
-            ++s.lost_originals;
-            pendingArq.push_back(i);
+        const int ra = be_.enc_add(i, len, &col);
+        tr_.on_event('a', ra, i, col);
+        col_of_[i] = col;
+        ++s_.originals;
+        if (ch_.lost()) {
+            ++s_.lost_originals;
+            pending_arq_.push_back(i);
         } else {
-            const int ro = be.dec_add_original(col, i, len);
-            tr.on_event('O', ro, col, 0);
-            if (!have[i]) have[i] = 1;
+            const int ro = be_.dec_add_original(col, i, len);
+            tr_.on_event('O', ro, col, 0);
+            if (!have_[i]) have_[i] = 1;
             decode_loop();
         }
 
-        tokens += p.fec_rate_q16;
-        while (tokens >= 65536u) {
-            tokens -= 65536u;
+        tokens_ += p_.fec_rate_q16;
+        while (tokens_ >= 65536u) {
+            tokens_ -= 65536u;
             send_recovery(true);
         }
 
-        if (p.ack_every && (i + 1) % p.ack_every == 0) {
-            std::vector<uint8_t> buf(p.ack_bytes);
+        if (p_.ack_every && (i + 1) % p_.ack_every == 0) {
+            uint8_t buf[2048];
+            const uint32_t limit = p_.ack_bytes < sizeof(buf) ? p_.ack_bytes : (uint32_t)sizeof(buf);
             uint32_t used = 0;
-            const int rd = be.dec_ack(buf.data(), p.ack_bytes, &used);
+            const int rd = be_.dec_ack(buf, limit, &used);
             uint32_t next = 0;
             int re = -1;
-            if (rd == 0 && used > 0) re = be.enc_ack(buf.data(), used, &next);
-            tr.on_ack(rd, buf.data(), used, re, next);
-            ++s.acks;
+            if (rd == 0 && used > 0) re = be_.enc_ack(buf, used, &next);
+            tr_.on_ack(rd, buf, used, re, next);
+            ++s_.acks;
         }
 
-        if (p.arq_lag) {
-            while (arqHead < pendingArq.size() && i - pendingArq[arqHead] >= p.arq_lag) {
-                const uint32_t j = pendingArq[arqHead++];
-                if (!have[j]) {
-                    const int ro = be.dec_add_original(colOf[j], j, payload_length(p, j));
-                    tr.on_event('X', ro, colOf[j], 0);
-                    have[j] = 1;
-                    ++s.arq_redelivered;
+        if (p_.arq_lag) {
+            while (arq_head_ < pending_arq_.size() && i - pending_arq_[arq_head_] >= p_.arq_lag) {
+                const uint32_t j = pending_arq_[arq_head_++];
+                if (!have_[j]) {
+                    const int ro = be_.dec_add_original(col_of_[j], j, payload_length(p_, j));
+                    tr_.on_event('X', ro, col_of_[j], 0);
+                    have_[j] = 1;
+                    ++s_.arq_redelivered;
                     decode_loop();
                 }
             }
         }
     }
+};
 
-    // End-of-stream flush: lossless recovery packets until the decoder has everything.
-    for (uint32_t k = 0; k < p.flush_max; ++k) {
-        bool complete = true;
-        for (uint32_t i = 0; i < p.n_originals; ++i) if (!have[i]) { complete = false; break; }
-        if (complete) break;
-        ++s.flush_encodes;
-        send_recovery(false);
-    }
-    for (uint32_t i = 0; i < p.n_originals; ++i) if (!have[i]) ++s.missing_at_end;
-
-    uint64_t es[9] = {0}, ds[11] = {0};
-    be.stats(es, ds);
-    tr.on_stats(es, ds);
-    return s;
+template <class Backend, class Transcript>
+Summary run_stream(const Params& p, Backend& be, Transcript& tr) {
+    Runner<Backend, Transcript> r(p, be, tr);
+    r.finish();
+    return r.summary();
 }
 
 } // namespace wl
