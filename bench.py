@@ -1,0 +1,226 @@
+#!/usr/bin/env python3
+"""Siamese FEC encode+decode throughput on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[3], per-GPU shard; weak scaling): every GPU runs 64
+independent connection streams (encoder + decoder + lossy channel each, stream ids
+rank*64 .. rank*64+63), 1300-byte payloads, 1% uniform loss on originals and recovery packets,
+recovery rate f = max(2p, 1%) = 2%, acknowledgements every 64 originals.  Payloads are
+synthetic (PCG, seed 1000 + stream id) and already resident in HBM when timing starts.
+
+A step = 4096 originals per stream: the host control planes (16 worker threads per GPU) turn
+every add/encode/ack/decode into device ops and each step's byte work runs as one merged
+program on the GPU, pipelined with the host building the next step.  `value` is whole-job
+payload GiB/s over all ranks; the timed region is bracketed by a barrier and a device sync.
+
+roofline: algorithmic HBM bytes (SURVEY.md s8(d) B_alg, counted exactly per step) divided by
+the summed duration of the tamd_exec launches of the timed steps (HIP events on the launch
+stream), against the 8.0 TB/s HBM3E peak.  cpu_baseline: the reference codec (compiled from
+/root/reference by oracle/Makefile, shipped prebuilt in oracle/_ref) on the same workload
+sample, rank 0 only.
+
+usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import tonk_amd  # noqa: E402
+
+METRIC = "Siamese FEC encode+decode GiB/s (device-resident), 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0
+STREAMS_PER_GPU = 64
+ORIGINALS_PER_STEP = 4096
+LOSS = 0.01
+ACK = 64
+PAYLOAD = 1300
+
+
+def host_threads(local_world: int) -> int:
+    try:
+        cpus = len(os.sched_getaffinity(0))
+    except Exception:
+        cpus = os.cpu_count() or 8
+    per = max(1, cpus // max(1, local_world))
+    env = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
+    return max(1, min(16, per, env))
+
+
+def cpu_baseline(threads: int, target_s: float = 10.0) -> dict | None:
+    """The reference codec (oracle/_ref, compiled from /root/reference sources) on a bounded
+    sample of the same workload: 64 streams x 16384 originals, repeated with fresh codecs until
+    about `target_s` seconds of wall time on `threads` host threads."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "golden_gen")
+    if not os.path.exists(exe):
+        return None
+    n = 4 * ORIGINALS_PER_STEP
+    wp = tonk_amd.WorkloadParams(n=n, payload=PAYLOAD, loss=LOSS, ack=ACK)
+
+    def run(reps: int) -> dict | None:
+        args = [exe, "time", f"threads={threads}", f"streams={STREAMS_PER_GPU}", f"reps={reps}"] + wp.args()
+        r = subprocess.run(args, capture_output=True, text=True, timeout=900)
+        if r.returncode != 0:
+            return None
+        return json.loads(r.stdout.strip().splitlines()[-1])
+
+    probe = run(2)
+    if probe is None:
+        return None
+    per_rep = max(probe["seconds"] / 2, 1e-3)
+    reps = int(min(400, max(2, round(target_s / per_rep))))
+    j = run(reps)
+    if j is None:
+        return None
+    return {"value": round(j["gib_per_s"], 4), "unit": "GiB/s", "cores": threads, "kind": "reference",
+            "sample": f"{STREAMS_PER_GPU} streams x {n} originals x {PAYLOAD} B x {reps} repetitions "
+                      f"(same loss/FEC/ack workload, fresh codecs per repetition), {threads} host threads, "
+                      f"{j['seconds']:.2f} s"}
+
+
+def stream_base(rank: int) -> int:
+    """Weak scaling: rank r owns streams [64 r, 64 r + 64) -- disjoint, no data-path exchange."""
+    return rank * STREAMS_PER_GPU
+
+
+class Dist:
+    """Control-plane synchronisation between ranks (gloo; the data path has no collective)."""
+
+    def __init__(self, world: int):
+        self.world = world
+        self.dist = None
+        if world > 1:
+            import torch.distributed as dist
+            if not dist.is_initialized():
+                dist.init_process_group("gloo")
+            self.dist = dist
+
+    def barrier(self) -> None:
+        if self.dist is not None:
+            self.dist.barrier()
+
+    def _reduce(self, x: float, op_name: str) -> float:
+        if self.dist is None:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self.dist.all_reduce(t, op=getattr(self.dist.ReduceOp, op_name))
+        return float(t.item())
+
+    def allmax(self, x: float) -> float:
+        return self._reduce(x, "MAX")
+
+    def allsum(self, x: float) -> float:
+        return self._reduce(x, "SUM")
+
+    def close(self) -> None:
+        if self.dist is not None:
+            self.dist.destroy_process_group()
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    a = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    d = Dist(world)
+
+    threads = host_threads(local_world)
+    total_steps = a.warmup + a.steps
+    n_orig = total_steps * ORIGINALS_PER_STEP
+    wp = tonk_amd.WorkloadParams(n=n_orig, payload=PAYLOAD, loss=LOSS, ack=ACK)
+    sess = tonk_amd.Session(wp, n_streams=STREAMS_PER_GPU, device=local_rank,
+                            stream_base=stream_base(rank), threads=threads,
+                            arena_bytes=(2 * n_orig * STREAMS_PER_GPU * 1344) + (4 << 30))
+    sess.generate()
+
+    for _ in range(a.warmup):
+        sess.step(ORIGINALS_PER_STEP)
+    sess.wait()
+    s0 = sess.summary()
+    sess.set_timing(True)
+    d.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        sess.step(ORIGINALS_PER_STEP)
+    sess.wait()
+    t1 = time.perf_counter()
+    d.barrier()
+    sess.set_timing(False)
+    kernel_ms, launches = sess.kernel_ms()
+    s1 = sess.summary()
+    elapsed = d.allmax(t1 - t0)
+
+    payload = s1["payload_bytes"] - s0["payload_bytes"]
+    alg = s1["alg_bytes"] - s0["alg_bytes"]
+    total_payload = d.allsum(payload)
+    value = total_payload / elapsed / 2**30
+
+    # Correctness of the run itself: finish the streams (lossless flush) and require that every
+    # original was received or recovered and no codec was disabled.
+    sess.finish()
+    fin = sess.summary()
+    ok = fin["missing_at_end"] == 0 and fin["disabled_codecs"] == 0
+    sess.close()
+
+    achieved = alg / (kernel_ms / 1e3) / 1e9 if kernel_ms > 0 else 0.0
+    out = {
+        "metric": METRIC,
+        "value": round(value, 4),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(elapsed * 1e3 / a.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic",
+        "config": {
+            "workload": "configs[3] per-GPU shard: 64 independent streams/GPU, 4096 originals per stream per step, "
+                        "1300 B payloads, 1% uniform loss, f=2%, ack every 64",
+            "streams_per_gpu": STREAMS_PER_GPU, "originals_per_step": ORIGINALS_PER_STEP, "payload_bytes": PAYLOAD,
+            "loss": LOSS, "ack_every": ACK, "host_threads_per_gpu": threads,
+            "parallelism": f"streams sharded {STREAMS_PER_GPU}/GPU x {world} GPU, no collective",
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 2),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": None,
+            "kernel": "tamd_exec",
+            "launches": launches,
+            "avg_launch_us": round(kernel_ms * 1e3 / launches, 3) if launches else None,
+            "alg_bytes_per_launch": round(alg / launches, 1) if launches else None,
+            "device_busy_frac": round((kernel_ms / 1e3) / (t1 - t0), 4),
+        },
+        "cpu_baseline": None,
+        "checks": {"all_recovered": ok, "recovered": fin["recovered"], "lost_originals": fin["lost_originals"],
+                   "lost_recoveries": fin["lost_recoveries"]},
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(threads)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    d.close()
+    return 0 if ok else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -7,7 +7,7 @@
 // packet is also checked against the true payload so a fixture can never pin a wrong decode.
 //
 // usage: golden_gen transcript <out.txt> key=value...
-//        golden_gen time threads=T streams=S key=value...
+//        golden_gen time threads=T streams=S reps=R key=value...
 #include "siamese.h"
 
 #include "../tonk_amd/csrc/workload.h"
@@ -48,6 +48,13 @@ struct RefBackend {
     ~RefBackend() {
         siamese_encoder_free(enc);
         siamese_decoder_free(dec);
+    }
+    // Fresh codecs for a repeated run over the same (already generated) payloads.
+    void reset_codecs() {
+        siamese_encoder_free(enc);
+        siamese_decoder_free(dec);
+        enc = siamese_encoder_create();
+        dec = siamese_decoder_create();
     }
     const uint8_t* pay(uint32_t i) const { return payloads.data() + (size_t)i * stride; }
 
@@ -165,7 +172,7 @@ struct RefTranscript {
     }
 };
 
-static bool parse_kv(Params& p, int& threads, int& streams, const char* kv) {
+static bool parse_kv(Params& p, int& threads, int& streams, int& reps, const char* kv) {
     const char* eq = strchr(kv, '=');
     if (!eq) return false;
     std::string k(kv, eq - kv);
@@ -188,6 +195,7 @@ static bool parse_kv(Params& p, int& threads, int& streams, const char* kv) {
     else if (k == "seed_loss") p.seed_loss = v;
     else if (k == "threads") threads = (int)v;
     else if (k == "streams") streams = (int)v;
+    else if (k == "reps") reps = (int)v;
     else return false;
     return true;
 }
@@ -199,11 +207,11 @@ int main(int argc, char** argv) {
     }
     if (siamese_init() != 0) { fprintf(stderr, "siamese_init failed\n"); return 3; }
     Params base;
-    int threads = 1, streams = 1;
+    int threads = 1, streams = 1, reps = 1;
     const bool timing = strcmp(argv[1], "time") == 0;
     const int first_kv = timing ? 2 : 3;
     for (int i = first_kv; i < argc; ++i) {
-        if (!parse_kv(base, threads, streams, argv[i])) { fprintf(stderr, "bad arg %s\n", argv[i]); return 2; }
+        if (!parse_kv(base, threads, streams, reps, argv[i])) { fprintf(stderr, "bad arg %s\n", argv[i]); return 2; }
     }
 
     if (!timing) {
@@ -226,7 +234,8 @@ int main(int argc, char** argv) {
     }
 
     // Timing: `streams` independent streams (stream id s uses seeds 1000+s / 2000+s) spread
-    // over `threads` host threads; payload generation happens before the clock starts.
+    // over `threads` host threads, each stream's workload run `reps` times with fresh codecs;
+    // payload generation happens before the clock starts.
     std::atomic<int> next{0};
     std::atomic<unsigned long long> bytes{0}, bad{0};
     std::vector<std::thread> pool;
@@ -244,12 +253,15 @@ int main(int argc, char** argv) {
             for (;;) {
                 const int s = next++;
                 if (s >= streams) break;
-                RefTranscript tr;
-                tr.enabled = false;
-                run_stream(ps[s], *bes[s], tr);
                 unsigned long long b = 0;
                 for (uint32_t i = 0; i < ps[s].n_originals; ++i) b += bes[s]->lens[i];
-                bytes += b;
+                for (int r = 0; r < reps; ++r) {
+                    if (r) bes[s]->reset_codecs();
+                    RefTranscript tr;
+                    tr.enabled = false;
+                    run_stream(ps[s], *bes[s], tr);
+                    bytes += b;
+                }
                 bad += bes[s]->bad_recoveries;
             }
         });
@@ -257,8 +269,8 @@ int main(int argc, char** argv) {
     for (auto& th : pool) th.join();
     const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     printf("{\"seconds\": %.6f, \"payload_bytes\": %llu, \"gib_per_s\": %.6f, \"threads\": %d, "
-           "\"streams\": %d, \"bad\": %llu}\n",
+           "\"streams\": %d, \"reps\": %d, \"bad\": %llu}\n",
            sec, (unsigned long long)bytes.load(), bytes.load() / sec / (1024.0 * 1024 * 1024),
-           threads, streams, (unsigned long long)bad.load());
+           threads, streams, reps, (unsigned long long)bad.load());
     return bad.load() ? 5 : 0;
 }

@@ -18,6 +18,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+from oracle_py import fnv1a, length_header, payload_lengths, payloads  # noqa: E402,F401
 NATIVE = os.path.join(ROOT, "tests", "native")
 
 
@@ -52,6 +54,15 @@ def golden_text(name: str) -> str:
 
 def sha256(text: str) -> str:
     return hashlib.sha256(text.encode()).hexdigest()
+
+
+def scenario_params(golden_index, name) -> dict:
+    sc = golden_index["scenarios"][name]
+    kv = {k: int(v) for k, v in (a.split("=") for a in sc["args"])}
+    kv["stream"] = sc["stream"]
+    kv["seed_data"] = 1000 + sc["stream"]
+    kv["seed_loss"] = 2000 + sc["stream"]
+    return kv
 
 
 def first_diff(a: str, b: str) -> str:

@@ -1,0 +1,153 @@
+// cp_bench.cpp -- TEST/PROFILING ONLY.  Host control-plane cost of the bench workload with no
+// device: the same backend the session uses (device rows are just handles; programs are built
+// and then dropped).  Reports ns per original per thread; build with -pg for gprof.
+//
+// usage: cp_bench streams=S n=N step=K [workload keys]
+#include "../../tonk_amd/csrc/decoder.h"
+#include "../../tonk_amd/csrc/workload.h"
+#include "../../tonk_amd/csrc/prof.h"
+
+#include <chrono>
+#include <memory>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <string>
+
+using namespace tamd;
+
+#ifdef TAMD_PROF
+namespace tamd { namespace prof {
+thread_local uint64_t cycles[kSlots];
+thread_local uint64_t calls[kSlots];
+const char* const names[kSlots] = {"enc_add", "enc_encode", "enc_ack", "dec_add_orig", "dec_add_rec", "dec_decode",
+    "dec_ack", "dec_is_ready", "gen_matrix", "ge", "elim", "lower_tri", "back_sub", "chain_flush", "sym_merge",
+    "flush_all"};
+} }
+#endif
+
+struct Null {
+    struct RecRef { RecoveryOut out; };
+    struct DecRef {};
+    Context* ctx;
+    Encoder* enc;
+    Decoder* dec;
+    std::vector<RowId> enc_rows, dec_rows;
+    uint64_t instrs = 0;
+    int enc_add(uint32_t index, uint32_t len, uint32_t* col) {
+        const uint32_t hb = length_header_bytes(len);
+        TAMD_PROF_SCOPE(kEncAdd);
+        return enc->add(enc_rows[index], hb + len, hb, len, nullptr, col);
+    }
+    int enc_encode(RecRef& r) { TAMD_PROF_SCOPE(kEncEncode); return enc->encode(r.out); }
+    int enc_ack(const uint8_t* b, uint32_t n, uint32_t* next) { TAMD_PROF_SCOPE(kEncAck); return enc->acknowledge(b, n, next); }
+    int dec_add_original(uint32_t col, uint32_t index, uint32_t len) {
+        const uint32_t hb = length_header_bytes(len);
+        TAMD_PROF_SCOPE(kDecAddOrig);
+        bool took = false;
+        const int r = dec->add_original(col, dec_rows[index], hb + len, hb, len, nullptr, &took);
+        if (!took) ctx->rows.free_deferred(dec_rows[index]);
+        return r;
+    }
+    void recovery_lost(const RecRef& r) { ctx->rows.free_deferred(r.out.row); }
+    int dec_add_recovery(const RecRef& r) {
+        uint8_t tail[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        const uint32_t tl = r.out.total() < 8 ? r.out.total() : 8;
+        memcpy(tail + tl - r.out.footer_len, r.out.footer, r.out.footer_len);
+        TAMD_PROF_SCOPE(kDecAddRec);
+        bool took = false;
+        const int rc = dec->add_recovery(r.out.row, r.out.total(), tail, nullptr, &took);
+        if (!took) ctx->rows.free_deferred(r.out.row);
+        return rc;
+    }
+    int dec_is_ready() { TAMD_PROF_SCOPE(kDecIsReady); return dec->is_ready(); }
+    std::vector<RecoveredPacket*> got;
+    int dec_decode(std::vector<uint32_t>& nums, DecRef&) {
+        TAMD_PROF_SCOPE(kDecDecode);
+        got.clear();
+        const int rc = dec->decode(got);
+        if (rc == 0) for (auto* p : got) nums.push_back(p->packet_num);
+        return rc;
+    }
+    int dec_ack(uint8_t* b, uint32_t l, uint32_t* u) { TAMD_PROF_SCOPE(kDecAck); return dec->ack(b, l, u); }
+    void stats(uint64_t e[9], uint64_t d[11]) { enc->stats(e, 9); dec->stats(d, 11); }
+};
+
+struct NoTr {
+    void on_encode(int, const Null::RecRef&) {}
+    void on_decode(int, const std::vector<uint32_t>&, const Null::DecRef&) {}
+    void on_ack(int, const uint8_t*, uint32_t, int, uint32_t) {}
+    void on_event(char, int, uint32_t, uint32_t) {}
+    void on_stats(const uint64_t*, const uint64_t*) {}
+};
+
+int main(int argc, char** argv) {
+    gf_init();
+    wl::Params p;
+    p.loss_thresh = 42949673;
+    p.fec_rate_q16 = 1311;
+    p.ack_every = 64;
+    uint32_t streams = 8, step = 4096;
+    p.n_originals = 4096 * 6;
+    for (int i = 1; i < argc; ++i) {
+        const char* eq = strchr(argv[i], '=');
+        if (!eq) continue;
+        std::string k(argv[i], eq - argv[i]);
+        const unsigned long long v = strtoull(eq + 1, nullptr, 0);
+        if (k == "streams") streams = (uint32_t)v;
+        else if (k == "n") p.n_originals = (uint32_t)v;
+        else if (k == "step") step = (uint32_t)v;
+        else if (k == "loss") p.loss_thresh = (uint32_t)v;
+        else if (k == "fec") p.fec_rate_q16 = (uint32_t)v;
+        else if (k == "ack") p.ack_every = (uint32_t)v;
+    }
+    Context ctx;
+    ctx.rows.init(64ull << 30);
+    std::vector<std::unique_ptr<Null>> be(streams);
+    std::vector<std::unique_ptr<Encoder>> encs(streams);
+    std::vector<std::unique_ptr<Decoder>> decs(streams);
+    std::vector<wl::Params> ps(streams, p);
+    NoTr tr;
+    std::vector<std::unique_ptr<wl::Runner<Null, NoTr>>> run(streams);
+    for (uint32_t s = 0; s < streams; ++s) {
+        ps[s].seed_data = 1000 + s;
+        ps[s].seed_loss = 2000 + s;
+        encs[s].reset(new Encoder(&ctx, 1344));
+        decs[s].reset(new Decoder(&ctx, 1344));
+        be[s].reset(new Null());
+        be[s]->ctx = &ctx;
+        be[s]->enc = encs[s].get();
+        be[s]->dec = decs[s].get();
+        for (uint32_t i = 0; i < p.n_originals; ++i) {
+            be[s]->enc_rows.push_back(ctx.rows.alloc(1302));
+            be[s]->dec_rows.push_back(ctx.rows.alloc(1302));
+        }
+        run[s].reset(new wl::Runner<Null, NoTr>(ps[s], *be[s], tr));
+    }
+    uint64_t instrs = 0, ops = 0;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t done = 0; done < p.n_originals; done += step) {
+        for (uint32_t s = 0; s < streams; ++s) run[s]->advance(step);
+        {
+        TAMD_PROF_SCOPE(kFlushAll);
+        ctx.prepare_flush();
+        instrs += ctx.pb.instrs().size();
+        ops += ctx.pb.ops().size();
+        const uint64_t e = ctx.epoch;
+        ctx.finish_flush();
+        ctx.rows.release_up_to(e);
+        }
+    }
+    const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    const double n = (double)streams * p.n_originals;
+    printf("{\"ns_per_original\": %.1f, \"instrs_per_original\": %.2f, \"ops_per_original\": %.3f, \"seconds\": %.3f}\n",
+           sec * 1e9 / n, instrs / n, ops / n, sec);
+#ifdef TAMD_PROF
+    const double ghz = 1.0 * 0 + 1;
+    for (int i = 0; i < prof::kSlots; ++i)
+        if (prof::calls[i])
+            fprintf(stderr, "%-14s calls/orig %8.4f  cyc/call %10.0f  cyc/orig %8.1f\n", prof::names[i],
+                    prof::calls[i] / n, (double)prof::cycles[i] / prof::calls[i], prof::cycles[i] / n * ghz);
+#endif
+    return 0;
+}

@@ -1,0 +1,55 @@
+"""Multi-rank bench logic on CPU (gloo, world_size 2): stream sharding and the max-over-ranks /
+sum-over-ranks reductions bench.py uses for `value` (the data path itself has no collective)."""
+from __future__ import annotations
+
+import os
+import socket
+import sys
+
+import torch.multiprocessing as mp
+
+from conftest import ROOT
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _rank_main(rank: int, world: int, port: int, q) -> None:
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    sys.path.insert(0, ROOT)
+    import bench
+    d = bench.Dist(world)
+    elapsed = 1.0 + rank            # rank 1 is the slow one
+    payload = 1000 * (rank + 1)
+    d.barrier()
+    out = (rank, bench.stream_base(rank), d.allmax(elapsed), d.allsum(payload))
+    d.barrier()
+    d.close()
+    q.put(out)
+
+
+def test_two_rank_reductions_and_shards():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (r0, base0, max0, sum0), (r1, base1, max1, sum1) = res
+    assert (r0, r1) == (0, 1)
+    assert max0 == max1 == 2.0          # value uses the slowest rank's time
+    assert sum0 == sum1 == 3000         # and every rank's bytes
+    import bench
+    per = bench.STREAMS_PER_GPU
+    assert base0 == 0 and base1 == per  # disjoint stream shards
+    shards = [set(range(b, b + per)) for b in (base0, base1)]
+    assert not (shards[0] & shards[1])

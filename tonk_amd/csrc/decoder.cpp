@@ -1,6 +1,7 @@
 // decoder.cpp -- Siamese decoder control plane.  Each function names the reference routine it
 // restates (SiameseDecoder.cpp line numbers); byte work becomes symbolic terms (engine.h).
 #include "decoder.h"
+#include "prof.h"
 
 #include <string.h>
 
@@ -871,15 +872,33 @@ Result Decoder::decode(std::vector<RecoveredPacket*>& out) {
 
 // Decoder::DecodeCheckedRegion (:729-810)
 Result Decoder::decode_checked_region() {
-    if (!generate_matrix()) { disabled_ = true; return kDisabled; }
-    if (!gaussian_elimination()) {
+    {
+        TAMD_PROF_SCOPE(kGenMatrix);
+        if (!generate_matrix()) { disabled_ = true; return kDisabled; }
+    }
+    bool solved;
+    {
+        TAMD_PROF_SCOPE(kGE);
+        solved = gaussian_elimination();
+    }
+    if (!solved) {
         cr_.solve_failed = true;
         stats_[8]++;
         return kNeedMoreData;
     }
-    if (!eliminate_original_data()) { disabled_ = true; return kDisabled; }
-    if (!multiply_lower_triangle()) { disabled_ = true; return kDisabled; }
-    const Result res = back_substitution();
+    {
+        TAMD_PROF_SCOPE(kElim);
+        if (!eliminate_original_data()) { disabled_ = true; return kDisabled; }
+    }
+    {
+        TAMD_PROF_SCOPE(kLowerTri);
+        if (!multiply_lower_triangle()) { disabled_ = true; return kDisabled; }
+    }
+    Result res;
+    {
+        TAMD_PROF_SCOPE(kBackSub);
+        res = back_substitution();
+    }
     checked_reset();
     return res;
 }

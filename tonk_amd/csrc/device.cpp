@@ -25,7 +25,6 @@ namespace tamd {
         }                                                                                \
     } while (0)
 
-static const uint32_t kSlice = 512;   // bytes per work item (64 lanes x 8 bytes)
 static const uint32_t kMaxGrid = 4096;
 
 Device::~Device() {
@@ -37,7 +36,8 @@ Device::~Device() {
         if (s.dev) hipFree(s.dev);
         if (s.done) hipEventDestroy((hipEvent_t)s.done);
     }
-    for (void* e : ticket_events_) if (e) hipEventDestroy((hipEvent_t)e);
+    for (auto& p : inflight_) hipEventDestroy((hipEvent_t)p.second);
+    for (void* e : free_events_) hipEventDestroy((hipEvent_t)e);
     for (auto& p : timing_events_) { hipEventDestroy((hipEvent_t)p.first); hipEventDestroy((hipEvent_t)p.second); }
     if (up_host_) hipHostFree(up_host_);
     if (up_event_) hipEventDestroy((hipEvent_t)up_event_);
@@ -99,87 +99,131 @@ bool Device::ensure_slot(Slot& s, size_t bytes) {
 }
 
 uint64_t Device::run(Context* const* ctxs, size_t n) {
-    hipStream_t st = (hipStream_t)stream_;
-    // Count everything first.
-    size_t n_instr = 0, n_ops = 0;
-    uint32_t max_level = 0;
+    begin(ctxs, n);
+    for (size_t i = 0; i < n; ++i) fill(i);
+    return launch();
+}
+
+void Device::begin(Context* const* ctxs, size_t n) {
+    Plan& P = plan_;
+    P.ctxs.assign(ctxs, ctxs + n);
+    P.levels = 0;
+    P.n_instr = P.n_ops = P.n_items = 0;
     for (size_t c = 0; c < n; ++c) {
         const ProgramBuilder& pb = ctxs[c]->pb;
-        n_instr += pb.instrs().size();
-        n_ops += pb.ops().size();
+        P.n_instr += pb.instrs().size();
+        P.n_ops += pb.ops().size();
         stats_.acc_bytes += pb.acc_bytes();
         stats_.store_bytes += pb.store_bytes();
-        if (pb.max_level() > max_level) max_level = pb.max_level();
+        if (pb.level_ops().size() > P.levels) P.levels = (uint32_t)pb.level_ops().size();
     }
-    const uint64_t ticket = ++ticket_;
-    if (n_ops == 0) {
-        completed_ = ticket;
-        return ticket;
-    }
-
-    // Items per op and per level.
-    std::vector<uint32_t> level_ops(max_level + 2, 0), level_items(max_level + 2, 0);
-    size_t n_items = 0;
-    for (size_t c = 0; c < n; ++c) {
-        const ProgramBuilder& pb = ctxs[c]->pb;
-        for (size_t i = 0; i < pb.ops().size(); ++i) {
-            const uint32_t l = pb.op_levels()[i];
-            const uint32_t slices = (pb.ops()[i].span + kSlice - 1) / kSlice;
-            level_ops[l]++;
-            level_items[l] += slices ? slices : 1;
-            n_items += slices ? slices : 1;
+    P.empty = P.n_ops == 0;
+    if (P.empty) return;
+    const uint32_t L = P.levels;
+    // Ops grouped by level; inside a level, by context.
+    P.op_start.assign(n * L, 0);
+    P.item_start.assign(n * L, 0);
+    P.level_items.assign(L, 0);
+    P.item_base.assign(L + 1, 0);
+    P.instr_base.assign(n, 0);
+    uint32_t op_at = 0, item_at = 0, instr_at = 0;
+    for (uint32_t l = 0; l < L; ++l) {
+        P.item_base[l] = item_at;
+        for (size_t c = 0; c < n; ++c) {
+            const ProgramBuilder& pb = ctxs[c]->pb;
+            P.op_start[c * L + l] = op_at;
+            P.item_start[c * L + l] = item_at;
+            if (l < pb.level_ops().size()) {
+                op_at += pb.level_ops()[l];
+                item_at += pb.level_items()[l];
+                P.level_items[l] += pb.level_items()[l];
+            }
         }
     }
-    const size_t bytes_instr = n_instr * sizeof(tamd_instr);
-    const size_t bytes_ops = n_ops * sizeof(tamd_op);
-    const size_t bytes_items = n_items * sizeof(uint32_t) * 2;
-    const size_t total = bytes_instr + bytes_ops + bytes_items;
+    P.item_base[L] = item_at;
+    for (size_t c = 0; c < n; ++c) {
+        P.instr_base[c] = instr_at;
+        instr_at += (uint32_t)ctxs[c]->pb.instrs().size();
+    }
+    P.n_items = item_at;
+    P.bytes_instr = P.n_instr * sizeof(tamd_instr);
+    P.bytes_ops = P.n_ops * sizeof(tamd_op);
+    P.total = P.bytes_instr + P.bytes_ops + P.n_items * sizeof(uint32_t) * 2;
 
     Slot& slot = slots_[next_slot_];
     next_slot_ ^= 1;
     if (slot.ticket) {
         HIPCHK(hipEventSynchronize((hipEvent_t)slot.done));
         if (slot.ticket > completed_) completed_ = slot.ticket;
+        slot.ticket = 0;
     }
-    if (!ensure_slot(slot, total)) { error_ = "program staging allocation failed"; return ticket; }
-
-    tamd_instr* hi = (tamd_instr*)slot.host;
-    tamd_op* ho = (tamd_op*)(slot.host + bytes_instr);
-    uint32_t* hitems = (uint32_t*)(slot.host + bytes_instr + bytes_ops);
-
-    // Level-ordered placement.
-    std::vector<uint32_t> op_base(max_level + 2, 0), item_base(max_level + 2, 0);
-    for (uint32_t l = 1; l <= max_level; ++l) {
-        op_base[l + 1] = op_base[l] + level_ops[l];
-        item_base[l + 1] = item_base[l] + level_items[l];
+    P.slot = &slot;
+    if (!ensure_slot(slot, P.total)) {
+        error_ = "program staging allocation failed";
+        P.empty = true;
     }
-    std::vector<uint32_t> op_fill(op_base), item_fill(item_base);
-    uint32_t instr_base = 0;
-    for (size_t c = 0; c < n; ++c) {
-        const ProgramBuilder& pb = ctxs[c]->pb;
-        memcpy(hi + instr_base, pb.instrs().data(), pb.instrs().size() * sizeof(tamd_instr));
-        for (size_t i = 0; i < pb.ops().size(); ++i) {
-            const uint32_t l = pb.op_levels()[i];
-            tamd_op op = pb.ops()[i];
-            op.first += instr_base;
-            const uint32_t oi = op_fill[l]++;
-            ho[oi] = op;
-            uint32_t slices = (op.span + kSlice - 1) / kSlice;
-            if (!slices) slices = 1;
-            for (uint32_t s = 0; s < slices; ++s) {
-                const uint32_t ii = item_fill[l]++;
-                hitems[2 * ii] = oi;
-                hitems[2 * ii + 1] = s;
-            }
+}
+
+void Device::fill(size_t c) {
+    Plan& P = plan_;
+    if (P.empty) return;
+    const ProgramBuilder& pb = P.ctxs[c]->pb;
+    const uint32_t L = P.levels;
+    tamd_instr* hi = (tamd_instr*)P.slot->host;
+    tamd_op* ho = (tamd_op*)(P.slot->host + P.bytes_instr);
+    uint32_t* hitems = (uint32_t*)(P.slot->host + P.bytes_instr + P.bytes_ops);
+    const uint32_t ibase = P.instr_base[c];
+    memcpy(hi + ibase, pb.instrs().data(), pb.instrs().size() * sizeof(tamd_instr));
+    uint32_t op_fill[64], item_fill[64];
+    std::vector<uint32_t> big_op, big_item;
+    uint32_t* of = op_fill;
+    uint32_t* itf = item_fill;
+    if (L > 64) {
+        big_op.resize(L);
+        big_item.resize(L);
+        of = big_op.data();
+        itf = big_item.data();
+    }
+    for (uint32_t l = 0; l < L; ++l) {
+        of[l] = P.op_start[c * L + l];
+        itf[l] = P.item_start[c * L + l];
+    }
+    const std::vector<tamd_op>& ops = pb.ops();
+    const std::vector<uint32_t>& lv = pb.op_levels();
+    for (size_t i = 0; i < ops.size(); ++i) {
+        const uint32_t l = lv[i];
+        tamd_op op = ops[i];
+        op.first += ibase;
+        const uint32_t oi = of[l]++;
+        ho[oi] = op;
+        uint32_t slices = (op.span + TAMD_SLICE_BYTES - 1) / TAMD_SLICE_BYTES;
+        if (!slices) slices = 1;
+        uint32_t ii = itf[l];
+        itf[l] += slices;
+        for (uint32_t s = 0; s < slices; ++s, ++ii) {
+            hitems[2 * ii] = oi;
+            hitems[2 * ii + 1] = s;
         }
-        instr_base += (uint32_t)pb.instrs().size();
     }
-    HIPCHK(hipMemcpyAsync(slot.dev, slot.host, total, hipMemcpyHostToDevice, st));
+}
+
+uint64_t Device::launch() {
+    Plan& P = plan_;
+    const uint64_t ticket = ++ticket_;
+    if (P.empty) {
+        ticket_is_empty_ = true;
+        mark(ticket);  // done once everything enqueued before it is done
+        ticket_is_empty_ = false;
+        return ticket;
+    }
+    hipStream_t st = (hipStream_t)stream_;
+    Slot& slot = *P.slot;
+    HIPCHK(hipMemcpyAsync(slot.dev, slot.host, P.total, hipMemcpyHostToDevice, st));
     const tamd_instr* di = (const tamd_instr*)slot.dev;
-    const tamd_op* dops = (const tamd_op*)(slot.dev + bytes_instr);
-    const uint2* ditems = (const uint2*)(slot.dev + bytes_instr + bytes_ops);
-    for (uint32_t l = 1; l <= max_level; ++l) {
-        const uint32_t cnt = level_items[l];
+    const tamd_op* dops = (const tamd_op*)(slot.dev + P.bytes_instr);
+    const uint2* ditems = (const uint2*)(slot.dev + P.bytes_instr + P.bytes_ops);
+    for (uint32_t l = 1; l < P.levels; ++l) {
+        const uint32_t cnt = P.level_items[l];
         if (!cnt) continue;
         uint32_t grid = (cnt + 3) / 4;
         if (grid > kMaxGrid) grid = kMaxGrid;
@@ -189,7 +233,7 @@ uint64_t Device::run(Context* const* ctxs, size_t n) {
             hipEventCreate(&e1);
             hipEventRecord(e0, st);
         }
-        hipLaunchKernelGGL(tamd_exec, dim3(grid), dim3(256), 0, st, dops, di, ditems + item_base[l], cnt,
+        hipLaunchKernelGGL(tamd_exec, dim3(grid), dim3(256), 0, st, dops, di, ditems + P.item_base[l], cnt,
                            arena_, d_gf_);
         if (timing_) {
             hipEventRecord(e1, st);
@@ -200,43 +244,56 @@ uint64_t Device::run(Context* const* ctxs, size_t n) {
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord((hipEvent_t)slot.done, st));
     slot.ticket = ticket;
+    mark(ticket);
     stats_.programs++;
-    stats_.ops += n_ops;
-    stats_.items += n_items;
-    stats_.instrs += n_instr;
-    stats_.upload_bytes += total;
+    stats_.ops += P.n_ops;
+    stats_.items += P.n_items;
+    stats_.instrs += P.n_instr;
+    stats_.upload_bytes += P.total;
     return ticket;
 }
 
-bool Device::completed(uint64_t ticket) {
-    if (ticket <= completed_) return true;
-    for (Slot& s : slots_) {
-        if (s.ticket == ticket) {
-            if (hipEventQuery((hipEvent_t)s.done) == hipSuccess) {
-                completed_ = ticket;
-                return true;
-            }
-            return false;
-        }
+void Device::mark(uint64_t ticket) {
+    if (inflight_.empty() && ticket_is_empty_) {
+        completed_ = ticket;
+        return;
     }
-    // Older than both slots: finished when the slots' older ticket is done.
+    void* e = nullptr;
+    if (!free_events_.empty()) {
+        e = free_events_.back();
+        free_events_.pop_back();
+    } else {
+        hipEvent_t he;
+        HIPCHK(hipEventCreateWithFlags(&he, hipEventDisableTiming));
+        e = he;
+    }
+    HIPCHK(hipEventRecord((hipEvent_t)e, (hipStream_t)stream_));
+    inflight_.push_back(std::make_pair(ticket, e));
+}
+
+bool Device::completed(uint64_t ticket) {
+    while (!inflight_.empty() && ticket > completed_) {
+        if (hipEventQuery((hipEvent_t)inflight_.front().second) != hipSuccess) break;
+        if (inflight_.front().first > completed_) completed_ = inflight_.front().first;
+        free_events_.push_back(inflight_.front().second);
+        inflight_.pop_front();
+    }
     return ticket <= completed_;
 }
 
 void Device::wait(uint64_t ticket) {
-    if (ticket <= completed_) return;
-    for (Slot& s : slots_) {
-        if (s.ticket == ticket) {
-            HIPCHK(hipEventSynchronize((hipEvent_t)s.done));
-            completed_ = ticket;
-            return;
-        }
+    while (!inflight_.empty() && ticket > completed_) {
+        HIPCHK(hipEventSynchronize((hipEvent_t)inflight_.front().second));
+        if (inflight_.front().first > completed_) completed_ = inflight_.front().first;
+        free_events_.push_back(inflight_.front().second);
+        inflight_.pop_front();
     }
-    synchronize();
 }
 
 void Device::synchronize() {
     HIPCHK(hipStreamSynchronize((hipStream_t)stream_));
+    for (auto& p : inflight_) free_events_.push_back(p.second);
+    inflight_.clear();
     completed_ = ticket_;
     up_used_ = 0;
 }
@@ -250,9 +307,7 @@ void Device::upload(uint64_t off, const void* src, size_t n) {
         return;
     }
     if (up_used_ + n > up_cap_) {
-        HIPCHK(hipStreamSynchronize(st));
-        completed_ = ticket_;
-        up_used_ = 0;
+        synchronize();
     }
     memcpy(up_host_ + up_used_, src, n);
     HIPCHK(hipMemcpyAsync(arena_ + off, up_host_ + up_used_, n, hipMemcpyHostToDevice, st));
@@ -263,9 +318,7 @@ void Device::download(void* dst, uint64_t off, size_t n) {
     if (n == 0) return;
     hipStream_t st = (hipStream_t)stream_;
     HIPCHK(hipMemcpyAsync(dst, arena_ + off, n, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    completed_ = ticket_;
-    up_used_ = 0;
+    synchronize();
 }
 
 void Device::generate_rows(const std::vector<GenDesc>& d, uint32_t row_cap) {

@@ -5,6 +5,7 @@
 #include "engine.h"
 
 #include <stdint.h>
+#include <deque>
 #include <vector>
 #include <string>
 
@@ -33,6 +34,13 @@ public:
     // completion ticket (monotonic); call completed() / wait() with it.
     uint64_t run(Context* const* ctxs, size_t n);
     uint64_t run(Context* ctx) { return run(&ctx, 1); }
+    // The same in three phases so host threads can fill their part of the merged program in
+    // parallel: begin() lays the program out (ops grouped by level, then by context) and waits
+    // for the staging slot; fill(i) copies context i (thread safe for distinct i); launch()
+    // uploads the program and enqueues one tamd_exec per level.  Returns the ticket.
+    void begin(Context* const* ctxs, size_t n);
+    void fill(size_t i);
+    uint64_t launch();
     bool completed(uint64_t ticket);
     void wait(uint64_t ticket);
     void synchronize();
@@ -70,9 +78,23 @@ private:
         uint64_t ticket = 0;
     };
     Slot slots_[2];
+    // layout of the program being assembled (begin/fill/launch)
+    struct Plan {
+        std::vector<Context*> ctxs;
+        std::vector<uint32_t> instr_base;          // per context
+        std::vector<uint32_t> op_start, item_start; // [context * levels + level]
+        std::vector<uint32_t> level_items, item_base;
+        uint32_t levels = 0;
+        size_t n_instr = 0, n_ops = 0, n_items = 0, bytes_instr = 0, bytes_ops = 0, total = 0;
+        Slot* slot = nullptr;
+        bool empty = true;
+    } plan_;
     int next_slot_ = 0;
     uint64_t ticket_ = 0, completed_ = 0;
-    std::vector<void*> ticket_events_;
+    std::deque<std::pair<uint64_t, void*>> inflight_;  // (ticket, hipEvent_t) in stream order
+    std::vector<void*> free_events_;
+    bool ticket_is_empty_ = false;
+    void mark(uint64_t ticket);
     // upload staging
     uint8_t* up_host_ = nullptr;
     size_t up_cap_ = 0, up_used_ = 0;

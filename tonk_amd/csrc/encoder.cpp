@@ -2,14 +2,17 @@
 // restates (SiameseEncoder.cpp line numbers); byte work becomes symbolic terms (engine.h).
 #include "encoder.h"
 
-#include <chrono>
 #include <string.h>
+#include <time.h>
 
 namespace tamd {
 
+// GetTimeMsec (SiameseTools.cpp).  Millisecond resolution is all the RTO logic uses, so the
+// coarse monotonic clock (a few ns, no TSC read) is enough; it is read once per original.
 uint64_t time_msec() {
-    return (uint64_t)std::chrono::duration_cast<std::chrono::milliseconds>(
-               std::chrono::steady_clock::now().time_since_epoch()).count();
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC_COARSE, &ts);
+    return (uint64_t)ts.tv_sec * 1000u + (uint64_t)ts.tv_nsec / 1000000u;
 }
 
 Encoder::Encoder(Context* ctx, uint32_t row_bytes, HostRelease release, void* user)

@@ -1,5 +1,6 @@
 // engine.cpp -- see engine.h.
 #include "engine.h"
+#include "prof.h"
 
 #include <string.h>
 
@@ -98,6 +99,8 @@ void ProgramBuilder::clear() {
     instrs_.clear();
     levels_.clear();
     written_.clear();
+    level_ops_.clear();
+    level_items_.clear();
     max_level_ = 0;
     acc_bytes_ = store_bytes_ = 0;
 }
@@ -159,6 +162,13 @@ uint32_t ProgramBuilder::end_op(uint32_t min_level) {
     op.tag = level;
     ops_.push_back(op);
     levels_.push_back(level);
+    if (level_ops_.size() <= level) {
+        level_ops_.resize(level + 1, 0);
+        level_items_.resize(level + 1, 0);
+    }
+    const uint32_t slices = (op.span + TAMD_SLICE_BYTES - 1) / TAMD_SLICE_BYTES;
+    level_ops_[level]++;
+    level_items_[level] += slices ? slices : 1;
     for (size_t i = cur_written_begin_; i < written_.size(); ++i) rows_->set_level(written_[i], level);
     if (level > max_level_) max_level_ = level;
     return level;
@@ -182,6 +192,7 @@ uint32_t ProgramBuilder::combine(RowId dst, const Term* terms, size_t n, uint32_
 // ---------------------------------------------------------------------------------------------
 void sym_merge(Sym& s) {
     if (s.size() < 2) return;
+    TAMD_PROF_SCOPE(kSymMerge);
     std::sort(s.begin(), s.end(), [](const Term& a, const Term& b) {
         return a.row != b.row ? a.row < b.row : a.len < b.len;
     });
@@ -299,6 +310,7 @@ void Chain::emit_scan(RowTable& rows, ProgramBuilder& pb, RowId base, uint32_t c
 
 void Chain::flush(RowTable& rows, ProgramBuilder& pb, const ExpansionTable& ex, uint32_t row_bytes) {
     (void)row_bytes;
+    TAMD_PROF_SCOPE(kChainFlush);
     for (Closed& c : closed_) {
         emit_scan(rows, pb, c.base, c.content, c.terms, c.snaps, kNoRow);
         rows.free_deferred(c.base);

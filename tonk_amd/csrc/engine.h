@@ -114,6 +114,9 @@ public:
     const std::vector<tamd_instr>& instrs() const { return instrs_; }
     const std::vector<uint32_t>& op_levels() const { return levels_; }
     const std::vector<RowId>& written_rows() const { return written_; }
+    // Per level (index = level): op count and work-item count (TAMD_SLICE_BYTES slices).
+    const std::vector<uint32_t>& level_ops() const { return level_ops_; }
+    const std::vector<uint32_t>& level_items() const { return level_items_; }
 
     uint64_t acc_bytes() const { return acc_bytes_; }       // sum of ACC lengths (op-trace)
     uint64_t store_bytes() const { return store_bytes_; }
@@ -124,6 +127,7 @@ private:
     std::vector<tamd_instr> instrs_;
     std::vector<uint32_t> levels_;
     std::vector<RowId> written_;
+    std::vector<uint32_t> level_ops_, level_items_;
     uint32_t max_level_ = 0;
     // op under construction
     uint32_t cur_first_ = 0, cur_span_ = 0, cur_level_in_ = 0;

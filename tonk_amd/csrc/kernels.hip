@@ -14,7 +14,8 @@
 
 #define TAMD_WAVES_PER_WG 4
 #define TAMD_LANE_BYTES 8
-#define TAMD_SLICE_BYTES (64 * TAMD_LANE_BYTES)
+#define TAMD_BATCH 8  // instructions whose loads are issued together (memory-level parallelism)
+static_assert(TAMD_SLICE_BYTES == 64 * TAMD_LANE_BYTES, "one wave covers one slice");
 
 typedef unsigned long long u64;
 
@@ -33,6 +34,36 @@ __device__ __forceinline__ u64 byte_mask(uint32_t nbytes) {  // low `nbytes` byt
 
 __device__ __forceinline__ uint32_t uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 
+__device__ __forceinline__ u64 gf_mul8(u64 v, uint32_t coef, const uint32_t* __restrict__ lds_perm) {
+    const uint32_t* t = &lds_perm[coef * 8u];
+    const uint32_t t0lo = t[0], t0hi = t[1], t1lo = t[2], t1hi = t[3], t2lo = t[4], t2hi = t[5];
+    const uint32_t lo = gf_mul4((uint32_t)v, t0lo, t0hi, t1lo, t1hi, t2lo, t2hi);
+    const uint32_t hi = gf_mul4((uint32_t)(v >> 32), t0lo, t0hi, t1lo, t1hi, t2lo, t2hi);
+    return ((u64)hi << 32) | lo;
+}
+
+__device__ __forceinline__ void store_slice(uint8_t* __restrict__ arena, const tamd_instr& in, const tamd_instr& f,
+                                            uint32_t o, u64 acc) {
+    const uint32_t len = in.len, cap = in.cap;
+    if (o >= cap) return;
+    const u64 footer = ((u64)f.len << 32) | f.row;
+    u64 keep;
+    if (o + 8u <= len) keep = ~0ull;
+    else if (o >= len) keep = 0;
+    else keep = byte_mask(len - o);
+    u64 fpart = 0;
+    if (o >= len) {
+        const uint32_t sh = o - len;
+        if (sh < 8u) fpart = footer >> (8u * sh);
+    } else {
+        const uint32_t sh = len - o;
+        if (sh < 8u) fpart = footer << (8u * sh);
+    }
+    *(u64*)(arena + (size_t)in.row * TAMD_ROW_UNIT + o) = (acc & keep) | fpart;
+}
+
+// Ops of one level never read a row written by an op of the same level, so every ACC load of
+// a batch can be issued before the batch's STOREs: TAMD_BATCH loads in flight per wave.
 extern "C" __global__ void __launch_bounds__(256)
 tamd_exec(const tamd_op* __restrict__ ops, const tamd_instr* __restrict__ instrs,
           const uint2* __restrict__ items, uint32_t n_items, uint8_t* __restrict__ arena,
@@ -50,48 +81,39 @@ tamd_exec(const tamd_op* __restrict__ ops, const tamd_instr* __restrict__ instrs
         const tamd_op op = ops[uniform(item.x)];
         const uint32_t o = uniform(item.y) * TAMD_SLICE_BYTES + lane * TAMD_LANE_BYTES;
         u64 acc = 0;
-        const uint32_t end = op.first + op.count;
-        for (uint32_t k = op.first; k < end; ++k) {
-            const tamd_instr in = instrs[k];
-            const uint32_t kind = in.w0 & 0xffu;
-            if (kind == TAMD_I_ACC) {
-                const uint32_t len = in.len;
-                if (o < len) {
-                    const u64* src = (const u64*)(arena + (size_t)in.row * TAMD_ROW_UNIT + o);
-                    u64 v = *src;
-                    if (o + 8u > len) v &= byte_mask(len - o);
-                    const uint32_t coef = (in.w0 >> 8) & 0xffu;
-                    if (coef != 1u) {
-                        const uint32_t* t = &lds_perm[coef * 8u];
-                        const uint32_t t0lo = t[0], t0hi = t[1], t1lo = t[2], t1hi = t[3], t2lo = t[4], t2hi = t[5];
-                        const uint32_t lo = gf_mul4((uint32_t)v, t0lo, t0hi, t1lo, t1hi, t2lo, t2hi);
-                        const uint32_t hi = gf_mul4((uint32_t)(v >> 32), t0lo, t0hi, t1lo, t1hi, t2lo, t2hi);
-                        v = ((u64)hi << 32) | lo;
-                    }
-                    acc ^= v;
+        const uint32_t first = uniform(op.first), end = uniform(op.first + op.count);
+        for (uint32_t k = first; k < end; k += TAMD_BATCH) {
+            tamd_instr in[TAMD_BATCH];
+            u64 v[TAMD_BATCH];
+#pragma unroll
+            for (uint32_t j = 0; j < TAMD_BATCH; ++j) {
+                v[j] = 0;
+                in[j].w0 = 0;
+                if (k + j < end) {
+                    in[j] = instrs[k + j];
+                    if ((in[j].w0 & 0xffu) == TAMD_I_ACC && o < in[j].len)
+                        v[j] = *(const u64*)(arena + (size_t)in[j].row * TAMD_ROW_UNIT + o);
                 }
-            } else if (kind == TAMD_I_STORE) {
-                const tamd_instr f = instrs[k + 1];
-                ++k;
-                const uint32_t len = in.len, cap = in.cap;
-                if (o < cap) {
-                    const u64 footer = ((u64)f.len << 32) | f.row;
-                    u64 keep;
-                    if (o + 8u <= len) keep = ~0ull;
-                    else if (o >= len) keep = 0;
-                    else keep = byte_mask(len - o);
-                    u64 fpart = 0;
-                    if (o >= len) {
-                        const uint32_t sh = o - len;
-                        if (sh < 8u) fpart = footer >> (8u * sh);
-                    } else {
-                        const uint32_t sh = len - o;
-                        if (sh < 8u) fpart = footer << (8u * sh);
+            }
+#pragma unroll
+            for (uint32_t j = 0; j < TAMD_BATCH; ++j) {
+                const uint32_t kind = in[j].w0 & 0xffu;
+                if (kind == TAMD_I_ACC) {
+                    const uint32_t len = in[j].len;
+                    if (o < len) {
+                        u64 x = v[j];
+                        if (o + 8u > len) x &= byte_mask(len - o);
+                        const uint32_t coef = (in[j].w0 >> 8) & 0xffu;
+                        if (coef != 1u) x = gf_mul8(x, coef, lds_perm);
+                        acc ^= x;
                     }
-                    *(u64*)(arena + (size_t)in.row * TAMD_ROW_UNIT + o) = (acc & keep) | fpart;
+                } else if (kind == TAMD_I_STORE) {
+                    // the FOOTER word follows the STORE (possibly in the next batch)
+                    const tamd_instr f = (j + 1 < TAMD_BATCH) ? in[j + 1 < TAMD_BATCH ? j + 1 : j] : instrs[k + j + 1];
+                    store_slice(arena, in[j], f, o, acc);
+                } else if (kind == TAMD_I_CLEAR) {
+                    acc = 0;
                 }
-            } else if (kind == TAMD_I_CLEAR) {
-                acc = 0;
             }
         }
     }

@@ -1,0 +1,29 @@
+// prof.h -- optional cycle accounting for control-plane tuning (compile with -DTAMD_PROF).
+// Zero cost otherwise.  Used by tests/native/cp_bench.
+#pragma once
+
+#ifdef TAMD_PROF
+#include <stdint.h>
+#include <x86intrin.h>
+
+namespace tamd {
+namespace prof {
+enum Slot {
+    kEncAdd, kEncEncode, kEncAck, kDecAddOrig, kDecAddRec, kDecDecode, kDecAck, kDecIsReady,
+    kGenMatrix, kGE, kElim, kLowerTri, kBackSub, kChainFlush, kSymMerge, kFlushAll, kSlots
+};
+extern thread_local uint64_t cycles[kSlots];
+extern thread_local uint64_t calls[kSlots];
+extern const char* const names[kSlots];
+struct Scope {
+    Slot s;
+    uint64_t t0;
+    explicit Scope(Slot slot) : s(slot), t0(__rdtsc()) {}
+    ~Scope() { cycles[s] += __rdtsc() - t0; calls[s]++; }
+};
+}  // namespace prof
+}  // namespace tamd
+#define TAMD_PROF_SCOPE(slot) ::tamd::prof::Scope tamd_prof_scope_##__LINE__(::tamd::prof::slot)
+#else
+#define TAMD_PROF_SCOPE(slot) do {} while (0)
+#endif

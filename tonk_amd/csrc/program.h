@@ -18,6 +18,7 @@
 #include <stdint.h>
 
 #define TAMD_ROW_UNIT 64u
+#define TAMD_SLICE_BYTES 512u  /* bytes of an op one work item (one wave) covers */
 
 enum tamd_instr_kind {
     TAMD_I_ACC    = 1,

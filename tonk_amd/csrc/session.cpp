@@ -146,6 +146,7 @@ struct Stream {
 };
 
 struct Worker {
+    size_t index = 0;
     Context ctx;
     std::vector<Stream*> streams;
 };
@@ -156,7 +157,7 @@ struct Session {
     std::vector<std::unique_ptr<Worker>> workers;
     std::vector<std::unique_ptr<Stream>> streams;
     std::vector<std::pair<uint64_t, uint64_t>> epoch_ticket;  // (epoch, ticket) awaiting release
-    uint64_t last_ticket = 0;
+    uint64_t last_ticket = 0, released_epoch = 0;
     uint32_t row_cap = 0;
     bool finished = false;
     std::string error;
@@ -221,27 +222,50 @@ struct Session {
         cv_done.wait(lk, [&] { return job_left == 0; });
     }
 
-    void release_completed() {
+    // Highest epoch whose program has completed on the device (its freed rows are reusable).
+    uint64_t completed_epoch() {
         size_t k = 0;
-        for (size_t i = 0; i < epoch_ticket.size(); ++i) {
-            if (dev.completed(epoch_ticket[i].second)) {
-                for (auto& w : workers) w->ctx.rows.release_up_to(epoch_ticket[i].first);
-            } else {
-                epoch_ticket[k++] = epoch_ticket[i];
-            }
+        while (k < epoch_ticket.size() && dev.completed(epoch_ticket[k].second)) {
+            released_epoch = epoch_ticket[k].first;
+            ++k;
         }
-        epoch_ticket.resize(k);
+        epoch_ticket.erase(epoch_ticket.begin(), epoch_ticket.begin() + k);
+        return released_epoch;
     }
 
-    // Merge every worker's pending program, enqueue it, close the epoch.
-    void flush_all() {
+    // Advance every worker's streams by `originals` (or finish them), then merge the workers'
+    // programs into one and enqueue it.  Every per-worker phase runs on the worker threads:
+    //   1. release rows of completed programs, run the control planes, emit the running-sum scans
+    //   2. (main) lay out the merged program, wait for a free staging slot
+    //   3. copy each worker's ops into the pinned staging buffer, close the worker's epoch
+    //   4. (main) upload the program and launch it level by level
+    void step(uint32_t originals, bool finish) {
+        const uint64_t rel = completed_epoch();
+        run_all([originals, finish, rel](Worker& w) {
+            w.ctx.rows.release_up_to(rel);
+            for (Stream* st : w.streams) {
+                if (finish) st->runner->finish();
+                else st->runner->advance(originals);
+            }
+            w.ctx.prepare_flush();
+        });
         std::vector<Context*> ctxs;
         for (auto& w : workers) ctxs.push_back(&w->ctx);
-        last_ticket = dev.run(ctxs.data(), ctxs.size());
+        dev.begin(ctxs.data(), ctxs.size());
         const uint64_t epoch = workers.empty() ? 0 : workers[0]->ctx.epoch;
-        for (auto& w : workers) w->ctx.finish_flush();
+        Device* d = &dev;
+        run_all([d](Worker& w) {
+            d->fill(w.index);
+            w.ctx.finish_flush();
+        });
+        last_ticket = dev.launch();
         epoch_ticket.push_back(std::make_pair(epoch, last_ticket));
         if (prm.record) resolve_transcripts();
+    }
+
+    void release_all() {
+        const uint64_t rel = completed_epoch();
+        run_all([rel](Worker& w) { w.ctx.rows.release_up_to(rel); });
     }
 
     void resolve_transcripts() {
@@ -297,6 +321,7 @@ void* tamd_session_create(const tamd_session_params* p, char* err, size_t err_le
     const uint64_t range = (s->dev.arena_bytes() / nthreads) & ~(uint64_t)(TAMD_ROW_UNIT - 1);
     for (uint32_t t = 0; t < nthreads; ++t) {
         std::unique_ptr<Worker> w(new Worker());
+        w->index = t;
         w->ctx.rows.init(range, (range / TAMD_ROW_UNIT) * t);
         s->workers.push_back(std::move(w));
     }
@@ -367,32 +392,22 @@ int tamd_session_generate(void* sp) {
 
 int tamd_session_step(void* sp, uint32_t originals) {
     Session* s = (Session*)sp;
-    s->release_completed();
-    s->run_all([originals](Worker& w) {
-        for (Stream* st : w.streams) st->runner->advance(originals);
-        w.ctx.prepare_flush();
-    });
-    s->flush_all();
+    s->step(originals, false);
     for (auto& w : s->workers) if (w->ctx.oom) { s->error = "arena exhausted"; return -1; }
-    return s->error.empty() ? 0 : -1;
+    return s->error.empty() && s->dev.error().empty() ? 0 : -1;
 }
 
 int tamd_session_wait(void* sp) {
     Session* s = (Session*)sp;
     s->dev.synchronize();
-    s->release_completed();
+    s->release_all();
     return s->dev.error().empty() && s->error.empty() ? 0 : -1;
 }
 
 int tamd_session_finish(void* sp) {
     Session* s = (Session*)sp;
     if (!s->finished) {
-        s->release_completed();
-        s->run_all([](Worker& w) {
-            for (Stream* st : w.streams) st->runner->finish();
-            w.ctx.prepare_flush();
-        });
-        s->flush_all();
+        s->step(0, true);
         s->finished = true;
     }
     return tamd_session_wait(sp);
