@@ -74,7 +74,7 @@ def cpu_baseline(threads: int, target_s: float = 10.0) -> dict | None:
     if probe is None:
         return None
     per_rep = max(probe["seconds"] / 2, 1e-3)
-    reps = int(min(400, max(2, round(target_s / per_rep))))
+    reps = int(min(4000, max(2, round(target_s / per_rep))))
     j = run(reps)
     if j is None:
         return None
