@@ -462,8 +462,13 @@ int oracle_recovery_row(const oracle_recovery_meta* m, oracle_get_row_fn get_row
    CPU interpreter for the device program (tonk_amd/csrc/program.h).  Word layouts are
    restated here (not included) so this file stays a stand-alone checker.
    ------------------------------------------------------------------------------------------ */
-enum { I_ACC = 1, I_STORE = 2, I_FOOTER = 3, I_CLEAR = 4 };
+enum { I_ACC = 1, I_STORE = 2, I_FOOTER = 3, I_CLEAR = 4, I_ACC3 = 5 };
 
+/* Each op owns three accumulators of `span` bytes (program.h):
+     ACC   w0 = 1 | coef << 8 | a << 16       acc_a ^= coef * row[0:len]
+     ACC3  w0 = 5 | c1 << 8 | c2 << 16        acc_0 ^= row, acc_1 ^= c1 * row, acc_2 ^= c2 * row
+     STORE w0 = 2 | flen << 8 | a << 16       row = acc_a[0:len] || footer || zeros to cap
+     CLEAR                                    all accumulators = 0 */
 int oracle_run_program(uint8_t* arena, size_t arena_bytes,
                        const uint32_t* ops, unsigned n_ops,
                        const uint32_t* instrs, unsigned n_instrs)
@@ -476,30 +481,41 @@ int oracle_run_program(uint8_t* arena, size_t arena_bytes,
         if (span > acc_cap) {
             free(acc);
             acc_cap = span;
-            acc = (uint8_t*)malloc(acc_cap);
+            acc = (uint8_t*)malloc(3 * acc_cap);
             if (!acc) return -2;
         }
-        if (span) memset(acc, 0, span);
+        if (span) memset(acc, 0, 3 * (size_t)span);
         for (uint32_t k = 0; k < count; ++k) {
             const uint32_t* w = instrs + 4 * (size_t)(first + k);
             const uint32_t kind = w[0] & 0xff;
             if (kind == I_CLEAR) {
-                if (span) memset(acc, 0, span);
+                if (span) memset(acc, 0, 3 * (size_t)span);
             } else if (kind == I_ACC) {
                 const uint8_t coef = (uint8_t)(w[0] >> 8);
+                const uint32_t a = (w[0] >> 16) & 0xff;
                 const size_t base = (size_t)w[1] * 64u;
                 const uint32_t len = w[2];
-                if (len > span || base + len > arena_bytes) { free(acc); return -3; }
-                if (coef == 1) oracle_add_mem(acc, arena + base, len);
-                else           oracle_muladd_mem(acc, coef, arena + base, len);
+                if (a > 2 || len > span || base + len > arena_bytes) { free(acc); return -3; }
+                uint8_t* dst = acc + (size_t)a * span;
+                if (coef == 1) oracle_add_mem(dst, arena + base, len);
+                else           oracle_muladd_mem(dst, coef, arena + base, len);
+            } else if (kind == I_ACC3) {
+                const uint8_t c1 = (uint8_t)(w[0] >> 8), c2 = (uint8_t)(w[0] >> 16);
+                const size_t base = (size_t)w[1] * 64u;
+                const uint32_t len = w[2];
+                if (len > span || base + len > arena_bytes) { free(acc); return -8; }
+                oracle_add_mem(acc, arena + base, len);
+                oracle_muladd_mem(acc + span, c1, arena + base, len);
+                oracle_muladd_mem(acc + 2 * (size_t)span, c2, arena + base, len);
             } else if (kind == I_STORE) {
                 if (k + 1 >= count) { free(acc); return -4; }
                 const uint32_t* f = w + 4;
                 if ((f[0] & 0xff) != I_FOOTER) { free(acc); return -5; }
                 const uint32_t flen = (w[0] >> 8) & 0xff;
+                const uint32_t a = (w[0] >> 16) & 0xff;
                 const size_t base = (size_t)w[1] * 64u;
                 const uint32_t len = w[2], cap = w[3];
-                if (len > span || flen > 8 || len + flen > cap || base + cap > arena_bytes) {
+                if (a > 2 || len > span || flen > 8 || len + flen > cap || base + cap > arena_bytes) {
                     free(acc); return -6;
                 }
                 uint8_t footer[8];
@@ -507,7 +523,7 @@ int oracle_run_program(uint8_t* arena, size_t arena_bytes,
                     footer[b]     = (uint8_t)(f[1] >> (8 * b));
                     footer[4 + b] = (uint8_t)(f[2] >> (8 * b));
                 }
-                memcpy(arena + base, acc, len);
+                memcpy(arena + base, acc + (size_t)a * span, len);
                 memcpy(arena + base + len, footer, flen);
                 memset(arena + base + len + flen, 0, cap - len - flen);
                 ++k; /* consumed the FOOTER word */

@@ -22,7 +22,7 @@ thread_local uint64_t cycles[kSlots];
 thread_local uint64_t calls[kSlots];
 const char* const names[kSlots] = {"enc_add", "enc_encode", "enc_ack", "dec_add_orig", "dec_add_rec", "dec_decode",
     "dec_ack", "dec_is_ready", "gen_matrix", "ge", "elim", "lower_tri", "back_sub", "chain_flush", "sym_merge",
-    "flush_all"};
+    "prepare_flush", "finish_flush", "release"};
 } }
 #endif
 
@@ -37,7 +37,7 @@ struct Null {
     int enc_add(uint32_t index, uint32_t len, uint32_t* col) {
         const uint32_t hb = length_header_bytes(len);
         TAMD_PROF_SCOPE(kEncAdd);
-        return enc->add(enc_rows[index], hb + len, hb, len, nullptr, col);
+        return enc->add(enc_rows[index], hb + len, hb, len, nullptr, col, true);
     }
     int enc_encode(RecRef& r) { TAMD_PROF_SCOPE(kEncEncode); return enc->encode(r.out); }
     int enc_ack(const uint8_t* b, uint32_t n, uint32_t* next) { TAMD_PROF_SCOPE(kEncAck); return enc->acknowledge(b, n, next); }
@@ -45,8 +45,7 @@ struct Null {
         const uint32_t hb = length_header_bytes(len);
         TAMD_PROF_SCOPE(kDecAddOrig);
         bool took = false;
-        const int r = dec->add_original(col, dec_rows[index], hb + len, hb, len, nullptr, &took);
-        if (!took) ctx->rows.free_deferred(dec_rows[index]);
+        const int r = dec->add_original(col, dec_rows[index], hb + len, hb, len, nullptr, &took, true);
         return r;
     }
     void recovery_lost(const RecRef& r) { ctx->rows.free_deferred(r.out.row); }
@@ -128,14 +127,20 @@ int main(int argc, char** argv) {
     const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t done = 0; done < p.n_originals; done += step) {
         for (uint32_t s = 0; s < streams; ++s) run[s]->advance(step);
+        const uint64_t e = ctx.epoch;
         {
-        TAMD_PROF_SCOPE(kFlushAll);
-        ctx.prepare_flush();
+            TAMD_PROF_SCOPE(kFlushAll);
+            ctx.prepare_flush();
+        }
         instrs += ctx.pb.instrs().size();
         ops += ctx.pb.ops().size();
-        const uint64_t e = ctx.epoch;
-        ctx.finish_flush();
-        ctx.rows.release_up_to(e);
+        {
+            TAMD_PROF_SCOPE(kFinish);
+            ctx.finish_flush();
+        }
+        {
+            TAMD_PROF_SCOPE(kRelease);
+            ctx.rows.release_up_to(e);
         }
     }
     const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();

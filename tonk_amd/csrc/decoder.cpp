@@ -43,18 +43,16 @@ Decoder::~Decoder() {
     for (Recovery* g : graveyard_) delete g;
     graveyard_.clear();
     pre_flush();  // snapshots already referenced by the pending program must still be written
-    for (unsigned l = 0; l < kLanes; ++l)
-        for (unsigned s = 0; s < kSums; ++s) lanes_[l][s].chain.release(ctx_->rows);
+    for (unsigned l = 0; l < kLanes; ++l) lanes_[l].sums.release(ctx_->rows);
     ctx_->detach(this);
 }
 
 void Decoder::pre_flush() {
-    for (unsigned l = 0; l < kLanes; ++l)
-        for (unsigned s = 0; s < kSums; ++s) lanes_[l][s].chain.flush(ctx_->rows, ctx_->pb, ctx_->ex, row_bytes_);
+    for (unsigned l = 0; l < kLanes; ++l) lanes_[l].sums.flush(ctx_->rows, ctx_->pb, ctx_->ex);
 }
 
 void Decoder::drop_original(StoredOriginal& o) {
-    if (o.row != kNoRow) ctx_->rows.free_deferred(o.row);
+    if (o.owned) ctx_->rows.free_deferred(o.row);
     if (o.host && release_) release_(o.host, user_);
     o = StoredOriginal();
 }
@@ -160,7 +158,7 @@ bool Decoder::grow_window(uint32_t end) {
 
 // DecoderPacketWindow::AddOriginal (:1467-1536)
 Result Decoder::add_original(uint32_t packet_num, RowId row, uint32_t framed_bytes, uint32_t header_bytes,
-                             uint32_t payload_bytes, void* host, bool* took) {
+                             uint32_t payload_bytes, void* host, bool* took, bool borrowed) {
     *took = false;
     if (disabled_) return kDisabled;
     const uint32_t e = to_element(packet_num);
@@ -180,9 +178,10 @@ Result Decoder::add_original(uint32_t packet_num, RowId row, uint32_t framed_byt
     o.row = row;
     o.bytes = framed_bytes;
     o.column = packet_num;
-    o.header_bytes = header_bytes;
+    o.header_bytes = (uint8_t)header_bytes;
+    o.owned = borrowed ? 0 : 1;
     o.host = host;
-    *took = true;
+    *took = !borrowed;
     s->got_count++;
     s->got |= 1ull << bit;
 
@@ -204,19 +203,12 @@ bool Decoder::plug_sum_holes(uint32_t element_start) {
         if (invalid_element(e)) continue;
         const uint32_t lane = column % kLanes;
         const uint32_t lane_start = next_lane_element(element_start, lane);
-        for (unsigned s = 0; s < kSums; ++s) {
-            LaneSum& sum = lanes_[lane][s];
-            if (e >= lane_start && e < sum.element_end) {
-                const StoredOriginal& o = elem(e);
-                if (o.bytes <= 0) return false;
-                if (o.bytes > sum.chain.bytes) sum.chain.grow(o.bytes);
-                uint8_t cx = 1;
-                if (s > 0) {
-                    cx = column_value(column);
-                    if (s == 2) cx = gf_sqr(cx);
-                }
-                sum.chain.accumulate(ctx_->rows, o.row, o.bytes, cx);
-            }
+        LaneSum& sum = lanes_[lane];
+        if (e >= lane_start && e < sum.element_end) {
+            const StoredOriginal& o = elem(e);
+            if (o.bytes <= 0) return false;
+            sum.sums.grow(o.bytes);
+            sum.sums.accumulate(ctx_->rows, o.row, o.bytes, column_value(column));
         }
     }
     recovered_columns_.clear();
@@ -227,12 +219,10 @@ bool Decoder::plug_sum_holes(uint32_t element_start) {
 void Decoder::reset_sums(uint32_t element_start) {
     for (unsigned l = 0; l < kLanes; ++l) {
         const uint32_t ls = next_lane_element(element_start, l);
-        for (unsigned s = 0; s < kSums; ++s) {
-            LaneSum& sum = lanes_[l][s];
-            sum.element_start = ls;
-            sum.element_end = ls;
-            sum.chain.reset(ctx_->rows);
-        }
+        LaneSum& sum = lanes_[l];
+        sum.element_start = ls;
+        sum.element_end = ls;
+        sum.sums.reset(ctx_->rows);
     }
     recovered_columns_.clear();
 }
@@ -241,42 +231,35 @@ void Decoder::reset_sums(uint32_t element_start) {
 bool Decoder::start_sums(uint32_t element_start, uint32_t buffer_bytes) {
     for (unsigned l = 0; l < kLanes; ++l) {
         const uint32_t ls = next_lane_element(element_start, l);
-        for (unsigned s = 0; s < kSums; ++s) {
-            LaneSum& sum = lanes_[l][s];
-            if (sum.chain.bytes == 0) {
-                sum.element_end = ls;
-            } else if (sum.element_start != ls) {
-                sum.element_end = ls;
-                sum.chain.reset(ctx_->rows);
-            }
-            sum.element_start = ls;
-            sum.chain.grow(buffer_bytes);
+        LaneSum& sum = lanes_[l];
+        if (sum.sums.bytes == 0) {
+            sum.element_end = ls;
+        } else if (sum.element_start != ls) {
+            sum.element_end = ls;
+            sum.sums.reset(ctx_->rows);
         }
+        sum.element_start = ls;
+        sum.sums.grow(buffer_bytes);
     }
     if (!recovered_columns_.empty() && !plug_sum_holes(element_start)) return false;
     return true;
 }
 
-// DecoderPacketWindow::GetSum (:1680-1739)
-Chain& Decoder::get_sum(uint32_t lane, uint32_t sum_index, uint32_t element_end) {
-    LaneSum& sum = lanes_[lane][sum_index];
+// DecoderPacketWindow::GetSum (:1680-1739), for the lane's three sums at once
+LaneSums& Decoder::get_lane(uint32_t lane, uint32_t element_end) {
+    LaneSum& sum = lanes_[lane];
     uint32_t e = sum.element_end;
-    if (e >= element_end) return sum.chain;
+    if (e >= element_end) return sum.sums;
     do {
         const StoredOriginal& o = elem(e);
         if (o.bytes > 0) {
-            if (o.bytes > sum.chain.bytes) sum.chain.grow(o.bytes);
-            uint8_t cx = 1;
-            if (sum_index > 0) {
-                cx = column_value(o.column);
-                if (sum_index == 2) cx = gf_sqr(cx);
-            }
-            sum.chain.accumulate(ctx_->rows, o.row, o.bytes, cx);
+            sum.sums.grow(o.bytes);
+            sum.sums.accumulate(ctx_->rows, o.row, o.bytes, column_value(o.column));
         }
         e += kLanes;
     } while (e < element_end);
     sum.element_end = e;
-    return sum.chain;
+    return sum.sums;
 }
 
 // DecoderPacketWindow::RemoveElements (:1778-2033)
@@ -334,13 +317,11 @@ void Decoder::remove_elements() {
             if (!start_sums(sum_elem, initial_bytes)) { disabled_ = true; return; }
         }
         for (unsigned l = 0; l < kLanes; ++l) {
-            for (unsigned s = 0; s < kSums; ++s) {
-                get_sum(l, s, removed);
-                LaneSum& sum = lanes_[l][s];
-                if (sum.element_start >= removed) sum.element_start -= removed;
-                else sum.element_start = l;
-                sum.element_end -= removed;
-            }
+            get_lane(l, removed);
+            LaneSum& sum = lanes_[l];
+            if (sum.element_start >= removed) sum.element_start -= removed;
+            else sum.element_start = l;
+            sum.element_end -= removed;
         }
     } else {
         sum_column_count_ = 0;
@@ -762,7 +743,8 @@ bool Decoder::add_single_recovery(RowId row, uint32_t data_bytes, const uint8_t*
     o.row = row;
     o.bytes = data_bytes;
     o.column = m.ColumnStart;
-    o.header_bytes = header;
+    o.header_bytes = (uint8_t)header;
+    o.owned = 1;
     *took = true;
 
     if (!has_recovered_) {
@@ -939,20 +921,14 @@ bool Decoder::eliminate_original_data() {
 
             for (unsigned l = 0; l < kLanes; ++l) {
                 const unsigned op = row_opcode(l, m.Row);
-                for (unsigned s = 0; s < kSums; ++s) {
-                    if (op & (1u << s)) {
-                        Chain& c = get_sum(l, s, ee);
-                        const uint32_t n = c.bytes < rbytes ? c.bytes : rbytes;
-                        if (n) c.read(ctx_->rows, ctx_->ex, buf, n, 1);
-                    }
-                }
-                for (unsigned s = 0; s < kSums; ++s) {
-                    if (op & (1u << (s + 3))) {
-                        Chain& c = get_sum(l, s, ee);
-                        const uint32_t n = c.bytes < rbytes ? c.bytes : rbytes;
-                        if (n) c.read(ctx_->rows, ctx_->ex, prod, n, 1);
-                    }
-                }
+                if (!op) continue;
+                LaneSums& c = get_lane(l, ee);
+                const uint32_t n = c.bytes < rbytes ? c.bytes : rbytes;
+                if (!n) continue;
+                for (unsigned s = 0; s < kSums; ++s)
+                    if (op & (1u << s)) c.read(ctx_->rows, ctx_->ex, buf, s, n, 1);
+                for (unsigned s = 0; s < kSums; ++s)
+                    if (op & (1u << (s + 3))) c.read(ctx_->rows, ctx_->ex, prod, s, n, 1);
             }
             Pcg32 prng;
             prng.seed(m.Row, m.LDPCCount);
@@ -1026,6 +1002,7 @@ Result Decoder::back_substitution() {
         o->bytes = bytes;
         o->column = mcols_[ci].column;
         o->header_bytes = 0;
+        o->owned = 1;
         rec->buf.clear();
         rec->bytes = 0;
 
@@ -1060,7 +1037,7 @@ void Decoder::set_recovered_length(uint32_t packet_num, uint32_t framed_bytes, u
     StoredOriginal& o = elem(e);
     if (o.column != packet_num || o.bytes == 0) { if (host && release_) release_(host, user_); return; }
     o.bytes = framed_bytes;
-    o.header_bytes = header_bytes;
+    o.header_bytes = (uint8_t)header_bytes;
     if (o.host && release_) release_(o.host, user_);
     o.host = host;
 }

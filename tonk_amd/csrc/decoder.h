@@ -30,9 +30,9 @@ public:
     ~Decoder();
 
     // siamese_decoder_add_original: `row` holds the framed original; ownership passes to the
-    // decoder on success only (on DuplicateData the caller keeps it).
+    // decoder on success only (on DuplicateData the caller keeps it), and never when `borrowed`.
     Result add_original(uint32_t packet_num, RowId row, uint32_t framed_bytes, uint32_t header_bytes,
-                        uint32_t payload_bytes, void* host, bool* took_ownership);
+                        uint32_t payload_bytes, void* host, bool* took_ownership, bool borrowed = false);
     // siamese_decoder_add_recovery: `row` holds the packet (data || footer), `tail` the last
     // min(total, 8) bytes of the packet (footer parsing), `host` the whole packet if available.
     // Ownership of `row` passes to the decoder when *took_ownership is set.
@@ -71,9 +71,12 @@ private:
         Sym buf;              // Buffer contents (symbolic)
         uint32_t bytes = 0;   // Buffer.Bytes
     };
+    // DecoderColumnLane (SiameseDecoder.h:121-137): the reference keeps ElementStart/End per
+    // sum, but every path sets them for all three sums of a lane together and reads are
+    // monotone in the element, so one range per lane drives the lane's three sums.
     struct LaneSum {
         uint32_t element_start = 0, element_end = 0;
-        Chain chain;
+        LaneSums sums;
     };
     struct MatRow { Recovery* rec = nullptr; bool used = false; uint32_t mcols = 0; };
     struct MatCol { StoredOriginal* orig = nullptr; uint32_t column = 0; uint8_t cx = 0; };
@@ -88,7 +91,7 @@ private:
     // ---- DecoderPacketWindow (SiameseDecoder.h:288-419) ----
     uint32_t count_ = 0, column_start_ = 0, next_expected_ = 0;
     std::vector<Subwindow*> subs_;
-    LaneSum lanes_[kLanes][kSums];
+    LaneSum lanes_[kLanes];
     uint32_t sum_column_start_ = 0, sum_column_count_ = 0;
     std::vector<RecoveredPacket> recovered_;
     bool has_recovered_ = false;
@@ -143,7 +146,7 @@ private:
     uint32_t find_next_got(uint32_t start);
     void iterate_next_expected(uint32_t start);
     bool grow_window(uint32_t end);
-    Chain& get_sum(uint32_t lane, uint32_t sum, uint32_t element_end);
+    LaneSums& get_lane(uint32_t lane, uint32_t element_end);
     bool start_sums(uint32_t element_start, uint32_t buffer_bytes);
     void reset_sums(uint32_t element_start);
     bool plug_sum_holes(uint32_t element_start);

@@ -18,8 +18,7 @@ uint64_t time_msec() {
 Encoder::Encoder(Context* ctx, uint32_t row_bytes, HostRelease release, void* user)
     : ctx_(ctx), row_bytes_(row_bytes), release_(release), user_(user) {
     // ClearWindow (SiameseEncoder.cpp:64-83)
-    for (unsigned l = 0; l < kLanes; ++l)
-        for (unsigned s = 0; s < kSums; ++s) lanes_[l].next_element[s] = l;
+    for (unsigned l = 0; l < kLanes; ++l) lanes_[l].next_element = l;
     ctx_->attach(this);
 }
 
@@ -27,25 +26,23 @@ Encoder::~Encoder() {
     pre_flush();  // snapshots already referenced by the pending program must still be written
     for (size_t i = 0; i < win_.size(); ++i) drop_original(win_[i]);
     win_.clear();
-    for (unsigned l = 0; l < kLanes; ++l)
-        for (unsigned s = 0; s < kSums; ++s) lanes_[l].sum[s].release(ctx_->rows);
+    for (unsigned l = 0; l < kLanes; ++l) lanes_[l].sums.release(ctx_->rows);
     ctx_->detach(this);
 }
 
 void Encoder::drop_original(StoredOriginal& o) {
-    if (o.row != kNoRow) ctx_->rows.free_deferred(o.row);
+    if (o.owned) ctx_->rows.free_deferred(o.row);
     if (o.host && release_) release_(o.host, user_);
     o = StoredOriginal();
 }
 
 void Encoder::pre_flush() {
-    for (unsigned l = 0; l < kLanes; ++l)
-        for (unsigned s = 0; s < kSums; ++s) lanes_[l].sum[s].flush(ctx_->rows, ctx_->pb, ctx_->ex, row_bytes_);
+    for (unsigned l = 0; l < kLanes; ++l) lanes_[l].sums.flush(ctx_->rows, ctx_->pb, ctx_->ex);
 }
 
 // EncoderPacketWindow::Add (SiameseEncoder.cpp:85-161)
 Result Encoder::add(RowId row, uint32_t framed_bytes, uint32_t header_bytes, uint32_t payload_bytes,
-                    void* host, uint32_t* packet_num) {
+                    void* host, uint32_t* packet_num, bool borrowed) {
     if (disabled_) return kDisabled;
     if (remaining_slots() <= 0) return kMaxPacketsReached;
 
@@ -65,7 +62,8 @@ Result Encoder::add(RowId row, uint32_t framed_bytes, uint32_t header_bytes, uin
     o.row = row;
     o.bytes = framed_bytes;
     o.column = column;
-    o.header_bytes = header_bytes;
+    o.header_bytes = (uint8_t)header_bytes;
+    o.owned = borrowed ? 0 : 1;
     o.send_msec = (uint32_t)time_msec();
     o.host = host;
     if (win_.size() == element) win_.push_back(o);
@@ -111,11 +109,8 @@ void Encoder::remove_before(uint32_t first_kept_column) {
 // EncoderPacketWindow::ResetSums (SiameseEncoder.cpp:218-237)
 void Encoder::reset_sums(uint32_t element_start) {
     for (unsigned l = 0; l < kLanes; ++l) {
-        const uint32_t next = next_lane_element(element_start, l);
-        for (unsigned s = 0; s < kSums; ++s) {
-            lanes_[l].next_element[s] = next;
-            lanes_[l].sum[s].reset(ctx_->rows);
-        }
+        lanes_[l].next_element = next_lane_element(element_start, l);
+        lanes_[l].sums.reset(ctx_->rows);
     }
     sum_start_ = element_start;
     sum_end_ = element_start;
@@ -130,10 +125,8 @@ void Encoder::remove_elements() {
 
     if (sum_end_ > sum_start_) {
         for (unsigned l = 0; l < kLanes; ++l) {
-            for (unsigned s = 0; s < kSums; ++s) {
-                get_sum(l, s, removed);
-                lanes_[l].next_element[s] -= removed;
-            }
+            get_lane(l, removed);
+            lanes_[l].next_element -= removed;
         }
         if (removed > sum_start_) sum_erased_ += removed - sum_start_;
         sum_end_ = sum_end_ > removed ? sum_end_ - removed : 0;
@@ -158,28 +151,22 @@ void Encoder::remove_elements() {
     if (sum_end_ <= sum_start_) reset_sums(first_unremoved_);
 }
 
-// EncoderPacketWindow::GetSum (SiameseEncoder.cpp:359-418)
-Chain& Encoder::get_sum(uint32_t lane_index, uint32_t sum_index, uint32_t element_end) {
+// EncoderPacketWindow::GetSum (SiameseEncoder.cpp:359-418), for the lane's three sums at once
+LaneSums& Encoder::get_lane(uint32_t lane_index, uint32_t element_end) {
     Lane& lane = lanes_[lane_index];
-    Chain& sum = lane.sum[sum_index];
-    uint32_t element = lane.next_element[sum_index];
+    LaneSums& sums = lane.sums;
+    uint32_t element = lane.next_element;
     if (element < element_end) {
-        if (lane.longest > 0) sum.grow(lane.longest);
+        if (lane.longest > 0) sums.grow(lane.longest);
         do {
             const StoredOriginal& o = win_[element];
-            const uint32_t add = o.bytes;
-            sum.grow(add);
-            uint8_t cx = 1;
-            if (sum_index > 0) {
-                cx = column_value(o.column);
-                if (sum_index == 2) cx = gf_sqr(cx);
-            }
-            sum.accumulate(ctx_->rows, o.row, add, cx);
+            sums.grow(o.bytes);
+            sums.accumulate(ctx_->rows, o.row, o.bytes, column_value(o.column));
             element += kLanes;
         } while (element < element_end);
-        lane.next_element[sum_index] = element;
+        lane.next_element = element;
     }
-    return sum;
+    return sums;
 }
 
 // ---- acknowledgements (SiameseEncoder.cpp:514-800) ----
@@ -482,20 +469,14 @@ Result Encoder::generate_cauchy(RecoveryOut& out) {
 void Encoder::add_dense(uint32_t row, uint32_t recovery_bytes, Sym& rec, Sym& prod) {
     for (unsigned l = 0; l < kLanes; ++l) {
         const unsigned op = row_opcode(l, row);
-        for (unsigned s = 0; s < kSums; ++s) {
-            if (op & (1u << s)) {
-                Chain& c = get_sum(l, s, count_);
-                const uint32_t n = c.bytes < recovery_bytes ? c.bytes : recovery_bytes;
-                if (n) c.read(ctx_->rows, ctx_->ex, rec, n, 1);
-            }
-        }
-        for (unsigned s = 0; s < kSums; ++s) {
-            if (op & (1u << (s + 3))) {
-                Chain& c = get_sum(l, s, count_);
-                const uint32_t n = c.bytes < recovery_bytes ? c.bytes : recovery_bytes;
-                if (n) c.read(ctx_->rows, ctx_->ex, prod, n, 1);
-            }
-        }
+        if (!op) continue;
+        LaneSums& c = get_lane(l, count_);
+        const uint32_t n = c.bytes < recovery_bytes ? c.bytes : recovery_bytes;
+        if (!n) continue;
+        for (unsigned s = 0; s < kSums; ++s)
+            if (op & (1u << s)) c.read(ctx_->rows, ctx_->ex, rec, s, n, 1);
+        for (unsigned s = 0; s < kSums; ++s)
+            if (op & (1u << (s + 3))) c.read(ctx_->rows, ctx_->ex, prod, s, n, 1);
     }
     sum_end_ = count_;
 }

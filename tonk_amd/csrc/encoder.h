@@ -35,8 +35,9 @@ struct StoredOriginal {
     RowId row = kNoRow;
     uint32_t bytes = 0;         // framed bytes (Buffer.Bytes)
     uint32_t column = 0;
-    uint32_t header_bytes = 0;
     uint32_t send_msec = 0;     // encoder only (retransmit timing)
+    uint8_t header_bytes = 0;
+    uint8_t owned = 0;          // the codec frees `row` when the packet leaves the window
     void* host = nullptr;       // optional host mirror (C-ABI: siamese_encoder_get/retransmit)
 };
 
@@ -50,9 +51,10 @@ public:
     unsigned remaining_slots() const { return kMaxPackets - count_; }
 
     // siamese_encoder_add: the caller provides the framed row already written to the arena.
-    // Ownership of `row` (and `host`) passes to the encoder on success.
+    // Ownership of `row` (and `host`) passes to the encoder on success unless `borrowed`: a
+    // borrowed row stays the caller's (device-resident inputs that outlive the codec).
     Result add(RowId row, uint32_t framed_bytes, uint32_t header_bytes, uint32_t payload_bytes,
-               void* host, uint32_t* packet_num);
+               void* host, uint32_t* packet_num, bool borrowed = false);
     Result get(uint32_t packet_num, const StoredOriginal** out);
     void remove_before(uint32_t first_kept_column);
     Result acknowledge(const uint8_t* data, uint32_t bytes, uint32_t* next_expected);
@@ -82,9 +84,11 @@ private:
     uint32_t next_column_ = 0, count_ = 0, column_start_ = 0, longest_ = 0;
     uint32_t first_unremoved_ = 0;
     uint32_t sum_start_ = 0, sum_end_ = 0, sum_column_start_ = 0, sum_erased_ = 0;
+    // The reference advances each of a lane's three sums lazily on its own; their values only
+    // depend on the element they are read at (always Count), so one position per lane suffices.
     struct Lane {
-        uint32_t next_element[kSums];
-        Chain sum[kSums];
+        uint32_t next_element = 0;
+        LaneSums sums;
         uint32_t longest = 0;
     } lanes_[kLanes];
 
@@ -116,7 +120,7 @@ private:
     void start_new_window(uint32_t column);
     void reset_sums(uint32_t element_start);
     void remove_elements();
-    Chain& get_sum(uint32_t lane, uint32_t sum, uint32_t element_end);
+    LaneSums& get_lane(uint32_t lane, uint32_t element_end);
 
     bool decode_next_range();
     bool next_loss_column(uint32_t& column);

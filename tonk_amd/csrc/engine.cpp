@@ -23,7 +23,8 @@ void RowTable::init(uint64_t arena_bytes, uint64_t base_units) {
     free_offsets_.assign(kSmallClasses + 1, std::vector<uint32_t>());
     free_big_.clear();
     pending_.clear();
-    unsealed_.clear();
+    pending_head_ = 0;
+    open_epoch_ = 1;
 }
 
 RowId RowTable::alloc(uint32_t bytes) {
@@ -73,22 +74,21 @@ void RowTable::release(RowId r) {
     free_handles_.push_back(r);
 }
 
-void RowTable::free_deferred(RowId r) {
-    if (r != kNoRow) unsealed_.push_back(r);
-}
-
-void RowTable::seal_epoch(uint64_t epoch) {
-    for (RowId r : unsealed_) pending_.push_back(Pending{epoch, r});
-    unsealed_.clear();
-}
+void RowTable::seal_epoch(uint64_t epoch) { open_epoch_ = epoch + 1; }
 
 void RowTable::release_up_to(uint64_t completed) {
-    size_t k = 0;
-    for (size_t i = 0; i < pending_.size(); ++i) {
-        if (pending_[i].epoch <= completed) release(pending_[i].row);
-        else pending_[k++] = pending_[i];
+    size_t i = pending_head_;
+    const size_t n = pending_.size();
+    while (i < n && pending_[i].epoch <= completed) release(pending_[i++].row);
+    if (i == n) {
+        pending_.clear();
+        pending_head_ = 0;
+    } else if (i > 4096 && i * 2 > n) {
+        pending_.erase(pending_.begin(), pending_.begin() + (std::ptrdiff_t)i);
+        pending_head_ = 0;
+    } else {
+        pending_head_ = i;
     }
-    pending_.resize(k);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -112,10 +112,22 @@ void ProgramBuilder::begin_op() {
     cur_written_begin_ = written_.size();
 }
 
-void ProgramBuilder::op_acc(RowId src, uint8_t coef, uint32_t len) {
+void ProgramBuilder::op_acc3(RowId src, uint8_t c1, uint8_t c2, uint32_t len) {
+    if (!len) return;
+    tamd_instr in;
+    in.w0 = tamd_w0(TAMD_I_ACC3, c1, c2);
+    in.row = rows_->offset(src);
+    in.len = len;
+    in.cap = 0;
+    instrs_.push_back(in);
+    if (len > cur_span_) cur_span_ = len;
+    acc_bytes_ += len;
+}
+
+void ProgramBuilder::op_acc(RowId src, uint8_t coef, uint32_t len, uint32_t acc) {
     if (!coef || !len) return;
     tamd_instr in;
-    in.w0 = tamd_w0(TAMD_I_ACC, coef);
+    in.w0 = tamd_w0(TAMD_I_ACC, coef, acc);
     in.row = rows_->offset(src);
     in.len = len;
     in.cap = 0;
@@ -127,9 +139,9 @@ void ProgramBuilder::op_acc(RowId src, uint8_t coef, uint32_t len) {
 }
 
 static void push_store(std::vector<tamd_instr>& v, uint32_t off, uint32_t len, uint32_t cap,
-                       const uint8_t* footer, uint32_t flen) {
+                       const uint8_t* footer, uint32_t flen, uint32_t acc = 0) {
     tamd_instr s;
-    s.w0 = tamd_w0(TAMD_I_STORE, flen);
+    s.w0 = tamd_w0(TAMD_I_STORE, flen, acc);
     s.row = off;
     s.len = len;
     s.cap = cap;
@@ -144,9 +156,9 @@ static void push_store(std::vector<tamd_instr>& v, uint32_t off, uint32_t len, u
     v.push_back(f);
 }
 
-void ProgramBuilder::op_store(RowId dst, uint32_t len) {
+void ProgramBuilder::op_store(RowId dst, uint32_t len, uint32_t acc) {
     const uint32_t cap = rows_->cap_bytes(dst);
-    push_store(instrs_, rows_->offset(dst), len, cap, nullptr, 0);
+    push_store(instrs_, rows_->offset(dst), len, cap, nullptr, 0, acc);
     if (cap > cur_span_) cur_span_ = cap;
     written_.push_back(dst);
     store_bytes_ += len;
@@ -234,20 +246,19 @@ void ExpansionTable::append(const RowTable& rows, RowId r, uint32_t len, uint8_t
 }
 
 // ---------------------------------------------------------------------------------------------
-// Chain
+// LaneSums
 // ---------------------------------------------------------------------------------------------
-void Chain::reset(RowTable& rows) {
+void LaneSums::reset(RowTable& rows) {
     if (!snaps_.empty()) {
         Closed c;
-        c.base = base_;
-        c.content = content_;
+        for (unsigned s = 0; s < 3; ++s) c.base[s] = base_[s];
         c.terms.swap(terms_);
         c.snaps.swap(snaps_);
         closed_.push_back(std::move(c));
     } else {
-        rows.free_deferred(base_);
+        for (unsigned s = 0; s < 3; ++s) rows.free_deferred(base_[s]);
     }
-    base_ = kNoRow;
+    for (unsigned s = 0; s < 3; ++s) base_[s] = kNoRow;
     terms_.clear();
     snaps_.clear();
     dyn_.clear();
@@ -255,120 +266,130 @@ void Chain::reset(RowTable& rows) {
     bytes = 0;
 }
 
-void Chain::accumulate(RowTable& rows, RowId row, uint32_t len, uint8_t coef) {
-    if (!coef || !len) return;
+void LaneSums::accumulate(RowTable& rows, RowId row, uint32_t len, uint8_t cx) {
+    if (!len) return;
     if (len > content_) content_ = len;
-    if (rows.level(row) == 0) terms_.push_back(Term{row, len, coef});
-    else dyn_.push_back(DynContribution{row, len, coef});
+    if (rows.level(row) == 0) terms_.push_back(T{row, len, cx});
+    else dyn_.push_back(T{row, len, cx});
 }
 
-void Chain::read(RowTable& rows, const ExpansionTable& ex, Sym& out, uint32_t limit, uint8_t coef) {
+void LaneSums::read(RowTable& rows, const ExpansionTable& ex, Sym& out, unsigned s, uint32_t limit, uint8_t coef) {
     if (!coef || !limit) return;
     const uint32_t clip = content_ < limit ? content_ : limit;
     if (!terms_.empty()) {
-        RowId snap;
-        if (!snaps_.empty() && snaps_.back().after == terms_.size()) {
-            snap = snaps_.back().row;
-        } else {
+        const uint32_t at = (uint32_t)terms_.size();
+        RowId snap = kNoRow;
+        for (size_t i = snaps_.size(); i-- > 0 && snaps_[i].after == at;)
+            if (snaps_[i].sum == s) { snap = snaps_[i].row; break; }
+        if (snap == kNoRow) {
             snap = rows.alloc(content_);
             if (snap == kNoRow) return;  // caller checks arena exhaustion via RowTable
             rows.set_level(snap, 1);
-            snaps_.push_back(Snap{snap, (uint32_t)terms_.size()});
+            snaps_.push_back(Snap{snap, at, s});
         }
         if (clip) out.push_back(Term{snap, clip, coef});
-    } else if (base_ != kNoRow && clip) {
-        out.push_back(Term{base_, clip, coef});
+    } else if (base_[s] != kNoRow && clip) {
+        out.push_back(Term{base_[s], clip, coef});
     }
-    for (const DynContribution& d : dyn_) {
+    for (const T& d : dyn_) {
         const uint32_t l = d.len < limit ? d.len : limit;
-        ex.append(rows, d.row, l, gf_mul(d.coef, coef), out);
+        ex.append(rows, d.row, l, gf_mul(sum_coef(s, d.cx), coef), out);
     }
 }
 
-void Chain::emit_scan(RowTable& rows, ProgramBuilder& pb, RowId base, uint32_t content,
-                      const std::vector<Term>& terms, const std::vector<Snap>& snaps,
-                      RowId final_row) {
-    (void)content;
+void LaneSums::emit_scan(RowTable& rows, ProgramBuilder& pb, const RowId* base, const std::vector<T>& terms,
+                         const std::vector<Snap>& snaps, const RowId* final_rows) {
     pb.begin_op();
-    uint32_t cur = 0;
-    if (base != kNoRow) {
-        pb.op_acc(base, 1, rows.cap_bytes(base));
-    }
+    for (unsigned s = 0; s < 3; ++s)
+        if (base[s] != kNoRow) pb.op_acc(base[s], 1, rows.cap_bytes(base[s]), s);
     size_t si = 0;
     for (size_t i = 0; i <= terms.size(); ++i) {
         while (si < snaps.size() && snaps[si].after == i) {
-            pb.op_store(snaps[si].row, rows.cap_bytes(snaps[si].row));
+            pb.op_store(snaps[si].row, rows.cap_bytes(snaps[si].row), snaps[si].sum);
             ++si;
         }
         if (i == terms.size()) break;
-        pb.op_acc(terms[i].row, terms[i].coef, terms[i].len);
-        if (terms[i].len > cur) cur = terms[i].len;
+        const T& t = terms[i];
+        pb.op_acc3(t.row, t.cx, gf_sqr(t.cx), t.len);
     }
-    if (final_row != kNoRow) pb.op_store(final_row, rows.cap_bytes(final_row));
+    if (final_rows)
+        for (unsigned s = 0; s < 3; ++s)
+            if (final_rows[s] != kNoRow) pb.op_store(final_rows[s], rows.cap_bytes(final_rows[s]), s);
     pb.end_op(1);
 }
 
-void Chain::flush(RowTable& rows, ProgramBuilder& pb, const ExpansionTable& ex, uint32_t row_bytes) {
-    (void)row_bytes;
+void LaneSums::flush(RowTable& rows, ProgramBuilder& pb, const ExpansionTable& ex) {
     TAMD_PROF_SCOPE(kChainFlush);
     for (Closed& c : closed_) {
-        emit_scan(rows, pb, c.base, c.content, c.terms, c.snaps, kNoRow);
-        rows.free_deferred(c.base);
-        for (const Snap& s : c.snaps) rows.free_deferred(s.row);
+        emit_scan(rows, pb, c.base, c.terms, c.snaps, nullptr);
+        for (unsigned s = 0; s < 3; ++s) rows.free_deferred(c.base[s]);
+        for (const Snap& sn : c.snaps) rows.free_deferred(sn.row);
     }
     closed_.clear();
 
     if (terms_.empty() && dyn_.empty()) {
-        // Nothing accumulated since the last flush: snapshots (if any) alias the base.
+        // Nothing accumulated since the last flush: snapshots (if any) alias the bases.
         snaps_.clear();
         return;
     }
 
-    RowId state = base_;  // row that holds the static value after the scan
+    RowId state[3] = {base_[0], base_[1], base_[2]};  // rows holding the static values after the scan
     bool state_is_new = false;
     if (!terms_.empty()) {
-        RowId final_row = kNoRow;
-        if (!snaps_.empty() && snaps_.back().after == terms_.size()) {
-            state = snaps_.back().row;
-        } else {
-            final_row = rows.alloc(content_);
-            state = final_row;
+        RowId final_rows[3] = {kNoRow, kNoRow, kNoRow};
+        const uint32_t at = (uint32_t)terms_.size();
+        for (unsigned s = 0; s < 3; ++s) {
+            RowId end_snap = kNoRow;
+            for (size_t i = snaps_.size(); i-- > 0 && snaps_[i].after == at;)
+                if (snaps_[i].sum == s) { end_snap = snaps_[i].row; break; }
+            if (end_snap != kNoRow) {
+                state[s] = end_snap;
+            } else {
+                final_rows[s] = rows.alloc(content_);
+                state[s] = final_rows[s];
+            }
         }
-        emit_scan(rows, pb, base_, content_, terms_, snaps_, final_row);
-        for (const Snap& s : snaps_)
-            if (s.row != state) rows.free_deferred(s.row);
+        emit_scan(rows, pb, base_, terms_, snaps_, final_rows);
+        for (const Snap& sn : snaps_)
+            if (sn.row != state[sn.sum]) rows.free_deferred(sn.row);
         state_is_new = true;
     }
 
     if (!dyn_.empty()) {
-        // Fold contributions of rows produced by this program into the carried value.
-        Sym t;
-        if (state != kNoRow) t.push_back(Term{state, rows.cap_bytes(state), 1});
-        for (const DynContribution& d : dyn_) ex.append(rows, d.row, d.len, d.coef, t);
-        sym_merge(t);
-        const RowId carry = rows.alloc(content_);
-        pb.combine(carry, t.data(), t.size(), content_);
-        if (state_is_new) rows.free_deferred(state);
-        if (base_ != kNoRow) rows.free_deferred(base_);
-        base_ = carry;
+        // Fold contributions of rows produced by this program into the carried values.
+        for (unsigned s = 0; s < 3; ++s) {
+            Sym t;
+            if (state[s] != kNoRow) t.push_back(Term{state[s], rows.cap_bytes(state[s]), 1});
+            for (const T& d : dyn_) ex.append(rows, d.row, d.len, sum_coef(s, d.cx), t);
+            sym_merge(t);
+            const RowId carry = rows.alloc(content_);
+            pb.combine(carry, t.data(), t.size(), content_);
+            if (state_is_new) rows.free_deferred(state[s]);
+            if (base_[s] != kNoRow) rows.free_deferred(base_[s]);
+            base_[s] = carry;
+        }
     } else {
-        if (base_ != kNoRow && base_ != state) rows.free_deferred(base_);
-        base_ = state;
+        for (unsigned s = 0; s < 3; ++s) {
+            if (base_[s] != kNoRow && base_[s] != state[s]) rows.free_deferred(base_[s]);
+            base_[s] = state[s];
+        }
     }
     terms_.clear();
     snaps_.clear();
     dyn_.clear();
 }
 
-void Chain::release(RowTable& rows) {
+void LaneSums::release(RowTable& rows) {
     for (Closed& c : closed_) {
-        rows.free_deferred(c.base);
-        for (const Snap& s : c.snaps) rows.free_deferred(s.row);
+        for (unsigned s = 0; s < 3; ++s) rows.free_deferred(c.base[s]);
+        for (const Snap& sn : c.snaps) rows.free_deferred(sn.row);
     }
     closed_.clear();
-    for (const Snap& s : snaps_) rows.free_deferred(s.row);
-    rows.free_deferred(base_);
-    base_ = kNoRow;
+    for (const Snap& sn : snaps_) rows.free_deferred(sn.row);
+    for (unsigned s = 0; s < 3; ++s) {
+        rows.free_deferred(base_[s]);
+        base_[s] = kNoRow;
+    }
     terms_.clear();
     snaps_.clear();
     dyn_.clear();

@@ -59,7 +59,9 @@ public:
     RowId alloc(uint32_t bytes);
     // Release a row.  The memory is not reused until release_deferred() (called by the owner
     // once every program that may still read the row has completed on the device).
-    void free_deferred(RowId r);
+    void free_deferred(RowId r) {
+        if (r != kNoRow) pending_.push_back(Pending{open_epoch_, r});
+    }
     // Make rows freed since the previous call reusable.  `epoch` must be the flush epoch whose
     // device work has completed.
     void release_up_to(uint64_t completed_epoch);
@@ -79,8 +81,9 @@ private:
     std::vector<std::vector<uint32_t>> free_offsets_;  // by size in units (small sizes)
     std::vector<std::pair<uint32_t, uint32_t>> free_big_; // (off, units) for large rows
     struct Pending { uint64_t epoch; RowId row; };
-    std::vector<Pending> pending_;
-    std::vector<RowId> unsealed_;
+    std::vector<Pending> pending_;  // nondecreasing epochs; [pending_head_, end) not yet released
+    size_t pending_head_ = 0;
+    uint64_t open_epoch_ = 1;       // epoch rows freed now belong to
     uint32_t total_units_ = 0, bump_ = 0;
     uint64_t base_ = 0;
     uint64_t used_units_ = 0;
@@ -100,10 +103,11 @@ public:
     uint32_t combine(RowId dst, const Term* terms, size_t n, uint32_t len,
                      const uint8_t* footer = nullptr, uint32_t footer_len = 0);
 
-    // Raw op construction for scans: begin, add ACC/STORE instructions, end.
+    // Raw op construction for scans: begin, add ACC/ACC3/STORE instructions, end.
     void begin_op();
-    void op_acc(RowId src, uint8_t coef, uint32_t len);
-    void op_store(RowId dst, uint32_t len);
+    void op_acc(RowId src, uint8_t coef, uint32_t len, uint32_t acc = 0);
+    void op_acc3(RowId src, uint8_t c1, uint8_t c2, uint32_t len);  // level-0 rows only
+    void op_store(RowId dst, uint32_t len, uint32_t acc = 0);
     uint32_t end_op(uint32_t min_level = 1);  // returns level; rows stored get that level
 
     bool empty() const { return ops_.empty(); }
@@ -174,48 +178,49 @@ inline void sym_clip(Sym& s, uint32_t limit) {
 void sym_merge(Sym& s);
 
 // ---------------------------------------------------------------------------------------------
-// Running sum (one lane x one sum index) as a chain.
+// The three running sums of one lane, as one scan.
+//
+// Sum s of a lane accumulates coef_s(cx) * row for every packet of the lane, where cx is the
+// packet's column value and coef = (1, cx, cx^2) (SiameseEncoder.cpp:359-418,
+// SiameseDecoder.cpp:1538-1739).  All three sums see the same packets in the same order, so
+// the device walks them together: one ACC3 instruction per packet reads the row once and
+// updates the three accumulators, and a snapshot STOREs one accumulator when a sum is read.
 // ---------------------------------------------------------------------------------------------
-struct DynContribution {
-    RowId row;      // row holding (or that will hold) the contributed data (level > 0)
-    uint32_t len;
-    uint8_t coef;
-};
-
 class ExpansionTable;  // rows produced in the pending program -> their symbolic content
 
-class Chain {
+class LaneSums {
 public:
     uint32_t bytes = 0;  // logical length, GrowingAlignedDataBuffer::Bytes semantics
 
-    bool empty() const { return base_ == kNoRow && terms_.empty() && dyn_.empty(); }
     // Reference "Bytes = 0": the contents restart from zero.
     void reset(RowTable& rows);
     // GrowZeroPadded: only the logical length changes (data beyond is zero by construction).
     void grow(uint32_t b) { if (b > bytes) bytes = b; }
-    // sum ^= coef * data  (data = row, possibly produced in the pending program)
-    void accumulate(RowTable& rows, RowId row, uint32_t len, uint8_t coef);
-    // Append the current value, clipped to `limit` bytes and scaled by `coef`, to `out`.
-    void read(RowTable& rows, const ExpansionTable& ex, Sym& out, uint32_t limit, uint8_t coef);
-    // Emit the chain's scan (and fix-up) ops for the pending program and rebase the chain.
-    void flush(RowTable& rows, ProgramBuilder& pb, const ExpansionTable& ex, uint32_t row_bytes);
+    // sum_s ^= cx^s * data for s = 0, 1, 2 (data = row, possibly produced in the pending program)
+    void accumulate(RowTable& rows, RowId row, uint32_t len, uint8_t cx);
+    // Append the current value of sum `s`, clipped to `limit` bytes and scaled by `coef`.
+    void read(RowTable& rows, const ExpansionTable& ex, Sym& out, unsigned s, uint32_t limit, uint8_t coef);
+    // Emit the scan (and fix-up) ops for the pending program and rebase the sums.
+    void flush(RowTable& rows, ProgramBuilder& pb, const ExpansionTable& ex);
     // Drop everything (codec destruction).
     void release(RowTable& rows);
 
 private:
-    struct Snap { RowId row; uint32_t after; };
-    RowId base_ = kNoRow;        // carry row from a previous flush (level 0)
-    uint32_t content_ = 0;       // bytes the accumulated content may occupy
-    std::vector<Term> terms_;    // level-0 terms accumulated since base_
+    struct T { RowId row; uint32_t len; uint8_t cx; };
+    struct Snap { RowId row; uint32_t after; uint32_t sum; };
+    RowId base_[3] = {kNoRow, kNoRow, kNoRow};  // carried values from a previous flush (level 0)
+    uint32_t content_ = 0;                      // bytes the accumulated content may occupy
+    std::vector<T> terms_;                      // level-0 packets accumulated since base_
     std::vector<Snap> snaps_;
-    std::vector<DynContribution> dyn_;  // contributions from rows produced in this program
+    std::vector<T> dyn_;                        // packets produced in this program (level > 0)
     // closed epochs (reset while the program was pending) still owe their snapshots
-    struct Closed { RowId base; uint32_t content; std::vector<Term> terms; std::vector<Snap> snaps; };
+    struct Closed { RowId base[3]; std::vector<T> terms; std::vector<Snap> snaps; };
     std::vector<Closed> closed_;
-    static void emit_scan(RowTable& rows, ProgramBuilder& pb, RowId base, uint32_t content,
-                          const std::vector<Term>& terms, const std::vector<Snap>& snaps,
-                          RowId final_row);
+    static void emit_scan(RowTable& rows, ProgramBuilder& pb, const RowId* base, const std::vector<T>& terms,
+                          const std::vector<Snap>& snaps, const RowId* final_rows);
 };
+
+inline uint8_t sum_coef(unsigned s, uint8_t cx) { return s == 0 ? 1 : (s == 1 ? cx : gf_sqr(cx)); }
 
 // Symbolic content of rows written by the pending program, so readers in the same flush can
 // use the content's terms instead of the row itself (which would add a level).

@@ -1,7 +1,7 @@
 // kernels.hip -- CDNA4 (gfx950) kernels of the Siamese engine.
 //
 // tamd_exec runs one level of a device program (program.h).  Work item = (op, 512-byte slice):
-// one 64-lane wave owns 8 bytes per lane of one op's accumulator and walks the op's
+// one 64-lane wave owns 8 bytes per lane of the op's three accumulators and walks the op's
 // instruction list (wave-uniform, scalar loads).  GF(2^8) byte multiplication by the
 // instruction's coefficient uses three 8-entry product tables per coefficient staged in LDS
 // and v_perm_b32 byte lookups (x*c = T0[x&7] ^ T1[(x>>3)&7] ^ T2[x>>6]), so a muladd costs
@@ -80,7 +80,7 @@ tamd_exec(const tamd_op* __restrict__ ops, const tamd_instr* __restrict__ instrs
         const uint2 item = items[it];
         const tamd_op op = ops[uniform(item.x)];
         const uint32_t o = uniform(item.y) * TAMD_SLICE_BYTES + lane * TAMD_LANE_BYTES;
-        u64 acc = 0;
+        u64 a0 = 0, a1 = 0, a2 = 0;  // the op's three accumulators (program.h)
         const uint32_t first = uniform(op.first), end = uniform(op.first + op.count);
         for (uint32_t k = first; k < end; k += TAMD_BATCH) {
             tamd_instr in[TAMD_BATCH];
@@ -91,7 +91,8 @@ tamd_exec(const tamd_op* __restrict__ ops, const tamd_instr* __restrict__ instrs
                 in[j].w0 = 0;
                 if (k + j < end) {
                     in[j] = instrs[k + j];
-                    if ((in[j].w0 & 0xffu) == TAMD_I_ACC && o < in[j].len)
+                    const uint32_t kind = in[j].w0 & 0xffu;
+                    if ((kind == TAMD_I_ACC || kind == TAMD_I_ACC3) && o < in[j].len)
                         v[j] = *(const u64*)(arena + (size_t)in[j].row * TAMD_ROW_UNIT + o);
                 }
             }
@@ -105,14 +106,27 @@ tamd_exec(const tamd_op* __restrict__ ops, const tamd_instr* __restrict__ instrs
                         if (o + 8u > len) x &= byte_mask(len - o);
                         const uint32_t coef = (in[j].w0 >> 8) & 0xffu;
                         if (coef != 1u) x = gf_mul8(x, coef, lds_perm);
-                        acc ^= x;
+                        const uint32_t a = (in[j].w0 >> 16) & 0xffu;
+                        if (a == 0) a0 ^= x;
+                        else if (a == 1) a1 ^= x;
+                        else a2 ^= x;
+                    }
+                } else if (kind == TAMD_I_ACC3) {
+                    const uint32_t len = in[j].len;
+                    if (o < len) {
+                        u64 x = v[j];
+                        if (o + 8u > len) x &= byte_mask(len - o);
+                        a0 ^= x;
+                        a1 ^= gf_mul8(x, (in[j].w0 >> 8) & 0xffu, lds_perm);
+                        a2 ^= gf_mul8(x, (in[j].w0 >> 16) & 0xffu, lds_perm);
                     }
                 } else if (kind == TAMD_I_STORE) {
                     // the FOOTER word follows the STORE (possibly in the next batch)
                     const tamd_instr f = (j + 1 < TAMD_BATCH) ? in[j + 1 < TAMD_BATCH ? j + 1 : j] : instrs[k + j + 1];
-                    store_slice(arena, in[j], f, o, acc);
+                    const uint32_t a = (in[j].w0 >> 16) & 0xffu;
+                    store_slice(arena, in[j], f, o, a == 0 ? a0 : (a == 1 ? a1 : a2));
                 } else if (kind == TAMD_I_CLEAR) {
-                    acc = 0;
+                    a0 = a1 = a2 = 0;
                 }
             }
         }

@@ -10,7 +10,8 @@ namespace tamd {
 namespace prof {
 enum Slot {
     kEncAdd, kEncEncode, kEncAck, kDecAddOrig, kDecAddRec, kDecDecode, kDecAck, kDecIsReady,
-    kGenMatrix, kGE, kElim, kLowerTri, kBackSub, kChainFlush, kSymMerge, kFlushAll, kSlots
+    kGenMatrix, kGE, kElim, kLowerTri, kBackSub, kChainFlush, kSymMerge, kFlushAll, kFinish, kRelease,
+    kSlots
 };
 extern thread_local uint64_t cycles[kSlots];
 extern thread_local uint64_t calls[kSlots];

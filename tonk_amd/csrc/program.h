@@ -4,11 +4,16 @@
 // A program is a flat list of independent ops.  Each op owns an accumulator the width of its
 // span and runs its instruction list in order:
 //
-//   ACC   (row, coef, len)             acc[j] ^= coef * row[j]          for j < len
-//   STORE (row, len, footer, cap)      row[j] = acc[j]                  for j < len
+//   ACC   (row, coef, len, a)          acc_a[j] ^= coef * row[j]        for j < len
+//   ACC3  (row, c1, c2, len)           acc_0[j] ^= row[j], acc_1[j] ^= c1 * row[j],
+//                                      acc_2[j] ^= c2 * row[j]          for j < len
+//   STORE (row, len, footer, cap, a)   row[j] = acc_a[j]                for j < len
 //                                      row[j] = footer[j - len]         for len <= j < len + F
 //                                      row[j] = 0                       for len + F <= j < cap
-//   CLEAR                              acc = 0
+//   CLEAR                              acc_0 = acc_1 = acc_2 = 0
+//
+// An op owns three accumulators; plain combines use acc_0 only, lane running-sum scans use all
+// three (sum s of a lane accumulates cx^s * packet, one ACC3 per packet).
 //
 // Rows are addressed in 64-byte units from the arena base.  Byte positions are independent in
 // GF(2^8) arithmetic, so an op is split into byte slices that the device runs in parallel with
@@ -25,11 +30,12 @@ enum tamd_instr_kind {
     TAMD_I_STORE  = 2,
     TAMD_I_FOOTER = 3,  // payload word that always follows a STORE
     TAMD_I_CLEAR  = 4,
+    TAMD_I_ACC3   = 5,
 };
 
 // 16-byte instruction word.
 typedef struct tamd_instr {
-    uint32_t w0;   // kind | (coef or footer_len) << 8
+    uint32_t w0;   // kind | (coef, c1 or footer_len) << 8 | (accumulator or c2) << 16
     uint32_t row;  // row offset in TAMD_ROW_UNIT units (ACC/STORE); footer bytes 0..3 (FOOTER)
     uint32_t len;  // byte length (ACC/STORE);                      footer bytes 4..7 (FOOTER)
     uint32_t cap;  // zero-fill end (STORE)
@@ -43,4 +49,6 @@ typedef struct tamd_op {
     uint32_t tag;    // free for the host (stream id / level), ignored by the executor
 } tamd_op;
 
-static inline uint32_t tamd_w0(uint32_t kind, uint32_t arg) { return kind | (arg << 8); }
+static inline uint32_t tamd_w0(uint32_t kind, uint32_t arg, uint32_t arg2 = 0) {
+    return kind | (arg << 8) | (arg2 << 16);
+}

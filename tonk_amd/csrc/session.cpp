@@ -54,9 +54,9 @@ struct Stream {
 
     int enc_add(uint32_t index, uint32_t len, uint32_t* col) {
         const uint32_t hb = length_header_bytes(len);
-        const Result r = enc->add(enc_rows[index], hb + len, hb, len, nullptr, col);
+        // input rows are generated once in HBM and borrowed by the codecs (never freed)
+        const Result r = enc->add(enc_rows[index], hb + len, hb, len, nullptr, col, true);
         if (r == kSuccess) {
-            enc_rows[index] = kNoRow;  // owned by the encoder now
             alg_bytes += hb + len;
             payload_bytes += len;
         }
@@ -70,12 +70,8 @@ struct Stream {
     int enc_ack(const uint8_t* buf, uint32_t n, uint32_t* next) { return enc->acknowledge(buf, n, next); }
     int dec_add_original(uint32_t col, uint32_t index, uint32_t len) {
         const uint32_t hb = length_header_bytes(len);
-        const RowId row = dec_rows[index];
-        if (row == kNoRow) return kInvalidInput;
         bool took = false;
-        const Result r = dec->add_original(col, row, hb + len, hb, len, nullptr, &took);
-        dec_rows[index] = kNoRow;
-        if (!took) ctx->rows.free_deferred(row);
+        const Result r = dec->add_original(col, dec_rows[index], hb + len, hb, len, nullptr, &took, true);
         alg_bytes += hb + len;
         return r;
     }
