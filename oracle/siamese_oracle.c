@@ -462,12 +462,14 @@ int oracle_recovery_row(const oracle_recovery_meta* m, oracle_get_row_fn get_row
    CPU interpreter for the device program (tonk_amd/csrc/program.h).  Word layouts are
    restated here (not included) so this file stays a stand-alone checker.
    ------------------------------------------------------------------------------------------ */
-enum { I_ACC = 1, I_STORE = 2, I_FOOTER = 3, I_CLEAR = 4, I_ACC3 = 5 };
+enum { I_ACC = 1, I_STORE = 2, I_FOOTER = 3, I_CLEAR = 4, I_ACC3 = 5, I_STOREC = 6 };
 
 /* Each op owns three accumulators of `span` bytes (program.h):
      ACC   w0 = 1 | coef << 8 | a << 16       acc_a ^= coef * row[0:len]
      ACC3  w0 = 5 | c1 << 8 | c2 << 16        acc_0 ^= row, acc_1 ^= c1 * row, acc_2 ^= c2 * row
      STORE w0 = 2 | flen << 8 | a << 16       row = acc_a[0:len] || footer || zeros to cap
+     STOREC w0 = 6 | c0 << 8 | c1 << 16 | c2 << 24
+                                              row = (c0*acc_0 ^ c1*acc_1 ^ c2*acc_2)[0:len] || zeros
      CLEAR                                    all accumulators = 0 */
 int oracle_run_program(uint8_t* arena, size_t arena_bytes,
                        const uint32_t* ops, unsigned n_ops,
@@ -507,6 +509,14 @@ int oracle_run_program(uint8_t* arena, size_t arena_bytes,
                 oracle_add_mem(acc, arena + base, len);
                 oracle_muladd_mem(acc + span, c1, arena + base, len);
                 oracle_muladd_mem(acc + 2 * (size_t)span, c2, arena + base, len);
+            } else if (kind == I_STOREC) {
+                const uint8_t c[3] = { (uint8_t)(w[0] >> 8), (uint8_t)(w[0] >> 16), (uint8_t)(w[0] >> 24) };
+                const size_t base = (size_t)w[1] * 64u;
+                const uint32_t len = w[2], cap = w[3];
+                if (len > span || len > cap || base + cap > arena_bytes) { free(acc); return -9; }
+                memset(arena + base, 0, cap);
+                for (unsigned a = 0; a < 3; ++a)
+                    if (c[a]) oracle_muladd_mem(arena + base, c[a], acc + (size_t)a * span, len);
             } else if (kind == I_STORE) {
                 if (k + 1 >= count) { free(acc); return -4; }
                 const uint32_t* f = w + 4;

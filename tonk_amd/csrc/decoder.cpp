@@ -919,16 +919,16 @@ bool Decoder::eliminate_original_data() {
             }
             sum_column_count_ = m.SumCount;
 
+            const uint8_t rx = row_value(m.Row);
             for (unsigned l = 0; l < kLanes; ++l) {
                 const unsigned op = row_opcode(l, m.Row);
                 if (!op) continue;
                 LaneSums& c = get_lane(l, ee);
                 const uint32_t n = c.bytes < rbytes ? c.bytes : rbytes;
                 if (!n) continue;
-                for (unsigned s = 0; s < kSums; ++s)
-                    if (op & (1u << s)) c.read(ctx_->rows, ctx_->ex, buf, s, n, 1);
-                for (unsigned s = 0; s < kSums; ++s)
-                    if (op & (1u << (s + 3))) c.read(ctx_->rows, ctx_->ex, prod, s, n, 1);
+                uint8_t k[3];
+                opcode_coefs(op, rx, k);  // sums and RX * product sums in one read
+                c.read(ctx_->rows, ctx_->ex, buf, k, n);
             }
             Pcg32 prng;
             prng.seed(m.Row, m.LDPCCount);

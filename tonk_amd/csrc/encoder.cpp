@@ -466,17 +466,19 @@ Result Encoder::generate_cauchy(RecoveryOut& out) {
 }
 
 // Encoder::AddDenseColumns (SiameseEncoder.cpp:1046-1098)
-void Encoder::add_dense(uint32_t row, uint32_t recovery_bytes, Sym& rec, Sym& prod) {
+// The product half (opcode bits 3..5) is folded in with its RX factor right here: both halves
+// are clipped to the same length, so rec + RX * prod reads each lane once.
+void Encoder::add_dense(uint32_t row, uint32_t recovery_bytes, Sym& rec) {
+    const uint8_t rx = row_value(row);
     for (unsigned l = 0; l < kLanes; ++l) {
         const unsigned op = row_opcode(l, row);
         if (!op) continue;
         LaneSums& c = get_lane(l, count_);
         const uint32_t n = c.bytes < recovery_bytes ? c.bytes : recovery_bytes;
         if (!n) continue;
-        for (unsigned s = 0; s < kSums; ++s)
-            if (op & (1u << s)) c.read(ctx_->rows, ctx_->ex, rec, s, n, 1);
-        for (unsigned s = 0; s < kSums; ++s)
-            if (op & (1u << (s + 3))) c.read(ctx_->rows, ctx_->ex, prod, s, n, 1);
+        uint8_t k[3];
+        opcode_coefs(op, rx, k);
+        c.read(ctx_->rows, ctx_->ex, rec, k, n);
     }
     sum_end_ = count_;
 }
@@ -522,7 +524,7 @@ Result Encoder::encode(RecoveryOut& out) {
 
     const uint32_t recovery_bytes = longest_;
     Sym rec, prod;
-    add_dense(row, recovery_bytes, rec, prod);
+    add_dense(row, recovery_bytes, rec);
     add_light(row, rec, prod);
     sym_add(rec, prod, recovery_bytes, row_value(row));
 

@@ -156,6 +156,19 @@ static void push_store(std::vector<tamd_instr>& v, uint32_t off, uint32_t len, u
     v.push_back(f);
 }
 
+void ProgramBuilder::op_storec(RowId dst, uint32_t len, const uint8_t* c) {
+    const uint32_t cap = rows_->cap_bytes(dst);
+    tamd_instr s;
+    s.w0 = TAMD_I_STOREC | ((uint32_t)c[0] << 8) | ((uint32_t)c[1] << 16) | ((uint32_t)c[2] << 24);
+    s.row = rows_->offset(dst);
+    s.len = len;
+    s.cap = cap;
+    instrs_.push_back(s);
+    if (cap > cur_span_) cur_span_ = cap;
+    written_.push_back(dst);
+    store_bytes_ += len;
+}
+
 void ProgramBuilder::op_store(RowId dst, uint32_t len, uint32_t acc) {
     const uint32_t cap = rows_->cap_bytes(dst);
     push_store(instrs_, rows_->offset(dst), len, cap, nullptr, 0, acc);
@@ -203,20 +216,47 @@ uint32_t ProgramBuilder::combine(RowId dst, const Term* terms, size_t n, uint32_
 // Term lists
 // ---------------------------------------------------------------------------------------------
 void sym_merge(Sym& s) {
-    if (s.size() < 2) return;
+    const size_t n = s.size();
+    if (n < 2) return;
     TAMD_PROF_SCOPE(kSymMerge);
-    std::sort(s.begin(), s.end(), [](const Term& a, const Term& b) {
-        return a.row != b.row ? a.row < b.row : a.len < b.len;
-    });
     size_t k = 0;
-    for (size_t i = 0; i < s.size();) {
-        Term t = s[i];
-        size_t j = i + 1;
-        while (j < s.size() && s[j].row == t.row && s[j].len == t.len) { t.coef ^= s[j].coef; ++j; }
-        if (t.coef) s[k++] = t;
-        i = j;
+    if (n <= 16) {
+        for (size_t i = 0; i < n; ++i) {
+            const Term t = s[i];
+            size_t j = 0;
+            while (j < k && (s[j].row != t.row || s[j].len != t.len)) ++j;
+            if (j < k) s[j].coef ^= t.coef;
+            else s[k++] = t;
+        }
+    } else {
+        // open addressing on the row id; slots hold output positions (< the input position)
+        thread_local std::vector<int32_t> tab;
+        size_t cap = 32;
+        while (cap < 2 * n) cap *= 2;
+        tab.assign(cap, -1);
+        const size_t mask = cap - 1;
+        for (size_t i = 0; i < n; ++i) {
+            const Term t = s[i];
+            size_t h = ((size_t)t.row * 0x9E3779B1u) >> 7 & mask;
+            for (;;) {
+                const int32_t at = tab[h];
+                if (at < 0) {
+                    tab[h] = (int32_t)k;
+                    s[k++] = t;
+                    break;
+                }
+                if (s[at].row == t.row && s[at].len == t.len) {
+                    s[at].coef ^= t.coef;
+                    break;
+                }
+                h = (h + 1) & mask;
+            }
+        }
     }
-    s.resize(k);
+    size_t m = 0;
+    for (size_t i = 0; i < k; ++i)
+        if (s[i].coef) s[m++] = s[i];
+    s.resize(m);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -273,27 +313,33 @@ void LaneSums::accumulate(RowTable& rows, RowId row, uint32_t len, uint8_t cx) {
     else dyn_.push_back(T{row, len, cx});
 }
 
-void LaneSums::read(RowTable& rows, const ExpansionTable& ex, Sym& out, unsigned s, uint32_t limit, uint8_t coef) {
-    if (!coef || !limit) return;
+static inline bool same_coefs(const uint8_t* a, const uint8_t* b) {
+    return a[0] == b[0] && a[1] == b[1] && a[2] == b[2];
+}
+
+void LaneSums::read(RowTable& rows, const ExpansionTable& ex, Sym& out, const uint8_t* c, uint32_t limit) {
+    if (!limit || (!c[0] && !c[1] && !c[2])) return;
     const uint32_t clip = content_ < limit ? content_ : limit;
     if (!terms_.empty()) {
         const uint32_t at = (uint32_t)terms_.size();
         RowId snap = kNoRow;
         for (size_t i = snaps_.size(); i-- > 0 && snaps_[i].after == at;)
-            if (snaps_[i].sum == s) { snap = snaps_[i].row; break; }
+            if (same_coefs(snaps_[i].c, c)) { snap = snaps_[i].row; break; }
         if (snap == kNoRow) {
             snap = rows.alloc(content_);
             if (snap == kNoRow) return;  // caller checks arena exhaustion via RowTable
             rows.set_level(snap, 1);
-            snaps_.push_back(Snap{snap, at, s});
+            snaps_.push_back(Snap{snap, at, {c[0], c[1], c[2]}});
         }
-        if (clip) out.push_back(Term{snap, clip, coef});
-    } else if (base_[s] != kNoRow && clip) {
-        out.push_back(Term{base_[s], clip, coef});
+        if (clip) out.push_back(Term{snap, clip, 1});
+    } else if (clip) {
+        for (unsigned s = 0; s < 3; ++s)
+            if (base_[s] != kNoRow && c[s]) out.push_back(Term{base_[s], clip, c[s]});
     }
     for (const T& d : dyn_) {
         const uint32_t l = d.len < limit ? d.len : limit;
-        ex.append(rows, d.row, l, gf_mul(sum_coef(s, d.cx), coef), out);
+        const uint8_t k = (uint8_t)(gf_mul(c[0], 1) ^ gf_mul(c[1], d.cx) ^ gf_mul(c[2], gf_sqr(d.cx)));
+        ex.append(rows, d.row, l, k, out);
     }
 }
 
@@ -305,16 +351,18 @@ void LaneSums::emit_scan(RowTable& rows, ProgramBuilder& pb, const RowId* base, 
     size_t si = 0;
     for (size_t i = 0; i <= terms.size(); ++i) {
         while (si < snaps.size() && snaps[si].after == i) {
-            pb.op_store(snaps[si].row, rows.cap_bytes(snaps[si].row), snaps[si].sum);
+            pb.op_storec(snaps[si].row, rows.cap_bytes(snaps[si].row), snaps[si].c);
             ++si;
         }
         if (i == terms.size()) break;
         const T& t = terms[i];
         pb.op_acc3(t.row, t.cx, gf_sqr(t.cx), t.len);
     }
-    if (final_rows)
+    if (final_rows) {
+        static const uint8_t unit[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
         for (unsigned s = 0; s < 3; ++s)
-            if (final_rows[s] != kNoRow) pb.op_store(final_rows[s], rows.cap_bytes(final_rows[s]), s);
+            if (final_rows[s] != kNoRow) pb.op_storec(final_rows[s], rows.cap_bytes(final_rows[s]), unit[s]);
+    }
     pb.end_op(1);
 }
 
@@ -337,21 +385,12 @@ void LaneSums::flush(RowTable& rows, ProgramBuilder& pb, const ExpansionTable& e
     bool state_is_new = false;
     if (!terms_.empty()) {
         RowId final_rows[3] = {kNoRow, kNoRow, kNoRow};
-        const uint32_t at = (uint32_t)terms_.size();
         for (unsigned s = 0; s < 3; ++s) {
-            RowId end_snap = kNoRow;
-            for (size_t i = snaps_.size(); i-- > 0 && snaps_[i].after == at;)
-                if (snaps_[i].sum == s) { end_snap = snaps_[i].row; break; }
-            if (end_snap != kNoRow) {
-                state[s] = end_snap;
-            } else {
-                final_rows[s] = rows.alloc(content_);
-                state[s] = final_rows[s];
-            }
+            final_rows[s] = rows.alloc(content_);
+            state[s] = final_rows[s];
         }
         emit_scan(rows, pb, base_, terms_, snaps_, final_rows);
-        for (const Snap& sn : snaps_)
-            if (sn.row != state[sn.sum]) rows.free_deferred(sn.row);
+        for (const Snap& sn : snaps_) rows.free_deferred(sn.row);
         state_is_new = true;
     }
 

@@ -108,6 +108,7 @@ public:
     void op_acc(RowId src, uint8_t coef, uint32_t len, uint32_t acc = 0);
     void op_acc3(RowId src, uint8_t c1, uint8_t c2, uint32_t len);  // level-0 rows only
     void op_store(RowId dst, uint32_t len, uint32_t acc = 0);
+    void op_storec(RowId dst, uint32_t len, const uint8_t* c);  // c0*acc_0 ^ c1*acc_1 ^ c2*acc_2
     uint32_t end_op(uint32_t min_level = 1);  // returns level; rows stored get that level
 
     bool empty() const { return ops_.empty(); }
@@ -184,7 +185,9 @@ void sym_merge(Sym& s);
 // packet's column value and coef = (1, cx, cx^2) (SiameseEncoder.cpp:359-418,
 // SiameseDecoder.cpp:1538-1739).  All three sums see the same packets in the same order, so
 // the device walks them together: one ACC3 instruction per packet reads the row once and
-// updates the three accumulators, and a snapshot STOREs one accumulator when a sum is read.
+// updates the three accumulators.  Recovery rows read the sums in fixed linear combinations
+// (opcode bits select sums into the row and into the RX product), so a read is one snapshot
+// row of c0*sum_0 + c1*sum_1 + c2*sum_2, written by a STOREC in the scan.
 // ---------------------------------------------------------------------------------------------
 class ExpansionTable;  // rows produced in the pending program -> their symbolic content
 
@@ -198,8 +201,8 @@ public:
     void grow(uint32_t b) { if (b > bytes) bytes = b; }
     // sum_s ^= cx^s * data for s = 0, 1, 2 (data = row, possibly produced in the pending program)
     void accumulate(RowTable& rows, RowId row, uint32_t len, uint8_t cx);
-    // Append the current value of sum `s`, clipped to `limit` bytes and scaled by `coef`.
-    void read(RowTable& rows, const ExpansionTable& ex, Sym& out, unsigned s, uint32_t limit, uint8_t coef);
+    // Append c[0]*sum_0 + c[1]*sum_1 + c[2]*sum_2 (current values, clipped to `limit` bytes).
+    void read(RowTable& rows, const ExpansionTable& ex, Sym& out, const uint8_t* c, uint32_t limit);
     // Emit the scan (and fix-up) ops for the pending program and rebase the sums.
     void flush(RowTable& rows, ProgramBuilder& pb, const ExpansionTable& ex);
     // Drop everything (codec destruction).
@@ -207,7 +210,7 @@ public:
 
 private:
     struct T { RowId row; uint32_t len; uint8_t cx; };
-    struct Snap { RowId row; uint32_t after; uint32_t sum; };
+    struct Snap { RowId row; uint32_t after; uint8_t c[3]; };
     RowId base_[3] = {kNoRow, kNoRow, kNoRow};  // carried values from a previous flush (level 0)
     uint32_t content_ = 0;                      // bytes the accumulated content may occupy
     std::vector<T> terms_;                      // level-0 packets accumulated since base_
@@ -221,6 +224,12 @@ private:
 };
 
 inline uint8_t sum_coef(unsigned s, uint8_t cx) { return s == 0 ? 1 : (s == 1 ? cx : gf_sqr(cx)); }
+// Coefficients of the lane sums a Siamese row reads (SiameseEncoder.cpp:1046-1098): opcode bit s
+// adds sum s to the row, bit s + 3 adds it to the product that is multiplied by RX.
+inline void opcode_coefs(unsigned op, uint8_t rx, uint8_t* c) {
+    for (unsigned s = 0; s < 3; ++s)
+        c[s] = (uint8_t)(((op >> s) & 1u) ^ (((op >> (s + 3)) & 1u) ? rx : 0u));
+}
 
 // Symbolic content of rows written by the pending program, so readers in the same flush can
 // use the content's terms instead of the row itself (which would add a level).

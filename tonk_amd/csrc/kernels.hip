@@ -125,6 +125,17 @@ tamd_exec(const tamd_op* __restrict__ ops, const tamd_instr* __restrict__ instrs
                     const tamd_instr f = (j + 1 < TAMD_BATCH) ? in[j + 1 < TAMD_BATCH ? j + 1 : j] : instrs[k + j + 1];
                     const uint32_t a = (in[j].w0 >> 16) & 0xffu;
                     store_slice(arena, in[j], f, o, a == 0 ? a0 : (a == 1 ? a1 : a2));
+                } else if (kind == TAMD_I_STOREC) {
+                    const uint32_t w = in[j].w0;
+                    const uint32_t c0 = (w >> 8) & 0xffu, c1 = (w >> 16) & 0xffu, c2 = w >> 24;
+                    u64 x = 0;
+                    if (c0 == 1u) x = a0; else if (c0) x = gf_mul8(a0, c0, lds_perm);
+                    if (c1 == 1u) x ^= a1; else if (c1) x ^= gf_mul8(a1, c1, lds_perm);
+                    if (c2 == 1u) x ^= a2; else if (c2) x ^= gf_mul8(a2, c2, lds_perm);
+                    tamd_instr f;
+                    f.w0 = TAMD_I_FOOTER;
+                    f.row = f.len = f.cap = 0;
+                    store_slice(arena, in[j], f, o, x);
                 } else if (kind == TAMD_I_CLEAR) {
                     a0 = a1 = a2 = 0;
                 }

@@ -10,10 +10,13 @@
 //   STORE (row, len, footer, cap, a)   row[j] = acc_a[j]                for j < len
 //                                      row[j] = footer[j - len]         for len <= j < len + F
 //                                      row[j] = 0                       for len + F <= j < cap
+//   STOREC(row, len, cap, c0, c1, c2)  row[j] = c0*acc_0[j] ^ c1*acc_1[j] ^ c2*acc_2[j] for j < len,
+//                                      0 for len <= j < cap       (no FOOTER word follows)
 //   CLEAR                              acc_0 = acc_1 = acc_2 = 0
 //
 // An op owns three accumulators; plain combines use acc_0 only, lane running-sum scans use all
-// three (sum s of a lane accumulates cx^s * packet, one ACC3 per packet).
+// three (sum s of a lane accumulates cx^s * packet, one ACC3 per packet) and a read of a lane's
+// sums in a recovery row is one STOREC of the combination the row's opcode selects.
 //
 // Rows are addressed in 64-byte units from the arena base.  Byte positions are independent in
 // GF(2^8) arithmetic, so an op is split into byte slices that the device runs in parallel with
@@ -31,6 +34,7 @@ enum tamd_instr_kind {
     TAMD_I_FOOTER = 3,  // payload word that always follows a STORE
     TAMD_I_CLEAR  = 4,
     TAMD_I_ACC3   = 5,
+    TAMD_I_STOREC = 6,  // w0 = kind | c0 << 8 | c1 << 16 | c2 << 24
 };
 
 // 16-byte instruction word.
