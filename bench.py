@@ -151,6 +151,7 @@ def main() -> int:
         sess.step(ORIGINALS_PER_STEP)
     sess.wait()
     s0 = sess.summary()
+    h0 = sess.host_ms()
     sess.set_timing(True)
     d.barrier()
     t0 = time.perf_counter()
@@ -162,6 +163,8 @@ def main() -> int:
     sess.set_timing(False)
     kernel_ms, launches = sess.kernel_ms()
     s1 = sess.summary()
+    h1 = sess.host_ms()
+    host = {k: round((h1[k] - h0[k]) / a.steps, 4) for k in h1}
     elapsed = d.allmax(t1 - t0)
 
     payload = s1["payload_bytes"] - s0["payload_bytes"]
@@ -211,6 +214,7 @@ def main() -> int:
             "device_busy_frac": round((kernel_ms / 1e3) / (t1 - t0), 4),
         },
         "cpu_baseline": None,
+        "host_ms_per_step": host,
         "checks": {"all_recovered": ok, "recovered": fin["recovered"], "lost_originals": fin["lost_originals"],
                    "lost_recoveries": fin["lost_recoveries"]},
     }

@@ -50,6 +50,11 @@ int   tamd_session_finish(void* s);                   /* end-of-stream flush, th
 int   tamd_session_summary(void* s, uint64_t* out, unsigned n);
 void  tamd_session_set_timing(void* s, int on);       /* HIP events around every launch */
 double tamd_session_kernel_ms(void* s, uint64_t* launches);
+/* Host time split of the steps so far, milliseconds (summed over steps):
+   [0] control planes (wall, all workers)   [1] sum over workers of their own control-plane time
+   [2] program layout + staging-slot wait    [3] parallel program fill + epoch close
+   [4] upload + launch enqueue               [5] max over workers of their control-plane time */
+void  tamd_session_host_ms(void* s, double out[6]);
 /* Transcript of one stream in the oracle's text format (record mode). Returns bytes needed. */
 size_t tamd_session_transcript(void* s, uint32_t stream, char* buf, size_t cap);
 void  tamd_session_destroy(void* s);

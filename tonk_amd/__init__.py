@@ -50,6 +50,8 @@ def lib() -> ctypes.CDLL:
         L.tamd_session_set_timing.argtypes = [vp, ctypes.c_int]
         L.tamd_session_kernel_ms.restype = ctypes.c_double
         L.tamd_session_kernel_ms.argtypes = [vp, ctypes.POINTER(u64)]
+        L.tamd_session_host_ms.restype = None
+        L.tamd_session_host_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
         L.tamd_session_transcript.restype = sz
         L.tamd_session_transcript.argtypes = [vp, u32, ctypes.c_char_p, sz]
         L.tamd_session_destroy.restype = None
@@ -170,6 +172,13 @@ class Session:
         n = ctypes.c_uint64(0)
         ms = lib().tamd_session_kernel_ms(self._h, ctypes.byref(n))
         return ms, int(n.value)
+
+    HOST_PHASES = ("control_wall", "control_sum", "layout", "fill", "launch", "control_max")
+
+    def host_ms(self) -> dict:
+        out = (ctypes.c_double * 6)()
+        lib().tamd_session_host_ms(self._h, out)
+        return dict(zip(self.HOST_PHASES, [float(v) for v in out]))
 
     def transcript(self, stream: int) -> str:
         need = lib().tamd_session_transcript(self._h, stream, None, 0)

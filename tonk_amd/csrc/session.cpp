@@ -12,6 +12,7 @@
 #include "device.h"
 #include "workload.h"
 
+#include <chrono>
 #include <condition_variable>
 #include <functional>
 #include <memory>
@@ -143,6 +144,7 @@ struct Stream {
 
 struct Worker {
     size_t index = 0;
+    double busy_ms = 0;  // control-plane time of the current step
     Context ctx;
     std::vector<Stream*> streams;
 };
@@ -154,6 +156,7 @@ struct Session {
     std::vector<std::unique_ptr<Stream>> streams;
     std::vector<std::pair<uint64_t, uint64_t>> epoch_ticket;  // (epoch, ticket) awaiting release
     uint64_t last_ticket = 0, released_epoch = 0;
+    double host_ms[6] = {0, 0, 0, 0, 0, 0};
     uint32_t row_cap = 0;
     bool finished = false;
     std::string error;
@@ -236,25 +239,46 @@ struct Session {
     //   3. copy each worker's ops into the pinned staging buffer, close the worker's epoch
     //   4. (main) upload the program and launch it level by level
     void step(uint32_t originals, bool finish) {
+        typedef std::chrono::steady_clock clk;
+        auto ms = [](clk::time_point a, clk::time_point b) {
+            return std::chrono::duration<double, std::milli>(b - a).count();
+        };
+        const auto t0 = clk::now();
         const uint64_t rel = completed_epoch();
-        run_all([originals, finish, rel](Worker& w) {
+        run_all([originals, finish, rel, &ms](Worker& w) {
+            const auto w0 = clk::now();
             w.ctx.rows.release_up_to(rel);
             for (Stream* st : w.streams) {
                 if (finish) st->runner->finish();
                 else st->runner->advance(originals);
             }
             w.ctx.prepare_flush();
+            w.busy_ms = ms(w0, clk::now());
         });
+        const auto t1 = clk::now();
+        double mx = 0;
+        for (auto& w : workers) {
+            host_ms[1] += w->busy_ms;
+            if (w->busy_ms > mx) mx = w->busy_ms;
+        }
+        host_ms[5] += mx;
         std::vector<Context*> ctxs;
         for (auto& w : workers) ctxs.push_back(&w->ctx);
         dev.begin(ctxs.data(), ctxs.size());
+        const auto t2 = clk::now();
         const uint64_t epoch = workers.empty() ? 0 : workers[0]->ctx.epoch;
         Device* d = &dev;
         run_all([d](Worker& w) {
             d->fill(w.index);
             w.ctx.finish_flush();
         });
+        const auto t3 = clk::now();
         last_ticket = dev.launch();
+        const auto t4 = clk::now();
+        host_ms[0] += ms(t0, t1);
+        host_ms[2] += ms(t1, t2);
+        host_ms[3] += ms(t2, t3);
+        host_ms[4] += ms(t3, t4);
         epoch_ticket.push_back(std::make_pair(epoch, last_ticket));
         if (prm.record) resolve_transcripts();
     }
@@ -458,6 +482,11 @@ size_t tamd_session_transcript(void* sp, uint32_t stream, char* buf, size_t cap)
         buf[n] = 0;
     }
     return all.size() + 1;
+}
+
+void tamd_session_host_ms(void* sp, double out[6]) {
+    Session* s = (Session*)sp;
+    for (int i = 0; i < 6; ++i) out[i] = s->host_ms[i];
 }
 
 void tamd_session_destroy(void* sp) { delete (Session*)sp; }
