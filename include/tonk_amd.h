@@ -53,8 +53,10 @@ double tamd_session_kernel_ms(void* s, uint64_t* launches);
 /* Host time split of the steps so far, milliseconds (summed over steps):
    [0] control planes (wall, all workers)   [1] sum over workers of their own control-plane time
    [2] program layout + staging-slot wait    [3] parallel program fill + epoch close
-   [4] upload + launch enqueue               [5] max over workers of their control-plane time */
-void  tamd_session_host_ms(void* s, double out[6]);
+   [4] upload + launch enqueue               [5] max over workers of their control-plane time
+   [6] of [2]: wait for the staging slot      [7] of [4]: H2D copy enqueue
+   [8] longest single H2D enqueue             [9] staging-slot reallocations (count) */
+void  tamd_session_host_ms(void* s, double out[10]);
 /* Transcript of one stream in the oracle's text format (record mode). Returns bytes needed. */
 size_t tamd_session_transcript(void* s, uint32_t stream, char* buf, size_t cap);
 void  tamd_session_destroy(void* s);

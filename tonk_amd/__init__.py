@@ -173,10 +173,11 @@ class Session:
         ms = lib().tamd_session_kernel_ms(self._h, ctypes.byref(n))
         return ms, int(n.value)
 
-    HOST_PHASES = ("control_wall", "control_sum", "layout", "fill", "launch", "control_max")
+    HOST_PHASES = ("control_wall", "control_sum", "layout", "fill", "launch", "control_max", "slot_wait",
+                   "upload_enqueue", "upload_enqueue_max", "slot_reallocs")
 
     def host_ms(self) -> dict:
-        out = (ctypes.c_double * 6)()
+        out = (ctypes.c_double * 10)()
         lib().tamd_session_host_ms(self._h, out)
         return dict(zip(self.HOST_PHASES, [float(v) for v in out]))
 

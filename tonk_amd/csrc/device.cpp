@@ -2,6 +2,7 @@
 #include "device.h"
 
 #include <hip/hip_runtime.h>
+#include <chrono>
 #include <stdio.h>
 #include <string.h>
 
@@ -39,6 +40,7 @@ Device::~Device() {
     for (auto& p : inflight_) hipEventDestroy((hipEvent_t)p.second);
     for (void* e : free_events_) hipEventDestroy((hipEvent_t)e);
     for (auto& p : timing_events_) { hipEventDestroy((hipEvent_t)p.first); hipEventDestroy((hipEvent_t)p.second); }
+    for (void* e : timing_pool_) hipEventDestroy((hipEvent_t)e);
     if (up_host_) hipHostFree(up_host_);
     if (up_event_) hipEventDestroy((hipEvent_t)up_event_);
     if (d_gf_) hipFree(d_gf_);
@@ -79,15 +81,23 @@ bool Device::init(int device, uint64_t arena_bytes) {
     up_event_ = ue;
     up_cap_ = 4u << 20;
     HIPCHK(hipHostMalloc((void**)&up_host_, up_cap_, hipHostMallocDefault));
+    // Staging slots up front, each touched by one copy, so no step pays first-use costs.
+    for (Slot& sl : slots_) {
+        if (!ensure_slot(sl, 16u << 20)) { error_ = "program staging allocation failed"; return false; }
+        memset(sl.host, 0, 4096);
+        HIPCHK(hipMemcpyAsync(sl.dev, sl.host, 4096, hipMemcpyHostToDevice, s));
+    }
+    stats_.slot_reallocs = 0;
     HIPCHK(hipStreamSynchronize(s));
     return error_.empty();
 }
 
 bool Device::ensure_slot(Slot& s, size_t bytes) {
     if (s.cap >= bytes) return true;
+    stats_.slot_reallocs++;
     if (s.host) hipHostFree(s.host);
     if (s.dev) hipFree(s.dev);
-    size_t cap = 1u << 20;
+    size_t cap = 16u << 20;  // a bench step's program is ~8 MB: avoid reallocating mid-run
     while (cap < bytes) cap *= 2;
     s.host = nullptr;
     s.dev = nullptr;
@@ -153,7 +163,9 @@ void Device::begin(Context* const* ctxs, size_t n) {
     Slot& slot = slots_[next_slot_];
     next_slot_ ^= 1;
     if (slot.ticket) {
+        const auto w0 = std::chrono::steady_clock::now();
         HIPCHK(hipEventSynchronize((hipEvent_t)slot.done));
+        stats_.slot_wait_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
         if (slot.ticket > completed_) completed_ = slot.ticket;
         slot.ticket = 0;
     }
@@ -218,7 +230,11 @@ uint64_t Device::launch() {
     }
     hipStream_t st = (hipStream_t)stream_;
     Slot& slot = *P.slot;
+    const auto u0 = std::chrono::steady_clock::now();
     HIPCHK(hipMemcpyAsync(slot.dev, slot.host, P.total, hipMemcpyHostToDevice, st));
+    const double up_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - u0).count();
+    stats_.upload_enqueue_ms += up_ms;
+    if (up_ms > stats_.upload_enqueue_max_ms) stats_.upload_enqueue_max_ms = up_ms;
     const tamd_instr* di = (const tamd_instr*)slot.dev;
     const tamd_op* dops = (const tamd_op*)(slot.dev + P.bytes_instr);
     const uint2* ditems = (const uint2*)(slot.dev + P.bytes_instr + P.bytes_ops);
@@ -229,8 +245,8 @@ uint64_t Device::launch() {
         if (grid > kMaxGrid) grid = kMaxGrid;
         hipEvent_t e0 = nullptr, e1 = nullptr;
         if (timing_) {
-            hipEventCreate(&e0);
-            hipEventCreate(&e1);
+            e0 = (hipEvent_t)timing_event();
+            e1 = (hipEvent_t)timing_event();
             hipEventRecord(e0, st);
         }
         hipLaunchKernelGGL(tamd_exec, dim3(grid), dim3(256), 0, st, dops, di, ditems + P.item_base[l], cnt,
@@ -367,6 +383,17 @@ bool Device::gf_selftest() {
     return error_.empty();
 }
 
+void* Device::timing_event() {
+    if (!timing_pool_.empty()) {
+        void* e = timing_pool_.back();
+        timing_pool_.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    HIPCHK(hipEventCreate(&e));
+    return e;
+}
+
 void Device::collect_timing() {
     for (auto& p : timing_events_) {
         float ms = 0;
@@ -375,8 +402,8 @@ void Device::collect_timing() {
             stats_.kernel_ms += ms;
             stats_.timed_launches++;
         }
-        hipEventDestroy((hipEvent_t)p.first);
-        hipEventDestroy((hipEvent_t)p.second);
+        timing_pool_.push_back(p.first);
+        timing_pool_.push_back(p.second);
     }
     timing_events_.clear();
 }

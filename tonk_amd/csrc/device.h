@@ -16,6 +16,9 @@ struct DeviceStats {
     uint64_t upload_bytes = 0;
     uint64_t acc_bytes = 0, store_bytes = 0;  // op-trace bytes of all programs run
     double kernel_ms = 0;  // sum of tamd_exec durations (when timing is enabled)
+    double slot_wait_ms = 0, upload_enqueue_ms = 0;  // host time in begin() waits / H2D enqueue
+    double upload_enqueue_max_ms = 0;
+    uint64_t slot_reallocs = 0;
     uint64_t timed_launches = 0;
 };
 
@@ -101,6 +104,8 @@ private:
     void* up_event_ = nullptr;
     bool timing_ = false;
     std::vector<std::pair<void*, void*>> timing_events_;
+    std::vector<void*> timing_pool_;
+    void* timing_event();
     DeviceStats stats_;
     bool ensure_slot(Slot& s, size_t bytes);
 };

@@ -1,10 +1,9 @@
 // session.cpp -- batched device-resident runner (include/tonk_amd.h).
 //
-// Streams are partitioned over host worker threads.  Each worker owns one Context (a disjoint
-// range of the HBM arena and its own pending program) and the encoder/decoder/channel of its
-// streams.  A step: every worker advances its streams by N originals (control planes emit
-// symbolic ops), then the main thread merges all workers' programs into one and enqueues it
-// level by level on the device stream.  The host then starts the next step while the device
+// Every stream (encoder + decoder + lossy channel) owns one Context: a disjoint range of the
+// HBM arena and its own pending program.  A step: host threads take streams dynamically and
+// advance each by N originals (control planes emit symbolic ops), then the streams' programs are
+// merged into one and enqueued level by level on the device stream.  The host then starts the next step while the device
 // executes; rows freed during a step are reused only once that step's program has completed.
 #include "../../include/tonk_amd.h"
 
@@ -13,6 +12,8 @@
 #include "workload.h"
 
 #include <chrono>
+#include <atomic>
+#include <algorithm>
 #include <condition_variable>
 #include <functional>
 #include <memory>
@@ -142,18 +143,14 @@ struct Stream {
     std::unique_ptr<wl::Runner<Stream, Stream>> runner;
 };
 
-struct Worker {
-    size_t index = 0;
-    double busy_ms = 0;  // control-plane time of the current step
-    Context ctx;
-    std::vector<Stream*> streams;
-};
-
+// One stream = one Context (its own arena range and pending program), so host threads can take
+// streams dynamically and a stream's ops are laid out contiguously in the merged program.
 struct Session {
     tamd_session_params prm;
     Device dev;
-    std::vector<std::unique_ptr<Worker>> workers;
     std::vector<std::unique_ptr<Stream>> streams;
+    std::vector<std::unique_ptr<Context>> ctxs;     // ctxs[i] belongs to streams[i]
+    std::vector<double> busy_ms;                    // per thread, control-plane time of a step
     std::vector<std::pair<uint64_t, uint64_t>> epoch_ticket;  // (epoch, ticket) awaiting release
     uint64_t last_ticket = 0, released_epoch = 0;
     double host_ms[6] = {0, 0, 0, 0, 0, 0};
@@ -161,11 +158,13 @@ struct Session {
     bool finished = false;
     std::string error;
 
-    // worker pool
+    // thread pool: run_all(f) calls f(stream index, thread index) for every stream, streams
+    // handed out dynamically (an atomic counter) so uneven streams balance across threads
     std::vector<std::thread> threads;
     std::mutex mu;
     std::condition_variable cv_start, cv_done;
-    std::function<void(Worker&)> job;
+    std::function<void(size_t, size_t)> job;
+    std::atomic<size_t> next_item{0};
     uint64_t job_gen = 0;
     size_t job_left = 0;
     bool quit = false;
@@ -186,10 +185,18 @@ struct Session {
         }
     }
 
-    void pool_loop(size_t wi) {
+    void drain(const std::function<void(size_t, size_t)>& f, size_t ti) {
+        for (;;) {
+            const size_t i = next_item.fetch_add(1);
+            if (i >= streams.size()) break;
+            f(i, ti);
+        }
+    }
+
+    void pool_loop(size_t ti) {
         uint64_t seen = 0;
         for (;;) {
-            std::function<void(Worker&)> f;
+            std::function<void(size_t, size_t)> f;
             {
                 std::unique_lock<std::mutex> lk(mu);
                 cv_start.wait(lk, [&] { return job_gen != seen; });
@@ -197,7 +204,7 @@ struct Session {
                 if (quit) return;
                 f = job;
             }
-            f(*workers[wi]);
+            drain(f, ti);
             {
                 std::lock_guard<std::mutex> lk(mu);
                 if (--job_left == 0) cv_done.notify_all();
@@ -205,15 +212,16 @@ struct Session {
         }
     }
 
-    void run_all(const std::function<void(Worker&)>& f) {
+    void run_all(const std::function<void(size_t, size_t)>& f) {
+        next_item = 0;
         if (threads.empty()) {
-            for (auto& w : workers) f(*w);
+            drain(f, 0);
             return;
         }
         {
             std::lock_guard<std::mutex> lk(mu);
             job = f;
-            job_left = workers.size();
+            job_left = threads.size();
             ++job_gen;
         }
         cv_start.notify_all();
@@ -232,11 +240,11 @@ struct Session {
         return released_epoch;
     }
 
-    // Advance every worker's streams by `originals` (or finish them), then merge the workers'
-    // programs into one and enqueue it.  Every per-worker phase runs on the worker threads:
+    // Advance every stream by `originals` (or finish it), then merge the streams' programs into
+    // one and enqueue it.  The per-stream phases run on the pool threads:
     //   1. release rows of completed programs, run the control planes, emit the running-sum scans
     //   2. (main) lay out the merged program, wait for a free staging slot
-    //   3. copy each worker's ops into the pinned staging buffer, close the worker's epoch
+    //   3. copy each stream's ops into the pinned staging buffer, close the stream's epoch
     //   4. (main) upload the program and launch it level by level
     void step(uint32_t originals, bool finish) {
         typedef std::chrono::steady_clock clk;
@@ -245,32 +253,31 @@ struct Session {
         };
         const auto t0 = clk::now();
         const uint64_t rel = completed_epoch();
-        run_all([originals, finish, rel, &ms](Worker& w) {
+        std::fill(busy_ms.begin(), busy_ms.end(), 0.0);
+        run_all([this, originals, finish, rel, &ms](size_t i, size_t ti) {
             const auto w0 = clk::now();
-            w.ctx.rows.release_up_to(rel);
-            for (Stream* st : w.streams) {
-                if (finish) st->runner->finish();
-                else st->runner->advance(originals);
-            }
-            w.ctx.prepare_flush();
-            w.busy_ms = ms(w0, clk::now());
+            Context& c = *ctxs[i];
+            c.rows.release_up_to(rel);
+            if (finish) streams[i]->runner->finish();
+            else streams[i]->runner->advance(originals);
+            c.prepare_flush();
+            busy_ms[ti] += ms(w0, clk::now());
         });
         const auto t1 = clk::now();
         double mx = 0;
-        for (auto& w : workers) {
-            host_ms[1] += w->busy_ms;
-            if (w->busy_ms > mx) mx = w->busy_ms;
+        for (double b : busy_ms) {
+            host_ms[1] += b;
+            if (b > mx) mx = b;
         }
         host_ms[5] += mx;
-        std::vector<Context*> ctxs;
-        for (auto& w : workers) ctxs.push_back(&w->ctx);
-        dev.begin(ctxs.data(), ctxs.size());
+        std::vector<Context*> cs;
+        for (auto& c : ctxs) cs.push_back(c.get());
+        dev.begin(cs.data(), cs.size());
         const auto t2 = clk::now();
-        const uint64_t epoch = workers.empty() ? 0 : workers[0]->ctx.epoch;
-        Device* d = &dev;
-        run_all([d](Worker& w) {
-            d->fill(w.index);
-            w.ctx.finish_flush();
+        const uint64_t epoch = ctxs.empty() ? 0 : ctxs[0]->epoch;
+        run_all([this](size_t i, size_t) {
+            dev.fill(i);
+            ctxs[i]->finish_flush();
         });
         const auto t3 = clk::now();
         last_ticket = dev.launch();
@@ -285,7 +292,7 @@ struct Session {
 
     void release_all() {
         const uint64_t rel = completed_epoch();
-        run_all([rel](Worker& w) { w.ctx.rows.release_up_to(rel); });
+        run_all([this, rel](size_t i, size_t) { ctxs[i]->rows.release_up_to(rel); });
     }
 
     void resolve_transcripts() {
@@ -338,18 +345,14 @@ void* tamd_session_create(const tamd_session_params* p, char* err, size_t err_le
     if (!s->dev.gf_selftest()) return fail("device GF(256) self test failed");
 
     const uint32_t nthreads = p->n_threads ? (p->n_threads < p->n_streams ? p->n_threads : p->n_streams) : 1;
-    const uint64_t range = (s->dev.arena_bytes() / nthreads) & ~(uint64_t)(TAMD_ROW_UNIT - 1);
-    for (uint32_t t = 0; t < nthreads; ++t) {
-        std::unique_ptr<Worker> w(new Worker());
-        w->index = t;
-        w->ctx.rows.init(range, (range / TAMD_ROW_UNIT) * t);
-        s->workers.push_back(std::move(w));
-    }
+    const uint64_t range = (s->dev.arena_bytes() / p->n_streams) & ~(uint64_t)(TAMD_ROW_UNIT - 1);
     s->row_cap = ((p->payload_max + 4 + 63) / 64) * 64;
+    s->busy_ms.assign(nthreads, 0.0);
     for (uint32_t i = 0; i < p->n_streams; ++i) {
+        std::unique_ptr<Context> ctx(new Context());
+        ctx->rows.init(range, (range / TAMD_ROW_UNIT) * i);
         std::unique_ptr<Stream> st(new Stream());
-        Worker& w = *s->workers[i % nthreads];
-        st->ctx = &w.ctx;
+        st->ctx = ctx.get();
         wl::Params& q = st->p;
         q.stream_id = p->stream_base + i;
         q.n_originals = p->n_originals;
@@ -367,11 +370,11 @@ void* tamd_session_create(const tamd_session_params* p, char* err, size_t err_le
         q.flush_max = p->flush_max;
         q.seed_data = 1000 + q.stream_id;
         q.seed_loss = 2000 + q.stream_id;
-        st->enc.reset(new Encoder(&w.ctx, s->row_cap));
-        st->dec.reset(new Decoder(&w.ctx, s->row_cap));
+        st->enc.reset(new Encoder(ctx.get(), s->row_cap));
+        st->dec.reset(new Decoder(ctx.get(), s->row_cap));
         st->tr.on = p->record != 0;
-        w.streams.push_back(st.get());
         s->streams.push_back(std::move(st));
+        s->ctxs.push_back(std::move(ctx));
     }
     for (auto& sp : s->streams) sp->runner.reset(new wl::Runner<Stream, Stream>(sp->p, *sp, *sp));
     if (nthreads > 1) {
@@ -413,7 +416,7 @@ int tamd_session_generate(void* sp) {
 int tamd_session_step(void* sp, uint32_t originals) {
     Session* s = (Session*)sp;
     s->step(originals, false);
-    for (auto& w : s->workers) if (w->ctx.oom) { s->error = "arena exhausted"; return -1; }
+    for (auto& c : s->ctxs) if (c->oom) { s->error = "arena exhausted"; return -1; }
     return s->error.empty() && s->dev.error().empty() ? 0 : -1;
 }
 
@@ -484,9 +487,13 @@ size_t tamd_session_transcript(void* sp, uint32_t stream, char* buf, size_t cap)
     return all.size() + 1;
 }
 
-void tamd_session_host_ms(void* sp, double out[6]) {
+void tamd_session_host_ms(void* sp, double out[10]) {
     Session* s = (Session*)sp;
     for (int i = 0; i < 6; ++i) out[i] = s->host_ms[i];
+    out[6] = s->dev.stats().slot_wait_ms;
+    out[7] = s->dev.stats().upload_enqueue_ms;
+    out[8] = s->dev.stats().upload_enqueue_max_ms;
+    out[9] = (double)s->dev.stats().slot_reallocs;
 }
 
 void tamd_session_destroy(void* sp) { delete (Session*)sp; }
