@@ -920,6 +920,7 @@ bool Decoder::eliminate_original_data() {
             sum_column_count_ = m.SumCount;
 
             const uint8_t rx = row_value(m.Row);
+            TAMD_PROF_SCOPE(kElimSums);
             for (unsigned l = 0; l < kLanes; ++l) {
                 const unsigned op = row_opcode(l, m.Row);
                 if (!op) continue;
@@ -947,6 +948,7 @@ bool Decoder::eliminate_original_data() {
         // Fold everything already in memory into one partial row so the triangular solve and
         // any later reader in this program touch one row instead of the whole elimination.
         sym_clip(buf, rec->bytes);
+        TAMD_PROF_SCOPE(kElimFold);
         const RowId p = fold_low_levels(ctx_->rows, ctx_->pb, buf, 3, rec->bytes, row_bytes_);
         if (p != kNoRow) ctx_->temps.push_back(p);
     }

@@ -1,6 +1,7 @@
 // encoder.cpp -- Siamese encoder control plane.  Each function names the reference routine it
 // restates (SiameseEncoder.cpp line numbers); byte work becomes symbolic terms (engine.h).
 #include "encoder.h"
+#include "prof.h"
 
 #include <string.h>
 #include <time.h>
@@ -403,9 +404,11 @@ Result Encoder::get(uint32_t packet_num, const StoredOriginal** out) {
 
 // ---- recovery generation ----
 
-Result Encoder::emit(const Sym& terms_in, uint32_t len, const RecoveryMeta& meta, RecoveryOut& out) {
-    Sym terms = terms_in;
-    sym_merge(terms);
+// `terms` is consumed.  Parity and Cauchy rows name each original once (`distinct`); Siamese
+// rows can repeat a row (LDPC pairs) and are merged first.
+Result Encoder::emit(Sym& terms, uint32_t len, const RecoveryMeta& meta, RecoveryOut& out, bool distinct) {
+    TAMD_PROF_SCOPE(kEncEmit);
+    if (!distinct) sym_merge(terms);
     out.meta = meta;
     out.footer_len = put_recovery_footer(meta, out.footer);
     out.data_len = len;
@@ -425,9 +428,10 @@ Result Encoder::generate_single(RecoveryOut& out) {
     m.LDPCCount = 1;
     m.ColumnStart = o.column;
     m.Row = 0;
-    Sym t;
+    Sym& t = scratch_;
+    t.clear();
     t.push_back(Term{o.row, o.bytes, 1});
-    return emit(t, o.bytes, m, out);
+    return emit(t, o.bytes, m, out, true);
 }
 
 // Encoder::GenerateCauchyPacket (SiameseEncoder.cpp:1334-1441)
@@ -438,8 +442,8 @@ Result Encoder::generate_cauchy(RecoveryOut& out) {
     m.LDPCCount = m.SumCount;
     m.ColumnStart = to_column(first);
     uint32_t used = 0;
-    Sym t;
-    t.reserve(count_ - first);
+    Sym& t = scratch_;
+    t.clear();
 
     const uint32_t next_parity = to_element(next_parity_column_);
     if (next_parity <= first || col_delta_negative(next_parity)) {
@@ -462,7 +466,7 @@ Result Encoder::generate_cauchy(RecoveryOut& out) {
             ccol = (ccol + 1) % kCauchyMaxColumns;
         }
     }
-    return emit(t, used, m, out);
+    return emit(t, used, m, out, true);
 }
 
 // Encoder::AddDenseColumns (SiameseEncoder.cpp:1046-1098)
@@ -524,9 +528,15 @@ Result Encoder::encode(RecoveryOut& out) {
 
     const uint32_t recovery_bytes = longest_;
     Sym rec, prod;
-    add_dense(row, recovery_bytes, rec);
-    add_light(row, rec, prod);
-    sym_add(rec, prod, recovery_bytes, row_value(row));
+    {
+        TAMD_PROF_SCOPE(kEncDense);
+        add_dense(row, recovery_bytes, rec);
+    }
+    {
+        TAMD_PROF_SCOPE(kEncLight);
+        add_light(row, rec, prod);
+        sym_add(rec, prod, recovery_bytes, row_value(row));
+    }
 
     RecoveryMeta m;
     m.SumCount = sum_end_ - sum_start_ + sum_erased_;
@@ -534,7 +544,7 @@ Result Encoder::encode(RecoveryOut& out) {
     m.ColumnStart = sum_column_start_;
     m.Row = row;
     sym_clip(rec, recovery_bytes);
-    return emit(rec, recovery_bytes, m, out);
+    return emit(rec, recovery_bytes, m, out, false);
 }
 
 // Encoder::GetStatistics (SiameseEncoder.cpp:1445-1457)

@@ -134,7 +134,8 @@ private:
     Result generate_cauchy(RecoveryOut& out);
     void add_dense(uint32_t row, uint32_t recovery_bytes, Sym& rec);
     void add_light(uint32_t row, Sym& rec, Sym& prod);
-    Result emit(const Sym& terms, uint32_t len, const RecoveryMeta& meta, RecoveryOut& out);
+    Result emit(Sym& terms, uint32_t len, const RecoveryMeta& meta, RecoveryOut& out, bool distinct);
+    Sym scratch_;
 };
 
 uint64_t time_msec();

@@ -18,7 +18,10 @@ void RowTable::init(uint64_t arena_bytes, uint64_t base_units) {
     bump_ = 0;
     used_units_ = 0;
     live_ = 0;
-    meta_.clear();
+    off_.clear();
+    units_.clear();
+    level_.clear();
+    hot_.clear();
     free_handles_.clear();
     free_offsets_.assign(kSmallClasses + 1, std::vector<uint32_t>());
     free_big_.clear();
@@ -54,22 +57,25 @@ RowId RowTable::alloc(uint32_t bytes) {
         h = free_handles_.back();
         free_handles_.pop_back();
     } else {
-        h = (RowId)meta_.size();
-        meta_.push_back(Meta());
+        h = (RowId)off_.size();
+        off_.push_back(0);
+        units_.push_back(0);
+        level_.push_back(0);
+        if ((h & 63) == 0) hot_.push_back(0);
     }
-    meta_[h].off = off;
-    meta_[h].units = units;
-    meta_[h].level = 0;
+    off_[h] = off;
+    units_[h] = units;
+    hot_[h >> 6] &= ~(1ull << (h & 63));
     used_units_ += units;
     ++live_;
     return h;
 }
 
 void RowTable::release(RowId r) {
-    const Meta& m = meta_[r];
-    if (m.units <= kSmallClasses) free_offsets_[m.units].push_back(m.off);
-    else free_big_.push_back(std::make_pair(m.off, m.units));
-    used_units_ -= m.units;
+    const uint32_t units = units_[r], off = off_[r];
+    if (units <= kSmallClasses) free_offsets_[units].push_back(off);
+    else free_big_.push_back(std::make_pair(off, units));
+    used_units_ -= units;
     --live_;
     free_handles_.push_back(r);
 }
@@ -110,6 +116,31 @@ void ProgramBuilder::begin_op() {
     cur_span_ = 0;
     cur_level_in_ = 0;
     cur_written_begin_ = written_.size();
+}
+
+void ProgramBuilder::op_acc3_run(const RowId* row, size_t stride, const uint32_t* len, const uint8_t* cx, size_t n) {
+    const size_t at = instrs_.size();
+    instrs_.resize(at + n);
+    tamd_instr* w = instrs_.data() + at;
+    uint32_t span = cur_span_;
+    uint64_t acc = 0;
+    size_t k = 0;
+    for (size_t i = 0; i < n; ++i) {
+        const RowId r = *(const RowId*)((const char*)row + i * stride);
+        const uint32_t l = *(const uint32_t*)((const char*)len + i * stride);
+        const uint8_t c = *(const uint8_t*)((const char*)cx + i * stride);
+        if (!l) continue;
+        w[k].w0 = tamd_w0(TAMD_I_ACC3, c, gf_sqr(c));
+        w[k].row = rows_->offset(r);
+        w[k].len = l;
+        w[k].cap = 0;
+        ++k;
+        if (l > span) span = l;
+        acc += l;
+    }
+    instrs_.resize(at + k);
+    cur_span_ = span;
+    acc_bytes_ += acc;
 }
 
 void ProgramBuilder::op_acc3(RowId src, uint8_t c1, uint8_t c2, uint32_t len) {
@@ -202,7 +233,30 @@ uint32_t ProgramBuilder::end_op(uint32_t min_level) {
 uint32_t ProgramBuilder::combine(RowId dst, const Term* terms, size_t n, uint32_t len,
                                  const uint8_t* footer, uint32_t footer_len) {
     begin_op();
-    for (size_t i = 0; i < n; ++i) op_acc(terms[i].row, terms[i].coef, terms[i].len);
+    // inline op_acc over the term list: one resize, then straight stores
+    const size_t at = instrs_.size();
+    instrs_.resize(at + n);
+    tamd_instr* w = instrs_.data() + at;
+    uint32_t span = cur_span_, lvl = cur_level_in_;
+    uint64_t acc = 0;
+    size_t k = 0;
+    for (size_t i = 0; i < n; ++i) {
+        const Term& t = terms[i];
+        if (!t.coef || !t.len) continue;
+        w[k].w0 = tamd_w0(TAMD_I_ACC, t.coef);
+        w[k].row = rows_->offset(t.row);
+        w[k].len = t.len;
+        w[k].cap = 0;
+        ++k;
+        if (t.len > span) span = t.len;
+        const uint32_t l = rows_->level(t.row);
+        if (l > lvl) lvl = l;
+        acc += t.len;
+    }
+    instrs_.resize(at + k);
+    cur_span_ = span;
+    cur_level_in_ = lvl;
+    acc_bytes_ += acc;
     const uint32_t cap = rows_->cap_bytes(dst);
     push_store(instrs_, rows_->offset(dst), len, cap, footer, footer_len);
     if (cap > cur_span_) cur_span_ = cap;
@@ -348,15 +402,17 @@ void LaneSums::emit_scan(RowTable& rows, ProgramBuilder& pb, const RowId* base, 
     pb.begin_op();
     for (unsigned s = 0; s < 3; ++s)
         if (base[s] != kNoRow) pb.op_acc(base[s], 1, rows.cap_bytes(base[s]), s);
-    size_t si = 0;
-    for (size_t i = 0; i <= terms.size(); ++i) {
+    size_t si = 0, i = 0;
+    const size_t n = terms.size();
+    for (;;) {
         while (si < snaps.size() && snaps[si].after == i) {
             pb.op_storec(snaps[si].row, rows.cap_bytes(snaps[si].row), snaps[si].c);
             ++si;
         }
-        if (i == terms.size()) break;
-        const T& t = terms[i];
-        pb.op_acc3(t.row, t.cx, gf_sqr(t.cx), t.len);
+        if (i == n) break;
+        const size_t end = si < snaps.size() ? snaps[si].after : n;  // next snapshot point
+        pb.op_acc3_run(&terms[i].row, sizeof(T), &terms[i].len, &terms[i].cx, end - i);
+        i = end;
     }
     if (final_rows) {
         static const uint8_t unit[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};

@@ -67,16 +67,26 @@ public:
     void release_up_to(uint64_t completed_epoch);
     void seal_epoch(uint64_t epoch);  // rows freed so far belong to `epoch`
 
-    uint32_t offset(RowId r) const { return (uint32_t)(base_ + meta_[r].off); }  // 64-B units
-    uint32_t cap_bytes(RowId r) const { return meta_[r].units * TAMD_ROW_UNIT; }
-    uint32_t level(RowId r) const { return meta_[r].level; }
-    void set_level(RowId r, uint32_t l) { meta_[r].level = l; }
+    uint32_t offset(RowId r) const { return (uint32_t)(base_ + off_[r]); }  // 64-B units
+    uint32_t cap_bytes(RowId r) const { return units_[r] * TAMD_ROW_UNIT; }
+    // Only rows written by the pending program have a level; a bitmap keeps the common case
+    // (level 0) to one bit test instead of a lookup in the (large, cold) per-row tables.
+    uint32_t level(RowId r) const { return ((hot_[r >> 6] >> (r & 63)) & 1u) ? level_[r] : 0u; }
+    void set_level(RowId r, uint32_t l) {
+        if (l) {
+            hot_[r >> 6] |= 1ull << (r & 63);
+            level_[r] = l;
+        } else {
+            hot_[r >> 6] &= ~(1ull << (r & 63));
+        }
+    }
     size_t live_rows() const { return live_; }
     uint64_t bytes_in_use() const { return (uint64_t)used_units_ * TAMD_ROW_UNIT; }
 
 private:
-    struct Meta { uint32_t off, units, level, pad; };
-    std::vector<Meta> meta_;
+    // per row handle (structure of arrays: offset lookups dominate)
+    std::vector<uint32_t> off_, units_, level_;
+    std::vector<uint64_t> hot_;  // bit per handle: level > 0
     std::vector<RowId> free_handles_;
     std::vector<std::vector<uint32_t>> free_offsets_;  // by size in units (small sizes)
     std::vector<std::pair<uint32_t, uint32_t>> free_big_; // (off, units) for large rows
@@ -107,6 +117,8 @@ public:
     void begin_op();
     void op_acc(RowId src, uint8_t coef, uint32_t len, uint32_t acc = 0);
     void op_acc3(RowId src, uint8_t c1, uint8_t c2, uint32_t len);  // level-0 rows only
+    // n ACC3 (coefficients cx, cx^2) from strided arrays of row ids, lengths and cx
+    void op_acc3_run(const RowId* row, size_t stride, const uint32_t* len, const uint8_t* cx, size_t n);
     void op_store(RowId dst, uint32_t len, uint32_t acc = 0);
     void op_storec(RowId dst, uint32_t len, const uint8_t* c);  // c0*acc_0 ^ c1*acc_1 ^ c2*acc_2
     uint32_t end_op(uint32_t min_level = 1);  // returns level; rows stored get that level
