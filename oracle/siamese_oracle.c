@@ -462,7 +462,8 @@ int oracle_recovery_row(const oracle_recovery_meta* m, oracle_get_row_fn get_row
    CPU interpreter for the device program (tonk_amd/csrc/program.h).  Word layouts are
    restated here (not included) so this file stays a stand-alone checker.
    ------------------------------------------------------------------------------------------ */
-enum { I_ACC = 1, I_STORE = 2, I_FOOTER = 3, I_CLEAR = 4, I_ACC3 = 5, I_STOREC = 6 };
+enum { I_ACC = 1, I_STORE = 2, I_FOOTER = 3, I_CLEAR = 4, I_ACC3 = 5, I_STOREC = 6, I_ACCR = 7, I_RANGE = 8 };
+enum { R_LANE3 = 1, R_CAUCHY = 2, R_CONST = 3 };
 
 /* Each op owns three accumulators of `span` bytes (program.h):
      ACC   w0 = 1 | coef << 8 | a << 16       acc_a ^= coef * row[0:len]
@@ -470,7 +471,11 @@ enum { I_ACC = 1, I_STORE = 2, I_FOOTER = 3, I_CLEAR = 4, I_ACC3 = 5, I_STOREC =
      STORE w0 = 2 | flen << 8 | a << 16       row = acc_a[0:len] || footer || zeros to cap
      STOREC w0 = 6 | c0 << 8 | c1 << 16 | c2 << 24
                                               row = (c0*acc_0 ^ c1*acc_1 ^ c2*acc_2)[0:len] || zeros
-     CLEAR                                    all accumulators = 0 */
+     CLEAR                                    all accumulators = 0
+     ACCR  w0 = 7 | mode << 8 | p << 16, row0, len, count; then RANGE w0 = 8, stride, col0, cstep:
+           row_k = row0 + k*stride, col_k = (col0 + k*cstep) mod 2^22, k < count
+           LANE3: as ACC3 with cx = CX(col_k); CAUCHY: acc_0 ^= CauchyElement(p, col_k mod 64)*row_k;
+           CONST: acc_0 ^= p*row_k */
 int oracle_run_program(uint8_t* arena, size_t arena_bytes,
                        const uint32_t* ops, unsigned n_ops,
                        const uint32_t* instrs, unsigned n_instrs)
@@ -509,6 +514,32 @@ int oracle_run_program(uint8_t* arena, size_t arena_bytes,
                 oracle_add_mem(acc, arena + base, len);
                 oracle_muladd_mem(acc + span, c1, arena + base, len);
                 oracle_muladd_mem(acc + 2 * (size_t)span, c2, arena + base, len);
+            } else if (kind == I_ACCR) {
+                if (k + 1 >= count) { free(acc); return -10; }
+                const uint32_t* r = w + 4;
+                if ((r[0] & 0xff) != I_RANGE) { free(acc); return -11; }
+                const uint32_t mode = (w[0] >> 8) & 0xff, p = (w[0] >> 16) & 0xff;
+                const uint32_t len = w[2], n = w[3], stride = r[1], col0 = r[2], cstep = r[3];
+                if (len > span) { free(acc); return -12; }
+                for (uint32_t e = 0; e < n; ++e) {
+                    const size_t base = ((size_t)w[1] + (size_t)e * stride) * 64u;
+                    const unsigned col = (unsigned)(((uint64_t)col0 + (uint64_t)e * cstep) % 0x400000u);
+                    if (base + len > arena_bytes) { free(acc); return -13; }
+                    const uint8_t* row = arena + base;
+                    if (mode == R_LANE3) {
+                        const uint8_t cx = oracle_column_value(col);
+                        oracle_add_mem(acc, row, len);
+                        oracle_muladd_mem(acc + span, cx, row, len);
+                        oracle_muladd_mem(acc + 2 * (size_t)span, oracle_gf_sqr(cx), row, len);
+                    } else if (mode == R_CAUCHY) {
+                        oracle_muladd_mem(acc, oracle_cauchy_element(p, col % 64u), row, len);
+                    } else if (mode == R_CONST) {
+                        oracle_muladd_mem(acc, (uint8_t)p, row, len);
+                    } else {
+                        free(acc); return -14;
+                    }
+                }
+                ++k; /* consumed the RANGE word */
             } else if (kind == I_STOREC) {
                 const uint8_t c[3] = { (uint8_t)(w[0] >> 8), (uint8_t)(w[0] >> 16), (uint8_t)(w[0] >> 24) };
                 const size_t base = (size_t)w[1] * 64u;

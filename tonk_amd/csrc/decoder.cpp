@@ -208,7 +208,7 @@ bool Decoder::plug_sum_holes(uint32_t element_start) {
             const StoredOriginal& o = elem(e);
             if (o.bytes <= 0) return false;
             sum.sums.grow(o.bytes);
-            sum.sums.accumulate(ctx_->rows, o.row, o.bytes, column_value(column));
+            sum.sums.accumulate(ctx_->rows, o.row, o.bytes, column);
         }
     }
     recovered_columns_.clear();
@@ -254,7 +254,7 @@ LaneSums& Decoder::get_lane(uint32_t lane, uint32_t element_end) {
         const StoredOriginal& o = elem(e);
         if (o.bytes > 0) {
             sum.sums.grow(o.bytes);
-            sum.sums.accumulate(ctx_->rows, o.row, o.bytes, column_value(o.column));
+            sum.sums.accumulate(ctx_->rows, o.row, o.bytes, o.column);
         }
         e += kLanes;
     } while (e < element_end);

@@ -69,8 +69,13 @@ bool Device::init(int device, uint64_t arena_bytes) {
     HIPCHK(hipMalloc((void**)&arena_, arena_bytes_));
     HIPCHK(hipMemsetAsync(arena_, 0, arena_bytes_, s));
     if (!gf_init()) { error_ = "gf self test failed"; return false; }
-    HIPCHK(hipMalloc((void**)&d_gf_, sizeof(g_gf.perm)));
-    HIPCHK(hipMemcpy(d_gf_, g_gf.perm, sizeof(g_gf.perm), hipMemcpyHostToDevice));
+    // kernels.hip TAMD_GF_DWORDS: perm tables, inv[256], sqr[256]
+    std::vector<uint8_t> tables(sizeof(g_gf.perm) + 512);
+    memcpy(tables.data(), g_gf.perm, sizeof(g_gf.perm));
+    memcpy(tables.data() + sizeof(g_gf.perm), g_gf.inv, 256);
+    memcpy(tables.data() + sizeof(g_gf.perm) + 256, g_gf.sqr, 256);
+    HIPCHK(hipMalloc((void**)&d_gf_, tables.size()));
+    HIPCHK(hipMemcpy(d_gf_, tables.data(), tables.size(), hipMemcpyHostToDevice));
     for (Slot& sl : slots_) {
         hipEvent_t e;
         HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));

@@ -162,7 +162,7 @@ LaneSums& Encoder::get_lane(uint32_t lane_index, uint32_t element_end) {
         do {
             const StoredOriginal& o = win_[element];
             sums.grow(o.bytes);
-            sums.accumulate(ctx_->rows, o.row, o.bytes, column_value(o.column));
+            sums.accumulate(ctx_->rows, o.row, o.bytes, o.column);
             element += kLanes;
         } while (element < element_end);
         lane.next_element = element;
@@ -441,32 +441,65 @@ Result Encoder::generate_cauchy(RecoveryOut& out) {
     m.SumCount = unacked();
     m.LDPCCount = m.SumCount;
     m.ColumnStart = to_column(first);
-    uint32_t used = 0;
-    Sym& t = scratch_;
-    t.clear();
-
+    uint32_t mode, crow = 0;
     const uint32_t next_parity = to_element(next_parity_column_);
     if (next_parity <= first || col_delta_negative(next_parity)) {
         next_parity_column_ = col_add(m.ColumnStart, m.SumCount);
         m.Row = 0;
-        for (uint32_t e = first; e < count_; ++e) {
-            const StoredOriginal& o = win_[e];
-            t.push_back(Term{o.row, o.bytes, 1});
-            if (used < o.bytes) used = o.bytes;
-        }
+        mode = TAMD_R_CONST;  // parity row: every coefficient 1
     } else {
-        const uint32_t crow = next_cauchy_row_;
+        crow = next_cauchy_row_;
         m.Row = crow + 1;
         if (++next_cauchy_row_ >= kCauchyMaxRows) next_cauchy_row_ = 0;
-        uint32_t ccol = m.ColumnStart % kCauchyMaxColumns;
-        for (uint32_t e = first; e < count_; ++e) {
-            const StoredOriginal& o = win_[e];
-            t.push_back(Term{o.row, o.bytes, cauchy_element(crow, ccol)});
-            if (used < o.bytes) used = o.bytes;
-            ccol = (ccol + 1) % kCauchyMaxColumns;
+        mode = TAMD_R_CAUCHY;  // CauchyElement(crow, column mod 64)
+    }
+
+    // The window's originals in runs of equal length at a fixed row stride: one ACCR per run.
+    RowTable& rows = ctx_->rows;
+    std::vector<Run>& runs = runs_;
+    runs.clear();
+    uint32_t used = 0;
+    for (uint32_t e = first; e < count_; ++e) {
+        const StoredOriginal& o = win_[e];
+        if (used < o.bytes) used = o.bytes;
+        const uint32_t off = rows.offset(o.row);
+        const bool level0 = rows.level(o.row) == 0;
+        if (!runs.empty() && level0) {
+            Run& b = runs.back();
+            if (b.level0 && b.len == o.bytes && col_add(b.col, b.count) == o.column) {
+                if (b.count == 1 && off > b.off) {
+                    b.stride = off - b.off;
+                    b.count = 2;
+                    continue;
+                }
+                if (b.count > 1 && off == b.off + b.stride * b.count) {
+                    ++b.count;
+                    continue;
+                }
+            }
+        }
+        runs.push_back(Run{o.row, off, 0, 1, o.bytes, o.column, level0});
+    }
+
+    out.meta = m;
+    out.footer_len = put_recovery_footer(m, out.footer);
+    out.data_len = used;
+    out.row = ctx_->alloc(used + out.footer_len);
+    if (out.row == kNoRow) { disabled_ = true; return kDisabled; }
+    ProgramBuilder& pb = ctx_->pb;
+    pb.begin_op();
+    for (const Run& r : runs) {
+        if (r.count == 1) {
+            const uint8_t c = mode == TAMD_R_CONST ? 1 : cauchy_element(crow, r.col % kCauchyMaxColumns);
+            pb.op_acc(r.row, c, r.len);
+        } else {
+            pb.op_accr(mode, mode == TAMD_R_CONST ? 1 : crow, r.off, r.stride, r.count, r.len, r.col, 1);
         }
     }
-    return emit(t, used, m, out, true);
+    pb.finish_combine(out.row, used, out.footer, out.footer_len);
+    stats_[2]++;
+    stats_[3] += out.total();
+    return kSuccess;
 }
 
 // Encoder::AddDenseColumns (SiameseEncoder.cpp:1046-1098)

@@ -136,6 +136,8 @@ private:
     void add_light(uint32_t row, Sym& rec, Sym& prod);
     Result emit(Sym& terms, uint32_t len, const RecoveryMeta& meta, RecoveryOut& out, bool distinct);
     Sym scratch_;
+    struct Run { RowId row; uint32_t off, stride, count, len, col; bool level0; };
+    std::vector<Run> runs_;
 };
 
 uint64_t time_msec();

@@ -100,6 +100,8 @@ void RowTable::release_up_to(uint64_t completed) {
 // ---------------------------------------------------------------------------------------------
 // ProgramBuilder
 // ---------------------------------------------------------------------------------------------
+static void push_store(std::vector<tamd_instr>& v, uint32_t off, uint32_t len, uint32_t cap,
+                       const uint8_t* footer, uint32_t flen, uint32_t acc = 0);
 void ProgramBuilder::clear() {
     ops_.clear();
     instrs_.clear();
@@ -118,41 +120,44 @@ void ProgramBuilder::begin_op() {
     cur_written_begin_ = written_.size();
 }
 
-void ProgramBuilder::op_acc3_run(const RowId* row, size_t stride, const uint32_t* len, const uint8_t* cx, size_t n) {
-    const size_t at = instrs_.size();
-    instrs_.resize(at + n);
-    tamd_instr* w = instrs_.data() + at;
-    uint32_t span = cur_span_;
-    uint64_t acc = 0;
-    size_t k = 0;
-    for (size_t i = 0; i < n; ++i) {
-        const RowId r = *(const RowId*)((const char*)row + i * stride);
-        const uint32_t l = *(const uint32_t*)((const char*)len + i * stride);
-        const uint8_t c = *(const uint8_t*)((const char*)cx + i * stride);
-        if (!l) continue;
-        w[k].w0 = tamd_w0(TAMD_I_ACC3, c, gf_sqr(c));
-        w[k].row = rows_->offset(r);
-        w[k].len = l;
-        w[k].cap = 0;
-        ++k;
-        if (l > span) span = l;
-        acc += l;
-    }
-    instrs_.resize(at + k);
-    cur_span_ = span;
-    acc_bytes_ += acc;
-}
-
-void ProgramBuilder::op_acc3(RowId src, uint8_t c1, uint8_t c2, uint32_t len) {
+void ProgramBuilder::op_acc3_off(uint32_t off, uint8_t c1, uint8_t c2, uint32_t len) {
     if (!len) return;
     tamd_instr in;
     in.w0 = tamd_w0(TAMD_I_ACC3, c1, c2);
-    in.row = rows_->offset(src);
+    in.row = off;
     in.len = len;
     in.cap = 0;
     instrs_.push_back(in);
     if (len > cur_span_) cur_span_ = len;
     acc_bytes_ += len;
+}
+
+void ProgramBuilder::op_accr(uint32_t mode, uint32_t param, uint32_t row0, uint32_t stride, uint32_t count,
+                             uint32_t len, uint32_t col0, uint32_t cstep) {
+    if (!len || !count) return;
+    tamd_instr a, r;
+    a.w0 = tamd_w0(TAMD_I_ACCR, mode, param);
+    a.row = row0;
+    a.len = len;
+    a.cap = count;
+    r.w0 = TAMD_I_RANGE;
+    r.row = stride;
+    r.len = col0;
+    r.cap = cstep;
+    instrs_.push_back(a);
+    instrs_.push_back(r);
+    if (len > cur_span_) cur_span_ = len;
+    acc_bytes_ += (uint64_t)len * count;
+}
+
+uint32_t ProgramBuilder::finish_combine(RowId dst, uint32_t len, const uint8_t* footer, uint32_t footer_len) {
+    const uint32_t cap = rows_->cap_bytes(dst);
+    push_store(instrs_, rows_->offset(dst), len, cap, footer, footer_len);
+    if (cap > cur_span_) cur_span_ = cap;
+    if (len > cur_span_) cur_span_ = len;
+    written_.push_back(dst);
+    store_bytes_ += len + footer_len;
+    return end_op(1);
 }
 
 void ProgramBuilder::op_acc(RowId src, uint8_t coef, uint32_t len, uint32_t acc) {
@@ -170,7 +175,7 @@ void ProgramBuilder::op_acc(RowId src, uint8_t coef, uint32_t len, uint32_t acc)
 }
 
 static void push_store(std::vector<tamd_instr>& v, uint32_t off, uint32_t len, uint32_t cap,
-                       const uint8_t* footer, uint32_t flen, uint32_t acc = 0) {
+                       const uint8_t* footer, uint32_t flen, uint32_t acc) {
     tamd_instr s;
     s.w0 = tamd_w0(TAMD_I_STORE, flen, acc);
     s.row = off;
@@ -354,17 +359,39 @@ void LaneSums::reset(RowTable& rows) {
     }
     for (unsigned s = 0; s < 3; ++s) base_[s] = kNoRow;
     terms_.clear();
+    n_ = 0;
     snaps_.clear();
     dyn_.clear();
     content_ = 0;
     bytes = 0;
 }
 
-void LaneSums::accumulate(RowTable& rows, RowId row, uint32_t len, uint8_t cx) {
+void LaneSums::accumulate(RowTable& rows, RowId row, uint32_t len, uint32_t column) {
     if (!len) return;
     if (len > content_) content_ = len;
-    if (rows.level(row) == 0) terms_.push_back(T{row, len, cx});
-    else dyn_.push_back(T{row, len, cx});
+    if (rows.level(row) != 0) {
+        dyn_.push_back(T{row, len, 0, 0, 1, column});
+        return;
+    }
+    const uint32_t off = rows.offset(row);
+    if (!terms_.empty()) {
+        T& b = terms_.back();
+        if (b.len == len && (b.col + kLanes * b.count) % TAMD_COLUMN_PERIOD == column) {
+            if (b.count == 1 && off > b.off) {
+                b.stride = off - b.off;
+                b.count = 2;
+                ++n_;
+                return;
+            }
+            if (b.count > 1 && off == b.off + b.stride * b.count) {
+                ++b.count;
+                ++n_;
+                return;
+            }
+        }
+    }
+    terms_.push_back(T{row, len, off, 0, 1, column});
+    ++n_;
 }
 
 static inline bool same_coefs(const uint8_t* a, const uint8_t* b) {
@@ -375,7 +402,7 @@ void LaneSums::read(RowTable& rows, const ExpansionTable& ex, Sym& out, const ui
     if (!limit || (!c[0] && !c[1] && !c[2])) return;
     const uint32_t clip = content_ < limit ? content_ : limit;
     if (!terms_.empty()) {
-        const uint32_t at = (uint32_t)terms_.size();
+        const uint32_t at = n_;
         RowId snap = kNoRow;
         for (size_t i = snaps_.size(); i-- > 0 && snaps_[i].after == at;)
             if (same_coefs(snaps_[i].c, c)) { snap = snaps_[i].row; break; }
@@ -392,7 +419,8 @@ void LaneSums::read(RowTable& rows, const ExpansionTable& ex, Sym& out, const ui
     }
     for (const T& d : dyn_) {
         const uint32_t l = d.len < limit ? d.len : limit;
-        const uint8_t k = (uint8_t)(gf_mul(c[0], 1) ^ gf_mul(c[1], d.cx) ^ gf_mul(c[2], gf_sqr(d.cx)));
+        const uint8_t cx = column_value(d.col);
+        const uint8_t k = (uint8_t)(c[0] ^ gf_mul(c[1], cx) ^ gf_mul(c[2], gf_sqr(cx)));
         ex.append(rows, d.row, l, k, out);
     }
 }
@@ -402,18 +430,33 @@ void LaneSums::emit_scan(RowTable& rows, ProgramBuilder& pb, const RowId* base, 
     pb.begin_op();
     for (unsigned s = 0; s < 3; ++s)
         if (base[s] != kNoRow) pb.op_acc(base[s], 1, rows.cap_bytes(base[s]), s);
-    size_t si = 0, i = 0;
-    const size_t n = terms.size();
-    for (;;) {
-        while (si < snaps.size() && snaps[si].after == i) {
+    size_t si = 0;
+    uint32_t pos = 0;  // packets emitted so far
+    auto snapshots = [&]() {
+        while (si < snaps.size() && snaps[si].after == pos) {
             pb.op_storec(snaps[si].row, rows.cap_bytes(snaps[si].row), snaps[si].c);
             ++si;
         }
-        if (i == n) break;
-        const size_t end = si < snaps.size() ? snaps[si].after : n;  // next snapshot point
-        pb.op_acc3_run(&terms[i].row, sizeof(T), &terms[i].len, &terms[i].cx, end - i);
-        i = end;
+    };
+    for (const T& t : terms) {
+        uint32_t done = 0;
+        while (done < t.count) {
+            snapshots();
+            const uint32_t until = si < snaps.size() ? snaps[si].after : 0xffffffffu;
+            uint32_t take = t.count - done;
+            if (until - pos < take) take = until - pos;
+            const uint32_t col = (t.col + kLanes * done) % TAMD_COLUMN_PERIOD;
+            if (take == 1) {
+                const uint8_t cx = column_value(col);
+                pb.op_acc3_off(t.off + t.stride * done, cx, gf_sqr(cx), t.len);
+            } else {
+                pb.op_accr(TAMD_R_LANE3, 0, t.off + t.stride * done, t.stride, take, t.len, col, kLanes);
+            }
+            done += take;
+            pos += take;
+        }
     }
+    snapshots();
     if (final_rows) {
         static const uint8_t unit[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
         for (unsigned s = 0; s < 3; ++s)
@@ -455,7 +498,7 @@ void LaneSums::flush(RowTable& rows, ProgramBuilder& pb, const ExpansionTable& e
         for (unsigned s = 0; s < 3; ++s) {
             Sym t;
             if (state[s] != kNoRow) t.push_back(Term{state[s], rows.cap_bytes(state[s]), 1});
-            for (const T& d : dyn_) ex.append(rows, d.row, d.len, sum_coef(s, d.cx), t);
+            for (const T& d : dyn_) ex.append(rows, d.row, d.len, sum_coef(s, column_value(d.col)), t);
             sym_merge(t);
             const RowId carry = rows.alloc(content_);
             pb.combine(carry, t.data(), t.size(), content_);
@@ -470,6 +513,7 @@ void LaneSums::flush(RowTable& rows, ProgramBuilder& pb, const ExpansionTable& e
         }
     }
     terms_.clear();
+    n_ = 0;
     snaps_.clear();
     dyn_.clear();
 }
@@ -486,6 +530,7 @@ void LaneSums::release(RowTable& rows) {
         base_[s] = kNoRow;
     }
     terms_.clear();
+    n_ = 0;
     snaps_.clear();
     dyn_.clear();
     content_ = bytes = 0;

@@ -69,6 +69,7 @@ public:
 
     uint32_t offset(RowId r) const { return (uint32_t)(base_ + off_[r]); }  // 64-B units
     uint32_t cap_bytes(RowId r) const { return units_[r] * TAMD_ROW_UNIT; }
+    uint32_t units(RowId r) const { return units_[r]; }
     // Only rows written by the pending program have a level; a bitmap keeps the common case
     // (level 0) to one bit test instead of a lookup in the (large, cold) per-row tables.
     uint32_t level(RowId r) const { return ((hot_[r >> 6] >> (r & 63)) & 1u) ? level_[r] : 0u; }
@@ -116,9 +117,12 @@ public:
     // Raw op construction for scans: begin, add ACC/ACC3/STORE instructions, end.
     void begin_op();
     void op_acc(RowId src, uint8_t coef, uint32_t len, uint32_t acc = 0);
-    void op_acc3(RowId src, uint8_t c1, uint8_t c2, uint32_t len);  // level-0 rows only
-    // n ACC3 (coefficients cx, cx^2) from strided arrays of row ids, lengths and cx
-    void op_acc3_run(const RowId* row, size_t stride, const uint32_t* len, const uint8_t* cx, size_t n);
+    void op_acc3_off(uint32_t off, uint8_t c1, uint8_t c2, uint32_t len);  // level-0 row at `off`
+    // A strided run of level-0 rows (program.h ACCR); row0/stride in 64-B units.
+    void op_accr(uint32_t mode, uint32_t param, uint32_t row0, uint32_t stride, uint32_t count, uint32_t len,
+                 uint32_t col0, uint32_t cstep);
+    // STORE (+FOOTER) of acc_0 into dst and close the op (the tail of combine()).
+    uint32_t finish_combine(RowId dst, uint32_t len, const uint8_t* footer, uint32_t footer_len);
     void op_store(RowId dst, uint32_t len, uint32_t acc = 0);
     void op_storec(RowId dst, uint32_t len, const uint8_t* c);  // c0*acc_0 ^ c1*acc_1 ^ c2*acc_2
     uint32_t end_op(uint32_t min_level = 1);  // returns level; rows stored get that level
@@ -211,8 +215,10 @@ public:
     void reset(RowTable& rows);
     // GrowZeroPadded: only the logical length changes (data beyond is zero by construction).
     void grow(uint32_t b) { if (b > bytes) bytes = b; }
-    // sum_s ^= cx^s * data for s = 0, 1, 2 (data = row, possibly produced in the pending program)
-    void accumulate(RowTable& rows, RowId row, uint32_t len, uint8_t cx);
+    // sum_s ^= cx^s * data for s = 0, 1, 2 (data = row, possibly produced in the pending program);
+    // `column` is the packet number (cx = column_value(column)).  Consecutive lane packets whose
+    // rows sit at a fixed stride are kept as one run (one ACCR on the device).
+    void accumulate(RowTable& rows, RowId row, uint32_t len, uint32_t column);
     // Append c[0]*sum_0 + c[1]*sum_1 + c[2]*sum_2 (current values, clipped to `limit` bytes).
     void read(RowTable& rows, const ExpansionTable& ex, Sym& out, const uint8_t* c, uint32_t limit);
     // Emit the scan (and fix-up) ops for the pending program and rebase the sums.
@@ -221,8 +227,10 @@ public:
     void release(RowTable& rows);
 
 private:
-    struct T { RowId row; uint32_t len; uint8_t cx; };
-    struct Snap { RowId row; uint32_t after; uint8_t c[3]; };
+    // a run of `count` lane packets: rows off + k*stride, columns col + 8k (count 1: a single row)
+    struct T { RowId row; uint32_t len, off, stride, count, col; };
+    struct Snap { RowId row; uint32_t after; uint8_t c[3]; };  // after = packets accumulated
+    uint32_t n_ = 0;                            // packets in terms_
     RowId base_[3] = {kNoRow, kNoRow, kNoRow};  // carried values from a previous flush (level 0)
     uint32_t content_ = 0;                      // bytes the accumulated content may occupy
     std::vector<T> terms_;                      // level-0 packets accumulated since base_

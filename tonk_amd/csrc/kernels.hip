@@ -62,14 +62,58 @@ __device__ __forceinline__ void store_slice(uint8_t* __restrict__ arena, const t
     *(u64*)(arena + (size_t)in.row * TAMD_ROW_UNIT + o) = (acc & keep) | fpart;
 }
 
+#define TAMD_GF_DWORDS (256 * 8 + 64 + 64)  // perm tables, then inv[256] and sqr[256] as bytes
+
+__device__ __forceinline__ uint32_t lds_byte(const uint32_t* __restrict__ lds, uint32_t byte_index) {
+    return (lds[byte_index >> 2] >> (8u * (byte_index & 3u))) & 0xffu;
+}
+
+// ACCR: a strided run of rows (program.h).  Loads of TAMD_BATCH rows are issued together.
+__device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& r, uint32_t o,
+                                         const uint8_t* __restrict__ arena, const uint32_t* __restrict__ lds,
+                                         u64& a0, u64& a1, u64& a2) {
+    const uint32_t mode = uniform((a.w0 >> 8) & 0xffu), p = uniform((a.w0 >> 16) & 0xffu);
+    const uint32_t row0 = uniform(a.row), len = uniform(a.len), count = uniform(a.cap);
+    const uint32_t stride = uniform(r.row), col0 = uniform(r.len), cstep = uniform(r.cap);
+    const bool live = o < len;
+    const u64 tail = (o + 8u > len && live) ? byte_mask(len - o) : ~0ull;
+    const uint32_t* inv = lds + 256 * 8;  // bytes
+    for (uint32_t e = 0; e < count; e += TAMD_BATCH) {
+        u64 d[TAMD_BATCH];
+#pragma unroll
+        for (uint32_t q = 0; q < TAMD_BATCH; ++q) {
+            d[q] = 0;
+            if (live && e + q < count)
+                d[q] = *(const u64*)(arena + ((size_t)row0 + (size_t)(e + q) * stride) * TAMD_ROW_UNIT + o);
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < TAMD_BATCH; ++q) {
+            if (e + q >= count) continue;
+            const u64 x = d[q] & tail;
+            const uint32_t col = (col0 + (e + q) * cstep) & (TAMD_COLUMN_PERIOD - 1u);
+            if (mode == TAMD_R_LANE3) {
+                const uint32_t cx = 3u + (199u * col) % 253u;  // GetColumnValue (SiameseCommon.h:89-93)
+                a0 ^= x;
+                a1 ^= gf_mul8(x, cx, lds);
+                a2 ^= gf_mul8(x, lds_byte(inv, 256u + cx), lds);
+            } else if (mode == TAMD_R_CAUCHY) {
+                const uint32_t c = lds_byte(inv, ((col & 63u) ^ (p + 64u)) & 0xffu);  // CauchyElement
+                a0 ^= gf_mul8(x, c, lds);
+            } else {
+                a0 ^= p == 1u ? x : gf_mul8(x, p, lds);
+            }
+        }
+    }
+}
+
 // Ops of one level never read a row written by an op of the same level, so every ACC load of
 // a batch can be issued before the batch's STOREs: TAMD_BATCH loads in flight per wave.
 extern "C" __global__ void __launch_bounds__(256)
 tamd_exec(const tamd_op* __restrict__ ops, const tamd_instr* __restrict__ instrs,
           const uint2* __restrict__ items, uint32_t n_items, uint8_t* __restrict__ arena,
           const uint32_t* __restrict__ gf_perm) {
-    __shared__ uint32_t lds_perm[256 * 8];
-    for (uint32_t i = threadIdx.x; i < 256 * 8; i += blockDim.x) lds_perm[i] = gf_perm[i];
+    __shared__ uint32_t lds_perm[TAMD_GF_DWORDS];
+    for (uint32_t i = threadIdx.x; i < TAMD_GF_DWORDS; i += blockDim.x) lds_perm[i] = gf_perm[i];
     __syncthreads();
 
     const uint32_t lane = threadIdx.x & 63u;
@@ -82,23 +126,34 @@ tamd_exec(const tamd_op* __restrict__ ops, const tamd_instr* __restrict__ instrs
         const uint32_t o = uniform(item.y) * TAMD_SLICE_BYTES + lane * TAMD_LANE_BYTES;
         u64 a0 = 0, a1 = 0, a2 = 0;  // the op's three accumulators (program.h)
         const uint32_t first = uniform(op.first), end = uniform(op.first + op.count);
-        for (uint32_t k = first; k < end; k += TAMD_BATCH) {
+        for (uint32_t k = first; k < end;) {
             tamd_instr in[TAMD_BATCH];
             u64 v[TAMD_BATCH];
+            // A batch runs up to (not including) the next ACCR; an ACCR at the head runs alone.
+            uint32_t nb = TAMD_BATCH;
 #pragma unroll
             for (uint32_t j = 0; j < TAMD_BATCH; ++j) {
-                v[j] = 0;
                 in[j].w0 = 0;
                 if (k + j < end) {
                     in[j] = instrs[k + j];
-                    const uint32_t kind = in[j].w0 & 0xffu;
-                    if ((kind == TAMD_I_ACC || kind == TAMD_I_ACC3) && o < in[j].len)
-                        v[j] = *(const u64*)(arena + (size_t)in[j].row * TAMD_ROW_UNIT + o);
+                    if ((in[j].w0 & 0xffu) == TAMD_I_ACCR && j < nb) nb = j;
                 }
+            }
+            if (nb == 0) {
+                run_accr(in[0], in[1], o, arena, lds_perm, a0, a1, a2);  // in[1] is its RANGE word
+                k += 2;
+                continue;
             }
 #pragma unroll
             for (uint32_t j = 0; j < TAMD_BATCH; ++j) {
+                v[j] = 0;
                 const uint32_t kind = in[j].w0 & 0xffu;
+                if (j < nb && (kind == TAMD_I_ACC || kind == TAMD_I_ACC3) && o < in[j].len)
+                    v[j] = *(const u64*)(arena + (size_t)in[j].row * TAMD_ROW_UNIT + o);
+            }
+#pragma unroll
+            for (uint32_t j = 0; j < TAMD_BATCH; ++j) {
+                const uint32_t kind = j < nb ? (in[j].w0 & 0xffu) : 0u;
                 if (kind == TAMD_I_ACC) {
                     const uint32_t len = in[j].len;
                     if (o < len) {
@@ -140,6 +195,7 @@ tamd_exec(const tamd_op* __restrict__ ops, const tamd_instr* __restrict__ instrs
                     a0 = a1 = a2 = 0;
                 }
             }
+            k += nb;
         }
     }
 }

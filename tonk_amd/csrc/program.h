@@ -13,6 +13,13 @@
 //   STOREC(row, len, cap, c0, c1, c2)  row[j] = c0*acc_0[j] ^ c1*acc_1[j] ^ c2*acc_2[j] for j < len,
 //                                      0 for len <= j < cap       (no FOOTER word follows)
 //   CLEAR                              acc_0 = acc_1 = acc_2 = 0
+//   ACCR  (mode, p, row0, count, len) + RANGE (stride, col0, cstep)
+//         for k < count: row_k = row0 + k*stride (64-B units), col_k = (col0 + k*cstep) mod 2^22
+//         LANE3:  acc_0 ^= row_k, acc_1 ^= cx*row_k, acc_2 ^= cx^2*row_k, cx = 3 + (199*col_k mod 253)
+//         CAUCHY: acc_0 ^= inv((col_k mod 64) ^ (p + 64)) * row_k
+//         CONST:  acc_0 ^= p * row_k
+//         (runs of equally long packets stored at a fixed stride: the window's originals, whose
+//         rows sit in a contiguous ring in HBM, become one instruction per run)
 //
 // An op owns three accumulators; plain combines use acc_0 only, lane running-sum scans use all
 // three (sum s of a lane accumulates cx^s * packet, one ACC3 per packet) and a read of a lane's
@@ -35,7 +42,17 @@ enum tamd_instr_kind {
     TAMD_I_CLEAR  = 4,
     TAMD_I_ACC3   = 5,
     TAMD_I_STOREC = 6,  // w0 = kind | c0 << 8 | c1 << 16 | c2 << 24
+    TAMD_I_ACCR   = 7,  // w0 = kind | mode << 8 | p << 16; row = row0, len, cap = count
+    TAMD_I_RANGE  = 8,  // payload word after ACCR: row = stride (units), len = col0, cap = cstep
 };
+
+enum tamd_range_mode {
+    TAMD_R_LANE3  = 1,
+    TAMD_R_CAUCHY = 2,
+    TAMD_R_CONST  = 3,
+};
+
+#define TAMD_COLUMN_PERIOD 0x400000u  /* packet numbers are 22-bit (SiameseCommon.h:105) */
 
 // 16-byte instruction word.
 typedef struct tamd_instr {

@@ -392,11 +392,12 @@ int tamd_session_generate(void* sp) {
         const uint32_t n = st.p.n_originals;
         st.enc_rows.assign(n, kNoRow);
         st.dec_rows.assign(n, kNoRow);
-        for (uint32_t i = 0; i < n; ++i) {
-            const uint32_t len = wl::payload_length(st.p, i);
-            const uint32_t framed = length_header_bytes(len) + len;
-            for (int side = 0; side < 2; ++side) {
-                const RowId r = st.ctx->alloc(framed);
+        // Each side's inputs are an array of equal slots (row_cap bytes) in packet order, so runs of
+        // a window's packets sit at a fixed stride (one ACCR instruction per run).
+        for (int side = 0; side < 2; ++side) {
+            for (uint32_t i = 0; i < n; ++i) {
+                const uint32_t len = wl::payload_length(st.p, i);
+                const RowId r = st.ctx->alloc(s->row_cap);
                 if (r == kNoRow) { s->error = "arena too small for the session inputs"; return -1; }
                 (side ? st.dec_rows : st.enc_rows)[i] = r;
                 Device::GenDesc g;
