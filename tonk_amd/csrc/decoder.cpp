@@ -176,6 +176,7 @@ Result Decoder::add_original(uint32_t packet_num, RowId row, uint32_t framed_byt
     }
     drop_original(o);
     o.row = row;
+    o.off = ctx_->rows.offset(row);
     o.bytes = framed_bytes;
     o.column = packet_num;
     o.header_bytes = (uint8_t)header_bytes;
@@ -254,7 +255,8 @@ LaneSums& Decoder::get_lane(uint32_t lane, uint32_t element_end) {
         const StoredOriginal& o = elem(e);
         if (o.bytes > 0) {
             sum.sums.grow(o.bytes);
-            sum.sums.accumulate(ctx_->rows, o.row, o.bytes, o.column);
+            if (ctx_->rows.level(o.row) == 0) sum.sums.accumulate_level0(o.row, o.off, o.bytes, o.column);
+            else sum.sums.accumulate(ctx_->rows, o.row, o.bytes, o.column);
         }
         e += kLanes;
     } while (e < element_end);
@@ -741,6 +743,7 @@ bool Decoder::add_single_recovery(RowId row, uint32_t data_bytes, const uint8_t*
     }
     drop_original(o);
     o.row = row;
+    o.off = ctx_->rows.offset(row);
     o.bytes = data_bytes;
     o.column = m.ColumnStart;
     o.header_bytes = (uint8_t)header;
@@ -1001,6 +1004,7 @@ Result Decoder::back_substitution() {
 
         drop_original(*o);
         o->row = out_row;
+        o->off = ctx_->rows.offset(out_row);
         o->bytes = bytes;
         o->column = mcols_[ci].column;
         o->header_bytes = 0;

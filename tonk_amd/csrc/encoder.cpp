@@ -61,11 +61,12 @@ Result Encoder::add(RowId row, uint32_t framed_bytes, uint32_t header_bytes, uin
     while (win_.size() < element) win_.push_back(StoredOriginal());
     StoredOriginal o;
     o.row = row;
+    o.off = ctx_->rows.offset(row);
     o.bytes = framed_bytes;
     o.column = column;
     o.header_bytes = (uint8_t)header_bytes;
     o.owned = borrowed ? 0 : 1;
-    o.send_msec = (uint32_t)time_msec();
+    o.send_msec = clock_ ? *clock_ : (uint32_t)time_msec();
     o.host = host;
     if (win_.size() == element) win_.push_back(o);
     else { drop_original(win_[element]); win_[element] = o; }
@@ -162,7 +163,7 @@ LaneSums& Encoder::get_lane(uint32_t lane_index, uint32_t element_end) {
         do {
             const StoredOriginal& o = win_[element];
             sums.grow(o.bytes);
-            sums.accumulate(ctx_->rows, o.row, o.bytes, o.column);
+            sums.accumulate_level0(o.row, o.off, o.bytes, o.column);
             element += kLanes;
         } while (element < element_end);
         lane.next_element = element;
@@ -454,31 +455,29 @@ Result Encoder::generate_cauchy(RecoveryOut& out) {
         mode = TAMD_R_CAUCHY;  // CauchyElement(crow, column mod 64)
     }
 
-    // The window's originals in runs of equal length at a fixed row stride: one ACCR per run.
-    RowTable& rows = ctx_->rows;
+    // The window's originals (level-0 rows) in runs of equal length at a fixed row stride:
+    // one ACCR per run.
     std::vector<Run>& runs = runs_;
     runs.clear();
     uint32_t used = 0;
     for (uint32_t e = first; e < count_; ++e) {
         const StoredOriginal& o = win_[e];
         if (used < o.bytes) used = o.bytes;
-        const uint32_t off = rows.offset(o.row);
-        const bool level0 = rows.level(o.row) == 0;
-        if (!runs.empty() && level0) {
+        if (!runs.empty()) {
             Run& b = runs.back();
-            if (b.level0 && b.len == o.bytes && col_add(b.col, b.count) == o.column) {
-                if (b.count == 1 && off > b.off) {
-                    b.stride = off - b.off;
+            if (b.len == o.bytes && col_add(b.col, b.count) == o.column) {
+                if (b.count == 1 && o.off > b.off) {
+                    b.stride = o.off - b.off;
                     b.count = 2;
                     continue;
                 }
-                if (b.count > 1 && off == b.off + b.stride * b.count) {
+                if (b.count > 1 && o.off == b.off + b.stride * b.count) {
                     ++b.count;
                     continue;
                 }
             }
         }
-        runs.push_back(Run{o.row, off, 0, 1, o.bytes, o.column, level0});
+        runs.push_back(Run{o.row, o.off, 0, 1, o.bytes, o.column});
     }
 
     out.meta = m;

@@ -36,6 +36,7 @@ struct StoredOriginal {
     uint32_t bytes = 0;         // framed bytes (Buffer.Bytes)
     uint32_t column = 0;
     uint32_t send_msec = 0;     // encoder only (retransmit timing)
+    uint32_t off = 0;           // arena offset of `row` (64-B units), cached for program emission
     uint8_t header_bytes = 0;
     uint8_t owned = 0;          // the codec frees `row` when the packet leaves the window
     void* host = nullptr;       // optional host mirror (C-ABI: siamese_encoder_get/retransmit)
@@ -50,7 +51,8 @@ public:
 
     unsigned remaining_slots() const { return kMaxPackets - count_; }
 
-    // siamese_encoder_add: the caller provides the framed row already written to the arena.
+    // siamese_encoder_add: the caller provides the framed row already written to the arena
+    // (a level-0 row: not produced by the pending program).
     // Ownership of `row` (and `host`) passes to the encoder on success unless `borrowed`: a
     // borrowed row stays the caller's (device-resident inputs that outlive the codec).
     Result add(RowId row, uint32_t framed_bytes, uint32_t header_bytes, uint32_t payload_bytes,
@@ -63,6 +65,9 @@ public:
     // ctx->rows.free_deferred once nothing reads it).
     Result encode(RecoveryOut& out);
     void stats(uint64_t* out, unsigned n);
+    // Millisecond clock for packet send times (RTO/retransmit only).  Default: the monotonic
+    // clock read per packet (GetTimeMsec); a batch driver may point it at a per-step value.
+    void set_clock(const uint32_t* msec) { clock_ = msec; }
 
     bool disabled() const { return disabled_; }
     uint64_t stat(unsigned i) const { return stats_[i]; }
@@ -78,6 +83,7 @@ private:
     void* user_;
     uint64_t stats_[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     bool disabled_ = false;
+    const uint32_t* clock_ = nullptr;
 
     // ---- EncoderPacketWindow (SiameseEncoder.h:104-232) ----
     Ring<StoredOriginal> win_;
@@ -136,7 +142,7 @@ private:
     void add_light(uint32_t row, Sym& rec, Sym& prod);
     Result emit(Sym& terms, uint32_t len, const RecoveryMeta& meta, RecoveryOut& out, bool distinct);
     Sym scratch_;
-    struct Run { RowId row; uint32_t off, stride, count, len, col; bool level0; };
+    struct Run { RowId row; uint32_t off, stride, count, len, col; };
     std::vector<Run> runs_;
 };
 

@@ -366,34 +366,6 @@ void LaneSums::reset(RowTable& rows) {
     bytes = 0;
 }
 
-void LaneSums::accumulate(RowTable& rows, RowId row, uint32_t len, uint32_t column) {
-    if (!len) return;
-    if (len > content_) content_ = len;
-    if (rows.level(row) != 0) {
-        dyn_.push_back(T{row, len, 0, 0, 1, column});
-        return;
-    }
-    const uint32_t off = rows.offset(row);
-    if (!terms_.empty()) {
-        T& b = terms_.back();
-        if (b.len == len && (b.col + kLanes * b.count) % TAMD_COLUMN_PERIOD == column) {
-            if (b.count == 1 && off > b.off) {
-                b.stride = off - b.off;
-                b.count = 2;
-                ++n_;
-                return;
-            }
-            if (b.count > 1 && off == b.off + b.stride * b.count) {
-                ++b.count;
-                ++n_;
-                return;
-            }
-        }
-    }
-    terms_.push_back(T{row, len, off, 0, 1, column});
-    ++n_;
-}
-
 static inline bool same_coefs(const uint8_t* a, const uint8_t* b) {
     return a[0] == b[0] && a[1] == b[1] && a[2] == b[2];
 }

@@ -218,7 +218,38 @@ public:
     // sum_s ^= cx^s * data for s = 0, 1, 2 (data = row, possibly produced in the pending program);
     // `column` is the packet number (cx = column_value(column)).  Consecutive lane packets whose
     // rows sit at a fixed stride are kept as one run (one ACCR on the device).
-    void accumulate(RowTable& rows, RowId row, uint32_t len, uint32_t column);
+    void accumulate(RowTable& rows, RowId row, uint32_t len, uint32_t column) {
+        if (!len) return;
+        if (rows.level(row) != 0) {
+            if (len > content_) content_ = len;
+            dyn_.push_back(T{row, len, 0, 0, 1, column});
+            return;
+        }
+        accumulate_level0(row, rows.offset(row), len, column);
+    }
+    // The same for a row known to be in memory already, at arena offset `off`.
+    void accumulate_level0(RowId row, uint32_t off, uint32_t len, uint32_t column) {
+        if (!len) return;
+        if (len > content_) content_ = len;
+        if (!terms_.empty()) {
+            T& b = terms_.back();
+            if (b.len == len && (b.col + 8u * b.count) % TAMD_COLUMN_PERIOD == column) {
+                if (b.count == 1 && off > b.off) {
+                    b.stride = off - b.off;
+                    b.count = 2;
+                    ++n_;
+                    return;
+                }
+                if (b.count > 1 && off == b.off + b.stride * b.count) {
+                    ++b.count;
+                    ++n_;
+                    return;
+                }
+            }
+        }
+        terms_.push_back(T{row, len, off, 0, 1, column});
+        ++n_;
+    }
     // Append c[0]*sum_0 + c[1]*sum_1 + c[2]*sum_2 (current values, clipped to `limit` bytes).
     void read(RowTable& rows, const ExpansionTable& ex, Sym& out, const uint8_t* c, uint32_t limit);
     // Emit the scan (and fix-up) ops for the pending program and rebase the sums.

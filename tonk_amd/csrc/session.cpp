@@ -154,6 +154,7 @@ struct Session {
     std::vector<std::pair<uint64_t, uint64_t>> epoch_ticket;  // (epoch, ticket) awaiting release
     uint64_t last_ticket = 0, released_epoch = 0;
     double host_ms[6] = {0, 0, 0, 0, 0, 0};
+    uint32_t clock_msec = 0;  // packet send times of a step (RTO bookkeeping only)
     uint32_t row_cap = 0;
     bool finished = false;
     std::string error;
@@ -252,6 +253,7 @@ struct Session {
             return std::chrono::duration<double, std::milli>(b - a).count();
         };
         const auto t0 = clk::now();
+        clock_msec = (uint32_t)time_msec();
         const uint64_t rel = completed_epoch();
         std::fill(busy_ms.begin(), busy_ms.end(), 0.0);
         run_all([this, originals, finish, rel, &ms](size_t i, size_t ti) {
@@ -371,6 +373,7 @@ void* tamd_session_create(const tamd_session_params* p, char* err, size_t err_le
         q.seed_data = 1000 + q.stream_id;
         q.seed_loss = 2000 + q.stream_id;
         st->enc.reset(new Encoder(ctx.get(), s->row_cap));
+        st->enc->set_clock(&s->clock_msec);
         st->dec.reset(new Decoder(ctx.get(), s->row_cap));
         st->tr.on = p->record != 0;
         s->streams.push_back(std::move(st));

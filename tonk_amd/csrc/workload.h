@@ -132,6 +132,7 @@ class Runner {
 public:
     Runner(const Params& p, Backend& be, Transcript& tr) : p_(p), be_(be), tr_(tr) {
         ch_.init(p_);
+        ack_countdown_ = p_.ack_every;
         have_.assign(p_.n_originals, 0);
         col_of_.assign(p_.n_originals, 0);
     }
@@ -171,6 +172,7 @@ private:
     std::vector<uint32_t> col_of_, pending_arq_;
     size_t arq_head_ = 0;
     uint32_t tokens_ = 0, next_ = 0;
+    uint32_t ack_countdown_ = 0;  // originals until the next acknowledgement
     std::vector<uint32_t> nums_;
 
     void decode_loop() {
@@ -227,7 +229,8 @@ private:
             send_recovery(true);
         }
 
-        if (p_.ack_every && (i + 1) % p_.ack_every == 0) {
+        if (p_.ack_every && --ack_countdown_ == 0) {
+            ack_countdown_ = p_.ack_every;
             uint8_t buf[2048];
             const uint32_t limit = p_.ack_bytes < sizeof(buf) ? p_.ack_bytes : (uint32_t)sizeof(buf);
             uint32_t used = 0;
