@@ -8,6 +8,9 @@
 #include "../../tonk_amd/csrc/prof.h"
 
 #include <chrono>
+#include <signal.h>
+#include <sys/time.h>
+#include <ucontext.h>
 #include <memory>
 #include <stdio.h>
 #include <stdlib.h>
@@ -23,7 +26,7 @@ thread_local uint64_t calls[kSlots];
 const char* const names[kSlots] = {"enc_add", "enc_encode", "enc_ack", "dec_add_orig", "dec_add_rec", "dec_decode",
     "dec_ack", "dec_is_ready", "gen_matrix", "ge", "elim", "lower_tri", "back_sub", "chain_flush", "sym_merge",
     "prepare_flush", "finish_flush", "release", "enc_dense", "enc_light", "enc_emit", "elim_sums", "elim_pairs",
-    "elim_fold"};
+    "elim_fold", "enc_cauchy", "enc_remove"};
 } }
 #endif
 
@@ -81,7 +84,22 @@ struct NoTr {
     void on_stats(const uint64_t*, const uint64_t*) {}
 };
 
+// Poor man's sampling profiler (no perf in the container): SIGPROF every 100 us of CPU time
+// records the interrupted PC; `sample=FILE` writes them for addr2line.
+static uint64_t g_samples[1 << 20];
+static volatile size_t g_nsamples = 0;
+static void on_prof(int, siginfo_t*, void* uc) {
+    const size_t n = g_nsamples;
+    if (n < (1u << 20)) {
+        g_samples[n] = (uint64_t)((ucontext_t*)uc)->uc_mcontext.gregs[REG_RIP];
+        g_nsamples = n + 1;
+    }
+}
+
 int main(int argc, char** argv) {
+    const char* sample_out = nullptr;
+    for (int i = 1; i < argc; ++i)
+        if (!strncmp(argv[i], "sample=", 7)) sample_out = argv[i] + 7;
     gf_init();
     wl::Params p;
     p.loss_thresh = 42949673;
@@ -93,6 +111,7 @@ int main(int argc, char** argv) {
         const char* eq = strchr(argv[i], '=');
         if (!eq) continue;
         std::string k(argv[i], eq - argv[i]);
+        if (k == "sample") continue;
         const unsigned long long v = strtoull(eq + 1, nullptr, 0);
         if (k == "streams") streams = (uint32_t)v;
         else if (k == "n") p.n_originals = (uint32_t)v;
@@ -125,6 +144,18 @@ int main(int argc, char** argv) {
         run[s].reset(new wl::Runner<Null, NoTr>(ps[s], *be[s], tr));
     }
     uint64_t instrs = 0, ops = 0;
+    if (sample_out) {
+        struct sigaction sa;
+        memset(&sa, 0, sizeof(sa));
+        sa.sa_sigaction = on_prof;
+        sa.sa_flags = SA_SIGINFO | SA_RESTART;
+        sigaction(SIGPROF, &sa, nullptr);
+        itimerval tv;
+        tv.it_interval.tv_sec = 0;
+        tv.it_interval.tv_usec = 100;
+        tv.it_value = tv.it_interval;
+        setitimer(ITIMER_PROF, &tv, nullptr);
+    }
     const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t done = 0; done < p.n_originals; done += step) {
         for (uint32_t s = 0; s < streams; ++s) run[s]->advance(step);
@@ -145,6 +176,14 @@ int main(int argc, char** argv) {
         }
     }
     const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    if (sample_out) {
+        itimerval off;
+        memset(&off, 0, sizeof(off));
+        setitimer(ITIMER_PROF, &off, nullptr);
+        FILE* f = fopen(sample_out, "w");
+        for (size_t i = 0; i < g_nsamples; ++i) fprintf(f, "%llx\n", (unsigned long long)g_samples[i]);
+        fclose(f);
+    }
     const double n = (double)streams * p.n_originals;
     printf("{\"ns_per_original\": %.1f, \"instrs_per_original\": %.2f, \"ops_per_original\": %.3f, \"seconds\": %.3f}\n",
            sec * 1e9 / n, instrs / n, ops / n, sec);

@@ -68,6 +68,15 @@ Result Encoder::add(RowId row, uint32_t framed_bytes, uint32_t header_bytes, uin
     o.owned = borrowed ? 0 : 1;
     o.send_msec = clock_ ? *clock_ : (uint32_t)time_msec();
     o.host = host;
+    o.run = 1;
+    if (element > 0) {
+        const StoredOriginal& p = win_[element - 1];
+        if (p.bytes == framed_bytes && o.off > p.off && p.run < 0xffff &&
+            (p.run == 1 || o.off - p.off == p.stride)) {
+            o.run = (uint16_t)(p.run + 1);
+            o.stride = o.off - p.off;
+        }
+    }
     if (win_.size() == element) win_.push_back(o);
     else { drop_original(win_[element]); win_[element] = o; }
 
@@ -122,6 +131,7 @@ void Encoder::reset_sums(uint32_t element_start) {
 
 // EncoderPacketWindow::RemoveElements (SiameseEncoder.cpp:239-357)
 void Encoder::remove_elements() {
+    TAMD_PROF_SCOPE(kEncRemove);
     const uint32_t first_kept_sub = first_unremoved_ / kSubwindow;
     const uint32_t removed = first_kept_sub * kSubwindow;
 
@@ -437,6 +447,7 @@ Result Encoder::generate_single(RecoveryOut& out) {
 
 // Encoder::GenerateCauchyPacket (SiameseEncoder.cpp:1334-1441)
 Result Encoder::generate_cauchy(RecoveryOut& out) {
+    TAMD_PROF_SCOPE(kEncCauchy);
     const uint32_t first = first_unremoved_;
     RecoveryMeta m;
     m.SumCount = unacked();
@@ -455,29 +466,19 @@ Result Encoder::generate_cauchy(RecoveryOut& out) {
         mode = TAMD_R_CAUCHY;  // CauchyElement(crow, column mod 64)
     }
 
-    // The window's originals (level-0 rows) in runs of equal length at a fixed row stride:
-    // one ACCR per run.
+    // The window's originals (level-0 rows) in runs of equal length at a fixed row stride,
+    // tracked at add time: one ACCR per run, found by walking the window back run by run.
     std::vector<Run>& runs = runs_;
     runs.clear();
     uint32_t used = 0;
-    for (uint32_t e = first; e < count_; ++e) {
-        const StoredOriginal& o = win_[e];
-        if (used < o.bytes) used = o.bytes;
-        if (!runs.empty()) {
-            Run& b = runs.back();
-            if (b.len == o.bytes && col_add(b.col, b.count) == o.column) {
-                if (b.count == 1 && o.off > b.off) {
-                    b.stride = o.off - b.off;
-                    b.count = 2;
-                    continue;
-                }
-                if (b.count > 1 && o.off == b.off + b.stride * b.count) {
-                    ++b.count;
-                    continue;
-                }
-            }
-        }
-        runs.push_back(Run{o.row, o.off, 0, 1, o.bytes, o.column});
+    for (uint32_t e = count_; e > first;) {
+        const StoredOriginal& last = win_[e - 1];
+        uint32_t r = last.run;
+        if (r > e - first) r = e - first;
+        const StoredOriginal& head = win_[e - r];
+        if (used < last.bytes) used = last.bytes;
+        runs.push_back(Run{head.row, head.off, last.stride, r, last.bytes, head.column});
+        e -= r;
     }
 
     out.meta = m;

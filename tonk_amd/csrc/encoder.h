@@ -37,6 +37,8 @@ struct StoredOriginal {
     uint32_t column = 0;
     uint32_t send_msec = 0;     // encoder only (retransmit timing)
     uint32_t off = 0;           // arena offset of `row` (64-B units), cached for program emission
+    uint32_t stride = 0;        // encoder: off - previous element's off when run > 1
+    uint16_t run = 0;           // encoder: packets of equal length at a fixed stride ending here
     uint8_t header_bytes = 0;
     uint8_t owned = 0;          // the codec frees `row` when the packet leaves the window
     void* host = nullptr;       // optional host mirror (C-ABI: siamese_encoder_get/retransmit)
