@@ -14,7 +14,8 @@
 
 #define TAMD_WAVES_PER_WG 4
 #define TAMD_LANE_BYTES 8
-#define TAMD_BATCH 8  // instructions whose loads are issued together (memory-level parallelism)
+#define TAMD_BATCH 8    // instructions whose loads are issued together (memory-level parallelism)
+#define TAMD_RBATCH 16  // rows of an ACCR run loaded together
 static_assert(TAMD_SLICE_BYTES == 64 * TAMD_LANE_BYTES, "one wave covers one slice");
 
 typedef unsigned long long u64;
@@ -78,16 +79,16 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
     const bool live = o < len;
     const u64 tail = (o + 8u > len && live) ? byte_mask(len - o) : ~0ull;
     const uint32_t* inv = lds + 256 * 8;  // bytes
-    for (uint32_t e = 0; e < count; e += TAMD_BATCH) {
-        u64 d[TAMD_BATCH];
+    for (uint32_t e = 0; e < count; e += TAMD_RBATCH) {
+        u64 d[TAMD_RBATCH];
 #pragma unroll
-        for (uint32_t q = 0; q < TAMD_BATCH; ++q) {
+        for (uint32_t q = 0; q < TAMD_RBATCH; ++q) {
             d[q] = 0;
             if (live && e + q < count)
                 d[q] = *(const u64*)(arena + ((size_t)row0 + (size_t)(e + q) * stride) * TAMD_ROW_UNIT + o);
         }
 #pragma unroll
-        for (uint32_t q = 0; q < TAMD_BATCH; ++q) {
+        for (uint32_t q = 0; q < TAMD_RBATCH; ++q) {
             if (e + q >= count) continue;
             const u64 x = d[q] & tail;
             const uint32_t col = (col0 + (e + q) * cstep) & (TAMD_COLUMN_PERIOD - 1u);
