@@ -1,0 +1,42 @@
+// pmc_calib.hip -- calibration for rocprofv3 FETCH_SIZE / WRITE_SIZE with tamd_exec's access
+// pattern (each wave reads/writes 512 contiguous bytes as 8 bytes per lane).  The guide's
+// gfx950 correction (FETCH_SIZE = half the bytes) is measured for 16-B/lane loads only; this
+// kernel moves a known byte count with 8-B/lane accesses so tools/pmc_traffic.py can scale the
+// counters of tamd_exec.  Sizes are far beyond the 256 MiB Infinity Cache.
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+
+typedef unsigned long long u64;
+
+extern "C" __global__ void calib_read8(const u64* __restrict__ src, size_t n_words, u64* __restrict__ sink) {
+    u64 acc = 0;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_words; i += (size_t)gridDim.x * blockDim.x)
+        acc ^= src[i];
+    if (acc == 0x123456789abcdefull) sink[0] = acc;  // keep the loads
+}
+
+extern "C" __global__ void calib_write8(u64* __restrict__ dst, size_t n_words) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_words; i += (size_t)gridDim.x * blockDim.x)
+        dst[i] = i;
+}
+
+int main() {
+    const size_t read_bytes = 2ull << 30, write_bytes = 1ull << 30;
+    u64 *src = nullptr, *dst = nullptr, *sink = nullptr;
+    if (hipMalloc((void**)&src, read_bytes) != hipSuccess || hipMalloc((void**)&dst, write_bytes) != hipSuccess ||
+        hipMalloc((void**)&sink, 64) != hipSuccess) {
+        fprintf(stderr, "alloc failed\n");
+        return 1;
+    }
+    (void)hipMemset(src, 1, read_bytes);
+    for (int rep = 0; rep < 3; ++rep) {
+        hipLaunchKernelGGL(calib_read8, dim3(4096), dim3(256), 0, 0, src, read_bytes / 8, sink);
+        hipLaunchKernelGGL(calib_write8, dim3(4096), dim3(256), 0, 0, dst, write_bytes / 8);
+    }
+    (void)hipDeviceSynchronize();
+    printf("{\"calib_read8_bytes\": %zu, \"calib_write8_bytes\": %zu}\n", read_bytes, write_bytes);
+    (void)hipFree(src);
+    (void)hipFree(dst);
+    (void)hipFree(sink);
+    return 0;
+}
