@@ -950,7 +950,13 @@ bool Decoder::eliminate_original_data() {
         if (ctx_->oom) return false;
         // Fold everything already in memory into one partial row so the triangular solve and
         // any later reader in this program touch one row instead of the whole elimination.
+        // A single unknown needs no triangular solve: back substitution scales the terms
+        // straight into the recovered row.
         sym_clip(buf, rec->bytes);
+        if (cr_.lost_count == 1) {
+            sym_merge(buf);
+            continue;
+        }
         TAMD_PROF_SCOPE(kElimFold);
         const RowId p = fold_low_levels(ctx_->rows, ctx_->pb, buf, 3, rec->bytes, row_bytes_);
         if (p != kNoRow) ctx_->temps.push_back(p);
