@@ -84,6 +84,18 @@ def cpu_baseline(threads: int, target_s: float = 10.0) -> dict | None:
                       f"{j['seconds']:.2f} s"}
 
 
+def pmc_traffic() -> tuple:
+    """HBM bytes per tamd_exec launch from the committed rocprofv3 PMC passes of this workload
+    (tools/gpu_round.sh -> tools/pmc_traffic.py -> profiles/pmc_traffic.json), or (None, None)."""
+    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(p) as f:
+            j = json.load(f)
+        return j.get("traffic_bytes_per_launch"), os.path.relpath(p, ROOT)
+    except (OSError, ValueError):
+        return None, None
+
+
 def stream_base(rank: int) -> int:
     """Weak scaling: rank r owns streams [64 r, 64 r + 64) -- disjoint, no data-path exchange."""
     return rank * STREAMS_PER_GPU
@@ -180,6 +192,7 @@ def main() -> int:
     sess.close()
 
     achieved = alg / (kernel_ms / 1e3) / 1e9 if kernel_ms > 0 else 0.0
+    traffic, traffic_src = pmc_traffic()
     out = {
         "metric": METRIC,
         "value": round(value, 4),
@@ -206,7 +219,8 @@ def main() -> int:
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": None,
+            "traffic": round(traffic, 1) if traffic else None,
+            "traffic_source": traffic_src,
             "kernel": "tamd_exec",
             "launches": launches,
             "avg_launch_us": round(kernel_ms * 1e3 / launches, 3) if launches else None,
