@@ -3,6 +3,7 @@
 #include "decoder.h"
 #include "prof.h"
 
+#include <algorithm>
 #include <string.h>
 
 namespace tamd {
@@ -42,6 +43,8 @@ Decoder::~Decoder() {
     while (r) { Recovery* n = r->next; free_recovery(r); r = n; }
     for (Recovery* g : graveyard_) delete g;
     graveyard_.clear();
+    for (Recovery* g : pool_) delete g;
+    pool_.clear();
     pre_flush();  // snapshots already referenced by the pending program must still be written
     for (unsigned l = 0; l < kLanes; ++l) lanes_[l].sums.release(ctx_->rows);
     ctx_->detach(this);
@@ -335,9 +338,7 @@ void Decoder::remove_elements() {
         s->got = 0;
         s->got_count = 0;
     }
-    std::vector<Subwindow*> moved(subs_.begin(), subs_.begin() + first_kept_sub);
-    subs_.erase(subs_.begin(), subs_.begin() + first_kept_sub);
-    subs_.insert(subs_.end(), moved.begin(), moved.end());
+    std::rotate(subs_.begin(), subs_.begin() + first_kept_sub, subs_.end());
 
     count_ -= removed;
     column_start_ = to_column(removed);
@@ -404,7 +405,7 @@ void Decoder::list_delete_before(uint32_t element) {
 void Decoder::checked_reset() {
     cr_ = Checked();
     matrix_reset();
-    for (Recovery* r : graveyard_) delete r;
+    for (Recovery* r : graveyard_) pool_.push_back(r);  // reused by add_recovery
     graveyard_.clear();
 }
 
@@ -711,7 +712,16 @@ Result Decoder::add_recovery(RowId row, uint32_t total_bytes, const uint8_t* tai
         return kSuccess;
     }
 
-    Recovery* r = new Recovery();
+    Recovery* r;
+    if (!pool_.empty()) {
+        r = pool_.back();
+        pool_.pop_back();
+        r->next = r->prev = nullptr;
+        r->lost_count = 0;
+        r->buf.clear();
+    } else {
+        r = new Recovery();
+    }
     r->bytes = total_bytes - (uint32_t)footer;
     r->row = row;
     *took = true;
@@ -910,7 +920,8 @@ bool Decoder::eliminate_original_data() {
             }
         } else {
             const uint32_t rbytes = rec->bytes;
-            Sym prod;
+            Sym& prod = prod_;
+            prod.clear();
             uint32_t sum_elem = to_element(m.ColumnStart);
             if (m.ColumnStart != sum_column_start_ || m.SumCount < sum_column_count_) {
                 if (invalid_element(sum_elem)) return false;
@@ -1000,7 +1011,8 @@ Result Decoder::back_substitution() {
         const uint8_t inv_y = gf_inv(y);
         const uint32_t bytes = rec->bytes;
 
-        Sym value;
+        Sym& value = value_;
+        value.clear();
         sym_add(value, rec->buf, bytes, inv_y);
         sym_merge(value);
         const RowId out_row = ctx_->alloc(bytes);

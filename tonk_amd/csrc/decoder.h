@@ -104,6 +104,7 @@ private:
     // reference frees them into its pool allocator, where stale pointers still read the old
     // fields (RecoveryPacketList::DeletePacketsBefore, SiameseDecoder.cpp:2637-2666).
     std::vector<Recovery*> graveyard_;
+    std::vector<Recovery*> pool_;  // recycled Recovery objects (keep their buffers' capacity)
     uint32_t recovery_count_ = 0;
     RecoveryMeta last_meta_;
     uint32_t last_bytes_ = 0;
@@ -126,6 +127,7 @@ private:
     uint32_t ge_resume_pivot_ = 0;
 
     uint32_t latest_column_ = 0;
+    Sym prod_, value_;  // scratch
 
     // helpers
     uint32_t to_element(uint32_t column) const { return col_sub(column, column_start_); }

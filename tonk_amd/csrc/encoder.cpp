@@ -560,7 +560,10 @@ Result Encoder::encode(RecoveryOut& out) {
     if (++next_row_ >= kRowPeriod) next_row_ = 0;
 
     const uint32_t recovery_bytes = longest_;
-    Sym rec, prod;
+    Sym& rec = rec_;
+    Sym& prod = prod_;
+    rec.clear();
+    prod.clear();
     {
         TAMD_PROF_SCOPE(kEncDense);
         add_dense(row, recovery_bytes, rec);

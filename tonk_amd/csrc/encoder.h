@@ -143,7 +143,7 @@ private:
     void add_dense(uint32_t row, uint32_t recovery_bytes, Sym& rec);
     void add_light(uint32_t row, Sym& rec, Sym& prod);
     Result emit(Sym& terms, uint32_t len, const RecoveryMeta& meta, RecoveryOut& out, bool distinct);
-    Sym scratch_;
+    Sym scratch_, rec_, prod_;
     struct Run { RowId row; uint32_t off, stride, count, len, col; };
     std::vector<Run> runs_;
 };

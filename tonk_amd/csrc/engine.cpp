@@ -288,22 +288,34 @@ void sym_merge(Sym& s) {
             else s[k++] = t;
         }
     } else {
-        // open addressing on the row id; slots hold output positions (< the input position)
-        thread_local std::vector<int32_t> tab;
+        // open addressing on the row id; slots hold output positions (< the input position) and
+        // are valid only when stamped with this call's generation (no clearing between calls)
+        struct Slot { uint32_t gen; int32_t at; };
+        thread_local std::vector<Slot> tab;
+        thread_local uint32_t gen = 0;
         size_t cap = 32;
         while (cap < 2 * n) cap *= 2;
-        tab.assign(cap, -1);
+        if (tab.size() < cap) {
+            tab.assign(cap, Slot{0, -1});
+            gen = 0;
+        }
+        if (++gen == 0) {
+            for (Slot& sl : tab) sl.gen = 0;
+            gen = 1;
+        }
         const size_t mask = cap - 1;
         for (size_t i = 0; i < n; ++i) {
             const Term t = s[i];
             size_t h = ((size_t)t.row * 0x9E3779B1u) >> 7 & mask;
             for (;;) {
-                const int32_t at = tab[h];
-                if (at < 0) {
-                    tab[h] = (int32_t)k;
+                Slot& sl = tab[h];
+                if (sl.gen != gen) {
+                    sl.gen = gen;
+                    sl.at = (int32_t)k;
                     s[k++] = t;
                     break;
                 }
+                const int32_t at = sl.at;
                 if (s[at].row == t.row && s[at].len == t.len) {
                     s[at].coef ^= t.coef;
                     break;
@@ -512,7 +524,9 @@ void LaneSums::release(RowTable& rows) {
 RowId fold_low_levels(RowTable& rows, ProgramBuilder& pb, Sym& s, uint32_t keep_level,
                       uint32_t len, uint32_t row_bytes) {
     (void)row_bytes;
-    Sym low, high;
+    thread_local Sym low, high;
+    low.clear();
+    high.clear();
     for (const Term& t : s) {
         if (rows.level(t.row) < keep_level) low.push_back(t);
         else high.push_back(t);
