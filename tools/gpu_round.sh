@@ -16,5 +16,4 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv 
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write_$TAG" -o run -- python3 "$R/bench.py" --no-cpu-baseline --steps 3 --warmup 1 > "$OUT/pmc_write.log" 2>&1 &&
 timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/calib_fetch_$TAG" -o run -- "$R/tools/pmc_calib" > "$OUT/calib_fetch.log" 2>&1 &&
 timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/calib_write_$TAG" -o run -- "$R/tools/pmc_calib" > "$OUT/calib_write.log" 2>&1 &&
-cd "$R" && { [ ! -x oracle/_ref/tonk/unit_tests_amd ] || timeout -k 10 900 oracle/_ref/tonk/unit_tests_amd < /dev/null > "$OUT/unit_tests_amd.log" 2>&1; } &&
-python tools/pmc_traffic.py "$OUT/pmc_fetch_$TAG" "$OUT/pmc_write_$TAG" "$OUT/calib_fetch_$TAG" "$OUT/calib_write_$TAG" "$OUT/pmc_traffic_$TAG.json" > "$OUT/pmc_traffic.log" 2>&1
+cd "$R" && python tools/pmc_traffic.py "$OUT/pmc_fetch_$TAG" "$OUT/pmc_write_$TAG" "$OUT/calib_fetch_$TAG" "$OUT/calib_write_$TAG" "$OUT/pmc_traffic_$TAG.json" > "$OUT/pmc_traffic.log" 2>&1
