@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <chrono>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 extern "C" __global__ void tamd_exec(const tamd_op*, const tamd_instr*, const uint2*, uint32_t, uint8_t*,
@@ -69,11 +70,18 @@ bool Device::init(int device, uint64_t arena_bytes) {
     HIPCHK(hipMalloc((void**)&arena_, arena_bytes_));
     HIPCHK(hipMemsetAsync(arena_, 0, arena_bytes_, s));
     if (!gf_init()) { error_ = "gf self test failed"; return false; }
-    // kernels.hip TAMD_GF_DWORDS: perm tables, inv[256], sqr[256]
-    std::vector<uint8_t> tables(sizeof(g_gf.perm) + 512);
+    // kernels.hip TAMD_GF_DWORDS: perm tables, inv[256], sqr[256], then the lane table: for
+    // i = 0..252 (column value cx = 3 + i) the perm dwords of cx and of cx^2
+    std::vector<uint8_t> tables(sizeof(g_gf.perm) + 512 + 253 * 12 * 4);
     memcpy(tables.data(), g_gf.perm, sizeof(g_gf.perm));
     memcpy(tables.data() + sizeof(g_gf.perm), g_gf.inv, 256);
     memcpy(tables.data() + sizeof(g_gf.perm) + 256, g_gf.sqr, 256);
+    for (unsigned i = 0; i < 253; ++i) {
+        const uint8_t cx = (uint8_t)(3 + i);
+        uint8_t* dst = tables.data() + sizeof(g_gf.perm) + 512 + i * 48;
+        memcpy(dst, g_gf.perm[cx], 24);
+        memcpy(dst + 24, g_gf.perm[gf_sqr(cx)], 24);
+    }
     HIPCHK(hipMalloc((void**)&d_gf_, tables.size()));
     HIPCHK(hipMemcpy(d_gf_, tables.data(), tables.size(), hipMemcpyHostToDevice));
     for (Slot& sl : slots_) {
@@ -239,6 +247,9 @@ uint64_t Device::launch() {
     HIPCHK(hipMemcpyAsync(slot.dev, slot.host, P.total, hipMemcpyHostToDevice, st));
     const double up_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - u0).count();
     stats_.upload_enqueue_ms += up_ms;
+    if (up_ms > 1.0 && getenv("TONK_AMD_TRACE_UPLOADS"))
+        fprintf(stderr, "tonk_amd: program %llu: H2D enqueue of %zu bytes took %.3f ms\n",
+                (unsigned long long)ticket, P.total, up_ms);
     if (up_ms > stats_.upload_enqueue_max_ms) stats_.upload_enqueue_max_ms = up_ms;
     const tamd_instr* di = (const tamd_instr*)slot.dev;
     const tamd_op* dops = (const tamd_op*)(slot.dev + P.bytes_instr);

@@ -233,7 +233,8 @@ public:
         if (len > content_) content_ = len;
         if (!terms_.empty()) {
             T& b = terms_.back();
-            if (b.len == len && (b.col + 8u * b.count) % TAMD_COLUMN_PERIOD == column) {
+            // (a run never wraps the 22-bit column period: the device steps cx by column)
+            if (b.len == len && b.col + 8u * b.count == column) {
                 if (b.count == 1 && off > b.off) {
                     b.stride = off - b.off;
                     b.count = 2;

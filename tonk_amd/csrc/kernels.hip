@@ -63,13 +63,30 @@ __device__ __forceinline__ void store_slice(uint8_t* __restrict__ arena, const t
     *(u64*)(arena + (size_t)in.row * TAMD_ROW_UNIT + o) = (acc & keep) | fpart;
 }
 
-#define TAMD_GF_DWORDS (256 * 8 + 64 + 64)  // perm tables, then inv[256] and sqr[256] as bytes
+// LDS image of the device tables (device.cpp uploads the same layout):
+//   [0, 2048)        perm tables, 8 dwords per coefficient (6 used)
+//   [2048, 2112)     inv[256] as bytes
+//   [2112, 2176)     sqr[256] as bytes
+//   [2176, +253*12)  lane table: for i = 0..252 (cx = 3 + i) the 6 perm dwords of cx, then of cx^2
+#define TAMD_LDS_INV 2048
+#define TAMD_LDS_LANE 2176
+#define TAMD_GF_DWORDS (TAMD_LDS_LANE + 253 * 12)
 
 __device__ __forceinline__ uint32_t lds_byte(const uint32_t* __restrict__ lds, uint32_t byte_index) {
     return (lds[byte_index >> 2] >> (8u * (byte_index & 3u))) & 0xffu;
 }
 
-// ACCR: a strided run of rows (program.h).  Loads of TAMD_BATCH rows are issued together.
+__device__ __forceinline__ u64 gf_mul8_t(u64 v, const uint32_t* __restrict__ t) {
+    const uint32_t t0lo = t[0], t0hi = t[1], t1lo = t[2], t1hi = t[3], t2lo = t[4], t2hi = t[5];
+    const uint32_t lo = gf_mul4((uint32_t)v, t0lo, t0hi, t1lo, t1hi, t2lo, t2hi);
+    const uint32_t hi = gf_mul4((uint32_t)(v >> 32), t0lo, t0hi, t1lo, t1hi, t2lo, t2hi);
+    return ((u64)hi << 32) | lo;
+}
+
+// ACCR: a strided run of rows (program.h).  TAMD_RBATCH row loads are issued together; every
+// element's coefficient table is found with one uniform LDS address: lane runs step the column
+// value index (cx = 3 + (199*col mod 253)) on the scalar unit and read the precomputed
+// (cx, cx^2) tables; Cauchy runs fetch their inverses for the whole batch first.
 __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& r, uint32_t o,
                                          const uint8_t* __restrict__ arena, const uint32_t* __restrict__ lds,
                                          u64& a0, u64& a1, u64& a2) {
@@ -78,7 +95,9 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
     const uint32_t stride = uniform(r.row), col0 = uniform(r.len), cstep = uniform(r.cap);
     const bool live = o < len;
     const u64 tail = (o + 8u > len && live) ? byte_mask(len - o) : ~0ull;
-    const uint32_t* inv = lds + 256 * 8;  // bytes
+    uint32_t ci = uniform((199u * (col0 % 253u)) % 253u);     // column value index of element 0
+    const uint32_t cstep_i = uniform((199u * (cstep % 253u)) % 253u);
+    uint32_t col = col0;
     for (uint32_t e = 0; e < count; e += TAMD_RBATCH) {
         u64 d[TAMD_RBATCH];
 #pragma unroll
@@ -87,22 +106,33 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
             if (live && e + q < count)
                 d[q] = *(const u64*)(arena + ((size_t)row0 + (size_t)(e + q) * stride) * TAMD_ROW_UNIT + o);
         }
+        if (mode == TAMD_R_LANE3) {
 #pragma unroll
-        for (uint32_t q = 0; q < TAMD_RBATCH; ++q) {
-            if (e + q >= count) continue;
-            const u64 x = d[q] & tail;
-            const uint32_t col = (col0 + (e + q) * cstep) & (TAMD_COLUMN_PERIOD - 1u);
-            if (mode == TAMD_R_LANE3) {
-                const uint32_t cx = 3u + (199u * col) % 253u;  // GetColumnValue (SiameseCommon.h:89-93)
-                a0 ^= x;
-                a1 ^= gf_mul8(x, cx, lds);
-                a2 ^= gf_mul8(x, lds_byte(inv, 256u + cx), lds);
-            } else if (mode == TAMD_R_CAUCHY) {
-                const uint32_t c = lds_byte(inv, ((col & 63u) ^ (p + 64u)) & 0xffu);  // CauchyElement
-                a0 ^= gf_mul8(x, c, lds);
-            } else {
-                a0 ^= p == 1u ? x : gf_mul8(x, p, lds);
+            for (uint32_t q = 0; q < TAMD_RBATCH; ++q) {
+                if (e + q < count) {
+                    const uint32_t* t = lds + TAMD_LDS_LANE + ci * 12u;
+                    const u64 x = d[q] & tail;
+                    a0 ^= x;
+                    a1 ^= gf_mul8_t(x, t);
+                    a2 ^= gf_mul8_t(x, t + 6);
+                }
+                ci += cstep_i;
+                if (ci >= 253u) ci -= 253u;
             }
+        } else if (mode == TAMD_R_CAUCHY) {
+            uint32_t c[TAMD_RBATCH];
+#pragma unroll
+            for (uint32_t q = 0; q < TAMD_RBATCH; ++q) {  // CauchyElement(p, col mod 64)
+                c[q] = uniform(lds_byte(lds + TAMD_LDS_INV, ((col & 63u) ^ (p + 64u)) & 0xffu));
+                col = (col + cstep) & (TAMD_COLUMN_PERIOD - 1u);
+            }
+#pragma unroll
+            for (uint32_t q = 0; q < TAMD_RBATCH; ++q)
+                if (e + q < count) a0 ^= gf_mul8_t(d[q] & tail, lds + c[q] * 8u);
+        } else {
+#pragma unroll
+            for (uint32_t q = 0; q < TAMD_RBATCH; ++q)
+                if (e + q < count) a0 ^= p == 1u ? (d[q] & tail) : gf_mul8_t(d[q] & tail, lds + p * 8u);
         }
     }
 }
