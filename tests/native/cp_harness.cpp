@@ -78,9 +78,10 @@ struct Harness {
         const uint32_t maxl = ctx.pb.max_level();
         std::vector<uint32_t> sorted;
         sorted.reserve(ops_v.size() * 4);
+        // op_levels() holds buckets 2*level (+1 for short ops); run level by level
         for (uint32_t l = 1; l <= maxl; ++l)
             for (size_t i = 0; i < ops_v.size(); ++i)
-                if (lv[i] == l) {
+                if (lv[i] / 2 == l) {
                     const tamd_op& o = ops_v[i];
                     sorted.push_back(o.first); sorted.push_back(o.count);
                     sorted.push_back(o.span); sorted.push_back(o.tag);

@@ -132,34 +132,38 @@ void Device::begin(Context* const* ctxs, size_t n) {
     P.ctxs.assign(ctxs, ctxs + n);
     P.levels = 0;
     P.n_instr = P.n_ops = P.n_items = 0;
+    uint32_t B = 0;  // buckets: 2 per level (long ops first), see ProgramBuilder::op_levels
     for (size_t c = 0; c < n; ++c) {
         const ProgramBuilder& pb = ctxs[c]->pb;
         P.n_instr += pb.instrs().size();
         P.n_ops += pb.ops().size();
         stats_.acc_bytes += pb.acc_bytes();
         stats_.store_bytes += pb.store_bytes();
-        if (pb.level_ops().size() > P.levels) P.levels = (uint32_t)pb.level_ops().size();
+        if (pb.level_ops().size() > B) B = (uint32_t)pb.level_ops().size();
     }
+    B = (B + 1) & ~1u;
+    P.levels = B / 2;
+    P.buckets = B;
     P.empty = P.n_ops == 0;
     if (P.empty) return;
     const uint32_t L = P.levels;
-    // Ops grouped by level; inside a level, by context.
-    P.op_start.assign(n * L, 0);
-    P.item_start.assign(n * L, 0);
+    // Ops grouped by bucket (level, then long before short); inside a bucket, by context.
+    P.op_start.assign(n * B, 0);
+    P.item_start.assign(n * B, 0);
     P.level_items.assign(L, 0);
     P.item_base.assign(L + 1, 0);
     P.instr_base.assign(n, 0);
     uint32_t op_at = 0, item_at = 0, instr_at = 0;
-    for (uint32_t l = 0; l < L; ++l) {
-        P.item_base[l] = item_at;
+    for (uint32_t b = 0; b < B; ++b) {
+        if ((b & 1) == 0) P.item_base[b / 2] = item_at;
         for (size_t c = 0; c < n; ++c) {
             const ProgramBuilder& pb = ctxs[c]->pb;
-            P.op_start[c * L + l] = op_at;
-            P.item_start[c * L + l] = item_at;
-            if (l < pb.level_ops().size()) {
-                op_at += pb.level_ops()[l];
-                item_at += pb.level_items()[l];
-                P.level_items[l] += pb.level_items()[l];
+            P.op_start[c * B + b] = op_at;
+            P.item_start[c * B + b] = item_at;
+            if (b < pb.level_ops().size()) {
+                op_at += pb.level_ops()[b];
+                item_at += pb.level_items()[b];
+                P.level_items[b / 2] += pb.level_items()[b];
             }
         }
     }
@@ -193,7 +197,7 @@ void Device::fill(size_t c) {
     Plan& P = plan_;
     if (P.empty) return;
     const ProgramBuilder& pb = P.ctxs[c]->pb;
-    const uint32_t L = P.levels;
+    const uint32_t L = P.buckets;
     tamd_instr* hi = (tamd_instr*)P.slot->host;
     tamd_op* ho = (tamd_op*)(P.slot->host + P.bytes_instr);
     uint32_t* hitems = (uint32_t*)(P.slot->host + P.bytes_instr + P.bytes_ops);

@@ -114,6 +114,7 @@ void ProgramBuilder::clear() {
 }
 
 void ProgramBuilder::begin_op() {
+    cur_acc_begin_ = acc_bytes_;
     cur_first_ = (uint32_t)instrs_.size();
     cur_span_ = 0;
     cur_level_in_ = 0;
@@ -222,14 +223,17 @@ uint32_t ProgramBuilder::end_op(uint32_t min_level) {
     op.span = (cur_span_ + 7u) & ~7u;
     op.tag = level;
     ops_.push_back(op);
-    levels_.push_back(level);
-    if (level_ops_.size() <= level) {
-        level_ops_.resize(level + 1, 0);
-        level_items_.resize(level + 1, 0);
+    // Bucket 2*level for long ops (lane scans: hundreds of rows walked by one wave), 2*level+1
+    // for the rest; the executor starts a level's long ops first so they overlap everything else.
+    const uint32_t bucket = 2 * level + (acc_bytes_ - cur_acc_begin_ >= kHeavyOpBytes ? 0u : 1u);
+    levels_.push_back(bucket);
+    if (level_ops_.size() <= bucket + 1) {
+        level_ops_.resize(bucket + 2, 0);
+        level_items_.resize(bucket + 2, 0);
     }
     const uint32_t slices = (op.span + TAMD_SLICE_BYTES - 1) / TAMD_SLICE_BYTES;
-    level_ops_[level]++;
-    level_items_[level] += slices ? slices : 1;
+    level_ops_[bucket]++;
+    level_items_[bucket] += slices ? slices : 1;
     for (size_t i = cur_written_begin_; i < written_.size(); ++i) rows_->set_level(written_[i], level);
     if (level > max_level_) max_level_ = level;
     return level;

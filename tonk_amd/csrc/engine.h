@@ -133,9 +133,11 @@ public:
 
     const std::vector<tamd_op>& ops() const { return ops_; }
     const std::vector<tamd_instr>& instrs() const { return instrs_; }
+    // Per op: its bucket, 2 * level (+1 unless the op reads >= kHeavyOpBytes).
     const std::vector<uint32_t>& op_levels() const { return levels_; }
+    static const uint64_t kHeavyOpBytes = 96 * 1024;
     const std::vector<RowId>& written_rows() const { return written_; }
-    // Per level (index = level): op count and work-item count (TAMD_SLICE_BYTES slices).
+    // Per bucket (see op_levels): op count and work-item count (TAMD_SLICE_BYTES slices).
     const std::vector<uint32_t>& level_ops() const { return level_ops_; }
     const std::vector<uint32_t>& level_items() const { return level_items_; }
 
@@ -153,7 +155,7 @@ private:
     // op under construction
     uint32_t cur_first_ = 0, cur_span_ = 0, cur_level_in_ = 0;
     size_t cur_written_begin_ = 0;
-    uint64_t acc_bytes_ = 0, store_bytes_ = 0;
+    uint64_t acc_bytes_ = 0, store_bytes_ = 0, cur_acc_begin_ = 0;
 };
 
 // ---------------------------------------------------------------------------------------------
