@@ -143,7 +143,7 @@ int main(int argc, char** argv) {
         }
         run[s].reset(new wl::Runner<Null, NoTr>(ps[s], *be[s], tr));
     }
-    uint64_t instrs = 0, ops = 0;
+    uint64_t instrs = 0, ops = 0, acc_bytes = 0, store_bytes = 0;
     if (sample_out) {
         struct sigaction sa;
         memset(&sa, 0, sizeof(sa));
@@ -166,6 +166,8 @@ int main(int argc, char** argv) {
         }
         instrs += ctx.pb.instrs().size();
         ops += ctx.pb.ops().size();
+        acc_bytes += ctx.pb.acc_bytes();
+        store_bytes += ctx.pb.store_bytes();
         {
             TAMD_PROF_SCOPE(kFinish);
             ctx.finish_flush();
@@ -185,8 +187,9 @@ int main(int argc, char** argv) {
         fclose(f);
     }
     const double n = (double)streams * p.n_originals;
-    printf("{\"ns_per_original\": %.1f, \"instrs_per_original\": %.2f, \"ops_per_original\": %.3f, \"seconds\": %.3f}\n",
-           sec * 1e9 / n, instrs / n, ops / n, sec);
+    printf("{\"ns_per_original\": %.1f, \"instrs_per_original\": %.2f, \"ops_per_original\": %.3f, "
+           "\"acc_bytes_per_original\": %.0f, \"store_bytes_per_original\": %.0f, \"seconds\": %.3f}\n",
+           sec * 1e9 / n, instrs / n, ops / n, acc_bytes / n, store_bytes / n, sec);
 #ifdef TAMD_PROF
     const double ghz = 1.0 * 0 + 1;
     for (int i = 0; i < prof::kSlots; ++i)

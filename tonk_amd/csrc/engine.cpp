@@ -397,7 +397,7 @@ void LaneSums::read(RowTable& rows, const ExpansionTable& ex, Sym& out, const ui
         if (snap == kNoRow) {
             snap = rows.alloc(content_);
             if (snap == kNoRow) return;  // caller checks arena exhaustion via RowTable
-            rows.set_level(snap, 1);
+            rows.set_level(snap, kSnapLevel);  // written by the scan's chain (or only) op
             snaps_.push_back(Snap{snap, at, {c[0], c[1], c[2]}});
         }
         if (clip) out.push_back(Term{snap, clip, 1});
@@ -413,44 +413,106 @@ void LaneSums::read(RowTable& rows, const ExpansionTable& ex, Sym& out, const ui
     }
 }
 
+// Emit packets [from, to) of a run list; `ri`/`rdone` is a cursor (run index, packets of it done).
+static void emit_packets(ProgramBuilder& pb, const std::vector<LaneSums::T>& terms, size_t& ri, uint32_t& rdone,
+                         uint32_t count) {
+    while (count > 0 && ri < terms.size()) {
+        const LaneSums::T& t = terms[ri];
+        uint32_t take = t.count - rdone;
+        if (take > count) take = count;
+        const uint32_t col = (t.col + kLanes * rdone) % TAMD_COLUMN_PERIOD;
+        if (take == 1) {
+            const uint8_t cx = column_value(col);
+            pb.op_acc3_off(t.off + t.stride * rdone, cx, gf_sqr(cx), t.len);
+        } else {
+            pb.op_accr(TAMD_R_LANE3, 0, t.off + t.stride * rdone, t.stride, take, t.len, col, kLanes);
+        }
+        rdone += take;
+        count -= take;
+        if (rdone == t.count) {
+            ++ri;
+            rdone = 0;
+        }
+    }
+}
+
+// One scan = the lane's packets in order with snapshots (STOREC) at their read points.  A long
+// scan would be one wave walking hundreds of rows, so it is cut into chunks of at most kChunk
+// packets, split at every snapshot point: each chunk op (level 1) writes its three partial sums
+// (deltas), and a chain op (level 2) adds base + deltas in order and takes the snapshots.
 void LaneSums::emit_scan(RowTable& rows, ProgramBuilder& pb, const RowId* base, const std::vector<T>& terms,
                          const std::vector<Snap>& snaps, const RowId* final_rows) {
-    pb.begin_op();
-    for (unsigned s = 0; s < 3; ++s)
-        if (base[s] != kNoRow) pb.op_acc(base[s], 1, rows.cap_bytes(base[s]), s);
-    size_t si = 0;
-    uint32_t pos = 0;  // packets emitted so far
-    auto snapshots = [&]() {
+    static const uint8_t unit[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+    uint32_t n = 0, width = 0;
+    for (const T& t : terms) {
+        n += t.count;
+        if (t.len > width) width = t.len;
+    }
+    size_t si = 0, ri = 0;
+    uint32_t rdone = 0;
+    auto snapshots = [&](uint32_t pos) {
         while (si < snaps.size() && snaps[si].after == pos) {
             pb.op_storec(snaps[si].row, rows.cap_bytes(snaps[si].row), snaps[si].c);
             ++si;
         }
     };
-    for (const T& t : terms) {
-        uint32_t done = 0;
-        while (done < t.count) {
-            snapshots();
-            const uint32_t until = si < snaps.size() ? snaps[si].after : 0xffffffffu;
-            uint32_t take = t.count - done;
-            if (until - pos < take) take = until - pos;
-            const uint32_t col = (t.col + kLanes * done) % TAMD_COLUMN_PERIOD;
-            if (take == 1) {
-                const uint8_t cx = column_value(col);
-                pb.op_acc3_off(t.off + t.stride * done, cx, gf_sqr(cx), t.len);
-            } else {
-                pb.op_accr(TAMD_R_LANE3, 0, t.off + t.stride * done, t.stride, take, t.len, col, kLanes);
-            }
-            done += take;
-            pos += take;
+    if (n <= kChunk) {
+        pb.begin_op();
+        for (unsigned s = 0; s < 3; ++s)
+            if (base[s] != kNoRow) pb.op_acc(base[s], 1, rows.cap_bytes(base[s]), s);
+        uint32_t pos = 0;
+        while (pos < n) {
+            snapshots(pos);
+            uint32_t until = si < snaps.size() ? snaps[si].after : n;
+            if (until > n) until = n;
+            emit_packets(pb, terms, ri, rdone, until - pos);
+            pos = until;
+        }
+        snapshots(n);
+        if (final_rows)
+            for (unsigned s = 0; s < 3; ++s)
+                if (final_rows[s] != kNoRow) pb.op_storec(final_rows[s], rows.cap_bytes(final_rows[s]), unit[s]);
+        pb.end_op(kSnapLevel);
+        return;
+    }
+
+    // chunk boundaries: every snapshot point, and at most kChunk packets apart
+    std::vector<uint32_t> cuts;
+    std::vector<RowId> deltas;
+    uint32_t pos = 0;
+    size_t sj = 0;
+    while (pos < n) {
+        while (sj < snaps.size() && snaps[sj].after <= pos) ++sj;
+        uint32_t end = pos + kChunk;
+        if (sj < snaps.size() && snaps[sj].after < end) end = snaps[sj].after;
+        if (end > n) end = n;
+        cuts.push_back(pos);
+        pb.begin_op();
+        emit_packets(pb, terms, ri, rdone, end - pos);
+        for (unsigned s = 0; s < 3; ++s) {
+            const RowId d = rows.alloc(width);
+            deltas.push_back(d);
+            if (d != kNoRow) pb.op_storec(d, rows.cap_bytes(d), unit[s]);
+        }
+        pb.end_op(1);
+        pos = end;
+    }
+    pb.begin_op();
+    for (unsigned s = 0; s < 3; ++s)
+        if (base[s] != kNoRow) pb.op_acc(base[s], 1, rows.cap_bytes(base[s]), s);
+    for (size_t k = 0; k < cuts.size(); ++k) {
+        snapshots(cuts[k]);
+        for (unsigned s = 0; s < 3; ++s) {
+            const RowId d = deltas[3 * k + s];
+            if (d != kNoRow) pb.op_acc(d, 1, rows.cap_bytes(d), s);
         }
     }
-    snapshots();
-    if (final_rows) {
-        static const uint8_t unit[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+    snapshots(n);
+    if (final_rows)
         for (unsigned s = 0; s < 3; ++s)
             if (final_rows[s] != kNoRow) pb.op_storec(final_rows[s], rows.cap_bytes(final_rows[s]), unit[s]);
-    }
-    pb.end_op(1);
+    pb.end_op(kSnapLevel);
+    for (RowId d : deltas) rows.free_deferred(d);  // read only inside this program
 }
 
 void LaneSums::flush(RowTable& rows, ProgramBuilder& pb, const ExpansionTable& ex) {

@@ -261,8 +261,16 @@ public:
     void release(RowTable& rows);
 
 private:
+public:
     // a run of `count` lane packets: rows off + k*stride, columns col + 8k (count 1: a single row)
     struct T { RowId row; uint32_t len, off, stride, count, col; };
+    static const uint32_t kChunk = 64;  // longest packet walk of one scan op (see emit_scan)
+    // Level of snapshot rows: chunk ops run at level 1, the chain op that stores the snapshots at
+    // level 2 (a short scan is one op, also placed at level 2).  Readers are assigned levels when
+    // they read, before the scan is emitted, so the level is fixed up front.
+    static const uint32_t kSnapLevel = 2;
+
+private:
     struct Snap { RowId row; uint32_t after; uint8_t c[3]; };  // after = packets accumulated
     uint32_t n_ = 0;                            // packets in terms_
     RowId base_[3] = {kNoRow, kNoRow, kNoRow};  // carried values from a previous flush (level 0)
