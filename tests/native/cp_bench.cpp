@@ -164,6 +164,11 @@ int main(int argc, char** argv) {
             TAMD_PROF_SCOPE(kFlushAll);
             ctx.prepare_flush();
         }
+        if (getenv("CP_BENCH_LEVELS") && done == step) {
+            for (size_t b = 0; b < ctx.pb.level_ops().size(); ++b)
+                fprintf(stderr, "bucket %zu (level %zu %s): ops %u items %u\n", b, b / 2, (b & 1) ? "short" : "long",
+                        ctx.pb.level_ops()[b], ctx.pb.level_items()[b]);
+        }
         instrs += ctx.pb.instrs().size();
         ops += ctx.pb.ops().size();
         acc_bytes += ctx.pb.acc_bytes();
