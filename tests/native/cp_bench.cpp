@@ -168,6 +168,34 @@ int main(int argc, char** argv) {
             for (size_t b = 0; b < ctx.pb.level_ops().size(); ++b)
                 fprintf(stderr, "bucket %zu (level %zu %s): ops %u items %u\n", b, b / 2, (b & 1) ? "short" : "long",
                         ctx.pb.level_ops()[b], ctx.pb.level_items()[b]);
+            // per bucket: row loads per op (ACC/ACC3 = 1, ACCR = count), histogram and max
+            const auto& ops = ctx.pb.ops();
+            const auto& ins = ctx.pb.instrs();
+            const auto& lv = ctx.pb.op_levels();
+            for (size_t b = 0; b < ctx.pb.level_ops().size(); ++b) {
+                uint64_t hist[8] = {0}, tot = 0, mx = 0, n = 0, instr = 0;
+                for (size_t i = 0; i < ops.size(); ++i) {
+                    if (lv[i] != b) continue;
+                    uint64_t loads = 0;
+                    for (uint32_t k = ops[i].first; k < ops[i].first + ops[i].count; ++k) {
+                        const uint32_t kind = ins[k].w0 & 0xff;
+                        if (kind == TAMD_I_ACC || kind == TAMD_I_ACC3) ++loads;
+                        else if (kind == TAMD_I_ACCR) loads += ins[k].cap;
+                    }
+                    int h = 0;
+                    while (h < 7 && (1ull << (2 * h + 2)) <= loads) ++h;
+                    ++hist[h];
+                    tot += loads;
+                    instr += ops[i].count;
+                    if (loads > mx) mx = loads;
+                    ++n;
+                }
+                if (!n) continue;
+                fprintf(stderr, "  bucket %zu: loads/op avg %.1f max %llu instrs/op %.1f  hist(<4,<16,<64,<256,..):", b,
+                        (double)tot / n, (unsigned long long)mx, (double)instr / n);
+                for (int h = 0; h < 8; ++h) fprintf(stderr, " %llu", (unsigned long long)hist[h]);
+                fprintf(stderr, "\n");
+            }
         }
         instrs += ctx.pb.instrs().size();
         ops += ctx.pb.ops().size();
