@@ -166,7 +166,7 @@ int main(int argc, char** argv) {
         }
         if (getenv("CP_BENCH_LEVELS") && done == step) {
             for (size_t b = 0; b < ctx.pb.level_ops().size(); ++b)
-                fprintf(stderr, "bucket %zu (level %zu %s): ops %u items %u\n", b, b / 2, (b & 1) ? "short" : "long",
+                fprintf(stderr, "bucket %zu (level %zu class %zu): ops %u items %u\n", b, b / TAMD_COST_CLASSES, b % TAMD_COST_CLASSES,
                         ctx.pb.level_ops()[b], ctx.pb.level_items()[b]);
             // per bucket: row loads per op (ACC/ACC3 = 1, ACCR = count), histogram and max
             const auto& ops = ctx.pb.ops();
@@ -195,6 +195,29 @@ int main(int argc, char** argv) {
                         (double)tot / n, (unsigned long long)mx, (double)instr / n);
                 for (int h = 0; h < 8; ++h) fprintf(stderr, " %llu", (unsigned long long)hist[h]);
                 fprintf(stderr, "\n");
+                // instruction mix: kind (ACC split by coef==1), ACCR by mode with its row count
+                uint64_t kinds[16] = {0}, rrows[4] = {0}, rcount[4] = {0};
+                for (size_t i = 0; i < ops.size(); ++i) {
+                    if (lv[i] != b) continue;
+                    for (uint32_t k = ops[i].first; k < ops[i].first + ops[i].count; ++k) {
+                        const uint32_t kind = ins[k].w0 & 0xff;
+                        if (kind == TAMD_I_ACC && ((ins[k].w0 >> 8) & 0xff) == 1) ++kinds[15];
+                        else ++kinds[kind & 15];
+                        if (kind == TAMD_I_ACCR) {
+                            const uint32_t m = (ins[k].w0 >> 8) & 3;
+                            ++rcount[m];
+                            rrows[m] += ins[k].cap;
+                        }
+                    }
+                }
+                fprintf(stderr, "    ACC(c!=1) %llu ACC(c=1) %llu ACC3 %llu STORE %llu STOREC %llu CLEAR %llu | "
+                        "ACCR lane3 %llu (%.1f rows) cauchy %llu (%.1f) const %llu (%.1f)\n",
+                        (unsigned long long)kinds[TAMD_I_ACC], (unsigned long long)kinds[15],
+                        (unsigned long long)kinds[TAMD_I_ACC3], (unsigned long long)kinds[TAMD_I_STORE],
+                        (unsigned long long)kinds[TAMD_I_STOREC], (unsigned long long)kinds[TAMD_I_CLEAR],
+                        (unsigned long long)rcount[1], rcount[1] ? (double)rrows[1] / rcount[1] : 0.0,
+                        (unsigned long long)rcount[2], rcount[2] ? (double)rrows[2] / rcount[2] : 0.0,
+                        (unsigned long long)rcount[3], rcount[3] ? (double)rrows[3] / rcount[3] : 0.0);
             }
         }
         instrs += ctx.pb.instrs().size();

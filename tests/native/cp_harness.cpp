@@ -78,13 +78,13 @@ struct Harness {
         const uint32_t maxl = ctx.pb.max_level();
         std::vector<uint32_t> sorted;
         sorted.reserve(ops_v.size() * 4);
-        // op_levels() holds buckets 2*level (+1 for short ops); run level by level
+        // op_levels() holds buckets TAMD_COST_CLASSES * level + class; run level by level
         for (uint32_t l = 1; l <= maxl; ++l)
             for (size_t i = 0; i < ops_v.size(); ++i)
-                if (lv[i] / 2 == l) {
+                if (lv[i] / TAMD_COST_CLASSES == l) {
                     const tamd_op& o = ops_v[i];
                     sorted.push_back(o.first); sorted.push_back(o.count);
-                    sorted.push_back(o.span); sorted.push_back(o.tag);
+                    sorted.push_back(o.span); sorted.push_back(o.full);
                 }
         if (!ops_v.empty()) {
             const int rc = oracle_run_program(arena.data(), arena.size(), sorted.data(),

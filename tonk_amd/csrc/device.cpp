@@ -8,7 +8,7 @@
 #include <string.h>
 
 extern "C" __global__ void tamd_exec(const tamd_op*, const tamd_instr*, const uint2*, uint32_t, uint8_t*,
-                                     const uint32_t*);
+                                     const uint32_t*, const uint8_t*, unsigned long long*);
 extern "C" __global__ void tamd_gf_selftest(const uint32_t*, uint8_t*);
 
 struct GenDescDev { uint32_t row, index, len, pad; unsigned long long seed; };
@@ -27,7 +27,6 @@ namespace tamd {
         }                                                                                \
     } while (0)
 
-static const uint32_t kMaxGrid = 4096;
 
 Device::~Device() {
     if (device_ < 0) return;
@@ -45,6 +44,7 @@ Device::~Device() {
     if (up_host_) hipHostFree(up_host_);
     if (up_event_) hipEventDestroy((hipEvent_t)up_event_);
     if (d_gf_) hipFree(d_gf_);
+    if (d_zero_) hipFree(d_zero_);
     if (arena_) hipFree(arena_);
     if (stream_) hipStreamDestroy((hipStream_t)stream_);
 }
@@ -62,6 +62,16 @@ bool Device::init(int device, uint64_t arena_bytes) {
         return false;
     }
     device_ = device;
+    // Persistent grid: exactly the workgroups that are resident at once (occupancy x CUs), so
+    // every workgroup stages the GF tables once and no workgroup starts late (kernels.hip).
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)tamd_exec, 256, 0) != hipSuccess ||
+        per_cu < 1)
+        per_cu = 1;
+    // The occupancy API ignores the SGPR limit (MI355X_MICROARCH.md, Correctness boundaries): at
+    // tamd_exec's ~106 SGPRs a SIMD holds floor(800 / 128) = 6 waves, i.e. 6 workgroups per CU.
+    if (per_cu > 6) per_cu = 6;
+    max_grid_ = (uint32_t)per_cu * (uint32_t)prop.multiProcessorCount;
     HIPCHK(hipSetDevice(device));
     hipStream_t s = nullptr;
     HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
@@ -82,6 +92,8 @@ bool Device::init(int device, uint64_t arena_bytes) {
         memcpy(dst, g_gf.perm[cx], 24);
         memcpy(dst + 24, g_gf.perm[gf_sqr(cx)], 24);
     }
+    HIPCHK(hipMalloc((void**)&d_zero_, 4096));  // the executor's dummy-load target (kernels.hip)
+    HIPCHK(hipMemsetAsync(d_zero_, 0, 4096, s));
     HIPCHK(hipMalloc((void**)&d_gf_, tables.size()));
     HIPCHK(hipMemcpy(d_gf_, tables.data(), tables.size(), hipMemcpyHostToDevice));
     for (Slot& sl : slots_) {
@@ -132,7 +144,7 @@ void Device::begin(Context* const* ctxs, size_t n) {
     P.ctxs.assign(ctxs, ctxs + n);
     P.levels = 0;
     P.n_instr = P.n_ops = P.n_items = 0;
-    uint32_t B = 0;  // buckets: 2 per level (long ops first), see ProgramBuilder::op_levels
+    uint32_t B = 0;  // buckets: TAMD_COST_CLASSES per level (expensive ops first), see ProgramBuilder::op_levels
     for (size_t c = 0; c < n; ++c) {
         const ProgramBuilder& pb = ctxs[c]->pb;
         P.n_instr += pb.instrs().size();
@@ -141,8 +153,8 @@ void Device::begin(Context* const* ctxs, size_t n) {
         stats_.store_bytes += pb.store_bytes();
         if (pb.level_ops().size() > B) B = (uint32_t)pb.level_ops().size();
     }
-    B = (B + 1) & ~1u;
-    P.levels = B / 2;
+    B = (B + TAMD_COST_CLASSES - 1) / TAMD_COST_CLASSES * TAMD_COST_CLASSES;
+    P.levels = B / TAMD_COST_CLASSES;
     P.buckets = B;
     P.empty = P.n_ops == 0;
     if (P.empty) return;
@@ -155,7 +167,7 @@ void Device::begin(Context* const* ctxs, size_t n) {
     P.instr_base.assign(n, 0);
     uint32_t op_at = 0, item_at = 0, instr_at = 0;
     for (uint32_t b = 0; b < B; ++b) {
-        if ((b & 1) == 0) P.item_base[b / 2] = item_at;
+        if (b % TAMD_COST_CLASSES == 0) P.item_base[b / TAMD_COST_CLASSES] = item_at;
         for (size_t c = 0; c < n; ++c) {
             const ProgramBuilder& pb = ctxs[c]->pb;
             P.op_start[c * B + b] = op_at;
@@ -163,7 +175,7 @@ void Device::begin(Context* const* ctxs, size_t n) {
             if (b < pb.level_ops().size()) {
                 op_at += pb.level_ops()[b];
                 item_at += pb.level_items()[b];
-                P.level_items[b / 2] += pb.level_items()[b];
+                P.level_items[b / TAMD_COST_CLASSES] += pb.level_items()[b];
             }
         }
     }
@@ -173,7 +185,8 @@ void Device::begin(Context* const* ctxs, size_t n) {
         instr_at += (uint32_t)ctxs[c]->pb.instrs().size();
     }
     P.n_items = item_at;
-    P.bytes_instr = P.n_instr * sizeof(tamd_instr);
+    // the executor reads a 64-instruction window without bounds checks: pad the region
+    P.bytes_instr = (P.n_instr + 64) * sizeof(tamd_instr);
     P.bytes_ops = P.n_ops * sizeof(tamd_op);
     P.total = P.bytes_instr + P.bytes_ops + P.n_items * sizeof(uint32_t) * 2;
 
@@ -225,7 +238,7 @@ void Device::fill(size_t c) {
         op.first += ibase;
         const uint32_t oi = of[l]++;
         ho[oi] = op;
-        uint32_t slices = (op.span + TAMD_SLICE_BYTES - 1) / TAMD_SLICE_BYTES;
+        uint32_t slices = (op.span + TAMD_ITEM_BYTES - 1) / TAMD_ITEM_BYTES;
         if (!slices) slices = 1;
         uint32_t ii = itf[l];
         itf[l] += slices;
@@ -258,11 +271,18 @@ uint64_t Device::launch() {
     const tamd_instr* di = (const tamd_instr*)slot.dev;
     const tamd_op* dops = (const tamd_op*)(slot.dev + P.bytes_instr);
     const uint2* ditems = (const uint2*)(slot.dev + P.bytes_instr + P.bytes_ops);
+    // Profiling only: TONK_AMD_STAMPS=<program number> records per-item start/end stamps of that
+    // program's launches and writes them to tonk_amd_stamps.bin (u64 triples per item; levels
+    // delimited by the item bases printed to stderr).
+    unsigned long long* stamps = nullptr;
+    static const char* stamp_env = getenv("TONK_AMD_STAMPS");
+    const bool stamp_this = stamp_env && (uint64_t)atoll(stamp_env) == stats_.programs;
+    if (stamp_this) HIPCHK(hipMalloc((void**)&stamps, P.n_items * 24 + 24));
     for (uint32_t l = 1; l < P.levels; ++l) {
         const uint32_t cnt = P.level_items[l];
         if (!cnt) continue;
         uint32_t grid = (cnt + 3) / 4;
-        if (grid > kMaxGrid) grid = kMaxGrid;
+        if (grid > max_grid_) grid = max_grid_;
         hipEvent_t e0 = nullptr, e1 = nullptr;
         if (timing_) {
             e0 = (hipEvent_t)timing_event();
@@ -270,7 +290,7 @@ uint64_t Device::launch() {
             hipEventRecord(e0, st);
         }
         hipLaunchKernelGGL(tamd_exec, dim3(grid), dim3(256), 0, st, dops, di, ditems + P.item_base[l], cnt,
-                           arena_, d_gf_);
+                           arena_, d_gf_, d_zero_, stamps ? stamps + 3 * P.item_base[l] : nullptr);
         if (timing_) {
             hipEventRecord(e1, st);
             timing_events_.push_back(std::make_pair((void*)e0, (void*)e1));
@@ -278,6 +298,24 @@ uint64_t Device::launch() {
         stats_.launches++;
     }
     HIPCHK(hipGetLastError());
+    if (stamp_this) {
+        std::vector<unsigned long long> h(P.n_items * 3);
+        HIPCHK(hipMemcpyAsync(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        hipFree(stamps);
+        FILE* f = fopen("tonk_amd_stamps.bin", "wb");
+        if (f) {
+            fwrite(h.data(), 8, h.size(), f);
+            fclose(f);
+        }
+        f = fopen("tonk_amd_program.bin", "wb");
+        if (f) {
+            fwrite(slot.host, 1, P.total, f);
+            fclose(f);
+        }
+        fprintf(stderr, "stamps: n_instr_bytes %zu n_ops_bytes %zu n_items %zu\n", P.bytes_instr, P.bytes_ops, P.n_items);
+        for (uint32_t l = 0; l <= P.levels; ++l) fprintf(stderr, "stamps level %u item_base %u\n", l, P.item_base[l]);
+    }
     HIPCHK(hipEventRecord((hipEvent_t)slot.done, st));
     slot.ticket = ticket;
     mark(ticket);

@@ -71,6 +71,8 @@ private:
     uint8_t* arena_ = nullptr;
     uint64_t arena_bytes_ = 0;
     uint32_t* d_gf_ = nullptr;
+    uint8_t* d_zero_ = nullptr;
+    uint32_t max_grid_ = 256;
     void* stream_ = nullptr;
     // program staging: pinned host buffers and device buffers, double buffered
     struct Slot {

@@ -117,6 +117,8 @@ void ProgramBuilder::begin_op() {
     cur_acc_begin_ = acc_bytes_;
     cur_first_ = (uint32_t)instrs_.size();
     cur_span_ = 0;
+    cur_full_ = ~0u;
+    cur_runs_ = 0;
     cur_level_in_ = 0;
     cur_written_begin_ = written_.size();
 }
@@ -130,6 +132,7 @@ void ProgramBuilder::op_acc3_off(uint32_t off, uint8_t c1, uint8_t c2, uint32_t 
     in.cap = 0;
     instrs_.push_back(in);
     if (len > cur_span_) cur_span_ = len;
+    if (len < cur_full_) cur_full_ = len;
     acc_bytes_ += len;
 }
 
@@ -147,7 +150,9 @@ void ProgramBuilder::op_accr(uint32_t mode, uint32_t param, uint32_t row0, uint3
     r.cap = cstep;
     instrs_.push_back(a);
     instrs_.push_back(r);
+    ++cur_runs_;
     if (len > cur_span_) cur_span_ = len;
+    if (len < cur_full_) cur_full_ = len;
     acc_bytes_ += (uint64_t)len * count;
 }
 
@@ -156,6 +161,7 @@ uint32_t ProgramBuilder::finish_combine(RowId dst, uint32_t len, const uint8_t* 
     push_store(instrs_, rows_->offset(dst), len, cap, footer, footer_len);
     if (cap > cur_span_) cur_span_ = cap;
     if (len > cur_span_) cur_span_ = len;
+    if (len < cur_full_) cur_full_ = len;
     written_.push_back(dst);
     store_bytes_ += len + footer_len;
     return end_op(1);
@@ -170,6 +176,7 @@ void ProgramBuilder::op_acc(RowId src, uint8_t coef, uint32_t len, uint32_t acc)
     in.cap = 0;
     instrs_.push_back(in);
     if (len > cur_span_) cur_span_ = len;
+    if (len < cur_full_) cur_full_ = len;
     const uint32_t l = rows_->level(src);
     if (l > cur_level_in_) cur_level_in_ = l;
     acc_bytes_ += len;
@@ -202,6 +209,7 @@ void ProgramBuilder::op_storec(RowId dst, uint32_t len, const uint8_t* c) {
     s.cap = cap;
     instrs_.push_back(s);
     if (cap > cur_span_) cur_span_ = cap;
+    if (len < cur_full_) cur_full_ = len;
     written_.push_back(dst);
     store_bytes_ += len;
 }
@@ -210,6 +218,7 @@ void ProgramBuilder::op_store(RowId dst, uint32_t len, uint32_t acc) {
     const uint32_t cap = rows_->cap_bytes(dst);
     push_store(instrs_, rows_->offset(dst), len, cap, nullptr, 0, acc);
     if (cap > cur_span_) cur_span_ = cap;
+    if (len < cur_full_) cur_full_ = len;
     written_.push_back(dst);
     store_bytes_ += len;
 }
@@ -221,17 +230,20 @@ uint32_t ProgramBuilder::end_op(uint32_t min_level) {
     op.first = cur_first_;
     op.count = (uint32_t)instrs_.size() - cur_first_;
     op.span = (cur_span_ + 7u) & ~7u;
-    op.tag = level;
+    op.full = cur_full_ < op.span ? cur_full_ : op.span;
     ops_.push_back(op);
-    // Bucket 2*level for long ops (lane scans: hundreds of rows walked by one wave), 2*level+1
-    // for the rest; the executor starts a level's long ops first so they overlap everything else.
-    const uint32_t bucket = 2 * level + (acc_bytes_ - cur_acc_begin_ >= kHeavyOpBytes ? 0u : 1u);
+    // Cost class from the op's length in the executor's terms: instructions, and row loads
+    // (an ACCR run is `count` rows); class 0 is the most expensive and starts first.
+    const uint64_t rows = (acc_bytes_ - cur_acc_begin_) / 1024u;
+    const uint64_t cost = op.count + 4u * cur_runs_ + rows / 2u;
+    const uint32_t cls = cost >= 64 ? 0u : cost >= 32 ? 1u : cost >= 12 ? 2u : 3u;
+    const uint32_t bucket = TAMD_COST_CLASSES * level + cls;
     levels_.push_back(bucket);
-    if (level_ops_.size() <= bucket + 1) {
-        level_ops_.resize(bucket + 2, 0);
-        level_items_.resize(bucket + 2, 0);
+    if (level_ops_.size() < TAMD_COST_CLASSES * (level + 1)) {
+        level_ops_.resize(TAMD_COST_CLASSES * (level + 1), 0);
+        level_items_.resize(TAMD_COST_CLASSES * (level + 1), 0);
     }
-    const uint32_t slices = (op.span + TAMD_SLICE_BYTES - 1) / TAMD_SLICE_BYTES;
+    const uint32_t slices = (op.span + TAMD_ITEM_BYTES - 1) / TAMD_ITEM_BYTES;
     level_ops_[bucket]++;
     level_items_[bucket] += slices ? slices : 1;
     for (size_t i = cur_written_begin_; i < written_.size(); ++i) rows_->set_level(written_[i], level);
@@ -246,7 +258,7 @@ uint32_t ProgramBuilder::combine(RowId dst, const Term* terms, size_t n, uint32_
     const size_t at = instrs_.size();
     instrs_.resize(at + n);
     tamd_instr* w = instrs_.data() + at;
-    uint32_t span = cur_span_, lvl = cur_level_in_;
+    uint32_t span = cur_span_, lvl = cur_level_in_, full = cur_full_;
     uint64_t acc = 0;
     size_t k = 0;
     for (size_t i = 0; i < n; ++i) {
@@ -258,18 +270,21 @@ uint32_t ProgramBuilder::combine(RowId dst, const Term* terms, size_t n, uint32_
         w[k].cap = 0;
         ++k;
         if (t.len > span) span = t.len;
+        if (t.len < full) full = t.len;
         const uint32_t l = rows_->level(t.row);
         if (l > lvl) lvl = l;
         acc += t.len;
     }
     instrs_.resize(at + k);
     cur_span_ = span;
+    cur_full_ = full;
     cur_level_in_ = lvl;
     acc_bytes_ += acc;
     const uint32_t cap = rows_->cap_bytes(dst);
     push_store(instrs_, rows_->offset(dst), len, cap, footer, footer_len);
     if (cap > cur_span_) cur_span_ = cap;
     if (len > cur_span_) cur_span_ = len;
+    if (len < cur_full_) cur_full_ = len;
     written_.push_back(dst);
     store_bytes_ += len + footer_len;
     return end_op(1);

@@ -133,11 +133,10 @@ public:
 
     const std::vector<tamd_op>& ops() const { return ops_; }
     const std::vector<tamd_instr>& instrs() const { return instrs_; }
-    // Per op: its bucket, 2 * level (+1 unless the op reads >= kHeavyOpBytes).
+    // Per op: its bucket, TAMD_COST_CLASSES * level + cost class (0 = most expensive).
     const std::vector<uint32_t>& op_levels() const { return levels_; }
-    static const uint64_t kHeavyOpBytes = 96 * 1024;
     const std::vector<RowId>& written_rows() const { return written_; }
-    // Per bucket (see op_levels): op count and work-item count (TAMD_SLICE_BYTES slices).
+    // Per bucket (see op_levels): op count and work-item count (TAMD_ITEM_BYTES chunks).
     const std::vector<uint32_t>& level_ops() const { return level_ops_; }
     const std::vector<uint32_t>& level_items() const { return level_items_; }
 
@@ -153,7 +152,7 @@ private:
     std::vector<uint32_t> level_ops_, level_items_;
     uint32_t max_level_ = 0;
     // op under construction
-    uint32_t cur_first_ = 0, cur_span_ = 0, cur_level_in_ = 0;
+    uint32_t cur_first_ = 0, cur_span_ = 0, cur_level_in_ = 0, cur_full_ = ~0u, cur_runs_ = 0;
     size_t cur_written_begin_ = 0;
     uint64_t acc_bytes_ = 0, store_bytes_ = 0, cur_acc_begin_ = 0;
 };

@@ -1,11 +1,11 @@
 // kernels.hip -- CDNA4 (gfx950) kernels of the Siamese engine.
 //
-// tamd_exec runs one level of a device program (program.h).  Work item = (op, 512-byte slice):
-// one 64-lane wave owns 8 bytes per lane of the op's three accumulators and walks the op's
-// instruction list (wave-uniform, scalar loads).  GF(2^8) byte multiplication by the
-// instruction's coefficient uses three 8-entry product tables per coefficient staged in LDS
-// and v_perm_b32 byte lookups (x*c = T0[x&7] ^ T1[(x>>3)&7] ^ T2[x>>6]), so a muladd costs
-// ~11 VALU ops per dword and no divergent LDS gathers.  Coefficient 1 is a plain XOR.
+// tamd_exec runs one level of a device program (program.h).  A work item is one op over a
+// 512-byte slice of its rows: one 64-lane wave owns 8 bytes per lane of the op's three
+// accumulators and walks the op's instruction list (wave-uniform, scalar loads).  GF(2^8)
+// multiplication by a wave-uniform coefficient uses three 8-entry product tables per
+// coefficient staged in LDS and v_perm_b32 byte lookups (x*c = T0[x&7] ^ T1[(x>>3)&7] ^
+// T2[x>>6]): ~11 VALU ops per dword, no divergent LDS gathers.  Coefficient 1 is a plain XOR.
 // No MFMA: this is GF(2^8) table/XOR work.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -14,9 +14,10 @@
 
 #define TAMD_WAVES_PER_WG 4
 #define TAMD_LANE_BYTES 8
-#define TAMD_BATCH 8    // instructions whose loads are issued together (memory-level parallelism)
-#define TAMD_RBATCH 16  // rows of an ACCR run loaded together
-static_assert(TAMD_SLICE_BYTES == 64 * TAMD_LANE_BYTES, "one wave covers one slice");
+#define TAMD_BATCH 8   // instructions whose loads are issued together (memory-level parallelism)
+#define TAMD_RBATCH 8  // rows of an ACCR run loaded together
+static_assert(TAMD_SLICE_BYTES == 64 * TAMD_LANE_BYTES, "one wave-wide load covers one slice");
+static_assert(TAMD_ITEM_BYTES == TAMD_SLICE_BYTES, "a work item is one slice");
 
 typedef unsigned long long u64;
 
@@ -34,20 +35,35 @@ __device__ __forceinline__ u64 byte_mask(uint32_t nbytes) {  // low `nbytes` byt
 }
 
 __device__ __forceinline__ uint32_t uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t lane) { return __builtin_amdgcn_readlane(v, lane); }
+__device__ __forceinline__ u64 ballot(bool p) { return __builtin_amdgcn_uicmp((uint32_t)p, 0u, 33 /*ne*/); }
 
-__device__ __forceinline__ u64 gf_mul8(u64 v, uint32_t coef, const uint32_t* __restrict__ lds_perm) {
-    const uint32_t* t = &lds_perm[coef * 8u];
-    const uint32_t t0lo = t[0], t0hi = t[1], t1lo = t[2], t1hi = t[3], t2lo = t[4], t2hi = t[5];
-    const uint32_t lo = gf_mul4((uint32_t)v, t0lo, t0hi, t1lo, t1hi, t2lo, t2hi);
-    const uint32_t hi = gf_mul4((uint32_t)(v >> 32), t0lo, t0hi, t1lo, t1hi, t2lo, t2hi);
-    return ((u64)hi << 32) | lo;
+// A wave-uniform value moved into a VGPR: LDS addresses built from it need no v_readfirstlane /
+// v_mov round trip.
+__device__ __forceinline__ uint32_t vgpr(uint32_t s) {
+    uint32_t v;
+    asm("v_mov_b32 %0, %1" : "=v"(v) : "s"(s));
+    return v;
 }
 
-__device__ __forceinline__ void store_slice(uint8_t* __restrict__ arena, const tamd_instr& in, const tamd_instr& f,
-                                            uint32_t o, u64 acc) {
-    const uint32_t len = in.len, cap = in.cap;
+// Bytes of this lane's 8 that lie below `len` (FULL: the whole slice does).
+template <bool FULL>
+__device__ __forceinline__ u64 keep_mask(uint32_t o, uint32_t len) {
+    if (FULL) return ~0ull;
+    if (o + 8u <= len) return ~0ull;
+    if (o >= len) return 0ull;
+    return byte_mask(len - o);
+}
+
+// Offset of this lane's load inside a row of `len` bytes: lanes past the end read the row's
+// first bytes (a valid address) and mask them to zero, so no load is exec-masked.
+template <bool FULL>
+__device__ __forceinline__ uint32_t load_off(uint32_t o, uint32_t len) { return (FULL || o < len) ? o : 0u; }
+
+// row[len, len + 8) = footer, row[len + 8, cap) = 0 around acc (one lane's 8 bytes at offset o).
+__device__ __forceinline__ void store_slice(uint8_t* __restrict__ arena, uint32_t row, uint32_t len, uint32_t cap,
+                                            u64 footer, uint32_t o, u64 acc) {
     if (o >= cap) return;
-    const u64 footer = ((u64)f.len << 32) | f.row;
     u64 keep;
     if (o + 8u <= len) keep = ~0ull;
     else if (o >= len) keep = 0;
@@ -60,7 +76,7 @@ __device__ __forceinline__ void store_slice(uint8_t* __restrict__ arena, const t
         const uint32_t sh = len - o;
         if (sh < 8u) fpart = footer << (8u * sh);
     }
-    *(u64*)(arena + (size_t)in.row * TAMD_ROW_UNIT + o) = (acc & keep) | fpart;
+    *(u64*)(arena + (size_t)row * TAMD_ROW_UNIT + o) = (acc & keep) | fpart;
 }
 
 // LDS image of the device tables (device.cpp uploads the same layout):
@@ -70,163 +86,237 @@ __device__ __forceinline__ void store_slice(uint8_t* __restrict__ arena, const t
 //   [2176, +253*12)  lane table: for i = 0..252 (cx = 3 + i) the 6 perm dwords of cx, then of cx^2
 #define TAMD_LDS_INV 2048
 #define TAMD_LDS_LANE 2176
-#define TAMD_GF_DWORDS (TAMD_LDS_LANE + 253 * 12)
+#define TAMD_GF_DWORDS (TAMD_LDS_LANE + 253 * 12)  // 5212, a multiple of 4
 
-__device__ __forceinline__ uint32_t lds_byte(const uint32_t* __restrict__ lds, uint32_t byte_index) {
-    return (lds[byte_index >> 2] >> (8u * (byte_index & 3u))) & 0xffu;
+// v_perm product tables of one coefficient from LDS (6 dwords at a 16-byte aligned address).
+struct PermT { uint32_t t[6]; };
+__device__ __forceinline__ PermT perm_at(const uint32_t* __restrict__ lds, uint32_t dword_index) {
+    PermT p;
+    const uint4 a = *(const uint4*)(lds + dword_index);
+    const uint2 b = *(const uint2*)(lds + dword_index + 4);
+    p.t[0] = a.x; p.t[1] = a.y; p.t[2] = a.z; p.t[3] = a.w; p.t[4] = b.x; p.t[5] = b.y;
+    return p;
+}
+// The same for tables at an 8-byte (not 16-byte) aligned address: the cx^2 half of a lane entry.
+__device__ __forceinline__ PermT perm_at_hi(const uint32_t* __restrict__ lds, uint32_t dword_index) {
+    PermT p;
+    const uint2 a = *(const uint2*)(lds + dword_index);
+    const uint4 b = *(const uint4*)(lds + dword_index + 2);
+    p.t[0] = a.x; p.t[1] = a.y; p.t[2] = b.x; p.t[3] = b.y; p.t[4] = b.z; p.t[5] = b.w;
+    return p;
 }
 
-__device__ __forceinline__ u64 gf_mul8_t(u64 v, const uint32_t* __restrict__ t) {
-    const uint32_t t0lo = t[0], t0hi = t[1], t1lo = t[2], t1hi = t[3], t2lo = t[4], t2hi = t[5];
-    const uint32_t lo = gf_mul4((uint32_t)v, t0lo, t0hi, t1lo, t1hi, t2lo, t2hi);
-    const uint32_t hi = gf_mul4((uint32_t)(v >> 32), t0lo, t0hi, t1lo, t1hi, t2lo, t2hi);
-    return ((u64)hi << 32) | lo;
+// Selectors of x shared by every product of x (ACC3 multiplies one row by two coefficients).
+struct Sel { uint32_t s0, s1, s2; };
+__device__ __forceinline__ Sel sel4(uint32_t x) {
+    Sel s;
+    s.s0 = x & 0x07070707u;
+    s.s1 = (x >> 3) & 0x07070707u;
+    s.s2 = (x >> 6) & 0x03030303u;
+    return s;
+}
+__device__ __forceinline__ uint32_t mul_sel(const Sel& s, const PermT& p) {
+    return __builtin_amdgcn_perm(p.t[1], p.t[0], s.s0) ^ __builtin_amdgcn_perm(p.t[3], p.t[2], s.s1) ^
+           __builtin_amdgcn_perm(p.t[5], p.t[4], s.s2);
+}
+__device__ __forceinline__ u64 mul8(u64 x, const PermT& p) {
+    const Sel lo = sel4((uint32_t)x), hi = sel4((uint32_t)(x >> 32));
+    return ((u64)mul_sel(hi, p) << 32) | mul_sel(lo, p);
 }
 
-// ACCR: a strided run of rows (program.h).  TAMD_RBATCH row loads are issued together; every
-// element's coefficient table is found with one uniform LDS address: lane runs step the column
-// value index (cx = 3 + (199*col mod 253)) on the scalar unit and read the precomputed
-// (cx, cx^2) tables; Cauchy runs fetch their inverses for the whole batch first.
+// ACCR: a strided run of equally long rows (program.h).  TAMD_RBATCH row loads are issued
+// together (the row index is clamped to the run, so no load is branched around); the per-row
+// table address stepping runs on the vector ALU: lane runs step the column value index
+// (cx = 3 + (199 col mod 253)) through the lane table, Cauchy runs fetch their inverses for the
+// whole batch first.
+template <bool FULL>
 __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& r, uint32_t o,
                                          const uint8_t* __restrict__ arena, const uint32_t* __restrict__ lds,
                                          u64& a0, u64& a1, u64& a2) {
-    const uint32_t mode = uniform((a.w0 >> 8) & 0xffu), p = uniform((a.w0 >> 16) & 0xffu);
-    const uint32_t row0 = uniform(a.row), len = uniform(a.len), count = uniform(a.cap);
-    const uint32_t stride = uniform(r.row), col0 = uniform(r.len), cstep = uniform(r.cap);
-    const bool live = o < len;
-    const u64 tail = (o + 8u > len && live) ? byte_mask(len - o) : ~0ull;
-    uint32_t ci = uniform((199u * (col0 % 253u)) % 253u);     // column value index of element 0
-    const uint32_t cstep_i = uniform((199u * (cstep % 253u)) % 253u);
-    uint32_t col = col0;
-    for (uint32_t e = 0; e < count; e += TAMD_RBATCH) {
-        u64 d[TAMD_RBATCH];
+    const uint32_t mode = (a.w0 >> 8) & 0xffu, p = (a.w0 >> 16) & 0xffu;
+    const uint32_t row0 = a.row, len = a.len, count = a.cap;
+    const uint32_t stride = r.row, col0 = r.len, cstep = r.cap;
+    const u64 keep = keep_mask<FULL>(o, len);
+    const uint8_t* src = arena + (size_t)row0 * TAMD_ROW_UNIT + load_off<FULL>(o, len);
+    const size_t step = (size_t)stride * TAMD_ROW_UNIT;
+    // loads past the run's end re-read its last row (never consumed)
+#define TAMD_RUN_ROW(q) (*(const u64*)(src + (size_t)min(e + (q), count - 1u) * step))
+    if (mode == TAMD_R_LANE3) {
+        // byte offset of the (cx, cx^2) tables in the lane table: 48 bytes per column value index
+        const uint32_t W = 253u * 48u;
+        uint32_t t = vgpr(((199u * (col0 % 253u)) % 253u) * 48u);
+        const uint32_t tstep = vgpr(((199u * (cstep % 253u)) % 253u) * 48u);
+        for (uint32_t e = 0; e < count; e += TAMD_RBATCH) {
+            u64 d[TAMD_RBATCH];
 #pragma unroll
-        for (uint32_t q = 0; q < TAMD_RBATCH; ++q) {
-            d[q] = 0;
-            if (live && e + q < count)
-                d[q] = *(const u64*)(arena + ((size_t)row0 + (size_t)(e + q) * stride) * TAMD_ROW_UNIT + o);
-        }
-        if (mode == TAMD_R_LANE3) {
+            for (uint32_t q = 0; q < TAMD_RBATCH; ++q) d[q] = TAMD_RUN_ROW(q);
 #pragma unroll
             for (uint32_t q = 0; q < TAMD_RBATCH; ++q) {
                 if (e + q < count) {
-                    const uint32_t* t = lds + TAMD_LDS_LANE + ci * 12u;
-                    const u64 x = d[q] & tail;
+                    const uint32_t ti = TAMD_LDS_LANE + (t >> 2);
+                    const PermT c1 = perm_at(lds, ti), c2 = perm_at_hi(lds, ti + 6u);
+                    const u64 x = FULL ? d[q] : (d[q] & keep);
+                    const Sel lo = sel4((uint32_t)x), hi = sel4((uint32_t)(x >> 32));
                     a0 ^= x;
-                    a1 ^= gf_mul8_t(x, t);
-                    a2 ^= gf_mul8_t(x, t + 6);
+                    a1 ^= ((u64)mul_sel(hi, c1) << 32) | mul_sel(lo, c1);
+                    a2 ^= ((u64)mul_sel(hi, c2) << 32) | mul_sel(lo, c2);
+                    t += tstep;
+                    t = min(t, t - W);  // t - W wraps above t while t < W
                 }
-                ci += cstep_i;
-                if (ci >= 253u) ci -= 253u;
             }
-        } else if (mode == TAMD_R_CAUCHY) {
+        }
+    } else if (mode == TAMD_R_CAUCHY) {
+        // CauchyElement(p, col mod 64) = inv((col mod 64) ^ (p + 64)) (SiameseCommon.h:212-218)
+        uint32_t col = vgpr(col0);
+        const uint32_t cs = vgpr(cstep), px = vgpr(p + 64u);
+        const uint8_t* inv = (const uint8_t*)(lds + TAMD_LDS_INV);
+        for (uint32_t e = 0; e < count; e += TAMD_RBATCH) {
+            u64 d[TAMD_RBATCH];
             uint32_t c[TAMD_RBATCH];
 #pragma unroll
-            for (uint32_t q = 0; q < TAMD_RBATCH; ++q) {  // CauchyElement(p, col mod 64)
-                c[q] = uniform(lds_byte(lds + TAMD_LDS_INV, ((col & 63u) ^ (p + 64u)) & 0xffu));
-                col = (col + cstep) & (TAMD_COLUMN_PERIOD - 1u);
+            for (uint32_t q = 0; q < TAMD_RBATCH; ++q) {
+                d[q] = TAMD_RUN_ROW(q);
+                c[q] = inv[(col & 63u) ^ px];
+                col += cs;
             }
 #pragma unroll
             for (uint32_t q = 0; q < TAMD_RBATCH; ++q)
-                if (e + q < count) a0 ^= gf_mul8_t(d[q] & tail, lds + c[q] * 8u);
-        } else {
+                if (e + q < count) a0 ^= mul8(FULL ? d[q] : (d[q] & keep), perm_at(lds, c[q] * 8u));
+        }
+    } else {
+        const bool plain = p == 1u;
+        const PermT cp = perm_at(lds, p * 8u);
+        for (uint32_t e = 0; e < count; e += TAMD_RBATCH) {
+            u64 d[TAMD_RBATCH];
+#pragma unroll
+            for (uint32_t q = 0; q < TAMD_RBATCH; ++q) d[q] = TAMD_RUN_ROW(q);
+            u64 x = 0;
 #pragma unroll
             for (uint32_t q = 0; q < TAMD_RBATCH; ++q)
-                if (e + q < count) a0 ^= p == 1u ? (d[q] & tail) : gf_mul8_t(d[q] & tail, lds + p * 8u);
+                if (e + q < count) x ^= FULL ? d[q] : (d[q] & keep);
+            a0 ^= plain ? x : mul8(x, cp);  // one coefficient: sum the batch's rows, one product
         }
+    }
+#undef TAMD_RUN_ROW
+}
+
+// One work item: the op's instruction list over this wave's 512-byte slice.  FULL items lie
+// below every length the op uses (op.full), so they need no per-lane length handling at all.
+template <bool FULL>
+__device__ __forceinline__ void run_item(const tamd_instr* __restrict__ instrs, uint32_t first, uint32_t end,
+                                         uint32_t o, uint32_t lane8, uint8_t* __restrict__ arena,
+                                         const uint8_t* __restrict__ zrow, const uint32_t* __restrict__ lds) {
+    u64 a0 = 0, a1 = 0, a2 = 0;  // the op's three accumulators (program.h)
+    for (uint32_t k = first; k < end;) {
+        tamd_instr in[TAMD_BATCH];
+#pragma unroll
+        for (uint32_t j = 0; j < TAMD_BATCH; ++j) in[j] = instrs[k + j];  // region padded by 64 words
+        // A batch runs up to (not including) the next ACCR; an ACCR at the head runs alone.
+        uint32_t nb = end - k < TAMD_BATCH ? end - k : TAMD_BATCH;
+#pragma unroll
+        for (uint32_t j = TAMD_BATCH; j-- > 0;)
+            if ((in[j].w0 & 0xffu) == TAMD_I_ACCR && j < nb) nb = j;
+        if (nb == 0) {
+            run_accr<FULL>(in[0], in[1], o, arena, lds, a0, a1, a2);  // in[1] is its RANGE word
+            k += 2;
+            continue;
+        }
+        // Every slot of the batch loads: ACC/ACC3 their row, the others the zero row (no branches,
+        // no exec changes; the values are never consumed).
+        u64 v[TAMD_BATCH];
+#pragma unroll
+        for (uint32_t j = 0; j < TAMD_BATCH; ++j) {
+            const uint32_t kind = in[j].w0 & 0xffu;
+            const bool ld = j < nb && (kind == TAMD_I_ACC || kind == TAMD_I_ACC3);
+            const uint8_t* p = ld ? arena + (size_t)in[j].row * TAMD_ROW_UNIT + load_off<FULL>(o, in[j].len)
+                                  : zrow + lane8;
+            v[j] = *(const u64*)p;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < TAMD_BATCH; ++j) {
+            const uint32_t w = in[j].w0, kind = j < nb ? (w & 0xffu) : 0u;
+            if (kind == TAMD_I_ACC) {
+                u64 x = FULL ? v[j] : (v[j] & keep_mask<FULL>(o, in[j].len));
+                const uint32_t coef = (w >> 8) & 0xffu;
+                if (coef != 1u) x = mul8(x, perm_at(lds, coef * 8u));
+                const uint32_t a = (w >> 16) & 0xffu;
+                if (a == 0) a0 ^= x;
+                else if (a == 1) a1 ^= x;
+                else a2 ^= x;
+            } else if (kind == TAMD_I_STOREC) {
+                const uint32_t c0 = (w >> 8) & 0xffu, c1 = (w >> 16) & 0xffu, c2 = w >> 24;
+                u64 x = 0;
+                if (c0 == 1u) x = a0; else if (c0) x = mul8(a0, perm_at(lds, c0 * 8u));
+                if (c1 == 1u) x ^= a1; else if (c1) x ^= mul8(a1, perm_at(lds, c1 * 8u));
+                if (c2 == 1u) x ^= a2; else if (c2) x ^= mul8(a2, perm_at(lds, c2 * 8u));
+                if (FULL) *(u64*)(arena + (size_t)in[j].row * TAMD_ROW_UNIT + o) = x;
+                else store_slice(arena, in[j].row, in[j].len, in[j].cap, 0, o, x);
+            } else if (kind == TAMD_I_ACC3) {
+                const u64 x = FULL ? v[j] : (v[j] & keep_mask<FULL>(o, in[j].len));
+                const PermT c1 = perm_at(lds, ((w >> 8) & 0xffu) * 8u), c2 = perm_at(lds, ((w >> 16) & 0xffu) * 8u);
+                const Sel lo = sel4((uint32_t)x), hi = sel4((uint32_t)(x >> 32));
+                a0 ^= x;
+                a1 ^= ((u64)mul_sel(hi, c1) << 32) | mul_sel(lo, c1);
+                a2 ^= ((u64)mul_sel(hi, c2) << 32) | mul_sel(lo, c2);
+            } else if (kind == TAMD_I_STORE) {
+                const uint32_t a = (w >> 16) & 0xffu;
+                const u64 x = a == 0 ? a0 : (a == 1 ? a1 : a2);
+                if (FULL) {
+                    *(u64*)(arena + (size_t)in[j].row * TAMD_ROW_UNIT + o) = x;
+                } else {
+                    // the FOOTER word follows the STORE (possibly past this batch)
+                    const tamd_instr f = instrs[k + j + 1];
+                    store_slice(arena, in[j].row, in[j].len, in[j].cap, ((u64)f.len << 32) | f.row, o, x);
+                }
+            } else if (kind == TAMD_I_CLEAR) {
+                a0 = a1 = a2 = 0;
+            }
+        }
+        k += nb;
     }
 }
 
-// Ops of one level never read a row written by an op of the same level, so every ACC load of
-// a batch can be issued before the batch's STOREs: TAMD_BATCH loads in flight per wave.
+// Ops of one level never read a row written by an op of the same level, so every load of a
+// batch can be issued before the batch's stores.  Persistent grid: each workgroup stages the
+// tables in LDS once and then claims items.
 extern "C" __global__ void __launch_bounds__(256)
 tamd_exec(const tamd_op* __restrict__ ops, const tamd_instr* __restrict__ instrs,
           const uint2* __restrict__ items, uint32_t n_items, uint8_t* __restrict__ arena,
-          const uint32_t* __restrict__ gf_perm) {
-    __shared__ uint32_t lds_perm[TAMD_GF_DWORDS];
-    for (uint32_t i = threadIdx.x; i < TAMD_GF_DWORDS; i += blockDim.x) lds_perm[i] = gf_perm[i];
-    __syncthreads();
+          const uint32_t* __restrict__ gf_perm, const uint8_t* __restrict__ zrow,
+          unsigned long long* __restrict__ stamps) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds_perm[TAMD_GF_DWORDS];
+    for (uint32_t i = threadIdx.x; i < TAMD_GF_DWORDS / 4; i += blockDim.x)
+        ((uint4*)lds_perm)[i] = ((const uint4*)gf_perm)[i];
 
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = uniform(threadIdx.x >> 6);
-    const uint32_t stride = gridDim.x * TAMD_WAVES_PER_WG;
 
-    for (uint32_t it = blockIdx.x * TAMD_WAVES_PER_WG + wave; it < n_items; it += stride) {
+    // Workgroup g owns items g, g + G, g + 2G, ... (a stratified sample of the level: items are
+    // ordered by cost class, most expensive first); its waves claim them one at a time through
+    // an LDS counter, so a wave that drew a long op does not hold up the others.
+    __shared__ uint32_t claim;
+    if (threadIdx.x == 0) claim = 0;
+    __syncthreads();
+    for (;;) {
+        uint32_t k = 0;
+        if (lane == 0) k = atomicAdd(&claim, 1u);
+        const uint32_t it = blockIdx.x + uniform(__shfl(k, 0)) * gridDim.x;
+        if (it >= n_items) break;
         const uint2 item = items[it];
         const tamd_op op = ops[uniform(item.x)];
-        const uint32_t o = uniform(item.y) * TAMD_SLICE_BYTES + lane * TAMD_LANE_BYTES;
-        u64 a0 = 0, a1 = 0, a2 = 0;  // the op's three accumulators (program.h)
+        const uint32_t s0 = uniform(item.y) * TAMD_SLICE_BYTES;
+        const uint32_t o = s0 + lane * TAMD_LANE_BYTES;
         const uint32_t first = uniform(op.first), end = uniform(op.first + op.count);
-        for (uint32_t k = first; k < end;) {
-            tamd_instr in[TAMD_BATCH];
-            u64 v[TAMD_BATCH];
-            // A batch runs up to (not including) the next ACCR; an ACCR at the head runs alone.
-            uint32_t nb = TAMD_BATCH;
-#pragma unroll
-            for (uint32_t j = 0; j < TAMD_BATCH; ++j) {
-                in[j].w0 = 0;
-                if (k + j < end) {
-                    in[j] = instrs[k + j];
-                    if ((in[j].w0 & 0xffu) == TAMD_I_ACCR && j < nb) nb = j;
-                }
-            }
-            if (nb == 0) {
-                run_accr(in[0], in[1], o, arena, lds_perm, a0, a1, a2);  // in[1] is its RANGE word
-                k += 2;
-                continue;
-            }
-#pragma unroll
-            for (uint32_t j = 0; j < TAMD_BATCH; ++j) {
-                v[j] = 0;
-                const uint32_t kind = in[j].w0 & 0xffu;
-                if (j < nb && (kind == TAMD_I_ACC || kind == TAMD_I_ACC3) && o < in[j].len)
-                    v[j] = *(const u64*)(arena + (size_t)in[j].row * TAMD_ROW_UNIT + o);
-            }
-#pragma unroll
-            for (uint32_t j = 0; j < TAMD_BATCH; ++j) {
-                const uint32_t kind = j < nb ? (in[j].w0 & 0xffu) : 0u;
-                if (kind == TAMD_I_ACC) {
-                    const uint32_t len = in[j].len;
-                    if (o < len) {
-                        u64 x = v[j];
-                        if (o + 8u > len) x &= byte_mask(len - o);
-                        const uint32_t coef = (in[j].w0 >> 8) & 0xffu;
-                        if (coef != 1u) x = gf_mul8(x, coef, lds_perm);
-                        const uint32_t a = (in[j].w0 >> 16) & 0xffu;
-                        if (a == 0) a0 ^= x;
-                        else if (a == 1) a1 ^= x;
-                        else a2 ^= x;
-                    }
-                } else if (kind == TAMD_I_ACC3) {
-                    const uint32_t len = in[j].len;
-                    if (o < len) {
-                        u64 x = v[j];
-                        if (o + 8u > len) x &= byte_mask(len - o);
-                        a0 ^= x;
-                        a1 ^= gf_mul8(x, (in[j].w0 >> 8) & 0xffu, lds_perm);
-                        a2 ^= gf_mul8(x, (in[j].w0 >> 16) & 0xffu, lds_perm);
-                    }
-                } else if (kind == TAMD_I_STORE) {
-                    // the FOOTER word follows the STORE (possibly in the next batch)
-                    const tamd_instr f = (j + 1 < TAMD_BATCH) ? in[j + 1 < TAMD_BATCH ? j + 1 : j] : instrs[k + j + 1];
-                    const uint32_t a = (in[j].w0 >> 16) & 0xffu;
-                    store_slice(arena, in[j], f, o, a == 0 ? a0 : (a == 1 ? a1 : a2));
-                } else if (kind == TAMD_I_STOREC) {
-                    const uint32_t w = in[j].w0;
-                    const uint32_t c0 = (w >> 8) & 0xffu, c1 = (w >> 16) & 0xffu, c2 = w >> 24;
-                    u64 x = 0;
-                    if (c0 == 1u) x = a0; else if (c0) x = gf_mul8(a0, c0, lds_perm);
-                    if (c1 == 1u) x ^= a1; else if (c1) x ^= gf_mul8(a1, c1, lds_perm);
-                    if (c2 == 1u) x ^= a2; else if (c2) x ^= gf_mul8(a2, c2, lds_perm);
-                    tamd_instr f;
-                    f.w0 = TAMD_I_FOOTER;
-                    f.row = f.len = f.cap = 0;
-                    store_slice(arena, in[j], f, o, x);
-                } else if (kind == TAMD_I_CLEAR) {
-                    a0 = a1 = a2 = 0;
-                }
-            }
-            k += nb;
+        const u64 t0 = stamps ? __builtin_amdgcn_s_memrealtime() : 0;
+        if (s0 + TAMD_SLICE_BYTES <= uniform(op.full))
+            run_item<true>(instrs, first, end, o, lane * TAMD_LANE_BYTES, arena, zrow, lds_perm);
+        else
+            run_item<false>(instrs, first, end, o, lane * TAMD_LANE_BYTES, arena, zrow, lds_perm);
+        if (stamps && lane == 0) {  // profiling only (TONK_AMD_STAMPS): vector stores of 100 MHz stamps
+            __atomic_signal_fence(__ATOMIC_SEQ_CST);
+            const u64 t1 = __builtin_amdgcn_s_memrealtime();
+            stamps[3 * it] = t0;
+            stamps[3 * it + 1] = t1;
+            stamps[3 * it + 2] = ((u64)blockIdx.x << 32) | (threadIdx.x >> 6);
         }
     }
 }

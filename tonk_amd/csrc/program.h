@@ -33,7 +33,9 @@
 #include <stdint.h>
 
 #define TAMD_ROW_UNIT 64u
-#define TAMD_SLICE_BYTES 512u  /* bytes of an op one work item (one wave) covers */
+#define TAMD_SLICE_BYTES 512u  /* bytes one wave-wide load covers (64 lanes x 8 B) */
+#define TAMD_ITEM_SLICES 1u
+#define TAMD_ITEM_BYTES (TAMD_SLICE_BYTES * TAMD_ITEM_SLICES)  /* bytes of an op one work item (one wave) covers */
 
 enum tamd_instr_kind {
     TAMD_I_ACC    = 1,
@@ -52,6 +54,10 @@ enum tamd_range_mode {
     TAMD_R_CONST  = 3,
 };
 
+// Ops of a level are grouped into cost classes (most expensive first) so the executor starts
+// the long dependency chains of a level before the short ops that fill in around them.
+#define TAMD_COST_CLASSES 4u
+
 #define TAMD_COLUMN_PERIOD 0x400000u  /* packet numbers are 22-bit (SiameseCommon.h:105) */
 
 // 16-byte instruction word.
@@ -67,7 +73,8 @@ typedef struct tamd_op {
     uint32_t first;  // index of first instruction
     uint32_t count;  // instruction count
     uint32_t span;   // bytes covered by the op's accumulator
-    uint32_t tag;    // free for the host (stream id / level), ignored by the executor
+    uint32_t full;   // min(span, every length the op's instructions use): slices below it need no
+                     // per-lane length handling (the executor's fast path)
 } tamd_op;
 
 static inline uint32_t tamd_w0(uint32_t kind, uint32_t arg, uint32_t arg2 = 0) {

@@ -1,0 +1,40 @@
+"""Per-item timing from TONK_AMD_STAMPS dumps (profiling only): per level, item duration vs op
+composition, wave busy time and the level's span."""
+import numpy as np, sys
+ibytes, obytes, nitems = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
+bases = [int(x) for x in sys.argv[4].split(',')]
+prog = np.fromfile('tonk_amd_program.bin', dtype=np.uint32)
+instr = prog[:ibytes // 4].reshape(-1, 4)
+ops = prog[ibytes // 4:(ibytes + obytes) // 4].reshape(-1, 4)
+items = prog[(ibytes + obytes) // 4:(ibytes + obytes) // 4 + 2 * nitems].reshape(-1, 2)
+st = np.fromfile('tonk_amd_stamps.bin', dtype=np.uint64).reshape(-1, 3)
+kinds = instr[:, 0] & 0xff
+for l in range(len(bases) - 1):
+    a, b = bases[l], bases[l + 1]
+    if a == b: continue
+    s = st[a:b].astype(np.int64)
+    dur = (s[:, 1] - s[:, 0]) * 10  # ns (100 MHz)
+    t0 = s[:, 0].min()
+    span = (s[:, 1].max() - t0) * 10
+    # per-item loads: ACC/ACC3 count 1, ACCR count rows
+    loads = np.zeros(b - a); ninstr = np.zeros(b - a); naccr = np.zeros(b - a)
+    for i in range(a, b):
+        op = ops[items[i, 0]]
+        ks = kinds[op[0]:op[0] + op[1]]
+        ii = instr[op[0]:op[0] + op[1]]
+        loads[i - a] = ((ks == 1) | (ks == 5)).sum() + ii[ks == 7, 3].sum()
+        ninstr[i - a] = op[1]
+        naccr[i - a] = (ks == 7).sum()
+    wave = s[:, 2]
+    uw, inv = np.unique(wave, return_inverse=True)
+    busy = np.bincount(inv, weights=dur)
+    first = np.array([s[inv == k, 0].min() for k in range(len(uw))]); last = np.array([s[inv == k, 1].max() for k in range(len(uw))])
+    print(f'level {l}: items {b-a} span {span/1e3:.1f} us; item dur median {np.median(dur)/1e3:.2f} p90 {np.percentile(dur,90)/1e3:.2f} max {dur.max()/1e3:.2f} us; waves {len(uw)} busy/wave mean {busy.mean()/1e3:.1f} max {busy.max()/1e3:.1f} us; wave start p50 {np.median(first-t0)*10/1e3:.1f} p99 {np.percentile(first-t0,99)*10/1e3:.1f} end p50 {np.median(last-t0)*10/1e3:.1f} us')
+    # duration vs loads / instrs regression
+    A = np.stack([np.ones_like(loads), loads, ninstr, naccr], 1)
+    coef = np.linalg.lstsq(A, dur, rcond=None)[0]
+    print(f'   dur ~ {coef[0]:.0f} ns + {coef[1]:.0f} ns/load + {coef[2]:.0f} ns/instr + {coef[3]:.0f} ns/accr;  loads mean {loads.mean():.1f} instrs mean {ninstr.mean():.1f}')
+    # timeline: active items over time in 10 bins
+    bins = np.linspace(0, span, 11)
+    act = [((s[:, 0] - t0) * 10 <= x).sum() - ((s[:, 1] - t0) * 10 <= x).sum() for x in bins[:-1] + span / 20]
+    print('   items in flight per tenth:', act)
