@@ -241,6 +241,14 @@ int main(int argc, char** argv) {
         FILE* f = fopen(sample_out, "w");
         for (size_t i = 0; i < g_nsamples; ++i) fprintf(f, "%llx\n", (unsigned long long)g_samples[i]);
         fclose(f);
+        // the process's mappings, to resolve samples inside shared libraries
+        std::string mp = std::string(sample_out) + ".maps";
+        FILE* in = fopen("/proc/self/maps", "r");
+        FILE* out = fopen(mp.c_str(), "w");
+        char line[512];
+        while (in && out && fgets(line, sizeof(line), in)) fputs(line, out);
+        if (in) fclose(in);
+        if (out) fclose(out);
     }
     const double n = (double)streams * p.n_originals;
     printf("{\"ns_per_original\": %.1f, \"instrs_per_original\": %.2f, \"ops_per_original\": %.3f, "
