@@ -96,6 +96,45 @@ def pmc_traffic() -> tuple:
         return None, None
 
 
+def end_to_end(threads: int, device: int, steps: int = 3, warmup: int = 1) -> dict | None:
+    """The PCIe-inclusive rate (north_star): the same workload with packets starting
+    and ending in pinned host memory -- every step copies its originals H2D for both codec
+    sides, its recovery packets and recovered originals D2H (packed by a gather kernel) and the
+    received recovery packets H2D again, on copy streams overlapped with the codec work.
+    Reported beside `value`, never as it."""
+    n_orig = (warmup + steps) * ORIGINALS_PER_STEP
+    wp = tonk_amd.WorkloadParams(n=n_orig, payload=PAYLOAD, loss=LOSS, ack=ACK)
+    try:
+        sess = tonk_amd.Session(wp, n_streams=STREAMS_PER_GPU, device=device, threads=threads,
+                                arena_bytes=(2 * n_orig * STREAMS_PER_GPU * 1344) + (4 << 30), stage_host=True)
+    except RuntimeError as e:
+        return {"error": str(e)}
+    try:
+        sess.generate()
+        for _ in range(warmup):
+            sess.step(ORIGINALS_PER_STEP)
+        sess.wait()
+        s0 = sess.summary()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            sess.step(ORIGINALS_PER_STEP)
+        sess.wait()
+        t1 = time.perf_counter()
+        s1 = sess.summary()
+    finally:
+        sess.close()
+    payload = s1["payload_bytes"] - s0["payload_bytes"]
+    h2d = s1["h2d_bytes"] - s0["h2d_bytes"]
+    d2h = s1["d2h_bytes"] - s0["d2h_bytes"]
+    dt = t1 - t0
+    return {"value": round(payload / dt / 2**30, 4), "unit": "GiB/s", "steps": steps,
+            "ms_per_step": round(dt * 1e3 / steps, 4),
+            "h2d_gb_per_s": round(h2d / dt / 1e9, 2), "d2h_gb_per_s": round(d2h / dt / 1e9, 2),
+            "h2d_bytes_per_step": h2d // steps, "d2h_bytes_per_step": d2h // steps,
+            "note": "pinned hipMemcpyAsync H2D of every original (encoder and decoder copies), D2H of "
+                    "recovery packets and recovered originals, H2D of received recovery packets"}
+
+
 def stream_base(rank: int) -> int:
     """Weak scaling: rank r owns streams [64 r, 64 r + 64) -- disjoint, no data-path exchange."""
     return rank * STREAMS_PER_GPU
@@ -142,6 +181,7 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-end-to-end", action="store_true", help="skip the PCIe-inclusive side measurement")
     a = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -234,6 +274,8 @@ def main() -> int:
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(threads)
+    if rank == 0 and world == 1 and not a.no_end_to_end:
+        out["end_to_end"] = end_to_end(threads, local_rank)
     if rank == 0:
         print(json.dumps(out), flush=True)
     d.close()

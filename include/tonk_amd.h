@@ -27,6 +27,10 @@ typedef struct tamd_session_params {
     uint32_t loss_thresh, ge_enable, gb_thresh, bg_thresh, loss_on_recovery;
     uint32_t fec_rate_q16, ack_every, ack_bytes, arq_lag, flush_max;
     uint32_t record;           /* 1: keep per-stream transcripts (parity checks, not timed) */
+    uint32_t stage_host;       /* 1: packets start and end in pinned host memory: every step copies
+                                  its originals H2D (both codec sides), its recovery packets and
+                                  recovered originals D2H and the received recovery packets H2D
+                                  (the PCIe-inclusive rate) */
     uint64_t arena_bytes;
 } tamd_session_params;
 
@@ -39,6 +43,8 @@ enum {
     TAMD_SUM_STORE_BYTES,      /* bytes written by STORE instructions */
     TAMD_SUM_PROGRAMS, TAMD_SUM_LAUNCHES, TAMD_SUM_OPS, TAMD_SUM_INSTRS, TAMD_SUM_UPLOAD_BYTES,
     TAMD_SUM_DISABLED_CODECS,
+    TAMD_SUM_H2D_BYTES,        /* stage_host: bytes copied host -> device */
+    TAMD_SUM_D2H_BYTES,        /* stage_host: bytes copied device -> host */
     TAMD_SUM_COUNT
 };
 

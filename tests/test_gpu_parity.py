@@ -52,7 +52,7 @@ def test_capi_matches_reference(golden_index, name):
     assert got == want, first_diff(want, got)
 
 
-def _session_transcript(golden_index, name, threads=1):
+def _session_transcript(golden_index, name, threads=1, stage_host=False):
     import tonk_amd
     sc = golden_index["scenarios"][name]
     kv = dict(a.split("=") for a in sc["args"])
@@ -60,7 +60,7 @@ def _session_transcript(golden_index, name, threads=1):
     for k in tonk_amd.WorkloadParams.KEYS:
         setattr(wp, k, int(kv[k]))
     s = tonk_amd.Session(wp, n_streams=1, stream_base=sc["stream"], threads=threads,
-                         arena_bytes=1 << 30, record=True)
+                         arena_bytes=1 << 30, record=True, stage_host=stage_host)
     try:
         s.generate()
         n = wp.n
@@ -83,6 +83,17 @@ def test_session_matches_reference(golden_index, name):
     assert got == want, first_diff(want, got)
     assert summ["missing_at_end"] == 0
     assert summ["disabled_codecs"] == 0
+
+
+@pytest.mark.parametrize("name", ["c2_4096_p1_ack64", "c3_4096_p2_ack64_s1", "burst8_p5"])
+def test_session_host_staged_matches_reference(golden_index, name):
+    """Packets staged through pinned host memory (the PCIe-inclusive path: H2D of the inputs
+    before every step's program, D2H of its outputs) give the same transcript."""
+    got, summ = _session_transcript(golden_index, name, stage_host=True)
+    want = golden_text(name)
+    want = "\n".join(l for l in want.splitlines() if not l.startswith("Z ")) + "\n"
+    assert got == want, first_diff(want, got)
+    assert summ["h2d_bytes"] > 0 and summ["d2h_bytes"] > 0
 
 
 def test_session_bench_config_streams(golden_index):

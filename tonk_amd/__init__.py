@@ -66,12 +66,13 @@ class _SessionParams(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint32) for n in (
         "device", "n_streams", "stream_base", "n_threads", "n_originals", "payload_min", "payload_max",
         "loss_thresh", "ge_enable", "gb_thresh", "bg_thresh", "loss_on_recovery", "fec_rate_q16",
-        "ack_every", "ack_bytes", "arq_lag", "flush_max", "record")] + [("arena_bytes", ctypes.c_uint64)]
+        "ack_every", "ack_bytes", "arq_lag", "flush_max", "record", "stage_host")] + [
+            ("arena_bytes", ctypes.c_uint64)]
 
 
 SUMMARY_FIELDS = ["originals", "lost_originals", "recoveries", "lost_recoveries", "recovered", "arq",
                   "missing_at_end", "payload_bytes", "alg_bytes", "acc_bytes", "store_bytes", "programs",
-                  "launches", "ops", "instrs", "upload_bytes", "disabled_codecs"]
+                  "launches", "ops", "instrs", "upload_bytes", "disabled_codecs", "h2d_bytes", "d2h_bytes"]
 
 
 def loss_threshold(p: float) -> int:
@@ -131,13 +132,14 @@ class Session:
     """Batched device-resident Siamese streams on one MI355X (include/tonk_amd.h)."""
 
     def __init__(self, wp: WorkloadParams, n_streams: int, device: int = 0, stream_base: int = 0,
-                 threads: int = 1, arena_bytes: int = 4 << 30, record: bool = False):
+                 threads: int = 1, arena_bytes: int = 4 << 30, record: bool = False, stage_host: bool = False):
         p = _SessionParams()
         p.device, p.n_streams, p.stream_base, p.n_threads = device, n_streams, stream_base, threads
         p.n_originals, p.payload_min, p.payload_max = wp.n, wp.pmin, wp.pmax
         p.loss_thresh, p.ge_enable, p.gb_thresh, p.bg_thresh = wp.loss, wp.ge, wp.gb, wp.bg
         p.loss_on_recovery, p.fec_rate_q16, p.ack_every, p.ack_bytes = wp.lossrec, wp.fec, wp.ack, wp.ackbytes
         p.arq_lag, p.flush_max, p.record, p.arena_bytes = wp.arq, wp.flush, 1 if record else 0, arena_bytes
+        p.stage_host = 1 if stage_host else 0
         self.n_streams = n_streams
         err = ctypes.create_string_buffer(512)
         self._h = lib().tamd_session_create(ctypes.byref(p), err, len(err))

@@ -10,6 +10,7 @@
 extern "C" __global__ void tamd_exec(const tamd_op*, const tamd_instr*, const uint2*, uint32_t, uint8_t*,
                                      const uint32_t*, const uint8_t*, unsigned long long*);
 extern "C" __global__ void tamd_gf_selftest(const uint32_t*, uint8_t*);
+extern "C" __global__ void tamd_gather_rows(const tamd::Device::GatherDesc*, uint32_t, const uint8_t*, uint8_t*);
 
 struct GenDescDev { uint32_t row, index, len, pad; unsigned long long seed; };
 struct DigestDescDev { uint32_t row, skip, len, pad; };
@@ -41,6 +42,16 @@ Device::~Device() {
     for (void* e : free_events_) hipEventDestroy((hipEvent_t)e);
     for (auto& p : timing_events_) { hipEventDestroy((hipEvent_t)p.first); hipEventDestroy((hipEvent_t)p.second); }
     for (void* e : timing_pool_) hipEventDestroy((hipEvent_t)e);
+    if (h2d_stream_) hipStreamSynchronize((hipStream_t)h2d_stream_);
+    if (d2h_stream_) hipStreamSynchronize((hipStream_t)d2h_stream_);
+    if (h2d_stream_) hipStreamDestroy((hipStream_t)h2d_stream_);
+    if (d2h_stream_) hipStreamDestroy((hipStream_t)d2h_stream_);
+    for (void* e : {h2d_done_, gather_done_, d2h_done_})
+        if (e) hipEventDestroy((hipEvent_t)e);
+    if (gather_dev_) hipFree(gather_dev_);
+    if (recv_dev_) hipFree(recv_dev_);
+    if (gdesc_dev_) hipFree(gdesc_dev_);
+    if (gdesc_host_) hipHostFree(gdesc_host_);
     if (up_host_) hipHostFree(up_host_);
     if (up_event_) hipEventDestroy((hipEvent_t)up_event_);
     if (d_gf_) hipFree(d_gf_);
@@ -393,6 +404,85 @@ void Device::download(void* dst, uint64_t off, size_t n) {
     hipStream_t st = (hipStream_t)stream_;
     HIPCHK(hipMemcpyAsync(dst, arena_ + off, n, hipMemcpyDeviceToHost, st));
     synchronize();
+}
+
+bool Device::enable_staging() {
+    if (h2d_stream_) return true;
+    hipStream_t a, b;
+    hipEvent_t e0, e1, e2;
+    if (hipStreamCreateWithFlags(&a, hipStreamNonBlocking) != hipSuccess) return false;
+    if (hipStreamCreateWithFlags(&b, hipStreamNonBlocking) != hipSuccess) return false;
+    if (hipEventCreateWithFlags(&e0, hipEventDisableTiming) != hipSuccess) return false;
+    if (hipEventCreateWithFlags(&e1, hipEventDisableTiming) != hipSuccess) return false;
+    if (hipEventCreateWithFlags(&e2, hipEventDisableTiming) != hipSuccess) return false;
+    h2d_stream_ = a;
+    d2h_stream_ = b;
+    h2d_done_ = e0;
+    gather_done_ = e1;
+    d2h_done_ = e2;
+    return true;
+}
+
+void Device::h2d(uint64_t off, const void* src, size_t n) {
+    if (n) HIPCHK(hipMemcpyAsync(arena_ + off, src, n, hipMemcpyHostToDevice, (hipStream_t)h2d_stream_));
+}
+
+void Device::h2d_fence() {
+    HIPCHK(hipEventRecord((hipEvent_t)h2d_done_, (hipStream_t)h2d_stream_));
+    HIPCHK(hipStreamWaitEvent((hipStream_t)stream_, (hipEvent_t)h2d_done_, 0));
+}
+
+void Device::d2h_gather(const std::vector<GatherDesc>& d, size_t bytes, void* dst) {
+    if (d.empty()) return;
+    hipStream_t st = (hipStream_t)stream_;
+    // the previous gather's copy-out must be done before the buffers are reused
+    HIPCHK(hipStreamWaitEvent(st, (hipEvent_t)d2h_done_, 0));
+    if (bytes > gather_cap_) {
+        HIPCHK(hipStreamSynchronize((hipStream_t)d2h_stream_));
+        HIPCHK(hipStreamSynchronize(st));
+        if (gather_dev_) hipFree(gather_dev_);
+        gather_cap_ = bytes + bytes / 2 + 4096;
+        HIPCHK(hipMalloc((void**)&gather_dev_, gather_cap_));
+    }
+    if (d.size() > gdesc_cap_) {
+        HIPCHK(hipStreamSynchronize(st));
+        if (gdesc_dev_) hipFree(gdesc_dev_);
+        if (gdesc_host_) hipHostFree(gdesc_host_);
+        gdesc_cap_ = d.size() + d.size() / 2 + 64;
+        HIPCHK(hipMalloc((void**)&gdesc_dev_, gdesc_cap_ * sizeof(GatherDesc)));
+        HIPCHK(hipHostMalloc((void**)&gdesc_host_, gdesc_cap_ * sizeof(GatherDesc), hipHostMallocDefault));
+    } else {
+        // the descriptor staging buffer is reused: wait for the previous gather to have read it
+        HIPCHK(hipEventSynchronize((hipEvent_t)gather_done_));
+    }
+    memcpy(gdesc_host_, d.data(), d.size() * sizeof(GatherDesc));
+    HIPCHK(hipMemcpyAsync(gdesc_dev_, gdesc_host_, d.size() * sizeof(GatherDesc), hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(tamd_gather_rows, dim3((uint32_t)d.size()), dim3(256), 0, st, gdesc_dev_, (uint32_t)d.size(),
+                       arena_, gather_dev_);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord((hipEvent_t)gather_done_, st));
+    hipStream_t ds = (hipStream_t)d2h_stream_;
+    HIPCHK(hipStreamWaitEvent(ds, (hipEvent_t)gather_done_, 0));
+    HIPCHK(hipMemcpyAsync(dst, gather_dev_, bytes, hipMemcpyDeviceToHost, ds));
+    HIPCHK(hipEventRecord((hipEvent_t)d2h_done_, ds));
+}
+
+void Device::h2d_after_d2h(const void* src, size_t n) {
+    if (!n) return;
+    hipStream_t hs = (hipStream_t)h2d_stream_;
+    if (n > recv_cap_) {
+        HIPCHK(hipStreamSynchronize(hs));
+        if (recv_dev_) hipFree(recv_dev_);
+        recv_cap_ = n + n / 2 + 4096;
+        HIPCHK(hipMalloc((void**)&recv_dev_, recv_cap_));
+    }
+    HIPCHK(hipStreamWaitEvent(hs, (hipEvent_t)d2h_done_, 0));
+    HIPCHK(hipMemcpyAsync(recv_dev_, src, n, hipMemcpyHostToDevice, hs));
+}
+
+void Device::sync_staging() {
+    if (h2d_stream_) HIPCHK(hipStreamSynchronize((hipStream_t)h2d_stream_));
+    if (d2h_stream_) HIPCHK(hipStreamSynchronize((hipStream_t)d2h_stream_));
 }
 
 void Device::generate_rows(const std::vector<GenDesc>& d, uint32_t row_cap) {

@@ -60,6 +60,19 @@ public:
     void digest_rows(const std::vector<DigestDesc>& d, std::vector<uint64_t>& out);
     bool gf_selftest();  // device v_perm multiply vs host tables, all 65536 products
 
+    // Host staging (the PCIe-inclusive path): packets start and end in pinned host
+    // memory.  h2d() copies on a dedicated stream; h2d_fence() makes every later launch wait for
+    // the copies enqueued so far.  d2h_gather() packs rows (after everything enqueued on the
+    // compute stream) into a device buffer and copies it to `pinned_dst` on a third stream;
+    // h2d_after_d2h() then copies `n` bytes of it back (the received-recovery direction).
+    struct GatherDesc { uint32_t row, len, out; };
+    bool enable_staging();
+    void h2d(uint64_t arena_offset, const void* pinned_src, size_t n);
+    void h2d_fence();
+    void d2h_gather(const std::vector<GatherDesc>& d, size_t bytes, void* pinned_dst);
+    void h2d_after_d2h(const void* pinned_src, size_t n);
+    void sync_staging();
+
     // Kernel timing with HIP events around every tamd_exec launch (on the launch stream).
     void set_timing(bool on) { timing_ = on; }
     DeviceStats& stats() { return stats_; }
@@ -73,6 +86,19 @@ private:
     uint32_t* d_gf_ = nullptr;
     uint8_t* d_zero_ = nullptr;
     uint32_t max_grid_ = 256;
+    // host staging
+    void* h2d_stream_ = nullptr;
+    void* d2h_stream_ = nullptr;
+    void* h2d_done_ = nullptr;   // hipEvent_t
+    void* gather_done_ = nullptr;
+    void* d2h_done_ = nullptr;
+    uint8_t* gather_dev_ = nullptr;  // packed rows
+    size_t gather_cap_ = 0;
+    uint8_t* recv_dev_ = nullptr;    // received-recovery landing area
+    size_t recv_cap_ = 0;
+    GatherDesc* gdesc_host_ = nullptr;
+    GatherDesc* gdesc_dev_ = nullptr;
+    size_t gdesc_cap_ = 0;
     void* stream_ = nullptr;
     // program staging: pinned host buffers and device buffers, double buffered
     struct Slot {

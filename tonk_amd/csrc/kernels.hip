@@ -385,6 +385,20 @@ extern "C" __global__ void tamd_gen_rows(const GenDesc* __restrict__ d, uint32_t
     for (uint32_t z = hb + len; z < cap; ++z) dst[z] = 0;
 }
 
+// Host staging (device.cpp d2h_gather): pack rows {arena row, bytes, output offset} into one
+// buffer for a single D2H copy.  One workgroup per row, 16-byte stores where aligned.
+struct GatherDesc { uint32_t row, len, out; };
+
+extern "C" __global__ void tamd_gather_rows(const GatherDesc* __restrict__ d, uint32_t n,
+                                            const uint8_t* __restrict__ arena, uint8_t* __restrict__ out) {
+    const GatherDesc g = d[blockIdx.x];
+    const uint8_t* src = arena + (size_t)g.row * TAMD_ROW_UNIT;  // rows are 64-B aligned
+    uint8_t* dst = out + g.out;                                   // outputs are 16-B aligned
+    const uint32_t n16 = g.len / 16u;
+    for (uint32_t i = threadIdx.x; i < n16; i += blockDim.x) ((uint4*)dst)[i] = ((const uint4*)src)[i];
+    for (uint32_t i = n16 * 16u + threadIdx.x; i < g.len; i += blockDim.x) dst[i] = src[i];
+}
+
 // Digest of rows (FNV-1a 64 over `len` bytes starting `skip` bytes into the row): one thread
 // per row, for output verification after a timed run (not on the timed path).
 struct DigestDesc { uint32_t row, skip, len, pad; };

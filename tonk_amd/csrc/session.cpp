@@ -11,6 +11,8 @@
 #include "device.h"
 #include "workload.h"
 
+#include <hip/hip_runtime.h>
+
 #include <chrono>
 #include <atomic>
 #include <algorithm>
@@ -49,6 +51,11 @@ struct Stream {
     std::vector<uint8_t> dec_row_used;
     SessTranscript tr;
     uint64_t alg_bytes = 0, payload_bytes = 0;
+    // stage_host: rows this step produced that leave through PCIe (recovery packets, recovered
+    // originals) and the recovery bytes the decoder received (which arrived through PCIe)
+    bool stage = false;
+    std::vector<std::pair<RowId, uint32_t>> out_rows;
+    uint64_t recv_bytes = 0;
 
     // ---- workload backend ----
     struct RecRef { RecoveryOut out; };
@@ -66,7 +73,10 @@ struct Stream {
     }
     int enc_encode(RecRef& r) {
         const Result rc = enc->encode(r.out);
-        if (rc == kSuccess) alg_bytes += r.out.total();
+        if (rc == kSuccess) {
+            alg_bytes += r.out.total();
+            if (stage) out_rows.push_back(std::make_pair(r.out.row, r.out.total()));
+        }
         return rc;
     }
     int enc_ack(const uint8_t* buf, uint32_t n, uint32_t* next) { return enc->acknowledge(buf, n, next); }
@@ -86,6 +96,7 @@ struct Stream {
         const Result rc = dec->add_recovery(r.out.row, r.out.total(), tail, nullptr, &took);
         if (!took) ctx->rows.free_deferred(r.out.row);
         alg_bytes += r.out.total();
+        recv_bytes += r.out.total();
         return rc;
     }
     int dec_is_ready() { return dec->is_ready(); }
@@ -97,6 +108,7 @@ struct Stream {
             for (RecoveredPacket* rp : got_) {
                 nums.push_back(rp->packet_num);
                 alg_bytes += rp->framed_upper;
+                if (stage) out_rows.push_back(std::make_pair(rp->row, rp->framed_upper));
                 if (tr.on) tr.pend_dec.push_back(SessTranscript::PendDec{rp->row, rp->framed_upper, tr.lines.size()});
             }
         }
@@ -156,6 +168,13 @@ struct Session {
     double host_ms[6] = {0, 0, 0, 0, 0, 0};
     uint32_t clock_msec = 0;  // packet send times of a step (RTO bookkeeping only)
     uint32_t row_cap = 0;
+    // stage_host: every stream's inputs (both sides, packet order) in pinned host memory, and
+    // the pinned landing buffer of a step's outgoing rows
+    uint8_t* host_in = nullptr;
+    size_t host_in_bytes = 0;
+    uint8_t* host_out = nullptr;
+    size_t host_out_cap = 0;
+    uint64_t h2d_bytes = 0, d2h_bytes = 0;
     bool finished = false;
     std::string error;
 
@@ -179,6 +198,9 @@ struct Session {
         cv_start.notify_all();
         for (auto& t : threads) t.join();
         dev.synchronize();
+        dev.sync_staging();
+        if (host_in) hipHostFree(host_in);
+        if (host_out) hipHostFree(host_out);
         for (auto& s : streams) {
             s->runner.reset();
             s->enc.reset();
@@ -254,6 +276,7 @@ struct Session {
         };
         const auto t0 = clk::now();
         clock_msec = (uint32_t)time_msec();
+        if (host_in && !finish) stage_inputs(originals);
         const uint64_t rel = completed_epoch();
         std::fill(busy_ms.begin(), busy_ms.end(), 0.0);
         run_all([this, originals, finish, rel, &ms](size_t i, size_t ti) {
@@ -282,7 +305,9 @@ struct Session {
             ctxs[i]->finish_flush();
         });
         const auto t3 = clk::now();
+        if (host_in) dev.h2d_fence();  // the program reads the rows copied in above
         last_ticket = dev.launch();
+        if (host_in) stage_outputs();
         const auto t4 = clk::now();
         host_ms[0] += ms(t0, t1);
         host_ms[2] += ms(t1, t2);
@@ -290,6 +315,60 @@ struct Session {
         host_ms[4] += ms(t3, t4);
         epoch_ticket.push_back(std::make_pair(epoch, last_ticket));
         if (prm.record) resolve_transcripts();
+    }
+
+    // H2D of the next `originals` input rows of every stream, both codec sides (each side's
+    // rows are one contiguous range of the arena in packet order, see generate()).
+    void stage_inputs(uint32_t originals) {
+        const size_t side_bytes = (size_t)streams[0]->p.n_originals * row_cap;
+        for (size_t i = 0; i < streams.size(); ++i) {
+            Stream& st = *streams[i];
+            const uint32_t next = (uint32_t)st.runner->summary().originals;
+            const uint32_t n = next + originals <= st.p.n_originals ? originals : st.p.n_originals - next;
+            if (!n) continue;
+            for (int side = 0; side < 2; ++side) {
+                const RowId r = (side ? st.dec_rows : st.enc_rows)[next];
+                const uint8_t* src = host_in + (2 * i + side) * side_bytes + (size_t)next * row_cap;
+                dev.h2d((uint64_t)st.ctx->rows.offset(r) * TAMD_ROW_UNIT, src, (size_t)n * row_cap);
+                h2d_bytes += (uint64_t)n * row_cap;
+            }
+        }
+    }
+
+    // D2H of the step's recovery packets and recovered originals (packed by a gather kernel
+    // after the step's program), then H2D of the recovery bytes the decoders received.
+    void stage_outputs() {
+        std::vector<Device::GatherDesc> d;
+        size_t bytes = 0, recv = 0;
+        for (auto& sp : streams) {
+            for (const auto& o : sp->out_rows) {
+                Device::GatherDesc g;
+                g.row = sp->ctx->rows.offset(o.first);
+                g.len = o.second;
+                g.out = (uint32_t)bytes;
+                d.push_back(g);
+                bytes += (o.second + 15u) & ~15u;
+            }
+            sp->out_rows.clear();
+            recv += sp->recv_bytes;
+            sp->recv_bytes = 0;
+        }
+        if (bytes > host_out_cap) {
+            dev.sync_staging();
+            if (host_out) hipHostFree(host_out);
+            host_out_cap = bytes + bytes / 2 + 4096;
+            if (hipHostMalloc((void**)&host_out, host_out_cap, hipHostMallocDefault) != hipSuccess) {
+                host_out = nullptr;
+                host_out_cap = 0;
+                error = "pinned staging allocation failed";
+                return;
+            }
+        }
+        dev.d2h_gather(d, bytes, host_out);
+        d2h_bytes += bytes;
+        if (recv > bytes) recv = bytes;
+        dev.h2d_after_d2h(host_out, recv);
+        h2d_bytes += recv;
     }
 
     void release_all() {
@@ -414,7 +493,33 @@ int tamd_session_generate(void* sp) {
         }
     }
     s->dev.generate_rows(d, s->row_cap);
-    return s->dev.error().empty() ? 0 : -2;
+    if (!s->dev.error().empty()) return -2;
+    if (s->prm.stage_host) {
+        // the pinned host copy of every input row: the bytes the steps copy in again
+        const size_t side_bytes = (size_t)s->streams[0]->p.n_originals * s->row_cap;
+        s->host_in_bytes = 2 * s->streams.size() * side_bytes;
+        if (!s->dev.enable_staging() ||
+            hipHostMalloc((void**)&s->host_in, s->host_in_bytes, hipHostMallocDefault) != hipSuccess) {
+            s->host_in = nullptr;
+            s->error = "pinned input staging allocation failed";
+            return -3;
+        }
+        for (size_t i = 0; i < s->streams.size(); ++i) {
+            Stream& st = *s->streams[i];
+            st.stage = true;
+            for (int side = 0; side < 2; ++side) {
+                const std::vector<RowId>& rows = side ? st.dec_rows : st.enc_rows;
+                const uint64_t base = st.ctx->rows.offset(rows[0]);
+                for (uint32_t k = 0; k < st.p.n_originals; ++k)
+                    if (st.ctx->rows.offset(rows[k]) != base + (uint64_t)k * (s->row_cap / TAMD_ROW_UNIT)) {
+                        s->error = "input rows are not contiguous";
+                        return -3;
+                    }
+                s->dev.download(s->host_in + (2 * i + side) * side_bytes, base * TAMD_ROW_UNIT, side_bytes);
+            }
+        }
+    }
+    return 0;
 }
 
 int tamd_session_step(void* sp, uint32_t originals) {
@@ -427,6 +532,7 @@ int tamd_session_step(void* sp, uint32_t originals) {
 int tamd_session_wait(void* sp) {
     Session* s = (Session*)sp;
     s->dev.synchronize();
+    s->dev.sync_staging();
     s->release_all();
     return s->dev.error().empty() && s->error.empty() ? 0 : -1;
 }
@@ -464,6 +570,8 @@ int tamd_session_summary(void* sp, uint64_t* out, unsigned n) {
     v[TAMD_SUM_UPLOAD_BYTES] = ds.upload_bytes;
     v[TAMD_SUM_ACC_BYTES] = ds.acc_bytes;
     v[TAMD_SUM_STORE_BYTES] = ds.store_bytes;
+    v[TAMD_SUM_H2D_BYTES] = s->h2d_bytes;
+    v[TAMD_SUM_D2H_BYTES] = s->d2h_bytes;
     if (n > TAMD_SUM_COUNT) n = TAMD_SUM_COUNT;
     for (unsigned i = 0; i < n; ++i) out[i] = v[i];
     return s->error.empty() ? 0 : -1;

@@ -11,9 +11,9 @@ timeout -k 10 600 python -m pytest tests -m gpu -x -q > "$OUT/gpu_tests.log" 2>&
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 &&
 timeout -k 10 900 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" &&
 cd /tmp && export TMPDIR=/tmp &&
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$TAG" -o run -- python3 "$R/bench.py" --no-cpu-baseline > "$OUT/bench_prof.json" 2> "$OUT/bench_prof.err" &&
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch_$TAG" -o run -- python3 "$R/bench.py" --no-cpu-baseline --steps 3 --warmup 1 > "$OUT/pmc_fetch.log" 2>&1 &&
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write_$TAG" -o run -- python3 "$R/bench.py" --no-cpu-baseline --steps 3 --warmup 1 > "$OUT/pmc_write.log" 2>&1 &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$TAG" -o run -- python3 "$R/bench.py" --no-cpu-baseline --no-end-to-end > "$OUT/bench_prof.json" 2> "$OUT/bench_prof.err" &&
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_fetch_$TAG" -o run -- python3 "$R/bench.py" --no-cpu-baseline --no-end-to-end --steps 3 --warmup 1 > "$OUT/pmc_fetch.log" 2>&1 &&
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/pmc_write_$TAG" -o run -- python3 "$R/bench.py" --no-cpu-baseline --no-end-to-end --steps 3 --warmup 1 > "$OUT/pmc_write.log" 2>&1 &&
 timeout -k 10 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d "$OUT/calib_fetch_$TAG" -o run -- "$R/tools/pmc_calib" > "$OUT/calib_fetch.log" 2>&1 &&
 timeout -k 10 120 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d "$OUT/calib_write_$TAG" -o run -- "$R/tools/pmc_calib" > "$OUT/calib_write.log" 2>&1 &&
 cd "$R" && python tools/pmc_traffic.py "$OUT/pmc_fetch_$TAG" "$OUT/pmc_write_$TAG" "$OUT/calib_fetch_$TAG" "$OUT/calib_write_$TAG" "$OUT/pmc_traffic_$TAG.json" > "$OUT/pmc_traffic.log" 2>&1
