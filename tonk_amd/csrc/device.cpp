@@ -7,7 +7,7 @@
 #include <stdlib.h>
 #include <string.h>
 
-extern "C" __global__ void tamd_exec(const tamd_op*, const tamd_instr*, const uint2*, uint32_t, uint8_t*,
+extern "C" __global__ void tamd_exec(const tamd_op*, const tamd_instr*, const uint2*, uint32_t, uint32_t, uint8_t*,
                                      const uint32_t*, const uint8_t*, unsigned long long*);
 extern "C" __global__ void tamd_gf_selftest(const uint32_t*, uint8_t*);
 extern "C" __global__ void tamd_gather_rows(const tamd::Device::GatherDesc*, uint32_t, const uint8_t*, uint8_t*);
@@ -174,6 +174,7 @@ void Device::begin(Context* const* ctxs, size_t n) {
     P.op_start.assign(n * B, 0);
     P.item_start.assign(n * B, 0);
     P.level_items.assign(L, 0);
+    P.level_coop.assign(L, 0);
     P.item_base.assign(L + 1, 0);
     P.instr_base.assign(n, 0);
     uint32_t op_at = 0, item_at = 0, instr_at = 0;
@@ -187,6 +188,7 @@ void Device::begin(Context* const* ctxs, size_t n) {
                 op_at += pb.level_ops()[b];
                 item_at += pb.level_items()[b];
                 P.level_items[b / TAMD_COST_CLASSES] += pb.level_items()[b];
+                if (b % TAMD_COST_CLASSES == 0) P.level_coop[b / TAMD_COST_CLASSES] += pb.level_items()[b];
             }
         }
     }
@@ -300,7 +302,11 @@ uint64_t Device::launch() {
             e1 = (hipEvent_t)timing_event();
             hipEventRecord(e0, st);
         }
+        // Class-0 ops are shared by a workgroup only in levels too small to fill the chip twice
+        // over with single-wave items; in the big levels they run as ordinary (first) items.
+        const uint32_t shared = cnt < 2u * 4u * max_grid_ ? P.level_coop[l] : 0u;
         hipLaunchKernelGGL(tamd_exec, dim3(grid), dim3(256), 0, st, dops, di, ditems + P.item_base[l], cnt,
+                           shared,
                            arena_, d_gf_, d_zero_, stamps ? stamps + 3 * P.item_base[l] : nullptr);
         if (timing_) {
             hipEventRecord(e1, st);

@@ -114,7 +114,7 @@ private:
         std::vector<Context*> ctxs;
         std::vector<uint32_t> instr_base;          // per context
         std::vector<uint32_t> op_start, item_start; // [context * levels + level]
-        std::vector<uint32_t> level_items, item_base;
+        std::vector<uint32_t> level_items, item_base, level_coop;  // level_coop: class-0 items (first)
         uint32_t levels = 0, buckets = 0;
         size_t n_instr = 0, n_ops = 0, n_items = 0, bytes_instr = 0, bytes_ops = 0, total = 0;
         Slot* slot = nullptr;

@@ -119,6 +119,7 @@ void ProgramBuilder::begin_op() {
     cur_span_ = 0;
     cur_full_ = ~0u;
     cur_runs_ = 0;
+    cur_pure_ = true;
     cur_level_in_ = 0;
     cur_written_begin_ = written_.size();
 }
@@ -126,6 +127,7 @@ void ProgramBuilder::begin_op() {
 void ProgramBuilder::op_acc3_off(uint32_t off, uint8_t c1, uint8_t c2, uint32_t len) {
     if (!len) return;
     tamd_instr in;
+    cur_pure_ = false;
     in.w0 = tamd_w0(TAMD_I_ACC3, c1, c2);
     in.row = off;
     in.len = len;
@@ -151,6 +153,7 @@ void ProgramBuilder::op_accr(uint32_t mode, uint32_t param, uint32_t row0, uint3
     instrs_.push_back(a);
     instrs_.push_back(r);
     ++cur_runs_;
+    if (mode == TAMD_R_LANE3) cur_pure_ = false;
     if (len > cur_span_) cur_span_ = len;
     if (len < cur_full_) cur_full_ = len;
     acc_bytes_ += (uint64_t)len * count;
@@ -170,6 +173,7 @@ uint32_t ProgramBuilder::finish_combine(RowId dst, uint32_t len, const uint8_t* 
 void ProgramBuilder::op_acc(RowId src, uint8_t coef, uint32_t len, uint32_t acc) {
     if (!coef || !len) return;
     tamd_instr in;
+    if (acc != 0) cur_pure_ = false;
     in.w0 = tamd_w0(TAMD_I_ACC, coef, acc);
     in.row = rows_->offset(src);
     in.len = len;
@@ -203,6 +207,7 @@ static void push_store(std::vector<tamd_instr>& v, uint32_t off, uint32_t len, u
 void ProgramBuilder::op_storec(RowId dst, uint32_t len, const uint8_t* c) {
     const uint32_t cap = rows_->cap_bytes(dst);
     tamd_instr s;
+    cur_pure_ = false;
     s.w0 = TAMD_I_STOREC | ((uint32_t)c[0] << 8) | ((uint32_t)c[1] << 16) | ((uint32_t)c[2] << 24);
     s.row = rows_->offset(dst);
     s.len = len;
@@ -215,6 +220,7 @@ void ProgramBuilder::op_storec(RowId dst, uint32_t len, const uint8_t* c) {
 }
 
 void ProgramBuilder::op_store(RowId dst, uint32_t len, uint32_t acc) {
+    cur_pure_ = false;  // (pure combines end with finish_combine / combine only)
     const uint32_t cap = rows_->cap_bytes(dst);
     push_store(instrs_, rows_->offset(dst), len, cap, nullptr, 0, acc);
     if (cap > cur_span_) cur_span_ = cap;
@@ -236,7 +242,7 @@ uint32_t ProgramBuilder::end_op(uint32_t min_level) {
     // (an ACCR run is `count` rows); class 0 is the most expensive and starts first.
     const uint64_t rows = (acc_bytes_ - cur_acc_begin_) / 1024u;
     const uint64_t cost = op.count + 4u * cur_runs_ + rows / 2u;
-    const uint32_t cls = cost >= 64 ? 0u : cost >= 32 ? 1u : cost >= 12 ? 2u : 3u;
+    const uint32_t cls = (cur_pure_ && rows >= 48) ? 0u : cost >= 64 ? 1u : cost >= 32 ? 2u : cost >= 12 ? 3u : 4u;
     const uint32_t bucket = TAMD_COST_CLASSES * level + cls;
     levels_.push_back(bucket);
     if (level_ops_.size() < TAMD_COST_CLASSES * (level + 1)) {

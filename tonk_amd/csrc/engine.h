@@ -153,6 +153,7 @@ private:
     uint32_t max_level_ = 0;
     // op under construction
     uint32_t cur_first_ = 0, cur_span_ = 0, cur_level_in_ = 0, cur_full_ = ~0u, cur_runs_ = 0;
+    bool cur_pure_ = true;  // only acc_0 sums and CONST/CAUCHY runs so far (see TAMD_COST_CLASSES)
     size_t cur_written_begin_ = 0;
     uint64_t acc_bytes_ = 0, store_bytes_ = 0, cur_acc_begin_ = 0;
 };

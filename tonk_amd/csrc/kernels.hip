@@ -129,10 +129,13 @@ __device__ __forceinline__ u64 mul8(u64 x, const PermT& p) {
 // table address stepping runs on the vector ALU: lane runs step the column value index
 // (cx = 3 + (199 col mod 253)) through the lane table, Cauchy runs fetch their inverses for the
 // whole batch first.
+// Batches of rows are numbered across the op (`unit`); with nw > 1 waves sharing the op, a
+// wave combines only the batches with unit mod nw == wid (the coefficient stepping still walks
+// every row).
 template <bool FULL>
 __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& r, uint32_t o,
                                          const uint8_t* __restrict__ arena, const uint32_t* __restrict__ lds,
-                                         u64& a0, u64& a1, u64& a2) {
+                                         uint32_t& unit, uint32_t nw, uint32_t wid, u64& a0, u64& a1, u64& a2) {
     const uint32_t mode = (a.w0 >> 8) & 0xffu, p = (a.w0 >> 16) & 0xffu;
     const uint32_t row0 = a.row, len = a.len, count = a.cap;
     const uint32_t stride = r.row, col0 = r.len, cstep = r.cap;
@@ -147,6 +150,14 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
         uint32_t t = vgpr(((199u * (col0 % 253u)) % 253u) * 48u);
         const uint32_t tstep = vgpr(((199u * (cstep % 253u)) % 253u) * 48u);
         for (uint32_t e = 0; e < count; e += TAMD_RBATCH) {
+            if ((unit++ & (nw - 1u)) != wid) {
+#pragma unroll
+                for (uint32_t q = 0; q < TAMD_RBATCH; ++q) {
+                    t += tstep;
+                    t = min(t, t - W);
+                }
+                continue;
+            }
             u64 d[TAMD_RBATCH];
 #pragma unroll
             for (uint32_t q = 0; q < TAMD_RBATCH; ++q) d[q] = TAMD_RUN_ROW(q);
@@ -171,6 +182,10 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
         const uint32_t cs = vgpr(cstep), px = vgpr(p + 64u);
         const uint8_t* inv = (const uint8_t*)(lds + TAMD_LDS_INV);
         for (uint32_t e = 0; e < count; e += TAMD_RBATCH) {
+            if ((unit++ & (nw - 1u)) != wid) {
+                col += cs * TAMD_RBATCH;
+                continue;
+            }
             u64 d[TAMD_RBATCH];
             uint32_t c[TAMD_RBATCH];
 #pragma unroll
@@ -187,6 +202,7 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
         const bool plain = p == 1u;
         const PermT cp = perm_at(lds, p * 8u);
         for (uint32_t e = 0; e < count; e += TAMD_RBATCH) {
+            if ((unit++ & (nw - 1u)) != wid) continue;
             u64 d[TAMD_RBATCH];
 #pragma unroll
             for (uint32_t q = 0; q < TAMD_RBATCH; ++q) d[q] = TAMD_RUN_ROW(q);
@@ -202,11 +218,17 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
 
 // One work item: the op's instruction list over this wave's 512-byte slice.  FULL items lie
 // below every length the op uses (op.full), so they need no per-lane length handling at all.
+//
+// Shared ops (nw = 4, the class-0 pure combines): every wave walks the instruction list, combines
+// only its share of the row batches and skips the final STORE; the caller reduces the waves'
+// acc_0 through LDS and stores.  Returns acc_0.
 template <bool FULL>
-__device__ __forceinline__ void run_item(const tamd_instr* __restrict__ instrs, uint32_t first, uint32_t end,
-                                         uint32_t o, uint32_t lane8, uint8_t* __restrict__ arena,
-                                         const uint8_t* __restrict__ zrow, const uint32_t* __restrict__ lds) {
+__device__ __forceinline__ u64 run_item(const tamd_instr* __restrict__ instrs, uint32_t first, uint32_t end,
+                                        uint32_t o, uint32_t lane8, uint8_t* __restrict__ arena,
+                                        const uint8_t* __restrict__ zrow, const uint32_t* __restrict__ lds,
+                                        uint32_t nw, uint32_t wid) {
     u64 a0 = 0, a1 = 0, a2 = 0;  // the op's three accumulators (program.h)
+    uint32_t unit = 0;
     for (uint32_t k = first; k < end;) {
         tamd_instr in[TAMD_BATCH];
 #pragma unroll
@@ -217,8 +239,12 @@ __device__ __forceinline__ void run_item(const tamd_instr* __restrict__ instrs, 
         for (uint32_t j = TAMD_BATCH; j-- > 0;)
             if ((in[j].w0 & 0xffu) == TAMD_I_ACCR && j < nb) nb = j;
         if (nb == 0) {
-            run_accr<FULL>(in[0], in[1], o, arena, lds, a0, a1, a2);  // in[1] is its RANGE word
+            run_accr<FULL>(in[0], in[1], o, arena, lds, unit, nw, wid, a0, a1, a2);  // in[1]: RANGE word
             k += 2;
+            continue;
+        }
+        if ((unit++ & (nw - 1u)) != wid) {  // another wave's batch (shared ops only)
+            k += nb;
             continue;
         }
         // Every slot of the batch loads: ACC/ACC3 their row, the others the zero row (no branches,
@@ -258,7 +284,7 @@ __device__ __forceinline__ void run_item(const tamd_instr* __restrict__ instrs, 
                 a0 ^= x;
                 a1 ^= ((u64)mul_sel(hi, c1) << 32) | mul_sel(lo, c1);
                 a2 ^= ((u64)mul_sel(hi, c2) << 32) | mul_sel(lo, c2);
-            } else if (kind == TAMD_I_STORE) {
+            } else if (kind == TAMD_I_STORE && nw == 1u) {
                 const uint32_t a = (w >> 16) & 0xffu;
                 const u64 x = a == 0 ? a0 : (a == 1 ? a1 : a2);
                 if (FULL) {
@@ -274,6 +300,7 @@ __device__ __forceinline__ void run_item(const tamd_instr* __restrict__ instrs, 
         }
         k += nb;
     }
+    return a0;
 }
 
 // Ops of one level never read a row written by an op of the same level, so every load of a
@@ -281,36 +308,75 @@ __device__ __forceinline__ void run_item(const tamd_instr* __restrict__ instrs, 
 // tables in LDS once and then claims items.
 extern "C" __global__ void __launch_bounds__(256)
 tamd_exec(const tamd_op* __restrict__ ops, const tamd_instr* __restrict__ instrs,
-          const uint2* __restrict__ items, uint32_t n_items, uint8_t* __restrict__ arena,
+          const uint2* __restrict__ items, uint32_t n_items, uint32_t n_shared, uint8_t* __restrict__ arena,
           const uint32_t* __restrict__ gf_perm, const uint8_t* __restrict__ zrow,
           unsigned long long* __restrict__ stamps) {
     __shared__ __attribute__((aligned(16))) uint32_t lds_perm[TAMD_GF_DWORDS];
+    __shared__ u64 partial[TAMD_WAVES_PER_WG][64];  // shared ops: the waves' acc_0
+    __shared__ uint32_t claim, shared_claim, shared_item;
     for (uint32_t i = threadIdx.x; i < TAMD_GF_DWORDS / 4; i += blockDim.x)
         ((uint4*)lds_perm)[i] = ((const uint4*)gf_perm)[i];
+    if (threadIdx.x == 0) claim = shared_claim = 0;
+    __syncthreads();
 
     const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = uniform(threadIdx.x >> 6);
+    const uint32_t lane8 = lane * TAMD_LANE_BYTES;
 
-    // Workgroup g owns items g, g + G, g + 2G, ... (a stratified sample of the level: items are
-    // ordered by cost class, most expensive first); its waves claim them one at a time through
-    // an LDS counter, so a wave that drew a long op does not hold up the others.
-    __shared__ uint32_t claim;
-    if (threadIdx.x == 0) claim = 0;
-    __syncthreads();
+    // Items [0, n_shared) are class-0 pure combines: the workgroup takes them one at a time
+    // (items g, g + G, ...), each wave combining every fourth batch of rows; wave 0 reduces the
+    // partial sums through LDS and executes the op's final STORE.
+    for (;;) {
+        if (threadIdx.x == 0) shared_item = shared_claim++;
+        __syncthreads();
+        const uint32_t it = blockIdx.x + shared_item * gridDim.x;
+        __syncthreads();  // every wave has read shared_item before it is claimed again
+        if (it >= n_shared) break;
+        const uint2 item = items[it];
+        const tamd_op op = ops[uniform(item.x)];
+        const uint32_t s0 = uniform(item.y) * TAMD_SLICE_BYTES;
+        const uint32_t o = s0 + lane8;
+        const uint32_t first = uniform(op.first), end = uniform(op.first + op.count);
+        const bool full = s0 + TAMD_SLICE_BYTES <= uniform(op.full);
+        const u64 t0 = stamps ? __builtin_amdgcn_s_memrealtime() : 0;
+        const u64 x = full ? run_item<true>(instrs, first, end, o, lane8, arena, zrow, lds_perm, TAMD_WAVES_PER_WG, wave)
+                           : run_item<false>(instrs, first, end, o, lane8, arena, zrow, lds_perm, TAMD_WAVES_PER_WG, wave);
+        partial[wave][lane] = x;
+        __syncthreads();
+        if (wave == 0) {
+            const u64 sum = partial[0][lane] ^ partial[1][lane] ^ partial[2][lane] ^ partial[3][lane];
+            const tamd_instr st = instrs[end - 2u], f = instrs[end - 1u];  // STORE (acc_0) + FOOTER
+            if (full) *(u64*)(arena + (size_t)st.row * TAMD_ROW_UNIT + o) = sum;
+            else store_slice(arena, st.row, st.len, st.cap, ((u64)f.len << 32) | f.row, o, sum);
+            if (stamps && lane == 0) {
+                __atomic_signal_fence(__ATOMIC_SEQ_CST);
+                stamps[3 * it] = t0;
+                stamps[3 * it + 1] = __builtin_amdgcn_s_memrealtime();
+                stamps[3 * it + 2] = ((u64)blockIdx.x << 32) | 4u;
+            }
+        }
+        // (the next claim's barriers order partial[] reuse)
+    }
+
+    // Items [n_shared, n_items): one wave per item.  Workgroup g owns items g, g + G, ... of
+    // them (a stratified sample of the level: ordered by cost class, most expensive first); its
+    // waves claim them one at a time through an LDS counter, so a wave that drew a long op does
+    // not hold up the others.
     for (;;) {
         uint32_t k = 0;
         if (lane == 0) k = atomicAdd(&claim, 1u);
-        const uint32_t it = blockIdx.x + uniform(__shfl(k, 0)) * gridDim.x;
+        const uint32_t it = n_shared + blockIdx.x + uniform(__shfl(k, 0)) * gridDim.x;
         if (it >= n_items) break;
         const uint2 item = items[it];
         const tamd_op op = ops[uniform(item.x)];
         const uint32_t s0 = uniform(item.y) * TAMD_SLICE_BYTES;
-        const uint32_t o = s0 + lane * TAMD_LANE_BYTES;
+        const uint32_t o = s0 + lane8;
         const uint32_t first = uniform(op.first), end = uniform(op.first + op.count);
         const u64 t0 = stamps ? __builtin_amdgcn_s_memrealtime() : 0;
         if (s0 + TAMD_SLICE_BYTES <= uniform(op.full))
-            run_item<true>(instrs, first, end, o, lane * TAMD_LANE_BYTES, arena, zrow, lds_perm);
+            run_item<true>(instrs, first, end, o, lane8, arena, zrow, lds_perm, 1u, 0u);
         else
-            run_item<false>(instrs, first, end, o, lane * TAMD_LANE_BYTES, arena, zrow, lds_perm);
+            run_item<false>(instrs, first, end, o, lane8, arena, zrow, lds_perm, 1u, 0u);
         if (stamps && lane == 0) {  // profiling only (TONK_AMD_STAMPS): vector stores of 100 MHz stamps
             __atomic_signal_fence(__ATOMIC_SEQ_CST);
             const u64 t1 = __builtin_amdgcn_s_memrealtime();

@@ -54,9 +54,11 @@ enum tamd_range_mode {
     TAMD_R_CONST  = 3,
 };
 
-// Ops of a level are grouped into cost classes (most expensive first) so the executor starts
-// the long dependency chains of a level before the short ops that fill in around them.
-#define TAMD_COST_CLASSES 4u
+// Ops of a level are grouped into classes: class 0 holds the long pure combines (ACC into acc_0,
+// CONST/CAUCHY runs, one final STORE), which a whole workgroup executes together (each wave
+// takes every fourth batch of rows, partial sums reduced through LDS); classes 1..4 hold the
+// other ops by cost, most expensive first, each run by one wave.  Long chains start first.
+#define TAMD_COST_CLASSES 5u
 
 #define TAMD_COLUMN_PERIOD 0x400000u  /* packet numbers are 22-bit (SiameseCommon.h:105) */
 
