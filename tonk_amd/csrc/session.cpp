@@ -23,6 +23,7 @@
 #include <string>
 #include <thread>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 using namespace tamd;
@@ -208,11 +209,16 @@ struct Session {
         }
     }
 
+    // Streams are handed out longest first (by their control-plane time in the previous step),
+    // so the step does not end waiting for one expensive stream picked up last.
+    std::vector<uint32_t> order;
+    std::vector<double> stream_ms;
+
     void drain(const std::function<void(size_t, size_t)>& f, size_t ti) {
         for (;;) {
             const size_t i = next_item.fetch_add(1);
             if (i >= streams.size()) break;
-            f(i, ti);
+            f(order.empty() ? i : order[i], ti);
         }
     }
 
@@ -279,6 +285,11 @@ struct Session {
         if (host_in && !finish) stage_inputs(originals);
         const uint64_t rel = completed_epoch();
         std::fill(busy_ms.begin(), busy_ms.end(), 0.0);
+        if (order.size() != streams.size()) {
+            order.resize(streams.size());
+            for (size_t i = 0; i < order.size(); ++i) order[i] = (uint32_t)i;
+            stream_ms.assign(streams.size(), 0.0);
+        }
         run_all([this, originals, finish, rel, &ms](size_t i, size_t ti) {
             const auto w0 = clk::now();
             Context& c = *ctxs[i];
@@ -286,8 +297,13 @@ struct Session {
             if (finish) streams[i]->runner->finish();
             else streams[i]->runner->advance(originals);
             c.prepare_flush();
-            busy_ms[ti] += ms(w0, clk::now());
+            const double t = ms(w0, clk::now());
+            busy_ms[ti] += t;
+            stream_ms[i] = t;
         });
+        static const bool lpt = getenv("TONK_AMD_STREAM_FIFO") == nullptr;  // A/B switch (profiling)
+        if (lpt)
+            std::sort(order.begin(), order.end(), [this](uint32_t a, uint32_t b) { return stream_ms[a] > stream_ms[b]; });
         const auto t1 = clk::now();
         double mx = 0;
         for (double b : busy_ms) {
