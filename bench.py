@@ -135,6 +135,61 @@ def end_to_end(threads: int, device: int, steps: int = 3, warmup: int = 1) -> di
                     "recovery packets and recovered originals, H2D of received recovery packets"}
 
 
+SINGLE_STREAM = {
+    # BASELINE.json configs[1]: one stream, 4096 originals, 1% loss, bit-exact vs CPU
+    "c2": dict(n=4096, loss=0.01, ack=64),
+    # BASELINE.json configs[4]: decoder stress, 65536 originals, 5% Gilbert-Elliott loss (mean
+    # burst 4), f = 10%, acks every 256, ARQ after 2048
+    "c5": dict(n=65536, loss=0.05, burst=4, fec=0.10, ack=256, arq=2048),
+}
+
+
+def single_stream(name: str, device: int, reps: int = 3) -> dict:
+    """One connection stream run start to finish (generate untimed; steps of 4096 originals,
+    end-of-stream flush and device sync timed), the median of `reps` fresh sessions, next to the
+    reference codec on one host thread over the same stream."""
+    wp = tonk_amd.WorkloadParams(payload=PAYLOAD, **SINGLE_STREAM[name])
+    times, payload, ok = [], 0, True
+    for _ in range(reps):
+        sess = tonk_amd.Session(wp, n_streams=1, device=device, threads=1, arena_bytes=(3 * wp.n * 1344) + (1 << 30))
+        try:
+            sess.generate()
+            sess.wait()
+            t0 = time.perf_counter()
+            done = 0
+            while done < wp.n:
+                sess.step(min(ORIGINALS_PER_STEP, wp.n - done))
+                done += ORIGINALS_PER_STEP
+            sess.finish()
+            t1 = time.perf_counter()
+            summ = sess.summary()
+        finally:
+            sess.close()
+        times.append(t1 - t0)
+        payload = summ["payload_bytes"]
+        ok = ok and summ["missing_at_end"] == 0 and summ["disabled_codecs"] == 0
+    times.sort()
+    dt = times[len(times) // 2]
+    out = {"metric": METRIC, "value": round(payload / dt / 2**30, 4), "unit": "GiB/s", "n_gpus": 1,
+           "ms_per_stream": round(dt * 1e3, 3), "higher_is_better": True, "dtype": "u8", "data": "synthetic",
+           "config": {"workload": f"BASELINE.json {name}: 1 stream", **SINGLE_STREAM[name], "payload_bytes": PAYLOAD},
+           "checks": {"all_recovered": ok}, "cpu_baseline": None}
+    exe = os.path.join(ROOT, "oracle", "_ref", "golden_gen")
+    if os.path.exists(exe):
+        def run(r: int) -> dict | None:
+            res = subprocess.run([exe, "time", "threads=1", "streams=1", f"reps={r}"] + wp.args(),
+                                 capture_output=True, text=True, timeout=600)
+            return json.loads(res.stdout.strip().splitlines()[-1]) if res.returncode == 0 else None
+        probe = run(1)
+        if probe:
+            r = int(min(200, max(1, round(3.0 / max(probe["seconds"], 1e-3)))))
+            j = run(r)
+            if j:
+                out["cpu_baseline"] = {"value": round(j["gib_per_s"], 4), "unit": "GiB/s", "cores": 1,
+                                       "kind": "reference", "sample": f"the same stream x {r} repetitions, 1 host thread"}
+    return out
+
+
 def stream_base(rank: int) -> int:
     """Weak scaling: rank r owns streams [64 r, 64 r + 64) -- disjoint, no data-path exchange."""
     return rank * STREAMS_PER_GPU
@@ -182,7 +237,12 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-end-to-end", action="store_true", help="skip the PCIe-inclusive side measurement")
+    ap.add_argument("--workload", choices=["c3"] + sorted(SINGLE_STREAM), default="c3",
+                    help="c3: the headline line (64 streams per GPU); c2 / c5: one stream, start to finish")
     a = ap.parse_args()
+    if a.workload != "c3":
+        print(json.dumps(single_stream(a.workload, int(os.environ.get("LOCAL_RANK", "0")))), flush=True)
+        return 0
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -119,6 +119,10 @@ int main(int argc, char** argv) {
         else if (k == "loss") p.loss_thresh = (uint32_t)v;
         else if (k == "fec") p.fec_rate_q16 = (uint32_t)v;
         else if (k == "ack") p.ack_every = (uint32_t)v;
+        else if (k == "ge") p.ge_enable = (uint32_t)v;
+        else if (k == "gb") p.gb_thresh = (uint32_t)v;
+        else if (k == "bg") p.bg_thresh = (uint32_t)v;
+        else if (k == "arq") p.arq_lag = (uint32_t)v;
     }
     Context ctx;
     ctx.rows.init(64ull << 30);
