@@ -975,45 +975,100 @@ bool Decoder::eliminate_original_data() {
     return !disabled_ && !ctx_->oom;
 }
 
-// Decoder::MultiplyLowerTriangle (:1065-1104)
+// Decoder::MultiplyLowerTriangle (:1065-1104), in coefficient space.  The reference adds row
+// ci (times the GE multiplier) into every later row; here those row operations run on the
+// L x L coefficients of the eliminated rows (tri_), which is O(L^3) byte operations instead of
+// O(L^3) symbolic term operations, and the rows' byte lengths follow the reference's
+// GrowZeroPadded.  Row ci's terms never reach past its length, so no clipping is lost.
 bool Decoder::multiply_lower_triangle() {
-    const uint32_t columns = cr_.lost_count;
-    for (uint32_t ci = 0; ci + 1 < columns; ++ci) {
-        Recovery* ri = mrows_[pivots_[ci]].rec;
-        sym_merge(ri->buf);  // row ci is final from here on; keep sources compact
-        const uint32_t src_bytes = ri->bytes;
-        for (uint32_t cj = ci + 1; cj < columns; ++cj) {
-            const uint32_t rj_index = pivots_[cj];
-            const uint8_t y = mat(rj_index, ci);
+    const uint32_t L = cr_.lost_count;
+    tri_.assign((size_t)L * L, 0);
+    tri_b_.resize(L);
+    for (uint32_t i = 0; i < L; ++i) {
+        tri_[(size_t)i * L + i] = 1;
+        Recovery* r = mrows_[pivots_[i]].rec;
+        sym_merge(r->buf);
+        tri_b_[i] = r->bytes;
+    }
+    for (uint32_t ci = 0; ci + 1 < L; ++ci) {
+        const uint8_t* src = &tri_[(size_t)ci * L];
+        for (uint32_t cj = ci + 1; cj < L; ++cj) {
+            const uint8_t y = mat(pivots_[cj], ci);
             if (y == 0) continue;
-            Recovery* rj = mrows_[rj_index].rec;
-            if (rj->bytes < src_bytes) rj->bytes = src_bytes;  // GrowZeroPadded
-            sym_add(rj->buf, ri->buf, src_bytes, y);
+            if (tri_b_[cj] < tri_b_[ci]) tri_b_[cj] = tri_b_[ci];  // GrowZeroPadded
+            uint8_t* dst = &tri_[(size_t)cj * L];
+            const uint8_t* my = g_gf.mul[y];
+            for (uint32_t k = 0; k <= ci; ++k)
+                if (src[k]) dst[k] ^= my[src[k]];
         }
     }
-    for (uint32_t ci = 0; ci < columns; ++ci) sym_merge(mrows_[pivots_[ci]].rec->buf);
     return true;
 }
 
-// Decoder::BackSubstitution (:1106-1238).  The recovered length is data dependent (the framed
-// header inside the recovered bytes); the symbolic solve uses the recovery row length, which
-// only adds zero bytes, and the exact length is read back with the data.
+// Decoder::BackSubstitution (:1106-1238).  Right to left, the recovered value of column ci is
+// inv(diag) * (row ci after the triangle + sum over later columns cj of M[ci][cj] * value_cj
+// clipped to row ci's length), exactly the reference's sequence of GF row operations and
+// min-length adds, accumulated as groups (eliminated row k, clip length, coefficient) -- one
+// group per (k, distinct length) -- and expanded into terms once per recovered row.  The
+// recovered length is data dependent (the framed header inside the recovered bytes); the
+// symbolic solve uses the recovery row length, which only adds zero bytes, and the exact length
+// is read back with the data.
 Result Decoder::back_substitution() {
-    const uint32_t columns = cr_.lost_count;
-    recovered_.assign(columns, RecoveredPacket());
+    const uint32_t L = cr_.lost_count;
+    recovered_.assign(L, RecoveredPacket());
+    tri_clips_.assign(tri_b_.begin(), tri_b_.end());
+    std::sort(tri_clips_.begin(), tri_clips_.end());
+    tri_clips_.erase(std::unique(tri_clips_.begin(), tri_clips_.end()), tri_clips_.end());
+    const uint32_t D = (uint32_t)tri_clips_.size();
+    auto clip_index = [this](uint32_t len) {
+        return (uint32_t)(std::lower_bound(tri_clips_.begin(), tri_clips_.end(), len) - tri_clips_.begin());
+    };
+    tri_groups_.clear();
+    tri_gstart_.assign((size_t)L + 1, 0);  // groups of column c: [tri_gstart_[c], tri_gstart_[c + 1])
+    // (columns are solved right to left; groups are appended in that order, so column c's
+    // range is recorded as it is produced and located through gpos)
+    std::vector<uint32_t>& gpos = tri_gstart_;
+    std::vector<uint32_t> gend(L, 0);
+    tri_acc_.resize((size_t)L * D);
     bool iterate = false;
-    for (int ci = (int)columns - 1; ci >= 0; --ci) {
+    for (int ci = (int)L - 1; ci >= 0; --ci) {
         const uint32_t ri = pivots_[ci];
         StoredOriginal* o = mcols_[ci].orig;
-        Recovery* rec = mrows_[ri].rec;
         const uint8_t y = mat(ri, (uint32_t)ci);
         if (y == 0) { disabled_ = true; return kDisabled; }
         const uint8_t inv_y = gf_inv(y);
-        const uint32_t bytes = rec->bytes;
+        const uint32_t bytes = tri_b_[ci];
+        const uint32_t bidx = clip_index(bytes);
+
+        std::fill(tri_acc_.begin(), tri_acc_.end(), 0);
+        const uint8_t* trow = &tri_[(size_t)ci * L];
+        for (uint32_t k = 0; k <= (uint32_t)ci; ++k)
+            if (trow[k]) tri_acc_[(size_t)k * D + bidx] ^= trow[k];
+        for (uint32_t cj = ci + 1; cj < L; ++cj) {
+            const uint8_t x = mat(ri, cj);
+            if (x == 0) continue;
+            const uint8_t* mx = g_gf.mul[x];
+            for (uint32_t g = gpos[cj]; g < gend[cj]; ++g) {
+                const Group& gr = tri_groups_[g];
+                const uint32_t c = gr.clip < bidx ? gr.clip : bidx;  // min(length) as index
+                tri_acc_[(size_t)gr.k * D + c] ^= mx[gr.coef];
+            }
+        }
+        gpos[ci] = (uint32_t)tri_groups_.size();
+        const uint8_t* my = g_gf.mul[inv_y];
+        for (uint32_t k = 0; k < L; ++k)
+            for (uint32_t c = 0; c < D; ++c) {
+                const uint8_t a = tri_acc_[(size_t)k * D + c];
+                if (a) tri_groups_.push_back(Group{k, c, my[a]});
+            }
+        gend[ci] = (uint32_t)tri_groups_.size();
 
         Sym& value = value_;
         value.clear();
-        sym_add(value, rec->buf, bytes, inv_y);
+        for (uint32_t g = gpos[ci]; g < gend[ci]; ++g) {
+            const Group& gr = tri_groups_[g];
+            sym_add(value, mrows_[pivots_[gr.k]].rec->buf, tri_clips_[gr.clip], gr.coef);
+        }
         sym_merge(value);
         const RowId out_row = ctx_->alloc(bytes);
         if (out_row == kNoRow) { disabled_ = true; return kDisabled; }
@@ -1027,8 +1082,6 @@ Result Decoder::back_substitution() {
         o->column = mcols_[ci].column;
         o->header_bytes = 0;
         o->owned = 1;
-        rec->buf.clear();
-        rec->bytes = 0;
 
         RecoveredPacket& rp = recovered_[ci];
         rp.packet_num = o->column;
@@ -1036,16 +1089,11 @@ Result Decoder::back_substitution() {
         rp.framed_upper = bytes;
         recovered_columns_.push_back(o->column);
         iterate |= mark_got(o->column);
-
-        for (uint32_t cj = 0; cj < (uint32_t)ci; ++cj) {
-            const uint32_t pj = pivots_[cj];
-            const uint8_t x = mat(pj, (uint32_t)ci);
-            if (x == 0) continue;
-            Recovery* bj = mrows_[pj].rec;
-            uint32_t add = bytes;
-            if (add > bj->bytes) add = bj->bytes;
-            sym_add(bj->buf, value, add, x);
-        }
+    }
+    for (uint32_t ci = 0; ci < L; ++ci) {
+        Recovery* rec = mrows_[pivots_[ci]].rec;
+        rec->buf.clear();
+        rec->bytes = 0;
     }
     if (!iterate) { disabled_ = true; return kDisabled; }
     iterate_next_expected(cr_.next_check_start);

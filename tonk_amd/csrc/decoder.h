@@ -128,6 +128,13 @@ private:
 
     uint32_t latest_column_ = 0;
     Sym prod_, value_;  // scratch
+    // Triangular solve in coefficient space (multiply_lower_triangle / back_substitution):
+    // tri_[j * L + k] = coefficient of eliminated row k in row j after the lower triangle,
+    // tri_b_[j] = row j's length; a recovered value is a list of groups (row k, clip, coef)
+    struct Group { uint32_t k, clip; uint8_t coef; };
+    std::vector<uint8_t> tri_, tri_acc_;
+    std::vector<uint32_t> tri_b_, tri_clips_, tri_gstart_;
+    std::vector<Group> tri_groups_;
 
     // helpers
     uint32_t to_element(uint32_t column) const { return col_sub(column, column_start_); }
