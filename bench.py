@@ -144,7 +144,7 @@ SINGLE_STREAM = {
 }
 
 
-def single_stream(name: str, device: int, reps: int = 3) -> dict:
+def single_stream(name: str, device: int, step: int, reps: int = 3) -> dict:
     """One connection stream run start to finish (generate untimed; steps of 4096 originals,
     end-of-stream flush and device sync timed), the median of `reps` fresh sessions, next to the
     reference codec on one host thread over the same stream."""
@@ -158,8 +158,8 @@ def single_stream(name: str, device: int, reps: int = 3) -> dict:
             t0 = time.perf_counter()
             done = 0
             while done < wp.n:
-                sess.step(min(ORIGINALS_PER_STEP, wp.n - done))
-                done += ORIGINALS_PER_STEP
+                sess.step(min(step, wp.n - done))
+                done += step
             sess.finish()
             t1 = time.perf_counter()
             summ = sess.summary()
@@ -172,7 +172,8 @@ def single_stream(name: str, device: int, reps: int = 3) -> dict:
     dt = times[len(times) // 2]
     out = {"metric": METRIC, "value": round(payload / dt / 2**30, 4), "unit": "GiB/s", "n_gpus": 1,
            "ms_per_stream": round(dt * 1e3, 3), "higher_is_better": True, "dtype": "u8", "data": "synthetic",
-           "config": {"workload": f"BASELINE.json {name}: 1 stream", **SINGLE_STREAM[name], "payload_bytes": PAYLOAD},
+           "config": {"workload": f"BASELINE.json {name}: 1 stream", **SINGLE_STREAM[name], "payload_bytes": PAYLOAD,
+                      "originals_per_step": step},
            "checks": {"all_recovered": ok}, "cpu_baseline": None}
     exe = os.path.join(ROOT, "oracle", "_ref", "golden_gen")
     if os.path.exists(exe):
@@ -239,9 +240,12 @@ def main() -> int:
     ap.add_argument("--no-end-to-end", action="store_true", help="skip the PCIe-inclusive side measurement")
     ap.add_argument("--workload", choices=["c3"] + sorted(SINGLE_STREAM), default="c3",
                     help="c3: the headline line (64 streams per GPU); c2 / c5: one stream, start to finish")
+    ap.add_argument("--step", type=int, default=0,
+                    help="c2 / c5: originals per device program (default 4096 for c2, 512 for c5)")
     a = ap.parse_args()
     if a.workload != "c3":
-        print(json.dumps(single_stream(a.workload, int(os.environ.get("LOCAL_RANK", "0")))), flush=True)
+        step = a.step or (512 if a.workload == "c5" else ORIGINALS_PER_STEP)
+        print(json.dumps(single_stream(a.workload, int(os.environ.get("LOCAL_RANK", "0")), step)), flush=True)
         return 0
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
