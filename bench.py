@@ -13,7 +13,7 @@ program on the GPU, pipelined with the host building the next step.  `value` is 
 payload GiB/s over all ranks; the timed region is bracketed by a barrier and a device sync.
 
 roofline: algorithmic HBM bytes (SURVEY.md s8(d) B_alg, counted exactly per step) divided by
-the summed duration of the tamd_exec launches of the timed steps (HIP events on the launch
+the summed duration of the executor (tamd_exec16) launches of the timed steps (HIP events on the launch
 stream), against the 8.0 TB/s HBM3E peak.  cpu_baseline: the reference codec (compiled from
 /root/reference by oracle/Makefile, shipped prebuilt in oracle/_ref) on the same workload
 sample, rank 0 only.
@@ -50,6 +50,8 @@ def host_threads(local_world: int) -> int:
         cpus = os.cpu_count() or 8
     per = max(1, cpus // max(1, local_world))
     env = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
+    if os.environ.get("TONK_AMD_HOST_THREADS"):  # A/B override (profiling)
+        return max(1, int(os.environ["TONK_AMD_HOST_THREADS"]))
     return max(1, min(16, per, env))
 
 
@@ -234,8 +236,8 @@ class Dist:
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-end-to-end", action="store_true", help="skip the PCIe-inclusive side measurement")
     ap.add_argument("--workload", choices=["c3"] + sorted(SINGLE_STREAM), default="c3",
@@ -325,7 +327,7 @@ def main() -> int:
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": round(traffic, 1) if traffic else None,
             "traffic_source": traffic_src,
-            "kernel": "tamd_exec",
+            "kernel": "tamd_exec" if os.environ.get("TONK_AMD_SLICE") == "512" else "tamd_exec16",
             "launches": launches,
             "avg_launch_us": round(kernel_ms * 1e3 / launches, 3) if launches else None,
             "alg_bytes_per_launch": round(alg / launches, 1) if launches else None,

@@ -9,6 +9,10 @@
 
 extern "C" __global__ void tamd_exec(const tamd_op*, const tamd_instr*, const uint2*, uint32_t, uint32_t, uint8_t*,
                                      const uint32_t*, const uint8_t*, unsigned long long*);
+extern "C" __global__ void tamd_exec16(const tamd_op*, const tamd_instr*, const uint2*, uint32_t, uint32_t, uint8_t*,
+                                       const uint32_t*, const uint8_t*, unsigned long long*);
+typedef void (*ExecFn)(const tamd_op*, const tamd_instr*, const uint2*, uint32_t, uint32_t, uint8_t*, const uint32_t*,
+                       const uint8_t*, unsigned long long*);
 extern "C" __global__ void tamd_gf_selftest(const uint32_t*, uint8_t*);
 extern "C" __global__ void tamd_gather_rows(const tamd::Device::GatherDesc*, uint32_t, const uint8_t*, uint8_t*);
 
@@ -76,7 +80,8 @@ bool Device::init(int device, uint64_t arena_bytes) {
     // Persistent grid: exactly the workgroups that are resident at once (occupancy x CUs), so
     // every workgroup stages the GF tables once and no workgroup starts late (kernels.hip).
     int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)tamd_exec, 256, 0) != hipSuccess ||
+    exec_kernel_ = slice_bytes() == TAMD_SLICE_BYTES ? (const void*)tamd_exec : (const void*)tamd_exec16;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, exec_kernel_, 256, 0) != hipSuccess ||
         per_cu < 1)
         per_cu = 1;
     // The occupancy API ignores the SGPR limit (MI355X_MICROARCH.md, Correctness boundaries): at
@@ -245,13 +250,14 @@ void Device::fill(size_t c) {
     }
     const std::vector<tamd_op>& ops = pb.ops();
     const std::vector<uint32_t>& lv = pb.op_levels();
+    const uint32_t sb = slice_bytes();
     for (size_t i = 0; i < ops.size(); ++i) {
         const uint32_t l = lv[i];
         tamd_op op = ops[i];
         op.first += ibase;
         const uint32_t oi = of[l]++;
         ho[oi] = op;
-        uint32_t slices = (op.span + TAMD_ITEM_BYTES - 1) / TAMD_ITEM_BYTES;
+        uint32_t slices = (op.span + sb - 1) / sb;
         if (!slices) slices = 1;
         uint32_t ii = itf[l];
         itf[l] += slices;
@@ -305,9 +311,9 @@ uint64_t Device::launch() {
         // Class-0 ops are shared by a workgroup only in levels too small to fill the chip twice
         // over with single-wave items; in the big levels they run as ordinary (first) items.
         const uint32_t shared = cnt < 2u * 4u * max_grid_ ? P.level_coop[l] : 0u;
-        hipLaunchKernelGGL(tamd_exec, dim3(grid), dim3(256), 0, st, dops, di, ditems + P.item_base[l], cnt,
-                           shared,
-                           arena_, d_gf_, d_zero_, stamps ? stamps + 3 * P.item_base[l] : nullptr);
+        const ExecFn fn = (ExecFn)exec_kernel_;
+        hipLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, st, dops, di, ditems + P.item_base[l], cnt, shared, arena_,
+                           d_gf_, d_zero_, stamps ? stamps + 3 * P.item_base[l] : nullptr);
         if (timing_) {
             hipEventRecord(e1, st);
             timing_events_.push_back(std::make_pair((void*)e0, (void*)e1));

@@ -2,9 +2,18 @@
 #include "engine.h"
 #include "prof.h"
 
+#include <stdlib.h>
 #include <string.h>
 
 namespace tamd {
+
+uint32_t slice_bytes() {
+    static const uint32_t b = [] {
+        const char* e = getenv("TONK_AMD_SLICE");
+        return (e && atoi(e) == (int)TAMD_SLICE_BYTES) ? TAMD_SLICE_BYTES : TAMD_SLICE_BYTES_WIDE;
+    }();
+    return b;
+}
 
 // ---------------------------------------------------------------------------------------------
 // RowTable
@@ -249,7 +258,8 @@ uint32_t ProgramBuilder::end_op(uint32_t min_level) {
         level_ops_.resize(TAMD_COST_CLASSES * (level + 1), 0);
         level_items_.resize(TAMD_COST_CLASSES * (level + 1), 0);
     }
-    const uint32_t slices = (op.span + TAMD_ITEM_BYTES - 1) / TAMD_ITEM_BYTES;
+    const uint32_t sb = slice_bytes();
+    const uint32_t slices = (op.span + sb - 1) / sb;
     level_ops_[bucket]++;
     level_items_[bucket] += slices ? slices : 1;
     for (size_t i = cur_written_begin_; i < written_.size(); ++i) rows_->set_level(written_[i], level);

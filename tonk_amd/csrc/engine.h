@@ -45,6 +45,10 @@ struct Term {
 // A symbolic buffer.  `terms` may contain duplicates; they are merged when materialized.
 typedef std::vector<Term> Sym;
 
+// Bytes of an op one device work item covers (program.h): TAMD_SLICE_BYTES_WIDE (tamd_exec16)
+// unless TONK_AMD_SLICE=512 selects the 8-byte-per-lane executor.  Fixed for the process.
+uint32_t slice_bytes();
+
 // ---------------------------------------------------------------------------------------------
 // Arena bookkeeping: rows are contiguous ranges of 64-byte units in one device allocation.
 // ---------------------------------------------------------------------------------------------
@@ -136,7 +140,7 @@ public:
     // Per op: its bucket, TAMD_COST_CLASSES * level + cost class (0 = most expensive).
     const std::vector<uint32_t>& op_levels() const { return levels_; }
     const std::vector<RowId>& written_rows() const { return written_; }
-    // Per bucket (see op_levels): op count and work-item count (TAMD_ITEM_BYTES chunks).
+    // Per bucket (see op_levels): op count and work-item count (slice_bytes() chunks).
     const std::vector<uint32_t>& level_ops() const { return level_ops_; }
     const std::vector<uint32_t>& level_items() const { return level_items_; }
 

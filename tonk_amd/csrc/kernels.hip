@@ -1,8 +1,8 @@
 // kernels.hip -- CDNA4 (gfx950) kernels of the Siamese engine.
 //
 // tamd_exec runs one level of a device program (program.h).  A work item is one op over a
-// 512-byte slice of its rows: one 64-lane wave owns 8 bytes per lane of the op's three
-// accumulators and walks the op's instruction list (wave-uniform, scalar loads).  GF(2^8)
+// slice of its rows (512 bytes, or 1024 in tamd_exec16): one 64-lane wave owns 8 (16) bytes per
+// lane of the op's three accumulators and walks the op's instruction list (wave-uniform, scalar loads).  GF(2^8)
 // multiplication by a wave-uniform coefficient uses three 8-entry product tables per
 // coefficient staged in LDS and v_perm_b32 byte lookups (x*c = T0[x&7] ^ T1[(x>>3)&7] ^
 // T2[x>>6]): ~11 VALU ops per dword, no divergent LDS gathers.  Coefficient 1 is a plain XOR.
@@ -13,11 +13,6 @@
 #include "program.h"
 
 #define TAMD_WAVES_PER_WG 4
-#define TAMD_LANE_BYTES 8
-#define TAMD_BATCH 8   // instructions whose loads are issued together (memory-level parallelism)
-#define TAMD_RBATCH 8  // rows of an ACCR run loaded together
-static_assert(TAMD_SLICE_BYTES == 64 * TAMD_LANE_BYTES, "one wave-wide load covers one slice");
-static_assert(TAMD_ITEM_BYTES == TAMD_SLICE_BYTES, "a work item is one slice");
 
 typedef unsigned long long u64;
 
@@ -124,6 +119,89 @@ __device__ __forceinline__ u64 mul8(u64 x, const PermT& p) {
     return ((u64)mul_sel(hi, p) << 32) | mul_sel(lo, p);
 }
 
+// A lane's bytes of a slice: NH 8-byte words.  NH = 1: 8 B per lane, 512-byte slices; NH = 2:
+// 16 B per lane, 1024-byte slices, one dwordx4 load per row (a 1302-byte row is two work items
+// instead of three, so the instruction walk, coefficient-table reads and selector math of an
+// item cover twice the bytes).
+typedef u64 u64x2 __attribute__((ext_vector_type(2)));
+template <int NH>
+struct LV {
+    u64 h[NH];
+    __device__ __forceinline__ LV& operator^=(const LV& b) {
+#pragma unroll
+        for (int i = 0; i < NH; ++i) h[i] ^= b.h[i];
+        return *this;
+    }
+};
+template <int NH>
+__device__ __forceinline__ LV<NH> lv_zero() {
+    LV<NH> r;
+#pragma unroll
+    for (int i = 0; i < NH; ++i) r.h[i] = 0;
+    return r;
+}
+template <int NH>
+__device__ __forceinline__ LV<NH> lv_load(const uint8_t* p) {
+    LV<NH> r;
+    if constexpr (NH == 1) {
+        r.h[0] = *(const u64*)p;
+    } else {
+        const u64x2 t = *(const u64x2*)p;
+        r.h[0] = t.x;
+        r.h[1] = t.y;
+    }
+    return r;
+}
+template <int NH>
+__device__ __forceinline__ void lv_store(uint8_t* p, const LV<NH>& v) {
+    if constexpr (NH == 1) {
+        *(u64*)p = v.h[0];
+    } else {
+        u64x2 t;
+        t.x = v.h[0];
+        t.y = v.h[1];
+        *(u64x2*)p = t;
+    }
+}
+// x with the bytes at or past `len` cleared (lane bytes start at offset o)
+template <bool FULL, int NH>
+__device__ __forceinline__ LV<NH> lv_keep(LV<NH> x, uint32_t o, uint32_t len) {
+    if (!FULL) {
+#pragma unroll
+        for (int i = 0; i < NH; ++i) x.h[i] &= keep_mask<false>(o + 8u * i, len);
+    }
+    return x;
+}
+template <int NH>
+__device__ __forceinline__ LV<NH> lv_mul(const LV<NH>& x, const PermT& p) {
+    LV<NH> r;
+#pragma unroll
+    for (int i = 0; i < NH; ++i) r.h[i] = mul8(x.h[i], p);
+    return r;
+}
+// acc_0 ^= x, acc_1 ^= c1 * x, acc_2 ^= c2 * x (one lane running-sum step, selectors shared)
+template <int NH>
+__device__ __forceinline__ void lv_acc3(const LV<NH>& x, const PermT& c1, const PermT& c2, LV<NH>& a0, LV<NH>& a1,
+                                        LV<NH>& a2) {
+#pragma unroll
+    for (int i = 0; i < NH; ++i) {
+        const Sel lo = sel4((uint32_t)x.h[i]), hi = sel4((uint32_t)(x.h[i] >> 32));
+        a0.h[i] ^= x.h[i];
+        a1.h[i] ^= ((u64)mul_sel(hi, c1) << 32) | mul_sel(lo, c1);
+        a2.h[i] ^= ((u64)mul_sel(hi, c2) << 32) | mul_sel(lo, c2);
+    }
+}
+template <bool FULL, int NH>
+__device__ __forceinline__ void lv_store_row(uint8_t* __restrict__ arena, uint32_t row, uint32_t len, uint32_t cap,
+                                             u64 footer, uint32_t o, const LV<NH>& x) {
+    if (FULL) {
+        lv_store<NH>(arena + (size_t)row * TAMD_ROW_UNIT + o, x);
+    } else {
+#pragma unroll
+        for (int i = 0; i < NH; ++i) store_slice(arena, row, len, cap, footer, o + 8u * i, x.h[i]);
+    }
+}
+
 // ACCR: a strided run of equally long rows (program.h).  TAMD_RBATCH row loads are issued
 // together (the row index is clamped to the run, so no load is branched around); the per-row
 // table address stepping runs on the vector ALU: lane runs step the column value index
@@ -132,18 +210,18 @@ __device__ __forceinline__ u64 mul8(u64 x, const PermT& p) {
 // Batches of rows are numbered across the op (`unit`); with nw > 1 waves sharing the op, a
 // wave combines only the batches with unit mod nw == wid (the coefficient stepping still walks
 // every row).
-template <bool FULL>
+template <bool FULL, int NH, uint32_t TAMD_RBATCH>
 __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& r, uint32_t o,
                                          const uint8_t* __restrict__ arena, const uint32_t* __restrict__ lds,
-                                         uint32_t& unit, uint32_t nw, uint32_t wid, u64& a0, u64& a1, u64& a2) {
+                                         uint32_t& unit, uint32_t nw, uint32_t wid, LV<NH>& a0, LV<NH>& a1,
+                                         LV<NH>& a2) {
     const uint32_t mode = (a.w0 >> 8) & 0xffu, p = (a.w0 >> 16) & 0xffu;
     const uint32_t row0 = a.row, len = a.len, count = a.cap;
     const uint32_t stride = r.row, col0 = r.len, cstep = r.cap;
-    const u64 keep = keep_mask<FULL>(o, len);
     const uint8_t* src = arena + (size_t)row0 * TAMD_ROW_UNIT + load_off<FULL>(o, len);
     const size_t step = (size_t)stride * TAMD_ROW_UNIT;
     // loads past the run's end re-read its last row (never consumed)
-#define TAMD_RUN_ROW(q) (*(const u64*)(src + (size_t)min(e + (q), count - 1u) * step))
+#define TAMD_RUN_ROW(q) lv_load<NH>(src + (size_t)min(e + (q), count - 1u) * step)
     if (mode == TAMD_R_LANE3) {
         // byte offset of the (cx, cx^2) tables in the lane table: 48 bytes per column value index
         const uint32_t W = 253u * 48u;
@@ -158,7 +236,7 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
                 }
                 continue;
             }
-            u64 d[TAMD_RBATCH];
+            LV<NH> d[TAMD_RBATCH];
 #pragma unroll
             for (uint32_t q = 0; q < TAMD_RBATCH; ++q) d[q] = TAMD_RUN_ROW(q);
 #pragma unroll
@@ -166,11 +244,7 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
                 if (e + q < count) {
                     const uint32_t ti = TAMD_LDS_LANE + (t >> 2);
                     const PermT c1 = perm_at(lds, ti), c2 = perm_at_hi(lds, ti + 6u);
-                    const u64 x = FULL ? d[q] : (d[q] & keep);
-                    const Sel lo = sel4((uint32_t)x), hi = sel4((uint32_t)(x >> 32));
-                    a0 ^= x;
-                    a1 ^= ((u64)mul_sel(hi, c1) << 32) | mul_sel(lo, c1);
-                    a2 ^= ((u64)mul_sel(hi, c2) << 32) | mul_sel(lo, c2);
+                    lv_acc3<NH>(lv_keep<FULL, NH>(d[q], o, len), c1, c2, a0, a1, a2);
                     t += tstep;
                     t = min(t, t - W);  // t - W wraps above t while t < W
                 }
@@ -186,7 +260,7 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
                 col += cs * TAMD_RBATCH;
                 continue;
             }
-            u64 d[TAMD_RBATCH];
+            LV<NH> d[TAMD_RBATCH];
             uint32_t c[TAMD_RBATCH];
 #pragma unroll
             for (uint32_t q = 0; q < TAMD_RBATCH; ++q) {
@@ -196,38 +270,38 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
             }
 #pragma unroll
             for (uint32_t q = 0; q < TAMD_RBATCH; ++q)
-                if (e + q < count) a0 ^= mul8(FULL ? d[q] : (d[q] & keep), perm_at(lds, c[q] * 8u));
+                if (e + q < count) a0 ^= lv_mul<NH>(lv_keep<FULL, NH>(d[q], o, len), perm_at(lds, c[q] * 8u));
         }
     } else {
         const bool plain = p == 1u;
         const PermT cp = perm_at(lds, p * 8u);
         for (uint32_t e = 0; e < count; e += TAMD_RBATCH) {
             if ((unit++ & (nw - 1u)) != wid) continue;
-            u64 d[TAMD_RBATCH];
+            LV<NH> d[TAMD_RBATCH];
 #pragma unroll
             for (uint32_t q = 0; q < TAMD_RBATCH; ++q) d[q] = TAMD_RUN_ROW(q);
-            u64 x = 0;
+            LV<NH> x = lv_zero<NH>();
 #pragma unroll
             for (uint32_t q = 0; q < TAMD_RBATCH; ++q)
-                if (e + q < count) x ^= FULL ? d[q] : (d[q] & keep);
-            a0 ^= plain ? x : mul8(x, cp);  // one coefficient: sum the batch's rows, one product
+                if (e + q < count) x ^= lv_keep<FULL, NH>(d[q], o, len);
+            a0 ^= plain ? x : lv_mul<NH>(x, cp);  // one coefficient: sum the batch's rows, one product
         }
     }
 #undef TAMD_RUN_ROW
 }
 
-// One work item: the op's instruction list over this wave's 512-byte slice.  FULL items lie
-// below every length the op uses (op.full), so they need no per-lane length handling at all.
+// One work item: the op's instruction list over this wave's slice.  FULL items lie below every
+// length the op uses (op.full), so they need no per-lane length handling at all.
 //
 // Shared ops (nw = 4, the class-0 pure combines): every wave walks the instruction list, combines
 // only its share of the row batches and skips the final STORE; the caller reduces the waves'
 // acc_0 through LDS and stores.  Returns acc_0.
-template <bool FULL>
-__device__ __forceinline__ u64 run_item(const tamd_instr* __restrict__ instrs, uint32_t first, uint32_t end,
-                                        uint32_t o, uint32_t lane8, uint8_t* __restrict__ arena,
-                                        const uint8_t* __restrict__ zrow, const uint32_t* __restrict__ lds,
-                                        uint32_t nw, uint32_t wid) {
-    u64 a0 = 0, a1 = 0, a2 = 0;  // the op's three accumulators (program.h)
+template <bool FULL, int NH, uint32_t TAMD_BATCH>
+__device__ __forceinline__ LV<NH> run_item(const tamd_instr* __restrict__ instrs, uint32_t first, uint32_t end,
+                                           uint32_t o, uint32_t laneb, uint8_t* __restrict__ arena,
+                                           const uint8_t* __restrict__ zrow, const uint32_t* __restrict__ lds,
+                                           uint32_t nw, uint32_t wid) {
+    LV<NH> a0 = lv_zero<NH>(), a1 = lv_zero<NH>(), a2 = lv_zero<NH>();  // the op's accumulators (program.h)
     uint32_t unit = 0;
     for (uint32_t k = first; k < end;) {
         tamd_instr in[TAMD_BATCH];
@@ -239,7 +313,7 @@ __device__ __forceinline__ u64 run_item(const tamd_instr* __restrict__ instrs, u
         for (uint32_t j = TAMD_BATCH; j-- > 0;)
             if ((in[j].w0 & 0xffu) == TAMD_I_ACCR && j < nb) nb = j;
         if (nb == 0) {
-            run_accr<FULL>(in[0], in[1], o, arena, lds, unit, nw, wid, a0, a1, a2);  // in[1]: RANGE word
+            run_accr<FULL, NH, TAMD_BATCH>(in[0], in[1], o, arena, lds, unit, nw, wid, a0, a1, a2);  // in[1]: RANGE word
             k += 2;
             continue;
         }
@@ -249,53 +323,49 @@ __device__ __forceinline__ u64 run_item(const tamd_instr* __restrict__ instrs, u
         }
         // Every slot of the batch loads: ACC/ACC3 their row, the others the zero row (no branches,
         // no exec changes; the values are never consumed).
-        u64 v[TAMD_BATCH];
+        LV<NH> v[TAMD_BATCH];
 #pragma unroll
         for (uint32_t j = 0; j < TAMD_BATCH; ++j) {
             const uint32_t kind = in[j].w0 & 0xffu;
             const bool ld = j < nb && (kind == TAMD_I_ACC || kind == TAMD_I_ACC3);
             const uint8_t* p = ld ? arena + (size_t)in[j].row * TAMD_ROW_UNIT + load_off<FULL>(o, in[j].len)
-                                  : zrow + lane8;
-            v[j] = *(const u64*)p;
+                                  : zrow + laneb;
+            v[j] = lv_load<NH>(p);
         }
 #pragma unroll
         for (uint32_t j = 0; j < TAMD_BATCH; ++j) {
             const uint32_t w = in[j].w0, kind = j < nb ? (w & 0xffu) : 0u;
             if (kind == TAMD_I_ACC) {
-                u64 x = FULL ? v[j] : (v[j] & keep_mask<FULL>(o, in[j].len));
+                LV<NH> x = lv_keep<FULL, NH>(v[j], o, in[j].len);
                 const uint32_t coef = (w >> 8) & 0xffu;
-                if (coef != 1u) x = mul8(x, perm_at(lds, coef * 8u));
+                if (coef != 1u) x = lv_mul<NH>(x, perm_at(lds, coef * 8u));
                 const uint32_t a = (w >> 16) & 0xffu;
                 if (a == 0) a0 ^= x;
                 else if (a == 1) a1 ^= x;
                 else a2 ^= x;
             } else if (kind == TAMD_I_STOREC) {
                 const uint32_t c0 = (w >> 8) & 0xffu, c1 = (w >> 16) & 0xffu, c2 = w >> 24;
-                u64 x = 0;
-                if (c0 == 1u) x = a0; else if (c0) x = mul8(a0, perm_at(lds, c0 * 8u));
-                if (c1 == 1u) x ^= a1; else if (c1) x ^= mul8(a1, perm_at(lds, c1 * 8u));
-                if (c2 == 1u) x ^= a2; else if (c2) x ^= mul8(a2, perm_at(lds, c2 * 8u));
-                if (FULL) *(u64*)(arena + (size_t)in[j].row * TAMD_ROW_UNIT + o) = x;
-                else store_slice(arena, in[j].row, in[j].len, in[j].cap, 0, o, x);
+                LV<NH> x = lv_zero<NH>();
+                if (c0 == 1u) x = a0; else if (c0) x = lv_mul<NH>(a0, perm_at(lds, c0 * 8u));
+                if (c1 == 1u) x ^= a1; else if (c1) x ^= lv_mul<NH>(a1, perm_at(lds, c1 * 8u));
+                if (c2 == 1u) x ^= a2; else if (c2) x ^= lv_mul<NH>(a2, perm_at(lds, c2 * 8u));
+                lv_store_row<FULL, NH>(arena, in[j].row, in[j].len, in[j].cap, 0, o, x);
             } else if (kind == TAMD_I_ACC3) {
-                const u64 x = FULL ? v[j] : (v[j] & keep_mask<FULL>(o, in[j].len));
+                const LV<NH> x = lv_keep<FULL, NH>(v[j], o, in[j].len);
                 const PermT c1 = perm_at(lds, ((w >> 8) & 0xffu) * 8u), c2 = perm_at(lds, ((w >> 16) & 0xffu) * 8u);
-                const Sel lo = sel4((uint32_t)x), hi = sel4((uint32_t)(x >> 32));
-                a0 ^= x;
-                a1 ^= ((u64)mul_sel(hi, c1) << 32) | mul_sel(lo, c1);
-                a2 ^= ((u64)mul_sel(hi, c2) << 32) | mul_sel(lo, c2);
+                lv_acc3<NH>(x, c1, c2, a0, a1, a2);
             } else if (kind == TAMD_I_STORE && nw == 1u) {
                 const uint32_t a = (w >> 16) & 0xffu;
-                const u64 x = a == 0 ? a0 : (a == 1 ? a1 : a2);
+                const LV<NH> x = a == 0 ? a0 : (a == 1 ? a1 : a2);
                 if (FULL) {
-                    *(u64*)(arena + (size_t)in[j].row * TAMD_ROW_UNIT + o) = x;
+                    lv_store<NH>(arena + (size_t)in[j].row * TAMD_ROW_UNIT + o, x);
                 } else {
                     // the FOOTER word follows the STORE (possibly past this batch)
                     const tamd_instr f = instrs[k + j + 1];
-                    store_slice(arena, in[j].row, in[j].len, in[j].cap, ((u64)f.len << 32) | f.row, o, x);
+                    lv_store_row<false, NH>(arena, in[j].row, in[j].len, in[j].cap, ((u64)f.len << 32) | f.row, o, x);
                 }
             } else if (kind == TAMD_I_CLEAR) {
-                a0 = a1 = a2 = 0;
+                a0 = a1 = a2 = lv_zero<NH>();
             }
         }
         k += nb;
@@ -305,14 +375,15 @@ __device__ __forceinline__ u64 run_item(const tamd_instr* __restrict__ instrs, u
 
 // Ops of one level never read a row written by an op of the same level, so every load of a
 // batch can be issued before the batch's stores.  Persistent grid: each workgroup stages the
-// tables in LDS once and then claims items.
-extern "C" __global__ void __launch_bounds__(256)
-tamd_exec(const tamd_op* __restrict__ ops, const tamd_instr* __restrict__ instrs,
-          const uint2* __restrict__ items, uint32_t n_items, uint32_t n_shared, uint8_t* __restrict__ arena,
-          const uint32_t* __restrict__ gf_perm, const uint8_t* __restrict__ zrow,
-          unsigned long long* __restrict__ stamps) {
+// tables in LDS once and then claims items.  A slice is 64 lanes x 8*NH bytes.
+template <int NH, uint32_t B>
+__device__ __forceinline__ void exec_level(const tamd_op* __restrict__ ops, const tamd_instr* __restrict__ instrs,
+                                           const uint2* __restrict__ items, uint32_t n_items, uint32_t n_shared,
+                                           uint8_t* __restrict__ arena, const uint32_t* __restrict__ gf_perm,
+                                           const uint8_t* __restrict__ zrow, unsigned long long* __restrict__ stamps) {
+    constexpr uint32_t SLICE = 64u * 8u * NH;
     __shared__ __attribute__((aligned(16))) uint32_t lds_perm[TAMD_GF_DWORDS];
-    __shared__ u64 partial[TAMD_WAVES_PER_WG][64];  // shared ops: the waves' acc_0
+    __shared__ LV<NH> partial[TAMD_WAVES_PER_WG][64];  // shared ops: the waves' acc_0
     __shared__ uint32_t claim, shared_claim, shared_item;
     for (uint32_t i = threadIdx.x; i < TAMD_GF_DWORDS / 4; i += blockDim.x)
         ((uint4*)lds_perm)[i] = ((const uint4*)gf_perm)[i];
@@ -321,7 +392,7 @@ tamd_exec(const tamd_op* __restrict__ ops, const tamd_instr* __restrict__ instrs
 
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = uniform(threadIdx.x >> 6);
-    const uint32_t lane8 = lane * TAMD_LANE_BYTES;
+    const uint32_t laneb = lane * 8u * NH;
 
     // Items [0, n_shared) are class-0 pure combines: the workgroup takes them one at a time
     // (items g, g + G, ...), each wave combining every fourth batch of rows; wave 0 reduces the
@@ -334,20 +405,23 @@ tamd_exec(const tamd_op* __restrict__ ops, const tamd_instr* __restrict__ instrs
         if (it >= n_shared) break;
         const uint2 item = items[it];
         const tamd_op op = ops[uniform(item.x)];
-        const uint32_t s0 = uniform(item.y) * TAMD_SLICE_BYTES;
-        const uint32_t o = s0 + lane8;
+        const uint32_t s0 = uniform(item.y) * SLICE;
+        const uint32_t o = s0 + laneb;
         const uint32_t first = uniform(op.first), end = uniform(op.first + op.count);
-        const bool full = s0 + TAMD_SLICE_BYTES <= uniform(op.full);
+        const bool full = s0 + SLICE <= uniform(op.full);
         const u64 t0 = stamps ? __builtin_amdgcn_s_memrealtime() : 0;
-        const u64 x = full ? run_item<true>(instrs, first, end, o, lane8, arena, zrow, lds_perm, TAMD_WAVES_PER_WG, wave)
-                           : run_item<false>(instrs, first, end, o, lane8, arena, zrow, lds_perm, TAMD_WAVES_PER_WG, wave);
+        const LV<NH> x = full ? run_item<true, NH, B>(instrs, first, end, o, laneb, arena, zrow, lds_perm, TAMD_WAVES_PER_WG, wave)
+                              : run_item<false, NH, B>(instrs, first, end, o, laneb, arena, zrow, lds_perm, TAMD_WAVES_PER_WG, wave);
         partial[wave][lane] = x;
         __syncthreads();
         if (wave == 0) {
-            const u64 sum = partial[0][lane] ^ partial[1][lane] ^ partial[2][lane] ^ partial[3][lane];
+            LV<NH> sum = partial[0][lane];
+            sum ^= partial[1][lane];
+            sum ^= partial[2][lane];
+            sum ^= partial[3][lane];
             const tamd_instr st = instrs[end - 2u], f = instrs[end - 1u];  // STORE (acc_0) + FOOTER
-            if (full) *(u64*)(arena + (size_t)st.row * TAMD_ROW_UNIT + o) = sum;
-            else store_slice(arena, st.row, st.len, st.cap, ((u64)f.len << 32) | f.row, o, sum);
+            if (full) lv_store<NH>(arena + (size_t)st.row * TAMD_ROW_UNIT + o, sum);
+            else lv_store_row<false, NH>(arena, st.row, st.len, st.cap, ((u64)f.len << 32) | f.row, o, sum);
             if (stamps && lane == 0) {
                 __atomic_signal_fence(__ATOMIC_SEQ_CST);
                 stamps[3 * it] = t0;
@@ -369,14 +443,14 @@ tamd_exec(const tamd_op* __restrict__ ops, const tamd_instr* __restrict__ instrs
         if (it >= n_items) break;
         const uint2 item = items[it];
         const tamd_op op = ops[uniform(item.x)];
-        const uint32_t s0 = uniform(item.y) * TAMD_SLICE_BYTES;
-        const uint32_t o = s0 + lane8;
+        const uint32_t s0 = uniform(item.y) * SLICE;
+        const uint32_t o = s0 + laneb;
         const uint32_t first = uniform(op.first), end = uniform(op.first + op.count);
         const u64 t0 = stamps ? __builtin_amdgcn_s_memrealtime() : 0;
-        if (s0 + TAMD_SLICE_BYTES <= uniform(op.full))
-            run_item<true>(instrs, first, end, o, lane8, arena, zrow, lds_perm, 1u, 0u);
+        if (s0 + SLICE <= uniform(op.full))
+            run_item<true, NH, B>(instrs, first, end, o, laneb, arena, zrow, lds_perm, 1u, 0u);
         else
-            run_item<false>(instrs, first, end, o, lane8, arena, zrow, lds_perm, 1u, 0u);
+            run_item<false, NH, B>(instrs, first, end, o, laneb, arena, zrow, lds_perm, 1u, 0u);
         if (stamps && lane == 0) {  // profiling only (TONK_AMD_STAMPS): vector stores of 100 MHz stamps
             __atomic_signal_fence(__ATOMIC_SEQ_CST);
             const u64 t1 = __builtin_amdgcn_s_memrealtime();
@@ -386,6 +460,21 @@ tamd_exec(const tamd_op* __restrict__ ops, const tamd_instr* __restrict__ instrs
         }
     }
 }
+
+// tamd_exec16 (the default): 16 B per lane, 1024-byte slices, 6 rows per load batch (94 VGPRs,
+// 5 waves/SIMD).  tamd_exec (TONK_AMD_SLICE=512): 8 B per lane, 512-byte slices, 8 rows per
+// batch (74 VGPRs, 6 waves/SIMD).  Measured on the bench program: 61.6-62.2 us vs 62.7-63.5 us
+// per launch; 16 B per lane with 8-row batches (108 VGPRs, 4 waves/SIMD) took 67 us.
+#define TAMD_EXEC_KERNEL(name, NH, B)                                                                  \
+    extern "C" __global__ void __launch_bounds__(256)                                                   \
+    name(const tamd_op* __restrict__ ops, const tamd_instr* __restrict__ instrs,                       \
+         const uint2* __restrict__ items, uint32_t n_items, uint32_t n_shared, uint8_t* __restrict__ arena, \
+         const uint32_t* __restrict__ gf_perm, const uint8_t* __restrict__ zrow,                       \
+         unsigned long long* __restrict__ stamps) {                                                    \
+        exec_level<NH, B>(ops, instrs, items, n_items, n_shared, arena, gf_perm, zrow, stamps);       \
+    }
+TAMD_EXEC_KERNEL(tamd_exec, 1, 8)
+TAMD_EXEC_KERNEL(tamd_exec16, 2, 6)
 
 // GF self test: out[y * 256 + x] = x * y through the same v_perm path the executor uses.
 extern "C" __global__ void tamd_gf_selftest(const uint32_t* __restrict__ gf_perm, uint8_t* __restrict__ out) {

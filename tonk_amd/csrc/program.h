@@ -33,9 +33,10 @@
 #include <stdint.h>
 
 #define TAMD_ROW_UNIT 64u
-#define TAMD_SLICE_BYTES 512u  /* bytes one wave-wide load covers (64 lanes x 8 B) */
-#define TAMD_ITEM_SLICES 1u
-#define TAMD_ITEM_BYTES (TAMD_SLICE_BYTES * TAMD_ITEM_SLICES)  /* bytes of an op one work item (one wave) covers */
+/* A work item (one wave) covers one slice of an op: 512 bytes (8 B per lane, tamd_exec) or
+   1024 bytes (16 B per lane, tamd_exec16); the host picks one per process (tamd::slice_bytes). */
+#define TAMD_SLICE_BYTES 512u
+#define TAMD_SLICE_BYTES_WIDE 1024u
 
 enum tamd_instr_kind {
     TAMD_I_ACC    = 1,

@@ -1,8 +1,9 @@
-// pmc_calib.hip -- calibration for rocprofv3 FETCH_SIZE / WRITE_SIZE with tamd_exec's access
-// pattern (each wave reads/writes 512 contiguous bytes as 8 bytes per lane).  The guide's
-// gfx950 correction (FETCH_SIZE = half the bytes) is measured for 16-B/lane loads only; this
-// kernel moves a known byte count with 8-B/lane accesses so tools/pmc_traffic.py can scale the
-// counters of tamd_exec.  Sizes are far beyond the 256 MiB Infinity Cache.
+// pmc_calib.hip -- calibration for rocprofv3 FETCH_SIZE / WRITE_SIZE with the executors' access
+// patterns: tamd_exec reads/writes 512 contiguous bytes per wave as 8 bytes per lane,
+// tamd_exec16 1024 bytes as 16 bytes per lane.  These kernels move a known byte count with each
+// width so tools/pmc_traffic.py can scale the executor's counters by a measured factor (the
+// guide's gfx950 correction is stated for 16-B/lane loads).  Sizes are far beyond the 256 MiB
+// Infinity Cache.
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 
@@ -20,6 +21,26 @@ extern "C" __global__ void calib_write8(u64* __restrict__ dst, size_t n_words) {
         dst[i] = i;
 }
 
+typedef u64 u64x2 __attribute__((ext_vector_type(2)));
+
+extern "C" __global__ void calib_read16(const u64x2* __restrict__ src, size_t n_pairs, u64* __restrict__ sink) {
+    u64 acc = 0;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_pairs; i += (size_t)gridDim.x * blockDim.x) {
+        const u64x2 v = src[i];
+        acc ^= v.x ^ v.y;
+    }
+    if (acc == 0x123456789abcdefull) sink[0] = acc;
+}
+
+extern "C" __global__ void calib_write16(u64x2* __restrict__ dst, size_t n_pairs) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_pairs; i += (size_t)gridDim.x * blockDim.x) {
+        u64x2 v;
+        v.x = i;
+        v.y = ~i;
+        dst[i] = v;
+    }
+}
+
 int main() {
     const size_t read_bytes = 2ull << 30, write_bytes = 1ull << 30;
     u64 *src = nullptr, *dst = nullptr, *sink = nullptr;
@@ -32,9 +53,11 @@ int main() {
     for (int rep = 0; rep < 3; ++rep) {
         hipLaunchKernelGGL(calib_read8, dim3(4096), dim3(256), 0, 0, src, read_bytes / 8, sink);
         hipLaunchKernelGGL(calib_write8, dim3(4096), dim3(256), 0, 0, dst, write_bytes / 8);
+        hipLaunchKernelGGL(calib_read16, dim3(4096), dim3(256), 0, 0, (const u64x2*)src, read_bytes / 16, sink);
+        hipLaunchKernelGGL(calib_write16, dim3(4096), dim3(256), 0, 0, (u64x2*)dst, write_bytes / 16);
     }
     (void)hipDeviceSynchronize();
-    printf("{\"calib_read8_bytes\": %zu, \"calib_write8_bytes\": %zu}\n", read_bytes, write_bytes);
+    printf("{\"calib_read_bytes\": %zu, \"calib_write_bytes\": %zu}\n", read_bytes, write_bytes);
     (void)hipFree(src);
     (void)hipFree(dst);
     (void)hipFree(sink);

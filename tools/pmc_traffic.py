@@ -4,8 +4,8 @@ usage: python tools/pmc_traffic.py FETCH_DIR WRITE_DIR CALIB_FETCH_DIR CALIB_WRI
 
 FETCH_SIZE and WRITE_SIZE are collected in separate passes (they do not fit one TCC pass).  Both
 are in KiB.  The gfx950 correction is measured, not assumed: tools/pmc_calib.hip moves a known
-byte count with tamd_exec's access width (8 B per lane, 512 B per wave), and the ratio
-known/counted scales tamd_exec's counters.
+byte count with the executor's access width (tamd_exec: 8 B per lane; tamd_exec16: 16 B per
+lane), and the ratio known/counted scales the executor's counters.
 """
 from __future__ import annotations
 
@@ -35,7 +35,7 @@ def counters(d: str) -> dict:
 
 def pick(c: dict, prefix: str, counter: str) -> list:
     for k, v in c.items():
-        if k.startswith(prefix) and counter in v:
+        if k.split("(")[0].strip() == prefix and counter in v:
             return v[counter]
     return []
 
@@ -45,14 +45,16 @@ def main() -> int:
     out_path = sys.argv[5] if len(sys.argv) > 5 else None
     F, W, CF, CW = counters(fetch), counters(write), counters(cfetch), counters(cwrite)
     read_known, write_known = 2 << 30, 1 << 30
-    cr = pick(CF, "calib_read8", "FETCH_SIZE")
-    cw = pick(CW, "calib_write8", "WRITE_SIZE")
+    kernel = "tamd_exec16" if any(k.split("(")[0].strip() == "tamd_exec16" for k in F) else "tamd_exec"
+    width = "16" if kernel == "tamd_exec16" else "8"
+    cr = pick(CF, "calib_read" + width, "FETCH_SIZE")
+    cw = pick(CW, "calib_write" + width, "WRITE_SIZE")
     read_scale = read_known / (sorted(cr)[len(cr) // 2] * 1024.0) if cr else 2.0
     write_scale = write_known / (sorted(cw)[len(cw) // 2] * 1024.0) if cw else 1.0
-    fv = pick(F, "tamd_exec", "FETCH_SIZE")
-    wv = pick(W, "tamd_exec", "WRITE_SIZE")
+    fv = pick(F, kernel, "FETCH_SIZE")
+    wv = pick(W, kernel, "WRITE_SIZE")
     res = {
-        "kernel": "tamd_exec",
+        "kernel": kernel,
         "dispatches_fetch": len(fv),
         "dispatches_write": len(wv),
         "fetch_kib_avg": sum(fv) / len(fv) if fv else None,
