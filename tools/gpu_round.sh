@@ -7,7 +7,7 @@ OUT=${GRAFT_REPO_ROOT:-$PWD}/gpurun_out
 R=${GRAFT_REPO_ROOT:-$PWD}
 TAG=${1:-r01}
 mkdir -p "$OUT" && cd "$R" && make -C tools > "$OUT/tools_build.log" 2>&1 &&
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > "$OUT/gpu_tests.log" 2>&1 &&
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$OUT/gpu_tests.log" 2>&1 &&
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 &&
 timeout -k 10 900 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" &&
 cd /tmp && export TMPDIR=/tmp &&
