@@ -17,12 +17,14 @@ EXE = os.path.join(ROOT, "oracle", "_ref", "tonk", "unit_tests_amd")
 
 @pytest.mark.gpu
 @pytest.mark.skipif(not os.environ.get("TONK_AMD_TONK_UNIT_TESTS"),
-                    reason="opt-in (TONK_AMD_TONK_UNIT_TESTS=1): round 1 result is a timeout of Tonk's "
-                           "100-connection BWC test through the synchronous C ABI (DESIGN.md s5)")
+                    reason="opt-in (TONK_AMD_TONK_UNIT_TESTS=1): ~5 min on one MI355X (SUCCESS, "
+                           "profiles/r01_tonk_unit_tests_gpu.txt), longer than a parity test should run")
 def test_tonk_unit_tests_with_mi355x_codec():
     if not os.path.exists(EXE):
         pytest.skip("oracle/_ref/tonk/unit_tests_amd not built (needs /root/reference at build time)")
-    r = subprocess.run([EXE], stdin=subprocess.DEVNULL, capture_output=True, text=True, timeout=1200)
+    # the C ABI watchdog prints call/wait counts to stderr every 5 s (Tonk's own log is buffered)
+    env = dict(os.environ, TONK_AMD_CAPI_WATCH="5")
+    r = subprocess.run([EXE], stdin=subprocess.DEVNULL, capture_output=True, text=True, timeout=1200, env=env)
     log = r.stdout + r.stderr
     assert r.returncode == 0, log[-3000:]
     assert "SUCCESS" in log, log[-3000:]

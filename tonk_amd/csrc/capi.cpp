@@ -12,10 +12,14 @@
 #include "decoder.h"
 #include "device.h"
 
+#include <atomic>
+#include <chrono>
 #include <mutex>
+#include <thread>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <string>
 
 using namespace tamd;
 
@@ -31,6 +35,42 @@ struct Runtime {
 Runtime* g_rt = nullptr;
 std::mutex g_init_mu;
 
+// Call accounting for the watchdog (TONK_AMD_CAPI_WATCH=<seconds>): a thread prints to stderr how
+// many API calls and device waits ran, the longest lock wait, and whether a call is inside a
+// device wait right now -- to tell a slow path from a stuck one under a real caller (Tonk).
+std::atomic<uint64_t> g_calls{0}, g_waits{0}, g_wait_ns{0}, g_lock_wait_max_ns{0};
+std::atomic<int64_t> g_in_wait_since{0};
+int64_t now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+struct ApiLock {
+    std::unique_lock<std::mutex> lk;
+    ApiLock() : lk(g_rt->mu, std::defer_lock) {
+        if (!lk.try_lock()) {
+            const int64_t t0 = now_ns();
+            lk.lock();
+            const uint64_t w = (uint64_t)(now_ns() - t0);
+            uint64_t m = g_lock_wait_max_ns.load(std::memory_order_relaxed);
+            while (w > m && !g_lock_wait_max_ns.compare_exchange_weak(m, w)) {}
+        }
+        g_calls.fetch_add(1, std::memory_order_relaxed);
+    }
+};
+
+void watch_loop(double period_s) {
+    const int64_t start = now_ns();
+    for (;;) {
+        std::this_thread::sleep_for(std::chrono::duration<double>(period_s));
+        const int64_t since = g_in_wait_since.load();
+        fprintf(stderr, "[tonk_amd capi] t=%.1fs calls=%llu device_waits=%llu wait_ms=%.1f lock_wait_max_ms=%.2f%s\n",
+                (now_ns() - start) * 1e-9, (unsigned long long)g_calls.load(), (unsigned long long)g_waits.load(),
+                g_wait_ns.load() * 1e-6, g_lock_wait_max_ns.exchange(0) * 1e-6,
+                since ? (" IN DEVICE WAIT for " + std::to_string((now_ns() - since) / 1000000) + " ms").c_str() : "");
+    }
+}
+
 void release_host(void* host, void*) { free(host); }
 
 struct CEncoder {
@@ -45,13 +85,23 @@ struct CDecoder {
 
 uint64_t row_byte_offset(RowId r) { return (uint64_t)g_rt->ctx.rows.offset(r) * TAMD_ROW_UNIT; }
 
-// Runs the pending program and waits for it (caller holds the lock).
-void flush_locked() {
+// Enqueues the pending program (caller holds the lock); reads of its results may be enqueued
+// behind it with Device::download_async before flush_complete() waits once for all of it.
+void flush_enqueue() {
     Context& ctx = g_rt->ctx;
     ctx.prepare_flush();
     if (!ctx.pb.empty()) g_rt->dev.run(&ctx);
+}
+
+void flush_complete() {
+    Context& ctx = g_rt->ctx;
     const uint64_t done = ctx.epoch;
+    const int64_t t0 = now_ns();
+    g_in_wait_since.store(t0);
     g_rt->dev.synchronize();
+    g_in_wait_since.store(0);
+    g_waits.fetch_add(1, std::memory_order_relaxed);
+    g_wait_ns.fetch_add((uint64_t)(now_ns() - t0), std::memory_order_relaxed);
     ctx.finish_flush();
     ctx.rows.release_up_to(done);
 }
@@ -100,6 +150,10 @@ SIAMESE_EXPORT int siamese_init_(int version) {
     }
     g_rt->ctx.rows.init(g_rt->dev.arena_bytes(), 0);
     g_rt->ok = true;
+    if (const char* w = getenv("TONK_AMD_CAPI_WATCH")) {
+        const double period = atof(w) > 0 ? atof(w) : 5.0;
+        std::thread(watch_loop, period).detach();
+    }
     return Siamese_Success;
 }
 
@@ -107,7 +161,7 @@ SIAMESE_EXPORT int siamese_init_(int version) {
 
 SIAMESE_EXPORT SiameseEncoder siamese_encoder_create() {
     if (!g_rt || !g_rt->ok) return nullptr;
-    std::lock_guard<std::mutex> lk(g_rt->mu);
+    ApiLock lk;
     CEncoder* e = new (std::nothrow) CEncoder();
     if (!e) return nullptr;
     e->enc = new Encoder(&g_rt->ctx, 0, release_host, nullptr);
@@ -117,7 +171,7 @@ SIAMESE_EXPORT SiameseEncoder siamese_encoder_create() {
 SIAMESE_EXPORT void siamese_encoder_free(SiameseEncoder encoder_t) {
     CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
     if (!e) return;
-    std::lock_guard<std::mutex> lk(g_rt->mu);
+    ApiLock lk;
     delete e->enc;
     delete e;
 }
@@ -125,7 +179,7 @@ SIAMESE_EXPORT void siamese_encoder_free(SiameseEncoder encoder_t) {
 SIAMESE_EXPORT SiameseResult siamese_encoder_is_ready(SiameseEncoder encoder_t) {
     CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
     if (!e) return Siamese_InvalidInput;
-    std::lock_guard<std::mutex> lk(g_rt->mu);
+    ApiLock lk;
     if (e->enc->remaining_slots() <= 2) return Siamese_MaxPacketsReached;
     return Siamese_Success;
 }
@@ -134,7 +188,7 @@ SIAMESE_EXPORT SiameseResult siamese_encoder_add(SiameseEncoder encoder_t, Siame
     CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
     if (!e || !packet || !packet->Data || packet->DataBytes <= 0 || packet->DataBytes > SIAMESE_MAX_PACKET_BYTES)
         return Siamese_InvalidInput;
-    std::lock_guard<std::mutex> lk(g_rt->mu);
+    ApiLock lk;
     if (e->enc->disabled()) return Siamese_Disabled;
     if (e->enc->remaining_slots() <= 0) return Siamese_MaxPacketsReached;
     uint8_t* host = nullptr;
@@ -155,7 +209,7 @@ SIAMESE_EXPORT SiameseResult siamese_encoder_add(SiameseEncoder encoder_t, Siame
 SIAMESE_EXPORT SiameseResult siamese_encoder_get(SiameseEncoder encoder_t, SiameseOriginalPacket* packet) {
     CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
     if (!e || !packet || packet->PacketNum > SIAMESE_PACKET_NUM_MAX) return Siamese_InvalidInput;
-    std::lock_guard<std::mutex> lk(g_rt->mu);
+    ApiLock lk;
     const StoredOriginal* o = nullptr;
     const Result r = e->enc->get(packet->PacketNum, &o);
     if (r != kSuccess) {
@@ -171,7 +225,7 @@ SIAMESE_EXPORT SiameseResult siamese_encoder_get(SiameseEncoder encoder_t, Siame
 SIAMESE_EXPORT SiameseResult siamese_encoder_remove_before(SiameseEncoder encoder_t, unsigned packetNum) {
     CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
     if (!e || packetNum > SIAMESE_PACKET_NUM_MAX) return Siamese_InvalidInput;
-    std::lock_guard<std::mutex> lk(g_rt->mu);
+    ApiLock lk;
     e->enc->remove_before(packetNum);
     return Siamese_Success;
 }
@@ -180,7 +234,7 @@ SIAMESE_EXPORT SiameseResult siamese_encoder_ack(SiameseEncoder encoder_t, const
                                                  unsigned* nextExpectedPacketNum) {
     CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
     if (!e || !buffer || bytes < 1 || !nextExpectedPacketNum) return Siamese_InvalidInput;
-    std::lock_guard<std::mutex> lk(g_rt->mu);
+    ApiLock lk;
     uint32_t next = 0;
     const Result r = e->enc->acknowledge((const uint8_t*)buffer, bytes, &next);
     if (r == kSuccess) *nextExpectedPacketNum = next;
@@ -190,7 +244,7 @@ SIAMESE_EXPORT SiameseResult siamese_encoder_ack(SiameseEncoder encoder_t, const
 SIAMESE_EXPORT SiameseResult siamese_encoder_retransmit(SiameseEncoder encoder_t, SiameseOriginalPacket* original) {
     CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
     if (!e || !original) return Siamese_InvalidInput;
-    std::lock_guard<std::mutex> lk(g_rt->mu);
+    ApiLock lk;
     original->Data = nullptr;
     original->DataBytes = 0;
     const StoredOriginal* o = nullptr;
@@ -205,16 +259,17 @@ SIAMESE_EXPORT SiameseResult siamese_encoder_retransmit(SiameseEncoder encoder_t
 SIAMESE_EXPORT SiameseResult siamese_encode(SiameseEncoder encoder_t, SiameseRecoveryPacket* recovery) {
     CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
     if (!e || !recovery) return Siamese_InvalidInput;
-    std::lock_guard<std::mutex> lk(g_rt->mu);
+    ApiLock lk;
     RecoveryOut out;
     const Result r = e->enc->encode(out);
     if (r != kSuccess) {
         if (r == kNeedMoreData) recovery->DataBytes = 0;
         return (SiameseResult)r;
     }
-    flush_locked();
+    flush_enqueue();
     e->recovery.resize(out.total());
-    g_rt->dev.download(e->recovery.data(), row_byte_offset(out.row), out.total());
+    g_rt->dev.download_async(e->recovery.data(), row_byte_offset(out.row), out.total());
+    flush_complete();
     g_rt->ctx.rows.free_deferred(out.row);
     recovery->Data = e->recovery.data();
     recovery->DataBytes = out.total();
@@ -224,7 +279,7 @@ SIAMESE_EXPORT SiameseResult siamese_encode(SiameseEncoder encoder_t, SiameseRec
 SIAMESE_EXPORT SiameseResult siamese_encoder_stats(SiameseEncoder encoder_t, uint64_t* statsOut, unsigned statsCount) {
     CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
     if (!e || !statsOut || statsCount <= 0) return Siamese_InvalidInput;
-    std::lock_guard<std::mutex> lk(g_rt->mu);
+    ApiLock lk;
     e->enc->stats(statsOut, statsCount);
     return Siamese_Success;
 }
@@ -233,7 +288,7 @@ SIAMESE_EXPORT SiameseResult siamese_encoder_stats(SiameseEncoder encoder_t, uin
 
 SIAMESE_EXPORT SiameseDecoder siamese_decoder_create() {
     if (!g_rt || !g_rt->ok) return nullptr;
-    std::lock_guard<std::mutex> lk(g_rt->mu);
+    ApiLock lk;
     CDecoder* d = new (std::nothrow) CDecoder();
     if (!d) return nullptr;
     d->dec = new Decoder(&g_rt->ctx, 0, release_host, nullptr);
@@ -243,7 +298,7 @@ SIAMESE_EXPORT SiameseDecoder siamese_decoder_create() {
 SIAMESE_EXPORT void siamese_decoder_free(SiameseDecoder decoder_t) {
     CDecoder* d = reinterpret_cast<CDecoder*>(decoder_t);
     if (!d) return;
-    std::lock_guard<std::mutex> lk(g_rt->mu);
+    ApiLock lk;
     delete d->dec;
     delete d;
 }
@@ -254,7 +309,7 @@ SIAMESE_EXPORT SiameseResult siamese_decoder_add_original(SiameseDecoder decoder
         packet->PacketNum > SIAMESE_PACKET_NUM_MAX)
         return Siamese_InvalidInput;
     if (!packet->Data) return Siamese_InvalidInput;
-    std::lock_guard<std::mutex> lk(g_rt->mu);
+    ApiLock lk;
     if (d->dec->disabled()) return Siamese_Disabled;
     uint8_t* host = nullptr;
     RowId row = kNoRow;
@@ -276,7 +331,7 @@ SIAMESE_EXPORT SiameseResult siamese_decoder_add_recovery(SiameseDecoder decoder
     CDecoder* d = reinterpret_cast<CDecoder*>(decoder_t);
     if (!d || !packet || !packet->Data || packet->DataBytes <= 0 || packet->DataBytes > SIAMESE_MAX_PACKET_BYTES)
         return Siamese_InvalidInput;
-    std::lock_guard<std::mutex> lk(g_rt->mu);
+    ApiLock lk;
     if (d->dec->disabled()) return Siamese_Disabled;
     const uint32_t total = packet->DataBytes;
     const RowId row = g_rt->ctx.alloc(total);
@@ -292,7 +347,7 @@ SIAMESE_EXPORT SiameseResult siamese_decoder_add_recovery(SiameseDecoder decoder
 SIAMESE_EXPORT SiameseResult siamese_decoder_get(SiameseDecoder decoder_t, SiameseOriginalPacket* packet) {
     CDecoder* d = reinterpret_cast<CDecoder*>(decoder_t);
     if (!d || !packet || packet->PacketNum > SIAMESE_PACKET_NUM_MAX) return Siamese_InvalidInput;
-    std::lock_guard<std::mutex> lk(g_rt->mu);
+    ApiLock lk;
     StoredOriginal* o = nullptr;
     const Result r = d->dec->get(packet->PacketNum, &o);
     if (r != kSuccess) {
@@ -301,10 +356,11 @@ SIAMESE_EXPORT SiameseResult siamese_decoder_get(SiameseDecoder decoder_t, Siame
         return (SiameseResult)r;
     }
     if (!o->host) {  // recovered data not read back yet
-        flush_locked();
+        flush_enqueue();
         uint8_t* host = (uint8_t*)malloc(o->bytes);
-        if (!host) return Siamese_Disabled;
-        g_rt->dev.download(host, row_byte_offset(o->row), o->bytes);
+        if (!host) { flush_complete(); return Siamese_Disabled; }
+        g_rt->dev.download_async(host, row_byte_offset(o->row), o->bytes);
+        flush_complete();
         unsigned len = 0;
         const int hb = get_length_header(host, o->bytes, len);
         if (hb < 1 || len == 0 || (uint32_t)hb + len > o->bytes) { free(host); d->dec->set_disabled(); return Siamese_Disabled; }
@@ -320,7 +376,7 @@ SIAMESE_EXPORT SiameseResult siamese_decoder_get(SiameseDecoder decoder_t, Siame
 SIAMESE_EXPORT SiameseResult siamese_decoder_is_ready(SiameseDecoder decoder_t) {
     CDecoder* d = reinterpret_cast<CDecoder*>(decoder_t);
     if (!d) return Siamese_InvalidInput;
-    std::lock_guard<std::mutex> lk(g_rt->mu);
+    ApiLock lk;
     return (SiameseResult)d->dec->is_ready();
 }
 
@@ -328,7 +384,7 @@ SIAMESE_EXPORT SiameseResult siamese_decode(SiameseDecoder decoder_t, SiameseOri
                                             unsigned* countOut) {
     CDecoder* d = reinterpret_cast<CDecoder*>(decoder_t);
     if (!d || (!packetsPtrOut != !countOut)) return Siamese_InvalidInput;
-    std::lock_guard<std::mutex> lk(g_rt->mu);
+    ApiLock lk;
     if (packetsPtrOut) {
         *packetsPtrOut = nullptr;
         *countOut = 0;
@@ -336,32 +392,49 @@ SIAMESE_EXPORT SiameseResult siamese_decode(SiameseDecoder decoder_t, SiameseOri
     std::vector<RecoveredPacket*> got;
     const Result r = d->dec->decode(got);
     if (r != kSuccess) return (SiameseResult)r;
-    flush_locked();
-    d->out.clear();
+    flush_enqueue();
+    // every recovered row not read back yet: one D2H each behind the program, then one wait
+    std::vector<std::pair<StoredOriginal*, uint8_t*>> reads;
+    std::vector<StoredOriginal*> outs;
+    bool failed = false;
     for (RecoveredPacket* rp : got) {
         StoredOriginal* o = nullptr;
-        if (d->dec->get(rp->packet_num, &o) != kSuccess || !o) { d->dec->set_disabled(); return Siamese_Disabled; }
+        if (d->dec->get(rp->packet_num, &o) != kSuccess || !o) { failed = true; break; }
+        outs.push_back(o);
         if (!o->host) {
             const uint32_t upper = rp->framed_upper;
             uint8_t* host = (uint8_t*)malloc(upper ? upper : 1);
-            if (!host) { d->dec->set_disabled(); return Siamese_Disabled; }
-            g_rt->dev.download(host, row_byte_offset(rp->row), upper);
-            unsigned len = 0;
-            const int hb = get_length_header(host, upper, len);
-            // BackSubstitution's length check (SiameseDecoder.cpp:1139-1154).
-            if (hb < 1 || len == 0 || (uint32_t)hb + len > upper) {
-                free(host);
-                d->dec->set_disabled();
-                return Siamese_Disabled;
-            }
-            o->host = host;
-            o->header_bytes = (uint32_t)hb;
-            o->bytes = (uint32_t)hb + len;
+            if (!host) { failed = true; break; }
+            g_rt->dev.download_async(host, row_byte_offset(rp->row), upper);
+            reads.push_back(std::make_pair(o, host));
+            o->bytes = upper;  // the upper bound until the header is parsed below
         }
+    }
+    flush_complete();
+    for (auto& rd : reads) {
+        StoredOriginal* o = rd.first;
+        uint8_t* host = rd.second;
+        if (failed) { free(host); continue; }
+        const uint32_t upper = o->bytes;
+        unsigned len = 0;
+        const int hb = get_length_header(host, upper, len);
+        // BackSubstitution's length check (SiameseDecoder.cpp:1139-1154).
+        if (hb < 1 || len == 0 || (uint32_t)hb + len > upper) {
+            free(host);
+            failed = true;
+            continue;
+        }
+        o->host = host;
+        o->header_bytes = (uint32_t)hb;
+        o->bytes = (uint32_t)hb + len;
+    }
+    if (failed) { d->dec->set_disabled(); return Siamese_Disabled; }
+    d->out.clear();
+    for (size_t i = 0; i < got.size(); ++i) {
         SiameseOriginalPacket p;
-        p.PacketNum = rp->packet_num;
-        p.Data = (const unsigned char*)o->host + o->header_bytes;
-        p.DataBytes = o->bytes - o->header_bytes;
+        p.PacketNum = got[i]->packet_num;
+        p.Data = (const unsigned char*)outs[i]->host + outs[i]->header_bytes;
+        p.DataBytes = outs[i]->bytes - outs[i]->header_bytes;
         d->out.push_back(p);
     }
     if (packetsPtrOut) {
@@ -375,7 +448,7 @@ SIAMESE_EXPORT SiameseResult siamese_decoder_ack(SiameseDecoder decoder_t, void*
                                                  unsigned* usedBytes) {
     CDecoder* d = reinterpret_cast<CDecoder*>(decoder_t);
     if (!d || !buffer || !usedBytes || byteLimit < SIAMESE_ACK_MIN_BYTES) return Siamese_InvalidInput;
-    std::lock_guard<std::mutex> lk(g_rt->mu);
+    ApiLock lk;
     uint32_t used = 0;
     const Result r = d->dec->ack((uint8_t*)buffer, byteLimit, &used);
     *usedBytes = used;
@@ -385,7 +458,7 @@ SIAMESE_EXPORT SiameseResult siamese_decoder_ack(SiameseDecoder decoder_t, void*
 SIAMESE_EXPORT SiameseResult siamese_decoder_stats(SiameseDecoder decoder_t, uint64_t* statsOut, unsigned statsCount) {
     CDecoder* d = reinterpret_cast<CDecoder*>(decoder_t);
     if (!d || !statsOut || statsCount <= 0) return Siamese_InvalidInput;
-    std::lock_guard<std::mutex> lk(g_rt->mu);
+    ApiLock lk;
     d->dec->stats(statsOut, statsCount);
     return Siamese_Success;
 }

@@ -15,6 +15,8 @@ typedef void (*ExecFn)(const tamd_op*, const tamd_instr*, const uint2*, uint32_t
                        const uint8_t*, unsigned long long*);
 extern "C" __global__ void tamd_gf_selftest(const uint32_t*, uint8_t*);
 extern "C" __global__ void tamd_gather_rows(const tamd::Device::GatherDesc*, uint32_t, const uint8_t*, uint8_t*);
+struct ScatterDescDev { uint32_t row, len, src, pad; };
+extern "C" __global__ void tamd_scatter_rows(const ScatterDescDev*, uint32_t, const uint8_t*, uint8_t*);
 
 struct GenDescDev { uint32_t row, index, len, pad; unsigned long long seed; };
 struct DigestDescDev { uint32_t row, skip, len, pad; };
@@ -57,6 +59,7 @@ Device::~Device() {
     if (gdesc_dev_) hipFree(gdesc_dev_);
     if (gdesc_host_) hipHostFree(gdesc_host_);
     if (up_host_) hipHostFree(up_host_);
+    if (up_dev_) hipFree(up_dev_);
     if (up_event_) hipEventDestroy((hipEvent_t)up_event_);
     if (d_gf_) hipFree(d_gf_);
     if (d_zero_) hipFree(d_zero_);
@@ -122,6 +125,7 @@ bool Device::init(int device, uint64_t arena_bytes) {
     up_event_ = ue;
     up_cap_ = 4u << 20;
     HIPCHK(hipHostMalloc((void**)&up_host_, up_cap_, hipHostMallocDefault));
+    HIPCHK(hipMalloc((void**)&up_dev_, up_cap_));
     // Staging slots up front, each touched by one copy, so no step pays first-use costs.
     for (Slot& sl : slots_) {
         if (!ensure_slot(sl, 16u << 20)) { error_ = "program staging allocation failed"; return false; }
@@ -269,6 +273,7 @@ void Device::fill(size_t c) {
 }
 
 uint64_t Device::launch() {
+    flush_uploads();  // staged packets land before the program reads them
     Plan& P = plan_;
     const uint64_t ticket = ++ticket_;
     if (P.empty) {
@@ -388,34 +393,64 @@ void Device::wait(uint64_t ticket) {
 }
 
 void Device::synchronize() {
+    flush_uploads();
     HIPCHK(hipStreamSynchronize((hipStream_t)stream_));
     for (auto& p : inflight_) free_events_.push_back(p.second);
     inflight_.clear();
     completed_ = ticket_;
-    up_used_ = 0;
+    up_used_ = up_flushed_ = 0;
 }
 
 void Device::upload(uint64_t off, const void* src, size_t n) {
     if (n == 0) return;
     hipStream_t st = (hipStream_t)stream_;
-    if (n > up_cap_) {
+    const size_t desc_room = (up_pending_.size() + 1) * sizeof(ScatterDesc);
+    if (n + 16 + desc_room > up_cap_ / 2 || off % TAMD_ROW_UNIT != 0 || off / TAMD_ROW_UNIT > 0xffffffffull) {
+        synchronize();
         HIPCHK(hipMemcpyAsync(arena_ + off, src, n, hipMemcpyHostToDevice, st));
         HIPCHK(hipStreamSynchronize(st));
         return;
     }
-    if (up_used_ + n > up_cap_) {
-        synchronize();
-    }
+    // packets and (at flush) their descriptors share the staging buffer
+    if (up_used_ + n + 16 + desc_room > up_cap_) synchronize();
     memcpy(up_host_ + up_used_, src, n);
-    HIPCHK(hipMemcpyAsync(arena_ + off, up_host_ + up_used_, n, hipMemcpyHostToDevice, st));
-    up_used_ += (n + 63) & ~(size_t)63;
+    ScatterDesc d;
+    d.row = (uint32_t)(off / TAMD_ROW_UNIT);
+    d.len = (uint32_t)n;
+    d.src = (uint32_t)up_used_;
+    d.pad = 0;
+    up_pending_.push_back(d);
+    up_used_ += (n + 15) & ~(size_t)15;
+}
+
+void Device::flush_uploads() {
+    if (up_pending_.empty()) return;
+    hipStream_t st = (hipStream_t)stream_;
+    const uint32_t cnt = (uint32_t)up_pending_.size();
+    const size_t dbytes = cnt * sizeof(ScatterDesc);
+    memcpy(up_host_ + up_used_, up_pending_.data(), dbytes);
+    const size_t begin = up_flushed_;
+    const size_t end = up_used_ + dbytes;
+    HIPCHK(hipMemcpyAsync(up_dev_ + begin, up_host_ + begin, end - begin, hipMemcpyHostToDevice, st));
+    // descriptor sources are offsets into up_dev_ (the same offsets as in up_host_)
+    hipLaunchKernelGGL(tamd_scatter_rows, dim3(cnt), dim3(64), 0, st, (const ScatterDescDev*)(up_dev_ + up_used_), cnt,
+                       (const uint8_t*)up_dev_, arena_);
+    HIPCHK(hipGetLastError());
+    up_used_ = (end + 15) & ~(size_t)15;
+    up_flushed_ = up_used_;
+    up_pending_.clear();
 }
 
 void Device::download(void* dst, uint64_t off, size_t n) {
     if (n == 0) return;
-    hipStream_t st = (hipStream_t)stream_;
-    HIPCHK(hipMemcpyAsync(dst, arena_ + off, n, hipMemcpyDeviceToHost, st));
+    download_async(dst, off, n);
     synchronize();
+}
+
+void Device::download_async(void* dst, uint64_t off, size_t n) {
+    if (n == 0) return;
+    flush_uploads();
+    HIPCHK(hipMemcpyAsync(dst, arena_ + off, n, hipMemcpyDeviceToHost, (hipStream_t)stream_));
 }
 
 bool Device::enable_staging() {
@@ -445,6 +480,7 @@ void Device::h2d_fence() {
 }
 
 void Device::d2h_gather(const std::vector<GatherDesc>& d, size_t bytes, void* dst) {
+    flush_uploads();
     if (d.empty()) return;
     hipStream_t st = (hipStream_t)stream_;
     // the previous gather's copy-out must be done before the buffers are reused
@@ -498,6 +534,7 @@ void Device::sync_staging() {
 }
 
 void Device::generate_rows(const std::vector<GenDesc>& d, uint32_t row_cap) {
+    flush_uploads();
     if (d.empty()) return;
     hipStream_t st = (hipStream_t)stream_;
     GenDescDev* dd = nullptr;
@@ -511,6 +548,7 @@ void Device::generate_rows(const std::vector<GenDesc>& d, uint32_t row_cap) {
 }
 
 void Device::digest_rows(const std::vector<DigestDesc>& d, std::vector<uint64_t>& out) {
+    flush_uploads();
     out.assign(d.size(), 0);
     if (d.empty()) return;
     hipStream_t st = (hipStream_t)stream_;

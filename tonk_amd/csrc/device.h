@@ -49,9 +49,14 @@ public:
     void synchronize();
 
     // Host <-> arena copies (stream ordered).  upload() copies `src` into a pinned staging
-    // buffer first so the caller may reuse it immediately.
+    // buffer so the caller may reuse it immediately; staged packets reach the arena in one H2D
+    // copy + one tamd_scatter_rows launch, enqueued before the next program, download or sync
+    // (flush_uploads()).  download() is synchronous; download_async() only enqueues the copy
+    // (the destination is valid after synchronize()).
     void upload(uint64_t arena_offset, const void* src, size_t n);
-    void download(void* dst, uint64_t arena_offset, size_t n);  // synchronous
+    void flush_uploads();
+    void download(void* dst, uint64_t arena_offset, size_t n);
+    void download_async(void* dst, uint64_t arena_offset, size_t n);
 
     // Bench helpers (kernels.hip).
     struct GenDesc { uint32_t row, index, len, pad; uint64_t seed; };
@@ -127,9 +132,12 @@ private:
     std::vector<void*> free_events_;
     bool ticket_is_empty_ = false;
     void mark(uint64_t ticket);
-    // upload staging
+    // upload staging: packets at [up_flushed_, up_used_) of up_host_ are not enqueued yet
+    struct ScatterDesc { uint32_t row, len, src, pad; };
     uint8_t* up_host_ = nullptr;
-    size_t up_cap_ = 0, up_used_ = 0;
+    uint8_t* up_dev_ = nullptr;
+    size_t up_cap_ = 0, up_used_ = 0, up_flushed_ = 0;
+    std::vector<ScatterDesc> up_pending_;
     void* up_event_ = nullptr;
     bool timing_ = false;
     std::vector<std::pair<void*, void*>> timing_events_;

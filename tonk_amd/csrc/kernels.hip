@@ -554,6 +554,20 @@ extern "C" __global__ void tamd_gather_rows(const GatherDesc* __restrict__ d, ui
     for (uint32_t i = n16 * 16u + threadIdx.x; i < g.len; i += blockDim.x) dst[i] = src[i];
 }
 
+// Coalesced uploads of the siamese.h C ABI (Device::upload): packets staged back to back in one
+// buffer (16-B aligned), one workgroup per packet copies it into its arena row (64-B aligned).
+struct ScatterDesc { uint32_t row, len, src, pad; };
+
+extern "C" __global__ void tamd_scatter_rows(const ScatterDesc* __restrict__ d, uint32_t n,
+                                             const uint8_t* __restrict__ in, uint8_t* __restrict__ arena) {
+    const ScatterDesc g = d[blockIdx.x];
+    const uint8_t* src = in + g.src;
+    uint8_t* dst = arena + (size_t)g.row * TAMD_ROW_UNIT;
+    const uint32_t n16 = g.len / 16u;
+    for (uint32_t i = threadIdx.x; i < n16; i += blockDim.x) ((uint4*)dst)[i] = ((const uint4*)src)[i];
+    for (uint32_t i = n16 * 16u + threadIdx.x; i < g.len; i += blockDim.x) dst[i] = src[i];
+}
+
 // Digest of rows (FNV-1a 64 over `len` bytes starting `skip` bytes into the row): one thread
 // per row, for output verification after a timed run (not on the timed path).
 struct DigestDesc { uint32_t row, skip, len, pad; };
