@@ -40,14 +40,31 @@ std::mutex g_init_mu;
 // device wait right now -- to tell a slow path from a stuck one under a real caller (Tonk).
 std::atomic<uint64_t> g_calls{0}, g_waits{0}, g_wait_ns{0}, g_lock_wait_max_ns{0};
 std::atomic<int64_t> g_in_wait_since{0};
+bool g_watch = false;
+std::atomic<uint64_t> g_prepare_ns{0}, g_run_ns{0};
 int64_t now_ns() {
     return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
         .count();
 }
 
+// Per-entry-point accounting: calls and time spent holding the lock.
+struct Site {
+    const char* name;
+    std::atomic<uint64_t> calls{0}, held_ns{0};
+    Site* next;
+    explicit Site(const char* n);
+};
+std::atomic<Site*> g_sites{nullptr};
+Site::Site(const char* n) : name(n), next(nullptr) {
+    Site* head = g_sites.load();
+    do { next = head; } while (!g_sites.compare_exchange_weak(head, this));
+}
+
 struct ApiLock {
     std::unique_lock<std::mutex> lk;
-    ApiLock() : lk(g_rt->mu, std::defer_lock) {
+    Site& site;
+    int64_t t_in = 0;
+    explicit ApiLock(Site& s) : lk(g_rt->mu, std::defer_lock), site(s) {
         if (!lk.try_lock()) {
             const int64_t t0 = now_ns();
             lk.lock();
@@ -56,8 +73,16 @@ struct ApiLock {
             while (w > m && !g_lock_wait_max_ns.compare_exchange_weak(m, w)) {}
         }
         g_calls.fetch_add(1, std::memory_order_relaxed);
+        if (g_watch) t_in = now_ns();
+    }
+    ~ApiLock() {
+        site.calls.fetch_add(1, std::memory_order_relaxed);
+        if (g_watch) site.held_ns.fetch_add((uint64_t)(now_ns() - t_in), std::memory_order_relaxed);
     }
 };
+#define API_LOCK()                   \
+    static Site api_site_(__func__); \
+    ApiLock lk(api_site_)
 
 void watch_loop(double period_s) {
     const int64_t start = now_ns();
@@ -68,6 +93,15 @@ void watch_loop(double period_s) {
                 (now_ns() - start) * 1e-9, (unsigned long long)g_calls.load(), (unsigned long long)g_waits.load(),
                 g_wait_ns.load() * 1e-6, g_lock_wait_max_ns.exchange(0) * 1e-6,
                 since ? (" IN DEVICE WAIT for " + std::to_string((now_ns() - since) / 1000000) + " ms").c_str() : "");
+        fprintf(stderr, "[tonk_amd capi]   flush: prepare_ms=%.1f launch_ms=%.1f programs=%llu launches=%llu\n",
+                g_prepare_ns.load() * 1e-6, g_run_ns.load() * 1e-6, (unsigned long long)g_rt->dev.stats().programs,
+                (unsigned long long)g_rt->dev.stats().launches);
+        for (Site* st = g_sites.load(); st; st = st->next) {
+            const uint64_t c = st->calls.load();
+            if (c)
+                fprintf(stderr, "[tonk_amd capi]   %-28s calls=%llu held_ms=%.1f\n", st->name, (unsigned long long)c,
+                        st->held_ns.load() * 1e-6);
+        }
     }
 }
 
@@ -89,8 +123,14 @@ uint64_t row_byte_offset(RowId r) { return (uint64_t)g_rt->ctx.rows.offset(r) * 
 // behind it with Device::download_async before flush_complete() waits once for all of it.
 void flush_enqueue() {
     Context& ctx = g_rt->ctx;
+    const int64_t t0 = g_watch ? now_ns() : 0;
     ctx.prepare_flush();
+    const int64_t t1 = g_watch ? now_ns() : 0;
     if (!ctx.pb.empty()) g_rt->dev.run(&ctx);
+    if (g_watch) {
+        g_prepare_ns.fetch_add((uint64_t)(t1 - t0), std::memory_order_relaxed);
+        g_run_ns.fetch_add((uint64_t)(now_ns() - t1), std::memory_order_relaxed);
+    }
 }
 
 void flush_complete() {
@@ -149,9 +189,11 @@ SIAMESE_EXPORT int siamese_init_(int version) {
         return Siamese_Disabled;
     }
     g_rt->ctx.rows.init(g_rt->dev.arena_bytes(), 0);
+    g_rt->ctx.track_dirty = true;
     g_rt->ok = true;
     if (const char* w = getenv("TONK_AMD_CAPI_WATCH")) {
         const double period = atof(w) > 0 ? atof(w) : 5.0;
+        g_watch = true;
         std::thread(watch_loop, period).detach();
     }
     return Siamese_Success;
@@ -161,7 +203,7 @@ SIAMESE_EXPORT int siamese_init_(int version) {
 
 SIAMESE_EXPORT SiameseEncoder siamese_encoder_create() {
     if (!g_rt || !g_rt->ok) return nullptr;
-    ApiLock lk;
+    API_LOCK();
     CEncoder* e = new (std::nothrow) CEncoder();
     if (!e) return nullptr;
     e->enc = new Encoder(&g_rt->ctx, 0, release_host, nullptr);
@@ -171,7 +213,7 @@ SIAMESE_EXPORT SiameseEncoder siamese_encoder_create() {
 SIAMESE_EXPORT void siamese_encoder_free(SiameseEncoder encoder_t) {
     CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
     if (!e) return;
-    ApiLock lk;
+    API_LOCK();
     delete e->enc;
     delete e;
 }
@@ -179,7 +221,8 @@ SIAMESE_EXPORT void siamese_encoder_free(SiameseEncoder encoder_t) {
 SIAMESE_EXPORT SiameseResult siamese_encoder_is_ready(SiameseEncoder encoder_t) {
     CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
     if (!e) return Siamese_InvalidInput;
-    ApiLock lk;
+    API_LOCK();
+    g_rt->ctx.touch(e->enc);
     if (e->enc->remaining_slots() <= 2) return Siamese_MaxPacketsReached;
     return Siamese_Success;
 }
@@ -188,7 +231,8 @@ SIAMESE_EXPORT SiameseResult siamese_encoder_add(SiameseEncoder encoder_t, Siame
     CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
     if (!e || !packet || !packet->Data || packet->DataBytes <= 0 || packet->DataBytes > SIAMESE_MAX_PACKET_BYTES)
         return Siamese_InvalidInput;
-    ApiLock lk;
+    API_LOCK();
+    g_rt->ctx.touch(e->enc);
     if (e->enc->disabled()) return Siamese_Disabled;
     if (e->enc->remaining_slots() <= 0) return Siamese_MaxPacketsReached;
     uint8_t* host = nullptr;
@@ -209,7 +253,8 @@ SIAMESE_EXPORT SiameseResult siamese_encoder_add(SiameseEncoder encoder_t, Siame
 SIAMESE_EXPORT SiameseResult siamese_encoder_get(SiameseEncoder encoder_t, SiameseOriginalPacket* packet) {
     CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
     if (!e || !packet || packet->PacketNum > SIAMESE_PACKET_NUM_MAX) return Siamese_InvalidInput;
-    ApiLock lk;
+    API_LOCK();
+    g_rt->ctx.touch(e->enc);
     const StoredOriginal* o = nullptr;
     const Result r = e->enc->get(packet->PacketNum, &o);
     if (r != kSuccess) {
@@ -225,7 +270,8 @@ SIAMESE_EXPORT SiameseResult siamese_encoder_get(SiameseEncoder encoder_t, Siame
 SIAMESE_EXPORT SiameseResult siamese_encoder_remove_before(SiameseEncoder encoder_t, unsigned packetNum) {
     CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
     if (!e || packetNum > SIAMESE_PACKET_NUM_MAX) return Siamese_InvalidInput;
-    ApiLock lk;
+    API_LOCK();
+    g_rt->ctx.touch(e->enc);
     e->enc->remove_before(packetNum);
     return Siamese_Success;
 }
@@ -234,7 +280,8 @@ SIAMESE_EXPORT SiameseResult siamese_encoder_ack(SiameseEncoder encoder_t, const
                                                  unsigned* nextExpectedPacketNum) {
     CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
     if (!e || !buffer || bytes < 1 || !nextExpectedPacketNum) return Siamese_InvalidInput;
-    ApiLock lk;
+    API_LOCK();
+    g_rt->ctx.touch(e->enc);
     uint32_t next = 0;
     const Result r = e->enc->acknowledge((const uint8_t*)buffer, bytes, &next);
     if (r == kSuccess) *nextExpectedPacketNum = next;
@@ -244,7 +291,8 @@ SIAMESE_EXPORT SiameseResult siamese_encoder_ack(SiameseEncoder encoder_t, const
 SIAMESE_EXPORT SiameseResult siamese_encoder_retransmit(SiameseEncoder encoder_t, SiameseOriginalPacket* original) {
     CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
     if (!e || !original) return Siamese_InvalidInput;
-    ApiLock lk;
+    API_LOCK();
+    g_rt->ctx.touch(e->enc);
     original->Data = nullptr;
     original->DataBytes = 0;
     const StoredOriginal* o = nullptr;
@@ -259,7 +307,8 @@ SIAMESE_EXPORT SiameseResult siamese_encoder_retransmit(SiameseEncoder encoder_t
 SIAMESE_EXPORT SiameseResult siamese_encode(SiameseEncoder encoder_t, SiameseRecoveryPacket* recovery) {
     CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
     if (!e || !recovery) return Siamese_InvalidInput;
-    ApiLock lk;
+    API_LOCK();
+    g_rt->ctx.touch(e->enc);
     RecoveryOut out;
     const Result r = e->enc->encode(out);
     if (r != kSuccess) {
@@ -279,7 +328,8 @@ SIAMESE_EXPORT SiameseResult siamese_encode(SiameseEncoder encoder_t, SiameseRec
 SIAMESE_EXPORT SiameseResult siamese_encoder_stats(SiameseEncoder encoder_t, uint64_t* statsOut, unsigned statsCount) {
     CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
     if (!e || !statsOut || statsCount <= 0) return Siamese_InvalidInput;
-    ApiLock lk;
+    API_LOCK();
+    g_rt->ctx.touch(e->enc);
     e->enc->stats(statsOut, statsCount);
     return Siamese_Success;
 }
@@ -288,7 +338,7 @@ SIAMESE_EXPORT SiameseResult siamese_encoder_stats(SiameseEncoder encoder_t, uin
 
 SIAMESE_EXPORT SiameseDecoder siamese_decoder_create() {
     if (!g_rt || !g_rt->ok) return nullptr;
-    ApiLock lk;
+    API_LOCK();
     CDecoder* d = new (std::nothrow) CDecoder();
     if (!d) return nullptr;
     d->dec = new Decoder(&g_rt->ctx, 0, release_host, nullptr);
@@ -298,7 +348,7 @@ SIAMESE_EXPORT SiameseDecoder siamese_decoder_create() {
 SIAMESE_EXPORT void siamese_decoder_free(SiameseDecoder decoder_t) {
     CDecoder* d = reinterpret_cast<CDecoder*>(decoder_t);
     if (!d) return;
-    ApiLock lk;
+    API_LOCK();
     delete d->dec;
     delete d;
 }
@@ -309,7 +359,8 @@ SIAMESE_EXPORT SiameseResult siamese_decoder_add_original(SiameseDecoder decoder
         packet->PacketNum > SIAMESE_PACKET_NUM_MAX)
         return Siamese_InvalidInput;
     if (!packet->Data) return Siamese_InvalidInput;
-    ApiLock lk;
+    API_LOCK();
+    g_rt->ctx.touch(d->dec);
     if (d->dec->disabled()) return Siamese_Disabled;
     uint8_t* host = nullptr;
     RowId row = kNoRow;
@@ -331,7 +382,8 @@ SIAMESE_EXPORT SiameseResult siamese_decoder_add_recovery(SiameseDecoder decoder
     CDecoder* d = reinterpret_cast<CDecoder*>(decoder_t);
     if (!d || !packet || !packet->Data || packet->DataBytes <= 0 || packet->DataBytes > SIAMESE_MAX_PACKET_BYTES)
         return Siamese_InvalidInput;
-    ApiLock lk;
+    API_LOCK();
+    g_rt->ctx.touch(d->dec);
     if (d->dec->disabled()) return Siamese_Disabled;
     const uint32_t total = packet->DataBytes;
     const RowId row = g_rt->ctx.alloc(total);
@@ -347,7 +399,8 @@ SIAMESE_EXPORT SiameseResult siamese_decoder_add_recovery(SiameseDecoder decoder
 SIAMESE_EXPORT SiameseResult siamese_decoder_get(SiameseDecoder decoder_t, SiameseOriginalPacket* packet) {
     CDecoder* d = reinterpret_cast<CDecoder*>(decoder_t);
     if (!d || !packet || packet->PacketNum > SIAMESE_PACKET_NUM_MAX) return Siamese_InvalidInput;
-    ApiLock lk;
+    API_LOCK();
+    g_rt->ctx.touch(d->dec);
     StoredOriginal* o = nullptr;
     const Result r = d->dec->get(packet->PacketNum, &o);
     if (r != kSuccess) {
@@ -376,7 +429,8 @@ SIAMESE_EXPORT SiameseResult siamese_decoder_get(SiameseDecoder decoder_t, Siame
 SIAMESE_EXPORT SiameseResult siamese_decoder_is_ready(SiameseDecoder decoder_t) {
     CDecoder* d = reinterpret_cast<CDecoder*>(decoder_t);
     if (!d) return Siamese_InvalidInput;
-    ApiLock lk;
+    API_LOCK();
+    g_rt->ctx.touch(d->dec);
     return (SiameseResult)d->dec->is_ready();
 }
 
@@ -384,7 +438,8 @@ SIAMESE_EXPORT SiameseResult siamese_decode(SiameseDecoder decoder_t, SiameseOri
                                             unsigned* countOut) {
     CDecoder* d = reinterpret_cast<CDecoder*>(decoder_t);
     if (!d || (!packetsPtrOut != !countOut)) return Siamese_InvalidInput;
-    ApiLock lk;
+    API_LOCK();
+    g_rt->ctx.touch(d->dec);
     if (packetsPtrOut) {
         *packetsPtrOut = nullptr;
         *countOut = 0;
@@ -448,7 +503,8 @@ SIAMESE_EXPORT SiameseResult siamese_decoder_ack(SiameseDecoder decoder_t, void*
                                                  unsigned* usedBytes) {
     CDecoder* d = reinterpret_cast<CDecoder*>(decoder_t);
     if (!d || !buffer || !usedBytes || byteLimit < SIAMESE_ACK_MIN_BYTES) return Siamese_InvalidInput;
-    ApiLock lk;
+    API_LOCK();
+    g_rt->ctx.touch(d->dec);
     uint32_t used = 0;
     const Result r = d->dec->ack((uint8_t*)buffer, byteLimit, &used);
     *usedBytes = used;
@@ -458,7 +514,8 @@ SIAMESE_EXPORT SiameseResult siamese_decoder_ack(SiameseDecoder decoder_t, void*
 SIAMESE_EXPORT SiameseResult siamese_decoder_stats(SiameseDecoder decoder_t, uint64_t* statsOut, unsigned statsCount) {
     CDecoder* d = reinterpret_cast<CDecoder*>(decoder_t);
     if (!d || !statsOut || statsCount <= 0) return Siamese_InvalidInput;
-    ApiLock lk;
+    API_LOCK();
+    g_rt->ctx.touch(d->dec);
     d->dec->stats(statsOut, statsCount);
     return Siamese_Success;
 }

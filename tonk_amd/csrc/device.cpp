@@ -60,6 +60,7 @@ Device::~Device() {
     if (gdesc_host_) hipHostFree(gdesc_host_);
     if (up_host_) hipHostFree(up_host_);
     if (up_dev_) hipFree(up_dev_);
+    if (rb_host_) hipHostFree(rb_host_);
     if (up_event_) hipEventDestroy((hipEvent_t)up_event_);
     if (d_gf_) hipFree(d_gf_);
     if (d_zero_) hipFree(d_zero_);
@@ -126,6 +127,8 @@ bool Device::init(int device, uint64_t arena_bytes) {
     up_cap_ = 4u << 20;
     HIPCHK(hipHostMalloc((void**)&up_host_, up_cap_, hipHostMallocDefault));
     HIPCHK(hipMalloc((void**)&up_dev_, up_cap_));
+    rb_cap_ = 2u << 20;
+    HIPCHK(hipHostMalloc((void**)&rb_host_, rb_cap_, hipHostMallocDefault));
     // Staging slots up front, each touched by one copy, so no step pays first-use costs.
     for (Slot& sl : slots_) {
         if (!ensure_slot(sl, 16u << 20)) { error_ = "program staging allocation failed"; return false; }
@@ -399,6 +402,9 @@ void Device::synchronize() {
     inflight_.clear();
     completed_ = ticket_;
     up_used_ = up_flushed_ = 0;
+    for (const Readback& r : rb_pending_) memcpy(r.dst, rb_host_ + r.off, r.n);
+    rb_pending_.clear();
+    rb_used_ = 0;
 }
 
 void Device::upload(uint64_t off, const void* src, size_t n) {
@@ -450,7 +456,21 @@ void Device::download(void* dst, uint64_t off, size_t n) {
 void Device::download_async(void* dst, uint64_t off, size_t n) {
     if (n == 0) return;
     flush_uploads();
-    HIPCHK(hipMemcpyAsync(dst, arena_ + off, n, hipMemcpyDeviceToHost, (hipStream_t)stream_));
+    hipStream_t st = (hipStream_t)stream_;
+    if (n > rb_cap_) {  // larger than the pinned buffer: a plain (synchronous) copy
+        synchronize();
+        HIPCHK(hipMemcpyAsync(dst, arena_ + off, n, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        return;
+    }
+    if (rb_used_ + n > rb_cap_) synchronize();
+    HIPCHK(hipMemcpyAsync(rb_host_ + rb_used_, arena_ + off, n, hipMemcpyDeviceToHost, st));
+    Readback r;
+    r.dst = dst;
+    r.off = rb_used_;
+    r.n = n;
+    rb_pending_.push_back(r);
+    rb_used_ += (n + 63) & ~(size_t)63;
 }
 
 bool Device::enable_staging() {

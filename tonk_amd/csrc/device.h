@@ -138,6 +138,12 @@ private:
     uint8_t* up_dev_ = nullptr;
     size_t up_cap_ = 0, up_used_ = 0, up_flushed_ = 0;
     std::vector<ScatterDesc> up_pending_;
+    // readback staging: download_async() lands rows in pinned rb_host_; synchronize() copies
+    // them to the callers' buffers
+    struct Readback { void* dst; size_t off, n; };
+    uint8_t* rb_host_ = nullptr;
+    size_t rb_cap_ = 0, rb_used_ = 0;
+    std::vector<Readback> rb_pending_;
     void* up_event_ = nullptr;
     bool timing_ = false;
     std::vector<std::pair<void*, void*>> timing_events_;

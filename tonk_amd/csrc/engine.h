@@ -330,6 +330,7 @@ public:
     virtual ~FlushClient() {}
     virtual void pre_flush() = 0;   // emit pending scans (running sums) into the program
     virtual void post_flush() = 0;  // drop per-program symbolic state
+    bool dirty = false;              // on Context::dirty (touched since the last flush)
 };
 
 struct Context {
@@ -355,18 +356,32 @@ struct Context {
     void attach(FlushClient* c) { clients.push_back(c); }
     void detach(FlushClient* c) {
         clients.erase(std::remove(clients.begin(), clients.end(), c), clients.end());
+        dirty.erase(std::remove(dirty.begin(), dirty.end(), c), dirty.end());
+    }
+    // Dirty tracking for contexts shared by many codecs (the siamese.h C ABI): a codec only has
+    // pending scans after a call on it, so a flush visits the codecs touched since the last one
+    // instead of every attached codec.  Off (every client visited) unless enabled.
+    bool track_dirty = false;
+    std::vector<FlushClient*> dirty;
+    void touch(FlushClient* c) {
+        if (!c->dirty) {
+            c->dirty = true;
+            dirty.push_back(c);
+        }
     }
     // Close the pending program: scans emitted, temps released after `epoch` completes.  The
     // caller then executes pb's ops and calls finish_flush().
     void prepare_flush() {
-        for (FlushClient* c : clients) c->pre_flush();
+        for (FlushClient* c : track_dirty ? dirty : clients) c->pre_flush();
     }
     void finish_flush() {
         for (RowId r : pb.written_rows()) rows.set_level(r, 0);
         for (RowId r : temps) rows.free_deferred(r);
         temps.clear();
         ex.clear();
-        for (FlushClient* c : clients) c->post_flush();
+        for (FlushClient* c : track_dirty ? dirty : clients) c->post_flush();
+        for (FlushClient* c : dirty) c->dirty = false;
+        dirty.clear();
         rows.seal_epoch(epoch);
         ++epoch;
         pb.clear();
