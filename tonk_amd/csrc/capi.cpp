@@ -109,7 +109,8 @@ void release_host(void* host, void*) { free(host); }
 
 struct CEncoder {
     Encoder* enc = nullptr;
-    std::vector<uint8_t> recovery;
+    uint8_t* recovery = nullptr;  // pinned: the D2H of each recovery packet lands here
+    size_t recovery_cap = 0;
 };
 
 struct CDecoder {
@@ -121,16 +122,18 @@ uint64_t row_byte_offset(RowId r) { return (uint64_t)g_rt->ctx.rows.offset(r) * 
 
 // Enqueues the pending program (caller holds the lock); reads of its results may be enqueued
 // behind it with Device::download_async before flush_complete() waits once for all of it.
-void flush_enqueue() {
+uint64_t flush_enqueue() {
     Context& ctx = g_rt->ctx;
+    uint64_t ticket = 0;
     const int64_t t0 = g_watch ? now_ns() : 0;
     ctx.prepare_flush();
     const int64_t t1 = g_watch ? now_ns() : 0;
-    if (!ctx.pb.empty()) g_rt->dev.run(&ctx);
+    if (!ctx.pb.empty()) ticket = g_rt->dev.run(&ctx);
     if (g_watch) {
         g_prepare_ns.fetch_add((uint64_t)(t1 - t0), std::memory_order_relaxed);
         g_run_ns.fetch_add((uint64_t)(now_ns() - t1), std::memory_order_relaxed);
     }
+    return ticket;
 }
 
 void flush_complete() {
@@ -214,6 +217,10 @@ SIAMESE_EXPORT void siamese_encoder_free(SiameseEncoder encoder_t) {
     CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
     if (!e) return;
     API_LOCK();
+    if (e->recovery) {
+        g_rt->dev.synchronize();  // no copy may still be landing in the buffer
+        Device::host_free(e->recovery);
+    }
     delete e->enc;
     delete e;
 }
@@ -307,21 +314,55 @@ SIAMESE_EXPORT SiameseResult siamese_encoder_retransmit(SiameseEncoder encoder_t
 SIAMESE_EXPORT SiameseResult siamese_encode(SiameseEncoder encoder_t, SiameseRecoveryPacket* recovery) {
     CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
     if (!e || !recovery) return Siamese_InvalidInput;
-    API_LOCK();
-    g_rt->ctx.touch(e->enc);
-    RecoveryOut out;
-    const Result r = e->enc->encode(out);
-    if (r != kSuccess) {
-        if (r == kNeedMoreData) recovery->DataBytes = 0;
-        return (SiameseResult)r;
+    void* ev = nullptr;
+    uint64_t done = 0, ticket = 0;
+    uint32_t total = 0;
+    {
+        API_LOCK();
+        g_rt->ctx.touch(e->enc);
+        RecoveryOut out;
+        const Result r = e->enc->encode(out);
+        if (r != kSuccess) {
+            if (r == kNeedMoreData) recovery->DataBytes = 0;
+            return (SiameseResult)r;
+        }
+        total = out.total();
+        if (total > e->recovery_cap) {
+            if (e->recovery) {
+                g_rt->dev.synchronize();
+                Device::host_free(e->recovery);
+            }
+            e->recovery_cap = total < 2048 ? 2048 : total;
+            e->recovery = (uint8_t*)Device::host_alloc(e->recovery_cap);
+            if (!e->recovery) {
+                e->recovery_cap = 0;
+                g_rt->ctx.rows.free_deferred(out.row);
+                e->enc->set_disabled();
+                return Siamese_Disabled;
+            }
+        }
+        // Enqueue the program and the read of the recovery row behind it, close the program's
+        // host bookkeeping (later programs are stream-ordered after it), and wait for the copy
+        // without the lock so other codecs' calls proceed meanwhile.
+        ticket = flush_enqueue();
+        g_rt->dev.download_pinned(e->recovery, row_byte_offset(out.row), total);
+        ev = g_rt->dev.record_event();
+        done = g_rt->ctx.epoch;
+        g_rt->ctx.finish_flush();
+        g_rt->ctx.rows.free_deferred(out.row);  // released once the next program completes
     }
-    flush_enqueue();
-    e->recovery.resize(out.total());
-    g_rt->dev.download_async(e->recovery.data(), row_byte_offset(out.row), out.total());
-    flush_complete();
-    g_rt->ctx.rows.free_deferred(out.row);
-    recovery->Data = e->recovery.data();
-    recovery->DataBytes = out.total();
+    const int64_t t0 = now_ns();
+    Device::event_wait(ev);
+    g_waits.fetch_add(1, std::memory_order_relaxed);
+    g_wait_ns.fetch_add((uint64_t)(now_ns() - t0), std::memory_order_relaxed);
+    {
+        API_LOCK();
+        g_rt->dev.event_release(ev);
+        g_rt->dev.completed(ticket);  // retire finished programs' events
+        g_rt->ctx.rows.release_up_to(done);
+    }
+    recovery->Data = e->recovery;
+    recovery->DataBytes = total;
     return Siamese_Success;
 }
 

@@ -473,6 +473,40 @@ void Device::download_async(void* dst, uint64_t off, size_t n) {
     rb_used_ += (n + 63) & ~(size_t)63;
 }
 
+void Device::download_pinned(void* dst, uint64_t off, size_t n) {
+    flush_uploads();
+    if (n) HIPCHK(hipMemcpyAsync(dst, arena_ + off, n, hipMemcpyDeviceToHost, (hipStream_t)stream_));
+}
+
+void* Device::record_event() {
+    void* e = nullptr;
+    if (!free_events_.empty()) {
+        e = free_events_.back();
+        free_events_.pop_back();
+    } else {
+        hipEvent_t he;
+        HIPCHK(hipEventCreateWithFlags(&he, hipEventDisableTiming));
+        e = he;
+    }
+    HIPCHK(hipEventRecord((hipEvent_t)e, (hipStream_t)stream_));
+    return e;
+}
+
+void Device::event_wait(void* ev) {
+    const hipError_t e = hipEventSynchronize((hipEvent_t)ev);
+    if (e != hipSuccess) fprintf(stderr, "tonk_amd: hipEventSynchronize failed: %s\n", hipGetErrorString(e));
+}
+
+void* Device::host_alloc(size_t n) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, n, hipHostMallocDefault) != hipSuccess) return nullptr;
+    return p;
+}
+
+void Device::host_free(void* p) {
+    if (p) hipHostFree(p);
+}
+
 bool Device::enable_staging() {
     if (h2d_stream_) return true;
     hipStream_t a, b;

@@ -57,6 +57,15 @@ public:
     void flush_uploads();
     void download(void* dst, uint64_t arena_offset, size_t n);
     void download_async(void* dst, uint64_t arena_offset, size_t n);
+    // Reads that complete outside the caller's lock (the C ABI's encode): D2H straight into the
+    // caller's pinned buffer, then an event recorded behind it.  event_wait() may run without
+    // any lock; record/release must hold the same lock as every other Device call.
+    void download_pinned(void* pinned_dst, uint64_t arena_offset, size_t n);
+    void* record_event();
+    static void event_wait(void* ev);
+    void event_release(void* ev) { free_events_.push_back(ev); }
+    static void* host_alloc(size_t n);  // pinned
+    static void host_free(void* p);
 
     // Bench helpers (kernels.hip).
     struct GenDesc { uint32_t row, index, len, pad; uint64_t seed; };

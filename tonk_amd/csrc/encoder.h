@@ -72,6 +72,7 @@ public:
     void set_clock(const uint32_t* msec) { clock_ = msec; }
 
     bool disabled() const { return disabled_; }
+    void set_disabled() { disabled_ = true; }
     uint64_t stat(unsigned i) const { return stats_[i]; }
 
     // FlushClient
