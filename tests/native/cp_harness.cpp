@@ -21,6 +21,9 @@ using namespace tamd;
 using namespace tamd::wl;
 
 static uint64_t g_arena_bytes = 512ull << 20;
+// dirty=1: the context visits only codecs touched since the last flush (Context::track_dirty,
+// as the siamese.h C ABI runs it); every backend call touches its codec like capi.cpp does.
+static bool g_dirty = false;
 
 struct Harness {
     Params p;
@@ -46,9 +49,18 @@ struct Harness {
     explicit Harness(const Params& prm) : p(prm) {
         row_bytes = ((p.payload_max + 4 + 8 + 63) / 64) * 64;
         ctx.rows.init(g_arena_bytes);
+        ctx.track_dirty = g_dirty;
         arena.assign(g_arena_bytes, 0);
         enc = new Encoder(&ctx, row_bytes);
         dec = new Decoder(&ctx, row_bytes);
+    }
+    Encoder* E() {
+        if (g_dirty) ctx.touch(enc);
+        return enc;
+    }
+    Decoder* D() {
+        if (g_dirty) ctx.touch(dec);
+        return dec;
     }
     ~Harness() {
         delete enc;
@@ -139,19 +151,19 @@ struct Harness {
         uint32_t framed = 0, header = 0;
         const RowId r = write_original(index, len, &framed, &header);
         if (r == kNoRow) { error = "arena full"; return 5; }
-        const Result rc = enc->add(r, framed, header, len, nullptr, col);
+        const Result rc = E()->add(r, framed, header, len, nullptr, col);
         if (rc != kSuccess) ctx.rows.free_deferred(r);
         if (batch && (index + 1) % batch == 0) flush();
         return rc;
     }
-    int enc_encode(RecRef& r) { return enc->encode(r.out); }
-    int enc_ack(const uint8_t* buf, uint32_t n, uint32_t* next) { return enc->acknowledge(buf, n, next); }
+    int enc_encode(RecRef& r) { return E()->encode(r.out); }
+    int enc_ack(const uint8_t* buf, uint32_t n, uint32_t* next) { return E()->acknowledge(buf, n, next); }
     int dec_add_original(uint32_t col, uint32_t index, uint32_t len) {
         uint32_t framed = 0, header = 0;
         const RowId r = write_original(index, len, &framed, &header);
         if (r == kNoRow) { error = "arena full"; return 5; }
         bool took = false;
-        const Result rc = dec->add_original(col, r, framed, header, len, nullptr, &took);
+        const Result rc = D()->add_original(col, r, framed, header, len, nullptr, &took);
         if (!took) ctx.rows.free_deferred(r);
         return rc;
     }
@@ -164,14 +176,14 @@ struct Harness {
         uint8_t tail[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         const uint32_t tl = r.out.total() < 8 ? r.out.total() : 8;
         memcpy(tail + tl - r.out.footer_len, r.out.footer, r.out.footer_len);
-        const Result rc = dec->add_recovery(r.out.row, r.out.total(), tail, nullptr, &took);
+        const Result rc = D()->add_recovery(r.out.row, r.out.total(), tail, nullptr, &took);
         if (!took) ctx.rows.free_deferred(r.out.row);
         return rc;
     }
-    int dec_is_ready() { return dec->is_ready(); }
+    int dec_is_ready() { return D()->is_ready(); }
     int dec_decode(std::vector<uint32_t>& nums, DecRef&) {
         std::vector<RecoveredPacket*> got;
-        const Result rc = dec->decode(got);
+        const Result rc = D()->decode(got);
         if (rc == kSuccess) {
             pend_dec.emplace_back();
             for (RecoveredPacket* rp : got) {
@@ -181,8 +193,8 @@ struct Harness {
         }
         return rc;
     }
-    int dec_ack(uint8_t* buf, uint32_t limit, uint32_t* used) { return dec->ack(buf, limit, used); }
-    void stats(uint64_t e[9], uint64_t d[11]) { enc->stats(e, 9); dec->stats(d, 11); }
+    int dec_ack(uint8_t* buf, uint32_t limit, uint32_t* used) { return D()->ack(buf, limit, used); }
+    void stats(uint64_t e[9], uint64_t d[11]) { E()->stats(e, 9); D()->stats(d, 11); }
 
     // ---- transcript interface ----
     void on_encode(int rc, const RecRef& r) {
@@ -235,6 +247,7 @@ int main(int argc, char** argv) {
         if (k == "mode") sync = strcmp(vs, "sync") == 0;
         else if (k == "batch") batch = (uint32_t)v;
         else if (k == "arena_mb") g_arena_bytes = v << 20;
+        else if (k == "dirty") g_dirty = v != 0;
         else if (k == "n") p.n_originals = (uint32_t)v;
         else if (k == "pmin") p.payload_min = (uint32_t)v;
         else if (k == "pmax") p.payload_max = (uint32_t)v;
