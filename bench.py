@@ -15,10 +15,13 @@ payload GiB/s over all ranks; the timed region is bracketed by a barrier and a d
 roofline: algorithmic HBM bytes (SURVEY.md s8(d) B_alg, counted exactly per step) divided by
 the summed duration of the executor (tamd_exec16) launches of the timed steps (HIP events on the launch
 stream), against the 8.0 TB/s HBM3E peak.  cpu_baseline: the reference codec (compiled from
-/root/reference by oracle/Makefile, shipped prebuilt in oracle/_ref) on the same workload
-sample, rank 0 only.
+/root/reference by oracle/Makefile, shipped prebuilt in oracle/_ref) on a sample of the same
+workload, on rank 0 after the timed region, with the host cores the job owns (16 per GPU).
 
-usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload cfg3|cfg2|cfg1|cfg4]
+
+--gpus N without torch.distributed.run starts N rank processes itself (one per GPU, gloo
+rendezvous on 127.0.0.1); under torch.distributed.run the ranks come from the environment.
 """
 from __future__ import annotations
 
@@ -55,10 +58,11 @@ def host_threads(local_world: int) -> int:
     return max(1, min(16, per, env))
 
 
-def cpu_baseline(threads: int, target_s: float = 10.0) -> dict | None:
+def cpu_baseline(threads: int, target_s: float = 12.0, reps_runs: int = 3) -> dict | None:
     """The reference codec (oracle/_ref, compiled from /root/reference sources) on a bounded
-    sample of the same workload: 64 streams x 16384 originals, repeated with fresh codecs until
-    about `target_s` seconds of wall time on `threads` host threads."""
+    sample of the same workload: 64 streams x 16384 originals per repetition (fresh codecs),
+    repeated to about target_s / reps_runs seconds per run on `threads` host threads; the run is
+    done `reps_runs` times and the median reported with the spread (min, max)."""
     exe = os.path.join(ROOT, "oracle", "_ref", "golden_gen")
     if not os.path.exists(exe):
         return None
@@ -72,18 +76,28 @@ def cpu_baseline(threads: int, target_s: float = 10.0) -> dict | None:
             return None
         return json.loads(r.stdout.strip().splitlines()[-1])
 
-    probe = run(2)
+    probe = run(max(1, threads // 8))
     if probe is None:
         return None
-    per_rep = max(probe["seconds"] / 2, 1e-3)
-    reps = int(min(4000, max(2, round(target_s / per_rep))))
-    j = run(reps)
-    if j is None:
+    per_rep = max(probe["seconds"] / max(1, threads // 8), 1e-3)
+    reps = int(min(4000, max(2, round(target_s / reps_runs / per_rep))))
+    runs = [run(reps) for _ in range(reps_runs)]
+    if any(j is None for j in runs):
         return None
-    return {"value": round(j["gib_per_s"], 4), "unit": "GiB/s", "cores": threads, "kind": "reference",
+    vals = sorted(j["gib_per_s"] for j in runs)
+    secs = sum(j["seconds"] for j in runs)
+    return {"value": round(vals[len(vals) // 2], 4), "unit": "GiB/s", "cores": threads, "kind": "reference",
+            "spread": [round(vals[0], 4), round(vals[-1], 4)],
             "sample": f"{STREAMS_PER_GPU} streams x {n} originals x {PAYLOAD} B x {reps} repetitions "
                       f"(same loss/FEC/ack workload, fresh codecs per repetition), {threads} host threads, "
-                      f"{j['seconds']:.2f} s"}
+                      f"median of {reps_runs} runs, {secs:.2f} s in total"}
+
+
+def host_cpus() -> int:
+    try:
+        return len(os.sched_getaffinity(0))
+    except Exception:
+        return os.cpu_count() or 8
 
 
 def pmc_traffic() -> tuple:
@@ -98,14 +112,14 @@ def pmc_traffic() -> tuple:
         return None, None
 
 
-def end_to_end(threads: int, device: int, steps: int = 3, warmup: int = 1) -> dict | None:
+def end_to_end(threads: int, device: int, loss: float, steps: int = 3, warmup: int = 1) -> dict | None:
     """The PCIe-inclusive rate (north_star): the same workload with packets starting
     and ending in pinned host memory -- every step copies its originals H2D for both codec
     sides, its recovery packets and recovered originals D2H (packed by a gather kernel) and the
     received recovery packets H2D again, on copy streams overlapped with the codec work.
     Reported beside `value`, never as it."""
     n_orig = (warmup + steps) * ORIGINALS_PER_STEP
-    wp = tonk_amd.WorkloadParams(n=n_orig, payload=PAYLOAD, loss=LOSS, ack=ACK)
+    wp = tonk_amd.WorkloadParams(n=n_orig, payload=PAYLOAD, loss=loss, ack=ACK)
     try:
         sess = tonk_amd.Session(wp, n_streams=STREAMS_PER_GPU, device=device, threads=threads,
                                 arena_bytes=(2 * n_orig * STREAMS_PER_GPU * 1344) + (4 << 30), stage_host=True)
@@ -137,12 +151,21 @@ def end_to_end(threads: int, device: int, steps: int = 3, warmup: int = 1) -> di
                     "recovery packets and recovered originals, H2D of received recovery packets"}
 
 
+# Workload names follow BASELINE.json's 0-based configs[] index.
 SINGLE_STREAM = {
     # BASELINE.json configs[1]: one stream, 4096 originals, 1% loss, bit-exact vs CPU
-    "c2": dict(n=4096, loss=0.01, ack=64),
+    "cfg1": dict(n=4096, loss=0.01, ack=64),
     # BASELINE.json configs[4]: decoder stress, 65536 originals, 5% Gilbert-Elliott loss (mean
     # burst 4), f = 10%, acks every 256, ARQ after 2048
-    "c5": dict(n=65536, loss=0.05, burst=4, fec=0.10, ack=256, arq=2048),
+    "cfg4": dict(n=65536, loss=0.05, burst=4, fec=0.10, ack=256, arq=2048),
+}
+# Batched configurations: 64 streams per GPU, `loss` uniform, f = max(2p, 1%), ack every 64.
+BATCHED = {
+    # BASELINE.json configs[3] (the headline): 512 streams sharded 64/GPU, 1% loss
+    "cfg3": dict(loss=0.01),
+    # BASELINE.json configs[2]: 64 streams x 4096 originals, 2% loss, batched on one GPU
+    # (4096 originals per stream per step)
+    "cfg2": dict(loss=0.02),
 }
 
 
@@ -228,9 +251,40 @@ class Dist:
     def allsum(self, x: float) -> float:
         return self._reduce(x, "SUM")
 
+    def gather(self, xs: list[float]) -> list[list[float]]:
+        """Every rank's `xs`, in rank order (all_gather)."""
+        if self.dist is None:
+            return [list(xs)]
+        import torch
+        t = torch.tensor(xs, dtype=torch.float64)
+        parts = [torch.zeros_like(t) for _ in range(self.world)]
+        self.dist.all_gather(parts, t)
+        return [p.tolist() for p in parts]
+
     def close(self) -> None:
         if self.dist is not None:
             self.dist.destroy_process_group()
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv: list[str]) -> int:
+    """`--gpus N` without a launcher: start N rank processes of this script (rank i on GPU i,
+    gloo rendezvous on 127.0.0.1) before anything here touches a GPU; rank 0 prints the line.
+    Returns the worst exit code."""
+    port = free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env))
+    rcs = [p.wait() for p in procs]
+    return max(abs(rc) for rc in rcs)
 
 
 def main() -> int:
@@ -240,26 +294,50 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-end-to-end", action="store_true", help="skip the PCIe-inclusive side measurement")
-    ap.add_argument("--workload", choices=["c3"] + sorted(SINGLE_STREAM), default="c3",
-                    help="c3: the headline line (64 streams per GPU); c2 / c5: one stream, start to finish")
+    ap.add_argument("--workload", choices=sorted(BATCHED) + sorted(SINGLE_STREAM), default="cfg3",
+                    help="BASELINE.json configs[] index: cfg3 (the headline, 64 streams per GPU), cfg2 (64 "
+                         "streams, 2%% loss), cfg1 / cfg4 (one stream, start to finish)")
     ap.add_argument("--step", type=int, default=0,
-                    help="c2 / c5: originals per device program (default 4096 for c2, 512 for c5)")
+                    help="cfg1 / cfg4: originals per device program (default 4096 for cfg1, 512 for cfg4)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="form the ranks and print the shard plan without touching a GPU (tests)")
     a = ap.parse_args()
-    if a.workload != "c3":
-        step = a.step or (512 if a.workload == "c5" else ORIGINALS_PER_STEP)
-        print(json.dumps(single_stream(a.workload, int(os.environ.get("LOCAL_RANK", "0")), step)), flush=True)
-        return 0
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = int(os.environ.get("WORLD_SIZE", "0") or 0)
+    if world == 0:
+        if a.gpus > 1:
+            return spawn_ranks(a.gpus, sys.argv[1:])
+        world = 1
+    elif a.gpus != world and a.gpus != 1:
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        return 2
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+
+    if a.workload in SINGLE_STREAM:
+        if world > 1:
+            print("bench.py: single-stream workloads run on one GPU (replicas only)", file=sys.stderr)
+            return 2
+        step = a.step or (512 if a.workload == "cfg4" else ORIGINALS_PER_STEP)
+        print(json.dumps(single_stream(a.workload, local_rank, step)), flush=True)
+        return 0
+
+    loss = BATCHED[a.workload]["loss"]
     d = Dist(world)
+    if a.dry_run:
+        bases = d.gather([float(stream_base(rank)), float(rank), float(local_rank)])
+        if rank == 0:
+            print(json.dumps({"dry_run": True, "n_gpus": world, "streams_per_gpu": STREAMS_PER_GPU,
+                              "ranks": [{"rank": int(r), "local_rank": int(lr), "stream_base": int(b)}
+                                        for b, r, lr in bases]}), flush=True)
+        d.close()
+        return 0
 
     threads = host_threads(local_world)
     total_steps = a.warmup + a.steps
     n_orig = total_steps * ORIGINALS_PER_STEP
-    wp = tonk_amd.WorkloadParams(n=n_orig, payload=PAYLOAD, loss=LOSS, ack=ACK)
+    wp = tonk_amd.WorkloadParams(n=n_orig, payload=PAYLOAD, loss=loss, ack=ACK)
     sess = tonk_amd.Session(wp, n_streams=STREAMS_PER_GPU, device=local_rank,
                             stream_base=stream_base(rank), threads=threads,
                             arena_bytes=(2 * n_orig * STREAMS_PER_GPU * 1344) + (4 << 30))
@@ -287,6 +365,7 @@ def main() -> int:
 
     payload = s1["payload_bytes"] - s0["payload_bytes"]
     alg = s1["alg_bytes"] - s0["alg_bytes"]
+    op_trace = (s1["acc_bytes"] - s0["acc_bytes"]) + (s1["store_bytes"] - s0["store_bytes"])
     total_payload = d.allsum(payload)
     value = total_payload / elapsed / 2**30
 
@@ -296,9 +375,16 @@ def main() -> int:
     fin = sess.summary()
     ok = fin["missing_at_end"] == 0 and fin["disabled_codecs"] == 0
     sess.close()
+    all_ok = d.allsum(0.0 if ok else 1.0) == 0.0
 
     achieved = alg / (kernel_ms / 1e3) / 1e9 if kernel_ms > 0 else 0.0
     traffic, traffic_src = pmc_traffic()
+    workload = {
+        "cfg3": "configs[3] per-GPU shard: 64 independent streams/GPU, 4096 originals per stream per step, "
+                "1300 B payloads, 1% uniform loss, f=2%, ack every 64",
+        "cfg2": "configs[2]: 64 independent streams/GPU, 4096 originals per stream per step, 1300 B payloads, "
+                "2% uniform loss, f=4%, ack every 64",
+    }[a.workload]
     out = {
         "metric": METRIC,
         "value": round(value, 4),
@@ -313,10 +399,9 @@ def main() -> int:
         "dtype": "u8",
         "data": "synthetic",
         "config": {
-            "workload": "configs[3] per-GPU shard: 64 independent streams/GPU, 4096 originals per stream per step, "
-                        "1300 B payloads, 1% uniform loss, f=2%, ack every 64",
+            "workload": workload,
             "streams_per_gpu": STREAMS_PER_GPU, "originals_per_step": ORIGINALS_PER_STEP, "payload_bytes": PAYLOAD,
-            "loss": LOSS, "ack_every": ACK, "host_threads_per_gpu": threads,
+            "loss": loss, "ack_every": ACK, "host_threads_per_gpu": threads,
             "parallelism": f"streams sharded {STREAMS_PER_GPU}/GPU x {world} GPU, no collective",
         },
         "roofline": {
@@ -327,25 +412,31 @@ def main() -> int:
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": round(traffic, 1) if traffic else None,
             "traffic_source": traffic_src,
-            "kernel": "tamd_exec" if os.environ.get("TONK_AMD_SLICE") == "512" else "tamd_exec16",
+            "kernel": "tamd_exec16",
             "launches": launches,
             "avg_launch_us": round(kernel_ms * 1e3 / launches, 3) if launches else None,
             "alg_bytes_per_launch": round(alg / launches, 1) if launches else None,
+            # op-trace bytes (every row an instruction reads or writes): the
+            # gap to alg_bytes is what L2 / Infinity Cache serve
+            "op_trace_bytes_per_launch": round(op_trace / launches, 1) if launches else None,
             "device_busy_frac": round((kernel_ms / 1e3) / (t1 - t0), 4),
         },
         "cpu_baseline": None,
         "host_ms_per_step": host,
-        "checks": {"all_recovered": ok, "recovered": fin["recovered"], "lost_originals": fin["lost_originals"],
+        "checks": {"all_recovered": all_ok, "recovered": fin["recovered"], "lost_originals": fin["lost_originals"],
                    "lost_recoveries": fin["lost_recoveries"]},
     }
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(threads)
+    # The CPU leg runs after every rank's timed region: the reference codec on the host cores the
+    # job owns (16 per GPU, so N x 16 at N GPUs, capped by this process's CPU set).
+    if rank == 0 and not a.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(min(host_cpus(), threads * local_world))
     if rank == 0 and world == 1 and not a.no_end_to_end:
-        out["end_to_end"] = end_to_end(threads, local_rank)
+        out["end_to_end"] = end_to_end(threads, local_rank, loss)
+    d.barrier()
     if rank == 0:
         print(json.dumps(out), flush=True)
     d.close()
-    return 0 if ok else 1
+    return 0 if all_ok else 1
 
 
 if __name__ == "__main__":

@@ -32,6 +32,9 @@ typedef struct tamd_session_params {
                                   recovered originals D2H and the received recovery packets H2D
                                   (the PCIe-inclusive rate) */
     uint64_t arena_bytes;
+    uint32_t rtx_every;        /* retransmission tick every rtx_every originals (0: off) under a
+                                  virtual clock advancing rtx_msec per original (workload.h) */
+    uint32_t rtx_msec;
 } tamd_session_params;
 
 /* Summary counters (tamd_session_summary indices). */
@@ -66,6 +69,11 @@ void  tamd_session_host_ms(void* s, double out[10]);
 /* Transcript of one stream in the oracle's text format (record mode). Returns bytes needed. */
 size_t tamd_session_transcript(void* s, uint32_t stream, char* buf, size_t cap);
 void  tamd_session_destroy(void* s);
+
+/* Test hook: the codecs' millisecond clock (GetTimeMsec: send times, RTO, retransmit) is read
+   from `fn` instead of the monotonic clock (null restores it).  Used to compare
+   siamese_encoder_retransmit with the reference under a virtual clock. */
+void  tamd_set_clock(uint64_t (*fn)(void));
 
 /* Device self test: v_perm GF(2^8) multiply against the host tables (all 65536 products). */
 int   tamd_device_selftest(uint32_t device, char* err, size_t err_len);

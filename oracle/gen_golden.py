@@ -49,7 +49,22 @@ def scenarios():
     s["norecloss_p5_arq"] = (WorkloadParams(n=3000, loss=0.05, ack=0, arq=300, loss_on_recovery=False), 0, True)
     s["single_p0"] = (WorkloadParams(n=200, loss=0.0, ack=1), 0, True)
     s["burst8_p5"] = (WorkloadParams(n=8192, loss=0.05, burst=8, fec=0.10, ack=128, arq=1024), 0, True)
+    # siamese_encoder_retransmit under a virtual clock (RTO from acks / the initial RTO without)
+    s["rtx_p2_ack64"] = (WorkloadParams(n=3000, loss=0.02, ack=64, rtx=16, rtx_msec=1), 0, True)
+    s["rtx_p5_ack32"] = (WorkloadParams(n=3000, loss=0.05, ack=32, rtx=8, rtx_msec=3), 0, True)
+    s["rtx_p3_noack"] = (WorkloadParams(n=2000, loss=0.03, ack=0, rtx=16, rtx_msec=2), 0, True)
     return s
+
+
+def batches():
+    """name -> (WorkloadParams, first stream id, stream count): many independent streams driven
+    through ONE batched session on one GPU; the fixture holds each stream's transcript digest."""
+    return {
+        # BASELINE.json configs[2]: 64 independent streams x 4096 originals, 2% loss, batched on 1 GPU
+        "cfg2_64x4096_p2_ack64": (WorkloadParams(n=4096, loss=0.02, ack=64), 0, 64),
+        # BASELINE.json configs[3], the shard of rank 7 of 8 (streams 448..511), 3 bench steps
+        "cfg3_rank7_64x12288_p1_ack64": (WorkloadParams(n=3 * 4096, loss=0.01, ack=64), 7 * 64, 64),
+    }
 
 
 def run(wp: WorkloadParams, sid: int) -> str:
@@ -75,8 +90,10 @@ def main() -> int:
                                     "lines": text.count("\n"), "summary": text.strip().splitlines()[-1],
                                     "file": f"{name}.txt.gz" if full else None}
         if full:
-            with gzip.open(os.path.join(OUT, f"{name}.txt.gz"), "wt") as f:
-                f.write(text)
+            # mtime 0: regenerating identical transcripts leaves the fixture files unchanged
+            with open(os.path.join(OUT, f"{name}.txt.gz"), "wb") as raw, \
+                    gzip.GzipFile(fileobj=raw, mode="wb", mtime=0) as f:
+                f.write(text.encode())
         print(f"{name}: {index['scenarios'][name]['lines']} lines {digest[:16]}")
 
     # Bench configuration (bench.py default): per-stream transcript digests for streams 0..S-1.
@@ -87,6 +104,15 @@ def main() -> int:
         bench["streams"][str(sid)] = {"sha256": hashlib.sha256(text.encode()).hexdigest(),
                                       "summary": text.strip().splitlines()[-1]}
     index["bench"] = bench
+    index["batches"] = {}
+    for name, (wp, base, count) in batches().items():
+        entry = {"args": wp.args(), "stream_base": base, "streams": {}}
+        for sid in range(base, base + count):
+            text = run(wp, sid)
+            entry["streams"][str(sid)] = {"sha256": hashlib.sha256(text.encode()).hexdigest(),
+                                          "summary": text.strip().splitlines()[-1]}
+        index["batches"][name] = entry
+        print(f"{name}: {count} streams from {base}")
     with open(os.path.join(OUT, "scenarios.json"), "w") as f:
         json.dump(index, f, indent=1, sort_keys=True)
     return 0

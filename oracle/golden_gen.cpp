@@ -14,6 +14,7 @@
 #include "transcript.h"
 
 #include <chrono>
+#include <dlfcn.h>
 #include <thread>
 #include <atomic>
 #include <memory>
@@ -21,6 +22,24 @@
 #include <string.h>
 
 using namespace tamd::wl;
+
+// Virtual millisecond clock of retransmit scenarios (workload.h rtx_every): per thread, so
+// concurrent streams each run on their own clock.  The reference codec reads the time through
+// siamese::GetTimeMsec (SiameseTools.h:110; SiameseEncoder.cpp:142, 595, 905); this executable
+// defines that symbol (linked with -rdynamic) so the reference library's calls resolve here.
+// The MI355X library takes the same clock through its tamd_set_clock hook (looked up at run
+// time, since this driver is linked against either library).
+static thread_local bool g_vclock_on = false;
+static thread_local uint64_t g_vclock_ms = 0;
+static uint64_t real_usec() {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+static uint64_t vclock_msec() { return g_vclock_on ? g_vclock_ms : real_usec() / 1000; }
+namespace siamese {
+uint64_t GetTimeUsec() { return g_vclock_on ? g_vclock_ms * 1000 : real_usec(); }
+uint64_t GetTimeMsec() { return vclock_msec(); }
+}  // namespace siamese
 
 struct RefBackend {
     struct RecRef { std::vector<uint8_t> bytes; };
@@ -112,6 +131,21 @@ struct RefBackend {
     int dec_ack(uint8_t* buf, uint32_t limit, uint32_t* used) {
         return siamese_decoder_ack(dec, buf, limit, used);
     }
+    void set_time(uint64_t ms) {
+        g_vclock_on = true;
+        g_vclock_ms = ms;
+    }
+    int enc_retransmit(uint32_t* num, uint32_t* bytes, const uint8_t** data) {
+        SiameseOriginalPacket o;
+        o.PacketNum = 0;
+        o.Data = nullptr;
+        o.DataBytes = 0;
+        const int rc = siamese_encoder_retransmit(enc, &o);
+        *num = o.PacketNum;
+        *bytes = o.DataBytes;
+        *data = o.Data;
+        return rc;
+    }
     void stats(uint64_t e[9], uint64_t d[11]) {
         siamese_encoder_stats(enc, e, 9);
         siamese_decoder_stats(dec, d, 11);
@@ -145,6 +179,9 @@ struct RefTranscript {
         if (!enabled) return;
         if (rc != 0) t.put("%c %d %u %u\n", kind, rc, a, b);
     }
+    void on_retransmit(int rc, uint32_t num, uint32_t bytes, uint64_t h) {
+        if (enabled) fmt_retransmit(t, rc, num, bytes, h);
+    }
     void on_stats(const uint64_t e[9], const uint64_t d[11]) {
         if (enabled) fmt_stats(t, e, d);
     }
@@ -177,26 +214,10 @@ static bool parse_kv(Params& p, int& threads, int& streams, int& reps, const cha
     if (!eq) return false;
     std::string k(kv, eq - kv);
     const unsigned long long v = strtoull(eq + 1, nullptr, 0);
-    if (k == "stream") p.stream_id = (uint32_t)v;
-    else if (k == "n") p.n_originals = (uint32_t)v;
-    else if (k == "pmin") p.payload_min = (uint32_t)v;
-    else if (k == "pmax") p.payload_max = (uint32_t)v;
-    else if (k == "loss") p.loss_thresh = (uint32_t)v;
-    else if (k == "ge") p.ge_enable = (uint32_t)v;
-    else if (k == "gb") p.gb_thresh = (uint32_t)v;
-    else if (k == "bg") p.bg_thresh = (uint32_t)v;
-    else if (k == "lossrec") p.loss_on_recovery = (uint32_t)v;
-    else if (k == "fec") p.fec_rate_q16 = (uint32_t)v;
-    else if (k == "ack") p.ack_every = (uint32_t)v;
-    else if (k == "ackbytes") p.ack_bytes = (uint32_t)v;
-    else if (k == "arq") p.arq_lag = (uint32_t)v;
-    else if (k == "flush") p.flush_max = (uint32_t)v;
-    else if (k == "seed_data") p.seed_data = v;
-    else if (k == "seed_loss") p.seed_loss = v;
-    else if (k == "threads") threads = (int)v;
+    if (k == "threads") threads = (int)v;
     else if (k == "streams") streams = (int)v;
     else if (k == "reps") reps = (int)v;
-    else return false;
+    else return parse_param(p, k, v);
     return true;
 }
 
@@ -206,6 +227,8 @@ int main(int argc, char** argv) {
         return 2;
     }
     if (siamese_init() != 0) { fprintf(stderr, "siamese_init failed\n"); return 3; }
+    typedef void (*SetClock)(uint64_t (*)(void));
+    if (SetClock set_clock = (SetClock)dlsym(RTLD_DEFAULT, "tamd_set_clock")) set_clock(vclock_msec);
     Params base;
     int threads = 1, streams = 1, reps = 1;
     const bool timing = strcmp(argv[1], "time") == 0;

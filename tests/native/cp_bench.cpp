@@ -74,6 +74,8 @@ struct Null {
     }
     int dec_ack(uint8_t* b, uint32_t l, uint32_t* u) { TAMD_PROF_SCOPE(kDecAck); return dec->ack(b, l, u); }
     void stats(uint64_t e[9], uint64_t d[11]) { enc->stats(e, 9); dec->stats(d, 11); }
+    void set_time(uint64_t) {}
+    int enc_retransmit(uint32_t*, uint32_t*, const uint8_t**) { return 2; }
 };
 
 struct NoTr {
@@ -82,6 +84,7 @@ struct NoTr {
     void on_ack(int, const uint8_t*, uint32_t, int, uint32_t) {}
     void on_event(char, int, uint32_t, uint32_t) {}
     void on_stats(const uint64_t*, const uint64_t*) {}
+    void on_retransmit(int, uint32_t, uint32_t, uint64_t) {}
 };
 
 // Poor man's sampling profiler (no perf in the container): SIGPROF every 100 us of CPU time

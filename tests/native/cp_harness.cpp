@@ -195,6 +195,21 @@ struct Harness {
     }
     int dec_ack(uint8_t* buf, uint32_t limit, uint32_t* used) { return D()->ack(buf, limit, used); }
     void stats(uint64_t e[9], uint64_t d[11]) { E()->stats(e, 9); D()->stats(d, 11); }
+    uint64_t vclock = 0;
+    void set_time(uint64_t ms) {
+        if (!vclock) enc->set_clock(&vclock);
+        vclock = ms;
+    }
+    int enc_retransmit(uint32_t* num, uint32_t* bytes, const uint8_t** data) {
+        const StoredOriginal* o = nullptr;
+        const Result rc = E()->retransmit(&o);
+        if (rc == kSuccess) {
+            *num = o->column;
+            *bytes = o->bytes - o->header_bytes;
+            *data = nullptr;
+        }
+        return rc;
+    }
 
     // ---- transcript interface ----
     void on_encode(int rc, const RecRef& r) {
@@ -220,6 +235,12 @@ struct Harness {
         char t[64];
         snprintf(t, sizeof(t), "%c %d %u %u", kind, rc, a, b);
         lines.push_back(t);
+    }
+    void on_retransmit(int rc, uint32_t num, uint32_t bytes, uint64_t h) {
+        TextSink t;
+        fmt_retransmit(t, rc, num, bytes, h);
+        t.text.pop_back();
+        lines.push_back(t.text);
     }
     void on_stats(const uint64_t e[9], const uint64_t d[11]) {
         flush();
@@ -248,22 +269,7 @@ int main(int argc, char** argv) {
         else if (k == "batch") batch = (uint32_t)v;
         else if (k == "arena_mb") g_arena_bytes = v << 20;
         else if (k == "dirty") g_dirty = v != 0;
-        else if (k == "n") p.n_originals = (uint32_t)v;
-        else if (k == "pmin") p.payload_min = (uint32_t)v;
-        else if (k == "pmax") p.payload_max = (uint32_t)v;
-        else if (k == "loss") p.loss_thresh = (uint32_t)v;
-        else if (k == "ge") p.ge_enable = (uint32_t)v;
-        else if (k == "gb") p.gb_thresh = (uint32_t)v;
-        else if (k == "bg") p.bg_thresh = (uint32_t)v;
-        else if (k == "lossrec") p.loss_on_recovery = (uint32_t)v;
-        else if (k == "fec") p.fec_rate_q16 = (uint32_t)v;
-        else if (k == "ack") p.ack_every = (uint32_t)v;
-        else if (k == "ackbytes") p.ack_bytes = (uint32_t)v;
-        else if (k == "arq") p.arq_lag = (uint32_t)v;
-        else if (k == "flush") p.flush_max = (uint32_t)v;
-        else if (k == "seed_data") p.seed_data = v;
-        else if (k == "seed_loss") p.seed_loss = v;
-        else if (k == "stream") p.stream_id = (uint32_t)v;
+        else if (parse_param(p, k, v)) {}
         else { fprintf(stderr, "bad key %s\n", k.c_str()); return 2; }
     }
     Harness h(p);

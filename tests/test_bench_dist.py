@@ -53,3 +53,23 @@ def test_two_rank_reductions_and_shards():
     assert base0 == 0 and base1 == per  # disjoint stream shards
     shards = [set(range(b, b + per)) for b in (base0, base1)]
     assert not (shards[0] & shards[1])
+
+
+def test_bench_gpus_flag_spawns_ranks():
+    """`bench.py --gpus 2` without a launcher starts two rank processes itself (no GPU is touched
+    in --dry-run): they rendezvous over gloo and own disjoint 64-stream shards."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout          # rank 0 prints the one line
+    j = json.loads(lines[0])
+    assert j["n_gpus"] == 2
+    ranks = j["ranks"]
+    assert [x["rank"] for x in ranks] == [0, 1] and [x["local_rank"] for x in ranks] == [0, 1]
+    per = j["streams_per_gpu"]
+    shards = [set(range(x["stream_base"], x["stream_base"] + per)) for x in ranks]
+    assert not (shards[0] & shards[1]) and ranks[1]["stream_base"] == per

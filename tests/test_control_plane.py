@@ -23,7 +23,7 @@ from conftest import NATIVE, _make, first_diff, golden_text
 SCENARIOS = ["c1_256_p3", "c2_4096_p1_ack64", "c2_4096_p1_noack", "c3_4096_p2_ack64_s0",
              "c3_4096_p2_ack64_s1", "c3_4096_p2_ack64_s63", "c4_4096_p1_ack64_s511", "c5_65536_ge5_b4",
              "var_1_1500_p2_ack32", "tiny_1_20_p5_ack16", "big_9000_p3_ack64", "hiloss_p20_arq",
-             "norecloss_p5_arq", "single_p0", "burst8_p5"]
+             "norecloss_p5_arq", "single_p0", "burst8_p5", "rtx_p2_ack64", "rtx_p5_ack32", "rtx_p3_noack"]
 MODES = [("sync", 0), ("batch", 1000), ("batch", 4096), ("sync-dirty", 0), ("batch-dirty", 1000)]
 
 
@@ -48,3 +48,19 @@ def test_control_plane_matches_reference(harness, golden_index, tmp_path, name, 
     got = out.read_text()
     want = golden_text(name)
     assert got == want, first_diff(want, got)
+
+
+@pytest.mark.parametrize("batch_name,sid", [("cfg2_64x4096_p2_ack64", 0), ("cfg2_64x4096_p2_ack64", 37),
+                                             ("cfg3_rank7_64x12288_p1_ack64", 448),
+                                             ("cfg3_rank7_64x12288_p1_ack64", 511)])
+def test_control_plane_batch_streams(harness, golden_index, tmp_path, batch_name, sid):
+    """Streams of the multi-stream fixtures (BASELINE configs[2], the rank-7 shard of configs[3])
+    through the control plane in the bench's batch mode: transcript digest == reference's."""
+    import hashlib
+    entry = golden_index["batches"][batch_name]
+    out = tmp_path / "t.txt"
+    args = [harness, str(out), "mode=batch", "batch=4096", "dirty=0"] + entry["args"] + [
+        f"seed_data={1000 + sid}", f"seed_loss={2000 + sid}"]
+    r = subprocess.run(args, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert hashlib.sha256(out.read_bytes()).hexdigest() == entry["streams"][str(sid)]["sha256"]

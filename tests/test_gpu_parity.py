@@ -22,11 +22,12 @@ pytestmark = pytest.mark.gpu
 
 SCEN_CAPI = ["c1_256_p3", "c2_4096_p1_ack64", "c2_4096_p1_noack", "c3_4096_p2_ack64_s0",
              "var_1_1500_p2_ack32", "tiny_1_20_p5_ack16", "big_9000_p3_ack64", "hiloss_p20_arq",
-             "norecloss_p5_arq", "single_p0", "burst8_p5", "c5_65536_ge5_b4"]
+             "norecloss_p5_arq", "single_p0", "burst8_p5", "c5_65536_ge5_b4",
+             "rtx_p2_ack64", "rtx_p5_ack32", "rtx_p3_noack"]
 SCEN_SESSION = ["c1_256_p3", "c2_4096_p1_ack64", "c2_4096_p1_noack", "c3_4096_p2_ack64_s1",
                 "c3_4096_p2_ack64_s63", "c4_4096_p1_ack64_s511", "var_1_1500_p2_ack32",
                 "tiny_1_20_p5_ack16", "big_9000_p3_ack64", "hiloss_p20_arq", "single_p0",
-                "burst8_p5", "c5_65536_ge5_b4"]
+                "burst8_p5", "c5_65536_ge5_b4", "rtx_p2_ack64", "rtx_p3_noack"]
 
 
 def _args(golden_index, name):
@@ -55,10 +56,7 @@ def test_capi_matches_reference(golden_index, name):
 def _session_transcript(golden_index, name, threads=1, stage_host=False):
     import tonk_amd
     sc = golden_index["scenarios"][name]
-    kv = dict(a.split("=") for a in sc["args"])
-    wp = tonk_amd.WorkloadParams()
-    for k in tonk_amd.WorkloadParams.KEYS:
-        setattr(wp, k, int(kv[k]))
+    wp = tonk_amd.WorkloadParams.from_args(sc["args"])
     s = tonk_amd.Session(wp, n_streams=1, stream_base=sc["stream"], threads=threads,
                          arena_bytes=1 << 30, record=True, stage_host=stage_host)
     try:
@@ -96,31 +94,47 @@ def test_session_host_staged_matches_reference(golden_index, name):
     assert summ["h2d_bytes"] > 0 and summ["d2h_bytes"] > 0
 
 
+def _batch_digests(entry, threads=16):
+    """Run every stream of a golden batch through ONE batched session on one GPU (4096 originals
+    per step, as the bench) and return the stream ids whose transcript digest differs."""
+    import tonk_amd
+    wp = tonk_amd.WorkloadParams.from_args(entry["args"])
+    base = int(entry.get("stream_base", 0))
+    n_streams = len(entry["streams"])
+    arena = 2 * wp.n * n_streams * 1344 + (4 << 30)
+    s = tonk_amd.Session(wp, n_streams=n_streams, stream_base=base, threads=threads, arena_bytes=arena, record=True)
+    try:
+        s.generate()
+        done = 0
+        while done < wp.n:
+            s.step(min(4096, wp.n - done))
+            done += 4096
+        s.finish()
+        bad = []
+        for i in range(n_streams):
+            t = s.transcript(i)
+            want = entry["streams"][str(base + i)]
+            # the golden digest covers the transcript plus its Z summary line
+            if sha256(t + want["summary"] + "\n") != want["sha256"]:
+                bad.append(base + i)
+        summ = s.summary()
+        assert summ["missing_at_end"] == 0 and summ["disabled_codecs"] == 0, summ
+        return bad
+    finally:
+        s.close()
+
+
 def test_session_bench_config_streams(golden_index):
     """Bench configuration (64 streams x 49152 originals, 1% loss, ack 64): every stream's full
     transcript digest equals the reference's, with 16 host threads as in the bench."""
-    import tonk_amd
-    b = golden_index["bench"]
-    kv = dict(a.split("=") for a in b["args"])
-    wp = tonk_amd.WorkloadParams()
-    for k in tonk_amd.WorkloadParams.KEYS:
-        setattr(wp, k, int(kv[k]))
-    n_streams = len(b["streams"])
-    s = tonk_amd.Session(wp, n_streams=n_streams, stream_base=0, threads=16, arena_bytes=24 << 30, record=True)
-    try:
-        s.generate()
-        for _ in range(wp.n // 4096):
-            s.step(4096)
-        s.finish()
-        bad = []
-        for sid in range(n_streams):
-            t = s.transcript(sid)
-            want = b["streams"][str(sid)]
-            # the golden digest covers the transcript plus its Z summary line
-            if sha256(t + want["summary"] + "\n") != want["sha256"]:
-                bad.append(sid)
-        assert not bad, f"streams differing from the reference: {bad}"
-        summ = s.summary()
-        assert summ["missing_at_end"] == 0 and summ["disabled_codecs"] == 0
-    finally:
-        s.close()
+    bad = _batch_digests(golden_index["bench"])
+    assert not bad, f"streams differing from the reference: {bad}"
+
+
+@pytest.mark.parametrize("name", ["cfg2_64x4096_p2_ack64", "cfg3_rank7_64x12288_p1_ack64"])
+def test_session_batch_matches_reference(golden_index, name):
+    """BASELINE.json configs[2] as specified (64 independent streams x 4096 originals, 2% loss,
+    one batched session on one GPU) and the shard rank 7 of 8 runs in configs[3] (streams
+    448..511): every stream's transcript digest equals the reference codec's."""
+    bad = _batch_digests(golden_index["batches"][name])
+    assert not bad, f"streams differing from the reference: {bad}"

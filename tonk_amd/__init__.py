@@ -67,7 +67,7 @@ class _SessionParams(ctypes.Structure):
         "device", "n_streams", "stream_base", "n_threads", "n_originals", "payload_min", "payload_max",
         "loss_thresh", "ge_enable", "gb_thresh", "bg_thresh", "loss_on_recovery", "fec_rate_q16",
         "ack_every", "ack_bytes", "arq_lag", "flush_max", "record", "stage_host")] + [
-            ("arena_bytes", ctypes.c_uint64)]
+            ("arena_bytes", ctypes.c_uint64), ("rtx_every", ctypes.c_uint32), ("rtx_msec", ctypes.c_uint32)]
 
 
 SUMMARY_FIELDS = ["originals", "lost_originals", "recoveries", "lost_recoveries", "recovered", "arq",
@@ -97,9 +97,11 @@ class WorkloadParams:
     """Synthetic workload parameters (tonk_amd/csrc/workload.h Params)."""
 
     KEYS = ("n", "pmin", "pmax", "loss", "ge", "gb", "bg", "lossrec", "fec", "ack", "ackbytes", "arq", "flush")
+    # retransmission ticks under a virtual clock (workload.h); written to args() only when on
+    OPTIONAL = ("rtx", "rtxms")
 
     def __init__(self, n=4096, payload=1300, payload_max=None, loss=0.01, burst=None, fec=None, ack=64,
-                 ack_bytes=256, arq=0, flush=4096, loss_on_recovery=True):
+                 ack_bytes=256, arq=0, flush=4096, loss_on_recovery=True, rtx=0, rtx_msec=1):
         self.n = n
         self.pmin = payload
         self.pmax = payload_max if payload_max is not None else payload
@@ -116,9 +118,22 @@ class WorkloadParams:
         self.arq = arq
         self.flush = flush
         self.lossrec = 1 if loss_on_recovery else 0
+        self.rtx = rtx
+        self.rtxms = rtx_msec
 
     def args(self) -> list[str]:
-        return [f"{k}={getattr(self, k)}" for k in self.KEYS]
+        keys = self.KEYS + (self.OPTIONAL if self.rtx else ())
+        return [f"{k}={getattr(self, k)}" for k in keys]
+
+    @classmethod
+    def from_args(cls, args: list[str]) -> "WorkloadParams":
+        """The inverse of args() (fixture argument lists)."""
+        wp = cls()
+        kv = dict(a.split("=") for a in args)
+        for k in cls.KEYS + cls.OPTIONAL:
+            if k in kv:
+                setattr(wp, k, int(kv[k]))
+        return wp
 
 
 def device_selftest(device: int = 0) -> None:
@@ -140,6 +155,7 @@ class Session:
         p.loss_on_recovery, p.fec_rate_q16, p.ack_every, p.ack_bytes = wp.lossrec, wp.fec, wp.ack, wp.ackbytes
         p.arq_lag, p.flush_max, p.record, p.arena_bytes = wp.arq, wp.flush, 1 if record else 0, arena_bytes
         p.stage_host = 1 if stage_host else 0
+        p.rtx_every, p.rtx_msec = wp.rtx, wp.rtxms
         self.n_streams = n_streams
         err = ctypes.create_string_buffer(512)
         self._h = lib().tamd_session_create(ctypes.byref(p), err, len(err))

@@ -7,8 +7,6 @@
 #include <stdlib.h>
 #include <string.h>
 
-extern "C" __global__ void tamd_exec(const tamd_op*, const tamd_instr*, const uint2*, uint32_t, uint32_t, uint8_t*,
-                                     const uint32_t*, const uint8_t*, unsigned long long*);
 extern "C" __global__ void tamd_exec16(const tamd_op*, const tamd_instr*, const uint2*, uint32_t, uint32_t, uint8_t*,
                                        const uint32_t*, const uint8_t*, unsigned long long*);
 typedef void (*ExecFn)(const tamd_op*, const tamd_instr*, const uint2*, uint32_t, uint32_t, uint8_t*, const uint32_t*,
@@ -84,12 +82,12 @@ bool Device::init(int device, uint64_t arena_bytes) {
     // Persistent grid: exactly the workgroups that are resident at once (occupancy x CUs), so
     // every workgroup stages the GF tables once and no workgroup starts late (kernels.hip).
     int per_cu = 0;
-    exec_kernel_ = slice_bytes() == TAMD_SLICE_BYTES ? (const void*)tamd_exec : (const void*)tamd_exec16;
+    exec_kernel_ = (const void*)tamd_exec16;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, exec_kernel_, 256, 0) != hipSuccess ||
         per_cu < 1)
         per_cu = 1;
     // The occupancy API ignores the SGPR limit (MI355X_MICROARCH.md, Correctness boundaries): at
-    // tamd_exec's ~106 SGPRs a SIMD holds floor(800 / 128) = 6 waves, i.e. 6 workgroups per CU.
+    // tamd_exec16's ~106 SGPRs a SIMD holds floor(800 / 128) = 6 waves, i.e. 6 workgroups per CU.
     if (per_cu > 6) per_cu = 6;
     max_grid_ = (uint32_t)per_cu * (uint32_t)prop.multiProcessorCount;
     HIPCHK(hipSetDevice(device));

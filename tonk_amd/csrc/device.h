@@ -100,7 +100,7 @@ private:
     uint32_t* d_gf_ = nullptr;
     uint8_t* d_zero_ = nullptr;
     uint32_t max_grid_ = 256;
-    const void* exec_kernel_ = nullptr;  // tamd_exec or tamd_exec16 (slice_bytes())
+    const void* exec_kernel_ = nullptr;  // tamd_exec16
     // host staging
     void* h2d_stream_ = nullptr;
     void* d2h_stream_ = nullptr;

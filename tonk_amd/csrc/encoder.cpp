@@ -8,9 +8,14 @@
 
 namespace tamd {
 
+// Test hook (tamd_set_clock): a virtual millisecond clock replacing the monotonic one.
+static uint64_t (*g_clock_fn)() = nullptr;
+void set_clock_source(uint64_t (*fn)()) { g_clock_fn = fn; }
+
 // GetTimeMsec (SiameseTools.cpp).  Millisecond resolution is all the RTO logic uses, so the
 // coarse monotonic clock (a few ns, no TSC read) is enough; it is read once per original.
 uint64_t time_msec() {
+    if (g_clock_fn) return g_clock_fn();
     timespec ts;
     clock_gettime(CLOCK_MONOTONIC_COARSE, &ts);
     return (uint64_t)ts.tv_sec * 1000u + (uint64_t)ts.tv_nsec / 1000000u;
@@ -66,7 +71,7 @@ Result Encoder::add(RowId row, uint32_t framed_bytes, uint32_t header_bytes, uin
     o.column = column;
     o.header_bytes = (uint8_t)header_bytes;
     o.owned = borrowed ? 0 : 1;
-    o.send_msec = clock_ ? *clock_ : (uint32_t)time_msec();
+    o.send_msec = (uint32_t)now_msec();
     o.host = host;
     o.run = 1;
     if (element > 0) {
@@ -244,7 +249,7 @@ void Encoder::update_rto() {
     uint32_t first_loss = to_element(ack_.next_expected);
     if (first_loss >= window_count) return;
 
-    const uint64_t now64 = time_msec();
+    const uint64_t now64 = now_msec();
     const uint32_t now = (uint32_t)now64;
     uint32_t longest = 0;
 
@@ -347,7 +352,7 @@ Result Encoder::retransmit(const StoredOriginal** out) {
     const uint32_t count = count_;
     if (col_delta_negative(first) || first < first_unremoved_ || first >= count) return kNeedMoreData;
 
-    const uint32_t now = (uint32_t)time_msec();
+    const uint32_t now = (uint32_t)now_msec();
     const uint32_t rto = ack_.rto_msec;
 
     if (ack_.found_oldest) {

@@ -67,9 +67,10 @@ public:
     // ctx->rows.free_deferred once nothing reads it).
     Result encode(RecoveryOut& out);
     void stats(uint64_t* out, unsigned n);
-    // Millisecond clock for packet send times (RTO/retransmit only).  Default: the monotonic
-    // clock read per packet (GetTimeMsec); a batch driver may point it at a per-step value.
-    void set_clock(const uint32_t* msec) { clock_ = msec; }
+    // Millisecond clock of send times, RTO updates and retransmit decisions (GetTimeMsec in
+    // SiameseEncoder.cpp:142, 595, 905).  Default: the monotonic clock; a batch driver may point
+    // it at a per-step value or a virtual clock.
+    void set_clock(const uint64_t* msec) { clock_ = msec; }
 
     bool disabled() const { return disabled_; }
     void set_disabled() { disabled_ = true; }
@@ -86,7 +87,8 @@ private:
     void* user_;
     uint64_t stats_[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
     bool disabled_ = false;
-    const uint32_t* clock_ = nullptr;
+    const uint64_t* clock_ = nullptr;
+    uint64_t now_msec() const;
 
     // ---- EncoderPacketWindow (SiameseEncoder.h:104-232) ----
     Ring<StoredOriginal> win_;
@@ -150,5 +152,7 @@ private:
 };
 
 uint64_t time_msec();
+void set_clock_source(uint64_t (*fn)());  // test hook: replaces the clock time_msec() reads
+inline uint64_t Encoder::now_msec() const { return clock_ ? *clock_ : time_msec(); }
 
 } // namespace tamd

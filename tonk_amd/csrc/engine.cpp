@@ -7,14 +7,6 @@
 
 namespace tamd {
 
-uint32_t slice_bytes() {
-    static const uint32_t b = [] {
-        const char* e = getenv("TONK_AMD_SLICE");
-        return (e && atoi(e) == (int)TAMD_SLICE_BYTES) ? TAMD_SLICE_BYTES : TAMD_SLICE_BYTES_WIDE;
-    }();
-    return b;
-}
-
 // ---------------------------------------------------------------------------------------------
 // RowTable
 // ---------------------------------------------------------------------------------------------

@@ -45,9 +45,8 @@ struct Term {
 // A symbolic buffer.  `terms` may contain duplicates; they are merged when materialized.
 typedef std::vector<Term> Sym;
 
-// Bytes of an op one device work item covers (program.h): TAMD_SLICE_BYTES_WIDE (tamd_exec16)
-// unless TONK_AMD_SLICE=512 selects the 8-byte-per-lane executor.  Fixed for the process.
-uint32_t slice_bytes();
+// Bytes of an op one device work item covers (program.h TAMD_SLICE_BYTES, tamd_exec16).
+inline uint32_t slice_bytes() { return TAMD_SLICE_BYTES; }
 
 // ---------------------------------------------------------------------------------------------
 // Arena bookkeeping: rows are contiguous ranges of 64-byte units in one device allocation.

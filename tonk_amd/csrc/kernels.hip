@@ -1,8 +1,8 @@
 // kernels.hip -- CDNA4 (gfx950) kernels of the Siamese engine.
 //
-// tamd_exec runs one level of a device program (program.h).  A work item is one op over a
-// slice of its rows (512 bytes, or 1024 in tamd_exec16): one 64-lane wave owns 8 (16) bytes per
-// lane of the op's three accumulators and walks the op's instruction list (wave-uniform, scalar loads).  GF(2^8)
+// tamd_exec16 runs one level of a device program (program.h).  A work item is one op over a
+// 1024-byte slice of its rows: one 64-lane wave owns 16 bytes per lane of the op's three
+// accumulators and walks the op's instruction list (wave-uniform, scalar loads).  GF(2^8)
 // multiplication by a wave-uniform coefficient uses three 8-entry product tables per
 // coefficient staged in LDS and v_perm_b32 byte lookups (x*c = T0[x&7] ^ T1[(x>>3)&7] ^
 // T2[x>>6]): ~11 VALU ops per dword, no divergent LDS gathers.  Coefficient 1 is a plain XOR.
@@ -461,10 +461,10 @@ __device__ __forceinline__ void exec_level(const tamd_op* __restrict__ ops, cons
     }
 }
 
-// tamd_exec16 (the default): 16 B per lane, 1024-byte slices, 6 rows per load batch (94 VGPRs,
-// 5 waves/SIMD).  tamd_exec (TONK_AMD_SLICE=512): 8 B per lane, 512-byte slices, 8 rows per
-// batch (74 VGPRs, 6 waves/SIMD).  Measured on the bench program: 61.6-62.2 us vs 62.7-63.5 us
-// per launch; 16 B per lane with 8-row batches (108 VGPRs, 4 waves/SIMD) took 67 us.
+// tamd_exec16: 16 B per lane, 1024-byte slices, 6 rows per load batch (94 VGPRs, 5 waves/SIMD).
+// Measured on the bench program (round 1): 61.6-62.2 us per launch, against 62.7-63.5 us for
+// 8 B per lane / 512-byte slices / 8-row batches and 67 us for 16 B per lane with 8-row batches
+// (108 VGPRs, 4 waves/SIMD); only this variant is built.
 #define TAMD_EXEC_KERNEL(name, NH, B)                                                                  \
     extern "C" __global__ void __launch_bounds__(256)                                                   \
     name(const tamd_op* __restrict__ ops, const tamd_instr* __restrict__ instrs,                       \
@@ -473,7 +473,6 @@ __device__ __forceinline__ void exec_level(const tamd_op* __restrict__ ops, cons
          unsigned long long* __restrict__ stamps) {                                                    \
         exec_level<NH, B>(ops, instrs, items, n_items, n_shared, arena, gf_perm, zrow, stamps);       \
     }
-TAMD_EXEC_KERNEL(tamd_exec, 1, 8)
 TAMD_EXEC_KERNEL(tamd_exec16, 2, 6)
 
 // GF self test: out[y * 256 + x] = x * y through the same v_perm path the executor uses.

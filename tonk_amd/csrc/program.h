@@ -33,10 +33,8 @@
 #include <stdint.h>
 
 #define TAMD_ROW_UNIT 64u
-/* A work item (one wave) covers one slice of an op: 512 bytes (8 B per lane, tamd_exec) or
-   1024 bytes (16 B per lane, tamd_exec16); the host picks one per process (tamd::slice_bytes). */
-#define TAMD_SLICE_BYTES 512u
-#define TAMD_SLICE_BYTES_WIDE 1024u
+/* A work item (one wave) covers one 1024-byte slice of an op (16 B per lane, tamd_exec16). */
+#define TAMD_SLICE_BYTES 1024u
 
 enum tamd_instr_kind {
     TAMD_I_ACC    = 1,

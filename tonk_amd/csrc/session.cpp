@@ -10,6 +10,7 @@
 #include "decoder.h"
 #include "device.h"
 #include "workload.h"
+#include "../../oracle/transcript.h"
 
 #include <hip/hip_runtime.h>
 
@@ -166,6 +167,21 @@ struct Stream {
     }
     int dec_ack(uint8_t* buf, uint32_t limit, uint32_t* used) { return dec->ack(buf, limit, used); }
     void stats(uint64_t e[9], uint64_t d[11]) { enc->stats(e, 9); dec->stats(d, 11); }
+    uint64_t vclock = 0;
+    void set_time(uint64_t ms) {
+        if (!vclock) enc->set_clock(&vclock);
+        vclock = ms;
+    }
+    int enc_retransmit(uint32_t* num, uint32_t* bytes, const uint8_t** data) {
+        const StoredOriginal* o = nullptr;
+        const Result rc = enc->retransmit(&o);
+        if (rc == kSuccess) {
+            *num = o->column;
+            *bytes = o->bytes - o->header_bytes;
+            *data = nullptr;  // the payload lives in HBM; the runner regenerates it for the digest
+        }
+        return rc;
+    }
 
     // ---- transcript ----
     void on_encode(int rc, const RecRef& r) {
@@ -193,6 +209,13 @@ struct Stream {
         snprintf(t, sizeof(t), "%c %d %u %u", kind, rc, a, b);
         tr.lines.push_back(t);
     }
+    void on_retransmit(int rc, uint32_t num, uint32_t bytes, uint64_t h) {
+        if (!tr.on) return;
+        wl::TextSink t;
+        wl::fmt_retransmit(t, rc, num, bytes, h);
+        t.text.pop_back();
+        tr.lines.push_back(t.text);
+    }
     void on_stats(const uint64_t e[9], const uint64_t d[11]) {
         if (!tr.on) return;
         std::string s = "S";
@@ -216,7 +239,7 @@ struct Session {
     std::vector<std::pair<uint64_t, uint64_t>> epoch_ticket;  // (epoch, ticket) awaiting release
     uint64_t last_ticket = 0, released_epoch = 0;
     double host_ms[6] = {0, 0, 0, 0, 0, 0};
-    uint32_t clock_msec = 0;  // packet send times of a step (RTO bookkeeping only)
+    uint64_t clock_msec = 0;  // packet send times of a step (RTO bookkeeping only)
     uint32_t row_cap = 0;
     // stage_host: every stream's inputs (both sides, packet order) in pinned host memory, and
     // the pinned landing buffer of a step's outgoing rows
@@ -337,7 +360,7 @@ struct Session {
             return std::chrono::duration<double, std::milli>(b - a).count();
         };
         const auto t0 = clk::now();
-        clock_msec = (uint32_t)time_msec();
+        clock_msec = time_msec();
         if (host_in && !finish) stage_inputs(originals);
         const uint64_t rel = completed_epoch();
         std::fill(busy_ms.begin(), busy_ms.end(), 0.0);
@@ -529,6 +552,8 @@ void* tamd_session_create(const tamd_session_params* p, char* err, size_t err_le
         q.ack_bytes = p->ack_bytes ? p->ack_bytes : 256;
         q.arq_lag = p->arq_lag;
         q.flush_max = p->flush_max;
+        q.rtx_every = p->rtx_every;
+        q.rtx_msec = p->rtx_msec ? p->rtx_msec : 1;
         q.seed_data = 1000 + q.stream_id;
         q.seed_loss = 2000 + q.stream_id;
         st->enc.reset(new Encoder(ctx.get(), raw->row_cap));
@@ -698,6 +723,8 @@ void tamd_session_host_ms(void* sp, double out[10]) {
 }
 
 void tamd_session_destroy(void* sp) { delete (Session*)sp; }
+
+void tamd_set_clock(uint64_t (*fn)(void)) { set_clock_source(fn); }
 
 int tamd_device_selftest(uint32_t device, char* err, size_t err_len) {
     Device d;

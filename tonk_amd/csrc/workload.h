@@ -58,8 +58,41 @@ struct Params {
     uint32_t ack_bytes = 256;  // decoder ack buffer size (>= SIAMESE_ACK_MIN_BYTES)
     uint32_t arq_lag = 0;      // 0: no ARQ
     uint32_t flush_max = 4096; // cap on end-of-stream recovery packets
+    // Retransmission (siamese_encoder_retransmit, SiameseEncoder.cpp:877-1044) under a virtual
+    // millisecond clock: every rtx_every originals the sender asks for up to kRtxPerTick
+    // retransmissions and sends them through the lossy channel; the clock advances rtx_msec per
+    // original so RTO decisions are deterministic.  0: off (the codec's own clock is used).
+    uint32_t rtx_every = 0, rtx_msec = 1;
     uint64_t seed_data = 1000, seed_loss = 2000;
 };
+
+static const uint32_t kRtxPerTick = 4;
+static const uint64_t kVirtualClockStart = 1000;  // ms (send times are never 0)
+
+// key=value workload arguments shared by every driver (golden_gen, cp_harness, cp_bench).
+// Returns false for an unknown key.
+inline bool parse_param(Params& p, const std::string& k, unsigned long long v) {
+    if (k == "stream") p.stream_id = (uint32_t)v;
+    else if (k == "n") p.n_originals = (uint32_t)v;
+    else if (k == "pmin") p.payload_min = (uint32_t)v;
+    else if (k == "pmax") p.payload_max = (uint32_t)v;
+    else if (k == "loss") p.loss_thresh = (uint32_t)v;
+    else if (k == "ge") p.ge_enable = (uint32_t)v;
+    else if (k == "gb") p.gb_thresh = (uint32_t)v;
+    else if (k == "bg") p.bg_thresh = (uint32_t)v;
+    else if (k == "lossrec") p.loss_on_recovery = (uint32_t)v;
+    else if (k == "fec") p.fec_rate_q16 = (uint32_t)v;
+    else if (k == "ack") p.ack_every = (uint32_t)v;
+    else if (k == "ackbytes") p.ack_bytes = (uint32_t)v;
+    else if (k == "arq") p.arq_lag = (uint32_t)v;
+    else if (k == "flush") p.flush_max = (uint32_t)v;
+    else if (k == "rtx") p.rtx_every = (uint32_t)v;
+    else if (k == "rtxms") p.rtx_msec = (uint32_t)v;
+    else if (k == "seed_data") p.seed_data = v;
+    else if (k == "seed_loss") p.seed_loss = v;
+    else return false;
+    return true;
+}
 
 // Payload bytes of original i (index within the stream).  Length and contents come from a
 // PCG stream seeded with (seed_data, i) so any packet can be regenerated independently (the
@@ -109,6 +142,7 @@ struct LossChannel {
 struct Summary {
     uint64_t originals = 0, lost_originals = 0, recoveries = 0, lost_recoveries = 0;
     uint64_t recovered = 0, arq_redelivered = 0, acks = 0, decode_calls = 0, flush_encodes = 0;
+    uint64_t retransmits = 0;
     uint64_t missing_at_end = 0;
 };
 
@@ -124,15 +158,21 @@ struct Summary {
 //   int  dec_decode(std::vector<uint32_t>& packetNums, DecRef& out)
 //   int  dec_ack(uint8_t* buf, uint32_t limit, uint32_t* used)
 //   void stats(uint64_t enc[9], uint64_t dec[11])
+//   void set_time(uint64_t msec)               -- virtual clock (retransmit scenarios only)
+//   int  enc_retransmit(uint32_t* packetNum, uint32_t* bytes, const uint8_t** data)
+//                                              -- data may be null (the runner regenerates it)
 // Transcript concept:
 //   on_encode(int rc, const RecRef&), on_decode(int rc, nums, const DecRef&), on_ack(...),
-//   on_event(char kind, int rc, uint32_t a, uint32_t b), on_stats(enc, dec)
+//   on_event(char kind, int rc, uint32_t a, uint32_t b), on_stats(enc, dec),
+//   on_retransmit(int rc, uint32_t packetNum, uint32_t bytes, uint64_t payload digest)
 template <class Backend, class Transcript>
 class Runner {
 public:
     Runner(const Params& p, Backend& be, Transcript& tr) : p_(p), be_(be), tr_(tr) {
         ch_.init(p_);
         ack_countdown_ = p_.ack_every;
+        rtx_countdown_ = p_.rtx_every;
+        now_ms_ = kVirtualClockStart;
         have_.assign(p_.n_originals, 0);
         col_of_.assign(p_.n_originals, 0);
     }
@@ -173,7 +213,38 @@ private:
     size_t arq_head_ = 0;
     uint32_t tokens_ = 0, next_ = 0;
     uint32_t ack_countdown_ = 0;  // originals until the next acknowledgement
+    uint32_t rtx_countdown_ = 0;  // originals until the next retransmission tick
+    uint64_t now_ms_ = 0;         // virtual clock (rtx_every > 0)
     std::vector<uint32_t> nums_;
+    std::vector<uint8_t> rtx_buf_;
+
+    // Retransmission tick (Tonk's PostRetransmit, TonkineseOutgoing.cpp:1079-1100): up to
+    // kRtxPerTick originals chosen by the encoder's RTO logic, each sent through the channel.
+    // Packet numbers equal stream indices here (every add succeeds from column 0).
+    void retransmit_tick() {
+        for (uint32_t k = 0; k < kRtxPerTick; ++k) {
+            uint32_t num = 0, bytes = 0;
+            const uint8_t* data = nullptr;
+            const int rc = be_.enc_retransmit(&num, &bytes, &data);
+            uint64_t h = 0;
+            if (rc == 0) {
+                if (!data && num < p_.n_originals) {
+                    rtx_buf_.resize(bytes ? bytes : 1);
+                    payload_bytes(p_, num, rtx_buf_.data(), bytes);
+                    data = rtx_buf_.data();
+                }
+                h = data ? fnv1a(data, bytes) : 0;
+            }
+            tr_.on_retransmit(rc, num, bytes, h);
+            if (rc != 0) break;
+            ++s_.retransmits;
+            if (ch_.lost() || num >= p_.n_originals) continue;
+            const int ro = be_.dec_add_original(num, num, bytes);
+            tr_.on_event('T', ro, num, 0);
+            if (!have_[num]) have_[num] = 1;
+            decode_loop();
+        }
+    }
 
     void decode_loop() {
         while (be_.dec_is_ready() == 0) {
@@ -207,6 +278,10 @@ private:
     }
 
     void one(uint32_t i) {
+        if (p_.rtx_every) {
+            now_ms_ += p_.rtx_msec;
+            be_.set_time(now_ms_);
+        }
         const uint32_t len = payload_length(p_, i);
         uint32_t col = 0;
         const int ra = be_.enc_add(i, len, &col);
@@ -240,6 +315,11 @@ private:
             if (rd == 0 && used > 0) re = be_.enc_ack(buf, used, &next);
             tr_.on_ack(rd, buf, used, re, next);
             ++s_.acks;
+        }
+
+        if (p_.rtx_every && --rtx_countdown_ == 0) {
+            rtx_countdown_ = p_.rtx_every;
+            retransmit_tick();
         }
 
         if (p_.arq_lag) {
