@@ -118,7 +118,10 @@ def _batch_digests(entry, threads=16):
             if sha256(t + want["summary"] + "\n") != want["sha256"]:
                 bad.append(base + i)
         summ = s.summary()
-        assert summ["missing_at_end"] == 0 and summ["disabled_codecs"] == 0, summ
+        # the reference does not always finish: stream 56 of cfg2 keeps 4 originals unrecovered
+        # after the 4096-packet end-of-stream flush; the session must agree stream by stream
+        want_missing = sum(int(v["summary"].split("missing=")[1].split()[0]) for v in entry["streams"].values())
+        assert summ["missing_at_end"] == want_missing and summ["disabled_codecs"] == 0, summ
         return bad
     finally:
         s.close()
