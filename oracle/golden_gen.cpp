@@ -131,6 +131,9 @@ struct RefBackend {
     int dec_ack(uint8_t* buf, uint32_t limit, uint32_t* used) {
         return siamese_decoder_ack(dec, buf, limit, used);
     }
+    // the reference is always driven one call at a time
+    bool enc_add_run(uint32_t, uint32_t, uint32_t, uint32_t*) { return false; }
+    bool dec_add_run(uint32_t, uint32_t, uint32_t, uint32_t) { return false; }
     void set_time(uint64_t ms) {
         g_vclock_on = true;
         g_vclock_ms = ms;

@@ -30,6 +30,9 @@ const char* const names[kSlots] = {"enc_add", "enc_encode", "enc_ack", "dec_add_
 } }
 #endif
 
+static int g_stub = 0;
+static int g_nobatch = 0;
+static uint64_t g_step_clock = 1000;  // nobatch=1: single adds only (the runner's fallback path)  // stub=1: encoder calls return at once; stub=2: decoder calls too
 struct Null {
     struct RecRef { RecoveryOut out; };
     struct DecRef {};
@@ -41,13 +44,27 @@ struct Null {
     int enc_add(uint32_t index, uint32_t len, uint32_t* col) {
         const uint32_t hb = length_header_bytes(len);
         TAMD_PROF_SCOPE(kEncAdd);
+        if (g_stub) { *col = index; return 0; }
         return enc->add(enc_rows[index], hb + len, hb, len, nullptr, col, true);
     }
-    int enc_encode(RecRef& r) { TAMD_PROF_SCOPE(kEncEncode); return enc->encode(r.out); }
+    bool enc_add_run(uint32_t index, uint32_t k, uint32_t len, uint32_t* col0) {
+        if (g_stub || g_nobatch) return false;
+        const uint32_t hb = length_header_bytes(len);
+        TAMD_PROF_SCOPE(kEncAdd);
+        return enc->add_run(&enc_rows[index], k, hb + len, hb, len, true, col0);
+    }
+    bool dec_add_run(uint32_t col0, uint32_t index, uint32_t k, uint32_t len) {
+        if (g_stub > 1 || g_nobatch) return false;
+        const uint32_t hb = length_header_bytes(len);
+        TAMD_PROF_SCOPE(kDecAddOrig);
+        return dec->add_run_inorder(col0, &dec_rows[index], k, hb + len, hb, len, true);
+    }
+    int enc_encode(RecRef& r) { TAMD_PROF_SCOPE(kEncEncode); if (g_stub) return 2; return enc->encode(r.out); }
     int enc_ack(const uint8_t* b, uint32_t n, uint32_t* next) { TAMD_PROF_SCOPE(kEncAck); return enc->acknowledge(b, n, next); }
     int dec_add_original(uint32_t col, uint32_t index, uint32_t len) {
         const uint32_t hb = length_header_bytes(len);
         TAMD_PROF_SCOPE(kDecAddOrig);
+        if (g_stub > 1) return 0;
         bool took = false;
         const int r = dec->add_original(col, dec_rows[index], hb + len, hb, len, nullptr, &took, true);
         return r;
@@ -63,7 +80,7 @@ struct Null {
         if (!took) ctx->rows.free_deferred(r.out.row);
         return rc;
     }
-    int dec_is_ready() { TAMD_PROF_SCOPE(kDecIsReady); return dec->is_ready(); }
+    int dec_is_ready() { TAMD_PROF_SCOPE(kDecIsReady); if (g_stub > 1) return 2; return dec->is_ready(); }
     std::vector<RecoveredPacket*> got;
     int dec_decode(std::vector<uint32_t>& nums, DecRef&) {
         TAMD_PROF_SCOPE(kDecDecode);
@@ -89,89 +106,23 @@ struct NoTr {
 
 // Poor man's sampling profiler (no perf in the container): SIGPROF every 100 us of CPU time
 // records the interrupted PC; `sample=FILE` writes them for addr2line.
-static uint64_t g_samples[1 << 20];
+static uint64_t g_samples[1 << 20], g_callers[1 << 20], g_callers2[1 << 20];
 static volatile size_t g_nsamples = 0;
 static void on_prof(int, siginfo_t*, void* uc) {
     const size_t n = g_nsamples;
     if (n < (1u << 20)) {
         g_samples[n] = (uint64_t)((ucontext_t*)uc)->uc_mcontext.gregs[REG_RIP];
+        // top of stack: the return address when the sample lands in a frameless leaf (memmove)
+        g_callers[n] = *(const uint64_t*)((ucontext_t*)uc)->uc_mcontext.gregs[REG_RSP];
+        // and the frame-pointer parent of that caller (builds with -fno-omit-frame-pointer)
+        const uint64_t* fp = (const uint64_t*)((ucontext_t*)uc)->uc_mcontext.gregs[REG_RBP];
+        const uint64_t sp = (uint64_t)((ucontext_t*)uc)->uc_mcontext.gregs[REG_RSP];
+        g_callers2[n] = ((uint64_t)fp >= sp && (uint64_t)fp < sp + (1u << 20) && ((uint64_t)fp & 7) == 0) ? fp[1] : 0;
         g_nsamples = n + 1;
     }
 }
 
-int main(int argc, char** argv) {
-    const char* sample_out = nullptr;
-    for (int i = 1; i < argc; ++i)
-        if (!strncmp(argv[i], "sample=", 7)) sample_out = argv[i] + 7;
-    gf_init();
-    wl::Params p;
-    p.loss_thresh = 42949673;
-    p.fec_rate_q16 = 1311;
-    p.ack_every = 64;
-    uint32_t streams = 8, step = 4096;
-    p.n_originals = 4096 * 6;
-    for (int i = 1; i < argc; ++i) {
-        const char* eq = strchr(argv[i], '=');
-        if (!eq) continue;
-        std::string k(argv[i], eq - argv[i]);
-        if (k == "sample") continue;
-        const unsigned long long v = strtoull(eq + 1, nullptr, 0);
-        if (k == "streams") streams = (uint32_t)v;
-        else if (k == "n") p.n_originals = (uint32_t)v;
-        else if (k == "step") step = (uint32_t)v;
-        else if (k == "loss") p.loss_thresh = (uint32_t)v;
-        else if (k == "fec") p.fec_rate_q16 = (uint32_t)v;
-        else if (k == "ack") p.ack_every = (uint32_t)v;
-        else if (k == "ge") p.ge_enable = (uint32_t)v;
-        else if (k == "gb") p.gb_thresh = (uint32_t)v;
-        else if (k == "bg") p.bg_thresh = (uint32_t)v;
-        else if (k == "arq") p.arq_lag = (uint32_t)v;
-    }
-    Context ctx;
-    ctx.rows.init(64ull << 30);
-    std::vector<std::unique_ptr<Null>> be(streams);
-    std::vector<std::unique_ptr<Encoder>> encs(streams);
-    std::vector<std::unique_ptr<Decoder>> decs(streams);
-    std::vector<wl::Params> ps(streams, p);
-    NoTr tr;
-    std::vector<std::unique_ptr<wl::Runner<Null, NoTr>>> run(streams);
-    for (uint32_t s = 0; s < streams; ++s) {
-        ps[s].seed_data = 1000 + s;
-        ps[s].seed_loss = 2000 + s;
-        encs[s].reset(new Encoder(&ctx, 1344));
-        decs[s].reset(new Decoder(&ctx, 1344));
-        be[s].reset(new Null());
-        be[s]->ctx = &ctx;
-        be[s]->enc = encs[s].get();
-        be[s]->dec = decs[s].get();
-        for (uint32_t i = 0; i < p.n_originals; ++i) {
-            be[s]->enc_rows.push_back(ctx.rows.alloc(1302));
-            be[s]->dec_rows.push_back(ctx.rows.alloc(1302));
-        }
-        run[s].reset(new wl::Runner<Null, NoTr>(ps[s], *be[s], tr));
-    }
-    uint64_t instrs = 0, ops = 0, acc_bytes = 0, store_bytes = 0;
-    if (sample_out) {
-        struct sigaction sa;
-        memset(&sa, 0, sizeof(sa));
-        sa.sa_sigaction = on_prof;
-        sa.sa_flags = SA_SIGINFO | SA_RESTART;
-        sigaction(SIGPROF, &sa, nullptr);
-        itimerval tv;
-        tv.it_interval.tv_sec = 0;
-        tv.it_interval.tv_usec = 100;
-        tv.it_value = tv.it_interval;
-        setitimer(ITIMER_PROF, &tv, nullptr);
-    }
-    const auto t0 = std::chrono::steady_clock::now();
-    for (uint32_t done = 0; done < p.n_originals; done += step) {
-        for (uint32_t s = 0; s < streams; ++s) run[s]->advance(step);
-        const uint64_t e = ctx.epoch;
-        {
-            TAMD_PROF_SCOPE(kFlushAll);
-            ctx.prepare_flush();
-        }
-        if (getenv("CP_BENCH_LEVELS") && done == step) {
+static void dump_levels(Context& ctx) {
             for (size_t b = 0; b < ctx.pb.level_ops().size(); ++b)
                 fprintf(stderr, "bucket %zu (level %zu class %zu): ops %u items %u\n", b, b / TAMD_COST_CLASSES, b % TAMD_COST_CLASSES,
                         ctx.pb.level_ops()[b], ctx.pb.level_items()[b]);
@@ -227,17 +178,99 @@ int main(int argc, char** argv) {
                         (unsigned long long)rcount[3], rcount[3] ? (double)rrows[3] / rcount[3] : 0.0);
             }
         }
-        instrs += ctx.pb.instrs().size();
-        ops += ctx.pb.ops().size();
-        acc_bytes += ctx.pb.acc_bytes();
-        store_bytes += ctx.pb.store_bytes();
-        {
-            TAMD_PROF_SCOPE(kFinish);
-            ctx.finish_flush();
-        }
-        {
-            TAMD_PROF_SCOPE(kRelease);
-            ctx.rows.release_up_to(e);
+
+int main(int argc, char** argv) {
+    const char* sample_out = nullptr;
+    for (int i = 1; i < argc; ++i)
+        if (!strncmp(argv[i], "sample=", 7)) sample_out = argv[i] + 7;
+    gf_init();
+    wl::Params p;
+    p.loss_thresh = 42949673;
+    p.fec_rate_q16 = 1311;
+    p.ack_every = 64;
+    uint32_t streams = 8, step = 4096;
+    p.n_originals = 4096 * 6;
+    for (int i = 1; i < argc; ++i) {
+        const char* eq = strchr(argv[i], '=');
+        if (!eq) continue;
+        std::string k(argv[i], eq - argv[i]);
+        if (k == "sample") continue;
+        if (k == "stub") { g_stub = atoi(eq + 1); continue; }
+        if (k == "nobatch") { g_nobatch = atoi(eq + 1); continue; }
+        const unsigned long long v = strtoull(eq + 1, nullptr, 0);
+        if (k == "streams") streams = (uint32_t)v;
+        else if (k == "n") p.n_originals = (uint32_t)v;
+        else if (k == "step") step = (uint32_t)v;
+        else if (k == "loss") p.loss_thresh = (uint32_t)v;
+        else if (k == "fec") p.fec_rate_q16 = (uint32_t)v;
+        else if (k == "ack") p.ack_every = (uint32_t)v;
+        else if (k == "ge") p.ge_enable = (uint32_t)v;
+        else if (k == "gb") p.gb_thresh = (uint32_t)v;
+        else if (k == "bg") p.bg_thresh = (uint32_t)v;
+        else if (k == "arq") p.arq_lag = (uint32_t)v;
+    }
+    // One Context per stream with each side's input rows contiguous, as the session lays them out
+    // (tamd_session_generate), and steps of `step` originals per stream.
+    std::vector<std::unique_ptr<Context>> ctxs(streams);
+    std::vector<std::unique_ptr<Null>> be(streams);
+    std::vector<std::unique_ptr<Encoder>> encs(streams);
+    std::vector<std::unique_ptr<Decoder>> decs(streams);
+    std::vector<wl::Params> ps(streams, p);
+    NoTr tr;
+    std::vector<std::unique_ptr<wl::Runner<Null, NoTr>>> run(streams);
+    for (uint32_t s = 0; s < streams; ++s) {
+        ps[s].seed_data = 1000 + s;
+        ps[s].seed_loss = 2000 + s;
+        ctxs[s].reset(new Context());
+        Context& ctx = *ctxs[s];
+        ctx.rows.init(4ull * p.n_originals * 1344 + (256u << 20));
+        encs[s].reset(new Encoder(&ctx, 1344));
+        encs[s]->set_clock(&g_step_clock);  // the session reads the clock once per step
+        decs[s].reset(new Decoder(&ctx, 1344));
+        be[s].reset(new Null());
+        be[s]->ctx = &ctx;
+        be[s]->enc = encs[s].get();
+        be[s]->dec = decs[s].get();
+        for (uint32_t i = 0; i < p.n_originals; ++i) be[s]->enc_rows.push_back(ctx.rows.alloc(1302));
+        for (uint32_t i = 0; i < p.n_originals; ++i) be[s]->dec_rows.push_back(ctx.rows.alloc(1302));
+        run[s].reset(new wl::Runner<Null, NoTr>(ps[s], *be[s], tr));
+    }
+    uint64_t instrs = 0, ops = 0, acc_bytes = 0, store_bytes = 0;
+    if (sample_out) {
+        struct sigaction sa;
+        memset(&sa, 0, sizeof(sa));
+        sa.sa_sigaction = on_prof;
+        sa.sa_flags = SA_SIGINFO | SA_RESTART;
+        sigaction(SIGPROF, &sa, nullptr);
+        itimerval tv;
+        tv.it_interval.tv_sec = 0;
+        tv.it_interval.tv_usec = 100;
+        tv.it_value = tv.it_interval;
+        setitimer(ITIMER_PROF, &tv, nullptr);
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t done = 0; done < p.n_originals; done += step) {
+        for (uint32_t s = 0; s < streams; ++s) {
+            Context& ctx = *ctxs[s];
+            run[s]->advance(step);
+            const uint64_t e = ctx.epoch;
+            {
+                TAMD_PROF_SCOPE(kFlushAll);
+                ctx.prepare_flush();
+            }
+            if (getenv("CP_BENCH_LEVELS") && done == step && s == 0) dump_levels(ctx);
+            instrs += ctx.pb.instrs().size();
+            ops += ctx.pb.ops().size();
+            acc_bytes += ctx.pb.acc_bytes();
+            store_bytes += ctx.pb.store_bytes();
+            {
+                TAMD_PROF_SCOPE(kFinish);
+                ctx.finish_flush();
+            }
+            {
+                TAMD_PROF_SCOPE(kRelease);
+                ctx.rows.release_up_to(e);
+            }
         }
     }
     const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -247,6 +280,11 @@ int main(int argc, char** argv) {
         setitimer(ITIMER_PROF, &off, nullptr);
         FILE* f = fopen(sample_out, "w");
         for (size_t i = 0; i < g_nsamples; ++i) fprintf(f, "%llx\n", (unsigned long long)g_samples[i]);
+        fclose(f);
+        f = fopen((std::string(sample_out) + ".callers").c_str(), "w");
+        for (size_t i = 0; i < g_nsamples; ++i)
+            fprintf(f, "%llx %llx %llx\n", (unsigned long long)g_samples[i], (unsigned long long)g_callers[i],
+                    (unsigned long long)g_callers2[i]);
         fclose(f);
         // the process's mappings, to resolve samples inside shared libraries
         std::string mp = std::string(sample_out) + ".maps";

@@ -24,6 +24,7 @@ static uint64_t g_arena_bytes = 512ull << 20;
 // dirty=1: the context visits only codecs touched since the last flush (Context::track_dirty,
 // as the siamese.h C ABI runs it); every backend call touches its codec like capi.cpp does.
 static bool g_dirty = false;
+static bool g_nobatch = false;  // nobatch=1: the runner's single-add path only
 
 struct Harness {
     Params p;
@@ -156,6 +157,36 @@ struct Harness {
         if (batch && (index + 1) % batch == 0) flush();
         return rc;
     }
+    // batched adds (the session's path), off with nobatch=1
+    bool enc_add_run(uint32_t index, uint32_t k, uint32_t len, uint32_t* col0) {
+        if (g_nobatch) return false;
+        std::vector<RowId> rows(k);
+        uint32_t framed = 0, header = 0;
+        for (uint32_t j = 0; j < k; ++j) {
+            rows[j] = write_original(index + j, len, &framed, &header);
+            if (rows[j] == kNoRow) { error = "arena full"; return false; }
+        }
+        if (!E()->add_run(rows.data(), k, framed, header, len, false, col0)) {
+            for (RowId r : rows) ctx.rows.free_deferred(r);
+            return false;
+        }
+        if (batch && (index + k) / batch != index / batch) flush();
+        return true;
+    }
+    bool dec_add_run(uint32_t col0, uint32_t index, uint32_t k, uint32_t len) {
+        if (g_nobatch) return false;
+        std::vector<RowId> rows(k);
+        uint32_t framed = 0, header = 0;
+        for (uint32_t j = 0; j < k; ++j) {
+            rows[j] = write_original(index + j, len, &framed, &header);
+            if (rows[j] == kNoRow) { error = "arena full"; return false; }
+        }
+        if (!D()->add_run_inorder(col0, rows.data(), k, framed, header, len, false)) {
+            for (RowId r : rows) ctx.rows.free_deferred(r);
+            return false;
+        }
+        return true;
+    }
     int enc_encode(RecRef& r) { return E()->encode(r.out); }
     int enc_ack(const uint8_t* buf, uint32_t n, uint32_t* next) { return E()->acknowledge(buf, n, next); }
     int dec_add_original(uint32_t col, uint32_t index, uint32_t len) {
@@ -269,6 +300,7 @@ int main(int argc, char** argv) {
         else if (k == "batch") batch = (uint32_t)v;
         else if (k == "arena_mb") g_arena_bytes = v << 20;
         else if (k == "dirty") g_dirty = v != 0;
+        else if (k == "nobatch") g_nobatch = v != 0;
         else if (parse_param(p, k, v)) {}
         else { fprintf(stderr, "bad key %s\n", k.c_str()); return 2; }
     }

@@ -200,6 +200,42 @@ Result Decoder::add_original(uint32_t packet_num, RowId row, uint32_t framed_byt
     return kSuccess;
 }
 
+// k add_original() calls for the next columns col0 .. col0 + k - 1 (rows[0..k)), batched.  Only taken while no recovery packet is pending: then none of
+// those calls can make is_ready() succeed (there is no recovery to check), and the new elements
+// lie beyond the window end, so each call only stores the row, sets its got bit and moves
+// NextExpected along (SiameseDecoder.cpp:1467-1536 restated for that case).
+bool Decoder::add_run_inorder(uint32_t col0, const RowId* rows, uint32_t k, uint32_t framed_bytes,
+                              uint32_t header_bytes, uint32_t payload_bytes, bool borrowed) {
+    if (disabled_ || head_ || has_recovered_ || !k) return false;
+    const uint32_t e0 = to_element(col0);
+    if (col_delta_negative(e0) || e0 < count_) return false;
+    grow_window(e0 + k);
+    for (uint32_t j = 0; j < k; ++j) {
+        const uint32_t e = e0 + j;
+        StoredOriginal& o = subs_[e / kSubwindow]->orig[e % kSubwindow];
+        if (o.row != kNoRow || o.host) drop_original(o);  // (slots past the window end are empty)
+        o.row = rows[j];
+        o.off = ctx_->rows.offset(rows[j]);
+        o.bytes = framed_bytes;
+        o.column = col_add(col0, j);
+        o.header_bytes = (uint8_t)header_bytes;
+        o.owned = borrowed ? 0 : 1;
+    }
+    for (uint32_t e = e0; e < e0 + k;) {  // got bits, a subwindow at a time
+        const uint32_t bit = e % kSubwindow;
+        const uint32_t n = std::min(kSubwindow - bit, e0 + k - e);
+        Subwindow* s = subs_[e / kSubwindow];
+        s->got |= (n == 64 ? ~0ull : ((1ull << n) - 1)) << bit;
+        s->got_count += n;
+        e += n;
+    }
+    if (e0 == next_expected_) next_expected_ = find_next_lost(e0 + k);
+    if (std::max(e0, cr_.element_start) < std::min(e0 + k, cr_.next_check_start)) checked_reset();
+    stats_[0] += k;
+    stats_[1] += (uint64_t)payload_bytes * k;
+    return true;
+}
+
 // PlugSumHoles (:1538-1602)
 bool Decoder::plug_sum_holes(uint32_t element_start) {
     for (uint32_t column : recovered_columns_) {

@@ -38,6 +38,11 @@ public:
     // Ownership of `row` passes to the decoder when *took_ownership is set.
     Result add_recovery(RowId row, uint32_t total_bytes, const uint8_t* tail, const uint8_t* host,
                         bool* took_ownership);
+    // Batched in-order add_original of columns col0 .. col0 + k - 1 (equal lengths, rows[0..k))
+    // while no recovery packet is pending, when is_ready() cannot succeed after any of them.
+    // Returns false, with nothing done, when that does not hold.
+    bool add_run_inorder(uint32_t col0, const RowId* rows, uint32_t k, uint32_t framed_bytes,
+                         uint32_t header_bytes, uint32_t payload_bytes, bool borrowed);
     Result is_ready();
     // siamese_decode: recovered packets are appended to `out` (increasing packet number).
     Result decode(std::vector<RecoveredPacket*>& out);

@@ -51,7 +51,24 @@ Result Encoder::add(RowId row, uint32_t framed_bytes, uint32_t header_bytes, uin
                     void* host, uint32_t* packet_num, bool borrowed) {
     if (disabled_) return kDisabled;
     if (remaining_slots() <= 0) return kMaxPacketsReached;
+    add_unchecked(row, ctx_->rows.offset(row), framed_bytes, header_bytes, payload_bytes, host, packet_num, borrowed);
+    return kSuccess;
+}
 
+// k consecutive add() calls that all succeed.
+bool Encoder::add_run(const RowId* rows, uint32_t k, uint32_t framed_bytes, uint32_t header_bytes,
+                      uint32_t payload_bytes, bool borrowed, uint32_t* first_col) {
+    if (disabled_ || remaining_slots() < k || !k) return false;
+    *first_col = next_column_;
+    uint32_t col = 0;
+    const RowTable& rt = ctx_->rows;
+    for (uint32_t j = 0; j < k; ++j)
+        add_unchecked(rows[j], rt.offset(rows[j]), framed_bytes, header_bytes, payload_bytes, nullptr, &col, borrowed);
+    return true;
+}
+
+inline void Encoder::add_unchecked(RowId row, uint32_t off, uint32_t framed_bytes, uint32_t header_bytes,
+                                   uint32_t payload_bytes, void* host, uint32_t* packet_num, bool borrowed) {
     const uint32_t column = next_column_;
     uint32_t element = count_;
     *packet_num = column;
@@ -66,7 +83,7 @@ Result Encoder::add(RowId row, uint32_t framed_bytes, uint32_t header_bytes, uin
     while (win_.size() < element) win_.push_back(StoredOriginal());
     StoredOriginal o;
     o.row = row;
-    o.off = ctx_->rows.offset(row);
+    o.off = off;
     o.bytes = framed_bytes;
     o.column = column;
     o.header_bytes = (uint8_t)header_bytes;
@@ -93,7 +110,6 @@ Result Encoder::add(RowId row, uint32_t framed_bytes, uint32_t header_bytes, uin
 
     stats_[0]++;
     stats_[1] += payload_bytes;
-    return kSuccess;
 }
 
 // EncoderPacketWindow::StartNewWindow (SiameseEncoder.cpp:163-181)

@@ -59,6 +59,10 @@ public:
     // borrowed row stays the caller's (device-resident inputs that outlive the codec).
     Result add(RowId row, uint32_t framed_bytes, uint32_t header_bytes, uint32_t payload_bytes,
                void* host, uint32_t* packet_num, bool borrowed = false);
+    // Batched add of k equally long packets (rows[0..k)): the window ends up exactly as after k
+    // add() calls.  Returns false, with nothing done, when one of those calls would not succeed.
+    bool add_run(const RowId* rows, uint32_t k, uint32_t framed_bytes, uint32_t header_bytes,
+                 uint32_t payload_bytes, bool borrowed, uint32_t* first_col);
     Result get(uint32_t packet_num, const StoredOriginal** out);
     void remove_before(uint32_t first_kept_column);
     Result acknowledge(const uint8_t* data, uint32_t bytes, uint32_t* next_expected);
@@ -128,6 +132,8 @@ private:
     }
 
     void drop_original(StoredOriginal& o);
+    void add_unchecked(RowId row, uint32_t off, uint32_t framed_bytes, uint32_t header_bytes, uint32_t payload_bytes,
+                       void* host, uint32_t* packet_num, bool borrowed);
     void start_new_window(uint32_t column);
     void reset_sums(uint32_t element_start);
     void remove_elements();

@@ -122,6 +122,19 @@ struct Stream {
         }
         return r;
     }
+    bool enc_add_run(uint32_t index, uint32_t k, uint32_t len, uint32_t* col0) {
+        const uint32_t hb = length_header_bytes(len);
+        if (!enc->add_run(&enc_rows[index], k, hb + len, hb, len, true, col0)) return false;
+        alg_bytes += (uint64_t)(hb + len) * k;
+        payload_bytes += (uint64_t)len * k;
+        return true;
+    }
+    bool dec_add_run(uint32_t col0, uint32_t index, uint32_t k, uint32_t len) {
+        const uint32_t hb = length_header_bytes(len);
+        if (!dec->add_run_inorder(col0, &dec_rows[index], k, hb + len, hb, len, true)) return false;
+        alg_bytes += (uint64_t)(hb + len) * k;
+        return true;
+    }
     int enc_encode(RecRef& r) {
         const Result rc = enc->encode(r.out);
         if (rc == kSuccess) {
@@ -554,6 +567,7 @@ void* tamd_session_create(const tamd_session_params* p, char* err, size_t err_le
         q.flush_max = p->flush_max;
         q.rtx_every = p->rtx_every;
         q.rtx_msec = p->rtx_msec ? p->rtx_msec : 1;
+        q.batch_adds = getenv("TONK_AMD_SINGLE_ADDS") ? 0 : 1;  // A/B switch (profiling)
         q.seed_data = 1000 + q.stream_id;
         q.seed_loss = 2000 + q.stream_id;
         st->enc.reset(new Encoder(ctx.get(), raw->row_cap));

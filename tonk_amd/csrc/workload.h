@@ -63,6 +63,7 @@ struct Params {
     // retransmissions and sends them through the lossy channel; the clock advances rtx_msec per
     // original so RTO decisions are deterministic.  0: off (the codec's own clock is used).
     uint32_t rtx_every = 0, rtx_msec = 1;
+    uint32_t batch_adds = 1;   // runs of quiet originals go to the backend as batched adds
     uint64_t seed_data = 1000, seed_loss = 2000;
 };
 
@@ -161,6 +162,13 @@ struct Summary {
 //   void set_time(uint64_t msec)               -- virtual clock (retransmit scenarios only)
 //   int  enc_retransmit(uint32_t* packetNum, uint32_t* bytes, const uint8_t** data)
 //                                              -- data may be null (the runner regenerates it)
+//   bool enc_add_run(uint32_t index, uint32_t k, uint32_t len, uint32_t* firstPacketNum)
+//   bool dec_add_run(uint32_t packetNum, uint32_t index, uint32_t k, uint32_t len)
+//        batched adds of k consecutive originals (all delivered, no event among them): each
+//        returns false, with nothing done, when it cannot give exactly the result of k single
+//        calls (for dec_add_run: k add_original calls each followed by an is_ready that reports
+//        NeedMoreData); the runner then makes the single calls.  A backend without batching
+//        returns false.
 // Transcript concept:
 //   on_encode(int rc, const RecRef&), on_decode(int rc, nums, const DecRef&), on_ack(...),
 //   on_event(char kind, int rc, uint32_t a, uint32_t b), on_stats(enc, dec),
@@ -180,10 +188,26 @@ public:
     uint32_t position() const { return next_; }
     const Summary& summary() const { return s_; }
 
-    // Feed the next `n` originals (and everything they trigger).
+    // Feed the next `n` originals (and everything they trigger).  Runs of originals that trigger
+    // nothing (delivered, no recovery packet, acknowledgement, retransmission or ARQ due after
+    // them) go to the backend as batched adds; the calls and results are those of single adds.
     void advance(uint32_t n) {
         const uint32_t end = std::min(p_.n_originals, next_ + n);
-        for (; next_ < end; ++next_) one(next_);
+        const bool batching = p_.batch_adds && !p_.rtx_every && p_.payload_min == p_.payload_max;
+        while (next_ < end) {
+            int drawn = -1;  // loss draw of original next_ made by quiet_run (-1: not drawn)
+            if (batching) {
+                const uint32_t k = quiet_run(end, drawn);
+                if (k > 1) {
+                    run_quiet(next_, k);
+                    next_ += k;
+                } else if (k == 1) {
+                    one(next_++, 0);
+                }
+                if (next_ >= end) break;
+            }
+            one(next_++, drawn);
+        }
     }
 
     // End of stream: lossless recovery packets until the decoder has everything, then stats.
@@ -277,7 +301,58 @@ private:
         decode_loop();
     }
 
-    void one(uint32_t i) {
+    // Length of the quiet run starting at next_ (at most end - next_): originals that are not
+    // lost and after which no recovery packet, acknowledgement or ARQ redelivery is due.  The
+    // channel is drawn for each of them; when the run ends at a lost original, that draw is
+    // returned in `drawn_next` (1) for the original's own call.
+    uint32_t quiet_run(uint32_t end, int& drawn_next) {
+        uint32_t kmax = end - next_;
+        if (p_.fec_rate_q16) {
+            const uint32_t room = (65535u - tokens_) / p_.fec_rate_q16;  // tokens stay below 65536
+            if (room < kmax) kmax = room;
+        }
+        if (p_.ack_every && ack_countdown_ - 1 < kmax) kmax = ack_countdown_ - 1;
+        if (p_.arq_lag && arq_head_ < pending_arq_.size()) {
+            const uint32_t due = pending_arq_[arq_head_] + p_.arq_lag;  // first index with ARQ
+            const uint32_t room = due > next_ ? due - next_ : 0;
+            if (room < kmax) kmax = room;
+        }
+        for (uint32_t j = 0; j < kmax; ++j) {
+            if (ch_.lost()) {
+                drawn_next = 1;
+                return j;
+            }
+        }
+        return kmax;
+    }
+
+    // k quiet originals from index i0 (every channel draw already made: all delivered).
+    void run_quiet(uint32_t i0, uint32_t k) {
+        const uint32_t len = payload_length(p_, i0);
+        uint32_t col0 = 0;
+        if (!be_.enc_add_run(i0, k, len, &col0)) {
+            for (uint32_t j = 0; j < k; ++j) one(i0 + j, 0);
+            return;
+        }
+        for (uint32_t j = 0; j < k; ++j) col_of_[i0 + j] = (col0 + j) & 0x3fffffu;
+        s_.originals += k;
+        if (be_.dec_add_run(col0, i0, k, len)) {
+            memset(&have_[i0], 1, k);
+        } else {
+            for (uint32_t j = 0; j < k; ++j) {
+                const int ro = be_.dec_add_original(col_of_[i0 + j], i0 + j, len);
+                tr_.on_event('O', ro, col_of_[i0 + j], 0);
+                have_[i0 + j] = 1;
+                decode_loop();
+            }
+        }
+        tokens_ += k * p_.fec_rate_q16;
+        if (p_.ack_every) ack_countdown_ -= k;
+    }
+
+    // One original: add, channel, recovery tokens, acknowledgement, retransmission, ARQ.
+    // `drawn`: its loss draw when already made (0 delivered, 1 lost), -1 to draw here.
+    void one(uint32_t i, int drawn = -1) {
         if (p_.rtx_every) {
             now_ms_ += p_.rtx_msec;
             be_.set_time(now_ms_);
@@ -288,7 +363,7 @@ private:
         tr_.on_event('a', ra, i, col);
         col_of_[i] = col;
         ++s_.originals;
-        if (ch_.lost()) {
+        if (drawn >= 0 ? drawn != 0 : ch_.lost()) {
             ++s_.lost_originals;
             pending_arq_.push_back(i);
         } else {
