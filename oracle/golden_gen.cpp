@@ -7,6 +7,9 @@
 // packet is also checked against the true payload so a fixture can never pin a wrong decode.
 //
 // usage: golden_gen transcript <out.txt> key=value...
+//        golden_gen transcripts <prefix> threads=T streams=S key=value...
+//                   (streams stream..stream+S-1 concurrently on T threads, one codec pair each;
+//                    <prefix><id>.txt per stream -- the C ABI's concurrent-codec check)
 //        golden_gen time threads=T streams=S reps=R key=value...
 #include "siamese.h"
 
@@ -235,17 +238,16 @@ int main(int argc, char** argv) {
     Params base;
     int threads = 1, streams = 1, reps = 1;
     const bool timing = strcmp(argv[1], "time") == 0;
+    const bool multi = strcmp(argv[1], "transcripts") == 0;
     const int first_kv = timing ? 2 : 3;
+    if (!timing && argc < 3) { fprintf(stderr, "missing output path\n"); return 2; }
     for (int i = first_kv; i < argc; ++i) {
         if (!parse_kv(base, threads, streams, reps, argv[i])) { fprintf(stderr, "bad arg %s\n", argv[i]); return 2; }
     }
 
-    if (!timing) {
-        RefBackend be(base);
-        RefTranscript tr;
-        Summary s = run_stream(base, be, tr);
-        FILE* f = fopen(argv[2], "wb");
-        if (!f) return 4;
+    auto write_transcript = [](const char* path, const RefTranscript& tr, const Summary& s, uint64_t bad) {
+        FILE* f = fopen(path, "wb");
+        if (!f) return false;
         fwrite(tr.t.text.data(), 1, tr.t.text.size(), f);
         fprintf(f, "Z originals=%llu lost=%llu recoveries=%llu lostrec=%llu recovered=%llu arq=%llu "
                    "acks=%llu decodes=%llu flush=%llu missing=%llu bad=%llu\n",
@@ -254,8 +256,42 @@ int main(int argc, char** argv) {
                 (unsigned long long)s.recovered, (unsigned long long)s.arq_redelivered,
                 (unsigned long long)s.acks, (unsigned long long)s.decode_calls,
                 (unsigned long long)s.flush_encodes, (unsigned long long)s.missing_at_end,
-                (unsigned long long)be.bad_recoveries);
+                (unsigned long long)bad);
         fclose(f);
+        return true;
+    };
+    if (multi) {
+        std::atomic<int> next{0};
+        std::atomic<unsigned long long> bad{0};
+        std::atomic<int> fails{0};
+        std::vector<std::thread> pool;
+        const std::string prefix = argv[2];
+        for (int t = 0; t < threads; ++t) {
+            pool.emplace_back([&]() {
+                for (;;) {
+                    const int s = next++;
+                    if (s >= streams) break;
+                    Params p = base;
+                    p.stream_id = base.stream_id + s;
+                    p.seed_data = 1000 + p.stream_id;
+                    p.seed_loss = 2000 + p.stream_id;
+                    RefBackend be(p);
+                    RefTranscript tr;
+                    const Summary sum = run_stream(p, be, tr);
+                    const std::string path = prefix + std::to_string(p.stream_id) + ".txt";
+                    if (!write_transcript(path.c_str(), tr, sum, be.bad_recoveries)) ++fails;
+                    bad += be.bad_recoveries;
+                }
+            });
+        }
+        for (auto& th : pool) th.join();
+        return fails.load() ? 4 : (bad.load() ? 5 : 0);
+    }
+    if (!timing) {
+        RefBackend be(base);
+        RefTranscript tr;
+        Summary s = run_stream(base, be, tr);
+        if (!write_transcript(argv[2], tr, s, be.bad_recoveries)) return 4;
         return be.bad_recoveries ? 5 : 0;
     }
 

@@ -141,3 +141,65 @@ def test_session_batch_matches_reference(golden_index, name):
     448..511): every stream's transcript digest equals the reference codec's."""
     bad = _batch_digests(golden_index["batches"][name])
     assert not bad, f"streams differing from the reference: {bad}"
+
+
+def test_capi_concurrent_codecs(golden_index, tmp_path):
+    """Sixteen encoder/decoder pairs driven through the siamese.h C ABI from eight threads at
+    once (each codec on one thread at a time, as siamese.h:58-59 requires): every stream's
+    transcript equals the reference codec's (BASELINE configs[2] streams 0..15)."""
+    import hashlib
+    exe = os.path.join(NATIVE, "_build", "capi_gen")
+    entry = golden_index["batches"]["cfg2_64x4096_p2_ack64"]
+    prefix = str(tmp_path / "s")
+    out = subprocess.run([exe, "transcripts", prefix, "threads=8", "streams=16", "stream=0"] + entry["args"],
+                         capture_output=True, timeout=600)
+    assert out.returncode == 0, out.stderr.decode()[-2000:]
+    bad = [s for s in range(16)
+           if hashlib.sha256(open(f"{prefix}{s}.txt", "rb").read()).hexdigest() != entry["streams"][str(s)]["sha256"]]
+    assert not bad, f"streams differing from the reference: {bad}"
+
+
+@pytest.mark.parametrize("name", ["c2_4096_p1_noack", "big_9000_p3_ack64"])
+def test_capi_arena_growth(golden_index, name):
+    """The C ABI arena starts at 2 MB with 64 KB segments, far below what these streams hold
+    (a 4096-packet window; 9000-byte packets): it must grow, not fail, and the transcript must
+    still equal the reference's (the reference only refuses past SIAMESE_MAX_PACKETS)."""
+    exe = os.path.join(NATIVE, "_build", "capi_gen")
+    args, _ = _args(golden_index, name)
+    env = dict(os.environ, TONK_AMD_ARENA_MB="2", TONK_AMD_SEGMENT_KB="64")
+    out = subprocess.run([exe, "transcript", "/dev/stdout"] + args, capture_output=True, timeout=600, env=env)
+    assert out.returncode == 0, out.stderr.decode()[-2000:]
+    want = golden_text(name)
+    assert out.stdout.decode() == want, first_diff(want, out.stdout.decode())
+
+
+def test_capi_device_failure_disables_codec(golden_index):
+    """A device failure (injected: every program after the 20th fails to stage) must surface as
+    Siamese_Disabled from siamese_encode / siamese_decode -- never as Success with stale bytes:
+    the driver memcmp-checks every recovered packet (exit 5 on a wrong one)."""
+    exe = os.path.join(NATIVE, "_build", "capi_gen")
+    args, _ = _args(golden_index, "c2_4096_p1_ack64")
+    env = dict(os.environ, TONK_AMD_FAIL_AFTER_PROGRAMS="20")
+    out = subprocess.run([exe, "transcript", "/dev/stdout"] + args, capture_output=True, timeout=600, env=env)
+    assert out.returncode == 0, out.stderr.decode()[-2000:]
+    lines = out.stdout.decode().splitlines()
+    assert "E 5" in lines, "encode never reported Siamese_Disabled after the device failure"
+    assert lines[-1].endswith("bad=0")
+
+
+def test_capi_arena_grows_past_many_chunks(golden_index, tmp_path):
+    """32 codec pairs alive at once with 48 MB segments each need about 3 GB: the C ABI arena
+    (256 MB to start) maps chunk after chunk of its reserved range, and every stream still
+    matches the reference."""
+    import hashlib
+    exe = os.path.join(NATIVE, "_build", "capi_gen")
+    entry = golden_index["batches"]["cfg2_64x4096_p2_ack64"]
+    prefix = str(tmp_path / "s")
+    env = dict(os.environ, TONK_AMD_SEGMENT_KB=str(48 << 10))
+    out = subprocess.run([exe, "transcripts", prefix, "threads=32", "streams=32", "stream=0"] + entry["args"],
+                         capture_output=True, timeout=600, env=env)
+    assert out.returncode == 0, out.stderr.decode()[-2000:]
+    assert b"cannot grow" not in out.stderr and b"disabled" not in out.stderr, out.stderr.decode()[-2000:]
+    bad = [s for s in range(32)
+           if hashlib.sha256(open(f"{prefix}{s}.txt", "rb").read()).hexdigest() != entry["streams"][str(s)]["sha256"]]
+    assert not bad, f"streams differing from the reference: {bad}"

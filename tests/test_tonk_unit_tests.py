@@ -16,15 +16,20 @@ EXE = os.path.join(ROOT, "oracle", "_ref", "tonk", "unit_tests_amd")
 
 
 @pytest.mark.gpu
-@pytest.mark.skipif(not os.environ.get("TONK_AMD_TONK_UNIT_TESTS"),
-                    reason="opt-in (TONK_AMD_TONK_UNIT_TESTS=1): ~5 min on one MI355X (SUCCESS, "
-                           "profiles/r01_tonk_unit_tests_gpu.txt), longer than a parity test should run")
+@pytest.mark.timeout(840)
 def test_tonk_unit_tests_with_mi355x_codec():
     if not os.path.exists(EXE):
         pytest.skip("oracle/_ref/tonk/unit_tests_amd not built (needs /root/reference at build time)")
     # the C ABI watchdog prints call/wait counts to stderr every 5 s (Tonk's own log is buffered)
+    # The log streams to gpurun_out/ while the test runs (a run that writes nothing for minutes
+    # looks hung to the GPU-box harness).
     env = dict(os.environ, TONK_AMD_CAPI_WATCH="5")
-    r = subprocess.run([EXE], stdin=subprocess.DEVNULL, capture_output=True, text=True, timeout=1200, env=env)
-    log = r.stdout + r.stderr
+    out_dir = os.path.join(ROOT, "gpurun_out")
+    os.makedirs(out_dir, exist_ok=True)
+    path = os.path.join(out_dir, "tonk_unit_tests.log")
+    with open(path, "w") as f:
+        r = subprocess.run([EXE], stdin=subprocess.DEVNULL, stdout=f, stderr=subprocess.STDOUT, timeout=800, env=env)
+    with open(path) as f:
+        log = f.read()
     assert r.returncode == 0, log[-3000:]
     assert "SUCCESS" in log, log[-3000:]

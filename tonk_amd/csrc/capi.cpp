@@ -6,6 +6,13 @@
 //   siamese_encode                                            : run program, D2H recovery row
 //   siamese_decode                                            : run program, D2H recovered rows
 // Host mirrors of originals back siamese_encoder_get/retransmit and siamese_decoder_get.
+//
+// Concurrency follows the reference contract (siamese.h:58-59): the caller serialises calls on
+// one codec, different codecs run concurrently.  Every codec owns its Context (pending program,
+// row table); their rows come from arena segments of a shared pool, and the arena grows by
+// mapping more memory into a reserved address range (no fixed cap short of the reservation).
+// Only Device calls (program upload/launch, copies, events) take the process-wide device lock,
+// and no lock is held while a call waits for the GPU.
 #define SIAMESE_BUILDING 1
 #include "../../include/siamese.h"
 
@@ -25,32 +32,24 @@ using namespace tamd;
 
 namespace {
 
-struct Runtime {
-    std::mutex mu;
-    Device dev;
-    Context ctx;
-    bool ok = false;
-};
-
-Runtime* g_rt = nullptr;
-std::mutex g_init_mu;
-
-// Call accounting for the watchdog (TONK_AMD_CAPI_WATCH=<seconds>): a thread prints to stderr how
-// many API calls and device waits ran, the longest lock wait, and whether a call is inside a
-// device wait right now -- to tell a slow path from a stuck one under a real caller (Tonk).
-std::atomic<uint64_t> g_calls{0}, g_waits{0}, g_wait_ns{0}, g_lock_wait_max_ns{0};
-std::atomic<int64_t> g_in_wait_since{0};
-bool g_watch = false;
-std::atomic<uint64_t> g_prepare_ns{0}, g_run_ns{0};
 int64_t now_ns() {
     return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
         .count();
 }
 
-// Per-entry-point accounting: calls and time spent holding the lock.
+// ---- call accounting for the watchdog (TONK_AMD_CAPI_WATCH=<seconds>) ----
+// A thread prints to stderr how many API calls and device waits ran, the longest device-lock
+// wait, and how many calls are inside a device wait right now -- to tell a slow path from a
+// stuck one under a real caller (Tonk).  Everything it reads is an atomic.
+std::atomic<uint64_t> g_calls{0}, g_waits{0}, g_wait_ns{0}, g_lock_wait_max_ns{0};
+std::atomic<uint64_t> g_programs{0}, g_launches{0}, g_prepare_ns{0}, g_run_ns{0};
+std::atomic<int> g_in_wait{0};
+std::atomic<int64_t> g_in_wait_since{0};  // start of the current run of overlapping waits
+bool g_watch = false;
+
 struct Site {
     const char* name;
-    std::atomic<uint64_t> calls{0}, held_ns{0};
+    std::atomic<uint64_t> calls{0}, ns{0};
     Site* next;
     explicit Site(const char* n);
 };
@@ -59,12 +58,43 @@ Site::Site(const char* n) : name(n), next(nullptr) {
     Site* head = g_sites.load();
     do { next = head; } while (!g_sites.compare_exchange_weak(head, this));
 }
-
-struct ApiLock {
-    std::unique_lock<std::mutex> lk;
+struct CallScope {
     Site& site;
-    int64_t t_in = 0;
-    explicit ApiLock(Site& s) : lk(g_rt->mu, std::defer_lock), site(s) {
+    int64_t t0;
+    explicit CallScope(Site& s) : site(s), t0(g_watch ? now_ns() : 0) { g_calls.fetch_add(1, std::memory_order_relaxed); }
+    ~CallScope() {
+        site.calls.fetch_add(1, std::memory_order_relaxed);
+        if (g_watch) site.ns.fetch_add((uint64_t)(now_ns() - t0), std::memory_order_relaxed);
+    }
+};
+#define API_CALL()                   \
+    static Site api_site_(__func__); \
+    CallScope api_scope_(api_site_)
+
+// ---- the process runtime: one device, one arena, a segment pool over it ----
+struct Runtime;
+Runtime* g_rt = nullptr;
+std::mutex g_init_mu;
+
+struct SegmentPool final : SegmentSource {
+    std::mutex mu;
+    uint64_t bump_units = 0;                                 // first never-used unit
+    std::vector<std::pair<uint64_t, uint32_t>> free_list;  // returned ranges
+    uint32_t seg_units = 1u << 16;                          // 4 MiB ranges by default
+    bool get(uint32_t min_units, uint64_t* base, uint32_t* units) override;
+    void put(uint64_t base, uint32_t units) override;
+};
+
+struct Runtime {
+    std::mutex dev_mu;  // every Device call
+    Device dev;
+    SegmentPool pool;
+    bool ok = false;
+};
+
+struct DevLock {
+    std::unique_lock<std::mutex> lk;
+    DevLock() : lk(g_rt->dev_mu, std::defer_lock) {
         if (!lk.try_lock()) {
             const int64_t t0 = now_ns();
             lk.lock();
@@ -72,85 +102,249 @@ struct ApiLock {
             uint64_t m = g_lock_wait_max_ns.load(std::memory_order_relaxed);
             while (w > m && !g_lock_wait_max_ns.compare_exchange_weak(m, w)) {}
         }
-        g_calls.fetch_add(1, std::memory_order_relaxed);
-        if (g_watch) t_in = now_ns();
-    }
-    ~ApiLock() {
-        site.calls.fetch_add(1, std::memory_order_relaxed);
-        if (g_watch) site.held_ns.fetch_add((uint64_t)(now_ns() - t_in), std::memory_order_relaxed);
     }
 };
-#define API_LOCK()                   \
-    static Site api_site_(__func__); \
-    ApiLock lk(api_site_)
+
+bool SegmentPool::get(uint32_t min_units, uint64_t* base, uint32_t* units) {
+    std::lock_guard<std::mutex> lk(mu);
+    for (size_t i = 0; i < free_list.size(); ++i) {
+        if (free_list[i].second >= min_units) {
+            *base = free_list[i].first;
+            *units = free_list[i].second;
+            free_list[i] = free_list.back();
+            free_list.pop_back();
+            return true;
+        }
+    }
+    const uint32_t n = min_units > seg_units ? min_units : seg_units;
+    const uint64_t end_bytes = (bump_units + n) * TAMD_ROW_UNIT;
+    {
+        DevLock dl;  // lock order: pool, then device
+        if (end_bytes > g_rt->dev.arena_bytes() && !g_rt->dev.grow_arena(end_bytes)) {
+            static std::atomic<int> reported{0};
+            if (!reported.exchange(1))
+                fprintf(stderr, "tonk_amd: the arena cannot grow to %llu MB (mapped %llu MB)\n",
+                        (unsigned long long)(end_bytes >> 20), (unsigned long long)(g_rt->dev.arena_bytes() >> 20));
+            return false;
+        }
+    }
+    *base = bump_units;
+    *units = n;
+    bump_units += n;
+    return true;
+}
+
+void SegmentPool::put(uint64_t base, uint32_t units) {
+    std::lock_guard<std::mutex> lk(mu);
+    free_list.push_back(std::make_pair(base, units));
+}
 
 void watch_loop(double period_s) {
     const int64_t start = now_ns();
     for (;;) {
         std::this_thread::sleep_for(std::chrono::duration<double>(period_s));
+        const int waiting = g_in_wait.load();
         const int64_t since = g_in_wait_since.load();
+        std::string w;
+        if (waiting > 0 && since)
+            w = " IN DEVICE WAIT: " + std::to_string(waiting) + " call(s), for " +
+                std::to_string((now_ns() - since) / 1000000) + " ms";
         fprintf(stderr, "[tonk_amd capi] t=%.1fs calls=%llu device_waits=%llu wait_ms=%.1f lock_wait_max_ms=%.2f%s\n",
                 (now_ns() - start) * 1e-9, (unsigned long long)g_calls.load(), (unsigned long long)g_waits.load(),
-                g_wait_ns.load() * 1e-6, g_lock_wait_max_ns.exchange(0) * 1e-6,
-                since ? (" IN DEVICE WAIT for " + std::to_string((now_ns() - since) / 1000000) + " ms").c_str() : "");
+                g_wait_ns.load() * 1e-6, g_lock_wait_max_ns.exchange(0) * 1e-6, w.c_str());
         fprintf(stderr, "[tonk_amd capi]   flush: prepare_ms=%.1f launch_ms=%.1f programs=%llu launches=%llu\n",
-                g_prepare_ns.load() * 1e-6, g_run_ns.load() * 1e-6, (unsigned long long)g_rt->dev.stats().programs,
-                (unsigned long long)g_rt->dev.stats().launches);
+                g_prepare_ns.load() * 1e-6, g_run_ns.load() * 1e-6, (unsigned long long)g_programs.load(),
+                (unsigned long long)g_launches.load());
         for (Site* st = g_sites.load(); st; st = st->next) {
             const uint64_t c = st->calls.load();
             if (c)
-                fprintf(stderr, "[tonk_amd capi]   %-28s calls=%llu held_ms=%.1f\n", st->name, (unsigned long long)c,
-                        st->held_ns.load() * 1e-6);
+                fprintf(stderr, "[tonk_amd capi]   %-28s calls=%llu ms=%.1f\n", st->name, (unsigned long long)c,
+                        st->ns.load() * 1e-6);
         }
     }
 }
 
 void release_host(void* host, void*) { free(host); }
 
-struct CEncoder {
-    Encoder* enc = nullptr;
-    uint8_t* recovery = nullptr;  // pinned: the D2H of each recovery packet lands here
-    size_t recovery_cap = 0;
+// A codec goes to Disabled (sticky, siamese.h:147-150): say why on stderr, once per reason.
+void report_disable(const char* where) {
+    static std::mutex mu;
+    static std::vector<const char*> seen;
+    std::lock_guard<std::mutex> lk(mu);
+    for (const char* w : seen)
+        if (w == where) return;
+    seen.push_back(where);
+    fprintf(stderr, "tonk_amd: codec disabled in %s%s\n", where, g_rt && g_rt->dev.failed() ? " (device failure)" : "");
+}
+#define DISABLE(codec) (report_disable(__func__), (codec)->set_disabled())
+
+// Packets added to a codec wait in the codec's own pinned staging (two halves) and reach the
+// arena in one H2D copy + one scatter launch: before the codec's next program, or when a half
+// fills up.  Adds never take the device lock.
+struct Staging {
+    static const size_t kFlushBytes = 1u << 20;  // packet bytes per half before it is sent
+    uint8_t* half[2] = {nullptr, nullptr};
+    size_t cap = 0;                  // bytes per half (packets + descriptors)
+    void* sent[2] = {nullptr, nullptr};  // event behind a sent half's copy (not yet waited for)
+    int cur = 0;
+    size_t used = 0;                 // packet bytes in the current half (16-B aligned)
+    std::vector<Device::ScatterIn> descs;
+
+    size_t need(size_t bytes, size_t n_desc) const { return ((bytes + 15) & ~(size_t)15) + n_desc * 16 + 16; }
+    // Enqueue the current half (caller holds the device lock).
+    void send_locked(Device& dev) {
+        if (descs.empty()) return;
+        dev.scatter_upload(half[cur], used, descs.data(), (uint32_t)descs.size());
+        descs.clear();
+        used = 0;
+    }
+    // Wait for (and forget) a half's pending copy.
+    static void settle(void*& ev) {
+        if (!ev) return;
+        Device::event_wait(ev);
+        DevLock dl;
+        g_rt->dev.event_release(ev);
+        ev = nullptr;
+    }
+    // After the codec waited for work enqueued behind every sent half: all halves are free.
+    void all_settled() {
+        for (void*& ev : sent)
+            if (ev) {
+                DevLock dl;
+                g_rt->dev.event_release(ev);
+                ev = nullptr;
+            }
+    }
+    bool grow(size_t want) {
+        settle(sent[0]);
+        settle(sent[1]);
+        for (uint8_t*& h : half) {
+            Device::host_free(h);
+            h = nullptr;
+        }
+        cap = want < (256u << 10) ? (256u << 10) : want;
+        for (uint8_t*& h : half)
+            if (!(h = (uint8_t*)Device::host_alloc(cap))) { cap = 0; return false; }
+        return true;
+    }
+    // Copy a packet into the staging for arena unit offset `row`.
+    bool stage(uint32_t row, const uint8_t* data, uint32_t n) {
+        if (used && (used + n > kFlushBytes || need(used + n, descs.size() + 1) > cap)) {
+            {
+                DevLock dl;
+                send_locked(g_rt->dev);
+                sent[cur] = g_rt->dev.record_event();
+                if (g_rt->dev.failed()) return false;
+            }
+            cur ^= 1;
+            settle(sent[cur]);
+        }
+        if (need(used + n, descs.size() + 1) > cap) {  // (only while the half is empty)
+            if (used) return false;
+            if (!grow(need(n, 1) + (64u << 10))) return false;
+        }
+        memcpy(half[cur] + used, data, n);
+        Device::ScatterIn d;
+        d.row = row;
+        d.len = n;
+        d.src = (uint32_t)used;
+        descs.push_back(d);
+        used = (used + n + 15) & ~(size_t)15;
+        return true;
+    }
+    ~Staging() {
+        for (uint8_t* h : half) Device::host_free(h);
+    }
 };
 
-struct CDecoder {
+// Per-codec state: its own Context (pending program + row table over pool segments).
+struct Codec {
+    Context ctx;
+    Staging staging;
+    uint8_t* pinned = nullptr;  // D2H landing buffer (recovery packet / recovered rows)
+    size_t pinned_cap = 0;
+    Codec() { ctx.rows.init_segmented(&g_rt->pool); }
+    uint64_t byte_offset(RowId r) const { return (uint64_t)ctx.rows.offset(r) * TAMD_ROW_UNIT; }
+    // The pinned buffer holds at least n bytes (no copy can be landing in it: every read into it
+    // was waited for before the call that issued it returned).
+    bool ensure_pinned(size_t n) {
+        if (n <= pinned_cap) return true;
+        Device::host_free(pinned);
+        pinned_cap = n < 4096 ? 4096 : n + n / 2;
+        pinned = (uint8_t*)Device::host_alloc(pinned_cap);
+        if (!pinned) pinned_cap = 0;
+        return pinned != nullptr;
+    }
+    // Before the codec's rows go back to the pool: nothing of its may still be in flight.
+    void quiesce() {
+        DevLock dl;
+        g_rt->dev.synchronize();
+        for (void*& ev : staging.sent)
+            if (ev) {
+                g_rt->dev.event_release(ev);
+                ev = nullptr;
+            }
+    }
+    ~Codec() { Device::host_free(pinned); }
+};
+
+struct CEncoder : Codec {
+    Encoder* enc = nullptr;
+};
+
+struct CDecoder : Codec {
     Decoder* dec = nullptr;
     std::vector<SiameseOriginalPacket> out;
 };
 
-uint64_t row_byte_offset(RowId r) { return (uint64_t)g_rt->ctx.rows.offset(r) * TAMD_ROW_UNIT; }
-
-// Enqueues the pending program (caller holds the lock); reads of its results may be enqueued
-// behind it with Device::download_async before flush_complete() waits once for all of it.
-uint64_t flush_enqueue() {
-    Context& ctx = g_rt->ctx;
-    uint64_t ticket = 0;
+// Close the codec's pending program and enqueue it with the reads `enqueue_reads` adds behind
+// it, then wait for all of it without any lock.  Returns false on a device failure.
+template <class Reads>
+bool run_and_read(Codec& c, Reads enqueue_reads) {
+    Context& ctx = c.ctx;
     const int64_t t0 = g_watch ? now_ns() : 0;
     ctx.prepare_flush();
     const int64_t t1 = g_watch ? now_ns() : 0;
-    if (!ctx.pb.empty()) ticket = g_rt->dev.run(&ctx);
+    void* ev = nullptr;
+    bool ok = true;
+    {
+        DevLock dl;
+        Device& dev = g_rt->dev;
+        const uint64_t launches = dev.stats().launches;
+        c.staging.send_locked(dev);  // packets added since the last program land first
+        if (!ctx.pb.empty()) {
+            dev.run(&ctx);
+            g_programs.fetch_add(1, std::memory_order_relaxed);
+            g_launches.fetch_add(dev.stats().launches - launches, std::memory_order_relaxed);
+        }
+        enqueue_reads(dev);
+        ev = dev.record_event();
+        ok = !dev.failed();
+    }
     if (g_watch) {
         g_prepare_ns.fetch_add((uint64_t)(t1 - t0), std::memory_order_relaxed);
         g_run_ns.fetch_add((uint64_t)(now_ns() - t1), std::memory_order_relaxed);
     }
-    return ticket;
-}
-
-void flush_complete() {
-    Context& ctx = g_rt->ctx;
     const uint64_t done = ctx.epoch;
-    const int64_t t0 = now_ns();
-    g_in_wait_since.store(t0);
-    g_rt->dev.synchronize();
-    g_in_wait_since.store(0);
-    g_waits.fetch_add(1, std::memory_order_relaxed);
-    g_wait_ns.fetch_add((uint64_t)(now_ns() - t0), std::memory_order_relaxed);
     ctx.finish_flush();
-    ctx.rows.release_up_to(done);
+    const int64_t w0 = now_ns();
+    if (g_in_wait.fetch_add(1) == 0) g_in_wait_since.store(w0);
+    ok = Device::event_wait(ev) && ok;
+    if (g_in_wait.fetch_sub(1) == 1) g_in_wait_since.store(0);
+    g_waits.fetch_add(1, std::memory_order_relaxed);
+    g_wait_ns.fetch_add((uint64_t)(now_ns() - w0), std::memory_order_relaxed);
+    {
+        DevLock dl;
+        g_rt->dev.event_release(ev);
+        ok = ok && !g_rt->dev.failed();
+    }
+    c.staging.all_settled();         // every staged copy was enqueued before `ev`
+    ctx.rows.release_up_to(done);  // every program of this codec up to `done` has completed
+    return ok;
 }
 
-// varint(len) || payload into a malloc'd host buffer and a device row.
-bool store_framed(const unsigned char* data, unsigned len, uint8_t** host_out, RowId* row_out,
+// varint(len) || payload into a malloc'd host buffer and a device row of `c`.
+bool store_framed(Codec& c, const unsigned char* data, unsigned len, uint8_t** host_out, RowId* row_out,
                   uint32_t* framed_out, uint32_t* header_out) {
     uint8_t hdr[4];
     const uint32_t hb = put_length_header(len, hdr);
@@ -159,9 +353,13 @@ bool store_framed(const unsigned char* data, unsigned len, uint8_t** host_out, R
     if (!host) return false;
     memcpy(host, hdr, hb);
     memcpy(host + hb, data, len);
-    const RowId row = g_rt->ctx.alloc(framed);
+    const RowId row = c.ctx.alloc(framed);
     if (row == kNoRow) { free(host); return false; }
-    g_rt->dev.upload(row_byte_offset(row), host, framed);
+    if (!c.staging.stage(c.ctx.rows.offset(row), host, framed)) {
+        c.ctx.rows.free_deferred(row);
+        free(host);
+        return false;
+    }
     *host_out = host;
     *row_out = row;
     *framed_out = framed;
@@ -181,9 +379,19 @@ SIAMESE_EXPORT int siamese_init_(int version) {
     if (!gf_init()) return Siamese_Disabled;
     int device = 0;
     if (const char* d = getenv("TONK_AMD_DEVICE")) device = atoi(d);
-    uint64_t arena_mb = 2048;
+    // Initial arena (grown on demand up to TONK_AMD_ARENA_MAX_MB of reserved address space) and
+    // the size of the ranges codecs take from it.
+    uint64_t arena_mb = 256, max_mb = 64 << 10, seg_kb = 4096;
     if (const char* a = getenv("TONK_AMD_ARENA_MB")) arena_mb = strtoull(a, nullptr, 10);
-    if (!g_rt->dev.init(device, arena_mb << 20)) {
+    if (const char* a = getenv("TONK_AMD_ARENA_MAX_MB")) max_mb = strtoull(a, nullptr, 10);
+    if (const char* a = getenv("TONK_AMD_SEGMENT_KB")) seg_kb = strtoull(a, nullptr, 10);
+    if (arena_mb < 2) arena_mb = 2;
+    if (seg_kb < 64) seg_kb = 64;
+    g_rt->pool.seg_units = (uint32_t)(seg_kb * 1024 / TAMD_ROW_UNIT);
+    // many codecs each submit small programs: 32 staging slots, so a program waits for the one
+    // 32 back to finish rather than the one 2 back
+    g_rt->dev.set_program_slots(32, 1u << 20);
+    if (!g_rt->dev.init_growable(device, arena_mb << 20, max_mb << 20)) {
         fprintf(stderr, "%s\n", g_rt->dev.error().c_str());
         return Siamese_Disabled;
     }
@@ -191,8 +399,6 @@ SIAMESE_EXPORT int siamese_init_(int version) {
         fprintf(stderr, "tonk_amd: device GF(256) self test failed\n");
         return Siamese_Disabled;
     }
-    g_rt->ctx.rows.init(g_rt->dev.arena_bytes(), 0);
-    g_rt->ctx.track_dirty = true;
     g_rt->ok = true;
     if (const char* w = getenv("TONK_AMD_CAPI_WATCH")) {
         const double period = atof(w) > 0 ? atof(w) : 5.0;
@@ -206,30 +412,27 @@ SIAMESE_EXPORT int siamese_init_(int version) {
 
 SIAMESE_EXPORT SiameseEncoder siamese_encoder_create() {
     if (!g_rt || !g_rt->ok) return nullptr;
-    API_LOCK();
+    API_CALL();
     CEncoder* e = new (std::nothrow) CEncoder();
     if (!e) return nullptr;
-    e->enc = new Encoder(&g_rt->ctx, 0, release_host, nullptr);
+    e->enc = new Encoder(&e->ctx, 0, release_host, nullptr);
     return reinterpret_cast<SiameseEncoder>(e);
 }
 
 SIAMESE_EXPORT void siamese_encoder_free(SiameseEncoder encoder_t) {
     CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
     if (!e) return;
-    API_LOCK();
-    if (e->recovery) {
-        g_rt->dev.synchronize();  // no copy may still be landing in the buffer
-        Device::host_free(e->recovery);
-    }
-    delete e->enc;
-    delete e;
+    API_CALL();
+    delete e->enc;  // (the destructor may still close scans into the pending program)
+    e->enc = nullptr;
+    e->quiesce();
+    delete e;       // rows and segments go back to the pool
 }
 
 SIAMESE_EXPORT SiameseResult siamese_encoder_is_ready(SiameseEncoder encoder_t) {
     CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
     if (!e) return Siamese_InvalidInput;
-    API_LOCK();
-    g_rt->ctx.touch(e->enc);
+    API_CALL();
     if (e->enc->remaining_slots() <= 2) return Siamese_MaxPacketsReached;
     return Siamese_Success;
 }
@@ -238,18 +441,20 @@ SIAMESE_EXPORT SiameseResult siamese_encoder_add(SiameseEncoder encoder_t, Siame
     CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
     if (!e || !packet || !packet->Data || packet->DataBytes <= 0 || packet->DataBytes > SIAMESE_MAX_PACKET_BYTES)
         return Siamese_InvalidInput;
-    API_LOCK();
-    g_rt->ctx.touch(e->enc);
+    API_CALL();
     if (e->enc->disabled()) return Siamese_Disabled;
     if (e->enc->remaining_slots() <= 0) return Siamese_MaxPacketsReached;
     uint8_t* host = nullptr;
     RowId row = kNoRow;
     uint32_t framed = 0, hb = 0;
-    if (!store_framed(packet->Data, packet->DataBytes, &host, &row, &framed, &hb)) return Siamese_Disabled;
+    if (!store_framed(*e, packet->Data, packet->DataBytes, &host, &row, &framed, &hb)) {
+        DISABLE(e->enc);
+        return Siamese_Disabled;
+    }
     uint32_t pn = 0;
     const Result r = e->enc->add(row, framed, hb, packet->DataBytes, host, &pn);
     if (r != kSuccess) {
-        g_rt->ctx.rows.free_deferred(row);
+        e->ctx.rows.free_deferred(row);
         free(host);
         return (SiameseResult)r;
     }
@@ -260,8 +465,7 @@ SIAMESE_EXPORT SiameseResult siamese_encoder_add(SiameseEncoder encoder_t, Siame
 SIAMESE_EXPORT SiameseResult siamese_encoder_get(SiameseEncoder encoder_t, SiameseOriginalPacket* packet) {
     CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
     if (!e || !packet || packet->PacketNum > SIAMESE_PACKET_NUM_MAX) return Siamese_InvalidInput;
-    API_LOCK();
-    g_rt->ctx.touch(e->enc);
+    API_CALL();
     const StoredOriginal* o = nullptr;
     const Result r = e->enc->get(packet->PacketNum, &o);
     if (r != kSuccess) {
@@ -277,8 +481,7 @@ SIAMESE_EXPORT SiameseResult siamese_encoder_get(SiameseEncoder encoder_t, Siame
 SIAMESE_EXPORT SiameseResult siamese_encoder_remove_before(SiameseEncoder encoder_t, unsigned packetNum) {
     CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
     if (!e || packetNum > SIAMESE_PACKET_NUM_MAX) return Siamese_InvalidInput;
-    API_LOCK();
-    g_rt->ctx.touch(e->enc);
+    API_CALL();
     e->enc->remove_before(packetNum);
     return Siamese_Success;
 }
@@ -287,8 +490,7 @@ SIAMESE_EXPORT SiameseResult siamese_encoder_ack(SiameseEncoder encoder_t, const
                                                  unsigned* nextExpectedPacketNum) {
     CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
     if (!e || !buffer || bytes < 1 || !nextExpectedPacketNum) return Siamese_InvalidInput;
-    API_LOCK();
-    g_rt->ctx.touch(e->enc);
+    API_CALL();
     uint32_t next = 0;
     const Result r = e->enc->acknowledge((const uint8_t*)buffer, bytes, &next);
     if (r == kSuccess) *nextExpectedPacketNum = next;
@@ -298,8 +500,7 @@ SIAMESE_EXPORT SiameseResult siamese_encoder_ack(SiameseEncoder encoder_t, const
 SIAMESE_EXPORT SiameseResult siamese_encoder_retransmit(SiameseEncoder encoder_t, SiameseOriginalPacket* original) {
     CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
     if (!e || !original) return Siamese_InvalidInput;
-    API_LOCK();
-    g_rt->ctx.touch(e->enc);
+    API_CALL();
     original->Data = nullptr;
     original->DataBytes = 0;
     const StoredOriginal* o = nullptr;
@@ -314,54 +515,25 @@ SIAMESE_EXPORT SiameseResult siamese_encoder_retransmit(SiameseEncoder encoder_t
 SIAMESE_EXPORT SiameseResult siamese_encode(SiameseEncoder encoder_t, SiameseRecoveryPacket* recovery) {
     CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
     if (!e || !recovery) return Siamese_InvalidInput;
-    void* ev = nullptr;
-    uint64_t done = 0, ticket = 0;
-    uint32_t total = 0;
-    {
-        API_LOCK();
-        g_rt->ctx.touch(e->enc);
-        RecoveryOut out;
-        const Result r = e->enc->encode(out);
-        if (r != kSuccess) {
-            if (r == kNeedMoreData) recovery->DataBytes = 0;
-            return (SiameseResult)r;
-        }
-        total = out.total();
-        if (total > e->recovery_cap) {
-            if (e->recovery) {
-                g_rt->dev.synchronize();
-                Device::host_free(e->recovery);
-            }
-            e->recovery_cap = total < 2048 ? 2048 : total;
-            e->recovery = (uint8_t*)Device::host_alloc(e->recovery_cap);
-            if (!e->recovery) {
-                e->recovery_cap = 0;
-                g_rt->ctx.rows.free_deferred(out.row);
-                e->enc->set_disabled();
-                return Siamese_Disabled;
-            }
-        }
-        // Enqueue the program and the read of the recovery row behind it, close the program's
-        // host bookkeeping (later programs are stream-ordered after it), and wait for the copy
-        // without the lock so other codecs' calls proceed meanwhile.
-        ticket = flush_enqueue();
-        g_rt->dev.download_pinned(e->recovery, row_byte_offset(out.row), total);
-        ev = g_rt->dev.record_event();
-        done = g_rt->ctx.epoch;
-        g_rt->ctx.finish_flush();
-        g_rt->ctx.rows.free_deferred(out.row);  // released once the next program completes
+    API_CALL();
+    RecoveryOut out;
+    const Result r = e->enc->encode(out);
+    if (r == kDisabled) report_disable("Encoder::encode");
+    if (r != kSuccess) {
+        if (r == kNeedMoreData) recovery->DataBytes = 0;
+        return (SiameseResult)r;
     }
-    const int64_t t0 = now_ns();
-    Device::event_wait(ev);
-    g_waits.fetch_add(1, std::memory_order_relaxed);
-    g_wait_ns.fetch_add((uint64_t)(now_ns() - t0), std::memory_order_relaxed);
-    {
-        API_LOCK();
-        g_rt->dev.event_release(ev);
-        g_rt->dev.completed(ticket);  // retire finished programs' events
-        g_rt->ctx.rows.release_up_to(done);
+    const uint32_t total = out.total();
+    bool ok = e->ensure_pinned(total);
+    // the program and the read of the recovery row behind it, waited for without a lock
+    if (ok)
+        ok = run_and_read(*e, [&](Device& dev) { dev.download_pinned(e->pinned, e->byte_offset(out.row), total); });
+    e->ctx.rows.free_deferred(out.row);  // released once the codec's next program completes
+    if (!ok) {
+        DISABLE(e->enc);
+        return Siamese_Disabled;
     }
-    recovery->Data = e->recovery;
+    recovery->Data = e->pinned;
     recovery->DataBytes = total;
     return Siamese_Success;
 }
@@ -369,8 +541,7 @@ SIAMESE_EXPORT SiameseResult siamese_encode(SiameseEncoder encoder_t, SiameseRec
 SIAMESE_EXPORT SiameseResult siamese_encoder_stats(SiameseEncoder encoder_t, uint64_t* statsOut, unsigned statsCount) {
     CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
     if (!e || !statsOut || statsCount <= 0) return Siamese_InvalidInput;
-    API_LOCK();
-    g_rt->ctx.touch(e->enc);
+    API_CALL();
     e->enc->stats(statsOut, statsCount);
     return Siamese_Success;
 }
@@ -379,18 +550,20 @@ SIAMESE_EXPORT SiameseResult siamese_encoder_stats(SiameseEncoder encoder_t, uin
 
 SIAMESE_EXPORT SiameseDecoder siamese_decoder_create() {
     if (!g_rt || !g_rt->ok) return nullptr;
-    API_LOCK();
+    API_CALL();
     CDecoder* d = new (std::nothrow) CDecoder();
     if (!d) return nullptr;
-    d->dec = new Decoder(&g_rt->ctx, 0, release_host, nullptr);
+    d->dec = new Decoder(&d->ctx, 0, release_host, nullptr);
     return reinterpret_cast<SiameseDecoder>(d);
 }
 
 SIAMESE_EXPORT void siamese_decoder_free(SiameseDecoder decoder_t) {
     CDecoder* d = reinterpret_cast<CDecoder*>(decoder_t);
     if (!d) return;
-    API_LOCK();
+    API_CALL();
     delete d->dec;
+    d->dec = nullptr;
+    d->quiesce();
     delete d;
 }
 
@@ -400,20 +573,19 @@ SIAMESE_EXPORT SiameseResult siamese_decoder_add_original(SiameseDecoder decoder
         packet->PacketNum > SIAMESE_PACKET_NUM_MAX)
         return Siamese_InvalidInput;
     if (!packet->Data) return Siamese_InvalidInput;
-    API_LOCK();
-    g_rt->ctx.touch(d->dec);
+    API_CALL();
     if (d->dec->disabled()) return Siamese_Disabled;
     uint8_t* host = nullptr;
     RowId row = kNoRow;
     uint32_t framed = 0, hb = 0;
-    if (!store_framed(packet->Data, packet->DataBytes, &host, &row, &framed, &hb)) {
-        d->dec->set_disabled();
+    if (!store_framed(*d, packet->Data, packet->DataBytes, &host, &row, &framed, &hb)) {
+        DISABLE(d->dec);
         return Siamese_Disabled;
     }
     bool took = false;
     const Result r = d->dec->add_original(packet->PacketNum, row, framed, hb, packet->DataBytes, host, &took);
     if (!took) {
-        g_rt->ctx.rows.free_deferred(row);
+        d->ctx.rows.free_deferred(row);
         free(host);
     }
     return (SiameseResult)r;
@@ -423,25 +595,62 @@ SIAMESE_EXPORT SiameseResult siamese_decoder_add_recovery(SiameseDecoder decoder
     CDecoder* d = reinterpret_cast<CDecoder*>(decoder_t);
     if (!d || !packet || !packet->Data || packet->DataBytes <= 0 || packet->DataBytes > SIAMESE_MAX_PACKET_BYTES)
         return Siamese_InvalidInput;
-    API_LOCK();
-    g_rt->ctx.touch(d->dec);
+    API_CALL();
     if (d->dec->disabled()) return Siamese_Disabled;
     const uint32_t total = packet->DataBytes;
-    const RowId row = g_rt->ctx.alloc(total);
-    if (row == kNoRow) { d->dec->set_disabled(); return Siamese_Disabled; }
-    g_rt->dev.upload(row_byte_offset(row), packet->Data, total);
+    const RowId row = d->ctx.alloc(total);
+    if (row == kNoRow) { DISABLE(d->dec); return Siamese_Disabled; }
+    if (!d->staging.stage(d->ctx.rows.offset(row), packet->Data, total)) {
+        d->ctx.rows.free_deferred(row);
+        DISABLE(d->dec);
+        return Siamese_Disabled;
+    }
     const uint32_t tl = total < 8 ? total : 8;
     bool took = false;
     const Result r = d->dec->add_recovery(row, total, packet->Data + total - tl, packet->Data, &took);
-    if (!took) g_rt->ctx.rows.free_deferred(row);
+    if (!took) d->ctx.rows.free_deferred(row);
     return (SiameseResult)r;
 }
+
+namespace {
+
+// The host copy of recovered rows: `rows` read back behind the decoder's pending program into
+// the decoder's pinned buffer, then each framed row's length header parsed (BackSubstitution's
+// length check, SiameseDecoder.cpp:1139-1154) and its bytes copied to a malloc'd mirror.
+bool read_back(CDecoder& d, const std::vector<std::pair<StoredOriginal*, RowId>>& rows, const std::vector<uint32_t>& upper) {
+    size_t total = 0;
+    std::vector<size_t> at(rows.size());
+    for (size_t i = 0; i < rows.size(); ++i) {
+        at[i] = total;
+        total += (upper[i] + 63) & ~(size_t)63;
+    }
+    if (!d.ensure_pinned(total ? total : 64)) return false;
+    const bool ok = run_and_read(d, [&](Device& dev) {
+        for (size_t i = 0; i < rows.size(); ++i) dev.download_pinned(d.pinned + at[i], d.byte_offset(rows[i].second), upper[i]);
+    });
+    if (!ok) return false;
+    for (size_t i = 0; i < rows.size(); ++i) {
+        StoredOriginal* o = rows[i].first;
+        const uint8_t* src = d.pinned + at[i];
+        unsigned len = 0;
+        const int hb = get_length_header(src, upper[i], len);
+        if (hb < 1 || len == 0 || (uint32_t)hb + len > upper[i]) return false;
+        uint8_t* host = (uint8_t*)malloc((size_t)hb + len);
+        if (!host) return false;
+        memcpy(host, src, (size_t)hb + len);
+        o->host = host;
+        o->header_bytes = (uint32_t)hb;
+        o->bytes = (uint32_t)hb + len;
+    }
+    return true;
+}
+
+} // namespace
 
 SIAMESE_EXPORT SiameseResult siamese_decoder_get(SiameseDecoder decoder_t, SiameseOriginalPacket* packet) {
     CDecoder* d = reinterpret_cast<CDecoder*>(decoder_t);
     if (!d || !packet || packet->PacketNum > SIAMESE_PACKET_NUM_MAX) return Siamese_InvalidInput;
-    API_LOCK();
-    g_rt->ctx.touch(d->dec);
+    API_CALL();
     StoredOriginal* o = nullptr;
     const Result r = d->dec->get(packet->PacketNum, &o);
     if (r != kSuccess) {
@@ -450,17 +659,9 @@ SIAMESE_EXPORT SiameseResult siamese_decoder_get(SiameseDecoder decoder_t, Siame
         return (SiameseResult)r;
     }
     if (!o->host) {  // recovered data not read back yet
-        flush_enqueue();
-        uint8_t* host = (uint8_t*)malloc(o->bytes);
-        if (!host) { flush_complete(); return Siamese_Disabled; }
-        g_rt->dev.download_async(host, row_byte_offset(o->row), o->bytes);
-        flush_complete();
-        unsigned len = 0;
-        const int hb = get_length_header(host, o->bytes, len);
-        if (hb < 1 || len == 0 || (uint32_t)hb + len > o->bytes) { free(host); d->dec->set_disabled(); return Siamese_Disabled; }
-        o->host = host;
-        o->header_bytes = (uint32_t)hb;
-        o->bytes = (uint32_t)hb + len;
+        std::vector<std::pair<StoredOriginal*, RowId>> rows(1, std::make_pair(o, o->row));
+        std::vector<uint32_t> upper(1, o->bytes);
+        if (!read_back(*d, rows, upper)) { DISABLE(d->dec); return Siamese_Disabled; }
     }
     packet->Data = (const unsigned char*)o->host + o->header_bytes;
     packet->DataBytes = o->bytes - o->header_bytes;
@@ -470,8 +671,7 @@ SIAMESE_EXPORT SiameseResult siamese_decoder_get(SiameseDecoder decoder_t, Siame
 SIAMESE_EXPORT SiameseResult siamese_decoder_is_ready(SiameseDecoder decoder_t) {
     CDecoder* d = reinterpret_cast<CDecoder*>(decoder_t);
     if (!d) return Siamese_InvalidInput;
-    API_LOCK();
-    g_rt->ctx.touch(d->dec);
+    API_CALL();
     return (SiameseResult)d->dec->is_ready();
 }
 
@@ -479,52 +679,29 @@ SIAMESE_EXPORT SiameseResult siamese_decode(SiameseDecoder decoder_t, SiameseOri
                                             unsigned* countOut) {
     CDecoder* d = reinterpret_cast<CDecoder*>(decoder_t);
     if (!d || (!packetsPtrOut != !countOut)) return Siamese_InvalidInput;
-    API_LOCK();
-    g_rt->ctx.touch(d->dec);
+    API_CALL();
     if (packetsPtrOut) {
         *packetsPtrOut = nullptr;
         *countOut = 0;
     }
     std::vector<RecoveredPacket*> got;
     const Result r = d->dec->decode(got);
+    if (r == kDisabled) report_disable("Decoder::decode");
     if (r != kSuccess) return (SiameseResult)r;
-    flush_enqueue();
-    // every recovered row not read back yet: one D2H each behind the program, then one wait
-    std::vector<std::pair<StoredOriginal*, uint8_t*>> reads;
+    // every recovered row not read back yet: one D2H each behind the program, one wait
+    std::vector<std::pair<StoredOriginal*, RowId>> rows;
+    std::vector<uint32_t> upper;
     std::vector<StoredOriginal*> outs;
-    bool failed = false;
     for (RecoveredPacket* rp : got) {
         StoredOriginal* o = nullptr;
-        if (d->dec->get(rp->packet_num, &o) != kSuccess || !o) { failed = true; break; }
+        if (d->dec->get(rp->packet_num, &o) != kSuccess || !o) { DISABLE(d->dec); return Siamese_Disabled; }
         outs.push_back(o);
         if (!o->host) {
-            const uint32_t upper = rp->framed_upper;
-            uint8_t* host = (uint8_t*)malloc(upper ? upper : 1);
-            if (!host) { failed = true; break; }
-            g_rt->dev.download_async(host, row_byte_offset(rp->row), upper);
-            reads.push_back(std::make_pair(o, host));
-            o->bytes = upper;  // the upper bound until the header is parsed below
+            rows.push_back(std::make_pair(o, rp->row));
+            upper.push_back(rp->framed_upper);
         }
     }
-    flush_complete();
-    for (auto& rd : reads) {
-        StoredOriginal* o = rd.first;
-        uint8_t* host = rd.second;
-        if (failed) { free(host); continue; }
-        const uint32_t upper = o->bytes;
-        unsigned len = 0;
-        const int hb = get_length_header(host, upper, len);
-        // BackSubstitution's length check (SiameseDecoder.cpp:1139-1154).
-        if (hb < 1 || len == 0 || (uint32_t)hb + len > upper) {
-            free(host);
-            failed = true;
-            continue;
-        }
-        o->host = host;
-        o->header_bytes = (uint32_t)hb;
-        o->bytes = (uint32_t)hb + len;
-    }
-    if (failed) { d->dec->set_disabled(); return Siamese_Disabled; }
+    if (!read_back(*d, rows, upper)) { DISABLE(d->dec); return Siamese_Disabled; }
     d->out.clear();
     for (size_t i = 0; i < got.size(); ++i) {
         SiameseOriginalPacket p;
@@ -544,8 +721,7 @@ SIAMESE_EXPORT SiameseResult siamese_decoder_ack(SiameseDecoder decoder_t, void*
                                                  unsigned* usedBytes) {
     CDecoder* d = reinterpret_cast<CDecoder*>(decoder_t);
     if (!d || !buffer || !usedBytes || byteLimit < SIAMESE_ACK_MIN_BYTES) return Siamese_InvalidInput;
-    API_LOCK();
-    g_rt->ctx.touch(d->dec);
+    API_CALL();
     uint32_t used = 0;
     const Result r = d->dec->ack((uint8_t*)buffer, byteLimit, &used);
     *usedBytes = used;
@@ -555,8 +731,7 @@ SIAMESE_EXPORT SiameseResult siamese_decoder_ack(SiameseDecoder decoder_t, void*
 SIAMESE_EXPORT SiameseResult siamese_decoder_stats(SiameseDecoder decoder_t, uint64_t* statsOut, unsigned statsCount) {
     CDecoder* d = reinterpret_cast<CDecoder*>(decoder_t);
     if (!d || !statsOut || statsCount <= 0) return Siamese_InvalidInput;
-    API_LOCK();
-    g_rt->ctx.touch(d->dec);
+    API_CALL();
     d->dec->stats(statsOut, statsCount);
     return Siamese_Success;
 }

@@ -29,6 +29,7 @@ namespace tamd {
         if (e_ != hipSuccess) {                                                          \
             fprintf(stderr, "tonk_amd: %s failed: %s\n", #x, hipGetErrorString(e_));     \
             error_ = std::string(#x) + ": " + hipGetErrorString(e_);                    \
+            failed_ = true;                                                              \
         }                                                                                \
     } while (0)
 
@@ -58,11 +59,18 @@ Device::~Device() {
     if (gdesc_host_) hipHostFree(gdesc_host_);
     if (up_host_) hipHostFree(up_host_);
     if (up_dev_) hipFree(up_dev_);
+    if (sc_dev_) hipFree(sc_dev_);
     if (rb_host_) hipHostFree(rb_host_);
     if (up_event_) hipEventDestroy((hipEvent_t)up_event_);
     if (d_gf_) hipFree(d_gf_);
     if (d_zero_) hipFree(d_zero_);
-    if (arena_) hipFree(arena_);
+    if (reserved_bytes_) {
+        hipMemUnmap(arena_, arena_bytes_);
+        for (auto& c : chunks_) hipMemRelease((hipMemGenericAllocationHandle_t)c.first);
+        hipMemAddressFree(arena_, reserved_bytes_);
+    } else if (arena_) {
+        hipFree(arena_);
+    }
     if (stream_) hipStreamDestroy((hipStream_t)stream_);
 }
 
@@ -94,8 +102,10 @@ bool Device::init(int device, uint64_t arena_bytes) {
     hipStream_t s = nullptr;
     HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     stream_ = s;
-    arena_bytes_ = (arena_bytes + 255) & ~255ull;
-    HIPCHK(hipMalloc((void**)&arena_, arena_bytes_));
+    if (!reserved_bytes_) {  // (init_growable mapped the arena already)
+        arena_bytes_ = (arena_bytes + 255) & ~255ull;
+        HIPCHK(hipMalloc((void**)&arena_, arena_bytes_));
+    }
     HIPCHK(hipMemsetAsync(arena_, 0, arena_bytes_, s));
     if (!gf_init()) { error_ = "gf self test failed"; return false; }
     // kernels.hip TAMD_GF_DWORDS: perm tables, inv[256], sqr[256], then the lane table: for
@@ -129,7 +139,7 @@ bool Device::init(int device, uint64_t arena_bytes) {
     HIPCHK(hipHostMalloc((void**)&rb_host_, rb_cap_, hipHostMallocDefault));
     // Staging slots up front, each touched by one copy, so no step pays first-use costs.
     for (Slot& sl : slots_) {
-        if (!ensure_slot(sl, 16u << 20)) { error_ = "program staging allocation failed"; return false; }
+        if (!ensure_slot(sl, slot_bytes_)) { error_ = "program staging allocation failed"; return false; }
         memset(sl.host, 0, 4096);
         HIPCHK(hipMemcpyAsync(sl.dev, sl.host, 4096, hipMemcpyHostToDevice, s));
     }
@@ -138,12 +148,89 @@ bool Device::init(int device, uint64_t arena_bytes) {
     return error_.empty();
 }
 
+bool Device::init_growable(int device, uint64_t arena_bytes, uint64_t max_bytes) {
+    int vmm = 0;
+    if (max_bytes <= arena_bytes ||
+        hipDeviceGetAttribute(&vmm, hipDeviceAttributeVirtualMemoryManagementSupported, device) != hipSuccess || !vmm)
+        return init(device, arena_bytes);
+    // reserve the address range, map the first chunk, then the usual setup on top of it
+    hipMemAllocationProp prop = {};
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = device;
+    size_t gran = 0;
+    if (hipSetDevice(device) != hipSuccess ||
+        hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum) != hipSuccess || !gran)
+        return init(device, arena_bytes);
+    granule_ = gran < (2u << 20) ? (2u << 20) : gran;
+    const uint64_t maxb = (max_bytes + granule_ - 1) / granule_ * granule_;
+    void* base = nullptr;
+    if (hipMemAddressReserve(&base, maxb, 0, nullptr, 0) != hipSuccess || !base) return init(device, arena_bytes);
+    arena_ = (uint8_t*)base;
+    reserved_bytes_ = maxb;
+    arena_bytes_ = 0;
+    device_ = device;
+    if (!grow_arena(arena_bytes)) {
+        hipMemAddressFree(base, maxb);
+        arena_ = nullptr;
+        reserved_bytes_ = 0;
+        return init(device, arena_bytes);
+    }
+    return init(device, 0);
+}
+
+bool Device::map_chunk(uint64_t bytes) {
+    bytes = (bytes + granule_ - 1) / granule_ * granule_;
+    if (arena_bytes_ + bytes > reserved_bytes_) return false;
+    hipMemAllocationProp prop = {};
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = device_ >= 0 ? device_ : 0;
+    hipMemGenericAllocationHandle_t h;
+    hipError_t e = hipMemCreate(&h, bytes, &prop, 0);
+    if (e != hipSuccess) {
+        fprintf(stderr, "tonk_amd: hipMemCreate(%llu) failed: %s\n", (unsigned long long)bytes, hipGetErrorString(e));
+        return false;
+    }
+    e = hipMemMap(arena_ + arena_bytes_, bytes, 0, h, 0);
+    if (e != hipSuccess) {
+        fprintf(stderr, "tonk_amd: hipMemMap(+%llu, %llu) failed: %s\n", (unsigned long long)arena_bytes_,
+                (unsigned long long)bytes, hipGetErrorString(e));
+        hipMemRelease(h);
+        return false;
+    }
+    hipMemAccessDesc ad = {};
+    ad.location = prop.location;
+    ad.flags = hipMemAccessFlagsProtReadWrite;
+    e = hipMemSetAccess(arena_ + arena_bytes_, bytes, &ad, 1);
+    if (e != hipSuccess) {
+        fprintf(stderr, "tonk_amd: hipMemSetAccess failed: %s\n", hipGetErrorString(e));
+        hipMemUnmap(arena_ + arena_bytes_, bytes);
+        hipMemRelease(h);
+        return false;
+    }
+    chunks_.push_back(std::make_pair((unsigned long long)h, bytes));
+    arena_bytes_ += bytes;
+    return true;
+}
+
+bool Device::grow_arena(uint64_t min_bytes) {
+    if (!reserved_bytes_) return min_bytes <= arena_bytes_;
+    // fixed-size physical chunks (256 MiB), mapped back to back
+    const uint64_t chunk = ((256ull << 20) + granule_ - 1) / granule_ * granule_;
+    while (arena_bytes_ < min_bytes) {
+        if (arena_bytes_ + chunk > reserved_bytes_) return false;
+        if (!map_chunk(chunk)) return false;
+    }
+    return true;
+}
+
 bool Device::ensure_slot(Slot& s, size_t bytes) {
     if (s.cap >= bytes) return true;
     stats_.slot_reallocs++;
     if (s.host) hipHostFree(s.host);
     if (s.dev) hipFree(s.dev);
-    size_t cap = 16u << 20;  // a bench step's program is ~8 MB: avoid reallocating mid-run
+    size_t cap = slot_bytes_;  // a bench step's program is ~8 MB: avoid reallocating mid-run
     while (cap < bytes) cap *= 2;
     s.host = nullptr;
     s.dev = nullptr;
@@ -214,7 +301,7 @@ void Device::begin(Context* const* ctxs, size_t n) {
     P.total = P.bytes_instr + P.bytes_ops + P.n_items * sizeof(uint32_t) * 2;
 
     Slot& slot = slots_[next_slot_];
-    next_slot_ ^= 1;
+    next_slot_ = (next_slot_ + 1) % (int)slots_.size();
     if (slot.ticket) {
         const auto w0 = std::chrono::steady_clock::now();
         HIPCHK(hipEventSynchronize((hipEvent_t)slot.done));
@@ -223,8 +310,12 @@ void Device::begin(Context* const* ctxs, size_t n) {
         slot.ticket = 0;
     }
     P.slot = &slot;
-    if (!ensure_slot(slot, P.total)) {
+    // Test hook: TONK_AMD_FAIL_AFTER_PROGRAMS=<n> makes every program after the n-th fail as a
+    // staging allocation failure would (the C ABI must then report Siamese_Disabled).
+    static const long long fail_after = getenv("TONK_AMD_FAIL_AFTER_PROGRAMS") ? atoll(getenv("TONK_AMD_FAIL_AFTER_PROGRAMS")) : -1;
+    if (!ensure_slot(slot, P.total) || (fail_after >= 0 && (long long)stats_.programs >= fail_after)) {
         error_ = "program staging allocation failed";
+        failed_ = true;
         P.empty = true;
     }
 }
@@ -445,6 +536,33 @@ void Device::flush_uploads() {
     up_pending_.clear();
 }
 
+void Device::scatter_upload(uint8_t* src, size_t bytes, const ScatterIn* d, uint32_t n) {
+    if (!n) return;
+    flush_uploads();  // (stream order of the shared staging buffer)
+    hipStream_t st = (hipStream_t)stream_;
+    const size_t at = (bytes + 15) & ~(size_t)15;
+    ScatterDesc* sd = (ScatterDesc*)(src + at);
+    for (uint32_t k = 0; k < n; ++k) {
+        sd[k].row = d[k].row;
+        sd[k].len = d[k].len;
+        sd[k].src = d[k].src;
+        sd[k].pad = 0;
+    }
+    const size_t total = at + (size_t)n * sizeof(ScatterDesc);
+    if (total > sc_cap_) {  // the device landing area grows (after the stream drains)
+        HIPCHK(hipStreamSynchronize(st));
+        if (sc_dev_) hipFree(sc_dev_);
+        sc_cap_ = total + total / 2;
+        HIPCHK(hipMalloc((void**)&sc_dev_, sc_cap_));
+    }
+    // (the landing area is reused batch after batch: copies and scatters are stream ordered)
+    HIPCHK(hipMemcpyAsync(sc_dev_, src, total, hipMemcpyHostToDevice, st));
+    hipLaunchKernelGGL(tamd_scatter_rows, dim3(n), dim3(64), 0, st, (const ScatterDescDev*)(sc_dev_ + at), n,
+                       (const uint8_t*)sc_dev_, arena_);
+    HIPCHK(hipGetLastError());
+    stats_.upload_bytes += total;
+}
+
 void Device::download(void* dst, uint64_t off, size_t n) {
     if (n == 0) return;
     download_async(dst, off, n);
@@ -490,9 +608,10 @@ void* Device::record_event() {
     return e;
 }
 
-void Device::event_wait(void* ev) {
+bool Device::event_wait(void* ev) {
     const hipError_t e = hipEventSynchronize((hipEvent_t)ev);
     if (e != hipSuccess) fprintf(stderr, "tonk_amd: hipEventSynchronize failed: %s\n", hipGetErrorString(e));
+    return e == hipSuccess;
 }
 
 void* Device::host_alloc(size_t n) {

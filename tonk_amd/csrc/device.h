@@ -28,7 +28,20 @@ public:
     // Opens `device`, allocates the arena and uploads the GF tables.  Returns false (with a
     // message in error()) when no usable gfx950 device is present: the engine has no CPU path.
     bool init(int device, uint64_t arena_bytes);
+    // The same with a growable arena: `max_bytes` of address space reserved, `arena_bytes`
+    // mapped now, grow_arena() maps more (HIP virtual memory management).  Falls back to a
+    // fixed arena of `arena_bytes` where the device does not support it.
+    bool init_growable(int device, uint64_t arena_bytes, uint64_t max_bytes);
+    bool grow_arena(uint64_t min_bytes);  // arena_bytes() >= min_bytes afterwards, or false
+    // Program staging: `count` pinned/device slot pairs of `bytes` each (grown on demand), used
+    // round robin; a program waits only for the program `count` back.  Call before init.
+    // Default 2 x 16 MB (the session's big step programs); the C ABI runs many small ones.
+    void set_program_slots(size_t count, size_t bytes) {
+        slots_.assign(count < 2 ? 2 : count, Slot());
+        slot_bytes_ = bytes;
+    }
     const std::string& error() const { return error_; }
+    bool failed() const { return failed_; }  // any HIP call failed (sticky; safe to read unlocked)
     uint64_t arena_bytes() const { return arena_bytes_; }
     uint8_t* arena() const { return arena_; }
     void* stream() const { return stream_; }
@@ -55,6 +68,12 @@ public:
     // (the destination is valid after synchronize()).
     void upload(uint64_t arena_offset, const void* src, size_t n);
     void flush_uploads();
+    // A caller-staged batch of packets: `bytes` of packet data in pinned `src`, followed there by
+    // room for `n` descriptors (written here); one H2D copy and one tamd_scatter_rows launch
+    // put packet k at arena unit offset rows[k].  `src` must stay untouched until an event
+    // recorded after this call has completed.
+    struct ScatterIn { uint32_t row, len, src; };
+    void scatter_upload(uint8_t* pinned_src, size_t bytes, const ScatterIn* d, uint32_t n);
     void download(void* dst, uint64_t arena_offset, size_t n);
     void download_async(void* dst, uint64_t arena_offset, size_t n);
     // Reads that complete outside the caller's lock (the C ABI's encode): D2H straight into the
@@ -62,7 +81,7 @@ public:
     // any lock; record/release must hold the same lock as every other Device call.
     void download_pinned(void* pinned_dst, uint64_t arena_offset, size_t n);
     void* record_event();
-    static void event_wait(void* ev);
+    static bool event_wait(void* ev);  // false when the wait failed
     void event_release(void* ev) { free_events_.push_back(ev); }
     static void* host_alloc(size_t n);  // pinned
     static void host_free(void* p);
@@ -94,6 +113,11 @@ public:
 
 private:
     std::string error_;
+    volatile bool failed_ = false;
+    // growable arena (init_growable): reserved range, mapped prefix, physical chunks
+    uint64_t reserved_bytes_ = 0, granule_ = 0;
+    std::vector<std::pair<unsigned long long, uint64_t>> chunks_;  // (hipMemGenericAllocationHandle_t, bytes)
+    bool map_chunk(uint64_t bytes);
     int device_ = -1;
     uint8_t* arena_ = nullptr;
     uint64_t arena_bytes_ = 0;
@@ -123,7 +147,8 @@ private:
         void* done = nullptr;  // hipEvent_t
         uint64_t ticket = 0;
     };
-    Slot slots_[2];
+    std::vector<Slot> slots_ = std::vector<Slot>(2);
+    size_t slot_bytes_ = 16u << 20;
     // layout of the program being assembled (begin/fill/launch)
     struct Plan {
         std::vector<Context*> ctxs;
@@ -145,6 +170,8 @@ private:
     struct ScatterDesc { uint32_t row, len, src, pad; };
     uint8_t* up_host_ = nullptr;
     uint8_t* up_dev_ = nullptr;
+    uint8_t* sc_dev_ = nullptr;  // scatter_upload landing area
+    size_t sc_cap_ = 0;
     size_t up_cap_ = 0, up_used_ = 0, up_flushed_ = 0;
     std::vector<ScatterDesc> up_pending_;
     // readback staging: download_async() lands rows in pinned rb_host_; synchronize() copies

@@ -12,11 +12,19 @@ namespace tamd {
 // ---------------------------------------------------------------------------------------------
 static const uint32_t kSmallClasses = 256;  // rows up to 16 KB use exact-size free lists
 
+RowTable::~RowTable() {
+    if (src_)
+        for (const auto& s : segments_) src_->put(s.first, s.second);
+}
+
 void RowTable::init(uint64_t arena_bytes, uint64_t base_units) {
-    base_ = base_units;
     const uint64_t units = arena_bytes / TAMD_ROW_UNIT;
-    total_units_ = units > 0xfffffff0ull ? 0xfffffff0u : (uint32_t)units;
-    bump_ = 0;
+    uint64_t end = base_units + units;
+    if (end > 0xfffffff0ull) end = 0xfffffff0ull;  // 32-bit unit offsets: 256 GiB of arena
+    bump_ = (uint32_t)base_units;
+    bump_end_ = (uint32_t)end;
+    src_ = nullptr;
+    segments_.clear();
     used_units_ = 0;
     live_ = 0;
     off_.clear();
@@ -49,7 +57,15 @@ RowId RowTable::alloc(uint32_t bytes) {
         }
     }
     if (off == 0xffffffffu) {
-        if ((uint64_t)bump_ + units > total_units_) return kNoRow;
+        if ((uint64_t)bump_ + units > bump_end_) {
+            uint64_t base = 0;
+            uint32_t got = 0;
+            if (!src_ || !src_->get(units, &base, &got) || got < units || base + got > 0xfffffff0ull) return kNoRow;
+            segments_.push_back(std::make_pair(base, got));
+            // the old range's tail stays unused (rows are exact-size; tails are small)
+            bump_ = (uint32_t)base;
+            bump_end_ = (uint32_t)(base + got);
+        }
         off = bump_;
         bump_ += units;
     }
@@ -70,6 +86,11 @@ RowId RowTable::alloc(uint32_t bytes) {
     used_units_ += units;
     ++live_;
     return h;
+}
+
+void RowTable::init_segmented(SegmentSource* src) {
+    init(0, 0);
+    src_ = src;
 }
 
 void RowTable::release(RowId r) {

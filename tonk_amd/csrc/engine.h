@@ -51,12 +51,24 @@ inline uint32_t slice_bytes() { return TAMD_SLICE_BYTES; }
 // ---------------------------------------------------------------------------------------------
 // Arena bookkeeping: rows are contiguous ranges of 64-byte units in one device allocation.
 // ---------------------------------------------------------------------------------------------
+// Source of further arena segments for a RowTable that may grow (the siamese.h C ABI: one table
+// per codec, segments handed out by a shared pool).  get() returns a free range of at least
+// `min_units` 64-byte units (false when the arena cannot grow); put() takes a range back once no
+// pending device work can touch it.
+class SegmentSource {
+public:
+    virtual ~SegmentSource() {}
+    virtual bool get(uint32_t min_units, uint64_t* base_units, uint32_t* units) = 0;
+    virtual void put(uint64_t base_units, uint32_t units) = 0;
+};
+
 class RowTable {
 public:
+    ~RowTable();
     // Manage `bytes` of the device arena starting at 64-byte unit `base_units`.
     void init(uint64_t bytes, uint64_t base_units = 0);
-    uint64_t arena_bytes() const { return (uint64_t)total_units_ * TAMD_ROW_UNIT; }
-    uint64_t base_units() const { return base_; }
+    // Grow on demand: every range comes from `src` (none up front); returned to it on destruction.
+    void init_segmented(SegmentSource* src);
 
     // Allocate a row with capacity >= bytes (rounded up to 64 B).  Returns kNoRow when full.
     RowId alloc(uint32_t bytes);
@@ -70,7 +82,7 @@ public:
     void release_up_to(uint64_t completed_epoch);
     void seal_epoch(uint64_t epoch);  // rows freed so far belong to `epoch`
 
-    uint32_t offset(RowId r) const { return (uint32_t)(base_ + off_[r]); }  // 64-B units
+    uint32_t offset(RowId r) const { return off_[r]; }  // 64-B units from the arena base
     uint32_t cap_bytes(RowId r) const { return units_[r] * TAMD_ROW_UNIT; }
     uint32_t units(RowId r) const { return units_[r]; }
     // Only rows written by the pending program have a level; a bitmap keeps the common case
@@ -98,8 +110,9 @@ private:
     std::vector<Pending> pending_;  // nondecreasing epochs; [pending_head_, end) not yet released
     size_t pending_head_ = 0;
     uint64_t open_epoch_ = 1;       // epoch rows freed now belong to
-    uint32_t total_units_ = 0, bump_ = 0;
-    uint64_t base_ = 0;
+    uint32_t bump_ = 0, bump_end_ = 0;  // free tail of the current range (absolute units)
+    SegmentSource* src_ = nullptr;
+    std::vector<std::pair<uint64_t, uint32_t>> segments_;  // ranges taken from src_
     uint64_t used_units_ = 0;
     size_t live_ = 0;
     void release(RowId r);
