@@ -25,6 +25,11 @@ static uint64_t g_arena_bytes = 512ull << 20;
 // as the siamese.h C ABI runs it); every backend call touches its codec like capi.cpp does.
 static bool g_dirty = false;
 static bool g_nobatch = false;  // nobatch=1: the runner's single-add path only
+// pipeline=1: levels above Context::kPipeDepth would run beside the next program's first levels
+// (the session's pipelined launches); every such pair of levels is checked for hazards (no op
+// of one reads or writes a row the other writes) before the programs run one after the other.
+static bool g_pipeline = false;
+#include <set>
 
 struct Harness {
     Params p;
@@ -38,6 +43,50 @@ struct Harness {
     TextSink out;
     uint64_t programs = 0, ops = 0, levels = 0, instrs = 0;
     std::string error;
+    // rows read / written per level of the previous program, for its levels above kPipeDepth
+    struct LevelRW { std::set<uint32_t> rd, wr; };
+    std::vector<LevelRW> tail;
+    uint64_t pipelined_pairs = 0;
+
+    std::vector<LevelRW> level_rw() const {
+        const auto& ops_v = ctx.pb.ops();
+        const auto& lv = ctx.pb.op_levels();
+        const auto& in = ctx.pb.instrs();
+        std::vector<LevelRW> out(ctx.pb.max_level() + 1);
+        for (size_t i = 0; i < ops_v.size(); ++i) {
+            LevelRW& r = out[lv[i] / TAMD_COST_CLASSES];
+            for (uint32_t k = ops_v[i].first; k < ops_v[i].first + ops_v[i].count; ++k) {
+                const uint32_t kind = in[k].w0 & 0xff;
+                if (kind == TAMD_I_ACC || kind == TAMD_I_ACC3) r.rd.insert(in[k].row);
+                else if (kind == TAMD_I_ACCR)
+                    for (uint32_t q = 0; q < in[k].cap; ++q) r.rd.insert(in[k].row + q * in[k + 1].row);
+                else if (kind == TAMD_I_STORE || kind == TAMD_I_STOREC) r.wr.insert(in[k].row);
+            }
+        }
+        return out;
+    }
+    static bool meets(const std::set<uint32_t>& a, const std::set<uint32_t>& b) {
+        for (uint32_t x : a)
+            if (b.count(x)) return true;
+        return false;
+    }
+    // Level j of this program runs beside level j + kPipeDepth of the previous one.
+    void check_pipeline() {
+        std::vector<LevelRW> cur = level_rw();
+        const uint32_t D = Context::kPipeDepth;
+        for (uint32_t j = 1; j < cur.size() && j <= D; ++j) {
+            const uint32_t pl = j + D;
+            if (pl >= tail.size()) continue;
+            const LevelRW& a = cur[j];
+            const LevelRW& b = tail[pl];
+            const char* what = meets(a.rd, b.wr) ? "reads a row the previous program writes"
+                               : meets(a.wr, b.wr) ? "writes a row the previous program writes"
+                               : meets(a.wr, b.rd) ? "writes a row the previous program reads" : nullptr;
+            if (what && error.empty()) error = "pipelined level " + std::to_string(j) + " " + what;
+            ++pipelined_pairs;
+        }
+        tail.swap(cur);
+    }
 
     // transcript entries waiting for their rows to be computed
     struct PendEnc { RowId row; uint32_t total; RecoveryMeta meta; size_t pos; };
@@ -51,6 +100,7 @@ struct Harness {
         row_bytes = ((p.payload_max + 4 + 8 + 63) / 64) * 64;
         ctx.rows.init(g_arena_bytes);
         ctx.track_dirty = g_dirty;
+        ctx.pipeline = g_pipeline;
         arena.assign(g_arena_bytes, 0);
         enc = new Encoder(&ctx, row_bytes);
         dec = new Decoder(&ctx, row_bytes);
@@ -86,6 +136,7 @@ struct Harness {
 
     void flush() {
         ctx.prepare_flush();
+        if (g_pipeline) check_pipeline();
         const auto& ops_v = ctx.pb.ops();
         const auto& lv = ctx.pb.op_levels();
         const uint32_t maxl = ctx.pb.max_level();
@@ -113,7 +164,9 @@ struct Harness {
         resolve();
         const uint64_t done = ctx.epoch;
         ctx.finish_flush();
-        ctx.rows.release_up_to(done);
+        // pipelined, a program completes only with the next one's first levels: rows it freed are
+        // reusable one program later (the session releases by device completion events)
+        ctx.rows.release_up_to(g_pipeline ? done - 1 : done);
     }
 
     void resolve() {
@@ -301,6 +354,7 @@ int main(int argc, char** argv) {
         else if (k == "arena_mb") g_arena_bytes = v << 20;
         else if (k == "dirty") g_dirty = v != 0;
         else if (k == "nobatch") g_nobatch = v != 0;
+        else if (k == "pipeline") g_pipeline = v != 0;
         else if (parse_param(p, k, v)) {}
         else { fprintf(stderr, "bad key %s\n", k.c_str()); return 2; }
     }
@@ -320,9 +374,9 @@ int main(int argc, char** argv) {
             (unsigned long long)s.acks, (unsigned long long)s.decode_calls,
             (unsigned long long)s.flush_encodes, (unsigned long long)s.missing_at_end);
     fclose(f);
-    fprintf(stderr, "programs=%llu ops=%llu instrs=%llu levels=%llu live_rows=%zu\n",
+    fprintf(stderr, "programs=%llu ops=%llu instrs=%llu levels=%llu live_rows=%zu pipelined_pairs=%llu\n",
             (unsigned long long)h.programs, (unsigned long long)h.ops, (unsigned long long)h.instrs,
-            (unsigned long long)h.levels, h.ctx.rows.live_rows());
+            (unsigned long long)h.levels, h.ctx.rows.live_rows(), (unsigned long long)h.pipelined_pairs);
     if (!h.error.empty()) { fprintf(stderr, "error: %s\n", h.error.c_str()); return 6; }
     return 0;
 }

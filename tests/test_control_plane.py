@@ -9,7 +9,8 @@ must equal the REFERENCE codec's transcript byte for byte.
 Modes: ``sync`` runs each program as soon as a result is needed (one program per API call, as
 the C-ABI does); ``batch`` defers execution over ``batch`` originals (as the device-resident
 session does), which exercises chain snapshots, expansion of in-flight rows and multi-level
-programs.
+programs; ``batch-pipe`` adds the session's level pipelining (a program's upper levels run
+beside the next program's first levels) and checks those pairs for read/write hazards.
 """
 from __future__ import annotations
 
@@ -24,7 +25,8 @@ SCENARIOS = ["c1_256_p3", "c2_4096_p1_ack64", "c2_4096_p1_noack", "c3_4096_p2_ac
              "c3_4096_p2_ack64_s1", "c3_4096_p2_ack64_s63", "c4_4096_p1_ack64_s511", "c5_65536_ge5_b4",
              "var_1_1500_p2_ack32", "tiny_1_20_p5_ack16", "big_9000_p3_ack64", "hiloss_p20_arq",
              "norecloss_p5_arq", "single_p0", "burst8_p5", "rtx_p2_ack64", "rtx_p5_ack32", "rtx_p3_noack"]
-MODES = [("sync", 0), ("batch", 1000), ("batch", 4096), ("sync-dirty", 0), ("batch-dirty", 1000)]
+MODES = [("sync", 0), ("batch", 1000), ("batch", 4096), ("sync-dirty", 0), ("batch-dirty", 1000),
+         ("batch-pipe", 1000), ("batch-pipe", 4096)]
 
 
 @pytest.fixture(scope="module")
@@ -39,9 +41,11 @@ def test_control_plane_matches_reference(harness, golden_index, tmp_path, name, 
     sc = golden_index["scenarios"][name]
     sid = sc["stream"]
     out = tmp_path / "t.txt"
-    # "-dirty": flushes visit only the codecs touched since the last one (the C ABI's context)
-    base, dirty = mode.split("-")[0], int(mode.endswith("-dirty"))
-    args = [harness, str(out), f"mode={base}", f"batch={batch}", f"dirty={dirty}"] + sc["args"] + [
+    # "-dirty": flushes visit only the codecs touched since the last one (the C ABI's context);
+    # "-pipe": levels pipelined across programs as the session launches them, every pair of
+    # levels that would run together checked for hazards
+    base, dirty, pipe = mode.split("-")[0], int(mode.endswith("-dirty")), int(mode.endswith("-pipe"))
+    args = [harness, str(out), f"mode={base}", f"batch={batch}", f"dirty={dirty}", f"pipeline={pipe}"] + sc["args"] + [
         f"seed_data={1000 + sid}", f"seed_loss={2000 + sid}"]
     r = subprocess.run(args, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]

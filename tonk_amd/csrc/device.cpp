@@ -7,10 +7,12 @@
 #include <stdlib.h>
 #include <string.h>
 
-extern "C" __global__ void tamd_exec16(const tamd_op*, const tamd_instr*, const uint2*, uint32_t, uint32_t, uint8_t*,
+extern "C" __global__ void tamd_exec16(const tamd_op*, const tamd_instr*, const uint2*, uint32_t, uint32_t,
+                                       const tamd_op*, const tamd_instr*, const uint2*, uint32_t, uint8_t*,
                                        const uint32_t*, const uint8_t*, unsigned long long*);
-typedef void (*ExecFn)(const tamd_op*, const tamd_instr*, const uint2*, uint32_t, uint32_t, uint8_t*, const uint32_t*,
-                       const uint8_t*, unsigned long long*);
+typedef void (*ExecFn)(const tamd_op*, const tamd_instr*, const uint2*, uint32_t, uint32_t, const tamd_op*,
+                       const tamd_instr*, const uint2*, uint32_t, uint8_t*, const uint32_t*, const uint8_t*,
+                       unsigned long long*);
 extern "C" __global__ void tamd_gf_selftest(const uint32_t*, uint8_t*);
 extern "C" __global__ void tamd_gather_rows(const tamd::Device::GatherDesc*, uint32_t, const uint8_t*, uint8_t*);
 struct ScatterDescDev { uint32_t row, len, src, pad; };
@@ -302,6 +304,7 @@ void Device::begin(Context* const* ctxs, size_t n) {
 
     Slot& slot = slots_[next_slot_];
     next_slot_ = (next_slot_ + 1) % (int)slots_.size();
+    if (tail_.active && tail_.slot == &slot) finish_tail(Context::kPipeDepth + 1);  // (slot still holds it)
     if (slot.ticket) {
         const auto w0 = std::chrono::steady_clock::now();
         HIPCHK(hipEventSynchronize((hipEvent_t)slot.done));
@@ -364,11 +367,57 @@ void Device::fill(size_t c) {
     }
 }
 
+// One executor launch over up to two item segments (a: the previous program's deferred level,
+// b: a level of the program being launched; either may be empty).
+void Device::launch_level(const LevelSeg& a, const LevelSeg& b, unsigned long long* stamps) {
+    const uint32_t cnt = a.count + b.count;
+    if (!cnt) return;
+    hipStream_t st = (hipStream_t)stream_;
+    uint32_t grid = (cnt + 3) / 4;
+    if (grid > max_grid_) grid = max_grid_;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (timing_) {
+        e0 = (hipEvent_t)timing_event();
+        e1 = (hipEvent_t)timing_event();
+        hipEventRecord(e0, st);
+    }
+    // Class-0 ops are shared by a workgroup only in levels too small to fill the chip twice
+    // over with single-wave items; in the big levels they run as ordinary (first) items.  Only
+    // the first segment's class-0 items (they lead it) can be shared.
+    static const int share_mode = getenv("TONK_AMD_SHARE") ? atoi(getenv("TONK_AMD_SHARE")) : 0;  // A/B (profiling)
+    const LevelSeg& f = a.count ? a : b;
+    const LevelSeg& g = a.count ? b : a;
+    const uint32_t shared = (share_mode == 1 || (share_mode == 0 && cnt < 2u * 4u * max_grid_)) ? f.coop : 0u;
+    const ExecFn fn = (ExecFn)exec_kernel_;
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, st, f.ops, f.instrs, (const uint2*)f.items, f.count, shared, g.ops,
+                       g.instrs, (const uint2*)g.items, g.count, arena_, d_gf_, d_zero_, stamps);
+    if (timing_) {
+        hipEventRecord(e1, st);
+        timing_events_.push_back(std::make_pair((void*)e0, (void*)e1));
+    }
+    stats_.launches++;
+}
+
+// The deferred levels of the previous program that did not run beside this one's, then its
+// completion (slot event, ticket).
+void Device::finish_tail(uint32_t from_level) {
+    if (!tail_.active) return;
+    LevelSeg none;
+    for (uint32_t l = from_level; l < tail_.levels; ++l) launch_level(tail_.level(l), none, nullptr);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord((hipEvent_t)tail_.slot->done, (hipStream_t)stream_));
+    tail_.slot->ticket = tail_.ticket;
+    mark(tail_.ticket);
+    tail_.active = false;
+}
+
 uint64_t Device::launch() {
     flush_uploads();  // staged packets land before the program reads them
     Plan& P = plan_;
     const uint64_t ticket = ++ticket_;
+    const uint32_t D = Context::kPipeDepth;
     if (P.empty) {
+        finish_tail(D + 1);
         ticket_is_empty_ = true;
         mark(ticket);  // done once everything enqueued before it is done
         ticket_is_empty_ = false;
@@ -384,39 +433,38 @@ uint64_t Device::launch() {
         fprintf(stderr, "tonk_amd: program %llu: H2D enqueue of %zu bytes took %.3f ms\n",
                 (unsigned long long)ticket, P.total, up_ms);
     if (up_ms > stats_.upload_enqueue_max_ms) stats_.upload_enqueue_max_ms = up_ms;
-    const tamd_instr* di = (const tamd_instr*)slot.dev;
-    const tamd_op* dops = (const tamd_op*)(slot.dev + P.bytes_instr);
-    const uint2* ditems = (const uint2*)(slot.dev + P.bytes_instr + P.bytes_ops);
+    Tail cur;
+    cur.instrs = (const tamd_instr*)slot.dev;
+    cur.ops = (const tamd_op*)(slot.dev + P.bytes_instr);
+    cur.items = (const void*)(slot.dev + P.bytes_instr + P.bytes_ops);
+    cur.levels = P.levels;
+    cur.level_items = P.level_items;
+    cur.item_base = P.item_base;
+    cur.level_coop = P.level_coop;
+    cur.slot = &slot;
+    cur.ticket = ticket;
     // Profiling only: TONK_AMD_STAMPS=<program number> records per-item start/end stamps of that
     // program's launches and writes them to tonk_amd_stamps.bin (u64 triples per item; levels
-    // delimited by the item bases printed to stderr).
+    // delimited by the item bases printed to stderr).  Stamped programs are not pipelined.
     unsigned long long* stamps = nullptr;
     static const char* stamp_env = getenv("TONK_AMD_STAMPS");
     const bool stamp_this = stamp_env && (uint64_t)atoll(stamp_env) == stats_.programs;
-    if (stamp_this) HIPCHK(hipMalloc((void**)&stamps, P.n_items * 24 + 24));
-    for (uint32_t l = 1; l < P.levels; ++l) {
-        const uint32_t cnt = P.level_items[l];
-        if (!cnt) continue;
-        uint32_t grid = (cnt + 3) / 4;
-        if (grid > max_grid_) grid = max_grid_;
-        hipEvent_t e0 = nullptr, e1 = nullptr;
-        if (timing_) {
-            e0 = (hipEvent_t)timing_event();
-            e1 = (hipEvent_t)timing_event();
-            hipEventRecord(e0, st);
-        }
-        // Class-0 ops are shared by a workgroup only in levels too small to fill the chip twice
-        // over with single-wave items; in the big levels they run as ordinary (first) items.
-        const uint32_t shared = cnt < 2u * 4u * max_grid_ ? P.level_coop[l] : 0u;
-        const ExecFn fn = (ExecFn)exec_kernel_;
-        hipLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, st, dops, di, ditems + P.item_base[l], cnt, shared, arena_,
-                           d_gf_, d_zero_, stamps ? stamps + 3 * P.item_base[l] : nullptr);
-        if (timing_) {
-            hipEventRecord(e1, st);
-            timing_events_.push_back(std::make_pair((void*)e0, (void*)e1));
-        }
-        stats_.launches++;
+    if (stamp_this) {
+        finish_tail(D + 1);
+        HIPCHK(hipMalloc((void**)&stamps, P.n_items * 24 + 24));
     }
+    // Pipelined: level j of this program runs beside level j + D of the previous one; this
+    // program's levels above D wait for the next launch() (Context::kPipeDepth, inherited levels).
+    const bool defer = pipelined_ && !stamp_this && P.levels > D + 1;
+    const uint32_t own = defer ? D + 1 : P.levels;  // this program's levels launched now: [1, own)
+    LevelSeg none;
+    uint32_t l = 1;
+    for (; l < own || (tail_.active && l + D < tail_.levels && l <= D); ++l) {
+        const LevelSeg a = tail_.active && l <= D ? tail_.level(l + D) : none;
+        const LevelSeg b = l < own ? cur.level(l) : none;
+        launch_level(a, b, stamps ? stamps + 3 * P.item_base[l] : nullptr);
+    }
+    finish_tail(2 * D + 1);  // (the previous program's levels beyond 2D, then its completion)
     HIPCHK(hipGetLastError());
     if (stamp_this) {
         std::vector<unsigned long long> h(P.n_items * 3);
@@ -434,11 +482,16 @@ uint64_t Device::launch() {
             fclose(f);
         }
         fprintf(stderr, "stamps: n_instr_bytes %zu n_ops_bytes %zu n_items %zu\n", P.bytes_instr, P.bytes_ops, P.n_items);
-        for (uint32_t l = 0; l <= P.levels; ++l) fprintf(stderr, "stamps level %u item_base %u\n", l, P.item_base[l]);
+        for (uint32_t k = 0; k <= P.levels; ++k) fprintf(stderr, "stamps level %u item_base %u\n", k, P.item_base[k]);
     }
-    HIPCHK(hipEventRecord((hipEvent_t)slot.done, st));
-    slot.ticket = ticket;
-    mark(ticket);
+    if (defer) {
+        cur.active = true;
+        tail_ = cur;
+    } else {
+        HIPCHK(hipEventRecord((hipEvent_t)slot.done, st));
+        slot.ticket = ticket;
+        mark(ticket);
+    }
     stats_.programs++;
     stats_.ops += P.n_ops;
     stats_.items += P.n_items;
@@ -476,6 +529,7 @@ bool Device::completed(uint64_t ticket) {
 }
 
 void Device::wait(uint64_t ticket) {
+    if (tail_.active && ticket >= tail_.ticket) finish_tail(Context::kPipeDepth + 1);
     while (!inflight_.empty() && ticket > completed_) {
         HIPCHK(hipEventSynchronize((hipEvent_t)inflight_.front().second));
         if (inflight_.front().first > completed_) completed_ = inflight_.front().first;
@@ -485,6 +539,7 @@ void Device::wait(uint64_t ticket) {
 }
 
 void Device::synchronize() {
+    finish_tail(Context::kPipeDepth + 1);
     flush_uploads();
     HIPCHK(hipStreamSynchronize((hipStream_t)stream_));
     for (auto& p : inflight_) free_events_.push_back(p.second);
@@ -561,6 +616,14 @@ void Device::scatter_upload(uint8_t* src, size_t bytes, const ScatterIn* d, uint
                        (const uint8_t*)sc_dev_, arena_);
     HIPCHK(hipGetLastError());
     stats_.upload_bytes += total;
+}
+
+void Device::download_now(void* dst, uint64_t off, size_t n) {
+    if (n == 0) return;
+    flush_uploads();
+    hipStream_t st = (hipStream_t)stream_;
+    HIPCHK(hipMemcpyAsync(dst, arena_ + off, n, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
 }
 
 void Device::download(void* dst, uint64_t off, size_t n) {

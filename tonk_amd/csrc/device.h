@@ -57,6 +57,9 @@ public:
     void begin(Context* const* ctxs, size_t n);
     void fill(size_t i);
     uint64_t launch();
+    // Level pipelining across programs (the session; Context::kPipeDepth): a program's levels
+    // above the depth are launched beside the next program's first levels.
+    void set_pipelined(bool on) { pipelined_ = on; }
     bool completed(uint64_t ticket);
     void wait(uint64_t ticket);
     void synchronize();
@@ -75,6 +78,9 @@ public:
     struct ScatterIn { uint32_t row, len, src; };
     void scatter_upload(uint8_t* pinned_src, size_t bytes, const ScatterIn* d, uint32_t n);
     void download(void* dst, uint64_t arena_offset, size_t n);
+    // Synchronous copy that waits only for work already enqueued (deferred program levels stay
+    // deferred, unlike download()).
+    void download_now(void* dst, uint64_t arena_offset, size_t n);
     void download_async(void* dst, uint64_t arena_offset, size_t n);
     // Reads that complete outside the caller's lock (the C ABI's encode): D2H straight into the
     // caller's pinned buffer, then an event recorded behind it.  event_wait() may run without
@@ -161,6 +167,36 @@ private:
         bool empty = true;
     } plan_;
     int next_slot_ = 0;
+    // device view of one level of a program, and the deferred levels of the previous program
+    struct LevelSeg {
+        const tamd_op* ops = nullptr;
+        const tamd_instr* instrs = nullptr;
+        const void* items = nullptr;  // uint2 pairs (op, slice)
+        uint32_t count = 0, coop = 0;
+    };
+    struct Tail {
+        bool active = false;
+        const tamd_op* ops = nullptr;
+        const tamd_instr* instrs = nullptr;
+        const void* items = nullptr;  // uint2 pairs (op, slice)
+        uint32_t levels = 0;
+        std::vector<uint32_t> level_items, item_base, level_coop;
+        Slot* slot = nullptr;
+        uint64_t ticket = 0;
+        LevelSeg level(uint32_t l) const {
+            LevelSeg s;
+            if (l >= levels) return s;
+            s.ops = ops;
+            s.instrs = instrs;
+            s.items = (const char*)items + 8ull * item_base[l];
+            s.count = level_items[l];
+            s.coop = level_coop[l];
+            return s;
+        }
+    } tail_;
+    bool pipelined_ = false;
+    void launch_level(const LevelSeg& a, const LevelSeg& b, unsigned long long* stamps);
+    void finish_tail(uint32_t from_level);
     uint64_t ticket_ = 0, completed_ = 0;
     std::deque<std::pair<uint64_t, void*>> inflight_;  // (ticket, hipEvent_t) in stream order
     std::vector<void*> free_events_;

@@ -407,6 +407,11 @@ void ExpansionTable::append(const RowTable& rows, RowId r, uint32_t len, uint8_t
 // ---------------------------------------------------------------------------------------------
 // LaneSums
 // ---------------------------------------------------------------------------------------------
+uint32_t LaneSums::chunk() {
+    static const uint32_t c = getenv("TONK_AMD_CHUNK") ? (uint32_t)atoi(getenv("TONK_AMD_CHUNK")) : 64u;  // A/B
+    return c ? c : 64u;
+}
+
 void LaneSums::reset(RowTable& rows) {
     if (!snaps_.empty()) {
         Closed c;
@@ -441,7 +446,7 @@ void LaneSums::read(RowTable& rows, const ExpansionTable& ex, Sym& out, const ui
         if (snap == kNoRow) {
             snap = rows.alloc(content_);
             if (snap == kNoRow) return;  // caller checks arena exhaustion via RowTable
-            rows.set_level(snap, kSnapLevel);  // written by the scan's chain (or only) op
+            rows.set_level(snap, snap_level(rows, base_));  // written by the scan's chain (or only) op
             snaps_.push_back(Snap{snap, at, {c[0], c[1], c[2]}});
         }
         if (clip) out.push_back(Term{snap, clip, 1});
@@ -500,6 +505,7 @@ void LaneSums::emit_scan(RowTable& rows, ProgramBuilder& pb, const RowId* base, 
             ++si;
         }
     };
+    const uint32_t kChunk = chunk();
     if (n <= kChunk) {
         pb.begin_op();
         for (unsigned s = 0; s < 3; ++s)
@@ -516,7 +522,7 @@ void LaneSums::emit_scan(RowTable& rows, ProgramBuilder& pb, const RowId* base, 
         if (final_rows)
             for (unsigned s = 0; s < 3; ++s)
                 if (final_rows[s] != kNoRow) pb.op_storec(final_rows[s], rows.cap_bytes(final_rows[s]), unit[s]);
-        pb.end_op(kSnapLevel);
+        pb.end_op(snap_level(rows, base));
         return;
     }
 
@@ -555,7 +561,7 @@ void LaneSums::emit_scan(RowTable& rows, ProgramBuilder& pb, const RowId* base, 
     if (final_rows)
         for (unsigned s = 0; s < 3; ++s)
             if (final_rows[s] != kNoRow) pb.op_storec(final_rows[s], rows.cap_bytes(final_rows[s]), unit[s]);
-    pb.end_op(kSnapLevel);
+    pb.end_op(snap_level(rows, base));
     for (RowId d : deltas) rows.free_deferred(d);  // read only inside this program
 }
 

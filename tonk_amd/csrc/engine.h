@@ -280,11 +280,19 @@ private:
 public:
     // a run of `count` lane packets: rows off + k*stride, columns col + 8k (count 1: a single row)
     struct T { RowId row; uint32_t len, off, stride, count, col; };
-    static const uint32_t kChunk = 64;  // longest packet walk of one scan op (see emit_scan)
+    static uint32_t chunk();  // longest packet walk of one scan op (see emit_scan)
     // Level of snapshot rows: chunk ops run at level 1, the chain op that stores the snapshots at
     // level 2 (a short scan is one op, also placed at level 2).  Readers are assigned levels when
     // they read, before the scan is emitted, so the level is fixed up front.
     static const uint32_t kSnapLevel = 2;
+    // Level of a scan's snapshot rows over carried values `base` (kSnapLevel, or above the
+    // bases when they are still being written: rows of this program or inherited ones).
+    static uint32_t snap_level(const RowTable& rows, const RowId* base) {
+        uint32_t l = kSnapLevel;
+        for (unsigned s = 0; s < 3; ++s)
+            if (base[s] != kNoRow && rows.level(base[s]) + 1 > l) l = rows.level(base[s]) + 1;
+        return l;
+    }
 
 private:
     struct Snap { RowId row; uint32_t after; uint8_t c[3]; };  // after = packets accumulated
@@ -354,6 +362,14 @@ struct Context {
     uint64_t epoch = 1;                // id of the pending program
     uint64_t arena_base_units = 0;     // offset of this context's range in the device arena
     bool oom = false;                  // arena exhausted (codecs go to Disabled)
+    // Level pipelining (the session): a program's levels above kPipeDepth run in the launches of
+    // the NEXT program's first levels (Device::set_pipelined), so a row it writes at level
+    // d > kPipeDepth is still being written while the next program's levels 1 .. d-kPipeDepth
+    // run: in the next program such a row keeps level d - kPipeDepth ("inherited"), and its
+    // readers land above it.
+    static const uint32_t kPipeDepth = 2;
+    bool pipeline = false;
+    std::vector<RowId> inherited;      // rows with an inherited level in the pending program
 
     RowId alloc(uint32_t bytes) {
         const RowId r = rows.alloc(bytes);
@@ -387,7 +403,17 @@ struct Context {
         for (FlushClient* c : track_dirty ? dirty : clients) c->pre_flush();
     }
     void finish_flush() {
-        for (RowId r : pb.written_rows()) rows.set_level(r, 0);
+        for (RowId r : inherited) rows.set_level(r, 0);
+        inherited.clear();
+        for (RowId r : pb.written_rows()) {
+            const uint32_t l = rows.level(r);
+            if (pipeline && l > kPipeDepth) {
+                rows.set_level(r, l - kPipeDepth);
+                inherited.push_back(r);
+            } else {
+                rows.set_level(r, 0);
+            }
+        }
         for (RowId r : temps) rows.free_deferred(r);
         temps.clear();
         ex.clear();

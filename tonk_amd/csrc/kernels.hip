@@ -376,9 +376,14 @@ __device__ __forceinline__ LV<NH> run_item(const tamd_instr* __restrict__ instrs
 // Ops of one level never read a row written by an op of the same level, so every load of a
 // batch can be issued before the batch's stores.  Persistent grid: each workgroup stages the
 // tables in LDS once and then claims items.  A slice is 64 lanes x 8*NH bytes.
+// Two item segments: [0, n_items) of program 1 (ops, instrs, items) and [n_items, n_items +
+// n_items2) of program 2 (ops2, instrs2, items2) -- a pipelined launch runs a level of the
+// previous program beside a level of the next one (Device::launch); n_items2 = 0 otherwise.
 template <int NH, uint32_t B>
 __device__ __forceinline__ void exec_level(const tamd_op* __restrict__ ops, const tamd_instr* __restrict__ instrs,
                                            const uint2* __restrict__ items, uint32_t n_items, uint32_t n_shared,
+                                           const tamd_op* __restrict__ ops2, const tamd_instr* __restrict__ instrs2,
+                                           const uint2* __restrict__ items2, uint32_t n_items2,
                                            uint8_t* __restrict__ arena, const uint32_t* __restrict__ gf_perm,
                                            const uint8_t* __restrict__ zrow, unsigned long long* __restrict__ stamps) {
     constexpr uint32_t SLICE = 64u * 8u * NH;
@@ -436,21 +441,24 @@ __device__ __forceinline__ void exec_level(const tamd_op* __restrict__ ops, cons
     // them (a stratified sample of the level: ordered by cost class, most expensive first); its
     // waves claim them one at a time through an LDS counter, so a wave that drew a long op does
     // not hold up the others.
+    const uint32_t n_all = n_items + n_items2;
     for (;;) {
         uint32_t k = 0;
         if (lane == 0) k = atomicAdd(&claim, 1u);
         const uint32_t it = n_shared + blockIdx.x + uniform(__shfl(k, 0)) * gridDim.x;
-        if (it >= n_items) break;
-        const uint2 item = items[it];
-        const tamd_op op = ops[uniform(item.x)];
+        if (it >= n_all) break;
+        const bool second = it >= n_items;
+        const tamd_instr* __restrict__ ins = second ? instrs2 : instrs;
+        const uint2 item = second ? items2[it - n_items] : items[it];
+        const tamd_op op = second ? ops2[uniform(item.x)] : ops[uniform(item.x)];
         const uint32_t s0 = uniform(item.y) * SLICE;
         const uint32_t o = s0 + laneb;
         const uint32_t first = uniform(op.first), end = uniform(op.first + op.count);
         const u64 t0 = stamps ? __builtin_amdgcn_s_memrealtime() : 0;
         if (s0 + SLICE <= uniform(op.full))
-            run_item<true, NH, B>(instrs, first, end, o, laneb, arena, zrow, lds_perm, 1u, 0u);
+            run_item<true, NH, B>(ins, first, end, o, laneb, arena, zrow, lds_perm, 1u, 0u);
         else
-            run_item<false, NH, B>(instrs, first, end, o, laneb, arena, zrow, lds_perm, 1u, 0u);
+            run_item<false, NH, B>(ins, first, end, o, laneb, arena, zrow, lds_perm, 1u, 0u);
         if (stamps && lane == 0) {  // profiling only (TONK_AMD_STAMPS): vector stores of 100 MHz stamps
             __atomic_signal_fence(__ATOMIC_SEQ_CST);
             const u64 t1 = __builtin_amdgcn_s_memrealtime();
@@ -468,10 +476,13 @@ __device__ __forceinline__ void exec_level(const tamd_op* __restrict__ ops, cons
 #define TAMD_EXEC_KERNEL(name, NH, B)                                                                  \
     extern "C" __global__ void __launch_bounds__(256)                                                   \
     name(const tamd_op* __restrict__ ops, const tamd_instr* __restrict__ instrs,                       \
-         const uint2* __restrict__ items, uint32_t n_items, uint32_t n_shared, uint8_t* __restrict__ arena, \
+         const uint2* __restrict__ items, uint32_t n_items, uint32_t n_shared,                         \
+         const tamd_op* __restrict__ ops2, const tamd_instr* __restrict__ instrs2,                     \
+         const uint2* __restrict__ items2, uint32_t n_items2, uint8_t* __restrict__ arena,             \
          const uint32_t* __restrict__ gf_perm, const uint8_t* __restrict__ zrow,                       \
          unsigned long long* __restrict__ stamps) {                                                    \
-        exec_level<NH, B>(ops, instrs, items, n_items, n_shared, arena, gf_perm, zrow, stamps);       \
+        exec_level<NH, B>(ops, instrs, items, n_items, n_shared, ops2, instrs2, items2, n_items2, arena, gf_perm, \
+                          zrow, stamps);                                                               \
     }
 TAMD_EXEC_KERNEL(tamd_exec16, 2, 6)
 

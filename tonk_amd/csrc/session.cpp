@@ -86,8 +86,9 @@ struct Stream;
 struct SessTranscript {
     bool on = false;
     std::vector<std::string> lines;
-    struct PendEnc { RowId row; uint32_t total; RecoveryMeta meta; size_t pos; };
-    struct PendDec { RowId row; uint32_t upper; size_t pos; };
+    // rows whose digest goes into line `pos` once their program (epoch) has completed
+    struct PendEnc { RowId row; uint32_t total; RecoveryMeta meta; size_t pos; uint64_t epoch; };
+    struct PendDec { RowId row; uint32_t upper; size_t pos; uint64_t epoch; };
     std::vector<PendEnc> pend_enc;
     std::vector<PendDec> pend_dec;
 };
@@ -173,7 +174,7 @@ struct Stream {
                 nums.push_back(rp->packet_num);
                 alg_bytes += rp->framed_upper;
                 if (stage) out_rows.push_back(std::make_pair(rp->row, rp->framed_upper));
-                if (tr.on) tr.pend_dec.push_back(SessTranscript::PendDec{rp->row, rp->framed_upper, tr.lines.size()});
+                if (tr.on) tr.pend_dec.push_back(SessTranscript::PendDec{rp->row, rp->framed_upper, tr.lines.size(), ctx->epoch});
             }
         }
         return rc;
@@ -200,7 +201,7 @@ struct Stream {
     void on_encode(int rc, const RecRef& r) {
         if (!tr.on) return;
         if (rc != 0) { tr.lines.push_back("E " + std::to_string(rc)); return; }
-        tr.pend_enc.push_back(SessTranscript::PendEnc{r.out.row, r.out.total(), r.out.meta, tr.lines.size()});
+        tr.pend_enc.push_back(SessTranscript::PendEnc{r.out.row, r.out.total(), r.out.meta, tr.lines.size(), ctx->epoch});
         tr.lines.push_back("E ?");
     }
     void on_decode(int rc, const std::vector<uint32_t>& nums, const DecRef&) {
@@ -250,7 +251,7 @@ struct Session {
     std::vector<std::unique_ptr<Context>> ctxs;     // ctxs[i] belongs to streams[i]
     std::vector<double> busy_ms;                    // per thread, control-plane time of a step
     std::vector<std::pair<uint64_t, uint64_t>> epoch_ticket;  // (epoch, ticket) awaiting release
-    uint64_t last_ticket = 0, released_epoch = 0;
+    uint64_t last_ticket = 0, released_epoch = 0, prev_ticket = 0;
     double host_ms[6] = {0, 0, 0, 0, 0, 0};
     uint64_t clock_msec = 0;  // packet send times of a step (RTO bookkeeping only)
     uint32_t row_cap = 0;
@@ -375,7 +376,9 @@ struct Session {
         const auto t0 = clk::now();
         clock_msec = time_msec();
         if (host_in && !finish) stage_inputs(originals);
-        const uint64_t rel = completed_epoch();
+        uint64_t rel = completed_epoch();
+        // record mode: the previous program's rows wait for their digests (after this launch)
+        if (prm.record && !ctxs.empty() && ctxs[0]->epoch >= 2 && rel > ctxs[0]->epoch - 2) rel = ctxs[0]->epoch - 2;
         std::fill(busy_ms.begin(), busy_ms.end(), 0.0);
         if (order.size() != streams.size()) {
             order.resize(streams.size());
@@ -422,7 +425,14 @@ struct Session {
         host_ms[3] += ms(t2, t3);
         host_ms[4] += ms(t3, t4);
         epoch_ticket.push_back(std::make_pair(epoch, last_ticket));
-        if (prm.record) resolve_transcripts();
+        // Record mode: the digests of the PREVIOUS program's rows, once it has completed -- its
+        // upper levels ran in this launch (pipelined), which the transcripts thereby check; its
+        // rows are not released before the next step.
+        if (prm.record) {
+            if (prev_ticket) dev.wait(prev_ticket);
+            resolve_transcripts(epoch);
+            prev_ticket = last_ticket;
+        }
     }
 
     // H2D of the next `originals` input rows of every stream, both codec sides (each side's
@@ -484,23 +494,28 @@ struct Session {
         run_all([this, rel](size_t i, size_t) { ctxs[i]->rows.release_up_to(rel); });
     }
 
-    void resolve_transcripts() {
-        dev.synchronize();
+    // Digests of pending transcript rows of programs before `before_epoch` (all when 0); those
+    // programs have completed (dev.wait / synchronize by the caller).
+    void resolve_transcripts(uint64_t before_epoch = 0) {
         std::vector<uint8_t> buf;
         for (auto& sp : streams) {
             Stream& s = *sp;
             char line[256];
+            size_t keep = 0;
             for (auto& e : s.tr.pend_enc) {
+                if (before_epoch && e.epoch >= before_epoch) { s.tr.pend_enc[keep++] = e; continue; }
                 buf.resize(e.total);
-                dev.download(buf.data(), (uint64_t)s.ctx->rows.offset(e.row) * TAMD_ROW_UNIT, e.total);
+                dev.download_now(buf.data(), (uint64_t)s.ctx->rows.offset(e.row) * TAMD_ROW_UNIT, e.total);
                 snprintf(line, sizeof(line), "E 0 %u %u %u %u %u %016llx", e.total, e.meta.Row, e.meta.ColumnStart,
                          e.meta.SumCount, e.meta.LDPCCount, (unsigned long long)wl::fnv1a(buf.data(), e.total));
                 s.tr.lines[e.pos] = line;
             }
-            s.tr.pend_enc.clear();
+            s.tr.pend_enc.resize(keep);
+            keep = 0;
             for (auto& d : s.tr.pend_dec) {
+                if (before_epoch && d.epoch >= before_epoch) { s.tr.pend_dec[keep++] = d; continue; }
                 buf.resize(d.upper);
-                dev.download(buf.data(), (uint64_t)s.ctx->rows.offset(d.row) * TAMD_ROW_UNIT, d.upper);
+                dev.download_now(buf.data(), (uint64_t)s.ctx->rows.offset(d.row) * TAMD_ROW_UNIT, d.upper);
                 unsigned len = 0;
                 const int hb = get_length_header(buf.data(), d.upper, len);
                 std::string& ln = s.tr.lines[d.pos];
@@ -512,7 +527,7 @@ struct Session {
                 const size_t at = ln.find('#');
                 if (at != std::string::npos) ln.replace(at, 1, line);
             }
-            s.tr.pend_dec.clear();
+            s.tr.pend_dec.resize(keep);
         }
     }
 };
@@ -531,6 +546,10 @@ void* tamd_session_create(const tamd_session_params* p, char* err, size_t err_le
     std::unique_ptr<Session> s(new Session());
     s->prm = *p;
     if (!s->dev.init((int)p->device, p->arena_bytes)) return fail(s->dev.error());
+    // Level pipelining (Device::set_pipelined): off when packets are staged through the host
+    // (the D2H gather right after a program needs all of its levels) and for A/B runs.
+    const bool pipe = !p->stage_host && getenv("TONK_AMD_NO_PIPELINE") == nullptr;
+    s->dev.set_pipelined(pipe);
     if (!s->dev.gf_selftest()) return fail("device GF(256) self test failed");
 
     const uint32_t nthreads = p->n_threads ? (p->n_threads < p->n_streams ? p->n_threads : p->n_streams) : 1;
@@ -545,9 +564,10 @@ void* tamd_session_create(const tamd_session_params* p, char* err, size_t err_le
     // Streams are built on the pool threads (first touch of their state on the device's node).
     s->streams.resize(p->n_streams);
     s->ctxs.resize(p->n_streams);
-    s->run_all([raw, p, range](size_t i, size_t) {
+    s->run_all([raw, p, range, pipe](size_t i, size_t) {
         std::unique_ptr<Context> ctx(new Context());
         ctx->rows.init(range, (range / TAMD_ROW_UNIT) * i);
+        ctx->pipeline = pipe;
         std::unique_ptr<Stream> st(new Stream());
         st->ctx = ctx.get();
         wl::Params& q = st->p;
@@ -661,6 +681,7 @@ int tamd_session_wait(void* sp) {
     Session* s = (Session*)sp;
     s->dev.synchronize();
     s->dev.sync_staging();
+    if (s->prm.record) s->resolve_transcripts();
     s->release_all();
     return s->dev.error().empty() && s->error.empty() ? 0 : -1;
 }

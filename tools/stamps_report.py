@@ -38,3 +38,27 @@ for l in range(len(bases) - 1):
     bins = np.linspace(0, span, 11)
     act = [((s[:, 0] - t0) * 10 <= x).sum() - ((s[:, 1] - t0) * 10 <= x).sum() for x in bins[:-1] + span / 20]
     print('   items in flight per tenth:', act)
+
+# Busy time by op signature per level: (ACCR modes, ACC/ACC3/STOREC counts bucketed)
+print()
+for l in range(len(bases) - 1):
+    a, b = bases[l], bases[l + 1]
+    if a == b: continue
+    s = st[a:b].astype(np.int64)
+    dur = (s[:, 1] - s[:, 0]) * 10
+    shared = (s[:, 2] & 0xffffffff) == 4
+    groups = {}
+    for i in range(a, b):
+        op = ops[items[i, 0]]
+        ks = kinds[op[0]:op[0] + op[1]]
+        ii = instr[op[0]:op[0] + op[1]]
+        modes = ((ii[ks == 7, 0] >> 8) & 0xff)
+        sig = ('SH ' if shared[i - a] else '') + f"accr{sorted(set(modes.tolist()))} acc{int((ks == 1).sum()) // 8 * 8}+ acc3{int((ks == 5).sum())} storec{int((ks == 6).sum())}"
+        g = groups.setdefault(sig, [0, 0.0, 0.0])
+        g[0] += 1
+        g[1] += dur[i - a]
+        g[2] = max(g[2], dur[i - a])
+    tot = sum(g[1] for g in groups.values())
+    print(f'level {l}: busy by signature (items, share of busy, mean us, max us)')
+    for sig, g in sorted(groups.items(), key=lambda kv: -kv[1][1])[:8]:
+        print(f'   {sig:55s} {g[0]:6d} {100 * g[1] / tot:5.1f}% {g[1] / g[0] / 1e3:6.2f} {g[2] / 1e3:6.2f}')
