@@ -69,6 +69,8 @@ void  tamd_session_host_ms(void* s, double out[10]);
 /* Transcript of one stream in the oracle's text format (record mode). Returns bytes needed. */
 size_t tamd_session_transcript(void* s, uint32_t stream, char* buf, size_t cap);
 void  tamd_session_destroy(void* s);
+/* The session's last error ("" when none). */
+const char* tamd_session_error(void* s);
 
 /* Test hook: the codecs' millisecond clock (GetTimeMsec: send times, RTO, retransmit) is read
    from `fn` instead of the monotonic clock (null restores it).  Used to compare

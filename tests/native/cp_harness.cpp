@@ -25,11 +25,14 @@ static uint64_t g_arena_bytes = 512ull << 20;
 // as the siamese.h C ABI runs it); every backend call touches its codec like capi.cpp does.
 static bool g_dirty = false;
 static bool g_nobatch = false;  // nobatch=1: the runner's single-add path only
-// pipeline=1: levels above Context::kPipeDepth would run beside the next program's first levels
-// (the session's pipelined launches); every such pair of levels is checked for hazards (no op
-// of one reads or writes a row the other writes) before the programs run one after the other.
+// pipeline=1: the session's pipelined launches (Device::launch_step: level 1 of a program beside
+// the next level of every older program in flight) are simulated and every launch is checked for
+// hazards (no segment reads or writes a row another writes) before the programs run in order.
 static bool g_pipeline = false;
+static uint32_t g_drain = 0;  // pipelined: complete every in-flight program after every g_drain-th (session record mode: 2)
+#include <map>
 #include <set>
+#include <unordered_map>
 
 struct Harness {
     Params p;
@@ -43,9 +46,8 @@ struct Harness {
     TextSink out;
     uint64_t programs = 0, ops = 0, levels = 0, instrs = 0;
     std::string error;
-    // rows read / written per level of the previous program, for its levels above kPipeDepth
+    // rows read / written per level of a program (pipelined launch checks)
     struct LevelRW { std::set<uint32_t> rd, wr; };
-    std::vector<LevelRW> tail;
     uint64_t pipelined_pairs = 0;
 
     std::vector<LevelRW> level_rw() const {
@@ -65,27 +67,87 @@ struct Harness {
         }
         return out;
     }
-    static bool meets(const std::set<uint32_t>& a, const std::set<uint32_t>& b) {
-        for (uint32_t x : a)
-            if (b.count(x)) return true;
-        return false;
-    }
-    // Level j of this program runs beside level j + kPipeDepth of the previous one.
+    // Every launch runs level 1 of this program beside the next level of each older program
+    // still in flight (Device::launch_step).  Each level's dependencies in program order (the
+    // last writer of every row it reads or writes, and the readers since, of any program) must
+    // have run in an EARLIER launch: same-launch and out-of-order hazards alike, including rows
+    // reused after release.
+    typedef std::pair<uint64_t, uint32_t> Lv;  // (program epoch, level)
+    struct RowHist { Lv w{0, 0}; std::vector<Lv> rd; };
+    std::unordered_map<uint32_t, RowHist> hist;
+    std::map<Lv, uint64_t> launched_at;
+    uint64_t launch_no = 0;
+    struct Prog { std::vector<LevelRW> levels; std::vector<std::vector<Lv>> deps; uint32_t next = 1; uint64_t epoch = 0; };
+    std::vector<Prog> inflight;
+    uint64_t launched = 0;
     void check_pipeline() {
-        std::vector<LevelRW> cur = level_rw();
-        const uint32_t D = Context::kPipeDepth;
-        for (uint32_t j = 1; j < cur.size() && j <= D; ++j) {
-            const uint32_t pl = j + D;
-            if (pl >= tail.size()) continue;
-            const LevelRW& a = cur[j];
-            const LevelRW& b = tail[pl];
-            const char* what = meets(a.rd, b.wr) ? "reads a row the previous program writes"
-                               : meets(a.wr, b.wr) ? "writes a row the previous program writes"
-                               : meets(a.wr, b.rd) ? "writes a row the previous program reads" : nullptr;
-            if (what && error.empty()) error = "pipelined level " + std::to_string(j) + " " + what;
-            ++pipelined_pairs;
+        Prog cur;
+        cur.levels = level_rw();
+        cur.epoch = ctx.epoch;
+        cur.deps.resize(cur.levels.size());
+        for (uint32_t d = 1; d < cur.levels.size(); ++d) {
+            const Lv me(cur.epoch, d);
+            std::set<Lv> dd;
+            for (uint32_t x : cur.levels[d].rd) {
+                const RowHist& h = hist[x];
+                if (h.w.first) dd.insert(h.w);
+            }
+            for (uint32_t x : cur.levels[d].wr) {
+                const RowHist& h = hist[x];
+                if (h.w.first) dd.insert(h.w);
+                dd.insert(h.rd.begin(), h.rd.end());
+            }
+            dd.erase(me);
+            cur.deps[d].assign(dd.begin(), dd.end());
+            for (uint32_t x : cur.levels[d].rd) hist[x].rd.push_back(me);
+            for (uint32_t x : cur.levels[d].wr) {
+                RowHist& h = hist[x];
+                h.w = me;
+                h.rd.clear();
+            }
         }
-        tail.swap(cur);
+        inflight.push_back(std::move(cur));
+        pipeline_step();
+        // Device::wait / synchronize: the remaining levels launch without a new program
+        if (g_drain && ++launched % g_drain == 0)
+            while (!inflight.empty()) pipeline_step();
+    }
+    void pipeline_step() {
+        std::vector<Prog*> run;
+        for (Prog& p : inflight)
+            if (p.next < p.levels.size()) run.push_back(&p);
+        for (Prog* p : run)
+            for (const Lv& dep : p->deps[p->next]) {
+                const auto it = launched_at.find(dep);
+                if ((it == launched_at.end() || it->second >= launch_no) && error.empty())
+                    error = "pipelined launch " + std::to_string(launch_no) + ": level " + std::to_string(p->next) +
+                            " of program " + std::to_string(p->epoch) + " runs before or with level " +
+                            std::to_string(dep.second) + " of program " + std::to_string(dep.first) +
+                            " it depends on";
+            }
+        static const bool trace = getenv("CP_TRACE") != nullptr;
+        if (trace) {
+            fprintf(stderr, "launch %llu:", (unsigned long long)launch_no);
+            for (Prog* p : run) fprintf(stderr, " (%llu,%u)", (unsigned long long)p->epoch, p->next);
+            fprintf(stderr, "\n");
+        }
+        for (Prog* p : run) launched_at[Lv(p->epoch, p->next++)] = launch_no;
+        ++launch_no;
+        if (run.size() > 1) ++pipelined_pairs;
+        size_t keep = 0;
+        for (size_t k = 0; k < inflight.size(); ++k)
+            if (inflight[k].next < inflight[k].levels.size()) {
+                if (k != keep) inflight[keep] = std::move(inflight[k]);  // (no self-move: it empties a vector)
+                ++keep;
+            }
+        inflight.resize(keep);
+    }
+    // Highest epoch whose programs have all run every level (in the simulated launch order).
+    uint64_t release_bound(uint64_t done) const {
+        uint64_t b = done;
+        for (const Prog& p : inflight)
+            if (p.epoch <= b) b = p.epoch - 1;
+        return b;
     }
 
     // transcript entries waiting for their rows to be computed
@@ -164,9 +226,9 @@ struct Harness {
         resolve();
         const uint64_t done = ctx.epoch;
         ctx.finish_flush();
-        // pipelined, a program completes only with the next one's first levels: rows it freed are
-        // reusable one program later (the session releases by device completion events)
-        ctx.rows.release_up_to(g_pipeline ? done - 1 : done);
+        // pipelined, a program completes only with later programs' launches: rows it freed are
+        // reusable once its last level has run (the session releases by device completion events)
+        ctx.rows.release_up_to(g_pipeline ? release_bound(done) : done);
     }
 
     void resolve() {
@@ -355,6 +417,7 @@ int main(int argc, char** argv) {
         else if (k == "dirty") g_dirty = v != 0;
         else if (k == "nobatch") g_nobatch = v != 0;
         else if (k == "pipeline") g_pipeline = v != 0;
+        else if (k == "drain") g_drain = (uint32_t)v;
         else if (parse_param(p, k, v)) {}
         else { fprintf(stderr, "bad key %s\n", k.c_str()); return 2; }
     }

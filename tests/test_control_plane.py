@@ -26,7 +26,7 @@ SCENARIOS = ["c1_256_p3", "c2_4096_p1_ack64", "c2_4096_p1_noack", "c3_4096_p2_ac
              "var_1_1500_p2_ack32", "tiny_1_20_p5_ack16", "big_9000_p3_ack64", "hiloss_p20_arq",
              "norecloss_p5_arq", "single_p0", "burst8_p5", "rtx_p2_ack64", "rtx_p5_ack32", "rtx_p3_noack"]
 MODES = [("sync", 0), ("batch", 1000), ("batch", 4096), ("sync-dirty", 0), ("batch-dirty", 1000),
-         ("batch-pipe", 1000), ("batch-pipe", 4096)]
+         ("batch-pipe", 1000), ("batch-pipe", 4096), ("batch-pipedrain", 1000)]
 
 
 @pytest.fixture(scope="module")
@@ -43,9 +43,12 @@ def test_control_plane_matches_reference(harness, golden_index, tmp_path, name, 
     out = tmp_path / "t.txt"
     # "-dirty": flushes visit only the codecs touched since the last one (the C ABI's context);
     # "-pipe": levels pipelined across programs as the session launches them, every pair of
-    # levels that would run together checked for hazards
-    base, dirty, pipe = mode.split("-")[0], int(mode.endswith("-dirty")), int(mode.endswith("-pipe"))
-    args = [harness, str(out), f"mode={base}", f"batch={batch}", f"dirty={dirty}", f"pipeline={pipe}"] + sc["args"] + [
+    # levels that would run together checked for hazards; "-pipedrain": every second program
+    # also completes all in-flight ones (the session's record mode), so rows are reused sooner
+    base, dirty = mode.split("-")[0], int(mode.endswith("-dirty"))
+    pipe, drain = int("-pipe" in mode), 2 * int(mode.endswith("-pipedrain"))
+    args = [harness, str(out), f"mode={base}", f"batch={batch}", f"dirty={dirty}", f"pipeline={pipe}",
+            f"drain={drain}"] + sc["args"] + [
         f"seed_data={1000 + sid}", f"seed_loss={2000 + sid}"]
     r = subprocess.run(args, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
@@ -59,11 +62,12 @@ def test_control_plane_matches_reference(harness, golden_index, tmp_path, name, 
                                              ("cfg3_rank7_64x12288_p1_ack64", 511)])
 def test_control_plane_batch_streams(harness, golden_index, tmp_path, batch_name, sid):
     """Streams of the multi-stream fixtures (BASELINE configs[2], the rank-7 shard of configs[3])
-    through the control plane in the bench's batch mode: transcript digest == reference's."""
+    through the control plane in the bench's batch mode, pipelined as the session launches it in
+    record mode: transcript digest == reference's, no launch-order hazard."""
     import hashlib
     entry = golden_index["batches"][batch_name]
     out = tmp_path / "t.txt"
-    args = [harness, str(out), "mode=batch", "batch=4096", "dirty=0"] + entry["args"] + [
+    args = [harness, str(out), "mode=batch", "batch=4096", "dirty=0", "pipeline=1", "drain=2"] + entry["args"] + [
         f"seed_data={1000 + sid}", f"seed_loss={2000 + sid}"]
     r = subprocess.run(args, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]

@@ -54,6 +54,8 @@ def lib() -> ctypes.CDLL:
         L.tamd_session_host_ms.argtypes = [vp, ctypes.POINTER(ctypes.c_double)]
         L.tamd_session_transcript.restype = sz
         L.tamd_session_transcript.argtypes = [vp, u32, ctypes.c_char_p, sz]
+        L.tamd_session_error.restype = ctypes.c_char_p
+        L.tamd_session_error.argtypes = [vp]
         L.tamd_session_destroy.restype = None
         L.tamd_session_destroy.argtypes = [vp]
         L.tamd_device_selftest.restype = ctypes.c_int
@@ -164,7 +166,8 @@ class Session:
 
     def _check(self, rc: int, what: str) -> None:
         if rc != 0:
-            raise RuntimeError(f"tonk_amd: {what} failed (rc={rc}); summary={self.summary()}")
+            err = lib().tamd_session_error(self._h).decode()
+            raise RuntimeError(f"tonk_amd: {what} failed (rc={rc}): {err}; summary={self.summary()}")
 
     def generate(self) -> None:
         self._check(lib().tamd_session_generate(self._h), "input generation")

@@ -7,11 +7,9 @@
 #include <stdlib.h>
 #include <string.h>
 
-extern "C" __global__ void tamd_exec16(const tamd_op*, const tamd_instr*, const uint2*, uint32_t, uint32_t,
-                                       const tamd_op*, const tamd_instr*, const uint2*, uint32_t, uint8_t*,
-                                       const uint32_t*, const uint8_t*, unsigned long long*);
-typedef void (*ExecFn)(const tamd_op*, const tamd_instr*, const uint2*, uint32_t, uint32_t, const tamd_op*,
-                       const tamd_instr*, const uint2*, uint32_t, uint8_t*, const uint32_t*, const uint8_t*,
+extern "C" __global__ void tamd_exec16(tamd_segments, const uint8_t*, uint32_t, uint8_t*, const uint32_t*,
+                                       const uint8_t*, unsigned long long*);
+typedef void (*ExecFn)(tamd_segments, const uint8_t*, uint32_t, uint8_t*, const uint32_t*, const uint8_t*,
                        unsigned long long*);
 extern "C" __global__ void tamd_gf_selftest(const uint32_t*, uint8_t*);
 extern "C" __global__ void tamd_gather_rows(const tamd::Device::GatherDesc*, uint32_t, const uint8_t*, uint8_t*);
@@ -42,9 +40,9 @@ Device::~Device() {
     hipStreamSynchronize((hipStream_t)stream_);
     for (Slot& s : slots_) {
         if (s.host) hipHostFree(s.host);
-        if (s.dev) hipFree(s.dev);
         if (s.done) hipEventDestroy((hipEvent_t)s.done);
     }
+    if (prog_dev_) hipFree(prog_dev_);
     for (auto& p : inflight_) hipEventDestroy((hipEvent_t)p.second);
     for (void* e : free_events_) hipEventDestroy((hipEvent_t)e);
     for (auto& p : timing_events_) { hipEventDestroy((hipEvent_t)p.first); hipEventDestroy((hipEvent_t)p.second); }
@@ -140,8 +138,8 @@ bool Device::init(int device, uint64_t arena_bytes) {
     rb_cap_ = 2u << 20;
     HIPCHK(hipHostMalloc((void**)&rb_host_, rb_cap_, hipHostMallocDefault));
     // Staging slots up front, each touched by one copy, so no step pays first-use costs.
+    if (!alloc_slots(slot_bytes_)) { error_ = "program staging allocation failed"; return false; }
     for (Slot& sl : slots_) {
-        if (!ensure_slot(sl, slot_bytes_)) { error_ = "program staging allocation failed"; return false; }
         memset(sl.host, 0, 4096);
         HIPCHK(hipMemcpyAsync(sl.dev, sl.host, 4096, hipMemcpyHostToDevice, s));
     }
@@ -227,20 +225,39 @@ bool Device::grow_arena(uint64_t min_bytes) {
     return true;
 }
 
-bool Device::ensure_slot(Slot& s, size_t bytes) {
-    if (s.cap >= bytes) return true;
-    stats_.slot_reallocs++;
-    if (s.host) hipHostFree(s.host);
-    if (s.dev) hipFree(s.dev);
-    size_t cap = slot_bytes_;  // a bench step's program is ~8 MB: avoid reallocating mid-run
-    while (cap < bytes) cap *= 2;
-    s.host = nullptr;
-    s.dev = nullptr;
-    s.cap = 0;
-    if (hipHostMalloc((void**)&s.host, cap, hipHostMallocDefault) != hipSuccess) return false;
-    if (hipMalloc((void**)&s.dev, cap) != hipSuccess) return false;
-    s.cap = cap;
+bool Device::alloc_slots(size_t cap) {
+    cap = (cap + 255) & ~(size_t)255;
+    if (cap * slots_.size() > 0xfffff000ull) return false;  // 32-bit program offsets
+    for (Slot& s : slots_) {
+        if (s.host) hipHostFree(s.host);
+        s.host = nullptr;
+        s.dev = nullptr;
+    }
+    if (prog_dev_) hipFree(prog_dev_);
+    prog_dev_ = nullptr;
+    slot_cap_ = 0;
+    if (hipMalloc((void**)&prog_dev_, cap * slots_.size()) != hipSuccess) return false;
+    for (size_t k = 0; k < slots_.size(); ++k) {
+        Slot& s = slots_[k];
+        if (hipHostMalloc((void**)&s.host, cap, hipHostMallocDefault) != hipSuccess) return false;
+        s.dev_off = (uint32_t)(k * cap);
+        s.dev = prog_dev_ + s.dev_off;
+    }
+    slot_cap_ = cap;
     return true;
+}
+
+bool Device::ensure_slot(Slot& s, size_t bytes) {
+    (void)s;
+    if (slot_cap_ >= bytes) return true;
+    stats_.slot_reallocs++;
+    // a bench step's program is ~8 MB: avoid reallocating mid-run
+    size_t cap = slot_cap_ ? slot_cap_ : slot_bytes_;
+    while (cap < bytes) cap *= 2;
+    drain_programs();
+    HIPCHK(hipStreamSynchronize((hipStream_t)stream_));
+    for (Slot& sl : slots_) sl.ticket = 0;
+    return alloc_slots(cap);
 }
 
 uint64_t Device::run(Context* const* ctxs, size_t n) {
@@ -304,7 +321,8 @@ void Device::begin(Context* const* ctxs, size_t n) {
 
     Slot& slot = slots_[next_slot_];
     next_slot_ = (next_slot_ + 1) % (int)slots_.size();
-    if (tail_.active && tail_.slot == &slot) finish_tail(Context::kPipeDepth + 1);  // (slot still holds it)
+    for (const Inflight& p : progs_)
+        if (p.slot == &slot) { drain_programs(); break; }  // (the slot still holds a program in flight)
     if (slot.ticket) {
         const auto w0 = std::chrono::steady_clock::now();
         HIPCHK(hipEventSynchronize((hipEvent_t)slot.done));
@@ -367,10 +385,27 @@ void Device::fill(size_t c) {
     }
 }
 
-// One executor launch over up to two item segments (a: the previous program's deferred level,
-// b: a level of the program being launched; either may be empty).
-void Device::launch_level(const LevelSeg& a, const LevelSeg& b, unsigned long long* stamps) {
-    const uint32_t cnt = a.count + b.count;
+// One executor launch: the next level of every program with levels left (oldest first), then
+// level 1 of `fresh` (the program being launched) if given.
+void Device::launch_step(Inflight* fresh, unsigned long long* stamps) {
+    tamd_segments sg;
+    memset(&sg, 0, sizeof(sg));
+    uint32_t cnt = 0, coop = 0;
+    auto add = [&](Inflight& p) {
+        if (p.done()) return;
+        const uint32_t l = p.next++;
+        const uint32_t c = p.level_items[l];
+        if (!c) return;
+        tamd_segment& g = sg.s[sg.n++];
+        g.ops = p.ops;
+        g.instrs = p.instrs;
+        g.items = p.items + 8u * p.item_base[l];
+        g.count = c;
+        if (sg.n == 1) coop = p.level_coop[l];
+        cnt += c;
+    };
+    for (Inflight& p : progs_) add(p);
+    if (fresh) add(*fresh);
     if (!cnt) return;
     hipStream_t st = (hipStream_t)stream_;
     uint32_t grid = (cnt + 3) / 4;
@@ -381,16 +416,14 @@ void Device::launch_level(const LevelSeg& a, const LevelSeg& b, unsigned long lo
         e1 = (hipEvent_t)timing_event();
         hipEventRecord(e0, st);
     }
-    // Class-0 ops are shared by a workgroup only in levels too small to fill the chip twice
-    // over with single-wave items; in the big levels they run as ordinary (first) items.  Only
-    // the first segment's class-0 items (they lead it) can be shared.
+    // Class-0 ops are shared by a workgroup only in launches too small to fill the chip twice
+    // over with single-wave items; in the big ones they run as ordinary (first) items.  Only the
+    // first segment's class-0 items (they lead it) can be shared.
     static const int share_mode = getenv("TONK_AMD_SHARE") ? atoi(getenv("TONK_AMD_SHARE")) : 0;  // A/B (profiling)
-    const LevelSeg& f = a.count ? a : b;
-    const LevelSeg& g = a.count ? b : a;
-    const uint32_t shared = (share_mode == 1 || (share_mode == 0 && cnt < 2u * 4u * max_grid_)) ? f.coop : 0u;
+    const uint32_t shared = (share_mode == 1 || (share_mode == 0 && cnt < 2u * 4u * max_grid_)) ? coop : 0u;
     const ExecFn fn = (ExecFn)exec_kernel_;
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, st, f.ops, f.instrs, (const uint2*)f.items, f.count, shared, g.ops,
-                       g.instrs, (const uint2*)g.items, g.count, arena_, d_gf_, d_zero_, stamps);
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, st, sg, (const uint8_t*)prog_dev_, shared, arena_, d_gf_, d_zero_,
+                       stamps);
     if (timing_) {
         hipEventRecord(e1, st);
         timing_events_.push_back(std::make_pair((void*)e0, (void*)e1));
@@ -398,26 +431,31 @@ void Device::launch_level(const LevelSeg& a, const LevelSeg& b, unsigned long lo
     stats_.launches++;
 }
 
-// The deferred levels of the previous program that did not run beside this one's, then its
-// completion (slot event, ticket).
-void Device::finish_tail(uint32_t from_level) {
-    if (!tail_.active) return;
-    LevelSeg none;
-    for (uint32_t l = from_level; l < tail_.levels; ++l) launch_level(tail_.level(l), none, nullptr);
+// Complete the oldest programs whose levels have all been launched (in ticket order).
+void Device::retire_done() {
+    while (!progs_.empty() && progs_.front().done()) {
+        Inflight& p = progs_.front();
+        HIPCHK(hipEventRecord((hipEvent_t)p.slot->done, (hipStream_t)stream_));
+        p.slot->ticket = p.ticket;
+        mark(p.ticket);
+        progs_.pop_front();
+    }
+}
+
+void Device::drain_programs() {
+    while (!progs_.empty()) {
+        launch_step(nullptr, nullptr);
+        retire_done();
+    }
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord((hipEvent_t)tail_.slot->done, (hipStream_t)stream_));
-    tail_.slot->ticket = tail_.ticket;
-    mark(tail_.ticket);
-    tail_.active = false;
 }
 
 uint64_t Device::launch() {
     flush_uploads();  // staged packets land before the program reads them
     Plan& P = plan_;
     const uint64_t ticket = ++ticket_;
-    const uint32_t D = Context::kPipeDepth;
     if (P.empty) {
-        finish_tail(D + 1);
+        drain_programs();
         ticket_is_empty_ = true;
         mark(ticket);  // done once everything enqueued before it is done
         ticket_is_empty_ = false;
@@ -433,10 +471,10 @@ uint64_t Device::launch() {
         fprintf(stderr, "tonk_amd: program %llu: H2D enqueue of %zu bytes took %.3f ms\n",
                 (unsigned long long)ticket, P.total, up_ms);
     if (up_ms > stats_.upload_enqueue_max_ms) stats_.upload_enqueue_max_ms = up_ms;
-    Tail cur;
-    cur.instrs = (const tamd_instr*)slot.dev;
-    cur.ops = (const tamd_op*)(slot.dev + P.bytes_instr);
-    cur.items = (const void*)(slot.dev + P.bytes_instr + P.bytes_ops);
+    Inflight cur;
+    cur.instrs = slot.dev_off;
+    cur.ops = slot.dev_off + (uint32_t)P.bytes_instr;
+    cur.items = slot.dev_off + (uint32_t)(P.bytes_instr + P.bytes_ops);
     cur.levels = P.levels;
     cur.level_items = P.level_items;
     cur.item_base = P.item_base;
@@ -445,26 +483,36 @@ uint64_t Device::launch() {
     cur.ticket = ticket;
     // Profiling only: TONK_AMD_STAMPS=<program number> records per-item start/end stamps of that
     // program's launches and writes them to tonk_amd_stamps.bin (u64 triples per item; levels
-    // delimited by the item bases printed to stderr).  Stamped programs are not pipelined.
+    // delimited by the item bases printed to stderr).  A stamped program runs alone.
     unsigned long long* stamps = nullptr;
     static const char* stamp_env = getenv("TONK_AMD_STAMPS");
     const bool stamp_this = stamp_env && (uint64_t)atoll(stamp_env) == stats_.programs;
-    if (stamp_this) {
-        finish_tail(D + 1);
-        HIPCHK(hipMalloc((void**)&stamps, P.n_items * 24 + 24));
+    const bool pipe = pipelined_ && !stamp_this;
+    if (!pipe) drain_programs();
+    if (stamp_this) HIPCHK(hipMalloc((void**)&stamps, P.n_items * 24 + 24));
+    // a launch holds at most TAMD_MAX_SEGMENTS levels: the oldest programs finish first if needed
+    while (progs_.size() + 1 > TAMD_MAX_SEGMENTS) {
+        launch_step(nullptr, nullptr);
+        retire_done();
     }
-    // Pipelined: level j of this program runs beside level j + D of the previous one; this
-    // program's levels above D wait for the next launch() (Context::kPipeDepth, inherited levels).
-    const bool defer = pipelined_ && !stamp_this && P.levels > D + 1;
-    const uint32_t own = defer ? D + 1 : P.levels;  // this program's levels launched now: [1, own)
-    LevelSeg none;
-    uint32_t l = 1;
-    for (; l < own || (tail_.active && l + D < tail_.levels && l <= D); ++l) {
-        const LevelSeg a = tail_.active && l <= D ? tail_.level(l + D) : none;
-        const LevelSeg b = l < own ? cur.level(l) : none;
-        launch_level(a, b, stamps ? stamps + 3 * P.item_base[l] : nullptr);
+    if (pipe) {
+        // Pipelined: this program's level 1 beside the next level of every program in flight;
+        // its level d runs d - 1 launches later (Context::kPipeDepth, inherited levels).
+        launch_step(&cur, nullptr);
+        progs_.push_back(cur);
+        retire_done();
+    } else {
+        for (uint32_t l = 1; l < P.levels; ++l) {
+            progs_.push_back(cur);  // (a single-program launch per level)
+            progs_.back().next = l;
+            progs_.back().levels = l + 1;
+            launch_step(nullptr, stamps ? stamps + 3 * P.item_base[l] : nullptr);
+            progs_.pop_back();
+        }
+        HIPCHK(hipEventRecord((hipEvent_t)slot.done, st));
+        slot.ticket = ticket;
+        mark(ticket);
     }
-    finish_tail(2 * D + 1);  // (the previous program's levels beyond 2D, then its completion)
     HIPCHK(hipGetLastError());
     if (stamp_this) {
         std::vector<unsigned long long> h(P.n_items * 3);
@@ -483,14 +531,6 @@ uint64_t Device::launch() {
         }
         fprintf(stderr, "stamps: n_instr_bytes %zu n_ops_bytes %zu n_items %zu\n", P.bytes_instr, P.bytes_ops, P.n_items);
         for (uint32_t k = 0; k <= P.levels; ++k) fprintf(stderr, "stamps level %u item_base %u\n", k, P.item_base[k]);
-    }
-    if (defer) {
-        cur.active = true;
-        tail_ = cur;
-    } else {
-        HIPCHK(hipEventRecord((hipEvent_t)slot.done, st));
-        slot.ticket = ticket;
-        mark(ticket);
     }
     stats_.programs++;
     stats_.ops += P.n_ops;
@@ -529,7 +569,7 @@ bool Device::completed(uint64_t ticket) {
 }
 
 void Device::wait(uint64_t ticket) {
-    if (tail_.active && ticket >= tail_.ticket) finish_tail(Context::kPipeDepth + 1);
+    if (!progs_.empty() && ticket >= progs_.front().ticket) drain_programs();
     while (!inflight_.empty() && ticket > completed_) {
         HIPCHK(hipEventSynchronize((hipEvent_t)inflight_.front().second));
         if (inflight_.front().first > completed_) completed_ = inflight_.front().first;
@@ -539,7 +579,7 @@ void Device::wait(uint64_t ticket) {
 }
 
 void Device::synchronize() {
-    finish_tail(Context::kPipeDepth + 1);
+    drain_programs();
     flush_uploads();
     HIPCHK(hipStreamSynchronize((hipStream_t)stream_));
     for (auto& p : inflight_) free_events_.push_back(p.second);

@@ -60,6 +60,7 @@ public:
     // Level pipelining across programs (the session; Context::kPipeDepth): a program's levels
     // above the depth are launched beside the next program's first levels.
     void set_pipelined(bool on) { pipelined_ = on; }
+    bool pending_levels() const { return !progs_.empty(); }
     bool completed(uint64_t ticket);
     void wait(uint64_t ticket);
     void synchronize();
@@ -146,15 +147,20 @@ private:
     size_t gdesc_cap_ = 0;
     void* stream_ = nullptr;
     // program staging: pinned host buffers and device buffers, double buffered
+    // Program memory: every slot's device half is a part of ONE allocation (prog_dev_, slot k
+    // at k * slot_cap_), so launches address programs by 32-bit offsets (tamd_segments).
     struct Slot {
-        uint8_t* host = nullptr;
-        uint8_t* dev = nullptr;
-        size_t cap = 0;
+        uint8_t* host = nullptr;   // pinned staging
+        uint8_t* dev = nullptr;    // prog_dev_ + dev_off
+        uint32_t dev_off = 0;
         void* done = nullptr;  // hipEvent_t
         uint64_t ticket = 0;
     };
     std::vector<Slot> slots_ = std::vector<Slot>(2);
-    size_t slot_bytes_ = 16u << 20;
+    size_t slot_bytes_ = 16u << 20;  // requested initial capacity
+    size_t slot_cap_ = 0;            // current capacity of every slot
+    uint8_t* prog_dev_ = nullptr;
+    bool alloc_slots(size_t cap);    // (re)allocate every slot; nothing may be in flight
     // layout of the program being assembled (begin/fill/launch)
     struct Plan {
         std::vector<Context*> ctxs;
@@ -167,36 +173,23 @@ private:
         bool empty = true;
     } plan_;
     int next_slot_ = 0;
-    // device view of one level of a program, and the deferred levels of the previous program
-    struct LevelSeg {
-        const tamd_op* ops = nullptr;
-        const tamd_instr* instrs = nullptr;
-        const void* items = nullptr;  // uint2 pairs (op, slice)
-        uint32_t count = 0, coop = 0;
-    };
-    struct Tail {
-        bool active = false;
-        const tamd_op* ops = nullptr;
-        const tamd_instr* instrs = nullptr;
-        const void* items = nullptr;  // uint2 pairs (op, slice)
-        uint32_t levels = 0;
+    // Programs with levels still to launch (level pipelining), oldest first.  Every launch runs
+    // the next level of each of them beside level 1 of the newest program; a program completes
+    // (slot event, ticket) once its last level is launched and every older one has completed.
+    struct Inflight {
+        uint32_t ops = 0, instrs = 0, items = 0;  // offsets into prog_dev_
+        uint32_t levels = 0, next = 1;
         std::vector<uint32_t> level_items, item_base, level_coop;
         Slot* slot = nullptr;
         uint64_t ticket = 0;
-        LevelSeg level(uint32_t l) const {
-            LevelSeg s;
-            if (l >= levels) return s;
-            s.ops = ops;
-            s.instrs = instrs;
-            s.items = (const char*)items + 8ull * item_base[l];
-            s.count = level_items[l];
-            s.coop = level_coop[l];
-            return s;
-        }
-    } tail_;
+        bool done() const { return next >= levels; }
+    };
+    std::deque<Inflight> progs_;
     bool pipelined_ = false;
-    void launch_level(const LevelSeg& a, const LevelSeg& b, unsigned long long* stamps);
-    void finish_tail(uint32_t from_level);
+    // one launch: the next level of every program in progs_ (+ `fresh`'s level 1 when given)
+    void launch_step(Inflight* fresh, unsigned long long* stamps);
+    void retire_done();
+    void drain_programs();  // launch every remaining level, complete every program
     uint64_t ticket_ = 0, completed_ = 0;
     std::deque<std::pair<uint64_t, void*>> inflight_;  // (ticket, hipEvent_t) in stream order
     std::vector<void*> free_events_;
@@ -222,7 +215,7 @@ private:
     std::vector<void*> timing_pool_;
     void* timing_event();
     DeviceStats stats_;
-    bool ensure_slot(Slot& s, size_t bytes);
+    bool ensure_slot(Slot& s, size_t bytes);  // every slot grows (after a full drain) when short
 };
 
 } // namespace tamd

@@ -362,14 +362,15 @@ struct Context {
     uint64_t epoch = 1;                // id of the pending program
     uint64_t arena_base_units = 0;     // offset of this context's range in the device arena
     bool oom = false;                  // arena exhausted (codecs go to Disabled)
-    // Level pipelining (the session): a program's levels above kPipeDepth run in the launches of
-    // the NEXT program's first levels (Device::set_pipelined), so a row it writes at level
-    // d > kPipeDepth is still being written while the next program's levels 1 .. d-kPipeDepth
-    // run: in the next program such a row keeps level d - kPipeDepth ("inherited"), and its
-    // readers land above it.
-    static const uint32_t kPipeDepth = 2;
+    // Level pipelining (the session, Device::set_pipelined): every launch runs level 1 of the
+    // newest program beside the next level of each older program still in flight, so level d
+    // of a program runs with level 1 of the program d - 1 later.  A row written at level d is
+    // therefore still being written while the next program's levels 1 .. d - 1 run: there it
+    // keeps level d - 1 ("inherited", one less per program), and its readers land above it.
+    static const uint32_t kPipeDepth = 1;
     bool pipeline = false;
     std::vector<RowId> inherited;      // rows with an inherited level in the pending program
+    std::vector<uint64_t> inherited_at;  // per handle: epoch of its last write
 
     RowId alloc(uint32_t bytes) {
         const RowId r = rows.alloc(bytes);
@@ -403,10 +404,13 @@ struct Context {
         for (FlushClient* c : track_dirty ? dirty : clients) c->pre_flush();
     }
     void finish_flush() {
-        for (RowId r : inherited) rows.set_level(r, 0);
-        inherited.clear();
+        // Rows written now first: their entry supersedes an older one for the same handle (a
+        // handle freed and reused while its old inherited level was counting down).
+        const size_t old = inherited.size();
         for (RowId r : pb.written_rows()) {
             const uint32_t l = rows.level(r);
+            if (r >= inherited_at.size()) inherited_at.resize((size_t)r + 1024, 0);
+            inherited_at[r] = epoch;
             if (pipeline && l > kPipeDepth) {
                 rows.set_level(r, l - kPipeDepth);
                 inherited.push_back(r);
@@ -414,6 +418,19 @@ struct Context {
                 rows.set_level(r, 0);
             }
         }
+        size_t keep = 0;
+        for (size_t k = 0; k < old; ++k) {  // (a row written at level d stays pending d - 1 programs)
+            const RowId r = inherited[k];
+            if (inherited_at[r] == epoch) continue;  // superseded above
+            const uint32_t l = rows.level(r);
+            if (l > kPipeDepth) {
+                rows.set_level(r, l - kPipeDepth);
+                inherited[keep++] = r;
+            } else {
+                rows.set_level(r, 0);
+            }
+        }
+        inherited.erase(inherited.begin() + keep, inherited.begin() + old);
         for (RowId r : temps) rows.free_deferred(r);
         temps.clear();
         ex.clear();

@@ -376,24 +376,37 @@ __device__ __forceinline__ LV<NH> run_item(const tamd_instr* __restrict__ instrs
 // Ops of one level never read a row written by an op of the same level, so every load of a
 // batch can be issued before the batch's stores.  Persistent grid: each workgroup stages the
 // tables in LDS once and then claims items.  A slice is 64 lanes x 8*NH bytes.
-// Two item segments: [0, n_items) of program 1 (ops, instrs, items) and [n_items, n_items +
-// n_items2) of program 2 (ops2, instrs2, items2) -- a pipelined launch runs a level of the
-// previous program beside a level of the next one (Device::launch); n_items2 = 0 otherwise.
+// A launch runs one level each of up to TAMD_MAX_SEGMENTS programs (level pipelining,
+// Device::launch): segment k holds program k's items; items are numbered across segments.
+// Programs live in one device allocation (`prog`); segments address them by byte offsets, so
+// every instruction fetch derives from one noalias argument and stays a scalar load (pointers
+// inside an argument struct would turn them into vector loads: +11 VGPRs, 4 waves/SIMD).
 template <int NH, uint32_t B>
-__device__ __forceinline__ void exec_level(const tamd_op* __restrict__ ops, const tamd_instr* __restrict__ instrs,
-                                           const uint2* __restrict__ items, uint32_t n_items, uint32_t n_shared,
-                                           const tamd_op* __restrict__ ops2, const tamd_instr* __restrict__ instrs2,
-                                           const uint2* __restrict__ items2, uint32_t n_items2,
-                                           uint8_t* __restrict__ arena, const uint32_t* __restrict__ gf_perm,
-                                           const uint8_t* __restrict__ zrow, unsigned long long* __restrict__ stamps) {
+__device__ __forceinline__ void exec_level(const tamd_segments& sg, const uint8_t* __restrict__ pbase,
+                                           uint32_t n_shared, uint8_t* __restrict__ arena,
+                                           const uint32_t* __restrict__ gf_perm, const uint8_t* __restrict__ zrow,
+                                           unsigned long long* __restrict__ stamps) {
     constexpr uint32_t SLICE = 64u * 8u * NH;
     __shared__ __attribute__((aligned(16))) uint32_t lds_perm[TAMD_GF_DWORDS];
     __shared__ LV<NH> partial[TAMD_WAVES_PER_WG][64];  // shared ops: the waves' acc_0
     __shared__ uint32_t claim, shared_claim, shared_item;
+    __shared__ tamd_segment lds_seg[TAMD_MAX_SEGMENTS + 1];  // + a sentinel (count ~0)
     for (uint32_t i = threadIdx.x; i < TAMD_GF_DWORDS / 4; i += blockDim.x)
         ((uint4*)lds_perm)[i] = ((const uint4*)gf_perm)[i];
-    if (threadIdx.x == 0) claim = shared_claim = 0;
+    if (threadIdx.x == 0) {
+        claim = shared_claim = 0;
+        // constant indices only (a dynamic index into the arguments would copy them to scratch)
+#pragma unroll
+        for (uint32_t k = 0; k < TAMD_MAX_SEGMENTS; ++k) {
+            lds_seg[k] = sg.s[k];
+            if (k >= sg.n) lds_seg[k].count = 0;
+        }
+        lds_seg[TAMD_MAX_SEGMENTS].count = ~0u;
+    }
     __syncthreads();
+    const tamd_op* __restrict__ ops = (const tamd_op*)(pbase + sg.s[0].ops);
+    const tamd_instr* __restrict__ instrs = (const tamd_instr*)(pbase + sg.s[0].instrs);
+    const uint2* __restrict__ items = (const uint2*)(pbase + sg.s[0].items);
 
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = uniform(threadIdx.x >> 6);
@@ -441,16 +454,21 @@ __device__ __forceinline__ void exec_level(const tamd_op* __restrict__ ops, cons
     // them (a stratified sample of the level: ordered by cost class, most expensive first); its
     // waves claim them one at a time through an LDS counter, so a wave that drew a long op does
     // not hold up the others.
-    const uint32_t n_all = n_items + n_items2;
+    uint32_t n_all = 0;
+    for (uint32_t k = 0; k < sg.n; ++k) n_all += sg.s[k].count;
     for (;;) {
         uint32_t k = 0;
         if (lane == 0) k = atomicAdd(&claim, 1u);
         const uint32_t it = n_shared + blockIdx.x + uniform(__shfl(k, 0)) * gridDim.x;
         if (it >= n_all) break;
-        const bool second = it >= n_items;
-        const tamd_instr* __restrict__ ins = second ? instrs2 : instrs;
-        const uint2 item = second ? items2[it - n_items] : items[it];
-        const tamd_op op = second ? ops2[uniform(item.x)] : ops[uniform(item.x)];
+        // the item's segment, from the LDS copy of the segment table (wave-uniform reads)
+        uint32_t seg = 0, rel = it;
+        while (rel >= lds_seg[seg].count) rel -= lds_seg[seg++].count;
+        const tamd_segment sd = lds_seg[seg];
+        const tamd_op* __restrict__ sops = (const tamd_op*)(pbase + uniform(sd.ops));
+        const tamd_instr* __restrict__ ins = (const tamd_instr*)(pbase + uniform(sd.instrs));
+        const uint2 item = ((const uint2*)(pbase + uniform(sd.items)))[uniform(rel)];
+        const tamd_op op = sops[uniform(item.x)];
         const uint32_t s0 = uniform(item.y) * SLICE;
         const uint32_t o = s0 + laneb;
         const uint32_t first = uniform(op.first), end = uniform(op.first + op.count);
@@ -475,14 +493,11 @@ __device__ __forceinline__ void exec_level(const tamd_op* __restrict__ ops, cons
 // (108 VGPRs, 4 waves/SIMD); only this variant is built.
 #define TAMD_EXEC_KERNEL(name, NH, B)                                                                  \
     extern "C" __global__ void __launch_bounds__(256)                                                   \
-    name(const tamd_op* __restrict__ ops, const tamd_instr* __restrict__ instrs,                       \
-         const uint2* __restrict__ items, uint32_t n_items, uint32_t n_shared,                         \
-         const tamd_op* __restrict__ ops2, const tamd_instr* __restrict__ instrs2,                     \
-         const uint2* __restrict__ items2, uint32_t n_items2, uint8_t* __restrict__ arena,             \
+    name(const tamd_segments segments, const uint8_t* __restrict__ prog, uint32_t n_shared,            \
+         uint8_t* __restrict__ arena,                                                                  \
          const uint32_t* __restrict__ gf_perm, const uint8_t* __restrict__ zrow,                       \
          unsigned long long* __restrict__ stamps) {                                                    \
-        exec_level<NH, B>(ops, instrs, items, n_items, n_shared, ops2, instrs2, items2, n_items2, arena, gf_perm, \
-                          zrow, stamps);                                                               \
+        exec_level<NH, B>(segments, prog, n_shared, arena, gf_perm, zrow, stamps);                    \
     }
 TAMD_EXEC_KERNEL(tamd_exec16, 2, 6)
 

@@ -78,6 +78,19 @@ typedef struct tamd_op {
                      // per-lane length handling (the executor's fast path)
 } tamd_op;
 
+// The item segments of one executor launch (level pipelining: one level each of up to
+// TAMD_MAX_SEGMENTS programs; items are numbered across the segments in order).  Passed by
+// value; byte offsets into the device's program memory.
+#define TAMD_MAX_SEGMENTS 6
+typedef struct tamd_segment {
+    uint32_t ops, instrs, items;  // offsets of the program's ops / instructions / this level's items
+    uint32_t count;               // items ((op index, slice) uint32 pairs)
+} tamd_segment;
+typedef struct tamd_segments {
+    tamd_segment s[TAMD_MAX_SEGMENTS];
+    uint32_t n, pad;
+} tamd_segments;
+
 static inline uint32_t tamd_w0(uint32_t kind, uint32_t arg, uint32_t arg2 = 0) {
     return kind | (arg << 8) | (arg2 << 16);
 }

@@ -545,10 +545,12 @@ void* tamd_session_create(const tamd_session_params* p, char* err, size_t err_le
     if (!gf_init()) return fail("gf self test failed");
     std::unique_ptr<Session> s(new Session());
     s->prm = *p;
-    if (!s->dev.init((int)p->device, p->arena_bytes)) return fail(s->dev.error());
     // Level pipelining (Device::set_pipelined): off when packets are staged through the host
-    // (the D2H gather right after a program needs all of its levels) and for A/B runs.
+    // (the D2H gather right after a program needs all of its levels) and for A/B runs.  A
+    // program stays in flight for as many launches as it has levels: 6 staging slots.
     const bool pipe = !p->stage_host && getenv("TONK_AMD_NO_PIPELINE") == nullptr;
+    s->dev.set_program_slots(pipe ? 6 : 2, 16u << 20);
+    if (!s->dev.init((int)p->device, p->arena_bytes)) return fail(s->dev.error());
     s->dev.set_pipelined(pipe);
     if (!s->dev.gf_selftest()) return fail("device GF(256) self test failed");
 
@@ -758,6 +760,12 @@ void tamd_session_host_ms(void* sp, double out[10]) {
 }
 
 void tamd_session_destroy(void* sp) { delete (Session*)sp; }
+
+const char* tamd_session_error(void* sp) {
+    Session* s = (Session*)sp;
+    if (!s->error.empty()) return s->error.c_str();
+    return s->dev.error().c_str();
+}
 
 void tamd_set_clock(uint64_t (*fn)(void)) { set_clock_source(fn); }
 
