@@ -188,7 +188,7 @@ int main(int argc, char** argv) {
     p.loss_thresh = 42949673;
     p.fec_rate_q16 = 1311;
     p.ack_every = 64;
-    uint32_t streams = 8, step = 4096;
+    uint32_t streams = 8, step = 4096, warm_steps = 0;  // warm: untimed, unsampled first steps
     p.n_originals = 4096 * 6;
     for (int i = 1; i < argc; ++i) {
         const char* eq = strchr(argv[i], '=');
@@ -197,6 +197,7 @@ int main(int argc, char** argv) {
         if (k == "sample") continue;
         if (k == "stub") { g_stub = atoi(eq + 1); continue; }
         if (k == "nobatch") { g_nobatch = atoi(eq + 1); continue; }
+        if (k == "warm") { warm_steps = (uint32_t)atoi(eq + 1); continue; }
         const unsigned long long v = strtoull(eq + 1, nullptr, 0);
         if (k == "streams") streams = (uint32_t)v;
         else if (k == "n") p.n_originals = (uint32_t)v;
@@ -236,7 +237,8 @@ int main(int argc, char** argv) {
         run[s].reset(new wl::Runner<Null, NoTr>(ps[s], *be[s], tr));
     }
     uint64_t instrs = 0, ops = 0, acc_bytes = 0, store_bytes = 0;
-    if (sample_out) {
+    auto start_sampling = [&]() {
+        if (!sample_out) return;
         struct sigaction sa;
         memset(&sa, 0, sizeof(sa));
         sa.sa_sigaction = on_prof;
@@ -247,9 +249,20 @@ int main(int argc, char** argv) {
         tv.it_interval.tv_usec = 100;
         tv.it_value = tv.it_interval;
         setitimer(ITIMER_PROF, &tv, nullptr);
-    }
-    const auto t0 = std::chrono::steady_clock::now();
-    for (uint32_t done = 0; done < p.n_originals; done += step) {
+    };
+    auto t0 = std::chrono::steady_clock::now();
+    uint32_t timed_originals = 0, step_no = 0;
+    if (!warm_steps) start_sampling();
+    for (uint32_t done = 0; done < p.n_originals; done += step, ++step_no) {
+        if (warm_steps && step_no == warm_steps) {
+            t0 = std::chrono::steady_clock::now();
+#ifdef TAMD_PROF
+            memset(prof::cycles, 0, sizeof(prof::cycles));
+            memset(prof::calls, 0, sizeof(prof::calls));
+#endif
+            start_sampling();
+        }
+        if (step_no >= warm_steps) timed_originals += (done + step <= p.n_originals ? step : p.n_originals - done);
         for (uint32_t s = 0; s < streams; ++s) {
             Context& ctx = *ctxs[s];
             run[s]->advance(step);
@@ -295,7 +308,8 @@ int main(int argc, char** argv) {
         if (in) fclose(in);
         if (out) fclose(out);
     }
-    const double n = (double)streams * p.n_originals;
+    if (getenv("CP_BENCH_WIN")) fprintf(stderr, "enc window %u\n", (unsigned)(kMaxPackets - encs[0]->remaining_slots()));
+    const double n = (double)streams * timed_originals;
     printf("{\"ns_per_original\": %.1f, \"instrs_per_original\": %.2f, \"ops_per_original\": %.3f, "
            "\"acc_bytes_per_original\": %.0f, \"store_bytes_per_original\": %.0f, \"seconds\": %.3f}\n",
            sec * 1e9 / n, instrs / n, ops / n, acc_bytes / n, store_bytes / n, sec);

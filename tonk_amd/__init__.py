@@ -20,6 +20,9 @@ __all__ = ["LIB_PATH", "build", "lib", "Session", "WorkloadParams", "loss_thresh
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libtonk_amd.so")
+# A/B runs of two builds on one box (tools/gpu_ab_lib.sh): another in-tree build of the library.
+if os.environ.get("TONK_AMD_LIB"):
+    LIB_PATH = os.path.join(_HERE, os.path.basename(os.environ["TONK_AMD_LIB"]))
 _lib = None
 
 

@@ -200,15 +200,20 @@ Result Decoder::add_original(uint32_t packet_num, RowId row, uint32_t framed_byt
     return kSuccess;
 }
 
-// k add_original() calls for the next columns col0 .. col0 + k - 1 (rows[0..k)), batched.  Only taken while no recovery packet is pending: then none of
-// those calls can make is_ready() succeed (there is no recovery to check), and the new elements
-// lie beyond the window end, so each call only stores the row, sets its got bit and moves
-// NextExpected along (SiameseDecoder.cpp:1467-1536 restated for that case).
+// k add_original() calls for the next columns col0 .. col0 + k - 1 (rows[0..k)), each followed
+// by an is_ready() that fails, batched.  The new elements lie beyond the window end, so each call
+// only stores the row, sets its got bit and moves NextExpected along (SiameseDecoder.cpp:
+// 1467-1536 restated for that case); is_ready() cannot succeed when no recovery is pending.
 bool Decoder::add_run_inorder(uint32_t col0, const RowId* rows, uint32_t k, uint32_t framed_bytes,
                               uint32_t header_bytes, uint32_t payload_bytes, bool borrowed) {
-    if (disabled_ || head_ || has_recovered_ || !k) return false;
+    if (disabled_ || has_recovered_ || !k) return false;
     const uint32_t e0 = to_element(col0);
     if (col_delta_negative(e0) || e0 < count_) return false;
+    // Recovery packets pending: the run is still batchable when an earlier element is lost (so
+    // NextExpected stays put and no recovery is deleted) and the decoder is not ready now.  The
+    // new elements lie past every pending recovery's range, so each single call's is_ready()
+    // would repeat this answer without changing any state.
+    if (head_ && (next_expected_ >= e0 || check_recovery_possible())) return false;
     grow_window(e0 + k);
     for (uint32_t j = 0; j < k; ++j) {
         const uint32_t e = e0 + j;

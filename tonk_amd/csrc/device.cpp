@@ -2,6 +2,7 @@
 #include "device.h"
 
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <chrono>
 #include <stdio.h>
 #include <stdlib.h>
@@ -12,6 +13,7 @@ extern "C" __global__ void tamd_exec16(tamd_segments, const uint8_t*, uint32_t, 
 typedef void (*ExecFn)(tamd_segments, const uint8_t*, uint32_t, uint8_t*, const uint32_t*, const uint8_t*,
                        unsigned long long*);
 extern "C" __global__ void tamd_gf_selftest(const uint32_t*, uint8_t*);
+extern "C" __global__ void tamd_timed_region();
 extern "C" __global__ void tamd_gather_rows(const tamd::Device::GatherDesc*, uint32_t, const uint8_t*, uint8_t*);
 struct ScatterDescDev { uint32_t row, len, src, pad; };
 extern "C" __global__ void tamd_scatter_rows(const ScatterDescDev*, uint32_t, const uint8_t*, uint8_t*);
@@ -414,7 +416,6 @@ void Device::launch_step(Inflight* fresh, unsigned long long* stamps) {
     if (timing_) {
         e0 = (hipEvent_t)timing_event();
         e1 = (hipEvent_t)timing_event();
-        hipEventRecord(e0, st);
     }
     // Class-0 ops are shared by a workgroup only in launches too small to fill the chip twice
     // over with single-wave items; in the big ones they run as ordinary (first) items.  Only the
@@ -422,13 +423,24 @@ void Device::launch_step(Inflight* fresh, unsigned long long* stamps) {
     static const int share_mode = getenv("TONK_AMD_SHARE") ? atoi(getenv("TONK_AMD_SHARE")) : 0;  // A/B (profiling)
     const uint32_t shared = (share_mode == 1 || (share_mode == 0 && cnt < 2u * 4u * max_grid_)) ? coop : 0u;
     const ExecFn fn = (ExecFn)exec_kernel_;
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, st, sg, (const uint8_t*)prog_dev_, shared, arena_, d_gf_, d_zero_,
-                       stamps);
+    // Timed: the events carry the dispatch's own start and end (hipExtLaunchKernelGGL), as a
+    // kernel trace does; events recorded around the launch would add the dispatch latency.
+    if (timing_)
+        hipExtLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, st, e0, e1, 0, sg, (const uint8_t*)prog_dev_, shared,
+                              arena_, d_gf_, d_zero_, stamps);
+    else
+        hipLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, st, sg, (const uint8_t*)prog_dev_, shared, arena_, d_gf_,
+                           d_zero_, stamps);
     if (timing_) {
-        hipEventRecord(e1, st);
         timing_events_.push_back(std::make_pair((void*)e0, (void*)e1));
     }
     stats_.launches++;
+}
+
+void Device::set_timing(bool on) {
+    if (on == timing_) return;
+    if (stream_) hipLaunchKernelGGL(tamd_timed_region, dim3(1), dim3(64), 0, (hipStream_t)stream_);
+    timing_ = on;
 }
 
 // Complete the oldest programs whose levels have all been launched (in ticket order).

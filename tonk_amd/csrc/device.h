@@ -114,7 +114,9 @@ public:
     void sync_staging();
 
     // Kernel timing with HIP events around every tamd_exec launch (on the launch stream).
-    void set_timing(bool on) { timing_ = on; }
+    // Turning timing on or off also launches the empty kernel tamd_timed_region, so a kernel
+    // trace of the run can average exactly the timed launches (tools/trace_region.py).
+    void set_timing(bool on);
     DeviceStats& stats() { return stats_; }
     void collect_timing();  // adds pending event pairs into stats().kernel_ms
 

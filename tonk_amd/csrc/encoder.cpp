@@ -81,7 +81,14 @@ inline void Encoder::add_unchecked(RowId row, uint32_t off, uint32_t framed_byte
     }
     // Elements below `element` in a fresh window are never read (placeholders).
     while (win_.size() < element) win_.push_back(StoredOriginal());
-    StoredOriginal o;
+    StoredOriginal* slot;
+    if (win_.size() == element) {
+        slot = &win_.push_slot();
+    } else {
+        slot = &win_[element];
+        drop_original(*slot);
+    }
+    StoredOriginal& o = *slot;
     o.row = row;
     o.off = off;
     o.bytes = framed_bytes;
@@ -91,6 +98,7 @@ inline void Encoder::add_unchecked(RowId row, uint32_t off, uint32_t framed_byte
     o.send_msec = (uint32_t)now_msec();
     o.host = host;
     o.run = 1;
+    o.stride = 0;
     if (element > 0) {
         const StoredOriginal& p = win_[element - 1];
         if (p.bytes == framed_bytes && o.off > p.off && p.run < 0xffff &&
@@ -99,8 +107,6 @@ inline void Encoder::add_unchecked(RowId row, uint32_t off, uint32_t framed_byte
             o.stride = o.off - p.off;
         }
     }
-    if (win_.size() == element) win_.push_back(o);
-    else { drop_original(win_[element]); win_[element] = o; }
 
     next_column_ = col_inc(next_column_);
 

@@ -16,6 +16,12 @@ public:
         buf_[(head_ + n_) & mask_] = v;
         ++n_;
     }
+    // Append a slot to fill in place (no temporary: a struct built in narrow fields and then
+    // copied with wide loads stalls on store forwarding).
+    T& push_slot() {
+        if (n_ == buf_.size()) grow();
+        return buf_[(head_ + n_++) & mask_];
+    }
     void pop_front(size_t k) {
         if (k > n_) k = n_;
         for (size_t i = 0; i < k; ++i) buf_[(head_ + i) & mask_] = T();
