@@ -1,0 +1,151 @@
+// lz_check.cpp -- TEST ONLY.  Checks the zstd block writer the compression kernel uses (the
+// host+device helpers of tonk_amd/csrc/lz.h: FSE tables of the predefined distributions,
+// literal/sequence headers, the backward sequence bit stream) against the reference's zstd
+// decoder (oracle/_ref/libmsgcodec_ref.so, MessageDecompressor restated over thirdparty/zstd),
+// with a plain greedy matcher standing in for the kernel's parse.  The GPU tests run the kernel
+// itself against the same decoder.
+//
+// usage: lz_check [messages] [seed]   -> prints "ok <compressed> <total>" or the first mismatch
+#include "../../tonk_amd/csrc/lz.h"
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <vector>
+
+extern "C" {
+void* ref_decomp_new(unsigned max);
+void ref_insert(void* d, const uint8_t* data, unsigned bytes);
+int ref_decomp(void* d, const uint8_t* src, unsigned bytes, uint8_t* out, unsigned cap);
+void ref_decomp_free(void* d);
+}
+
+static uint32_t rng_state = 1;
+static uint32_t rnd() {
+    rng_state = rng_state * 1664525u + 1013904223u;
+    return rng_state >> 8;
+}
+
+int main(int argc, char** argv) {
+    const unsigned n_msgs = argc > 1 ? (unsigned)atoi(argv[1]) : 400;
+    rng_state = argc > 2 ? (uint32_t)atoi(argv[2]) : 1;
+    const unsigned kMax = 1300, kDict = 24000;
+    uint8_t fse[TAMD_FSE_BYTES];
+    tamd_fse_blob(fse);
+    // a stream of messages: words from a small vocabulary, random bytes, repeats of old messages
+    std::vector<uint8_t> stream;
+    std::vector<unsigned> lens;
+    const char* words[] = {"siamese ", "tonk ", "packet ", "recovery ", "window ", "lane ", "sum ", "ack ", "0123 "};
+    for (unsigned k = 0; k < n_msgs; ++k) {
+        const unsigned n = 8 + rnd() % (kMax - 8);
+        const unsigned kind = rnd() % 4;
+        const size_t at = stream.size();
+        if (kind == 3 && at > 4000) {  // repeat an earlier stretch
+            const size_t from = at - 1 - rnd() % (at < 40000 ? at - 1 : 40000);
+            for (unsigned i = 0; i < n; ++i) stream.push_back(stream[from + i < at ? from + i : at - 1]);
+        } else {
+            for (unsigned i = 0; i < n;) {
+                if (kind == 0) {
+                    stream.push_back((uint8_t)rnd());
+                    ++i;
+                } else {
+                    const char* w = words[rnd() % 9];
+                    for (const char* c = w; *c && i < n; ++c, ++i) stream.push_back((uint8_t)*c);
+                }
+            }
+        }
+        lens.push_back(n);
+    }
+    void* dec = ref_decomp_new(kMax);
+    // ring bookkeeping of compress.cpp (RingTrack) restated for the check
+    unsigned next = 0;
+    uint64_t lin = 0, seg = 0, prev = 0;
+    bool have_prev = false;
+    std::vector<int64_t> table(1u << 14, -1);
+    uint64_t total_in = 0, total_out = 0;
+    unsigned compressed = 0;
+    std::vector<uint8_t> out(kMax + 64), got(kMax + 64);
+    for (unsigned k = 0; k < n_msgs; ++k) {
+        const unsigned n = lens[k];
+        if (next + kMax > kDict) {
+            if (next) {
+                prev = seg;
+                have_prev = true;
+                seg = lin;
+            }
+            next = 0;
+        }
+        const uint64_t pos = lin;
+        uint64_t win = seg;
+        if (have_prev) win = prev + next + n < seg ? prev + next + n : seg;
+        // greedy parse
+        std::vector<uint32_t> lo, off;
+        const uint8_t* s = stream.data();
+        auto hash = [&](uint64_t p) {
+            uint32_t w;
+            memcpy(&w, s + p, 4);
+            return (w * 2654435761u) >> 18;
+        };
+        uint32_t lit_start = 0, i = 0;
+        while (i + 4 <= n) {
+            const uint64_t p = pos + i;
+            const int64_t c = table[hash(p)];
+            table[hash(p)] = (int64_t)p;
+            uint32_t len = 0;
+            if (c >= 0 && (uint64_t)c >= win && (uint64_t)c < p)
+                while (len < n - i && s[c + len] == s[p + len]) ++len;
+            if (len >= 4) {
+                lo.push_back((i - lit_start) | (len << 16));
+                off.push_back((uint32_t)(p - (uint64_t)c));
+                for (uint32_t j = 1; j < len && i + j + 4 <= n; ++j) table[hash(p + j)] = (int64_t)(p + j);
+                i += len;
+                lit_start = i;
+            } else {
+                ++i;
+            }
+        }
+        unsigned w = 0;
+        if (!lo.empty()) {
+            uint32_t lits = n - lit_start;
+            for (uint32_t v : lo) lits += v & 0xffffu;
+            uint8_t h[4];
+            w = tamd_lits_header(lits, out.data());
+            uint32_t src = 0;
+            for (size_t q = 0; q <= lo.size(); ++q) {
+                const uint32_t ll = q < lo.size() ? (lo[q] & 0xffffu) : n - lit_start;
+                memcpy(&out[w], s + pos + src, ll);
+                w += ll;
+                if (q < lo.size()) src += ll + (lo[q] >> 16);
+            }
+            const uint32_t hs = tamd_seq_header((uint32_t)lo.size(), h);
+            memcpy(&out[w], h, hs);
+            w += hs;
+            if (w < n - 1) {
+                const uint32_t nb = tamd_fse_sequences(lo.data(), off.data(), (uint32_t)lo.size(), fse, &out[w],
+                                                       n - 1 - w);
+                w = nb ? w + nb : 0;
+            } else {
+                w = 0;
+            }
+        }
+        if (w && w < n) {
+            const int r = ref_decomp(dec, out.data(), w, got.data(), (unsigned)got.size());
+            if (r != (int)n || memcmp(got.data(), s + pos, n) != 0) {
+                printf("mismatch at message %u (n %u, block %u bytes, %zu sequences, rc %d)\n", k, n, w, lo.size(), r);
+                return 1;
+            }
+            ++compressed;
+            total_out += w;
+        } else {
+            ref_insert(dec, s + pos, n);
+            total_out += n;
+        }
+        total_in += n;
+        next += n;
+        lin += n;
+    }
+    ref_decomp_free(dec);
+    printf("ok %u/%u compressed, %llu -> %llu bytes\n", compressed, n_msgs, (unsigned long long)total_in,
+           (unsigned long long)total_out);
+    return 0;
+}

@@ -57,7 +57,11 @@ void Decoder::pre_flush() {
 void Decoder::drop_original(StoredOriginal& o) {
     if (o.owned) ctx_->rows.free_deferred(o.row);
     if (o.host && release_) release_(o.host, user_);
-    o = StoredOriginal();
+    // an empty slot is bytes == 0 (every add writes all the other fields)
+    o.row = kNoRow;
+    o.bytes = 0;
+    o.owned = 0;
+    o.host = nullptr;
 }
 
 void Decoder::free_recovery(Recovery* r) {

@@ -36,9 +36,13 @@ Encoder::~Encoder() {
     ctx_->detach(this);
 }
 
-void Encoder::drop_original(StoredOriginal& o) {
+void Encoder::release_original(const StoredOriginal& o) {
     if (o.owned) ctx_->rows.free_deferred(o.row);
     if (o.host && release_) release_(o.host, user_);
+}
+
+void Encoder::drop_original(StoredOriginal& o) {
+    release_original(o);
     o = StoredOriginal();
 }
 
@@ -172,7 +176,7 @@ void Encoder::remove_elements() {
         sum_start_ = sum_start_ > removed ? sum_start_ - removed : 0;
     }
 
-    for (uint32_t i = 0; i < removed && i < win_.size(); ++i) drop_original(win_[i]);
+    for (uint32_t i = 0; i < removed && i < win_.size(); ++i) release_original(win_[i]);
     win_.pop_front(removed);
     count_ -= removed;
     column_start_ = to_column(removed);

@@ -93,6 +93,7 @@ private:
     bool disabled_ = false;
     const uint64_t* clock_ = nullptr;
     uint64_t now_msec() const;
+    void release_original(const StoredOriginal& o);  // frees what the slot owns (slot left as is)
 
     // ---- EncoderPacketWindow (SiameseEncoder.h:104-232) ----
     Ring<StoredOriginal> win_;

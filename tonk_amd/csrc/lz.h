@@ -1,0 +1,247 @@
+// lz.h -- layouts shared by the compression kernel (lz.hip) and its host side (compress.cpp):
+// job and message descriptors, the FSE table blob, and the zstd length-code tables
+// (RFC 8878 s3.1.1.3.2.1.1, the literal-length and match-length codes; offsets are coded as
+// Offset_Value = offset + 3, code = highbit(Offset_Value), value bits = the rest).
+#pragma once
+#include <stdint.h>
+
+#define TAMD_LZ_MAX_MESSAGE 2048u  // larger messages are stored uncompressed (written = 0)
+#define TAMD_LZ_WINDOW 32768u      // history bytes inserted into a job's hash table
+
+// A run of consecutive messages of one stream.  `buf` holds the stream's bytes at their linear
+// positions (masked by `mask`: a power-of-two ring, or ~0 for a linear array).
+typedef struct tamd_lz_job {
+    const uint8_t* buf;
+    uint32_t mask, first, count, pad;
+} tamd_lz_job;
+
+// One message: linear position and length, the start of the bytes the decompressor holds when it
+// decodes it (previous history segment start), and its output slot.
+typedef struct tamd_lz_msg {
+    uint32_t pos, len, win, out, cap, pad[3];
+} tamd_lz_msg;
+
+// FSE tables of the predefined distributions, one blob:
+//   *_ENC[symbol][next_state] = the state of `symbol` whose bit range holds next_state
+//   *_DEC[state] = {nbBits, newState} of the decoding table (FSE_buildDTable's layout)
+#define TAMD_FSE_LL_ENC 0u
+#define TAMD_FSE_ML_ENC (TAMD_FSE_LL_ENC + 36u * 64u)
+#define TAMD_FSE_OF_ENC (TAMD_FSE_ML_ENC + 53u * 64u)
+#define TAMD_FSE_LL_DEC (TAMD_FSE_OF_ENC + 29u * 32u)
+#define TAMD_FSE_ML_DEC (TAMD_FSE_LL_DEC + 64u * 2u)
+#define TAMD_FSE_OF_DEC (TAMD_FSE_ML_DEC + 64u * 2u)
+#define TAMD_FSE_BYTES (TAMD_FSE_OF_DEC + 32u * 2u)
+
+#ifdef __HIPCC__
+#define TAMD_HD __host__ __device__
+#else
+#define TAMD_HD
+#endif
+
+// literal length codes 16..24 have the irregular bases; from 25 on, base 2^(code-19)
+TAMD_HD static inline uint32_t tamd_ll_bits(uint32_t code) {
+    if (code < 16) return 0;
+    if (code < 20) return 1;
+    if (code < 22) return 2;
+    if (code < 24) return 3;
+    if (code == 24) return 4;
+    return code - 19;
+}
+TAMD_HD static inline uint32_t tamd_ll_base(uint32_t code) {
+    if (code < 16) return code;
+    if (code < 20) return 16 + 2 * (code - 16);
+    if (code < 22) return 24 + 4 * (code - 20);
+    if (code < 24) return 32 + 8 * (code - 22);
+    if (code == 24) return 48;
+    return 1u << (code - 19);
+}
+// match length codes: 0..31 are lengths 3..34; 32..42 irregular; from 43 on, base 2^(code-36)+3
+TAMD_HD static inline uint32_t tamd_ml_bits(uint32_t code) {
+    if (code < 32) return 0;
+    if (code < 36) return 1;
+    if (code < 38) return 2;
+    if (code < 40) return 3;
+    if (code < 42) return 4;
+    if (code == 42) return 5;
+    return code - 36;
+}
+TAMD_HD static inline uint32_t tamd_ml_base(uint32_t code) {
+    if (code < 32) return code + 3;
+    if (code < 36) return 35 + 2 * (code - 32);
+    if (code < 38) return 43 + 4 * (code - 36);
+    if (code < 40) return 51 + 8 * (code - 38);
+    if (code < 42) return 67 + 16 * (code - 40);
+    if (code == 42) return 99;
+    return (1u << (code - 36)) + 3;
+}
+
+// Code of a literal length / match length (the inverse of the tables above).
+TAMD_HD static inline uint32_t tamd_ll_code(uint32_t ll) {
+    if (ll < 16) return ll;
+    if (ll < 24) return 16 + ((ll - 16) >> 1);
+    if (ll < 32) return 20 + ((ll - 24) >> 2);
+    if (ll < 48) return 22 + ((ll - 32) >> 3);
+    if (ll < 64) return 24;
+    return 19 + (31 - (uint32_t)__builtin_clz(ll));  // 64-127: 25, 128-255: 26, ...
+}
+TAMD_HD static inline uint32_t tamd_ml_code(uint32_t ml) {  // ml >= 3
+    if (ml < 35) return ml - 3;
+    if (ml < 43) return 32 + ((ml - 35) >> 1);
+    if (ml < 51) return 36 + ((ml - 43) >> 2);
+    if (ml < 67) return 38 + ((ml - 51) >> 3);
+    if (ml < 99) return 40 + ((ml - 67) >> 4);
+    if (ml < 131) return 42;
+    return 36 + (31 - (uint32_t)__builtin_clz(ml - 3));  // 131-258: 43, 259-514: 44, ...
+}
+
+// Literals section header of raw literals (RFC 8878 s3.1.1.3.1.1): 1, 2 or 3 bytes.
+TAMD_HD static inline uint32_t tamd_lits_header(uint32_t lits, uint8_t* h) {
+    if (lits < 32) {
+        h[0] = (uint8_t)(lits << 3);
+        return 1;
+    }
+    if (lits < 4096) {
+        h[0] = (uint8_t)(0x04u | ((lits & 15u) << 4));
+        h[1] = (uint8_t)(lits >> 4);
+        return 2;
+    }
+    h[0] = (uint8_t)(0x0cu | ((lits & 15u) << 4));
+    h[1] = (uint8_t)(lits >> 4);
+    h[2] = (uint8_t)(lits >> 12);
+    return 3;
+}
+
+// Sequences section header (s3.1.1.3.2.1): the count, then the modes byte (0: the predefined
+// distributions for all three codes) when there are sequences.
+TAMD_HD static inline uint32_t tamd_seq_header(uint32_t n, uint8_t* h) {
+    uint32_t w = 0;
+    if (n < 128) {
+        h[w++] = (uint8_t)n;
+    } else if (n < 0x7f00) {
+        h[w++] = (uint8_t)(0x80u + (n >> 8));
+        h[w++] = (uint8_t)n;
+    } else {
+        h[w++] = 0xff;
+        h[w++] = (uint8_t)(n - 0x7f00u);
+        h[w++] = (uint8_t)((n - 0x7f00u) >> 8);
+    }
+    if (n) h[w++] = 0;
+    return w;
+}
+
+// The sequences' bit stream (s3.1.1.3.2.2 / 4.1): written forward here, read backward by the
+// decoder.  The decoder reads the initial LL, OF, ML states, then per sequence the offset, match
+// length and literal length value bits followed (except after the last sequence) by the LL, ML,
+// OF state updates; so the writer starts from the last sequence and emits everything in the
+// reverse order.  Sequence k: seq_lo[k] = literal length | match length << 16, seq_off[k] =
+// offset (no repeat codes: Offset_Value = offset + 3).  Returns the bytes written (end mark
+// included), 0 when they would exceed cap.
+TAMD_HD static inline uint32_t tamd_fse_sequences(const uint32_t* seq_lo, const uint32_t* seq_off, uint32_t nseq,
+                                                 const uint8_t* tabs, uint8_t* out, uint32_t cap) {
+    uint64_t acc = 0;
+    uint32_t nbits = 0, pos = 0;
+    bool over = false;
+    auto add = [&](uint32_t v, uint32_t bits) {
+        if (!bits) return;
+        acc |= (uint64_t)(v & ((1u << bits) - 1u)) << nbits;
+        nbits += bits;
+        while (nbits >= 8) {
+            if (pos < cap) out[pos] = (uint8_t)acc;
+            else over = true;
+            ++pos;
+            acc >>= 8;
+            nbits -= 8;
+        }
+    };
+    const uint8_t* ll_enc = tabs + TAMD_FSE_LL_ENC;
+    const uint8_t* ml_enc = tabs + TAMD_FSE_ML_ENC;
+    const uint8_t* of_enc = tabs + TAMD_FSE_OF_ENC;
+    const uint8_t* ll_dec = tabs + TAMD_FSE_LL_DEC;
+    const uint8_t* ml_dec = tabs + TAMD_FSE_ML_DEC;
+    const uint8_t* of_dec = tabs + TAMD_FSE_OF_DEC;
+    uint32_t s = nseq - 1;
+    uint32_t ll = seq_lo[s] & 0xffffu, ml = seq_lo[s] >> 16, off = seq_off[s] + 3u;
+    uint32_t llc = tamd_ll_code(ll), mlc = tamd_ml_code(ml), ofc = 31u - (uint32_t)__builtin_clz(off);
+    // any state of the symbol can start: take the one whose range holds next-state 0
+    uint32_t st_ll = ll_enc[llc * 64], st_ml = ml_enc[mlc * 64], st_of = of_enc[ofc * 32];
+    add(ll - tamd_ll_base(llc), tamd_ll_bits(llc));
+    add(ml - tamd_ml_base(mlc), tamd_ml_bits(mlc));
+    add(off, ofc);
+    while (s-- > 0) {
+        ll = seq_lo[s] & 0xffffu;
+        ml = seq_lo[s] >> 16;
+        off = seq_off[s] + 3u;
+        llc = tamd_ll_code(ll);
+        mlc = tamd_ml_code(ml);
+        ofc = 31u - (uint32_t)__builtin_clz(off);
+        // into the states of sequence s + 1: offsets, match lengths, literal lengths
+        uint32_t u = of_enc[ofc * 32 + st_of];
+        add(st_of - of_dec[2 * u + 1], of_dec[2 * u]);
+        st_of = u;
+        u = ml_enc[mlc * 64 + st_ml];
+        add(st_ml - ml_dec[2 * u + 1], ml_dec[2 * u]);
+        st_ml = u;
+        u = ll_enc[llc * 64 + st_ll];
+        add(st_ll - ll_dec[2 * u + 1], ll_dec[2 * u]);
+        st_ll = u;
+        add(ll - tamd_ll_base(llc), tamd_ll_bits(llc));
+        add(ml - tamd_ml_base(mlc), tamd_ml_bits(mlc));
+        add(off, ofc);
+    }
+    add(st_ml, 6);  // the initial states, read first by the decoder: LL, OF, ML
+    add(st_of, 5);
+    add(st_ll, 6);
+    add(1, 1);  // end mark
+    if (nbits) add(0, 8 - nbits);
+    return over ? 0 : pos;
+}
+
+// Host: the FSE blob of the predefined distributions (RFC 8878 s3.1.1.3.2.2; zstd_internal.h
+// LL/ML/OF_defaultNorm).  Each decoding table is laid out as FSE_buildDTable does
+// (fse_decompress.c:93-148 restated: probability -1 symbols at the top, the others spread with
+// step 5/8 of the table + 3, then per state its bit count and next-state base); the encoder's map
+// inverts it: for a symbol and the state the decoder must reach next, the state to be in now.
+static inline void tamd_build_fse(const int16_t* norm, uint32_t nsym, uint32_t log, uint8_t* enc, uint8_t* dec) {
+    const uint32_t size = 1u << log;
+    uint32_t sym[64], next[64];
+    uint32_t high = size - 1;
+    for (uint32_t s = 0; s < nsym; ++s) {
+        if (norm[s] == -1) {
+            sym[high--] = s;
+            next[s] = 1;
+        } else {
+            next[s] = (uint32_t)norm[s];
+        }
+    }
+    const uint32_t step = (size >> 1) + (size >> 3) + 3, mask = size - 1;
+    uint32_t pos = 0;
+    for (uint32_t s = 0; s < nsym; ++s)
+        for (int i = 0; i < norm[s]; ++i) {
+            sym[pos] = s;
+            pos = (pos + step) & mask;
+            while (pos > high) pos = (pos + step) & mask;
+        }
+    for (uint32_t u = 0; u < size; ++u) {
+        const uint32_t s = sym[u];
+        const uint32_t ns = next[s]++;
+        const uint32_t nb = log - (31u - (uint32_t)__builtin_clz(ns));
+        const uint32_t base = (ns << nb) - size;
+        dec[2 * u] = (uint8_t)nb;
+        dec[2 * u + 1] = (uint8_t)base;
+        for (uint32_t y = base; y < base + (1u << nb); ++y) enc[s * size + y] = (uint8_t)u;
+    }
+}
+
+static inline void tamd_fse_blob(uint8_t* blob) {
+    static const int16_t ll[36] = {4, 3, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 1, 1, 1, 2, 2,
+                                   2, 2, 2, 2, 2, 2, 2, 3, 2, 1, 1, 1, 1, 1, -1, -1, -1, -1};
+    static const int16_t ml[53] = {1, 4, 3, 2, 2, 2, 2, 2, 2, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                                   1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+                                   1, 1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1, -1, -1};
+    static const int16_t of[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1,
+                                   1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
+    for (uint32_t i = 0; i < TAMD_FSE_BYTES; ++i) blob[i] = 0;
+    tamd_build_fse(ll, 36, 6, blob + TAMD_FSE_LL_ENC, blob + TAMD_FSE_LL_DEC);
+    tamd_build_fse(ml, 53, 6, blob + TAMD_FSE_ML_ENC, blob + TAMD_FSE_ML_DEC);
+    tamd_build_fse(of, 29, 5, blob + TAMD_FSE_OF_ENC, blob + TAMD_FSE_OF_DEC);
+}

@@ -24,7 +24,7 @@ public:
     }
     void pop_front(size_t k) {
         if (k > n_) k = n_;
-        for (size_t i = 0; i < k; ++i) buf_[(head_ + i) & mask_] = T();
+        // (popped slots keep stale contents: push_back and push_slot rewrite every field)
         head_ = (head_ + k) & mask_;
         n_ -= k;
     }

@@ -10,6 +10,9 @@ mkdir -p "$OUT" && cd "$R" && make -C tools > "$OUT/tools_build.log" 2>&1 &&
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$OUT/gpu_tests.log" 2>&1 &&
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1 &&
 timeout -k 10 900 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" &&
+timeout -k 10 300 python bench.py --workload cfg2 --no-cpu-baseline --no-end-to-end > "$OUT/bench_cfg2.json" 2> "$OUT/bench_cfg2.err" &&
+timeout -k 10 300 python bench.py --workload cfg1 > "$OUT/bench_cfg1.json" 2> "$OUT/bench_cfg1.err" &&
+timeout -k 10 300 python bench.py --workload cfg4 > "$OUT/bench_cfg4.json" 2> "$OUT/bench_cfg4.err" &&
 cd /tmp && export TMPDIR=/tmp &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$TAG" -o run -- python3 "$R/bench.py" --no-cpu-baseline --no-end-to-end > "$OUT/bench_prof.json" 2> "$OUT/bench_prof.err" &&
 python3 "$R/tools/trace_region.py" "$OUT/prof_$TAG/run_kernel_trace.csv" > "$OUT/trace_region_$TAG.json" &&
