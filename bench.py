@@ -216,6 +216,104 @@ def single_stream(name: str, device: int, step: int, reps: int = 3) -> dict:
     return out
 
 
+def compress_messages(n_streams: int, n_msgs: int, seed: int = 7):
+    """Synthetic reliable-message streams for the compression step: per stream, messages of
+    64..1300 bytes mixing word runs (compressible), random bytes (not) and repeats of earlier
+    stretches within the 24 KB history.  Returns (uint8 [streams, stride], lengths)."""
+    import numpy as np
+    rng = np.random.default_rng(seed)
+    words = [b"siamese ", b"tonk ", b"packet ", b"recovery ", b"window ", b"lane ", b"sum ", b"ack ",
+             b"datagram ", b"stream ", b"0x1f ", b"42 "]
+    text = np.frombuffer(b"".join(words[i] for i in rng.integers(0, len(words), 400000)), dtype=np.uint8)
+    lens = rng.integers(64, 1301, size=(n_streams, n_msgs)).astype(np.uint32)
+    kinds = rng.integers(0, 4, size=(n_streams, n_msgs))
+    stride = int(lens.sum(axis=1).max()) + 64
+    data = np.zeros((n_streams, stride), dtype=np.uint8)
+    noise = rng.integers(0, 256, 1 << 20, dtype=np.uint8)
+    for s in range(n_streams):
+        pos = 0
+        for k in range(n_msgs):
+            n = int(lens[s, k])
+            kind = int(kinds[s, k])
+            if kind == 3 and pos > 4096:
+                src = pos - int(rng.integers(n, min(pos, 20000) + 1))
+                data[s, pos:pos + n] = data[s, src:src + n]
+            elif kind == 0:
+                o = int(rng.integers(0, len(noise) - n))
+                data[s, pos:pos + n] = noise[o:o + n]
+            else:
+                o = int(rng.integers(0, len(text) - n))
+                data[s, pos:pos + n] = text[o:o + n]
+            pos += n
+    return data, lens.reshape(-1).tolist(), stride
+
+
+def compress_bench(device: int, steps: int, warmup: int, cpu: bool) -> dict:
+    """`--workload compress`: SURVEY s8(f)4, Tonk's MessageCompressor (PacketCompression.h:92)
+    on 64 streams x 1024 messages per step, device resident; the reference compressor (zstd level
+    1 over the same ring, oracle/_ref/libmsgcodec_ref.so) on 16 host threads beside it."""
+    import ctypes
+    import torch
+    from tonk_amd.compress import compress_batch
+    n_streams, n_msgs, max_bytes = 64, 1024, 1300
+    data, lens, stride = compress_messages(n_streams, n_msgs)
+    import numpy as np
+    lens_np = np.asarray(lens, dtype=np.uint32)
+    torch.cuda.set_device(device)
+    dev = torch.from_numpy(data).cuda()
+    out = torch.zeros(n_streams * n_msgs * max_bytes, dtype=torch.uint8, device="cuda")
+    in_bytes = float(sum(lens))
+    per_job = int(os.environ.get("TONK_AMD_LZ_JOB", "16"))  # consecutive messages per wave (A/B knob)
+    for _ in range(warmup):
+        compress_batch(dev.data_ptr(), stride, n_streams, n_msgs, lens_np, max_bytes, out.data_ptr(), per_job)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    kms = 0.0
+    written = []
+    for _ in range(steps):
+        written, ms = compress_batch(dev.data_ptr(), stride, n_streams, n_msgs, lens_np, max_bytes, out.data_ptr(),
+                                     per_job)
+        kms += ms
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    out_bytes = float(np.where(written > 0, written, lens_np).sum())
+    line = {
+        "metric": "Tonk MessageCompressor input GiB/s (device-resident, zstd-block compatible)",
+        "value": round(in_bytes * steps / (t1 - t0) / 2**30, 4), "unit": "GiB/s", "n_gpus": 1, "steps": steps,
+        "warmup": warmup, "ms_per_step": round((t1 - t0) * 1e3 / steps, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+        "config": {"workload": "64 streams x 1024 messages of 64-1300 B (word runs, random, repeats), max 1300",
+                   "streams": n_streams, "messages_per_stream": n_msgs, "messages_per_wave": per_job},
+        "ratio": round(in_bytes / out_bytes, 4),
+        "compressed_messages": int((written > 0).sum()),
+        "kernel": {"name": "tamd_lz_compress", "ms_per_step": round(kms / steps, 4),
+                   "input_gib_per_s": round(in_bytes * steps / (kms / 1e3) / 2**30, 4) if kms else None},
+        "cpu_baseline": None,
+    }
+    ref = os.path.join(ROOT, "oracle", "_ref", "libmsgcodec_ref.so")
+    if cpu and os.path.exists(ref):
+        L = ctypes.CDLL(ref)
+        L.ref_comp_bench.restype = ctypes.c_double
+        L.ref_comp_bench.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint, ctypes.c_uint,
+                                     ctypes.POINTER(ctypes.c_uint), ctypes.c_uint, ctypes.c_uint, ctypes.c_uint,
+                                     ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
+        threads = min(16, host_cpus())
+        arr = (ctypes.c_uint * len(lens))(*lens)
+        bi, bo = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        runs = []
+        for _ in range(3):
+            sec = L.ref_comp_bench(data.ctypes.data, stride, n_streams, n_msgs, arr, max_bytes, threads, 2,
+                                   ctypes.byref(bi), ctypes.byref(bo))
+            runs.append(in_bytes * 2 / sec / 2**30)
+        runs.sort()
+        line["cpu_baseline"] = {"value": round(runs[1], 4), "unit": "GiB/s", "cores": threads, "kind": "reference",
+                                "spread": [round(runs[0], 4), round(runs[-1], 4)],
+                                "ratio": round(bi.value / bo.value, 4) if bo.value else None,
+                                "sample": "the same 64 streams x 1024 messages, fresh compressors, 2 repetitions "
+                                          "per run, median of 3 runs"}
+    return line
+
+
 def stream_base(rank: int) -> int:
     """Weak scaling: rank r owns streams [64 r, 64 r + 64) -- disjoint, no data-path exchange."""
     return rank * STREAMS_PER_GPU
@@ -294,7 +392,7 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-end-to-end", action="store_true", help="skip the PCIe-inclusive side measurement")
-    ap.add_argument("--workload", choices=sorted(BATCHED) + sorted(SINGLE_STREAM), default="cfg3",
+    ap.add_argument("--workload", choices=sorted(BATCHED) + sorted(SINGLE_STREAM) + ["compress"], default="cfg3",
                     help="BASELINE.json configs[] index: cfg3 (the headline, 64 streams per GPU), cfg2 (64 "
                          "streams, 2%% loss), cfg1 / cfg4 (one stream, start to finish)")
     ap.add_argument("--step", type=int, default=0,
@@ -314,6 +412,14 @@ def main() -> int:
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+
+    if a.workload == "compress":  # SURVEY s8(f)4 side line (not the headline)
+        if world > 1:
+            print("bench.py: the compress workload runs on one GPU", file=sys.stderr)
+            return 2
+        print(json.dumps(compress_bench(local_rank, min(a.steps, 10), min(a.warmup, 2), not a.no_cpu_baseline)),
+              flush=True)
+        return 0
 
     if a.workload in SINGLE_STREAM:
         if world > 1:

@@ -31,8 +31,9 @@ int   tamd_compressor_compress(void* c, const uint8_t* data, unsigned bytes, uin
 void  tamd_compressor_destroy(void* c);
 
 /* The device-resident batch (bench.py --workload compress): n_streams independent compressor
-   streams, stream s's messages back to back at dev_data + s * stride (device memory), message k of
-   stream s is lens[s * n_msgs + k] bytes (1..max_bytes).  Every stream starts fresh (history
+   streams, stream s's messages back to back at dev_data + s * stride (device memory, with at
+   least 8 readable bytes after a stream's last message), message k of stream s is
+   lens[s * n_msgs + k] bytes (1..max_bytes).  Every stream starts fresh (history
    empty) and applies MessageCompressor's Allocate(max)/Commit ring rule.  Outputs: message
    (s, k) compressed at dev_out + (s * n_msgs + k) * max_bytes, written_host[s * n_msgs + k]
    (0: send uncompressed).  msgs_per_job consecutive messages of a stream share one wave's hash
@@ -40,6 +41,12 @@ void  tamd_compressor_destroy(void* c);
 int   tamd_compress_batch(const void* dev_data, uint64_t stride, uint32_t n_streams, uint32_t n_msgs,
                           const uint32_t* lens, uint32_t max_bytes, void* dev_out, uint32_t* written_host,
                           uint32_t msgs_per_job, float* kernel_ms);
+
+/* The same batch from host memory: host_data is copied to the device first and the compressed
+   messages come back to host_out (n_streams * n_msgs * max_bytes bytes). */
+int   tamd_compress_batch_host(const void* host_data, uint64_t stride, uint32_t n_streams, uint32_t n_msgs,
+                               const uint32_t* lens, uint32_t max_bytes, void* host_out, uint32_t* written_host,
+                               uint32_t msgs_per_job, float* kernel_ms);
 
 #ifdef __cplusplus
 }

@@ -3,6 +3,8 @@
 # sources under REF, twice:
 #   _ref/tonk/unit_tests_ref : with the reference Siamese codec (gf256/siamese/Siamese*.cpp)
 #   _ref/tonk/unit_tests_amd : the same Tonk objects, the codec replaced by libtonk_amd.so
+#   _ref/tonk/unit_tests_amd_lz : and the compressor too: PacketCompression.cpp replaced by
+#                                 integration/tonk/PacketCompressionAmd.cpp
 # Nothing is copied into the repository; outputs go to oracle/_ref/ (git-ignored).
 #
 #   make -C oracle -f tonk.mk -j8
@@ -35,7 +37,7 @@ obj = $(OUT)/obj/$(subst /,_,$(1)).o
 TONK_OBJS  := $(foreach f,$(TONK_CPP) $(TONK_C) $(TEST_CPP),$(call obj,$(f)))
 CODEC_OBJS := $(foreach f,$(CODEC_CPP),$(call obj,$(f)))
 
-all: $(OUT)/unit_tests_ref $(OUT)/unit_tests_amd
+all: $(OUT)/unit_tests_ref $(OUT)/unit_tests_amd $(OUT)/unit_tests_amd_lz
 
 define compile_rule
 $(call obj,$(1)): $(REF)/$(1)
@@ -50,5 +52,14 @@ $(OUT)/unit_tests_ref: $(TONK_OBJS) $(CODEC_OBJS)
 
 $(OUT)/unit_tests_amd: $(TONK_OBJS) ../tonk_amd/libtonk_amd.so
 	$(CXX) -o $@ $(TONK_OBJS) -L../tonk_amd -ltonk_amd -Wl,-rpath,'$$ORIGIN/../../../tonk_amd' -lpthread -ldl
+
+LZ_SHIM := $(OUT)/obj/PacketCompressionAmd.o
+$(LZ_SHIM): ../integration/tonk/PacketCompressionAmd.cpp ../include/tonk_compress.h
+	@mkdir -p $(OUT)/obj
+	$(CXX) $(CXXFLAGS) $(LIB_DEFS) -c -o $@ $<
+
+$(OUT)/unit_tests_amd_lz: $(filter-out $(call obj,PacketCompression.cpp),$(TONK_OBJS)) $(LZ_SHIM) ../tonk_amd/libtonk_amd.so
+	$(CXX) -o $@ $(filter-out $(call obj,PacketCompression.cpp),$(TONK_OBJS)) $(LZ_SHIM) -L../tonk_amd -ltonk_amd \
+	    -Wl,-rpath,'$$ORIGIN/../../../tonk_amd' -lpthread -ldl
 
 .PHONY: all

@@ -32,6 +32,22 @@ int main(int argc, char** argv) {
     const unsigned kMax = 1300, kDict = 24000;
     uint8_t fse[TAMD_FSE_BYTES];
     tamd_fse_blob(fse);
+    {  // the kernel's packed maps agree with the encoder/decoder tables the host writer uses
+        const uint16_t* e16 = (const uint16_t*)(fse + TAMD_FSE_E16);
+        const struct { uint32_t enc, dec, e, nsym, size; } t[3] = {
+            {TAMD_FSE_LL_ENC, TAMD_FSE_LL_DEC, TAMD_FSE_LL_E16, 36, 64},
+            {TAMD_FSE_ML_ENC, TAMD_FSE_ML_DEC, TAMD_FSE_ML_E16, 53, 64},
+            {TAMD_FSE_OF_ENC, TAMD_FSE_OF_DEC, TAMD_FSE_OF_E16, 29, 32}};
+        for (const auto& c : t)
+            for (uint32_t sy = 0; sy < c.nsym; ++sy)
+                for (uint32_t y = 0; y < c.size; ++y) {
+                    const uint32_t u = fse[c.enc + sy * c.size + y], w = e16[c.e + sy * c.size + y];
+                    if ((w & 63u) != u || ((w >> 6) & 15u) != fse[c.dec + 2 * u] || (w >> 10) != y - fse[c.dec + 2 * u + 1]) {
+                        printf("packed FSE map differs (symbol %u, state %u)\n", sy, y);
+                        return 1;
+                    }
+                }
+    }
     // a stream of messages: words from a small vocabulary, random bytes, repeats of old messages
     std::vector<uint8_t> stream;
     std::vector<unsigned> lens;

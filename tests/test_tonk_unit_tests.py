@@ -1,8 +1,10 @@
 """Tonk's own unit_tests (tests/TonkUnitTest.cpp of the reference: sender bandwidth control,
 lossy full-duplex transfers under the Mau simulator with memcmp checks, compression, time sync)
-built from the reference sources with the Siamese codec replaced by libtonk_amd.so
-(oracle/tonk.mk -> oracle/_ref/tonk/unit_tests_amd).  Tonk's sources are linked unchanged: this is
-the drop-in check of SURVEY.md s8(f)1."""
+built from the reference sources with the Siamese codec replaced by libtonk_amd.so and
+PacketCompression.cpp by integration/tonk/PacketCompressionAmd.cpp (the GPU MessageCompressor)
+(oracle/tonk.mk -> oracle/_ref/tonk/unit_tests_amd_lz).  Tonk's sources are linked unchanged: this
+is the drop-in check of SURVEY.md s8(f)1 and s8(f)4 (TestCompression, TonkUnitTest.cpp:599).
+unit_tests_amd (the codec alone) is built beside it for diagnosis."""
 from __future__ import annotations
 
 import os
@@ -12,12 +14,12 @@ import pytest
 
 from conftest import ROOT
 
-EXE = os.path.join(ROOT, "oracle", "_ref", "tonk", "unit_tests_amd")
+EXE = os.path.join(ROOT, "oracle", "_ref", "tonk", os.environ.get("TONK_AMD_TONK_BINARY", "unit_tests_amd_lz"))
 
 
 @pytest.mark.gpu
 @pytest.mark.timeout(840)
-def test_tonk_unit_tests_with_mi355x_codec():
+def test_tonk_unit_tests_with_mi355x_codec_and_compressor():
     if not os.path.exists(EXE):
         pytest.skip("oracle/_ref/tonk/unit_tests_amd not built (needs /root/reference at build time)")
     # the C ABI watchdog prints call/wait counts to stderr every 5 s (Tonk's own log is buffered)

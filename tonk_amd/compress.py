@@ -30,6 +30,9 @@ def _lib() -> ctypes.CDLL:
         L.tamd_compress_batch.restype = ctypes.c_int
         L.tamd_compress_batch.argtypes = [vp, u64, u32, u32, ctypes.POINTER(u32), u32, vp, ctypes.POINTER(u32), u32,
                                           ctypes.POINTER(ctypes.c_float)]
+        L.tamd_compress_batch_host.restype = ctypes.c_int
+        L.tamd_compress_batch_host.argtypes = [vp, u64, u32, u32, ctypes.POINTER(u32), u32, vp, ctypes.POINTER(u32),
+                                               u32, ctypes.POINTER(ctypes.c_float)]
         _bound = True
     return L
 
@@ -61,15 +64,36 @@ class MessageCompressor:
 
 
 def compress_batch(dev_data: int, stride: int, n_streams: int, n_msgs: int, lens, max_bytes: int, dev_out: int,
-                   msgs_per_job: int = 16) -> tuple[list[int], float]:
+                   msgs_per_job: int = 16):
     """Compress every message of `n_streams` fresh streams (device pointers from the caller, e.g.
-    torch tensors' data_ptr()).  Returns (written bytes per message, 0 = uncompressed; kernel ms)."""
+    torch tensors' data_ptr()).  `lens`: uint32 per message (any sequence; a contiguous numpy
+    uint32 array is passed without a copy).  Returns (written bytes per message as a numpy array,
+    0 = uncompressed; kernel ms)."""
+    import numpy as np
+    total = n_streams * n_msgs
+    L = np.ascontiguousarray(lens, dtype=np.uint32)
+    W = np.zeros(total, dtype=np.uint32)
+    ms = ctypes.c_float(0.0)
+    u32p = ctypes.POINTER(ctypes.c_uint32)
+    rc = _lib().tamd_compress_batch(dev_data, stride, n_streams, n_msgs, L.ctypes.data_as(u32p), max_bytes, dev_out,
+                                    W.ctypes.data_as(u32p), msgs_per_job, ctypes.byref(ms))
+    if rc != 0:
+        raise RuntimeError(f"tonk_amd: compress_batch failed (rc={rc})")
+    return W, ms.value
+
+
+def compress_batch_host(data, stride: int, n_streams: int, n_msgs: int, lens, max_bytes: int,
+                        msgs_per_job: int = 16) -> tuple[bytes, list[int], float]:
+    """compress_batch from a host buffer (bytes-like of n_streams * stride): returns (the output
+    slots, max_bytes per message; written per message; kernel ms)."""
     total = n_streams * n_msgs
     L = (ctypes.c_uint32 * total)(*lens)
     W = (ctypes.c_uint32 * total)()
+    src = ctypes.create_string_buffer(bytes(data), n_streams * stride)
+    out = ctypes.create_string_buffer(total * max_bytes)
     ms = ctypes.c_float(0.0)
-    rc = _lib().tamd_compress_batch(dev_data, stride, n_streams, n_msgs, L, max_bytes, dev_out, W, msgs_per_job,
-                                    ctypes.byref(ms))
+    rc = _lib().tamd_compress_batch_host(src, stride, n_streams, n_msgs, L, max_bytes, out, W, msgs_per_job,
+                                         ctypes.byref(ms))
     if rc != 0:
-        raise RuntimeError(f"tonk_amd: compress_batch failed (rc={rc})")
-    return list(W), ms.value
+        raise RuntimeError(f"tonk_amd: compress_batch_host failed (rc={rc})")
+    return out.raw, list(W), ms.value

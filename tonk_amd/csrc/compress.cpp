@@ -8,12 +8,13 @@
 #include <hip/hip_ext.h>
 
 #include <mutex>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <vector>
 
 extern "C" __global__ void tamd_lz_compress(const tamd_lz_job*, const tamd_lz_msg*, const uint8_t*, uint8_t*,
-                                            uint32_t*);
+                                            uint32_t*, unsigned long long*);
 
 namespace tamd {
 namespace {
@@ -107,6 +108,7 @@ struct Compressor {
 };
 
 static const uint32_t kRing = 1u << 16;
+static const uint32_t kMirror = 64;  // the ring's first bytes repeated after it (wide loads at its end)
 // pinned staging of the per-message path: [message | descriptor | written | compressed block]
 static size_t stage_msg(uint32_t max) { return ((size_t)max + 63u) & ~(size_t)63u; }
 static size_t stage_written(uint32_t max) { return stage_msg(max) + 64u; }
@@ -126,7 +128,7 @@ extern "C" void* tamd_compressor_create(unsigned max_bytes) {
     hipGetDevice(&c->device);
     bool ok = (c->fse = device_fse(c->device)) != nullptr;
     ok = ok && hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
-    ok = ok && hipMalloc((void**)&c->ring, kRing) == hipSuccess;
+    ok = ok && hipMalloc((void**)&c->ring, kRing + kMirror) == hipSuccess;
     ok = ok && hipMalloc((void**)&c->d_job, sizeof(tamd_lz_job)) == hipSuccess;
     ok = ok && hipMalloc((void**)&c->d_msg, sizeof(tamd_lz_msg)) == hipSuccess;
     ok = ok && hipMalloc((void**)&c->d_out, max_bytes + 64) == hipSuccess;
@@ -188,10 +190,21 @@ extern "C" int tamd_compressor_compress(void* cp, const uint8_t* data, unsigned 
     if (first < bytes)
         ok = ok && hipMemcpyAsync(c->ring, c->h_stage + first, bytes - first, hipMemcpyHostToDevice, c->stream) ==
                        hipSuccess;
+    // ring bytes [0, kMirror) also live at [kRing, kRing + kMirror)
+    if (first < bytes) {
+        const uint32_t k = bytes - first < kMirror ? bytes - first : kMirror;
+        ok = ok && hipMemcpyAsync(c->ring + kRing, c->h_stage + first, k, hipMemcpyHostToDevice, c->stream) ==
+                       hipSuccess;
+    }
+    if (slot < kMirror) {
+        const uint32_t k = (kMirror - slot) < first ? kMirror - slot : first;
+        ok = ok && hipMemcpyAsync(c->ring + kRing + slot, c->h_stage, k, hipMemcpyHostToDevice, c->stream) ==
+                       hipSuccess;
+    }
     ok = ok && hipMemcpyAsync(c->d_msg, &m, sizeof(m), hipMemcpyHostToDevice, c->stream) == hipSuccess;
     if (ok) {
         hipLaunchKernelGGL(tamd_lz_compress, dim3(1), dim3(64), 0, c->stream, c->d_job, c->d_msg, c->fse, c->d_out,
-                           c->d_written);
+                           c->d_written, (unsigned long long*)nullptr);
         ok = hipGetLastError() == hipSuccess;
     }
     uint32_t* h_written = (uint32_t*)(c->h_stage + stage_written(c->max));
@@ -237,7 +250,7 @@ extern "C" int tamd_compress_batch(const void* dev_data, uint64_t stride, uint32
             if (n == 0 || n > max_bytes) return -1;
             uint64_t pos = 0, win = 0;
             rt.place(n, &pos, &win);
-            if (pos + n > stride) return -1;
+            if (pos + n + 8 > stride) return -1;  // (8 readable bytes past the last message)
             tamd_lz_msg& m = msgs[(uint64_t)s * n_msgs + k];
             memset(&m, 0, sizeof(m));
             m.pos = (uint32_t)pos;
@@ -258,24 +271,59 @@ extern "C" int tamd_compress_batch(const void* dev_data, uint64_t stride, uint32
     }
     if (total * max_bytes > 0xffffffffull) return -1;  // output offsets are 32-bit
     for (uint64_t i = 0; i < total; ++i) msgs[i].out = (uint32_t)(i * max_bytes);
-    hipStream_t st = nullptr;
-    tamd_lz_job* d_jobs = nullptr;
-    tamd_lz_msg* d_msgs = nullptr;
-    uint32_t* d_written = nullptr;
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    bool ok = hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess;
-    ok = ok && hipMalloc((void**)&d_jobs, jobs.size() * sizeof(tamd_lz_job)) == hipSuccess;
-    ok = ok && hipMalloc((void**)&d_msgs, total * sizeof(tamd_lz_msg)) == hipSuccess;
-    ok = ok && hipMalloc((void**)&d_written, total * 4) == hipSuccess;
-    ok = ok && hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess;
+    // persistent launch state (grown on demand): stream, descriptor and result buffers, events
+    static std::mutex mu;
+    static hipStream_t st = nullptr;
+    static tamd_lz_job* d_jobs = nullptr;
+    static tamd_lz_msg* d_msgs = nullptr;
+    static uint32_t* d_written = nullptr;
+    static size_t cap_jobs = 0, cap_msgs = 0;
+    static hipEvent_t e0 = nullptr, e1 = nullptr;
+    std::lock_guard<std::mutex> g(mu);
+    bool ok = true;
+    if (!st) ok = hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess &&
+                  hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess;
+    if (ok && jobs.size() > cap_jobs) {
+        if (d_jobs) hipFree(d_jobs);
+        d_jobs = nullptr;
+        cap_jobs = jobs.size() + jobs.size() / 2;
+        ok = hipMalloc((void**)&d_jobs, cap_jobs * sizeof(tamd_lz_job)) == hipSuccess;
+        if (!ok) cap_jobs = 0;
+    }
+    if (ok && total > cap_msgs) {
+        if (d_msgs) hipFree(d_msgs);
+        if (d_written) hipFree(d_written);
+        d_msgs = nullptr;
+        d_written = nullptr;
+        cap_msgs = total + total / 2;
+        ok = hipMalloc((void**)&d_msgs, cap_msgs * sizeof(tamd_lz_msg)) == hipSuccess &&
+             hipMalloc((void**)&d_written, cap_msgs * 4) == hipSuccess;
+        if (!ok) cap_msgs = 0;
+    }
     ok = ok && hipMemcpyAsync(d_jobs, jobs.data(), jobs.size() * sizeof(tamd_lz_job), hipMemcpyHostToDevice, st) ==
                    hipSuccess;
     ok = ok && hipMemcpyAsync(d_msgs, msgs.data(), total * sizeof(tamd_lz_msg), hipMemcpyHostToDevice, st) ==
                    hipSuccess;
+    // profiling only: TONK_AMD_LZ_PROF=1 prints the phase totals of the launch (lz.hip LZ_PHASE)
+    static const bool prof_on = getenv("TONK_AMD_LZ_PROF") != nullptr;
+    unsigned long long* d_prof = nullptr;
+    if (ok && prof_on) ok = hipMalloc((void**)&d_prof, jobs.size() * 5 * 8) == hipSuccess;
     if (ok) {
         hipExtLaunchKernelGGL(tamd_lz_compress, dim3((uint32_t)jobs.size()), dim3(64), 0, st, e0, e1, 0, d_jobs,
-                              d_msgs, fse, (uint8_t*)dev_out, d_written);
+                              d_msgs, fse, (uint8_t*)dev_out, d_written, d_prof);
         ok = hipGetLastError() == hipSuccess;
+    }
+    if (ok && d_prof) {
+        std::vector<unsigned long long> h(jobs.size() * 5);
+        ok = hipMemcpyAsync(h.data(), d_prof, h.size() * 8, hipMemcpyDeviceToHost, st) == hipSuccess &&
+             hipStreamSynchronize(st) == hipSuccess;
+        double t[5] = {0, 0, 0, 0, 0};
+        for (size_t j = 0; j < jobs.size(); ++j)
+            for (int k = 0; k < 5; ++k) t[k] += (double)h[5 * j + k];
+        fprintf(stderr, "lz phases (us per job): window %.1f probe %.1f parse %.1f fse %.1f out %.1f\n",
+                t[0] / jobs.size() / 100.0, t[1] / jobs.size() / 100.0, t[2] / jobs.size() / 100.0,
+                t[3] / jobs.size() / 100.0, t[4] / jobs.size() / 100.0);
+        hipFree(d_prof);
     }
     ok = ok && hipMemcpyAsync(written_host, d_written, total * 4, hipMemcpyDeviceToHost, st) == hipSuccess;
     ok = ok && hipStreamSynchronize(st) == hipSuccess;
@@ -284,11 +332,24 @@ extern "C" int tamd_compress_batch(const void* dev_data, uint64_t stride, uint32
         hipEventElapsedTime(&ms, e0, e1);
         *kernel_ms = ms;
     }
-    if (e0) hipEventDestroy(e0);
-    if (e1) hipEventDestroy(e1);
-    if (d_jobs) hipFree(d_jobs);
-    if (d_msgs) hipFree(d_msgs);
-    if (d_written) hipFree(d_written);
-    if (st) hipStreamDestroy(st);
     return ok ? 0 : -2;
+}
+
+extern "C" int tamd_compress_batch_host(const void* host_data, uint64_t stride, uint32_t n_streams, uint32_t n_msgs,
+                                        const uint32_t* lens, uint32_t max_bytes, void* host_out,
+                                        uint32_t* written_host, uint32_t msgs_per_job, float* kernel_ms) {
+    if (!host_data || !host_out || !n_streams || !n_msgs || !max_bytes) return -1;
+    if (!device_ok()) return -3;
+    const size_t in_bytes = (size_t)stride * n_streams, out_bytes = (size_t)n_streams * n_msgs * max_bytes;
+    void *d_in = nullptr, *d_out = nullptr;
+    int rc = -2;
+    if (hipMalloc(&d_in, in_bytes) == hipSuccess && hipMalloc(&d_out, out_bytes) == hipSuccess &&
+        hipMemcpy(d_in, host_data, in_bytes, hipMemcpyHostToDevice) == hipSuccess) {
+        rc = tamd_compress_batch(d_in, stride, n_streams, n_msgs, lens, max_bytes, d_out, written_host, msgs_per_job,
+                                 kernel_ms);
+        if (rc == 0 && hipMemcpy(host_out, d_out, out_bytes, hipMemcpyDeviceToHost) != hipSuccess) rc = -2;
+    }
+    if (d_in) hipFree(d_in);
+    if (d_out) hipFree(d_out);
+    return rc;
 }

@@ -219,21 +219,25 @@ bool Decoder::add_run_inorder(uint32_t col0, const RowId* rows, uint32_t k, uint
     // would repeat this answer without changing any state.
     if (head_ && (next_expected_ >= e0 || check_recovery_possible())) return false;
     grow_window(e0 + k);
-    for (uint32_t j = 0; j < k; ++j) {
-        const uint32_t e = e0 + j;
-        StoredOriginal& o = subs_[e / kSubwindow]->orig[e % kSubwindow];
-        if (o.row != kNoRow || o.host) drop_original(o);  // (slots past the window end are empty)
-        o.row = rows[j];
-        o.off = ctx_->rows.offset(rows[j]);
-        o.bytes = framed_bytes;
-        o.column = col_add(col0, j);
-        o.header_bytes = (uint8_t)header_bytes;
-        o.owned = borrowed ? 0 : 1;
-    }
-    for (uint32_t e = e0; e < e0 + k;) {  // got bits, a subwindow at a time
+    const RowTable& rt = ctx_->rows;
+    const uint8_t owned = borrowed ? 0 : 1;
+    uint32_t column = col0;
+    const RowId* r = rows;
+    for (uint32_t e = e0; e < e0 + k;) {  // a subwindow at a time: slots, then got bits
         const uint32_t bit = e % kSubwindow;
         const uint32_t n = std::min(kSubwindow - bit, e0 + k - e);
         Subwindow* s = subs_[e / kSubwindow];
+        StoredOriginal* o = s->orig + bit;
+        for (uint32_t t = 0; t < n; ++t, ++o, ++r) {
+            if (o->row != kNoRow || o->host) drop_original(*o);  // (slots past the window end are empty)
+            o->row = *r;
+            o->off = rt.offset(*r);
+            o->bytes = framed_bytes;
+            o->column = column;
+            o->header_bytes = (uint8_t)header_bytes;
+            o->owned = owned;
+            column = col_inc(column);
+        }
         s->got |= (n == 64 ? ~0ull : ((1ull << n) - 1)) << bit;
         s->got_count += n;
         e += n;

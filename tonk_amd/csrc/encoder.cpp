@@ -66,8 +66,64 @@ bool Encoder::add_run(const RowId* rows, uint32_t k, uint32_t framed_bytes, uint
     *first_col = next_column_;
     uint32_t col = 0;
     const RowTable& rt = ctx_->rows;
-    for (uint32_t j = 0; j < k; ++j)
-        add_unchecked(rows[j], rt.offset(rows[j]), framed_bytes, header_bytes, payload_bytes, nullptr, &col, borrowed);
+    // the first add may start a window; the rest append to it (count_ > 0, element == count_)
+    add_unchecked(rows[0], rt.offset(rows[0]), framed_bytes, header_bytes, payload_bytes, nullptr, &col, borrowed);
+    if (k == 1) return true;
+    // k - 1 more appends, as add_unchecked would do them, with the window state in locals
+    uint32_t element = count_;
+    if (win_.size() != element) {  // (placeholder slots would be overwritten: the general path)
+        for (uint32_t j = 1; j < k; ++j)
+            add_unchecked(rows[j], rt.offset(rows[j]), framed_bytes, header_bytes, payload_bytes, nullptr, &col,
+                          borrowed);
+        return true;
+    }
+    win_.reserve_more(k - 1);
+    StoredOriginal* base = win_.slot_base();
+    const size_t mask = win_.slot_mask();
+    size_t idx = win_.slot_index(element - 1);
+    uint32_t prev_off = base[idx].off, prev_stride = base[idx].stride, prev_bytes = base[idx].bytes;
+    uint32_t prev_run = base[idx].run;
+    uint32_t column = next_column_;
+    const uint32_t now = (uint32_t)now_msec();
+    const uint8_t owned = borrowed ? 0 : 1;
+    for (uint32_t j = 1; j < k; ++j) {
+        idx = (idx + 1) & mask;
+        StoredOriginal& o = base[idx];
+        const uint32_t off = rt.offset(rows[j]);
+        uint32_t run = 1, stride = 0;
+        if (prev_bytes == framed_bytes && off > prev_off && prev_run < 0xffff &&
+            (prev_run == 1 || off - prev_off == prev_stride)) {
+            run = prev_run + 1;
+            stride = off - prev_off;
+        }
+        o.row = rows[j];
+        o.bytes = framed_bytes;
+        o.column = column;
+        o.send_msec = now;
+        o.off = off;
+        o.stride = stride;
+        o.run = (uint16_t)run;
+        o.header_bytes = (uint8_t)header_bytes;
+        o.owned = owned;
+        o.host = nullptr;
+        prev_off = off;
+        prev_stride = stride;
+        prev_bytes = framed_bytes;
+        prev_run = run;
+        column = col_inc(column);
+    }
+    win_.commit(k - 1);
+    count_ += k - 1;
+    next_column_ = column;
+    // every lane one of these columns fell on (all k - 1 have the same length)
+    const uint32_t first = col_inc(*first_col);
+    for (uint32_t j = 0; j < k - 1 && j < kLanes; ++j) {
+        Lane& lane = lanes_[(first + j) % kLanes];
+        if (lane.longest < framed_bytes) lane.longest = framed_bytes;
+    }
+    if (longest_ < framed_bytes) longest_ = framed_bytes;
+    stats_[0] += k - 1;
+    stats_[1] += (uint64_t)payload_bytes * (k - 1);
     return true;
 }
 

@@ -30,7 +30,14 @@ typedef struct tamd_lz_msg {
 #define TAMD_FSE_LL_DEC (TAMD_FSE_OF_ENC + 29u * 32u)
 #define TAMD_FSE_ML_DEC (TAMD_FSE_LL_DEC + 64u * 2u)
 #define TAMD_FSE_OF_DEC (TAMD_FSE_ML_DEC + 64u * 2u)
-#define TAMD_FSE_BYTES (TAMD_FSE_OF_DEC + 32u * 2u)
+// The same encoder maps with the decoding info folded in, one 16-bit word per (symbol, next
+// state): state | nbBits << 6 | (next state - base) << 10 (the kernel's chains read only these).
+#define TAMD_FSE_E16 (TAMD_FSE_OF_DEC + 32u * 2u)
+#define TAMD_FSE_LL_E16 0u  // (word offsets inside the E16 section)
+#define TAMD_FSE_ML_E16 (36u * 64u)
+#define TAMD_FSE_OF_E16 (TAMD_FSE_ML_E16 + 53u * 64u)
+#define TAMD_FSE_E16_WORDS (TAMD_FSE_OF_E16 + 29u * 32u)
+#define TAMD_FSE_BYTES (TAMD_FSE_E16 + 2u * TAMD_FSE_E16_WORDS)
 
 #ifdef __HIPCC__
 #define TAMD_HD __host__ __device__
@@ -94,39 +101,52 @@ TAMD_HD static inline uint32_t tamd_ml_code(uint32_t ml) {  // ml >= 3
     return 36 + (31 - (uint32_t)__builtin_clz(ml - 3));  // 131-258: 43, 259-514: 44, ...
 }
 
-// Literals section header of raw literals (RFC 8878 s3.1.1.3.1.1): 1, 2 or 3 bytes.
-TAMD_HD static inline uint32_t tamd_lits_header(uint32_t lits, uint8_t* h) {
+// Literals section header of raw literals (RFC 8878 s3.1.1.3.1.1): 1, 2 or 3 bytes, packed
+// little-endian into a word (*len bytes).
+TAMD_HD static inline uint32_t tamd_lits_header_word(uint32_t lits, uint32_t* len) {
     if (lits < 32) {
-        h[0] = (uint8_t)(lits << 3);
-        return 1;
+        *len = 1;
+        return lits << 3;
     }
     if (lits < 4096) {
-        h[0] = (uint8_t)(0x04u | ((lits & 15u) << 4));
-        h[1] = (uint8_t)(lits >> 4);
-        return 2;
+        *len = 2;
+        return 0x04u | ((lits & 15u) << 4) | ((lits >> 4) << 8);
     }
-    h[0] = (uint8_t)(0x0cu | ((lits & 15u) << 4));
-    h[1] = (uint8_t)(lits >> 4);
-    h[2] = (uint8_t)(lits >> 12);
-    return 3;
+    *len = 3;
+    return 0x0cu | ((lits & 15u) << 4) | (((lits >> 4) & 0xffu) << 8) | ((lits >> 12) << 16);
 }
 
 // Sequences section header (s3.1.1.3.2.1): the count, then the modes byte (0: the predefined
-// distributions for all three codes) when there are sequences.
-TAMD_HD static inline uint32_t tamd_seq_header(uint32_t n, uint8_t* h) {
-    uint32_t w = 0;
-    if (n < 128) {
-        h[w++] = (uint8_t)n;
-    } else if (n < 0x7f00) {
-        h[w++] = (uint8_t)(0x80u + (n >> 8));
-        h[w++] = (uint8_t)n;
-    } else {
-        h[w++] = 0xff;
-        h[w++] = (uint8_t)(n - 0x7f00u);
-        h[w++] = (uint8_t)((n - 0x7f00u) >> 8);
+// distributions for all three codes) when there are sequences; packed like the above.
+TAMD_HD static inline uint32_t tamd_seq_header_word(uint32_t n, uint32_t* len) {
+    if (n == 0) {
+        *len = 1;
+        return 0;
     }
-    if (n) h[w++] = 0;
-    return w;
+    if (n < 128) {
+        *len = 2;
+        return n;
+    }
+    if (n < 0x7f00) {
+        *len = 3;
+        return (0x80u + (n >> 8)) | ((n & 0xffu) << 8);
+    }
+    *len = 4;
+    return 0xffu | (((n - 0x7f00u) & 0xffu) << 8) | (((n - 0x7f00u) >> 8) << 16);
+}
+
+TAMD_HD static inline uint32_t tamd_lits_header(uint32_t lits, uint8_t* h) {
+    uint32_t len = 0;
+    const uint32_t w = tamd_lits_header_word(lits, &len);
+    for (uint32_t k = 0; k < len; ++k) h[k] = (uint8_t)(w >> (8 * k));
+    return len;
+}
+
+TAMD_HD static inline uint32_t tamd_seq_header(uint32_t n, uint8_t* h) {
+    uint32_t len = 0;
+    const uint32_t w = tamd_seq_header_word(n, &len);
+    for (uint32_t k = 0; k < len; ++k) h[k] = (uint8_t)(w >> (8 * k));
+    return len;
 }
 
 // The sequences' bit stream (s3.1.1.3.2.2 / 4.1): written forward here, read backward by the
@@ -201,7 +221,8 @@ TAMD_HD static inline uint32_t tamd_fse_sequences(const uint32_t* seq_lo, const 
 // (fse_decompress.c:93-148 restated: probability -1 symbols at the top, the others spread with
 // step 5/8 of the table + 3, then per state its bit count and next-state base); the encoder's map
 // inverts it: for a symbol and the state the decoder must reach next, the state to be in now.
-static inline void tamd_build_fse(const int16_t* norm, uint32_t nsym, uint32_t log, uint8_t* enc, uint8_t* dec) {
+static inline void tamd_build_fse(const int16_t* norm, uint32_t nsym, uint32_t log, uint8_t* enc, uint8_t* dec,
+                                  uint16_t* e16) {
     const uint32_t size = 1u << log;
     uint32_t sym[64], next[64];
     uint32_t high = size - 1;
@@ -228,7 +249,10 @@ static inline void tamd_build_fse(const int16_t* norm, uint32_t nsym, uint32_t l
         const uint32_t base = (ns << nb) - size;
         dec[2 * u] = (uint8_t)nb;
         dec[2 * u + 1] = (uint8_t)base;
-        for (uint32_t y = base; y < base + (1u << nb); ++y) enc[s * size + y] = (uint8_t)u;
+        for (uint32_t y = base; y < base + (1u << nb); ++y) {
+            enc[s * size + y] = (uint8_t)u;
+            e16[s * size + y] = (uint16_t)(u | (nb << 6) | ((y - base) << 10));
+        }
     }
 }
 
@@ -241,7 +265,8 @@ static inline void tamd_fse_blob(uint8_t* blob) {
     static const int16_t of[29] = {1, 1, 1, 1, 1, 1, 2, 2, 2, 1, 1, 1, 1, 1, 1,
                                    1, 1, 1, 1, 1, 1, 1, 1, 1, -1, -1, -1, -1, -1};
     for (uint32_t i = 0; i < TAMD_FSE_BYTES; ++i) blob[i] = 0;
-    tamd_build_fse(ll, 36, 6, blob + TAMD_FSE_LL_ENC, blob + TAMD_FSE_LL_DEC);
-    tamd_build_fse(ml, 53, 6, blob + TAMD_FSE_ML_ENC, blob + TAMD_FSE_ML_DEC);
-    tamd_build_fse(of, 29, 5, blob + TAMD_FSE_OF_ENC, blob + TAMD_FSE_OF_DEC);
+    uint16_t* e16 = (uint16_t*)(blob + TAMD_FSE_E16);
+    tamd_build_fse(ll, 36, 6, blob + TAMD_FSE_LL_ENC, blob + TAMD_FSE_LL_DEC, e16 + TAMD_FSE_LL_E16);
+    tamd_build_fse(ml, 53, 6, blob + TAMD_FSE_ML_ENC, blob + TAMD_FSE_ML_DEC, e16 + TAMD_FSE_ML_E16);
+    tamd_build_fse(of, 29, 5, blob + TAMD_FSE_OF_ENC, blob + TAMD_FSE_OF_DEC, e16 + TAMD_FSE_OF_E16);
 }

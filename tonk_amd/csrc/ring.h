@@ -16,6 +16,14 @@ public:
         buf_[(head_ + n_) & mask_] = v;
         ++n_;
     }
+    // Bulk append: make room for k more, fill slot(n + j) for j < k, then commit(k).
+    void reserve_more(size_t k) {
+        while (n_ + k > buf_.size()) grow();
+    }
+    T* slot_base() { return buf_.data(); }
+    size_t slot_index(size_t i) const { return (head_ + i) & mask_; }
+    size_t slot_mask() const { return mask_; }
+    void commit(size_t k) { n_ += k; }
     // Append a slot to fill in place (no temporary: a struct built in narrow fields and then
     // copied with wide loads stalls on store forwarding).
     T& push_slot() {
