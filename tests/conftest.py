@@ -28,7 +28,11 @@ def pytest_configure(config):
 
 
 def _make(path: str, *targets: str) -> None:
-    subprocess.run(["make", "-C", path, "-j8", *targets], check=True, stdout=subprocess.DEVNULL)
+    # one build at a time across pytest-xdist workers (targets share objects)
+    import fcntl
+    with open(os.path.join(ROOT, ".build.lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        subprocess.run(["make", "-C", path, "-j8", *targets], check=True, stdout=subprocess.DEVNULL)
 
 
 @pytest.fixture(scope="session")
