@@ -95,7 +95,6 @@ struct RingTrack {
 struct Compressor {
     uint32_t max = 0;
     int device = 0;
-    hipStream_t stream = nullptr;
     const uint8_t* fse = nullptr;
     uint8_t* ring = nullptr;  // 64 KB device ring of the stream's bytes (linear position & 0xffff)
     tamd_lz_job* d_job = nullptr;
@@ -119,6 +118,40 @@ static size_t stage_bytes(uint32_t max) { return stage_out(max) + max + 64u; }
 
 using namespace tamd;
 
+// Every compressor of the process enqueues on one stream (each call is a synchronous round trip);
+// Tonk creates a compressor per connection, most of which may never compress, so a compressor's
+// device buffers are made on its first message.
+static std::mutex g_lz_mu;
+static hipStream_t g_lz_stream = nullptr;
+
+static bool ensure_device(Compressor* c) {
+    if (c->ring) return true;
+    bool ok = (c->fse = device_fse(c->device)) != nullptr;
+    if (ok && !g_lz_stream) ok = hipStreamCreateWithFlags(&g_lz_stream, hipStreamNonBlocking) == hipSuccess;
+    ok = ok && hipMalloc((void**)&c->d_job, sizeof(tamd_lz_job)) == hipSuccess;
+    ok = ok && hipMalloc((void**)&c->d_msg, sizeof(tamd_lz_msg)) == hipSuccess;
+    ok = ok && hipMalloc((void**)&c->d_out, c->max + 64) == hipSuccess;
+    ok = ok && hipMalloc((void**)&c->d_written, 64) == hipSuccess;
+    ok = ok && hipHostMalloc((void**)&c->h_stage, stage_bytes(c->max), hipHostMallocDefault) == hipSuccess;
+    uint8_t* ring = nullptr;
+    ok = ok && hipMalloc((void**)&ring, kRing + kMirror) == hipSuccess;
+    if (ok) {
+        tamd_lz_job job;
+        memset(&job, 0, sizeof(job));
+        job.buf = ring;
+        job.mask = kRing - 1;
+        job.first = 0;
+        job.count = 1;
+        ok = hipMemcpy(c->d_job, &job, sizeof(job), hipMemcpyHostToDevice) == hipSuccess;
+    }
+    if (!ok) {
+        if (ring) hipFree(ring);
+        return false;
+    }
+    c->ring = ring;
+    return true;
+}
+
 extern "C" void* tamd_compressor_create(unsigned max_bytes) {
     if (max_bytes == 0 || max_bytes + max_bytes > kRing || max_bytes > kDictBytes) return nullptr;
     if (!device_ok()) return nullptr;
@@ -126,42 +159,21 @@ extern "C" void* tamd_compressor_create(unsigned max_bytes) {
     c->max = max_bytes;
     c->ring_track.max = max_bytes;
     hipGetDevice(&c->device);
-    bool ok = (c->fse = device_fse(c->device)) != nullptr;
-    ok = ok && hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) == hipSuccess;
-    ok = ok && hipMalloc((void**)&c->ring, kRing + kMirror) == hipSuccess;
-    ok = ok && hipMalloc((void**)&c->d_job, sizeof(tamd_lz_job)) == hipSuccess;
-    ok = ok && hipMalloc((void**)&c->d_msg, sizeof(tamd_lz_msg)) == hipSuccess;
-    ok = ok && hipMalloc((void**)&c->d_out, max_bytes + 64) == hipSuccess;
-    ok = ok && hipMalloc((void**)&c->d_written, 64) == hipSuccess;
-    ok = ok && hipHostMalloc((void**)&c->h_stage, stage_bytes(max_bytes), hipHostMallocDefault) == hipSuccess;
-    if (!ok) {
-        tamd_compressor_destroy(c);
-        return nullptr;
-    }
-    tamd_lz_job job;
-    memset(&job, 0, sizeof(job));
-    job.buf = c->ring;
-    job.mask = kRing - 1;
-    job.first = 0;
-    job.count = 1;
-    if (hipMemcpy(c->d_job, &job, sizeof(job), hipMemcpyHostToDevice) != hipSuccess) {
-        tamd_compressor_destroy(c);
-        return nullptr;
-    }
     return c;
 }
 
 extern "C" void tamd_compressor_destroy(void* cp) {
     Compressor* c = (Compressor*)cp;
     if (!c) return;
-    if (c->stream) hipStreamSynchronize(c->stream);
+    {
+        std::lock_guard<std::mutex> g(g_lz_mu);  // (no call of this compressor is in flight)
+    }
     if (c->ring) hipFree(c->ring);
     if (c->d_job) hipFree(c->d_job);
     if (c->d_msg) hipFree(c->d_msg);
     if (c->d_out) hipFree(c->d_out);
     if (c->d_written) hipFree(c->d_written);
     if (c->h_stage) hipHostFree(c->h_stage);
-    if (c->stream) hipStreamDestroy(c->stream);
     delete c;
 }
 
@@ -171,6 +183,12 @@ extern "C" int tamd_compressor_compress(void* cp, const uint8_t* data, unsigned 
     if (written) *written = 0;
     if (!c || !data || !dest || !written || bytes == 0 || bytes > c->max) return -1;
     if (c->failed) return -2;
+    std::lock_guard<std::mutex> lock(g_lz_mu);
+    if (!ensure_device(c)) {
+        c->failed = true;
+        return -2;
+    }
+    hipStream_t const stream = g_lz_stream;
     uint64_t pos = 0, win = 0;
     c->ring_track.place(bytes, &pos, &win);
     // positions passed to the kernel are rebased to a multiple of the ring size below the window
@@ -186,32 +204,32 @@ extern "C" int tamd_compressor_compress(void* cp, const uint8_t* data, unsigned 
     memcpy(c->h_stage, data, bytes);
     const uint32_t slot = (uint32_t)(pos & (kRing - 1));
     const uint32_t first = bytes < kRing - slot ? bytes : kRing - slot;
-    bool ok = hipMemcpyAsync(c->ring + slot, c->h_stage, first, hipMemcpyHostToDevice, c->stream) == hipSuccess;
+    bool ok = hipMemcpyAsync(c->ring + slot, c->h_stage, first, hipMemcpyHostToDevice, stream) == hipSuccess;
     if (first < bytes)
-        ok = ok && hipMemcpyAsync(c->ring, c->h_stage + first, bytes - first, hipMemcpyHostToDevice, c->stream) ==
+        ok = ok && hipMemcpyAsync(c->ring, c->h_stage + first, bytes - first, hipMemcpyHostToDevice, stream) ==
                        hipSuccess;
     // ring bytes [0, kMirror) also live at [kRing, kRing + kMirror)
     if (first < bytes) {
         const uint32_t k = bytes - first < kMirror ? bytes - first : kMirror;
-        ok = ok && hipMemcpyAsync(c->ring + kRing, c->h_stage + first, k, hipMemcpyHostToDevice, c->stream) ==
+        ok = ok && hipMemcpyAsync(c->ring + kRing, c->h_stage + first, k, hipMemcpyHostToDevice, stream) ==
                        hipSuccess;
     }
     if (slot < kMirror) {
         const uint32_t k = (kMirror - slot) < first ? kMirror - slot : first;
-        ok = ok && hipMemcpyAsync(c->ring + kRing + slot, c->h_stage, k, hipMemcpyHostToDevice, c->stream) ==
+        ok = ok && hipMemcpyAsync(c->ring + kRing + slot, c->h_stage, k, hipMemcpyHostToDevice, stream) ==
                        hipSuccess;
     }
-    ok = ok && hipMemcpyAsync(c->d_msg, &m, sizeof(m), hipMemcpyHostToDevice, c->stream) == hipSuccess;
+    ok = ok && hipMemcpyAsync(c->d_msg, &m, sizeof(m), hipMemcpyHostToDevice, stream) == hipSuccess;
     if (ok) {
-        hipLaunchKernelGGL(tamd_lz_compress, dim3(1), dim3(64), 0, c->stream, c->d_job, c->d_msg, c->fse, c->d_out,
+        hipLaunchKernelGGL(tamd_lz_compress, dim3(1), dim3(64), 0, stream, c->d_job, c->d_msg, c->fse, c->d_out,
                            c->d_written, (unsigned long long*)nullptr);
         ok = hipGetLastError() == hipSuccess;
     }
     uint32_t* h_written = (uint32_t*)(c->h_stage + stage_written(c->max));
     uint8_t* h_out = c->h_stage + stage_out(c->max);
-    ok = ok && hipMemcpyAsync(h_written, c->d_written, 4, hipMemcpyDeviceToHost, c->stream) == hipSuccess;
-    ok = ok && hipMemcpyAsync(h_out, c->d_out, c->max, hipMemcpyDeviceToHost, c->stream) == hipSuccess;
-    ok = ok && hipStreamSynchronize(c->stream) == hipSuccess;
+    ok = ok && hipMemcpyAsync(h_written, c->d_written, 4, hipMemcpyDeviceToHost, stream) == hipSuccess;
+    ok = ok && hipMemcpyAsync(h_out, c->d_out, c->max, hipMemcpyDeviceToHost, stream) == hipSuccess;
+    ok = ok && hipStreamSynchronize(stream) == hipSuccess;
     if (!ok) {
         c->failed = true;
         return -2;
