@@ -21,6 +21,10 @@ void ref_decomp_free(void* d);
 }
 
 static uint32_t rng_state = 1;
+static bool g_huffman = true;
+static uint32_t g_minmatch = 4;
+static unsigned huffman_blocks = 0;
+static uint64_t lit_bytes = 0, seq_bytes = 0, n_seqs = 0, lit_small = 0;
 static uint32_t rnd() {
     rng_state = rng_state * 1664525u + 1013904223u;
     return rng_state >> 8;
@@ -29,6 +33,8 @@ static uint32_t rnd() {
 int main(int argc, char** argv) {
     const unsigned n_msgs = argc > 1 ? (unsigned)atoi(argv[1]) : 400;
     rng_state = argc > 2 ? (uint32_t)atoi(argv[2]) : 1;
+    g_huffman = argc > 3 ? atoi(argv[3]) != 0 : true;
+    g_minmatch = argc > 4 ? (uint32_t)atoi(argv[4]) : 4;
     const unsigned kMax = 1300, kDict = 24000;
     uint8_t fse[TAMD_FSE_BYTES];
     tamd_fse_blob(fse);
@@ -64,6 +70,10 @@ int main(int argc, char** argv) {
                 if (kind == 0) {
                     stream.push_back((uint8_t)rnd());
                     ++i;
+                } else if (kind == 2) {  // novel text: skewed letters (Huffman-coded literals)
+                    const uint32_t r = rnd() % 100;
+                    stream.push_back((uint8_t)(r < 40 ? 'e' + r % 4 : r < 80 ? 'a' + r % 12 : ' ' + r % 64));
+                    ++i;
                 } else {
                     const char* w = words[rnd() % 9];
                     for (const char* c = w; *c && i < n; ++c, ++i) stream.push_back((uint8_t)*c);
@@ -80,7 +90,7 @@ int main(int argc, char** argv) {
     std::vector<int64_t> table(1u << 14, -1);
     uint64_t total_in = 0, total_out = 0;
     unsigned compressed = 0;
-    std::vector<uint8_t> out(kMax + 64), got(kMax + 64);
+    std::vector<uint8_t> out(2 * kMax + 64), got(kMax + 64);
     for (unsigned k = 0; k < n_msgs; ++k) {
         const unsigned n = lens[k];
         if (next + kMax > kDict) {
@@ -110,7 +120,7 @@ int main(int argc, char** argv) {
             uint32_t len = 0;
             if (c >= 0 && (uint64_t)c >= win && (uint64_t)c < p)
                 while (len < n - i && s[c + len] == s[p + len]) ++len;
-            if (len >= 4) {
+            if (len >= g_minmatch) {
                 lo.push_back((i - lit_start) | (len << 16));
                 off.push_back((uint32_t)(p - (uint64_t)c));
                 for (uint32_t j = 1; j < len && i + j + 4 <= n; ++j) table[hash(p + j)] = (int64_t)(p + j);
@@ -125,13 +135,35 @@ int main(int argc, char** argv) {
             uint32_t lits = n - lit_start;
             for (uint32_t v : lo) lits += v & 0xffffu;
             uint8_t h[4];
-            w = tamd_lits_header(lits, out.data());
+            // the literals in order, then the smaller of the raw and Huffman sections
+            std::vector<uint8_t> litbuf;
             uint32_t src = 0;
             for (size_t q = 0; q <= lo.size(); ++q) {
                 const uint32_t ll = q < lo.size() ? (lo[q] & 0xffffu) : n - lit_start;
-                memcpy(&out[w], s + pos + src, ll);
-                w += ll;
+                litbuf.insert(litbuf.end(), s + pos + src, s + pos + src + ll);
                 if (q < lo.size()) src += ll + (lo[q] >> 16);
+            }
+            uint32_t count[TAMD_HUF_SYMS] = {0};
+            bool small = true;
+            for (uint8_t c : litbuf) {
+                if (c >= TAMD_HUF_SYMS) small = false;
+                else ++count[c];
+            }
+            const uint32_t raw = tamd_lits_header(lits, out.data()) + lits;
+            lit_bytes += lits;
+            n_seqs += lo.size();
+            if (small) lit_small += lits;
+            uint32_t huf = 0;
+            std::vector<uint8_t> hsec(raw + 64);
+            if (g_huffman && small) huf = tamd_huf_section(litbuf.data(), lits, count, hsec.data(), raw);
+            if (huf && huf < raw) {
+                memcpy(out.data(), hsec.data(), huf);
+                w = huf;
+                ++huffman_blocks;
+            } else {
+                w = tamd_lits_header(lits, out.data());
+                memcpy(&out[w], litbuf.data(), lits);
+                w += lits;
             }
             const uint32_t hs = tamd_seq_header((uint32_t)lo.size(), h);
             memcpy(&out[w], h, hs);
@@ -139,6 +171,7 @@ int main(int argc, char** argv) {
             if (w < n - 1) {
                 const uint32_t nb = tamd_fse_sequences(lo.data(), off.data(), (uint32_t)lo.size(), fse, &out[w],
                                                        n - 1 - w);
+                seq_bytes += nb + hs;
                 w = nb ? w + nb : 0;
             } else {
                 w = 0;
@@ -161,7 +194,10 @@ int main(int argc, char** argv) {
         lin += n;
     }
     ref_decomp_free(dec);
-    printf("ok %u/%u compressed, %llu -> %llu bytes\n", compressed, n_msgs, (unsigned long long)total_in,
-           (unsigned long long)total_out);
+    fprintf(stderr, "literal bytes %llu (in Huffman-able sections %llu), sequences %llu in %llu bytes\n",
+            (unsigned long long)lit_bytes, (unsigned long long)lit_small, (unsigned long long)n_seqs,
+            (unsigned long long)seq_bytes);
+    printf("ok %u/%u compressed (%u with Huffman literals), %llu -> %llu bytes\n", compressed, n_msgs,
+           huffman_blocks, (unsigned long long)total_in, (unsigned long long)total_out);
     return 0;
 }

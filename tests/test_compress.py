@@ -236,3 +236,40 @@ def test_gpu_compress_batch_streams():
             total_out += w if w else len(m)
     print(f"batch: {total_in} -> {total_out} bytes, kernel {ms:.3f} ms")
     assert total_out < 0.8 * total_in
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("max_bytes", [1300, 4000])
+def test_gpu_compressor_edge_cases(max_bytes):
+    """Tiny messages (below the kernel's 8-byte floor: sent as is), runs of one byte (matches that
+    overlap their own output, distance 1), messages of exactly max bytes, messages above the
+    kernel's 2048-byte bound (max 4000: sent as is), and enough of them to restart the 24,000-byte
+    ring many times; every one restored by the reference decompressor."""
+    from tonk_amd.compress import MessageCompressor
+    L = ref_lib()
+    rng = np.random.default_rng(max_bytes)
+    msgs = []
+    for k in range(300):
+        kind = k % 6
+        if kind == 0:
+            msgs.append(bytes(rng.integers(0, 256, int(rng.integers(1, 9)), dtype=np.uint8)))
+        elif kind == 1:
+            msgs.append(bytes([k & 0xFF]) * int(rng.integers(9, max_bytes + 1)))
+        elif kind == 2:
+            msgs.append((b"abc" * max_bytes)[:max_bytes])
+        elif kind == 3:
+            msgs.append(bytes(rng.integers(0, 4, max_bytes, dtype=np.uint8)))
+        elif kind == 4 and max_bytes > 2048:
+            msgs.append((b"tonk siamese " * 400)[:int(rng.integers(2049, max_bytes + 1))])
+        else:
+            msgs.append(msgs[-1] if msgs else b"x" * 20)
+    comp, dec = MessageCompressor(max_bytes), RefDecompressor(L, max_bytes)
+    n_comp = 0
+    for m in msgs:
+        blk = comp.compress(m)
+        assert len(blk) < len(m) or not blk
+        if len(m) < 8 or len(m) > 2048:
+            assert blk == b""
+        n_comp += bool(blk)
+        assert dec.feed(blk, m) == m
+    assert n_comp > 100

@@ -270,3 +270,197 @@ static inline void tamd_fse_blob(uint8_t* blob) {
     tamd_build_fse(ml, 53, 6, blob + TAMD_FSE_ML_ENC, blob + TAMD_FSE_ML_DEC, e16 + TAMD_FSE_ML_E16);
     tamd_build_fse(of, 29, 5, blob + TAMD_FSE_OF_ENC, blob + TAMD_FSE_OF_DEC, e16 + TAMD_FSE_OF_E16);
 }
+
+// ---- Huffman-coded literals (RFC 8878 s3.1.1.3.1, s4.2) ----------------------------------------
+// Literal byte values 0..128 only (the direct weight representation, s4.2.1.1 headerByte >= 128);
+// code lengths limited to TAMD_HUF_MAX_BITS and complete (the decoder completes the last weight
+// to a power of two).
+#define TAMD_HUF_MAX_BITS 11u
+#define TAMD_HUF_SYMS 129u
+
+// Code lengths from the histogram `count[0..129)`; returns the longest length (0: fewer than two
+// symbols, or a symbol above 128 occurs: no Huffman block).  Scratch: arrays of 2 * 129 entries.
+TAMD_HD static inline uint32_t tamd_huf_lengths(const uint32_t* count, uint8_t* len, uint32_t* w, uint16_t* sym,
+                                               uint16_t* parent) {
+    uint32_t n = 0;
+    for (uint32_t s = 0; s < TAMD_HUF_SYMS; ++s) {
+        len[s] = 0;
+        if (count[s]) sym[n++] = (uint16_t)s;
+    }
+    if (n < 2) return 0;
+    for (uint32_t i = 1; i < n; ++i) {  // ascending count, then symbol (insertion sort, n <= 129)
+        const uint16_t x = sym[i];
+        uint32_t j = i;
+        while (j > 0 && count[sym[j - 1]] > count[x]) {
+            sym[j] = sym[j - 1];
+            --j;
+        }
+        sym[j] = x;
+    }
+    // two-queue Huffman: leaves 0..n-1 (sorted), internal nodes n.. in creation order
+    for (uint32_t i = 0; i < n; ++i) w[i] = count[sym[i]];
+    uint32_t leaf = 0, node = n, made = n;
+    for (uint32_t k = 0; k + 1 < n; ++k) {
+        uint32_t pick[2];
+        for (uint32_t t = 0; t < 2; ++t) {
+            if (leaf < n && (node >= made || w[leaf] <= w[node])) pick[t] = leaf++;
+            else pick[t] = node++;
+        }
+        w[made] = w[pick[0]] + w[pick[1]];
+        parent[pick[0]] = parent[pick[1]] = (uint16_t)made;
+        ++made;
+    }
+    // depths from the root (the last node) down; a leaf's depth is its code length
+    w[made - 1] = 0;
+    for (uint32_t k = made - 1; k-- > 0;) w[k] = w[parent[k]] + 1;
+    uint32_t maxlen = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+        uint32_t l = w[i];
+        if (l > TAMD_HUF_MAX_BITS) l = TAMD_HUF_MAX_BITS;
+        len[sym[i]] = (uint8_t)l;
+    }
+    // length limit: restore Kraft equality at 2^MAX (longer codes for the rarest, shorter for the
+    // most frequent)
+    const uint32_t target = 1u << TAMD_HUF_MAX_BITS;
+    uint32_t total = 0;
+    for (uint32_t i = 0; i < n; ++i) total += 1u << (TAMD_HUF_MAX_BITS - len[sym[i]]);
+    while (total > target) {
+        for (uint32_t i = 0; i < n && total > target; ++i) {  // rarest first
+            const uint32_t s = sym[i];
+            if (len[s] < TAMD_HUF_MAX_BITS) {
+                total -= 1u << (TAMD_HUF_MAX_BITS - len[s] - 1);
+                ++len[s];
+            }
+        }
+    }
+    bool changed = true;
+    while (total < target && changed) {
+        changed = false;
+        for (uint32_t i = n; i-- > 0 && total < target;) {  // most frequent first
+            const uint32_t s = sym[i];
+            if (len[s] > 1 && total + (1u << (TAMD_HUF_MAX_BITS - len[s])) <= target) {
+                total += 1u << (TAMD_HUF_MAX_BITS - len[s]);
+                --len[s];
+                changed = true;
+            }
+        }
+    }
+    if (total != target) return 0;
+    for (uint32_t s = 0; s < TAMD_HUF_SYMS; ++s)
+        if (len[s] > maxlen) maxlen = len[s];
+    return maxlen;
+}
+
+// Canonical codes (s4.2.1.3: by increasing weight = decreasing length, then by symbol value,
+// values counting up from 0 at the longest length).
+TAMD_HD static inline void tamd_huf_codes(const uint8_t* len, uint32_t maxlen, uint16_t* code) {
+    uint32_t c = 0;
+    for (uint32_t l = maxlen; l >= 1; --l) {
+        for (uint32_t s = 0; s < TAMD_HUF_SYMS; ++s)
+            if (len[s] == l) code[s] = (uint16_t)c++;
+        c >>= 1;
+    }
+}
+
+// Tree description, direct representation: header byte 127 + N, then the weights of symbols
+// 0..N-1 two per byte (high nibble first); N = the largest symbol present, whose weight the
+// decoder deduces.  Returns its size.
+TAMD_HD static inline uint32_t tamd_huf_tree(const uint8_t* len, uint32_t maxlen, uint8_t* out) {
+    uint32_t top = 0;
+    for (uint32_t s = 0; s < TAMD_HUF_SYMS; ++s)
+        if (len[s]) top = s;
+    out[0] = (uint8_t)(127u + top);
+    for (uint32_t s = 0; s < top; s += 2) {
+        const uint32_t w0 = len[s] ? maxlen + 1 - len[s] : 0;
+        const uint32_t w1 = s + 1 < top && len[s + 1] ? maxlen + 1 - len[s + 1] : 0;
+        out[1 + s / 2] = (uint8_t)((w0 << 4) | w1);
+    }
+    return 1 + (top + 1) / 2;
+}
+
+// One Huffman stream of lits[0..n) (the decoder reads the first literal first, so the writer goes
+// from the last), end mark and padding.  Returns its bytes, 0 when they would exceed cap.
+TAMD_HD static inline uint32_t tamd_huf_stream(const uint8_t* lits, uint32_t n, const uint8_t* len,
+                                              const uint16_t* code, uint8_t* out, uint32_t cap) {
+    uint64_t acc = 0;
+    uint32_t nbits = 0, pos = 0;
+    for (uint32_t i = n; i-- > 0;) {
+        const uint32_t s = lits[i];
+        acc |= (uint64_t)code[s] << nbits;
+        nbits += len[s];
+        while (nbits >= 8) {
+            if (pos >= cap) return 0;
+            out[pos++] = (uint8_t)acc;
+            acc >>= 8;
+            nbits -= 8;
+        }
+    }
+    acc |= 1ull << nbits;  // end mark
+    ++nbits;
+    while (nbits > 0) {
+        if (pos >= cap) return 0;
+        out[pos++] = (uint8_t)acc;
+        acc >>= 8;
+        nbits = nbits > 8 ? nbits - 8 : 0;
+    }
+    return pos;
+}
+
+// The whole Huffman literals section (header, tree, one or four streams) of lits[0..n) into out;
+// returns its size, 0 when Huffman does not apply or the section would not beat `cap` bytes.
+TAMD_HD static inline uint32_t tamd_huf_section(const uint8_t* lits, uint32_t n, const uint32_t* count,
+                                               uint8_t* out, uint32_t cap) {
+    uint8_t len[TAMD_HUF_SYMS];
+    uint16_t code[TAMD_HUF_SYMS], sym[TAMD_HUF_SYMS], parent[2 * TAMD_HUF_SYMS];
+    uint32_t w[2 * TAMD_HUF_SYMS];
+    if (n < 16 || n > 16383 || cap < 8) return 0;
+    const uint32_t maxlen = tamd_huf_lengths(count, len, w, sym, parent);
+    if (!maxlen) return 0;
+    tamd_huf_codes(len, maxlen, code);
+    const bool single = n <= 1023;
+    const uint32_t hsize = single ? 3u : (n <= 1023 ? 3u : 4u);
+    uint32_t at = hsize;
+    at += tamd_huf_tree(len, maxlen, out + at);
+    if (at >= cap) return 0;
+    if (single) {
+        const uint32_t b = tamd_huf_stream(lits, n, len, code, out + at, cap - at);
+        if (!b) return 0;
+        at += b;
+    } else {
+        const uint32_t seg = (n + 3) / 4, jt = at;
+        at += 6;
+        if (at >= cap) return 0;
+        for (uint32_t k = 0; k < 4; ++k) {
+            const uint32_t a = k * seg, e = a + seg < n ? a + seg : n;
+            const uint32_t b = tamd_huf_stream(lits + a, e - a, len, code, out + at, cap - at);
+            if (!b) return 0;
+            if (k < 3) {
+                out[jt + 2 * k] = (uint8_t)b;
+                out[jt + 2 * k + 1] = (uint8_t)(b >> 8);
+            }
+            at += b;
+        }
+    }
+    const uint32_t comp = at - hsize;  // tree + (jump table +) streams
+    if (single) {
+        if (comp > 1023) return 0;
+        const uint32_t v = 2u | (n << 4) | (comp << 14);
+        out[0] = (uint8_t)v;
+        out[1] = (uint8_t)(v >> 8);
+        out[2] = (uint8_t)(v >> 16);
+    } else if (hsize == 3) {
+        if (comp > 1023) return 0;
+        const uint32_t v = 2u | (1u << 2) | (n << 4) | (comp << 14);
+        out[0] = (uint8_t)v;
+        out[1] = (uint8_t)(v >> 8);
+        out[2] = (uint8_t)(v >> 16);
+    } else {
+        if (comp > 16383) return 0;
+        const uint32_t v = 2u | (2u << 2) | (n << 4) | (comp << 18);
+        out[0] = (uint8_t)v;
+        out[1] = (uint8_t)(v >> 8);
+        out[2] = (uint8_t)(v >> 16);
+        out[3] = (uint8_t)(v >> 24);
+    }
+    return at;
+}
