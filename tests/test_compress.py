@@ -248,17 +248,18 @@ def test_gpu_compressor_edge_cases(max_bytes):
     from tonk_amd.compress import MessageCompressor
     L = ref_lib()
     rng = np.random.default_rng(max_bytes)
+    top = min(max_bytes, 2048)  # the kernel's message bound
     msgs = []
     for k in range(300):
         kind = k % 6
         if kind == 0:
             msgs.append(bytes(rng.integers(0, 256, int(rng.integers(1, 9)), dtype=np.uint8)))
         elif kind == 1:
-            msgs.append(bytes([k & 0xFF]) * int(rng.integers(9, max_bytes + 1)))
+            msgs.append(bytes([k & 0xFF]) * int(rng.integers(9, top + 1)))
         elif kind == 2:
-            msgs.append((b"abc" * max_bytes)[:max_bytes])
+            msgs.append((b"abc" * top)[:top])
         elif kind == 3:
-            msgs.append(bytes(rng.integers(0, 4, max_bytes, dtype=np.uint8)))
+            msgs.append(bytes(rng.integers(0, 4, top, dtype=np.uint8)))
         elif kind == 4 and max_bytes > 2048:
             msgs.append((b"tonk siamese " * 400)[:int(rng.integers(2049, max_bytes + 1))])
         else:
