@@ -269,6 +269,7 @@ struct Session {
     // handed out dynamically (an atomic counter) so uneven streams balance across threads
     std::vector<std::thread> threads;
     std::vector<int> cpus;  // pool threads' CPU set (device_local_cpus), empty = not pinned
+    size_t threads_wanted = 0;
     std::mutex mu;
     std::condition_variable cv_start, cv_done;
     std::function<void(size_t, size_t)> job;
@@ -301,7 +302,22 @@ struct Session {
     std::vector<uint32_t> order;
     std::vector<double> stream_ms;
 
+    // Sticky mode (default): thread t first runs its own streams (s % T == t) so a stream's
+    // state stays in the same core's caches from step to step, then takes any stream still
+    // unclaimed, longest first.  Without it streams are handed out longest first only.
+    std::vector<std::atomic<uint8_t>> claimed;
+    bool sticky_job = false;
     void drain(const std::function<void(size_t, size_t)>& f, size_t ti) {
+        if (sticky_job) {
+            const size_t T = threads.size(), n = streams.size();
+            for (size_t s = ti; s < n; s += T)
+                if (!claimed[s].exchange(1)) f(s, ti);
+            for (size_t k = 0; k < n; ++k) {
+                const size_t s = order.empty() ? k : order[k];
+                if (!claimed[s].exchange(1)) f(s, ti);
+            }
+            return;
+        }
         for (;;) {
             const size_t i = next_item.fetch_add(1);
             if (i >= streams.size()) break;
@@ -310,10 +326,17 @@ struct Session {
     }
 
     void pool_loop(size_t ti) {
+        // Each pool thread on a core of its own (with sticky streams its streams' state stays in
+        // that core's caches); TONK_AMD_PIN=set lets every thread float over the whole CPU set.
+        static const bool pin_set = getenv("TONK_AMD_PIN") && !strcmp(getenv("TONK_AMD_PIN"), "set");
         if (!cpus.empty()) {
             cpu_set_t set;
             CPU_ZERO(&set);
-            for (int c : cpus) CPU_SET(c, &set);
+            if (pin_set || cpus.size() < threads_wanted) {
+                for (int c : cpus) CPU_SET(c, &set);
+            } else {
+                CPU_SET(cpus[ti % cpus.size()], &set);
+            }
             pthread_setaffinity_np(pthread_self(), sizeof(set), &set);
         }
         uint64_t seen = 0;
@@ -335,7 +358,13 @@ struct Session {
     }
 
     void run_all(const std::function<void(size_t, size_t)>& f) {
+        static const bool sticky = getenv("TONK_AMD_NO_STICKY") == nullptr;  // A/B switch (profiling)
         next_item = 0;
+        sticky_job = sticky && !threads.empty();
+        if (sticky_job) {
+            if (claimed.size() != streams.size()) claimed = std::vector<std::atomic<uint8_t>>(streams.size());
+            for (auto& c : claimed) c.store(0, std::memory_order_relaxed);
+        }
         if (threads.empty()) {
             drain(f, 0);
             return;
@@ -561,6 +590,7 @@ void* tamd_session_create(const tamd_session_params* p, char* err, size_t err_le
     Session* raw = s.get();
     if (nthreads > 1) {
         raw->cpus = device_local_cpus((int)p->device);
+        raw->threads_wanted = nthreads;
         for (uint32_t t = 0; t < nthreads; ++t) raw->threads.emplace_back([raw, t] { raw->pool_loop(t); });
     }
     // Streams are built on the pool threads (first touch of their state on the device's node).
