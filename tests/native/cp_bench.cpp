@@ -188,7 +188,7 @@ int main(int argc, char** argv) {
     p.loss_thresh = 42949673;
     p.fec_rate_q16 = 1311;
     p.ack_every = 64;
-    uint32_t streams = 8, step = 4096, warm_steps = 0;  // warm: untimed, unsampled first steps
+    uint32_t streams = 8, step = 4096, warm_steps = 0, expand = ~0u;  // warm: untimed, unsampled first steps
     p.n_originals = 4096 * 6;
     for (int i = 1; i < argc; ++i) {
         const char* eq = strchr(argv[i], '=');
@@ -198,6 +198,7 @@ int main(int argc, char** argv) {
         if (k == "stub") { g_stub = atoi(eq + 1); continue; }
         if (k == "nobatch") { g_nobatch = atoi(eq + 1); continue; }
         if (k == "warm") { warm_steps = (uint32_t)atoi(eq + 1); continue; }
+        if (k == "expand") { expand = (uint32_t)strtoul(eq + 1, nullptr, 0); continue; }
         const unsigned long long v = strtoull(eq + 1, nullptr, 0);
         if (k == "streams") streams = (uint32_t)v;
         else if (k == "n") p.n_originals = (uint32_t)v;
@@ -224,6 +225,7 @@ int main(int argc, char** argv) {
         ps[s].seed_loss = 2000 + s;
         ctxs[s].reset(new Context());
         Context& ctx = *ctxs[s];
+        ctx.ex.expand_limit = expand;
         ctx.rows.init(4ull * p.n_originals * 1344 + (256u << 20));
         encs[s].reset(new Encoder(&ctx, 1344));
         encs[s]->set_clock(&g_step_clock);  // the session reads the clock once per step

@@ -25,6 +25,8 @@ static bool g_huffman = true;
 static uint32_t g_minmatch = 4;
 static unsigned huffman_blocks = 0;
 static uint64_t lit_bytes = 0, seq_bytes = 0, n_seqs = 0, lit_small = 0;
+static double est_fitted = 0;  // estimated bytes of the sequence streams with block-fitted tables
+#include <math.h>
 static uint32_t rnd() {
     rng_state = rng_state * 1664525u + 1013904223u;
     return rng_state >> 8;
@@ -172,6 +174,22 @@ int main(int argc, char** argv) {
                 const uint32_t nb = tamd_fse_sequences(lo.data(), off.data(), (uint32_t)lo.size(), fse, &out[w],
                                                        n - 1 - w);
                 seq_bytes += nb + hs;
+                {  // entropy of the three code streams per block + the same extra bits + ~8 B of table headers each
+                    uint32_t hl[64] = {0}, hm[64] = {0}, ho[32] = {0};
+                    double extra = 0;
+                    for (size_t q = 0; q < lo.size(); ++q) {
+                        const uint32_t llc = tamd_ll_code(lo[q] & 0xffffu), mlc = tamd_ml_code(lo[q] >> 16);
+                        const uint32_t ofc = 31u - (uint32_t)__builtin_clz(off[q] + 3u);
+                        ++hl[llc]; ++hm[mlc]; ++ho[ofc];
+                        extra += tamd_ll_bits(llc) + tamd_ml_bits(mlc) + ofc;
+                    }
+                    auto ent = [&](const uint32_t* h, int k) {
+                        double e = 0, t = (double)lo.size();
+                        for (int i = 0; i < k; ++i) if (h[i]) e -= h[i] * log2(h[i] / t);
+                        return e;
+                    };
+                    est_fitted += (ent(hl, 64) + ent(hm, 64) + ent(ho, 32) + extra) / 8.0 + 3 * 8 + hs;
+                }
                 w = nb ? w + nb : 0;
             } else {
                 w = 0;
@@ -194,6 +212,8 @@ int main(int argc, char** argv) {
         lin += n;
     }
     ref_decomp_free(dec);
+    fprintf(stderr, "sequence sections now %llu bytes, with block-fitted tables about %.0f\n",
+            (unsigned long long)seq_bytes, est_fitted);
     fprintf(stderr, "literal bytes %llu (in Huffman-able sections %llu), sequences %llu in %llu bytes\n",
             (unsigned long long)lit_bytes, (unsigned long long)lit_small, (unsigned long long)n_seqs,
             (unsigned long long)seq_bytes);

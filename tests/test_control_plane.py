@@ -26,7 +26,7 @@ SCENARIOS = ["c1_256_p3", "c2_4096_p1_ack64", "c2_4096_p1_noack", "c3_4096_p2_ac
              "var_1_1500_p2_ack32", "tiny_1_20_p5_ack16", "big_9000_p3_ack64", "hiloss_p20_arq",
              "norecloss_p5_arq", "single_p0", "burst8_p5", "rtx_p2_ack64", "rtx_p5_ack32", "rtx_p3_noack"]
 MODES = [("sync", 0), ("batch", 1000), ("batch", 4096), ("sync-dirty", 0), ("batch-dirty", 1000),
-         ("batch-pipe", 1000), ("batch-pipe", 4096), ("batch-pipedrain", 1000)]
+         ("batch-pipe", 1000), ("batch-pipe", 4096), ("batch-pipedrain", 1000), ("batch-pipeexp", 512)]
 
 
 @pytest.fixture(scope="module")
@@ -46,9 +46,12 @@ def test_control_plane_matches_reference(harness, golden_index, tmp_path, name, 
     # levels that would run together checked for hazards; "-pipedrain": every second program
     # also completes all in-flight ones (the session's record mode), so rows are reused sooner
     base, dirty = mode.split("-")[0], int(mode.endswith("-dirty"))
+    # "-pipeexp": also the few-stream session's expansion limit (expansions over 16 terms are
+    # read as rows, one level up)
     pipe, drain = int("-pipe" in mode), 2 * int(mode.endswith("-pipedrain"))
+    expand = 16 if mode.endswith("-pipeexp") else 0xFFFFFFFF
     args = [harness, str(out), f"mode={base}", f"batch={batch}", f"dirty={dirty}", f"pipeline={pipe}",
-            f"drain={drain}"] + sc["args"] + [
+            f"drain={drain}", f"expand={expand}"] + sc["args"] + [
         f"seed_data={1000 + sid}", f"seed_loss={2000 + sid}"]
     r = subprocess.run(args, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]

@@ -397,7 +397,7 @@ void ExpansionTable::clear() {
 
 void ExpansionTable::append(const RowTable& rows, RowId r, uint32_t len, uint8_t coef, Sym& out) const {
     if (!coef || !len) return;
-    if (rows.level(r) == 0 || !has(r)) {
+    if (rows.level(r) == 0 || !has(r) || get(r).size() > expand_limit) {
         out.push_back(Term{r, len, coef});
         return;
     }

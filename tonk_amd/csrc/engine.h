@@ -321,6 +321,11 @@ inline void opcode_coefs(unsigned op, uint8_t rx, uint8_t* c) {
 // use the content's terms instead of the row itself (which would add a level).
 class ExpansionTable {
 public:
+    // Expansions longer than this many terms are not inlined: the reader takes the row itself and
+    // lands one level above its writer.  Unlimited by default (flat programs: one launch per
+    // level); a pipelined session, whose levels overlap across programs, bounds it (the cost of
+    // inlining grows with the solves per program).
+    uint32_t expand_limit = ~0u;
     void set(RowId r, const Sym& s);
     bool has(RowId r) const { return r < index_.size() && index_[r] >= 0; }
     const Sym& get(RowId r) const { return pool_[index_[r]]; }

@@ -600,6 +600,15 @@ void* tamd_session_create(const tamd_session_params* p, char* err, size_t err_le
         std::unique_ptr<Context> ctx(new Context());
         ctx->rows.init(range, (range / TAMD_ROW_UNIT) * i);
         ctx->pipeline = pipe;
+        // Pipelined sessions of one or a few streams reference expansions of more than 16 terms
+        // as rows: their launches are small, so the extra levels cost little, while inlining
+        // grows with the solves per program and sets the host time (configs[4] decoder stress:
+        // 1.84 -> 3.63 GiB/s).  Batched sessions keep inlining: there the extra levels are extra
+        // full-width launches (configs[3]: 33 -> 57 launches per 30 steps, device time per step
+        // +11 %, no host gain).  TONK_AMD_EXPAND=<terms> overrides (A/B knob).
+        static const char* expand_env = getenv("TONK_AMD_EXPAND");
+        const uint32_t expand = expand_env ? (uint32_t)atoi(expand_env) : (p->n_streams <= 4 ? 16u : ~0u);
+        if (pipe) ctx->ex.expand_limit = expand;
         std::unique_ptr<Stream> st(new Stream());
         st->ctx = ctx.get();
         wl::Params& q = st->p;
