@@ -268,14 +268,15 @@ uint64_t Device::run(Context* const* ctxs, size_t n) {
     return launch();
 }
 
-void Device::begin(Context* const* ctxs, size_t n) {
+void Device::begin(Context* const* ctxs, size_t n, bool closed) {
     Plan& P = plan_;
-    P.ctxs.assign(ctxs, ctxs + n);
+    P.pbs.resize(n);
+    for (size_t c = 0; c < n; ++c) P.pbs[c] = closed ? &ctxs[c]->closed : &ctxs[c]->pb;
     P.levels = 0;
     P.n_instr = P.n_ops = P.n_items = 0;
     uint32_t B = 0;  // buckets: TAMD_COST_CLASSES per level (expensive ops first), see ProgramBuilder::op_levels
     for (size_t c = 0; c < n; ++c) {
-        const ProgramBuilder& pb = ctxs[c]->pb;
+        const ProgramBuilder& pb = *P.pbs[c];
         P.n_instr += pb.instrs().size();
         P.n_ops += pb.ops().size();
         stats_.acc_bytes += pb.acc_bytes();
@@ -299,7 +300,7 @@ void Device::begin(Context* const* ctxs, size_t n) {
     for (uint32_t b = 0; b < B; ++b) {
         if (b % TAMD_COST_CLASSES == 0) P.item_base[b / TAMD_COST_CLASSES] = item_at;
         for (size_t c = 0; c < n; ++c) {
-            const ProgramBuilder& pb = ctxs[c]->pb;
+            const ProgramBuilder& pb = *P.pbs[c];
             P.op_start[c * B + b] = op_at;
             P.item_start[c * B + b] = item_at;
             if (b < pb.level_ops().size()) {
@@ -313,7 +314,7 @@ void Device::begin(Context* const* ctxs, size_t n) {
     P.item_base[L] = item_at;
     for (size_t c = 0; c < n; ++c) {
         P.instr_base[c] = instr_at;
-        instr_at += (uint32_t)ctxs[c]->pb.instrs().size();
+        instr_at += (uint32_t)P.pbs[c]->instrs().size();
     }
     P.n_items = item_at;
     // the executor reads a 64-instruction window without bounds checks: pad the region
@@ -346,7 +347,7 @@ void Device::begin(Context* const* ctxs, size_t n) {
 void Device::fill(size_t c) {
     Plan& P = plan_;
     if (P.empty) return;
-    const ProgramBuilder& pb = P.ctxs[c]->pb;
+    const ProgramBuilder& pb = *P.pbs[c];
     const uint32_t L = P.buckets;
     tamd_instr* hi = (tamd_instr*)P.slot->host;
     tamd_op* ho = (tamd_op*)(P.slot->host + P.bytes_instr);

@@ -53,8 +53,10 @@ public:
     // The same in three phases so host threads can fill their part of the merged program in
     // parallel: begin() lays the program out (ops grouped by level, then by context) and waits
     // for the staging slot; fill(i) copies context i (thread safe for distinct i); launch()
-    // uploads the program and enqueues one tamd_exec per level.  Returns the ticket.
-    void begin(Context* const* ctxs, size_t n);
+    // uploads the program and enqueues one tamd_exec per level.  Returns the ticket.  With
+    // `closed` the program is each context's closed program (Context::close_flush) instead of
+    // its pending one, so the next program can be built while this one is filled.
+    void begin(Context* const* ctxs, size_t n, bool closed = false);
     void fill(size_t i);
     uint64_t launch();
     // Level pipelining across programs (the session; Context::kPipeDepth): a program's levels
@@ -165,7 +167,7 @@ private:
     bool alloc_slots(size_t cap);    // (re)allocate every slot; nothing may be in flight
     // layout of the program being assembled (begin/fill/launch)
     struct Plan {
-        std::vector<Context*> ctxs;
+        std::vector<const ProgramBuilder*> pbs;      // per context
         std::vector<uint32_t> instr_base;          // per context
         std::vector<uint32_t> op_start, item_start; // [context * levels + level]
         std::vector<uint32_t> level_items, item_base, level_coop;  // level_coop: class-0 items (first)

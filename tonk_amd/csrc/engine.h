@@ -145,6 +145,18 @@ public:
 
     bool empty() const { return ops_.empty(); }
     void clear();
+    // Exchange the finished contents (no op may be under construction in either builder).
+    void swap_contents(ProgramBuilder& o) {
+        ops_.swap(o.ops_);
+        instrs_.swap(o.instrs_);
+        levels_.swap(o.levels_);
+        written_.swap(o.written_);
+        level_ops_.swap(o.level_ops_);
+        level_items_.swap(o.level_items_);
+        std::swap(max_level_, o.max_level_);
+        std::swap(acc_bytes_, o.acc_bytes_);
+        std::swap(store_bytes_, o.store_bytes_);
+    }
     uint32_t max_level() const { return max_level_; }
 
     const std::vector<tamd_op>& ops() const { return ops_; }
@@ -361,6 +373,9 @@ public:
 struct Context {
     RowTable rows;
     ProgramBuilder pb{&rows};
+    // The last program closed by finish_flush(true): kept for the executor while the next one
+    // is built (the session fills a program during the next step's control plane).
+    ProgramBuilder closed{&rows};
     ExpansionTable ex;
     std::vector<RowId> temps;          // rows only read inside the pending program
     std::vector<FlushClient*> clients;
@@ -408,7 +423,7 @@ struct Context {
     void prepare_flush() {
         for (FlushClient* c : track_dirty ? dirty : clients) c->pre_flush();
     }
-    void finish_flush() {
+    void finish_flush(bool keep_closed = false) {
         // Rows written now first: their entry supersedes an older one for the same handle (a
         // handle freed and reused while its old inherited level was counting down).
         const size_t old = inherited.size();
@@ -444,6 +459,7 @@ struct Context {
         dirty.clear();
         rows.seal_epoch(epoch);
         ++epoch;
+        if (keep_closed) closed.swap_contents(pb);
         pb.clear();
     }
 };

@@ -250,6 +250,7 @@ struct Session {
     std::vector<std::unique_ptr<Stream>> streams;
     std::vector<std::unique_ptr<Context>> ctxs;     // ctxs[i] belongs to streams[i]
     std::vector<double> busy_ms;                    // per thread, control-plane time of a step
+    std::vector<double> fill_ms;                    // per thread, program fill time (deferred mode)
     std::vector<std::pair<uint64_t, uint64_t>> epoch_ticket;  // (epoch, ticket) awaiting release
     uint64_t last_ticket = 0, released_epoch = 0, prev_ticket = 0;
     double host_ms[6] = {0, 0, 0, 0, 0, 0};
@@ -271,18 +272,16 @@ struct Session {
     std::vector<int> cpus;  // pool threads' CPU set (device_local_cpus), empty = not pinned
     size_t threads_wanted = 0;
     std::mutex mu;
-    std::condition_variable cv_start, cv_done;
-    std::function<void(size_t, size_t)> job;
+    std::condition_variable cv_start;
+    const std::function<void(size_t, size_t)>* job = nullptr;  // the pass being run (run_all)
     std::atomic<size_t> next_item{0};
-    uint64_t job_gen = 0;
-    size_t job_left = 0;
-    bool quit = false;
+    std::atomic<bool> quit{false};
 
     ~Session() {
+        quit.store(true);
         {
             std::lock_guard<std::mutex> lk(mu);
-            quit = true;
-            ++job_gen;
+            gen.fetch_add(1);
         }
         cv_start.notify_all();
         for (auto& t : threads) t.join();
@@ -325,6 +324,19 @@ struct Session {
         }
     }
 
+    // Workers spin on the job generation for a while before sleeping on the condition variable,
+    // and the main thread spins for the end of a pass: a step is a few hundred microseconds, so
+    // a futex wake-up of 16 threads (and of the main thread) per pass is a visible share of it.
+    // TONK_AMD_SPIN_US sets the spin window (0: always sleep).
+    static uint64_t spin_ns() {
+        static const uint64_t v = getenv("TONK_AMD_SPIN_US") ? 1000ull * strtoull(getenv("TONK_AMD_SPIN_US"), nullptr, 10)
+                                                            : 300000ull;
+        return v;
+    }
+    std::atomic<uint64_t> gen{0};
+    std::atomic<size_t> left{0};
+    std::atomic<int> sleepers{0};
+
     void pool_loop(size_t ti) {
         // Each pool thread on a core of its own (with sticky streams its streams' state stays in
         // that core's caches); TONK_AMD_PIN=set lets every thread float over the whole CPU set.
@@ -341,19 +353,24 @@ struct Session {
         }
         uint64_t seen = 0;
         for (;;) {
-            std::function<void(size_t, size_t)> f;
-            {
+            if (gen.load(std::memory_order_acquire) == seen) {
+                const auto until = std::chrono::steady_clock::now() + std::chrono::nanoseconds(spin_ns());
+                unsigned k = 0;
+                while (gen.load(std::memory_order_acquire) == seen) {
+                    __builtin_ia32_pause();
+                    if ((++k & 255) == 0 && std::chrono::steady_clock::now() > until) break;
+                }
+            }
+            if (gen.load(std::memory_order_acquire) == seen) {
                 std::unique_lock<std::mutex> lk(mu);
-                cv_start.wait(lk, [&] { return job_gen != seen; });
-                seen = job_gen;
-                if (quit) return;
-                f = job;
+                sleepers.fetch_add(1);
+                cv_start.wait(lk, [&] { return gen.load() != seen; });
+                sleepers.fetch_sub(1);
             }
-            drain(f, ti);
-            {
-                std::lock_guard<std::mutex> lk(mu);
-                if (--job_left == 0) cv_done.notify_all();
-            }
+            seen = gen.load(std::memory_order_acquire);
+            if (quit.load(std::memory_order_acquire)) return;
+            drain(*job, ti);
+            left.fetch_sub(1, std::memory_order_acq_rel);
         }
     }
 
@@ -369,15 +386,14 @@ struct Session {
             drain(f, 0);
             return;
         }
-        {
+        job = &f;
+        left.store(threads.size(), std::memory_order_relaxed);
+        gen.fetch_add(1, std::memory_order_seq_cst);
+        if (sleepers.load(std::memory_order_seq_cst) > 0) {
             std::lock_guard<std::mutex> lk(mu);
-            job = f;
-            job_left = threads.size();
-            ++job_gen;
+            cv_start.notify_all();
         }
-        cv_start.notify_all();
-        std::unique_lock<std::mutex> lk(mu);
-        cv_done.wait(lk, [&] { return job_left == 0; });
+        while (left.load(std::memory_order_acquire) != 0) __builtin_ia32_pause();
     }
 
     // Highest epoch whose program has completed on the device (its freed rows are reusable).
@@ -397,7 +413,17 @@ struct Session {
     //   2. (main) lay out the merged program, wait for a free staging slot
     //   3. copy each stream's ops into the pinned staging buffer, close the stream's epoch
     //   4. (main) upload the program and launch it level by level
+    // Deferred mode (the default with level pipelining): phase 3 of a program runs at the start
+    // of the NEXT step's phase 1, in the same per-stream job (the stream's closed program is
+    // still in that core's caches), and the program is launched after it.  A step is then one
+    // pass over the pool instead of two; the device runs one program behind the host, which
+    // costs nothing while the host sets the pace.
+    bool deferred = false;       // set at create: pipelined and not host-staged
+    bool have_closed = false;    // a closed program is laid out (dev.begin) and awaits its fill
+    uint64_t closed_epoch = 0;
+
     void step(uint32_t originals, bool finish) {
+        if (deferred) { step_deferred(originals, finish); return; }
         typedef std::chrono::steady_clock clk;
         auto ms = [](clk::time_point a, clk::time_point b) {
             return std::chrono::duration<double, std::milli>(b - a).count();
@@ -409,11 +435,7 @@ struct Session {
         // record mode: the previous program's rows wait for their digests (after this launch)
         if (prm.record && !ctxs.empty() && ctxs[0]->epoch >= 2 && rel > ctxs[0]->epoch - 2) rel = ctxs[0]->epoch - 2;
         std::fill(busy_ms.begin(), busy_ms.end(), 0.0);
-        if (order.size() != streams.size()) {
-            order.resize(streams.size());
-            for (size_t i = 0; i < order.size(); ++i) order[i] = (uint32_t)i;
-            stream_ms.assign(streams.size(), 0.0);
-        }
+        init_order();
         run_all([this, originals, finish, rel, &ms](size_t i, size_t ti) {
             const auto w0 = clk::now();
             Context& c = *ctxs[i];
@@ -425,16 +447,9 @@ struct Session {
             busy_ms[ti] += t;
             stream_ms[i] = t;
         });
-        static const bool lpt = getenv("TONK_AMD_STREAM_FIFO") == nullptr;  // A/B switch (profiling)
-        if (lpt)
-            std::sort(order.begin(), order.end(), [this](uint32_t a, uint32_t b) { return stream_ms[a] > stream_ms[b]; });
+        sort_order();
         const auto t1 = clk::now();
-        double mx = 0;
-        for (double b : busy_ms) {
-            host_ms[1] += b;
-            if (b > mx) mx = b;
-        }
-        host_ms[5] += mx;
+        account_busy();
         std::vector<Context*> cs;
         for (auto& c : ctxs) cs.push_back(c.get());
         dev.begin(cs.data(), cs.size());
@@ -462,6 +477,98 @@ struct Session {
             resolve_transcripts(epoch);
             prev_ticket = last_ticket;
         }
+    }
+
+    void init_order() {
+        if (order.size() != streams.size()) {
+            order.resize(streams.size());
+            for (size_t i = 0; i < order.size(); ++i) order[i] = (uint32_t)i;
+            stream_ms.assign(streams.size(), 0.0);
+        }
+    }
+    void sort_order() {
+        static const bool lpt = getenv("TONK_AMD_STREAM_FIFO") == nullptr;  // A/B switch (profiling)
+        if (lpt)
+            std::sort(order.begin(), order.end(), [this](uint32_t a, uint32_t b) { return stream_ms[a] > stream_ms[b]; });
+    }
+    void account_busy() {
+        double mx = 0;
+        for (double b : busy_ms) {
+            host_ms[1] += b;
+            if (b > mx) mx = b;
+        }
+        host_ms[5] += mx;
+    }
+
+    // One pass over the pool: fill the closed program of the previous step (if any), then the
+    // control planes of this step, each stream closing its new program; then (main) launch the
+    // filled program and lay out the new one.  host_ms[3] (fill) is the fill part of the pass.
+    void step_deferred(uint32_t originals, bool finish) {
+        typedef std::chrono::steady_clock clk;
+        auto ms = [](clk::time_point a, clk::time_point b) {
+            return std::chrono::duration<double, std::milli>(b - a).count();
+        };
+        const auto t0 = clk::now();
+        clock_msec = time_msec();
+        uint64_t rel = completed_epoch();
+        // Record mode: rows of programs whose digests are still unread stay allocated.  At this
+        // point the digests of every program before the one launched last step are read.
+        if (prm.record && !ctxs.empty() && rel + 3 > ctxs[0]->epoch) rel = ctxs[0]->epoch >= 3 ? ctxs[0]->epoch - 3 : 0;
+        std::fill(busy_ms.begin(), busy_ms.end(), 0.0);
+        std::fill(fill_ms.begin(), fill_ms.end(), 0.0);
+        init_order();
+        const bool fill = have_closed;
+        run_all([this, originals, finish, rel, fill, &ms](size_t i, size_t ti) {
+            const auto w0 = clk::now();
+            Context& c = *ctxs[i];
+            if (fill) {
+                dev.fill(i);
+                fill_ms[ti] += ms(w0, clk::now());
+            }
+            c.rows.release_up_to(rel);
+            if (finish) streams[i]->runner->finish();
+            else streams[i]->runner->advance(originals);
+            c.prepare_flush();
+            c.finish_flush(true);
+            const double t = ms(w0, clk::now());
+            busy_ms[ti] += t;
+            stream_ms[i] = t;
+        });
+        sort_order();
+        const auto t1 = clk::now();
+        account_busy();
+        for (double f : fill_ms) host_ms[3] += f / (double)fill_ms.size();
+        if (fill) launch_closed();
+        const auto t2 = clk::now();
+        std::vector<Context*> cs;
+        for (auto& c : ctxs) cs.push_back(c.get());
+        dev.begin(cs.data(), cs.size(), true);
+        have_closed = true;
+        closed_epoch = ctxs.empty() ? 0 : ctxs[0]->epoch - 1;
+        const auto t3 = clk::now();
+        host_ms[0] += ms(t0, t1);
+        host_ms[4] += ms(t1, t2);
+        host_ms[2] += ms(t2, t3);
+    }
+
+    // Launch the closed program (filled), and in record mode read the digests of the program
+    // launched before it, which this launch completes.
+    void launch_closed() {
+        last_ticket = dev.launch();
+        have_closed = false;
+        epoch_ticket.push_back(std::make_pair(closed_epoch, last_ticket));
+        if (prm.record) {
+            if (prev_ticket) dev.wait(prev_ticket);
+            resolve_transcripts(closed_epoch);
+            prev_ticket = last_ticket;
+        }
+    }
+
+    // Fill and launch a closed program still waiting (end of a run: wait / finish).
+    void flush_closed() {
+        if (!have_closed) return;
+        run_all([this](size_t i, size_t) { dev.fill(i); });
+        launch_closed();
     }
 
     // H2D of the next `originals` input rows of every stream, both codec sides (each side's
@@ -587,6 +694,8 @@ void* tamd_session_create(const tamd_session_params* p, char* err, size_t err_le
     const uint64_t range = (s->dev.arena_bytes() / p->n_streams) & ~(uint64_t)(TAMD_ROW_UNIT - 1);
     s->row_cap = ((p->payload_max + 4 + 63) / 64) * 64;
     s->busy_ms.assign(nthreads, 0.0);
+    s->fill_ms.assign(nthreads, 0.0);
+    s->deferred = pipe && getenv("TONK_AMD_NO_DEFER") == nullptr;
     Session* raw = s.get();
     if (nthreads > 1) {
         raw->cpus = device_local_cpus((int)p->device);
@@ -720,6 +829,7 @@ int tamd_session_step(void* sp, uint32_t originals) {
 
 int tamd_session_wait(void* sp) {
     Session* s = (Session*)sp;
+    s->flush_closed();
     s->dev.synchronize();
     s->dev.sync_staging();
     if (s->prm.record) s->resolve_transcripts();
