@@ -32,6 +32,7 @@ const char* const names[kSlots] = {"enc_add", "enc_encode", "enc_ack", "dec_add_
 
 static int g_stub = 0;
 static int g_nobatch = 0;
+static int g_pipe = 1;
 static uint64_t g_step_clock = 1000;  // nobatch=1: single adds only (the runner's fallback path)  // stub=1: encoder calls return at once; stub=2: decoder calls too
 struct Null {
     struct RecRef { RecoveryOut out; };
@@ -199,6 +200,7 @@ int main(int argc, char** argv) {
         if (k == "nobatch") { g_nobatch = atoi(eq + 1); continue; }
         if (k == "warm") { warm_steps = (uint32_t)atoi(eq + 1); continue; }
         if (k == "expand") { expand = (uint32_t)strtoul(eq + 1, nullptr, 0); continue; }
+        if (k == "pipe") { g_pipe = atoi(eq + 1); continue; }  // level pipelining as the session runs it
         const unsigned long long v = strtoull(eq + 1, nullptr, 0);
         if (k == "streams") streams = (uint32_t)v;
         else if (k == "n") p.n_originals = (uint32_t)v;
@@ -226,6 +228,7 @@ int main(int argc, char** argv) {
         ctxs[s].reset(new Context());
         Context& ctx = *ctxs[s];
         ctx.ex.expand_limit = expand;
+        ctx.pipeline = g_pipe != 0;
         ctx.rows.init(4ull * p.n_originals * 1344 + (256u << 20));
         encs[s].reset(new Encoder(&ctx, 1344));
         encs[s]->set_clock(&g_step_clock);  // the session reads the clock once per step

@@ -384,15 +384,18 @@ void sym_merge(Sym& s) {
 void ExpansionTable::set(RowId r, const Sym& s) {
     if (r >= index_.size()) index_.resize((size_t)r + 1, -1);
     if (index_[r] >= 0) { pool_[index_[r]] = s; return; }
-    index_[r] = (int32_t)pool_.size();
-    pool_.push_back(s);
+    index_[r] = (int32_t)n_pool_;
+    // pool entries keep their storage across programs (no allocation per expansion)
+    if (n_pool_ < pool_.size()) pool_[n_pool_].assign(s.begin(), s.end());
+    else pool_.push_back(s);
+    ++n_pool_;
     used_.push_back(r);
 }
 
 void ExpansionTable::clear() {
     for (RowId r : used_) index_[r] = -1;
     used_.clear();
-    pool_.clear();
+    n_pool_ = 0;
 }
 
 void ExpansionTable::append(const RowTable& rows, RowId r, uint32_t len, uint8_t coef, Sym& out) const {

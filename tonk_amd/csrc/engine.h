@@ -348,7 +348,8 @@ public:
 
 private:
     std::vector<int32_t> index_;
-    std::vector<Sym> pool_;
+    std::vector<Sym> pool_;  // [0, n_pool_) in use
+    size_t n_pool_ = 0;
     std::vector<RowId> used_;
 };
 
@@ -390,7 +391,7 @@ struct Context {
     static const uint32_t kPipeDepth = 1;
     bool pipeline = false;
     std::vector<RowId> inherited;      // rows with an inherited level in the pending program
-    std::vector<uint64_t> inherited_at;  // per handle: epoch of its last write
+    std::vector<uint64_t> written_mark;  // bitmap over handles, all zero between flushes
 
     RowId alloc(uint32_t bytes) {
         const RowId r = rows.alloc(bytes);
@@ -424,33 +425,44 @@ struct Context {
         for (FlushClient* c : track_dirty ? dirty : clients) c->pre_flush();
     }
     void finish_flush(bool keep_closed = false) {
-        // Rows written now first: their entry supersedes an older one for the same handle (a
-        // handle freed and reused while its old inherited level was counting down).
-        const size_t old = inherited.size();
-        for (RowId r : pb.written_rows()) {
-            const uint32_t l = rows.level(r);
-            if (r >= inherited_at.size()) inherited_at.resize((size_t)r + 1024, 0);
-            inherited_at[r] = epoch;
-            if (pipeline && l > kPipeDepth) {
-                rows.set_level(r, l - kPipeDepth);
-                inherited.push_back(r);
-            } else {
-                rows.set_level(r, 0);
+        const std::vector<RowId>& w = pb.written_rows();
+        if (pipeline) {
+            // Inherited entries of earlier programs count down one level (a row written at level
+            // d stays pending d - 1 programs); a row written again now is superseded by its new
+            // entry (a handle rewritten, or freed and reused while it was counting down).  The
+            // rows written now are marked in a bitmap for that test: a per-handle epoch array
+            // costs a cache miss per written row.
+            if (!inherited.empty()) {
+                for (RowId r : w) {
+                    if ((r >> 6) >= written_mark.size()) written_mark.resize((r >> 6) + 1024, 0);
+                    written_mark[r >> 6] |= 1ull << (r & 63);
+                }
+                size_t keep = 0;
+                for (RowId r : inherited) {
+                    if ((r >> 6) < written_mark.size() && ((written_mark[r >> 6] >> (r & 63)) & 1u)) continue;
+                    const uint32_t l = rows.level(r);
+                    if (l > kPipeDepth) {
+                        rows.set_level(r, l - kPipeDepth);
+                        inherited[keep++] = r;
+                    } else {
+                        rows.set_level(r, 0);
+                    }
+                }
+                inherited.resize(keep);
+                for (RowId r : w) written_mark[r >> 6] = 0;
             }
-        }
-        size_t keep = 0;
-        for (size_t k = 0; k < old; ++k) {  // (a row written at level d stays pending d - 1 programs)
-            const RowId r = inherited[k];
-            if (inherited_at[r] == epoch) continue;  // superseded above
-            const uint32_t l = rows.level(r);
-            if (l > kPipeDepth) {
-                rows.set_level(r, l - kPipeDepth);
-                inherited[keep++] = r;
-            } else {
-                rows.set_level(r, 0);
+            for (RowId r : w) {
+                const uint32_t l = rows.level(r);
+                if (l > kPipeDepth) {
+                    rows.set_level(r, l - kPipeDepth);
+                    inherited.push_back(r);
+                } else {
+                    rows.set_level(r, 0);
+                }
             }
+        } else {
+            for (RowId r : w) rows.set_level(r, 0);
         }
-        inherited.erase(inherited.begin() + keep, inherited.begin() + old);
         for (RowId r : temps) rows.free_deferred(r);
         temps.clear();
         ex.clear();
