@@ -13,6 +13,9 @@
 #include "program.h"
 
 #define TAMD_WAVES_PER_WG 4
+#ifndef TAMD_ROLL
+#define TAMD_ROLL 1  // rolling row loads in ACCR runs (run_accr)
+#endif
 
 typedef unsigned long long u64;
 
@@ -227,6 +230,38 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
         const uint32_t W = 253u * 48u;
         uint32_t t = vgpr(((199u * (col0 % 253u)) % 253u) * 48u);
         const uint32_t tstep = vgpr(((199u * (cstep % 253u)) % 253u) * 48u);
+        if (TAMD_ROLL && nw == 1u) {
+            // Rolling loads: the rows of the next batch half are loaded as soon as a half has been
+            // combined, so a wave keeps 3-6 row loads in flight while it computes instead of
+            // waiting a full memory round trip per batch (same registers as a plain batch).
+            constexpr uint32_t H = TAMD_RBATCH / 2;
+            LV<NH> d[TAMD_RBATCH];
+#pragma unroll
+            for (uint32_t q = 0; q < TAMD_RBATCH; ++q) d[q] = lv_load<NH>(src + (size_t)min(q, count - 1u) * step);
+            for (uint32_t e = 0; e < count; e += TAMD_RBATCH) {
+                const bool more = e + TAMD_RBATCH < count;
+#pragma unroll
+                for (uint32_t h = 0; h < 2; ++h) {
+#pragma unroll
+                    for (uint32_t q = h * H; q < h * H + H; ++q) {
+                        if (e + q < count) {
+                            const uint32_t ti = TAMD_LDS_LANE + (t >> 2);
+                            const PermT c1 = perm_at(lds, ti), c2 = perm_at_hi(lds, ti + 6u);
+                            lv_acc3<NH>(lv_keep<FULL, NH>(d[q], o, len), c1, c2, a0, a1, a2);
+                            t += tstep;
+                            t = min(t, t - W);
+                        }
+                    }
+                    if (more) {
+#pragma unroll
+                        for (uint32_t q = h * H; q < h * H + H; ++q)
+                            d[q] = lv_load<NH>(src + (size_t)min(e + TAMD_RBATCH + q, count - 1u) * step);
+                    }
+                }
+            }
+            unit += (count + TAMD_RBATCH - 1) / TAMD_RBATCH;
+            return;
+        }
         for (uint32_t e = 0; e < count; e += TAMD_RBATCH) {
             if ((unit++ & (nw - 1u)) != wid) {
 #pragma unroll
@@ -255,6 +290,31 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
         uint32_t col = vgpr(col0);
         const uint32_t cs = vgpr(cstep), px = vgpr(p + 64u);
         const uint8_t* inv = (const uint8_t*)(lds + TAMD_LDS_INV);
+        if (TAMD_ROLL && nw == 1u) {  // rolling loads, as for LANE3 runs
+            constexpr uint32_t H = TAMD_RBATCH / 2;
+            LV<NH> d[TAMD_RBATCH];
+#pragma unroll
+            for (uint32_t q = 0; q < TAMD_RBATCH; ++q) d[q] = lv_load<NH>(src + (size_t)min(q, count - 1u) * step);
+            for (uint32_t e = 0; e < count; e += TAMD_RBATCH) {
+                const bool more = e + TAMD_RBATCH < count;
+#pragma unroll
+                for (uint32_t h = 0; h < 2; ++h) {
+#pragma unroll
+                    for (uint32_t q = h * H; q < h * H + H; ++q) {
+                        const uint32_t c = inv[(col & 63u) ^ px];
+                        col += cs;
+                        if (e + q < count) a0 ^= lv_mul<NH>(lv_keep<FULL, NH>(d[q], o, len), perm_at(lds, c * 8u));
+                    }
+                    if (more) {
+#pragma unroll
+                        for (uint32_t q = h * H; q < h * H + H; ++q)
+                            d[q] = lv_load<NH>(src + (size_t)min(e + TAMD_RBATCH + q, count - 1u) * step);
+                    }
+                }
+            }
+            unit += (count + TAMD_RBATCH - 1) / TAMD_RBATCH;
+            return;
+        }
         for (uint32_t e = 0; e < count; e += TAMD_RBATCH) {
             if ((unit++ & (nw - 1u)) != wid) {
                 col += cs * TAMD_RBATCH;

@@ -272,7 +272,8 @@ struct Session {
     std::vector<int> cpus;  // pool threads' CPU set (device_local_cpus), empty = not pinned
     size_t threads_wanted = 0;
     std::mutex mu;
-    std::condition_variable cv_start;
+    std::condition_variable cv_start, cv_done;
+    std::atomic<bool> main_sleeping{false};
     const std::function<void(size_t, size_t)>* job = nullptr;  // the pass being run (run_all)
     std::atomic<size_t> next_item{0};
     std::atomic<bool> quit{false};
@@ -370,7 +371,10 @@ struct Session {
             seen = gen.load(std::memory_order_acquire);
             if (quit.load(std::memory_order_acquire)) return;
             drain(*job, ti);
-            left.fetch_sub(1, std::memory_order_acq_rel);
+            if (left.fetch_sub(1, std::memory_order_acq_rel) == 1 && main_sleeping.load()) {
+                std::lock_guard<std::mutex> lk(mu);
+                cv_done.notify_one();
+            }
         }
     }
 
@@ -393,7 +397,21 @@ struct Session {
             std::lock_guard<std::mutex> lk(mu);
             cv_start.notify_all();
         }
-        while (left.load(std::memory_order_acquire) != 0) __builtin_ia32_pause();
+        // The caller blocks for the end of the pass (after a short spin): the workers already
+        // occupy the job's CPU share (cpu.max on the GPU box), a spinning 17th thread would
+        // push the process over its quota and get it throttled.
+        const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(20);
+        unsigned k = 0;
+        while (left.load(std::memory_order_acquire) != 0) {
+            __builtin_ia32_pause();
+            if ((++k & 255) == 0 && std::chrono::steady_clock::now() > until) {
+                std::unique_lock<std::mutex> lk(mu);
+                main_sleeping.store(true);
+                cv_done.wait(lk, [&] { return left.load() == 0; });
+                main_sleeping.store(false);
+                break;
+            }
+        }
     }
 
     // Highest epoch whose program has completed on the device (its freed rows are reusable).
