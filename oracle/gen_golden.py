@@ -53,6 +53,10 @@ def scenarios():
     s["rtx_p2_ack64"] = (WorkloadParams(n=3000, loss=0.02, ack=64, rtx=16, rtx_msec=1), 0, True)
     s["rtx_p5_ack32"] = (WorkloadParams(n=3000, loss=0.05, ack=32, rtx=8, rtx_msec=3), 0, True)
     s["rtx_p3_noack"] = (WorkloadParams(n=2000, loss=0.03, ack=0, rtx=16, rtx_msec=2), 0, True)
+    # frequent acks that acknowledge everything, so the encoder window restarts (StartNewWindow)
+    # and the next RTT scan starts on placeholder elements (their send timestamps persist)
+    s["rtx_restart_p1_ack4"] = (WorkloadParams(n=3000, loss=0.01, ack=4, rtx=2, rtx_msec=5), 0, True)
+    s["rtx_restart_p2_ack2"] = (WorkloadParams(n=3000, loss=0.02, ack=2, rtx=1, rtx_msec=7), 0, True)
     return s
 
 

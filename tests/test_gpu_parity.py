@@ -23,11 +23,12 @@ pytestmark = pytest.mark.gpu
 SCEN_CAPI = ["c1_256_p3", "c2_4096_p1_ack64", "c2_4096_p1_noack", "c3_4096_p2_ack64_s0",
              "var_1_1500_p2_ack32", "tiny_1_20_p5_ack16", "big_9000_p3_ack64", "hiloss_p20_arq",
              "norecloss_p5_arq", "single_p0", "burst8_p5", "c5_65536_ge5_b4",
-             "rtx_p2_ack64", "rtx_p5_ack32", "rtx_p3_noack"]
+             "rtx_p2_ack64", "rtx_p5_ack32", "rtx_p3_noack",
+             "rtx_restart_p1_ack4", "rtx_restart_p2_ack2"]
 SCEN_SESSION = ["c1_256_p3", "c2_4096_p1_ack64", "c2_4096_p1_noack", "c3_4096_p2_ack64_s1",
                 "c3_4096_p2_ack64_s63", "c4_4096_p1_ack64_s511", "var_1_1500_p2_ack32",
                 "tiny_1_20_p5_ack16", "big_9000_p3_ack64", "hiloss_p20_arq", "single_p0",
-                "burst8_p5", "c5_65536_ge5_b4", "rtx_p2_ack64", "rtx_p3_noack"]
+                "burst8_p5", "c5_65536_ge5_b4", "rtx_p2_ack64", "rtx_p3_noack", "rtx_restart_p1_ack4"]
 
 
 def _args(golden_index, name):

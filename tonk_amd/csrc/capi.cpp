@@ -41,7 +41,7 @@ int64_t now_ns() {
 // A thread prints to stderr how many API calls and device waits ran, the longest device-lock
 // wait, and how many calls are inside a device wait right now -- to tell a slow path from a
 // stuck one under a real caller (Tonk).  Everything it reads is an atomic.
-std::atomic<uint64_t> g_calls{0}, g_waits{0}, g_wait_ns{0}, g_lock_wait_max_ns{0};
+std::atomic<uint64_t> g_calls{0}, g_waits{0}, g_wait_ns{0}, g_lock_wait_max_ns{0}, g_lock_hold_max_ns{0};
 std::atomic<uint64_t> g_programs{0}, g_launches{0}, g_prepare_ns{0}, g_run_ns{0};
 std::atomic<int> g_in_wait{0};
 std::atomic<int64_t> g_in_wait_since{0};  // start of the current run of overlapping waits
@@ -50,6 +50,7 @@ bool g_watch = false;
 struct Site {
     const char* name;
     std::atomic<uint64_t> calls{0}, ns{0};
+    std::atomic<uint64_t> rc[8] = {};  // result codes, for the sites that record them (API_RC)
     Site* next;
     explicit Site(const char* n);
 };
@@ -70,6 +71,8 @@ struct CallScope {
 #define API_CALL()                   \
     static Site api_site_(__func__); \
     CallScope api_scope_(api_site_)
+// Return `r`, counting it in the site's result histogram (watchdog diagnostics).
+#define API_RC(r) do { const int rc_ = (int)(r); api_site_.rc[(unsigned)rc_ & 7u].fetch_add(1, std::memory_order_relaxed); return (SiameseResult)rc_; } while (0)
 
 // ---- the process runtime: one device, one arena, a segment pool over it ----
 struct Runtime;
@@ -94,6 +97,7 @@ struct Runtime {
 
 struct DevLock {
     std::unique_lock<std::mutex> lk;
+    int64_t held_since = 0;
     DevLock() : lk(g_rt->dev_mu, std::defer_lock) {
         if (!lk.try_lock()) {
             const int64_t t0 = now_ns();
@@ -102,6 +106,13 @@ struct DevLock {
             uint64_t m = g_lock_wait_max_ns.load(std::memory_order_relaxed);
             while (w > m && !g_lock_wait_max_ns.compare_exchange_weak(m, w)) {}
         }
+        if (g_watch) held_since = now_ns();
+    }
+    ~DevLock() {
+        if (!g_watch) return;
+        const uint64_t h = (uint64_t)(now_ns() - held_since);
+        uint64_t m = g_lock_hold_max_ns.load(std::memory_order_relaxed);
+        while (h > m && !g_lock_hold_max_ns.compare_exchange_weak(m, h)) {}
     }
 };
 
@@ -139,6 +150,13 @@ void SegmentPool::put(uint64_t base, uint32_t units) {
     free_list.push_back(std::make_pair(base, units));
 }
 
+// Live encoders, for the watchdog's state dump (TONK_AMD_CAPI_WATCH_STATE=1).  The dump reads
+// scalar fields of codecs other threads may be using: diagnostics only.
+struct CEncoder;
+std::mutex g_enc_mu;
+std::vector<CEncoder*> g_encs;
+void dump_encoders();
+
 void watch_loop(double period_s) {
     const int64_t start = now_ns();
     for (;;) {
@@ -149,18 +167,23 @@ void watch_loop(double period_s) {
         if (waiting > 0 && since)
             w = " IN DEVICE WAIT: " + std::to_string(waiting) + " call(s), for " +
                 std::to_string((now_ns() - since) / 1000000) + " ms";
-        fprintf(stderr, "[tonk_amd capi] t=%.1fs calls=%llu device_waits=%llu wait_ms=%.1f lock_wait_max_ms=%.2f%s\n",
+        fprintf(stderr, "[tonk_amd capi] t=%.1fs calls=%llu device_waits=%llu wait_ms=%.1f lock_wait_max_ms=%.2f lock_hold_max_ms=%.2f%s\n",
                 (now_ns() - start) * 1e-9, (unsigned long long)g_calls.load(), (unsigned long long)g_waits.load(),
-                g_wait_ns.load() * 1e-6, g_lock_wait_max_ns.exchange(0) * 1e-6, w.c_str());
+                g_wait_ns.load() * 1e-6, g_lock_wait_max_ns.exchange(0) * 1e-6, g_lock_hold_max_ns.exchange(0) * 1e-6,
+                w.c_str());
         fprintf(stderr, "[tonk_amd capi]   flush: prepare_ms=%.1f launch_ms=%.1f programs=%llu launches=%llu\n",
                 g_prepare_ns.load() * 1e-6, g_run_ns.load() * 1e-6, (unsigned long long)g_programs.load(),
                 (unsigned long long)g_launches.load());
         for (Site* st = g_sites.load(); st; st = st->next) {
             const uint64_t c = st->calls.load();
-            if (c)
-                fprintf(stderr, "[tonk_amd capi]   %-28s calls=%llu ms=%.1f\n", st->name, (unsigned long long)c,
-                        st->ns.load() * 1e-6);
+            if (!c) continue;
+            std::string h;
+            for (int k = 0; k < 8; ++k)
+                if (const uint64_t v = st->rc[k].load()) h += " rc" + std::to_string(k) + "=" + std::to_string(v);
+            fprintf(stderr, "[tonk_amd capi]   %-28s calls=%llu ms=%.1f%s\n", st->name, (unsigned long long)c,
+                    st->ns.load() * 1e-6, h.c_str());
         }
+        dump_encoders();
     }
 }
 
@@ -292,6 +315,18 @@ struct CEncoder : Codec {
     Encoder* enc = nullptr;
 };
 
+void dump_encoders() {
+    static const bool on = getenv("TONK_AMD_CAPI_WATCH_STATE") != nullptr;
+    if (!on) return;
+    std::lock_guard<std::mutex> lk(g_enc_mu);
+    char line[512];
+    for (size_t i = 0; i < g_encs.size(); ++i) {
+        if (!g_encs[i]->enc) continue;
+        g_encs[i]->enc->debug_state(line, sizeof(line));
+        fprintf(stderr, "[tonk_amd capi]   encoder %zu: %s\n", i, line);
+    }
+}
+
 struct CDecoder : Codec {
     Decoder* dec = nullptr;
     std::vector<SiameseOriginalPacket> out;
@@ -388,9 +423,10 @@ SIAMESE_EXPORT int siamese_init_(int version) {
     if (arena_mb < 2) arena_mb = 2;
     if (seg_kb < 64) seg_kb = 64;
     g_rt->pool.seg_units = (uint32_t)(seg_kb * 1024 / TAMD_ROW_UNIT);
-    // many codecs each submit small programs: 32 staging slots, so a program waits for the one
-    // 32 back to finish rather than the one 2 back
-    g_rt->dev.set_program_slots(32, 1u << 20);
+    // Many slots of modest size: a codec waits for its own program before its next one, so with
+    // hundreds of codecs (a Tonk server) hundreds of programs are in flight, and a slot still in
+    // use is waited for under the device lock, which stalls every codec behind it.
+    g_rt->dev.set_program_slots(128, 1u << 20);
     if (!g_rt->dev.init_growable(device, arena_mb << 20, max_mb << 20)) {
         fprintf(stderr, "%s\n", g_rt->dev.error().c_str());
         return Siamese_Disabled;
@@ -416,6 +452,10 @@ SIAMESE_EXPORT SiameseEncoder siamese_encoder_create() {
     CEncoder* e = new (std::nothrow) CEncoder();
     if (!e) return nullptr;
     e->enc = new Encoder(&e->ctx, 0, release_host, nullptr);
+    if (g_watch) {
+        std::lock_guard<std::mutex> lk(g_enc_mu);
+        g_encs.push_back(e);
+    }
     return reinterpret_cast<SiameseEncoder>(e);
 }
 
@@ -423,6 +463,10 @@ SIAMESE_EXPORT void siamese_encoder_free(SiameseEncoder encoder_t) {
     CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
     if (!e) return;
     API_CALL();
+    if (g_watch) {
+        std::lock_guard<std::mutex> lk(g_enc_mu);
+        g_encs.erase(std::remove(g_encs.begin(), g_encs.end(), e), g_encs.end());
+    }
     delete e->enc;  // (the destructor may still close scans into the pending program)
     e->enc = nullptr;
     e->quiesce();
@@ -433,8 +477,8 @@ SIAMESE_EXPORT SiameseResult siamese_encoder_is_ready(SiameseEncoder encoder_t) 
     CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
     if (!e) return Siamese_InvalidInput;
     API_CALL();
-    if (e->enc->remaining_slots() <= 2) return Siamese_MaxPacketsReached;
-    return Siamese_Success;
+    if (e->enc->remaining_slots() <= 2) API_RC(Siamese_MaxPacketsReached);
+    API_RC(Siamese_Success);
 }
 
 SIAMESE_EXPORT SiameseResult siamese_encoder_add(SiameseEncoder encoder_t, SiameseOriginalPacket* packet) {
@@ -505,11 +549,11 @@ SIAMESE_EXPORT SiameseResult siamese_encoder_retransmit(SiameseEncoder encoder_t
     original->DataBytes = 0;
     const StoredOriginal* o = nullptr;
     const Result r = e->enc->retransmit(&o);
-    if (r != kSuccess) return (SiameseResult)r;
+    if (r != kSuccess) API_RC(r);
     original->PacketNum = o->column;
     original->Data = (const unsigned char*)o->host + o->header_bytes;
     original->DataBytes = o->bytes - o->header_bytes;
-    return Siamese_Success;
+    API_RC(Siamese_Success);
 }
 
 SIAMESE_EXPORT SiameseResult siamese_encode(SiameseEncoder encoder_t, SiameseRecoveryPacket* recovery) {

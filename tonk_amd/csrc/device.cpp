@@ -40,10 +40,9 @@ Device::~Device() {
     if (device_ < 0) return;
     hipSetDevice(device_);
     hipStreamSynchronize((hipStream_t)stream_);
-    for (Slot& s : slots_) {
-        if (s.host) hipHostFree(s.host);
+    for (Slot& s : slots_)
         if (s.done) hipEventDestroy((hipEvent_t)s.done);
-    }
+    if (prog_host_) hipHostFree(prog_host_);
     if (prog_dev_) hipFree(prog_dev_);
     for (auto& p : inflight_) hipEventDestroy((hipEvent_t)p.second);
     for (void* e : free_events_) hipEventDestroy((hipEvent_t)e);
@@ -218,11 +217,15 @@ bool Device::map_chunk(uint64_t bytes) {
 
 bool Device::grow_arena(uint64_t min_bytes) {
     if (!reserved_bytes_) return min_bytes <= arena_bytes_;
-    // fixed-size physical chunks (256 MiB), mapped back to back
+    // Physical 256 MiB chunks mapped back to back.  A growth maps at least half the size mapped so
+    // far: it runs under the C ABI's device lock, so a window-filling Tonk server should take a
+    // handful of growths, not one per 256 MiB.
     const uint64_t chunk = ((256ull << 20) + granule_ - 1) / granule_ * granule_;
-    while (arena_bytes_ < min_bytes) {
-        if (arena_bytes_ + chunk > reserved_bytes_) return false;
-        if (!map_chunk(chunk)) return false;
+    uint64_t target = arena_bytes_ + arena_bytes_ / 2;
+    if (target < min_bytes) target = min_bytes;
+    while (arena_bytes_ < target) {
+        if (arena_bytes_ + chunk > reserved_bytes_) return arena_bytes_ >= min_bytes;
+        if (!map_chunk(chunk)) return arena_bytes_ >= min_bytes;
     }
     return true;
 }
@@ -231,17 +234,20 @@ bool Device::alloc_slots(size_t cap) {
     cap = (cap + 255) & ~(size_t)255;
     if (cap * slots_.size() > 0xfffff000ull) return false;  // 32-bit program offsets
     for (Slot& s : slots_) {
-        if (s.host) hipHostFree(s.host);
         s.host = nullptr;
         s.dev = nullptr;
     }
+    if (prog_host_) hipHostFree(prog_host_);
     if (prog_dev_) hipFree(prog_dev_);
+    prog_host_ = nullptr;
     prog_dev_ = nullptr;
     slot_cap_ = 0;
+    // one pinned and one device allocation, split into the slots
     if (hipMalloc((void**)&prog_dev_, cap * slots_.size()) != hipSuccess) return false;
+    if (hipHostMalloc((void**)&prog_host_, cap * slots_.size(), hipHostMallocDefault) != hipSuccess) return false;
     for (size_t k = 0; k < slots_.size(); ++k) {
         Slot& s = slots_[k];
-        if (hipHostMalloc((void**)&s.host, cap, hipHostMallocDefault) != hipSuccess) return false;
+        s.host = prog_host_ + k * cap;
         s.dev_off = (uint32_t)(k * cap);
         s.dev = prog_dev_ + s.dev_off;
     }

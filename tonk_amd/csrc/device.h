@@ -164,6 +164,7 @@ private:
     size_t slot_bytes_ = 16u << 20;  // requested initial capacity
     size_t slot_cap_ = 0;            // current capacity of every slot
     uint8_t* prog_dev_ = nullptr;
+    uint8_t* prog_host_ = nullptr;   // pinned twin of prog_dev_
     bool alloc_slots(size_t cap);    // (re)allocate every slot; nothing may be in flight
     // layout of the program being assembled (begin/fill/launch)
     struct Plan {

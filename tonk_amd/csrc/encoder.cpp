@@ -12,12 +12,12 @@ namespace tamd {
 static uint64_t (*g_clock_fn)() = nullptr;
 void set_clock_source(uint64_t (*fn)()) { g_clock_fn = fn; }
 
-// GetTimeMsec (SiameseTools.cpp).  Millisecond resolution is all the RTO logic uses, so the
-// coarse monotonic clock (a few ns, no TSC read) is enough; it is read once per original.
+// GetTimeMsec (SiameseTools.cpp:105-117): wall-clock milliseconds, the time base the reference's
+// 32-bit send timestamps and RTT arithmetic run on.  Read once per original.
 uint64_t time_msec() {
     if (g_clock_fn) return g_clock_fn();
     timespec ts;
-    clock_gettime(CLOCK_MONOTONIC_COARSE, &ts);
+    clock_gettime(CLOCK_REALTIME, &ts);  // gettimeofday's clock, as the reference (vDSO, no syscall)
     return (uint64_t)ts.tv_sec * 1000u + (uint64_t)ts.tv_nsec / 1000000u;
 }
 
@@ -139,8 +139,13 @@ inline void Encoder::add_unchecked(RowId row, uint32_t off, uint32_t framed_byte
         element = column % kLanes;
         start_new_window(column);
     }
-    // Elements below `element` in a fresh window are never read (placeholders).
-    while (win_.size() < element) win_.push_back(StoredOriginal());
+    // Elements below `element` in a fresh window are placeholders: only the RTT scan reads them,
+    // and only their send timestamps.
+    while (win_.size() < element) {
+        StoredOriginal p;
+        p.send_msec = placeholder_msec_[win_.size() % kLanes];
+        win_.push_back(p);
+    }
     StoredOriginal* slot;
     if (win_.size() == element) {
         slot = &win_.push_slot();
@@ -180,7 +185,9 @@ inline void Encoder::add_unchecked(RowId row, uint32_t off, uint32_t framed_byte
 
 // EncoderPacketWindow::StartNewWindow (SiameseEncoder.cpp:163-181)
 void Encoder::start_new_window(uint32_t column) {
-    // Everything from the previous window is unreachable once Count reached zero.
+    // Everything from the previous window is unreachable once Count reached zero (only the send
+    // timestamps of its first elements stay visible to the RTT scan, see placeholder_msec_).
+    for (uint32_t e = 0; e < kLanes; ++e) placeholder_msec_[e] = e < win_.size() ? win_[e].send_msec : placeholder_msec_[e];
     for (size_t i = 0; i < win_.size(); ++i) drop_original(win_[i]);
     win_.clear();
     const uint32_t element = column % kLanes;

@@ -8,6 +8,8 @@
 // combine op (plus running-sum scans) in the context's device program.
 #pragma once
 
+#include <stdio.h>
+
 #include "engine.h"
 #include "ring.h"
 #include "serial.h"
@@ -97,6 +99,12 @@ private:
 
     // ---- EncoderPacketWindow (SiameseEncoder.h:104-232) ----
     Ring<StoredOriginal> win_;
+    // Send timestamps the placeholder elements of a restarted window read: the reference keeps
+    // them in its subwindows' LastSendMsec arrays (SiameseEncoder.h:96), which a window restart
+    // (StartNewWindow, SiameseEncoder.cpp:163) does not clear, so an RTT scan that starts on a
+    // placeholder (UpdateRTO from a NextRTOColumn before the new window's first packet) sees the
+    // previous window's send time at that element, not zero.
+    uint32_t placeholder_msec_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t next_column_ = 0, count_ = 0, column_start_ = 0, longest_ = 0;
     uint32_t first_unremoved_ = 0;
     uint32_t sum_start_ = 0, sum_end_ = 0, sum_column_start_ = 0, sum_erased_ = 0;
@@ -126,6 +134,19 @@ private:
     uint32_t to_column(uint32_t element) const { return col_add(element, column_start_); }
     uint32_t unacked() const { return count_ - first_unremoved_; }
     StoredOriginal& elem(uint32_t e) { return win_[e]; }
+public:
+    // Diagnostics (the C ABI watchdog): window and acknowledgement state in one line.
+    int debug_state(char* buf, size_t n) const {
+        const uint32_t now = (uint32_t)now_msec();
+        const uint32_t first = col_sub(ack_.next_expected, column_start_);
+        const uint32_t age = first < count_ && first < win_.size() ? now - win_[first].send_msec : 0;
+        return snprintf(buf, n,
+                        "count=%u first_unremoved=%u next_column=%u column_start=%u ack_next=%u ack_bytes=%u "
+                        "rto=%u found_oldest=%d first_age_ms=%u disabled=%d",
+                        count_, first_unremoved_, next_column_, column_start_, ack_.next_expected, ack_.data_bytes,
+                        ack_.rto_msec, (int)ack_.found_oldest, age, (int)disabled_);
+    }
+private:
     uint32_t next_lane_element(uint32_t element, uint32_t lane) const {
         uint32_t n = element - (element % kLanes) + lane;
         if (n < element) n += kLanes;
