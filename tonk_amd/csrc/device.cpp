@@ -215,8 +215,23 @@ bool Device::map_chunk(uint64_t bytes) {
     return true;
 }
 
+// Diagnostics (TONK_AMD_CAPI_WATCH): device operations that block for long (they run under the
+// C ABI's device lock) are reported on stderr.
+static void report_slow(const char* what, std::chrono::steady_clock::time_point t0, uint64_t a, uint64_t b) {
+    static const bool on = getenv("TONK_AMD_CAPI_WATCH") != nullptr;
+    if (!on) return;
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (ms >= 10.0) fprintf(stderr, "tonk_amd: slow %s: %.1f ms (%llu, %llu)\n", what, ms, (unsigned long long)a, (unsigned long long)b);
+}
+
 bool Device::grow_arena(uint64_t min_bytes) {
     if (!reserved_bytes_) return min_bytes <= arena_bytes_;
+    const auto t0 = std::chrono::steady_clock::now();
+    struct Report {
+        std::chrono::steady_clock::time_point t0;
+        const uint64_t* mapped;
+        ~Report() { report_slow("arena growth", t0, *mapped >> 20, 0); }
+    } rep{t0, &arena_bytes_};
     // Physical 256 MiB chunks mapped back to back.  A growth maps at least half the size mapped so
     // far: it runs under the C ABI's device lock, so a window-filling Tonk server should take a
     // handful of growths, not one per 256 MiB.
@@ -262,10 +277,13 @@ bool Device::ensure_slot(Slot& s, size_t bytes) {
     // a bench step's program is ~8 MB: avoid reallocating mid-run
     size_t cap = slot_cap_ ? slot_cap_ : slot_bytes_;
     while (cap < bytes) cap *= 2;
+    const auto t0 = std::chrono::steady_clock::now();
     drain_programs();
     HIPCHK(hipStreamSynchronize((hipStream_t)stream_));
     for (Slot& sl : slots_) sl.ticket = 0;
-    return alloc_slots(cap);
+    const bool ok = alloc_slots(cap);
+    report_slow("program slot growth", t0, cap >> 10, bytes >> 10);
+    return ok;
 }
 
 uint64_t Device::run(Context* const* ctxs, size_t n) {
@@ -336,6 +354,7 @@ void Device::begin(Context* const* ctxs, size_t n, bool closed) {
         const auto w0 = std::chrono::steady_clock::now();
         HIPCHK(hipEventSynchronize((hipEvent_t)slot.done));
         stats_.slot_wait_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
+        report_slow("program slot wait", w0, 0, 0);
         if (slot.ticket > completed_) completed_ = slot.ticket;
         slot.ticket = 0;
     }
