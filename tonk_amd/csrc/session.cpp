@@ -302,16 +302,26 @@ struct Session {
     std::vector<uint32_t> order;
     std::vector<double> stream_ms;
 
-    // Sticky mode (default): thread t first runs its own streams (s % T == t) so a stream's
-    // state stays in the same core's caches from step to step, then takes any stream still
-    // unclaimed, longest first.  Without it streams are handed out longest first only.
+    // Sticky mode (default): thread t first runs its own streams (s % T == t), longest first, so
+    // a stream's state stays in the same core's caches from step to step, then takes any stream
+    // still unclaimed, longest first.  Without it streams are handed out longest first only.
     std::vector<std::atomic<uint8_t>> claimed;
     bool sticky_job = false;
     void drain(const std::function<void(size_t, size_t)>& f, size_t ti) {
         if (sticky_job) {
+            // own streams longest first (by the previous pass), so what is left for others to
+            // steal at the end of a pass is a slow thread's shortest streams
+            static const bool own_fifo = getenv("TONK_AMD_OWN_FIFO") != nullptr;  // A/B switch (profiling)
             const size_t T = threads.size(), n = streams.size();
-            for (size_t s = ti; s < n; s += T)
-                if (!claimed[s].exchange(1)) f(s, ti);
+            if (own_fifo || order.empty()) {
+                for (size_t s = ti; s < n; s += T)
+                    if (!claimed[s].exchange(1)) f(s, ti);
+            } else {
+                for (size_t k = 0; k < n; ++k) {
+                    const size_t s = order[k];
+                    if (s % T == ti && !claimed[s].exchange(1)) f(s, ti);
+                }
+            }
             for (size_t k = 0; k < n; ++k) {
                 const size_t s = order.empty() ? k : order[k];
                 if (!claimed[s].exchange(1)) f(s, ti);
@@ -328,10 +338,12 @@ struct Session {
     // Workers spin on the job generation for a while before sleeping on the condition variable,
     // and the main thread spins for the end of a pass: a step is a few hundred microseconds, so
     // a futex wake-up of 16 threads (and of the main thread) per pass is a visible share of it.
-    // TONK_AMD_SPIN_US sets the spin window (0: always sleep).
+    // TONK_AMD_SPIN_US sets the spin window (0: always sleep); 100 us covers the caller's work
+    // between passes (launch + layout, ~0.05 ms) without keeping 16 spinning threads beside the
+    // caller for long (the job's CPU quota counts them).
     static uint64_t spin_ns() {
         static const uint64_t v = getenv("TONK_AMD_SPIN_US") ? 1000ull * strtoull(getenv("TONK_AMD_SPIN_US"), nullptr, 10)
-                                                            : 300000ull;
+                                                            : 100000ull;
         return v;
     }
     std::atomic<uint64_t> gen{0};
