@@ -206,6 +206,7 @@ void report_disable(const char* where) {
 // fills up.  Adds never take the device lock.
 struct Staging {
     static const size_t kFlushBytes = 1u << 20;  // packet bytes per half before it is sent
+    unsigned stream = 0;             // the codec's launch stream (Device::select_stream)
     uint8_t* half[2] = {nullptr, nullptr};
     size_t cap = 0;                  // bytes per half (packets + descriptors)
     void* sent[2] = {nullptr, nullptr};  // event behind a sent half's copy (not yet waited for)
@@ -255,6 +256,7 @@ struct Staging {
         if (used && (used + n > kFlushBytes || need(used + n, descs.size() + 1) > cap)) {
             {
                 DevLock dl;
+                g_rt->dev.select_stream(stream);
                 send_locked(g_rt->dev);
                 sent[cur] = g_rt->dev.record_event();
                 if (g_rt->dev.failed()) return false;
@@ -286,7 +288,14 @@ struct Codec {
     Staging staging;
     uint8_t* pinned = nullptr;  // D2H landing buffer (recovery packet / recovered rows)
     size_t pinned_cap = 0;
-    Codec() { ctx.rows.init_segmented(&g_rt->pool); }
+    // Codecs are spread over the device's launch streams round robin (a codec's work stays on
+    // its stream, in order; different codecs' programs overlap instead of queueing behind each
+    // other on one stream).
+    Codec() {
+        ctx.rows.init_segmented(&g_rt->pool);
+        static std::atomic<unsigned> next{0};
+        staging.stream = next.fetch_add(1) % g_rt->dev.stream_count();
+    }
     uint64_t byte_offset(RowId r) const { return (uint64_t)ctx.rows.offset(r) * TAMD_ROW_UNIT; }
     // The pinned buffer holds at least n bytes (no copy can be landing in it: every read into it
     // was waited for before the call that issued it returned).
@@ -345,6 +354,7 @@ bool run_and_read(Codec& c, Reads enqueue_reads) {
     {
         DevLock dl;
         Device& dev = g_rt->dev;
+        dev.select_stream(c.staging.stream);
         const uint64_t launches = dev.stats().launches;
         c.staging.send_locked(dev);  // packets added since the last program land first
         if (!ctx.pb.empty()) {
@@ -435,6 +445,11 @@ SIAMESE_EXPORT int siamese_init_(int version) {
         fprintf(stderr, "tonk_amd: device GF(256) self test failed\n");
         return Siamese_Disabled;
     }
+    // One launch stream per hardware queue the runtime gives a process (GPU_MAX_HW_QUEUES, 4 by
+    // default); TONK_AMD_CAPI_STREAMS overrides (1: every codec on one stream).
+    unsigned nstreams = 4;
+    if (const char* a = getenv("TONK_AMD_CAPI_STREAMS")) nstreams = (unsigned)atoi(a);
+    if (nstreams > 1) g_rt->dev.add_streams(nstreams);
     g_rt->ok = true;
     if (const char* w = getenv("TONK_AMD_CAPI_WATCH")) {
         const double period = atof(w) > 0 ? atof(w) : 5.0;

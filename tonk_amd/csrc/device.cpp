@@ -39,7 +39,8 @@ namespace tamd {
 Device::~Device() {
     if (device_ < 0) return;
     hipSetDevice(device_);
-    hipStreamSynchronize((hipStream_t)stream_);
+    if (streams_.empty()) hipStreamSynchronize((hipStream_t)stream_);
+    else for (void* st : streams_) hipStreamSynchronize((hipStream_t)st);
     for (Slot& s : slots_)
         if (s.done) hipEventDestroy((hipEvent_t)s.done);
     if (prog_host_) hipHostFree(prog_host_);
@@ -60,7 +61,7 @@ Device::~Device() {
     if (gdesc_host_) hipHostFree(gdesc_host_);
     if (up_host_) hipHostFree(up_host_);
     if (up_dev_) hipFree(up_dev_);
-    if (sc_dev_) hipFree(sc_dev_);
+    if (sc_dev_ && sc_per_stream_.empty()) hipFree(sc_dev_);
     if (rb_host_) hipHostFree(rb_host_);
     if (up_event_) hipEventDestroy((hipEvent_t)up_event_);
     if (d_gf_) hipFree(d_gf_);
@@ -72,7 +73,32 @@ Device::~Device() {
     } else if (arena_) {
         hipFree(arena_);
     }
-    if (stream_) hipStreamDestroy((hipStream_t)stream_);
+    if (streams_.empty()) {
+        if (stream_) hipStreamDestroy((hipStream_t)stream_);
+    } else {
+        for (void* st : streams_) hipStreamDestroy((hipStream_t)st);
+        for (auto& a : sc_per_stream_)
+            if (a.first) hipFree(a.first);
+    }
+}
+
+void Device::add_streams(unsigned k) {
+    if (!stream_ || !streams_.empty() || k < 2) return;
+    streams_.push_back(stream_);
+    for (unsigned i = 1; i < k; ++i) {
+        hipStream_t st = nullptr;
+        HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        streams_.push_back(st);
+    }
+    sc_per_stream_.assign(k, std::make_pair((uint8_t*)nullptr, (size_t)0));
+}
+
+void Device::sync_all_streams() {
+    if (streams_.empty()) {
+        HIPCHK(hipStreamSynchronize((hipStream_t)stream_));
+        return;
+    }
+    for (void* st : streams_) HIPCHK(hipStreamSynchronize((hipStream_t)st));
 }
 
 bool Device::init(int device, uint64_t arena_bytes) {
@@ -279,7 +305,7 @@ bool Device::ensure_slot(Slot& s, size_t bytes) {
     while (cap < bytes) cap *= 2;
     const auto t0 = std::chrono::steady_clock::now();
     drain_programs();
-    HIPCHK(hipStreamSynchronize((hipStream_t)stream_));
+    sync_all_streams();  // a program on any stream may still read its slot
     for (Slot& sl : slots_) sl.ticket = 0;
     const bool ok = alloc_slots(cap);
     report_slow("program slot growth", t0, cap >> 10, bytes >> 10);
@@ -594,6 +620,13 @@ void Device::mark(uint64_t ticket) {
     }
     HIPCHK(hipEventRecord((hipEvent_t)e, (hipStream_t)stream_));
     inflight_.push_back(std::make_pair(ticket, e));
+    // Callers that wait on their own events (the C ABI) never poll completed(): retire finished
+    // entries here so the list (and the events it holds) stays short.
+    while (inflight_.size() > 64 && hipEventQuery((hipEvent_t)inflight_.front().second) == hipSuccess) {
+        if (inflight_.front().first > completed_) completed_ = inflight_.front().first;
+        free_events_.push_back(inflight_.front().second);
+        inflight_.pop_front();
+    }
 }
 
 bool Device::completed(uint64_t ticket) {
@@ -619,7 +652,7 @@ void Device::wait(uint64_t ticket) {
 void Device::synchronize() {
     drain_programs();
     flush_uploads();
-    HIPCHK(hipStreamSynchronize((hipStream_t)stream_));
+    sync_all_streams();
     for (auto& p : inflight_) free_events_.push_back(p.second);
     inflight_.clear();
     completed_ = ticket_;
@@ -682,11 +715,17 @@ void Device::scatter_upload(uint8_t* src, size_t bytes, const ScatterIn* d, uint
         sd[k].pad = 0;
     }
     const size_t total = at + (size_t)n * sizeof(ScatterDesc);
+    // each stream has its own landing area (reused batch after batch in that stream's order)
+    if (!sc_per_stream_.empty()) {
+        sc_dev_ = sc_per_stream_[cur_stream_].first;
+        sc_cap_ = sc_per_stream_[cur_stream_].second;
+    }
     if (total > sc_cap_) {  // the device landing area grows (after the stream drains)
         HIPCHK(hipStreamSynchronize(st));
         if (sc_dev_) hipFree(sc_dev_);
         sc_cap_ = total + total / 2;
         HIPCHK(hipMalloc((void**)&sc_dev_, sc_cap_));
+        if (!sc_per_stream_.empty()) sc_per_stream_[cur_stream_] = std::make_pair(sc_dev_, sc_cap_);
     }
     // (the landing area is reused batch after batch: copies and scatters are stream ordered)
     HIPCHK(hipMemcpyAsync(sc_dev_, src, total, hipMemcpyHostToDevice, st));

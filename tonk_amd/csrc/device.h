@@ -45,6 +45,15 @@ public:
     uint64_t arena_bytes() const { return arena_bytes_; }
     uint8_t* arena() const { return arena_; }
     void* stream() const { return stream_; }
+    // Several launch streams (the C ABI): add_streams(k) creates k - 1 more streams beside the
+    // first; select_stream(i) makes stream i the one every following enqueue uses (the caller
+    // serialises Device calls).  Work of one codec stays on one stream, so it stays ordered;
+    // work of different codecs overlaps.  synchronize() and slot growth wait for all streams.
+    void add_streams(unsigned k);
+    void select_stream(unsigned i) {
+        if (i < streams_.size()) { stream_ = streams_[i]; cur_stream_ = i; }
+    }
+    unsigned stream_count() const { return streams_.empty() ? 1u : (unsigned)streams_.size(); }
 
     // Enqueue the pending programs of `ctxs` as one merged program (asynchronous).  Returns the
     // completion ticket (monotonic); call completed() / wait() with it.
@@ -204,8 +213,12 @@ private:
     struct ScatterDesc { uint32_t row, len, src, pad; };
     uint8_t* up_host_ = nullptr;
     uint8_t* up_dev_ = nullptr;
-    uint8_t* sc_dev_ = nullptr;  // scatter_upload landing area
+    uint8_t* sc_dev_ = nullptr;  // scatter_upload landing area (of the current stream)
     size_t sc_cap_ = 0;
+    std::vector<void*> streams_;  // all launch streams (add_streams), streams_[0] = the first
+    std::vector<std::pair<uint8_t*, size_t>> sc_per_stream_;  // landing areas of the others
+    unsigned cur_stream_ = 0;
+    void sync_all_streams();
     size_t up_cap_ = 0, up_used_ = 0, up_flushed_ = 0;
     std::vector<ScatterDesc> up_pending_;
     // readback staging: download_async() lands rows in pinned rb_host_; synchronize() copies
