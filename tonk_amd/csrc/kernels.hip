@@ -13,6 +13,9 @@
 #include "program.h"
 
 #define TAMD_WAVES_PER_WG 4
+#ifndef TAMD_BITOP3
+#define TAMD_BITOP3 1  // three-input XORs as v_bitop3_b32 (mul_sel)
+#endif
 #ifndef TAMD_ROLL
 #define TAMD_ROLL 1  // rolling row loads in ACCR runs (run_accr)
 #endif
@@ -113,9 +116,19 @@ __device__ __forceinline__ Sel sel4(uint32_t x) {
     s.s2 = (x >> 6) & 0x03030303u;
     return s;
 }
+// a ^ b ^ c in one gfx950 v_bitop3_b32 (truth table 0x96); the compiler emits two v_xor_b32.
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+#if TAMD_BITOP3
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+#else
+    return a ^ b ^ c;
+#endif
+}
 __device__ __forceinline__ uint32_t mul_sel(const Sel& s, const PermT& p) {
-    return __builtin_amdgcn_perm(p.t[1], p.t[0], s.s0) ^ __builtin_amdgcn_perm(p.t[3], p.t[2], s.s1) ^
-           __builtin_amdgcn_perm(p.t[5], p.t[4], s.s2);
+    return xor3(__builtin_amdgcn_perm(p.t[1], p.t[0], s.s0), __builtin_amdgcn_perm(p.t[3], p.t[2], s.s1),
+                __builtin_amdgcn_perm(p.t[5], p.t[4], s.s2));
 }
 __device__ __forceinline__ u64 mul8(u64 x, const PermT& p) {
     const Sel lo = sel4((uint32_t)x), hi = sel4((uint32_t)(x >> 32));
