@@ -381,7 +381,8 @@ void Device::begin(Context* const* ctxs, size_t n, bool closed) {
         HIPCHK(hipEventSynchronize((hipEvent_t)slot.done));
         stats_.slot_wait_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
         report_slow("program slot wait", w0, 0, 0);
-        if (slot.ticket > completed_) completed_ = slot.ticket;
+        // (ticket order is completion order only on a single stream)
+        if (streams_.empty() && slot.ticket > completed_) completed_ = slot.ticket;
         slot.ticket = 0;
     }
     P.slot = &slot;
@@ -623,7 +624,7 @@ void Device::mark(uint64_t ticket) {
     // Callers that wait on their own events (the C ABI) never poll completed(): retire finished
     // entries here so the list (and the events it holds) stays short.
     while (inflight_.size() > 64 && hipEventQuery((hipEvent_t)inflight_.front().second) == hipSuccess) {
-        if (inflight_.front().first > completed_) completed_ = inflight_.front().first;
+        if (streams_.empty() && inflight_.front().first > completed_) completed_ = inflight_.front().first;
         free_events_.push_back(inflight_.front().second);
         inflight_.pop_front();
     }

@@ -48,7 +48,9 @@ public:
     // Several launch streams (the C ABI): add_streams(k) creates k - 1 more streams beside the
     // first; select_stream(i) makes stream i the one every following enqueue uses (the caller
     // serialises Device calls).  Work of one codec stays on one stream, so it stays ordered;
-    // work of different codecs overlaps.  synchronize() and slot growth wait for all streams.
+    // work of different codecs overlaps.  synchronize() and slot growth wait for all streams;
+    // completed()/wait() tickets assume one stream (the session), callers with several streams
+    // wait on their own events (record_event / event_wait).
     void add_streams(unsigned k);
     void select_stream(unsigned i) {
         if (i < streams_.size()) { stream_ = streams_[i]; cur_stream_ = i; }
