@@ -417,11 +417,13 @@ uint32_t LaneSums::chunk() {
 
 void LaneSums::reset(RowTable& rows) {
     if (!snaps_.empty()) {
-        Closed c;
+        // Closed entries are reused across flushes: the swap hands this scan's lists to the entry
+        // and takes back the storage of an earlier one, so neither side reallocates as it grows.
+        if (n_closed_ == closed_.size()) closed_.emplace_back();
+        Closed& c = closed_[n_closed_++];
         for (unsigned s = 0; s < 3; ++s) c.base[s] = base_[s];
         c.terms.swap(terms_);
         c.snaps.swap(snaps_);
-        closed_.push_back(std::move(c));
     } else {
         for (unsigned s = 0; s < 3; ++s) rows.free_deferred(base_[s]);
     }
@@ -570,12 +572,13 @@ void LaneSums::emit_scan(RowTable& rows, ProgramBuilder& pb, const RowId* base, 
 
 void LaneSums::flush(RowTable& rows, ProgramBuilder& pb, const ExpansionTable& ex) {
     TAMD_PROF_SCOPE(kChainFlush);
-    for (Closed& c : closed_) {
+    for (size_t i = 0; i < n_closed_; ++i) {
+        Closed& c = closed_[i];
         emit_scan(rows, pb, c.base, c.terms, c.snaps, nullptr);
         for (unsigned s = 0; s < 3; ++s) rows.free_deferred(c.base[s]);
         for (const Snap& sn : c.snaps) rows.free_deferred(sn.row);
     }
-    closed_.clear();
+    n_closed_ = 0;
 
     if (terms_.empty() && dyn_.empty()) {
         // Nothing accumulated since the last flush: snapshots (if any) alias the bases.
@@ -622,11 +625,12 @@ void LaneSums::flush(RowTable& rows, ProgramBuilder& pb, const ExpansionTable& e
 }
 
 void LaneSums::release(RowTable& rows) {
-    for (Closed& c : closed_) {
+    for (size_t i = 0; i < n_closed_; ++i) {
+        Closed& c = closed_[i];
         for (unsigned s = 0; s < 3; ++s) rows.free_deferred(c.base[s]);
         for (const Snap& sn : c.snaps) rows.free_deferred(sn.row);
     }
-    closed_.clear();
+    n_closed_ = 0;
     for (const Snap& sn : snaps_) rows.free_deferred(sn.row);
     for (unsigned s = 0; s < 3; ++s) {
         rows.free_deferred(base_[s]);

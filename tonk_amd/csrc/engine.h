@@ -316,7 +316,8 @@ private:
     std::vector<T> dyn_;                        // packets produced in this program (level > 0)
     // closed epochs (reset while the program was pending) still owe their snapshots
     struct Closed { RowId base[3]; std::vector<T> terms; std::vector<Snap> snaps; };
-    std::vector<Closed> closed_;
+    std::vector<Closed> closed_;  // [0, n_closed_) pending; the rest keep storage for reuse
+    size_t n_closed_ = 0;
     static void emit_scan(RowTable& rows, ProgramBuilder& pb, const RowId* base, const std::vector<T>& terms,
                           const std::vector<Snap>& snaps, const RowId* final_rows);
 };
