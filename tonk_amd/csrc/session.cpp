@@ -450,6 +450,7 @@ struct Session {
     // costs nothing while the host sets the pace.
     bool deferred = false;       // set at create: pipelined and not host-staged
     bool have_closed = false;    // a closed program is laid out (dev.begin) and awaits its fill
+    std::atomic<size_t> fills_left{0};  // early launch: streams of the pass not yet filled
     uint64_t closed_epoch = 0;
 
     void step(uint32_t originals, bool finish) {
@@ -548,12 +549,19 @@ struct Session {
         std::fill(fill_ms.begin(), fill_ms.end(), 0.0);
         init_order();
         const bool fill = have_closed;
-        run_all([this, originals, finish, rel, fill, &ms](size_t i, size_t ti) {
+        // Early launch: the thread that fills the last stream launches the program at once
+        // (the other threads only run control planes, which touch no device state) instead of the
+        // caller after the pass.  Record mode reads digests at launch, so it launches after.
+        static const bool early_ok = getenv("TONK_AMD_LATE_LAUNCH") == nullptr;  // A/B switch
+        const bool early = fill && early_ok && !prm.record && !threads.empty();
+        if (early) fills_left.store(streams.size(), std::memory_order_relaxed);
+        run_all([this, originals, finish, rel, fill, early, &ms](size_t i, size_t ti) {
             const auto w0 = clk::now();
             Context& c = *ctxs[i];
             if (fill) {
                 dev.fill(i);
                 fill_ms[ti] += ms(w0, clk::now());
+                if (early && fills_left.fetch_sub(1, std::memory_order_acq_rel) == 1) launch_closed();
             }
             c.rows.release_up_to(rel);
             if (finish) streams[i]->runner->finish();
@@ -568,7 +576,7 @@ struct Session {
         const auto t1 = clk::now();
         account_busy();
         for (double f : fill_ms) host_ms[3] += f / (double)fill_ms.size();
-        if (fill) launch_closed();
+        if (fill && !early) launch_closed();
         const auto t2 = clk::now();
         std::vector<Context*> cs;
         for (auto& c : ctxs) cs.push_back(c.get());
