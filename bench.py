@@ -100,16 +100,114 @@ def host_cpus() -> int:
         return os.cpu_count() or 8
 
 
-def pmc_traffic() -> tuple:
-    """HBM bytes per tamd_exec launch from the committed rocprofv3 PMC passes of this workload
-    (tools/gpu_round.sh -> tools/pmc_traffic.py -> profiles/pmc_traffic.json), or (None, None)."""
-    p = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+def _timed_counter_values(csv_dir: str, counter: str, kernel: str = "tamd_exec16") -> list[float]:
+    """Per-dispatch values of `counter` for `kernel`'s dispatches inside the timed region (between
+    the two tamd_timed_region markers Device::set_timing launches), in dispatch order."""
+    import csv
+    import glob
+    rows = []
+    for f in glob.glob(os.path.join(csv_dir, "**", "*counter_collection*.csv"), recursive=True):
+        with open(f) as fh:
+            for r in csv.DictReader(fh):
+                if r.get("Counter_Name") == counter:
+                    rows.append((int(r["Dispatch_Id"]), r["Kernel_Name"], float(r["Counter_Value"])))
+    rows.sort()
+    marks = [i for i, r in enumerate(rows) if r[1].startswith("tamd_timed_region")]
+    if len(marks) < 2:
+        return []
+    return [v for _, k, v in rows[marks[0] + 1:marks[1]] if k.split("(")[0].strip() == kernel]
+
+
+def pmc_traffic(workload: str, steps: int, warmup: int, timeout_s: int = 240) -> dict | None:
+    """HBM traffic per timed executor launch of THIS workload, measured now: two rocprofv3 PMC
+    passes (FETCH_SIZE, then WRITE_SIZE: they do not fit one TCC pass) over a rerun of the same
+    workload with the same steps (child processes), restricted to the dispatches between the
+    timed-region markers, so the launches counted are the ones the line's roofline averages.  gfx950 corrections (MI355X_MICROARCH.md, HBM): FETCH_SIZE counts half
+    the bytes of 16-B-per-lane reads (the executor's width), so it is doubled; WRITE_SIZE is exact
+    for 16-B stores.  Both counters are KiB and count L2 fabric requests (Infinity-Cache hits
+    included).  Returns None when rocprofv3 is unavailable or a pass fails."""
+    import shutil
+    import signal
+    import tempfile
+    rp = shutil.which("rocprofv3")
+    if not rp:
+        return None
+    vals, alg = {}, []
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = tempfile.mkdtemp(prefix=f"tamd_pmc_{counter.lower()}_", dir="/tmp")
+        cmd = [rp, "--pmc", counter, "--kernel-trace", "--output-format", "csv", "-d", d, "-o", "run", "--",
+               sys.executable, os.path.abspath(__file__), "--workload", workload, "--steps", str(steps),
+               "--warmup", str(warmup), "--no-cpu-baseline", "--no-end-to-end", "--no-verify", "--no-pmc"]
+        env = dict(os.environ, TMPDIR="/tmp")
+        p = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True, cwd="/tmp",
+                             env=env, start_new_session=True)
+        try:
+            out, _ = p.communicate(timeout=timeout_s)
+        except subprocess.TimeoutExpired:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.wait()
+            return {"error": f"{counter} pass timed out"}
+        if p.returncode != 0:
+            return {"error": f"{counter} pass exited {p.returncode}"}
+        try:
+            line = json.loads([l for l in out.splitlines() if l.startswith("{")][-1])
+            alg.append(float(line["roofline"]["alg_bytes_per_launch"]))
+        except (IndexError, KeyError, TypeError, ValueError):
+            return {"error": f"{counter} pass printed no bench line"}
+        vals[counter] = _timed_counter_values(d, counter)
+        shutil.rmtree(d, ignore_errors=True)
+        if not vals[counter]:
+            return {"error": f"{counter}: no timed tamd_exec16 dispatches in the counter csv"}
+    f, w = vals["FETCH_SIZE"], vals["WRITE_SIZE"]
+    per = [(a * 2.0 + b) * 1024.0 for a, b in zip(f, w)]
+    mean = sum(per) / len(per)
+    alg_pl = sum(alg) / len(alg)
+    return {"traffic_per_timed_launch": round(mean, 1), "traffic_over_alg": round(mean / alg_pl, 4),
+            "alg_bytes_per_launch": round(alg_pl, 1), "timed_dispatches": len(per),
+            "per_launch_mb": [round(x / 1e6, 1) for x in per],
+            "read_bytes_per_launch": round(sum(f) / len(f) * 2048.0, 1),
+            "write_bytes_per_launch": round(sum(w) / len(w) * 1024.0, 1),
+            "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this workload (--steps {steps} "
+                      f"--warmup {warmup}), timed-region dispatches; FETCH x2, WRITE x1 (gfx950)"}
+
+
+def verify_schedule(threads: int, device: int) -> dict:
+    """Byte-check of the timed schedule (untimed pass): the bench configuration's fixture
+    (tests/golden/scenarios.json "bench": 64 streams x 49152 originals, 1% loss, ack 64, made by
+    the reference codec) through one session with the bench's threads, deferred fill and early
+    launch, rows released at their program's completion; every recovery packet and recovered
+    original is digested on the launch stream right after the launch that completes its
+    program (record mode), and each stream's transcript digest must equal the reference's."""
+    import hashlib
+    path = os.path.join(ROOT, "tests", "golden", "scenarios.json")
     try:
-        with open(p) as f:
-            j = json.load(f)
-        return j.get("traffic_bytes_per_launch"), os.path.relpath(p, ROOT)
-    except (OSError, ValueError):
-        return None, None
+        with open(path) as f:
+            entry = json.load(f)["bench"]
+    except (OSError, ValueError, KeyError):
+        return {"digests_match": None, "note": "fixture missing"}
+    wp = tonk_amd.WorkloadParams.from_args(entry["args"])
+    n_streams = len(entry["streams"])
+    t0 = time.perf_counter()
+    sess = tonk_amd.Session(wp, n_streams=n_streams, device=device, threads=threads,
+                            arena_bytes=2 * wp.n * n_streams * 1344 + (4 << 30), record=True)
+    try:
+        sess.generate()
+        done = 0
+        while done < wp.n:
+            sess.step(min(ORIGINALS_PER_STEP, wp.n - done))
+            done += ORIGINALS_PER_STEP
+        sess.finish()
+        bad = []
+        for i in range(n_streams):
+            want = entry["streams"][str(i)]
+            got = hashlib.sha256((sess.transcript(i) + want["summary"] + "\n").encode()).hexdigest()
+            if got != want["sha256"]:
+                bad.append(i)
+    finally:
+        sess.close()
+    return {"digests_match": not bad, "streams_differing": bad, "streams": n_streams, "originals_per_stream": wp.n,
+            "seconds": round(time.perf_counter() - t0, 2),
+            "schedule": f"{threads} host threads, deferred fill, early launch, release at completion"}
 
 
 def end_to_end(threads: int, device: int, loss: float, steps: int = 3, warmup: int = 1) -> dict | None:
@@ -364,6 +462,19 @@ class Dist:
             self.dist.destroy_process_group()
 
 
+MAX_CORES = 128
+
+
+def pad_cores(cores: list[int]) -> list[float]:
+    """A rank's core list as a fixed-size vector for all_gather (-1 = none)."""
+    c = list(cores)[:MAX_CORES]
+    return [float(x) for x in c] + [-1.0] * (MAX_CORES - len(c))
+
+
+def unpad_cores(v: list[float]) -> list[int]:
+    return [int(x) for x in v if x >= 0]
+
+
 def free_port() -> int:
     import socket
     with socket.socket() as so:
@@ -392,6 +503,8 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-end-to-end", action="store_true", help="skip the PCIe-inclusive side measurement")
+    ap.add_argument("--no-verify", action="store_true", help="skip the untimed byte check of the timed schedule")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 HBM-traffic passes (roofline.traffic)")
     ap.add_argument("--workload", choices=sorted(BATCHED) + sorted(SINGLE_STREAM) + ["compress"], default="cfg3",
                     help="BASELINE.json configs[] index: cfg3 (the headline, 64 streams per GPU), cfg2 (64 "
                          "streams, 2%% loss), cfg1 / cfg4 (one stream, start to finish)")
@@ -432,11 +545,19 @@ def main() -> int:
     loss = BATCHED[a.workload]["loss"]
     d = Dist(world)
     if a.dry_run:
-        bases = d.gather([float(stream_base(rank)), float(rank), float(local_rank)])
+        # Host-core plan without a GPU: TONK_AMD_TOPOLOGY lists every device's NUMA local_cpulist
+        # (';'-separated, one CPU per core), as /sys/bus/pci/devices/<gpu>/local_cpulist gives
+        # them on a GPU node; the session computes the same plan there (tamd_cpu_share).
+        topo = os.environ.get("TONK_AMD_TOPOLOGY")
+        cores = []
+        if topo:
+            lists = topo.split(";")
+            cores = tonk_amd.cpu_share(lists, local_rank, lists[local_rank], os.environ.get("TONK_AMD_CPU_SLOT"))
+        bases = d.gather([float(stream_base(rank)), float(rank), float(local_rank)] + pad_cores(cores))
         if rank == 0:
             print(json.dumps({"dry_run": True, "n_gpus": world, "streams_per_gpu": STREAMS_PER_GPU,
-                              "ranks": [{"rank": int(r), "local_rank": int(lr), "stream_base": int(b)}
-                                        for b, r, lr in bases]}), flush=True)
+                              "ranks": [{"rank": int(v[1]), "local_rank": int(v[2]), "stream_base": int(v[0]),
+                                         "host_cores": unpad_cores(v[3:])} for v in bases]}), flush=True)
         d.close()
         return 0
 
@@ -448,6 +569,7 @@ def main() -> int:
                             stream_base=stream_base(rank), threads=threads,
                             arena_bytes=(2 * n_orig * STREAMS_PER_GPU * 1344) + (4 << 30))
     sess.generate()
+    rank_cores = d.gather(pad_cores(sess.cpus()))
 
     for _ in range(a.warmup):
         sess.step(ORIGINALS_PER_STEP)
@@ -484,7 +606,8 @@ def main() -> int:
     all_ok = d.allsum(0.0 if ok else 1.0) == 0.0
 
     achieved = alg / (kernel_ms / 1e3) / 1e9 if kernel_ms > 0 else 0.0
-    traffic, traffic_src = pmc_traffic()
+    pmc = pmc_traffic(a.workload, a.steps, a.warmup) if (rank == 0 and world == 1 and not a.no_pmc) else None
+    traffic = pmc.get("traffic_per_timed_launch") if pmc else None
     workload = {
         "cfg3": "configs[3] per-GPU shard: 64 independent streams/GPU, 4096 originals per stream per step, "
                 "1300 B payloads, 1% uniform loss, f=2%, ack every 64",
@@ -509,6 +632,8 @@ def main() -> int:
             "streams_per_gpu": STREAMS_PER_GPU, "originals_per_step": ORIGINALS_PER_STEP, "payload_bytes": PAYLOAD,
             "loss": loss, "ack_every": ACK, "host_threads_per_gpu": threads,
             "parallelism": f"streams sharded {STREAMS_PER_GPU}/GPU x {world} GPU, no collective",
+            # each rank's pinned worker cores (its share of its GPU's NUMA node, tamd_cpu_share)
+            "host_cores": [unpad_cores(v) for v in rank_cores],
         },
         "roofline": {
             "bound": "hbm",
@@ -517,7 +642,8 @@ def main() -> int:
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": round(traffic, 1) if traffic else None,
-            "traffic_source": traffic_src,
+            "traffic_over_alg": pmc.get("traffic_over_alg") if pmc else None,
+            "pmc": pmc,
             "kernel": "tamd_exec16",
             "launches": launches,
             "avg_launch_us": round(kernel_ms * 1e3 / launches, 3) if launches else None,
@@ -538,11 +664,15 @@ def main() -> int:
         out["cpu_baseline"] = cpu_baseline(min(host_cpus(), threads * local_world))
     if rank == 0 and world == 1 and not a.no_end_to_end:
         out["end_to_end"] = end_to_end(threads, local_rank, loss)
+    if rank == 0 and a.workload == "cfg3" and not a.no_verify:
+        v = verify_schedule(threads, local_rank)
+        out["checks"]["digests_match"] = v["digests_match"]
+        out["checks"]["verify"] = v
     d.barrier()
     if rank == 0:
         print(json.dumps(out), flush=True)
     d.close()
-    return 0 if all_ok else 1
+    return 0 if all_ok and out["checks"].get("digests_match") is not False else 1
 
 
 if __name__ == "__main__":

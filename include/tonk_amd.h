@@ -26,7 +26,10 @@ typedef struct tamd_session_params {
     uint32_t payload_min, payload_max;
     uint32_t loss_thresh, ge_enable, gb_thresh, bg_thresh, loss_on_recovery;
     uint32_t fec_rate_q16, ack_every, ack_bytes, arq_lag, flush_max;
-    uint32_t record;           /* 1: keep per-stream transcripts (parity checks, not timed) */
+    uint32_t record;           /* 1: keep per-stream transcripts (parity checks, not timed).  The
+                                  schedule is the timed one (early launch, rows released at their
+                                  program's completion); the rows are digested on the launch
+                                  stream right after the launch that completes their program. */
     uint32_t stage_host;       /* 1: packets start and end in pinned host memory: every step copies
                                   its originals H2D (both codec sides), its recovery packets and
                                   recovered originals D2H and the received recovery packets H2D
@@ -76,6 +79,16 @@ const char* tamd_session_error(void* s);
    from `fn` instead of the monotonic clock (null restores it).  Used to compare
    siamese_encoder_retransmit with the reference under a virtual clock. */
 void  tamd_set_clock(uint64_t (*fn)(void));
+
+/* The CPUs the session's worker threads are pinned to (count returned; empty = not pinned). */
+unsigned tamd_session_cpus(void* s, int* out, unsigned cap);
+/* Host-core plan of one GPU's worker pool (pure, no device needed): `dev_cpulists` holds every
+   device's NUMA local_cpulist separated by ';', `node_cores` the usable cores of `device`'s node
+   (one CPU per core).  The devices sharing that node split its cores into equal contiguous
+   shares in device order; `slot_override` "k/n" (TONK_AMD_CPU_SLOT) fixes the share instead.
+   Returns the number of CPUs of the share (written to out[0..cap)). */
+unsigned tamd_cpu_share(const char* dev_cpulists, unsigned device, const char* node_cores,
+                        const char* slot_override, int* out, unsigned cap);
 
 /* Device self test: v_perm GF(2^8) multiply against the host tables (all 65536 products). */
 int   tamd_device_selftest(uint32_t device, char* err, size_t err_len);

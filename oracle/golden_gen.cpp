@@ -14,7 +14,7 @@
 #include "siamese.h"
 
 #include "../tonk_amd/csrc/workload.h"
-#include "transcript.h"
+#include "../tonk_amd/csrc/transcript.h"
 
 #include <chrono>
 #include <dlfcn.h>

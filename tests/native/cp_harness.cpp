@@ -9,7 +9,7 @@
 #include "../../tonk_amd/csrc/encoder.h"
 #include "../../tonk_amd/csrc/decoder.h"
 #include "../../tonk_amd/csrc/workload.h"
-#include "../../oracle/transcript.h"
+#include "../../tonk_amd/csrc/transcript.h"
 #include "../../oracle/siamese_oracle.h"
 
 #include <stdio.h>

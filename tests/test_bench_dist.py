@@ -73,3 +73,52 @@ def test_bench_gpus_flag_spawns_ranks():
     per = j["streams_per_gpu"]
     shards = [set(range(x["stream_base"], x["stream_base"] + per)) for x in ranks]
     assert not (shards[0] & shards[1]) and ranks[1]["stream_base"] == per
+
+
+# A 2-socket 8-GPU node as the MI355X platform lays it out: GPUs 0-3 on socket 0 (cores 0-63,
+# SMT siblings 128-191), GPUs 4-7 on socket 1 (64-127, 192-255); one CPU per core is usable.
+NODE0 = ",".join(str(c) for c in range(64))
+NODE1 = ",".join(str(c) for c in range(64, 128))
+TOPOLOGY = [NODE0] * 4 + [NODE1] * 4
+
+
+def test_cpu_share_eight_ranks_disjoint():
+    """Each GPU's worker pool gets its own 16 cores of its socket: the 8 ranks' sets are
+    disjoint, every set lies in its GPU's NUMA node, and together they cover the 128 cores."""
+    import tonk_amd
+    shares = [tonk_amd.cpu_share(TOPOLOGY, d, TOPOLOGY[d]) for d in range(8)]
+    for d, s in enumerate(shares):
+        assert len(s) == 16, (d, s)
+        node = set(range(0, 64)) if d < 4 else set(range(64, 128))
+        assert set(s) <= node
+    flat = [c for s in shares for c in s]
+    assert len(flat) == len(set(flat)) == 128
+
+
+def test_cpu_share_edge_cases():
+    import tonk_amd
+    # one GPU per node keeps the whole node; an uneven split gives the remainder to the first
+    assert tonk_amd.cpu_share(["0-7"], 0, "0-7") == list(range(8))
+    three = [tonk_amd.cpu_share(["0-9"] * 3, d, "0-9") for d in range(3)]
+    assert three == [[0, 1, 2, 3], [4, 5, 6], [7, 8, 9]]
+    # more ranks than cores: no share is possible, every rank keeps the node (not pinned apart)
+    assert tonk_amd.cpu_share(["0-1"] * 4, 3, "0-1") == [0, 1]
+    # the override fixes the share when a launcher hides the other GPUs
+    assert tonk_amd.cpu_share(["0-63"], 0, NODE0, "2/4") == list(range(32, 48))
+    assert tonk_amd.cpu_share(["0-63"], 0, NODE0, "9/4") == list(range(64))  # invalid: ignored
+
+
+def test_bench_dry_run_core_plan_disjoint():
+    """`bench.py --gpus 2 --dry-run` on two GPUs of one socket: each rank reports its planned
+    cores and the two lists are disjoint."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
+    env["TONK_AMD_TOPOLOGY"] = ";".join(TOPOLOGY)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    j = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    c0, c1 = (x["host_cores"] for x in j["ranks"])
+    assert c0 == list(range(16)) and c1 == list(range(16, 32))
+    assert not set(c0) & set(c1)

@@ -16,7 +16,7 @@ import os
 import subprocess
 
 __all__ = ["LIB_PATH", "build", "lib", "Session", "WorkloadParams", "loss_threshold", "ge_thresholds",
-           "fec_q16", "device_selftest", "SUMMARY_FIELDS"]
+           "fec_q16", "device_selftest", "cpu_share", "SUMMARY_FIELDS"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libtonk_amd.so")
@@ -61,6 +61,10 @@ def lib() -> ctypes.CDLL:
         L.tamd_session_error.argtypes = [vp]
         L.tamd_session_destroy.restype = None
         L.tamd_session_destroy.argtypes = [vp]
+        L.tamd_session_cpus.restype = ctypes.c_uint
+        L.tamd_session_cpus.argtypes = [vp, ctypes.POINTER(ctypes.c_int), ctypes.c_uint]
+        L.tamd_cpu_share.restype = ctypes.c_uint
+        L.tamd_cpu_share.argtypes = [cp, ctypes.c_uint, cp, cp, ctypes.POINTER(ctypes.c_int), ctypes.c_uint]
         L.tamd_device_selftest.restype = ctypes.c_int
         L.tamd_device_selftest.argtypes = [u32, cp, sz]
         _lib = L
@@ -141,6 +145,15 @@ class WorkloadParams:
         return wp
 
 
+def cpu_share(dev_cpulists: list[str], device: int, node_cores: str, slot_override: str | None = None) -> list[int]:
+    """Host cores of `device`'s worker pool (include/tonk_amd.h tamd_cpu_share; pure, no GPU):
+    the devices with the same NUMA local_cpulist split `node_cores` in device order."""
+    out = (ctypes.c_int * 4096)()
+    n = lib().tamd_cpu_share(";".join(dev_cpulists).encode(), device, node_cores.encode(),
+                             slot_override.encode() if slot_override else None, out, 4096)
+    return [int(out[i]) for i in range(min(n, 4096))]
+
+
 def device_selftest(device: int = 0) -> None:
     err = ctypes.create_string_buffer(512)
     rc = lib().tamd_device_selftest(device, err, len(err))
@@ -204,6 +217,12 @@ class Session:
         out = (ctypes.c_double * 10)()
         lib().tamd_session_host_ms(self._h, out)
         return dict(zip(self.HOST_PHASES, [float(v) for v in out]))
+
+    def cpus(self) -> list[int]:
+        """CPUs the worker threads are pinned to (empty: not pinned)."""
+        out = (ctypes.c_int * 1024)()
+        n = lib().tamd_session_cpus(self._h, out, 1024)
+        return [int(out[i]) for i in range(min(n, 1024))]
 
     def transcript(self, stream: int) -> str:
         need = lib().tamd_session_transcript(self._h, stream, None, 0)

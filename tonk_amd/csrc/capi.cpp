@@ -107,6 +107,7 @@ struct DevLock {
             while (w > m && !g_lock_wait_max_ns.compare_exchange_weak(m, w)) {}
         }
         if (g_watch) held_since = now_ns();
+        g_rt->dev.bind_thread();  // Tonk calls from many threads; every Device call targets its GPU
     }
     ~DevLock() {
         if (!g_watch) return;

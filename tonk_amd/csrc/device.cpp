@@ -22,6 +22,9 @@ struct GenDescDev { uint32_t row, index, len, pad; unsigned long long seed; };
 struct DigestDescDev { uint32_t row, skip, len, pad; };
 extern "C" __global__ void tamd_gen_rows(const GenDescDev*, uint32_t, uint8_t*, uint32_t);
 extern "C" __global__ void tamd_digest_rows(const DigestDescDev*, uint32_t, const uint8_t*, unsigned long long*);
+struct VerifyDescDev { uint32_t row, len, mode, pad; };
+struct VerifyOutDev { unsigned long long hash; uint32_t len, ok; };
+extern "C" __global__ void tamd_verify_rows(const VerifyDescDev*, uint32_t, const uint8_t*, VerifyOutDev*);
 
 namespace tamd {
 
@@ -66,6 +69,8 @@ Device::~Device() {
     if (up_event_) hipEventDestroy((hipEvent_t)up_event_);
     if (d_gf_) hipFree(d_gf_);
     if (d_zero_) hipFree(d_zero_);
+    for (VerifyBatch& b : vbatches_)
+        if (b.dev_desc) hipFree(b.dev_desc);
     if (reserved_bytes_) {
         hipMemUnmap(arena_, arena_bytes_);
         for (auto& c : chunks_) hipMemRelease((hipMemGenericAllocationHandle_t)c.first);
@@ -80,6 +85,10 @@ Device::~Device() {
         for (auto& a : sc_per_stream_)
             if (a.first) hipFree(a.first);
     }
+}
+
+void Device::bind_thread() const {
+    if (device_ >= 0) hipSetDevice(device_);  // (a thread-local assignment in HIP: cheap)
 }
 
 void Device::add_streams(unsigned k) {
@@ -503,6 +512,7 @@ void Device::retire_done() {
         HIPCHK(hipEventRecord((hipEvent_t)p.slot->done, (hipStream_t)stream_));
         p.slot->ticket = p.ticket;
         mark(p.ticket);
+        if (p.verify >= 0) run_verify(p.verify);
         progs_.pop_front();
     }
 }
@@ -524,6 +534,8 @@ uint64_t Device::launch() {
         ticket_is_empty_ = true;
         mark(ticket);  // done once everything enqueued before it is done
         ticket_is_empty_ = false;
+        if (pending_verify_ >= 0) run_verify(pending_verify_);
+        pending_verify_ = -1;
         return ticket;
     }
     hipStream_t st = (hipStream_t)stream_;
@@ -546,6 +558,8 @@ uint64_t Device::launch() {
     cur.level_coop = P.level_coop;
     cur.slot = &slot;
     cur.ticket = ticket;
+    cur.verify = pending_verify_;
+    pending_verify_ = -1;
     // Profiling only: TONK_AMD_STAMPS=<program number> records per-item start/end stamps of that
     // program's launches and writes them to tonk_amd_stamps.bin (u64 triples per item; levels
     // delimited by the item bases printed to stderr).  A stamped program runs alone.
@@ -577,6 +591,7 @@ uint64_t Device::launch() {
         HIPCHK(hipEventRecord((hipEvent_t)slot.done, st));
         slot.ticket = ticket;
         mark(ticket);
+        if (cur.verify >= 0) run_verify(cur.verify);
     }
     HIPCHK(hipGetLastError());
     if (stamp_this) {
@@ -916,6 +931,53 @@ void Device::digest_rows(const std::vector<DigestDesc>& d, std::vector<uint64_t>
     HIPCHK(hipStreamSynchronize(st));
     hipFree(dd);
     hipFree(dout);
+}
+
+void Device::verify_next(const std::vector<VerifyDesc>& d) {
+    if (d.empty()) return;
+    VerifyBatch b;
+    b.host = d;
+    b.count = (uint32_t)d.size();
+    uint8_t* mem = nullptr;
+    HIPCHK(hipMalloc((void**)&mem, d.size() * (sizeof(VerifyDesc) + sizeof(VerifyOut))));
+    if (!mem) return;
+    b.dev_desc = (VerifyDesc*)mem;
+    b.dev_out = (VerifyOut*)(mem + d.size() * sizeof(VerifyDesc));
+    HIPCHK(hipMemcpyAsync(b.dev_desc, b.host.data(), d.size() * sizeof(VerifyDesc), hipMemcpyHostToDevice,
+                          (hipStream_t)stream_));
+    vbatches_.push_back(std::move(b));
+    if (pending_verify_ >= 0) run_verify(pending_verify_);  // (a batch no launch took: digest now)
+    pending_verify_ = (int)vbatches_.size() - 1;
+}
+
+void Device::run_verify(int batch) {
+    const VerifyBatch& b = vbatches_[batch];
+    hipLaunchKernelGGL(tamd_verify_rows, dim3((b.count + 63) / 64), dim3(64), 0, (hipStream_t)stream_,
+                       (const VerifyDescDev*)b.dev_desc, b.count, (const uint8_t*)arena_, (VerifyOutDev*)b.dev_out);
+    HIPCHK(hipGetLastError());
+}
+
+void Device::verify_results(std::vector<VerifyOut>& out) {
+    if (pending_verify_ >= 0) {  // registered but never launched: its rows exist already
+        run_verify(pending_verify_);
+        pending_verify_ = -1;
+    }
+    synchronize();
+    out.clear();
+    for (size_t k = vread_; k < vbatches_.size(); ++k) {
+        const VerifyBatch& b = vbatches_[k];
+        const size_t at = out.size();
+        out.resize(at + b.count);
+        HIPCHK(hipMemcpy(out.data() + at, b.dev_out, b.count * sizeof(VerifyOut), hipMemcpyDeviceToHost));
+    }
+}
+
+void Device::verify_reset() {
+    for (size_t k = vread_; k < vbatches_.size(); ++k) {
+        if (vbatches_[k].dev_desc) hipFree(vbatches_[k].dev_desc);
+        vbatches_[k] = VerifyBatch();
+    }
+    vread_ = vbatches_.size();
 }
 
 bool Device::gf_selftest() {

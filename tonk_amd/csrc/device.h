@@ -43,6 +43,10 @@ public:
     const std::string& error() const { return error_; }
     bool failed() const { return failed_; }  // any HIP call failed (sticky; safe to read unlocked)
     uint64_t arena_bytes() const { return arena_bytes_; }
+    int device() const { return device_; }
+    // Make this device current on the calling thread: HIP's current device is
+    // per thread, and events, streams and allocations of a call belong to the current one.
+    void bind_thread() const;
     uint8_t* arena() const { return arena_; }
     void* stream() const { return stream_; }
     // Several launch streams (the C ABI): add_streams(k) creates k - 1 more streams beside the
@@ -111,6 +115,19 @@ public:
     void generate_rows(const std::vector<GenDesc>& d, uint32_t row_cap);
     struct DigestDesc { uint32_t row, skip, len, pad; };
     void digest_rows(const std::vector<DigestDesc>& d, std::vector<uint64_t>& out);
+
+    // Output verification of the schedule as it runs (the session's record mode): the rows of
+    // the next launched program are digested on the launch stream right after the launch that
+    // completes that program, i.e. before any later launch can rewrite or reuse them, so the
+    // timed schedule (early launch, release at completion) is checked unchanged.  `mode` 0:
+    // FNV-1a over `len` bytes; 1: a length-prefixed original (`len` = its upper bound), FNV-1a
+    // over the payload the header announces.  Results are read after synchronize(), in the
+    // order the descriptors were given over all calls.
+    struct VerifyDesc { uint32_t row, len, mode, pad; };
+    struct VerifyOut { uint64_t hash; uint32_t len, ok; };
+    void verify_next(const std::vector<VerifyDesc>& d);
+    void verify_results(std::vector<VerifyOut>& out);  // all results so far (synchronizes)
+    void verify_reset();                               // drop results read (after verify_results)
     bool gf_selftest();  // device v_perm multiply vs host tables, all 65536 products
 
     // Host staging (the PCIe-inclusive path): packets start and end in pinned host
@@ -198,8 +215,20 @@ private:
         std::vector<uint32_t> level_items, item_base, level_coop;
         Slot* slot = nullptr;
         uint64_t ticket = 0;
+        int verify = -1;  // index into vbatches_ (digested when the program completes)
         bool done() const { return next >= levels; }
     };
+    // verification batches (verify_next): descriptors and results in device memory
+    struct VerifyBatch {
+        std::vector<VerifyDesc> host;  // kept until the end: the H2D copy reads it asynchronously
+        VerifyDesc* dev_desc = nullptr;
+        VerifyOut* dev_out = nullptr;
+        uint32_t count = 0;
+    };
+    std::vector<VerifyBatch> vbatches_;
+    size_t vread_ = 0;       // batches whose results verify_results() has returned
+    int pending_verify_ = -1;
+    void run_verify(int batch);
     std::deque<Inflight> progs_;
     bool pipelined_ = false;
     // one launch: the next level of every program in progs_ (+ `fresh`'s level 1 when given)

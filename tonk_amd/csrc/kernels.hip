@@ -681,5 +681,42 @@ extern "C" __global__ void tamd_digest_rows(const DigestDesc* __restrict__ d, ui
     out[i] = h;
 }
 
+// Verification digests of a program's output rows (Device::verify_next): enqueued on the launch
+// stream right after the launch that completes the program.  mode 0: FNV-1a over `len` bytes
+// (a recovery packet, footer included); mode 1: a recovered original -- parse its length
+// prefix (serial.h get_length_header, `len` bytes available) and hash the payload it announces.
+// One thread per row; verification only, never in a timed region.
+struct VerifyDesc { uint32_t row, len, mode, pad; };
+struct VerifyOut { u64 hash; uint32_t len, ok; };
+
+extern "C" __global__ void tamd_verify_rows(const VerifyDesc* __restrict__ d, uint32_t n,
+                                            const uint8_t* __restrict__ arena, VerifyOut* __restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const VerifyDesc g = d[i];
+    const uint8_t* p = arena + (size_t)g.row * TAMD_ROW_UNIT;
+    uint32_t skip = 0, len = g.len, ok = 1;
+    if (g.mode == 1) {
+        const uint32_t b0 = g.len >= 1 ? p[0] : 0u;
+        const uint32_t top = b0 >> 6;
+        uint32_t hb = 0;
+        if (g.len < 1) ok = 0;
+        else if (top <= 1) { len = b0; hb = 1; }
+        else if (top == 2) { hb = 2; len = ((b0 << 8) | p[1]) & 0x3fffu; }
+        else if ((b0 & 0xE0u) == 0xC0u) { hb = 3; len = ((b0 << 16) | ((uint32_t)p[1] << 8) | p[2]) & 0x1fffffu; }
+        else { hb = 4; len = ((b0 << 24) | ((uint32_t)p[1] << 16) | ((uint32_t)p[2] << 8) | p[3]) & 0x1fffffffu; }
+        if (ok && (hb > g.len || len > g.len - hb)) ok = 0;
+        skip = hb;
+        if (!ok) len = 0;
+    }
+    u64 h = 1469598103934665603ULL;
+    for (uint32_t k = 0; k < len; ++k) { h ^= p[skip + k]; h *= 1099511628211ULL; }
+    VerifyOut o;
+    o.hash = h;
+    o.len = len;
+    o.ok = ok;
+    out[i] = o;
+}
+
 // Marks the start and end of a bench's timed region in kernel traces (Device::set_timing).
 extern "C" __global__ void tamd_timed_region() {}

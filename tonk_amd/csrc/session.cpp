@@ -10,7 +10,7 @@
 #include "decoder.h"
 #include "device.h"
 #include "workload.h"
-#include "../../oracle/transcript.h"
+#include "transcript.h"
 
 #include <hip/hip_runtime.h>
 
@@ -33,64 +33,124 @@ using namespace tamd;
 
 namespace {
 
-// CPUs of the device's NUMA node (the PCI device's local_cpulist) that this process may run on,
-// one hardware thread per core; TONK_AMD_AFFINITY=node keeps both SMT threads, =none returns
-// nothing (no pinning).  The control-plane threads run there so their stream state lives in the
-// node next to the GPU.  Bench A/B on one box (40 steps, twice each): 224-227 GiB/s with one
-// thread per core, 212-226 with the node's CPUs, 199-217 unpinned.
-std::vector<int> device_local_cpus(int device) {
-    const char* mode = getenv("TONK_AMD_AFFINITY");
+// "0-3,8,10-11" -> {0,1,2,3,8,10,11}
+std::vector<int> parse_cpulist(const char* text) {
     std::vector<int> out;
-    if (mode && !strcmp(mode, "none")) return out;
-    char bus[64] = {0};
-    if (hipDeviceGetPCIBusId(bus, sizeof(bus), device) != hipSuccess) return out;
-    for (char* c = bus; *c; ++c) *c = (char)tolower(*c);
-    std::string path = std::string("/sys/bus/pci/devices/") + bus + "/local_cpulist";
-    FILE* f = fopen(path.c_str(), "r");
-    if (!f) return out;
-    char line[4096] = {0};
-    const bool ok = fgets(line, sizeof(line), f) != nullptr;
-    fclose(f);
-    if (!ok) return out;
-    cpu_set_t allowed;
-    CPU_ZERO(&allowed);
-    if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return out;
-    const bool one_per_core = !(mode && !strcmp(mode, "node"));
-    for (char* tok = strtok(line, ",\n"); tok; tok = strtok(nullptr, ",\n")) {
+    std::string line(text ? text : "");
+    size_t at = 0;
+    while (at < line.size()) {
+        size_t end = line.find_first_of(",\n", at);
+        if (end == std::string::npos) end = line.size();
         int a = 0, b = 0;
-        const int n = sscanf(tok, "%d-%d", &a, &b);
-        if (n < 1) continue;
-        if (n == 1) b = a;
-        for (int c = a; c <= b && c < CPU_SETSIZE; ++c) {
-            if (!CPU_ISSET(c, &allowed)) continue;
-            if (one_per_core) {
-                char tp[128];
-                snprintf(tp, sizeof(tp), "/sys/devices/system/cpu/cpu%d/topology/thread_siblings_list", c);
-                FILE* g = fopen(tp, "r");
-                int first = c;
-                if (g) {
-                    if (fscanf(g, "%d", &first) != 1) first = c;
-                    fclose(g);
-                }
-                if (first != c) continue;
-            }
-            out.push_back(c);
+        const int n = sscanf(line.substr(at, end - at).c_str(), "%d-%d", &a, &b);
+        if (n >= 1) {
+            if (n == 1) b = a;
+            for (int c = a; c <= b && c >= 0 && c < CPU_SETSIZE; ++c) out.push_back(c);
         }
+        at = end + 1;
     }
     return out;
 }
 
+// The share of a NUMA node's cores that one GPU's pool takes when several GPUs hang off the same
+// node (4 per socket on an 8-GPU MI355X node): the devices whose local_cpulist equals this
+// device's split `node_cores` into equal contiguous shares in device order (the remainder to
+// the first), so the ranks of one node never pin their threads to the same cores (the
+// reference's equivalent is one worker pool per process over all cores,
+// TonkineseSession.cpp:71-102).  `slot_override` "k/n" (TONK_AMD_CPU_SLOT) replaces the device
+// scan, for launchers that give each rank only its own GPU.  Pure: tested on CPU.
+std::vector<int> node_core_share(const std::vector<std::string>& dev_cpulists, unsigned device,
+                                 const std::vector<int>& node_cores, const char* slot_override,
+                                 unsigned* slot_out = nullptr, unsigned* nslots_out = nullptr) {
+    unsigned slot = 0, nslots = 1;
+    unsigned k = 0, n = 0;
+    if (slot_override && sscanf(slot_override, "%u/%u", &k, &n) == 2 && n >= 1 && k < n) {
+        slot = k;
+        nslots = n;
+    } else if (device < dev_cpulists.size()) {
+        nslots = 0;
+        for (size_t d = 0; d < dev_cpulists.size(); ++d) {
+            if (dev_cpulists[d] != dev_cpulists[device]) continue;
+            if (d < device) ++slot;
+            ++nslots;
+        }
+    }
+    if (slot_out) *slot_out = slot;
+    if (nslots_out) *nslots_out = nslots;
+    const size_t N = node_cores.size();
+    if (nslots <= 1 || N < nslots) return node_cores;
+    const size_t base = N / nslots, extra = N % nslots;
+    const size_t begin = slot * base + (slot < extra ? slot : extra);
+    const size_t len = base + (slot < extra ? 1 : 0);
+    return std::vector<int>(node_cores.begin() + begin, node_cores.begin() + begin + len);
+}
+
+std::string read_line(const std::string& path) {
+    FILE* f = fopen(path.c_str(), "r");
+    if (!f) return std::string();
+    char line[4096] = {0};
+    const bool ok = fgets(line, sizeof(line), f) != nullptr;
+    fclose(f);
+    std::string s = ok ? std::string(line) : std::string();
+    while (!s.empty() && (s.back() == '\n' || s.back() == ' ')) s.pop_back();
+    return s;
+}
+
+std::string device_cpulist(int device) {
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, sizeof(bus), device) != hipSuccess) return std::string();
+    for (char* c = bus; *c; ++c) *c = (char)tolower(*c);
+    return read_line(std::string("/sys/bus/pci/devices/") + bus + "/local_cpulist");
+}
+
+// CPUs of the device's NUMA node (the PCI device's local_cpulist) that this process may run on,
+// one hardware thread per core, and of those this device's share (node_core_share);
+// TONK_AMD_AFFINITY=node keeps both SMT threads, =none returns nothing (no pinning).  The
+// control-plane threads run there so their stream state lives in the node next to the GPU.
+// Bench A/B on one box (40 steps, twice each): 224-227 GiB/s with one thread per core, 212-226
+// with the node's CPUs, 199-217 unpinned.
+std::vector<int> device_local_cpus(int device) {
+    const char* mode = getenv("TONK_AMD_AFFINITY");
+    std::vector<int> out;
+    if (mode && !strcmp(mode, "none")) return out;
+    const std::string mine = device_cpulist(device);
+    if (mine.empty()) return out;
+    cpu_set_t allowed;
+    CPU_ZERO(&allowed);
+    if (sched_getaffinity(0, sizeof(allowed), &allowed) != 0) return out;
+    const bool one_per_core = !(mode && !strcmp(mode, "node"));
+    for (int c : parse_cpulist(mine.c_str())) {
+        if (!CPU_ISSET(c, &allowed)) continue;
+        if (one_per_core) {
+            char tp[128];
+            snprintf(tp, sizeof(tp), "/sys/devices/system/cpu/cpu%d/topology/thread_siblings_list", c);
+            const std::vector<int> sib = parse_cpulist(read_line(tp).c_str());
+            if (!sib.empty() && sib[0] != c) continue;
+        }
+        out.push_back(c);
+    }
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+    std::vector<std::string> lists;
+    for (int d = 0; d < n; ++d) lists.push_back(device_cpulist(d));
+    return node_core_share(lists, (unsigned)device, out, getenv("TONK_AMD_CPU_SLOT"));
+}
+
 struct Stream;
 
-// Transcript in the oracle's format; digests of device rows are filled after each program.
+// Transcript in the oracle's format (record mode).  The digests of device rows are computed on
+// the device (Device::verify_next) right after the launch that completes their program, and
+// filled into the lines at the end of the run.
 struct SessTranscript {
     bool on = false;
     std::vector<std::string> lines;
-    // rows whose digest goes into line `pos` once their program (epoch) has completed
-    struct PendEnc { RowId row; uint32_t total; RecoveryMeta meta; size_t pos; uint64_t epoch; };
-    struct PendDec { RowId row; uint32_t upper; size_t pos; uint64_t epoch; };
+    // rows whose digest goes into line `pos`; `v` = index of the digest among the session's
+    // verification results (assigned when the rows are registered after their pass)
+    struct PendEnc { RowId row; uint32_t total; RecoveryMeta meta; size_t pos; uint64_t v; };
+    struct PendDec { RowId row; uint32_t upper; size_t pos; uint64_t v; };
     std::vector<PendEnc> pend_enc;
     std::vector<PendDec> pend_dec;
+    size_t reg_enc = 0, reg_dec = 0;  // entries [0, reg_*) are registered
 };
 
 struct Stream {
@@ -174,7 +234,7 @@ struct Stream {
                 nums.push_back(rp->packet_num);
                 alg_bytes += rp->framed_upper;
                 if (stage) out_rows.push_back(std::make_pair(rp->row, rp->framed_upper));
-                if (tr.on) tr.pend_dec.push_back(SessTranscript::PendDec{rp->row, rp->framed_upper, tr.lines.size(), ctx->epoch});
+                if (tr.on) tr.pend_dec.push_back(SessTranscript::PendDec{rp->row, rp->framed_upper, tr.lines.size(), 0});
             }
         }
         return rc;
@@ -201,7 +261,7 @@ struct Stream {
     void on_encode(int rc, const RecRef& r) {
         if (!tr.on) return;
         if (rc != 0) { tr.lines.push_back("E " + std::to_string(rc)); return; }
-        tr.pend_enc.push_back(SessTranscript::PendEnc{r.out.row, r.out.total(), r.out.meta, tr.lines.size(), ctx->epoch});
+        tr.pend_enc.push_back(SessTranscript::PendEnc{r.out.row, r.out.total(), r.out.meta, tr.lines.size(), 0});
         tr.lines.push_back("E ?");
     }
     void on_decode(int rc, const std::vector<uint32_t>& nums, const DecRef&) {
@@ -252,7 +312,7 @@ struct Session {
     std::vector<double> busy_ms;                    // per thread, control-plane time of a step
     std::vector<double> fill_ms;                    // per thread, program fill time (deferred mode)
     std::vector<std::pair<uint64_t, uint64_t>> epoch_ticket;  // (epoch, ticket) awaiting release
-    uint64_t last_ticket = 0, released_epoch = 0, prev_ticket = 0;
+    uint64_t last_ticket = 0, released_epoch = 0;
     double host_ms[6] = {0, 0, 0, 0, 0, 0};
     uint64_t clock_msec = 0;  // packet send times of a step (RTO bookkeeping only)
     uint32_t row_cap = 0;
@@ -351,6 +411,9 @@ struct Session {
     std::atomic<int> sleepers{0};
 
     void pool_loop(size_t ti) {
+        // A pool thread may launch the step's program (early launch): its HIP calls (events,
+        // launches) must target the session's device, not device 0.
+        dev.bind_thread();
         // Each pool thread on a core of its own (with sticky streams its streams' state stays in
         // that core's caches); TONK_AMD_PIN=set lets every thread float over the whole CPU set.
         static const bool pin_set = getenv("TONK_AMD_PIN") && !strcmp(getenv("TONK_AMD_PIN"), "set");
@@ -462,9 +525,7 @@ struct Session {
         const auto t0 = clk::now();
         clock_msec = time_msec();
         if (host_in && !finish) stage_inputs(originals);
-        uint64_t rel = completed_epoch();
-        // record mode: the previous program's rows wait for their digests (after this launch)
-        if (prm.record && !ctxs.empty() && ctxs[0]->epoch >= 2 && rel > ctxs[0]->epoch - 2) rel = ctxs[0]->epoch - 2;
+        const uint64_t rel = completed_epoch();
         std::fill(busy_ms.begin(), busy_ms.end(), 0.0);
         init_order();
         run_all([this, originals, finish, rel, &ms](size_t i, size_t ti) {
@@ -492,6 +553,7 @@ struct Session {
         });
         const auto t3 = clk::now();
         if (host_in) dev.h2d_fence();  // the program reads the rows copied in above
+        if (prm.record) register_verify();
         last_ticket = dev.launch();
         if (host_in) stage_outputs();
         const auto t4 = clk::now();
@@ -500,14 +562,6 @@ struct Session {
         host_ms[3] += ms(t2, t3);
         host_ms[4] += ms(t3, t4);
         epoch_ticket.push_back(std::make_pair(epoch, last_ticket));
-        // Record mode: the digests of the PREVIOUS program's rows, once it has completed -- its
-        // upper levels ran in this launch (pipelined), which the transcripts thereby check; its
-        // rows are not released before the next step.
-        if (prm.record) {
-            if (prev_ticket) dev.wait(prev_ticket);
-            resolve_transcripts(epoch);
-            prev_ticket = last_ticket;
-        }
     }
 
     void init_order() {
@@ -541,19 +595,17 @@ struct Session {
         };
         const auto t0 = clk::now();
         clock_msec = time_msec();
-        uint64_t rel = completed_epoch();
-        // Record mode: rows of programs whose digests are still unread stay allocated.  At this
-        // point the digests of every program before the one launched last step are read.
-        if (prm.record && !ctxs.empty() && rel + 3 > ctxs[0]->epoch) rel = ctxs[0]->epoch >= 3 ? ctxs[0]->epoch - 3 : 0;
+        const uint64_t rel = completed_epoch();
         std::fill(busy_ms.begin(), busy_ms.end(), 0.0);
         std::fill(fill_ms.begin(), fill_ms.end(), 0.0);
         init_order();
         const bool fill = have_closed;
         // Early launch: the thread that fills the last stream launches the program at once
         // (the other threads only run control planes, which touch no device state) instead of the
-        // caller after the pass.  Record mode reads digests at launch, so it launches after.
+        // caller after the pass.  Record mode runs the same schedule (its digests are enqueued by
+        // the launches themselves).
         static const bool early_ok = getenv("TONK_AMD_LATE_LAUNCH") == nullptr;  // A/B switch
-        const bool early = fill && early_ok && !prm.record && !threads.empty();
+        const bool early = fill && early_ok && !threads.empty();
         if (early) fills_left.store(streams.size(), std::memory_order_relaxed);
         run_all([this, originals, finish, rel, fill, early, &ms](size_t i, size_t ti) {
             const auto w0 = clk::now();
@@ -581,6 +633,7 @@ struct Session {
         std::vector<Context*> cs;
         for (auto& c : ctxs) cs.push_back(c.get());
         dev.begin(cs.data(), cs.size(), true);
+        if (prm.record) register_verify();  // rows of the program just closed (launched next pass)
         have_closed = true;
         closed_epoch = ctxs.empty() ? 0 : ctxs[0]->epoch - 1;
         const auto t3 = clk::now();
@@ -589,17 +642,11 @@ struct Session {
         host_ms[2] += ms(t2, t3);
     }
 
-    // Launch the closed program (filled), and in record mode read the digests of the program
-    // launched before it, which this launch completes.
+    // Launch the closed program (filled).
     void launch_closed() {
         last_ticket = dev.launch();
         have_closed = false;
         epoch_ticket.push_back(std::make_pair(closed_epoch, last_ticket));
-        if (prm.record) {
-            if (prev_ticket) dev.wait(prev_ticket);
-            resolve_transcripts(closed_epoch);
-            prev_ticket = last_ticket;
-        }
     }
 
     // Fill and launch a closed program still waiting (end of a run: wait / finish).
@@ -668,41 +715,66 @@ struct Session {
         run_all([this, rel](size_t i, size_t) { ctxs[i]->rows.release_up_to(rel); });
     }
 
-    // Digests of pending transcript rows of programs before `before_epoch` (all when 0); those
-    // programs have completed (dev.wait / synchronize by the caller).
-    void resolve_transcripts(uint64_t before_epoch = 0) {
-        std::vector<uint8_t> buf;
+    // Record mode: hand the rows of the program about to be launched (every transcript entry
+    // not registered yet) to the device's verification, which digests them right after the
+    // launch that completes the program.  Main thread, between passes (no stream is running).
+    uint64_t verify_count = 0, verify_base = 0;
+    void register_verify() {
+        std::vector<Device::VerifyDesc> d;
+        for (auto& sp : streams) {
+            SessTranscript& t = sp->tr;
+            for (size_t k = t.reg_enc; k < t.pend_enc.size(); ++k) {
+                auto& e = t.pend_enc[k];
+                e.v = verify_count++;
+                d.push_back(Device::VerifyDesc{(uint32_t)sp->ctx->rows.offset(e.row), e.total, 0, 0});
+            }
+            for (size_t k = t.reg_dec; k < t.pend_dec.size(); ++k) {
+                auto& e = t.pend_dec[k];
+                e.v = verify_count++;
+                d.push_back(Device::VerifyDesc{(uint32_t)sp->ctx->rows.offset(e.row), e.upper, 1, 0});
+            }
+            t.reg_enc = t.pend_enc.size();
+            t.reg_dec = t.pend_dec.size();
+        }
+        dev.verify_next(d);
+    }
+
+    // Fill the transcript lines from the device digests (end of a run: every program done).
+    void resolve_transcripts() {
+        register_verify();  // (entries of a program never launched: none, unless the run failed)
+        std::vector<Device::VerifyOut> res;
+        dev.verify_results(res);
+        if (verify_base + res.size() != verify_count) {
+            error = "verification digests missing";
+            return;
+        }
+        auto get = [&](uint64_t v) -> const Device::VerifyOut& { return res[v - verify_base]; };
         for (auto& sp : streams) {
             Stream& s = *sp;
             char line[256];
-            size_t keep = 0;
             for (auto& e : s.tr.pend_enc) {
-                if (before_epoch && e.epoch >= before_epoch) { s.tr.pend_enc[keep++] = e; continue; }
-                buf.resize(e.total);
-                dev.download_now(buf.data(), (uint64_t)s.ctx->rows.offset(e.row) * TAMD_ROW_UNIT, e.total);
+                const Device::VerifyOut& o = get(e.v);
                 snprintf(line, sizeof(line), "E 0 %u %u %u %u %u %016llx", e.total, e.meta.Row, e.meta.ColumnStart,
-                         e.meta.SumCount, e.meta.LDPCCount, (unsigned long long)wl::fnv1a(buf.data(), e.total));
+                         e.meta.SumCount, e.meta.LDPCCount, (unsigned long long)o.hash);
                 s.tr.lines[e.pos] = line;
             }
-            s.tr.pend_enc.resize(keep);
-            keep = 0;
             for (auto& d : s.tr.pend_dec) {
-                if (before_epoch && d.epoch >= before_epoch) { s.tr.pend_dec[keep++] = d; continue; }
-                buf.resize(d.upper);
-                dev.download_now(buf.data(), (uint64_t)s.ctx->rows.offset(d.row) * TAMD_ROW_UNIT, d.upper);
-                unsigned len = 0;
-                const int hb = get_length_header(buf.data(), d.upper, len);
-                std::string& ln = s.tr.lines[d.pos];
-                if (hb < 1 || len + (unsigned)hb > d.upper) {
+                const Device::VerifyOut& o = get(d.v);
+                if (!o.ok) {
                     error = "recovered row with a corrupt length header";
                     continue;
                 }
-                snprintf(line, sizeof(line), ":%u:%016llx", len, (unsigned long long)wl::fnv1a(buf.data() + hb, len));
+                std::string& ln = s.tr.lines[d.pos];
+                snprintf(line, sizeof(line), ":%u:%016llx", o.len, (unsigned long long)o.hash);
                 const size_t at = ln.find('#');
                 if (at != std::string::npos) ln.replace(at, 1, line);
             }
-            s.tr.pend_dec.resize(keep);
+            s.tr.pend_enc.clear();
+            s.tr.pend_dec.clear();
+            s.tr.reg_enc = s.tr.reg_dec = 0;
         }
+        verify_base = verify_count;
+        dev.verify_reset();
     }
 };
 
@@ -955,6 +1027,28 @@ const char* tamd_session_error(void* sp) {
 }
 
 void tamd_set_clock(uint64_t (*fn)(void)) { set_clock_source(fn); }
+
+unsigned tamd_session_cpus(void* sp, int* out, unsigned cap) {
+    Session* s = (Session*)sp;
+    for (unsigned i = 0; i < cap && i < s->cpus.size(); ++i) out[i] = s->cpus[i];
+    return (unsigned)s->cpus.size();
+}
+
+unsigned tamd_cpu_share(const char* dev_cpulists, unsigned device, const char* node_cores, const char* slot_override,
+                        int* out, unsigned cap) {
+    std::vector<std::string> lists;
+    const std::string all(dev_cpulists ? dev_cpulists : "");
+    size_t at = 0;
+    while (at <= all.size() && !all.empty()) {
+        size_t end = all.find(';', at);
+        if (end == std::string::npos) end = all.size();
+        lists.push_back(all.substr(at, end - at));
+        at = end + 1;
+    }
+    const std::vector<int> share = node_core_share(lists, device, parse_cpulist(node_cores), slot_override);
+    for (unsigned i = 0; i < cap && i < share.size(); ++i) out[i] = share[i];
+    return (unsigned)share.size();
+}
 
 int tamd_device_selftest(uint32_t device, char* err, size_t err_len) {
     Device d;

@@ -1,4 +1,4 @@
-// transcript.h -- TEST INFRASTRUCTURE.  Text transcript of one workload stream, written the
+// transcript.h -- text transcript of one workload stream, written the
 // same way for every backend so runs can be compared line by line against the reference.
 //
 // Lines:
