@@ -7,9 +7,9 @@ rank*64 .. rank*64+63), 1300-byte payloads, 1% uniform loss on originals and rec
 recovery rate f = max(2p, 1%) = 2%, acknowledgements every 64 originals.  Payloads are
 synthetic (PCG, seed 1000 + stream id) and already resident in HBM when timing starts.
 
-A step = 4096 originals per stream: the host control planes (16 worker threads per GPU) turn
-every add/encode/ack/decode into device ops and each step's byte work runs as one merged
-program on the GPU, pipelined with the host building the next step.  `value` is whole-job
+A step = 16384 originals per stream, in 4 device programs of 4096: the host control planes (16
+worker threads per GPU) turn every add/encode/ack/decode into device ops and each program's byte
+work runs as one merged launch sequence on the GPU, pipelined with the host building the next.  `value` is whole-job
 payload GiB/s over all ranks; the timed region is bracketed by a barrier and a device sync.
 
 roofline: algorithmic HBM bytes (SURVEY.md s8(d) B_alg, counted exactly per step) divided by
@@ -40,7 +40,8 @@ import tonk_amd  # noqa: E402
 METRIC = "Siamese FEC encode+decode GiB/s (device-resident), 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0
 STREAMS_PER_GPU = 64
-ORIGINALS_PER_STEP = 4096
+ORIGINALS_PER_STEP = 4096   # per stream per device program (tamd_session_step)
+PROGRAMS_PER_STEP = 4       # a bench step: 4 programs, 16384 originals per stream
 LOSS = 0.01
 ACK = 64
 PAYLOAD = 1300
@@ -465,6 +466,64 @@ class Dist:
 MAX_CORES = 128
 
 
+class HostEnv:
+    """Host-side conditions of the timed region (the headline is host-bound): the
+    cgroup CPU-quota throttling of this job (cpu.stat), this process's CPU time, and how busy the
+    worker cores were in total (/proc/stat, every process) -- busy well above our own CPU time
+    on those cores means another job's threads shared them."""
+
+    def __init__(self, cores: list[int]):
+        self.cores = list(cores)
+        self.a = self._sample()
+
+    @staticmethod
+    def _cpu_stat() -> dict:
+        out = {}
+        try:
+            with open("/sys/fs/cgroup/cpu.stat") as f:
+                for line in f:
+                    k, v = line.split()
+                    out[k] = int(v)
+        except (OSError, ValueError):
+            pass
+        return out
+
+    def _proc_stat(self) -> dict:
+        busy = {}
+        try:
+            with open("/proc/stat") as f:
+                for line in f:
+                    if line.startswith("cpu") and line[3].isdigit():
+                        v = line.split()
+                        c = int(v[0][3:])
+                        if c in self.cores:
+                            t = [int(x) for x in v[1:]]
+                            busy[c] = (sum(t) - t[3] - t[4], sum(t))  # (busy, total) jiffies
+        except (OSError, ValueError):
+            pass
+        return busy
+
+    def _sample(self):
+        return (time.perf_counter(), os.times(), self._cpu_stat(), self._proc_stat())
+
+    def report(self) -> dict:
+        t1, o1, c1, p1 = self._sample()
+        t0, o0, c0, p0 = self.a
+        wall = t1 - t0
+        own = (o1.user + o1.system) - (o0.user + o0.system)
+        out = {"wall_s": round(wall, 4), "process_cpu_s": round(own, 4)}
+        if c0 and c1:
+            out["throttled_ms"] = round((c1.get("throttled_usec", 0) - c0.get("throttled_usec", 0)) / 1e3, 3)
+            out["nr_throttled"] = c1.get("nr_throttled", 0) - c0.get("nr_throttled", 0)
+        if p0 and p1:
+            b = sum(p1[c][0] - p0[c][0] for c in p1 if c in p0)
+            tot = sum(p1[c][1] - p0[c][1] for c in p1 if c in p0)
+            out["worker_cores_busy_frac"] = round(b / tot, 4) if tot else None
+            hz = os.sysconf("SC_CLK_TCK")
+            out["worker_cores_busy_s"] = round(b / hz, 3)
+        return out
+
+
 def pad_cores(cores: list[int]) -> list[float]:
     """A rank's core list as a fixed-size vector for all_gather (-1 = none)."""
     c = list(cores)[:MAX_CORES]
@@ -499,8 +558,8 @@ def spawn_ranks(n: int, argv: list[str]) -> int:
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=40)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-end-to-end", action="store_true", help="skip the PCIe-inclusive side measurement")
     ap.add_argument("--no-verify", action="store_true", help="skip the untimed byte check of the timed schedule")
@@ -563,7 +622,7 @@ def main() -> int:
 
     threads = host_threads(local_world)
     total_steps = a.warmup + a.steps
-    n_orig = total_steps * ORIGINALS_PER_STEP
+    n_orig = total_steps * ORIGINALS_PER_STEP * PROGRAMS_PER_STEP
     wp = tonk_amd.WorkloadParams(n=n_orig, payload=PAYLOAD, loss=loss, ack=ACK)
     sess = tonk_amd.Session(wp, n_streams=STREAMS_PER_GPU, device=local_rank,
                             stream_base=stream_base(rank), threads=threads,
@@ -571,24 +630,27 @@ def main() -> int:
     sess.generate()
     rank_cores = d.gather(pad_cores(sess.cpus()))
 
-    for _ in range(a.warmup):
+    for _ in range(a.warmup * PROGRAMS_PER_STEP):
         sess.step(ORIGINALS_PER_STEP)
     sess.wait()
     s0 = sess.summary()
     h0 = sess.host_ms()
     sess.set_timing(True)
     d.barrier()
+    env = HostEnv(sess.cpus())
     t0 = time.perf_counter()
-    for _ in range(a.steps):
+    for _ in range(a.steps * PROGRAMS_PER_STEP):
         sess.step(ORIGINALS_PER_STEP)
     sess.wait()
     t1 = time.perf_counter()
+    host_env = env.report()
     d.barrier()
     sess.set_timing(False)
     kernel_ms, launches = sess.kernel_ms()
     s1 = sess.summary()
     h1 = sess.host_ms()
-    host = {k: round((h1[k] - h0[k]) / a.steps, 4) for k in h1}
+    # per device program (a quarter of a bench step)
+    host = {k: round((h1[k] - h0[k]) / (a.steps * PROGRAMS_PER_STEP), 4) for k in h1}
     elapsed = d.allmax(t1 - t0)
 
     payload = s1["payload_bytes"] - s0["payload_bytes"]
@@ -609,9 +671,9 @@ def main() -> int:
     pmc = pmc_traffic(a.workload, a.steps, a.warmup) if (rank == 0 and world == 1 and not a.no_pmc) else None
     traffic = pmc.get("traffic_per_timed_launch") if pmc else None
     workload = {
-        "cfg3": "configs[3] per-GPU shard: 64 independent streams/GPU, 4096 originals per stream per step, "
+        "cfg3": "configs[3] per-GPU shard: 64 independent streams/GPU, 16384 originals per stream per step (4 programs), "
                 "1300 B payloads, 1% uniform loss, f=2%, ack every 64",
-        "cfg2": "configs[2]: 64 independent streams/GPU, 4096 originals per stream per step, 1300 B payloads, "
+        "cfg2": "configs[2]: 64 independent streams/GPU, 16384 originals per stream per step (4 programs), 1300 B payloads, "
                 "2% uniform loss, f=4%, ack every 64",
     }[a.workload]
     out = {
@@ -629,7 +691,8 @@ def main() -> int:
         "data": "synthetic",
         "config": {
             "workload": workload,
-            "streams_per_gpu": STREAMS_PER_GPU, "originals_per_step": ORIGINALS_PER_STEP, "payload_bytes": PAYLOAD,
+            "streams_per_gpu": STREAMS_PER_GPU, "originals_per_step": ORIGINALS_PER_STEP * PROGRAMS_PER_STEP,
+            "originals_per_program": ORIGINALS_PER_STEP, "payload_bytes": PAYLOAD,
             "loss": loss, "ack_every": ACK, "host_threads_per_gpu": threads,
             "parallelism": f"streams sharded {STREAMS_PER_GPU}/GPU x {world} GPU, no collective",
             # each rank's pinned worker cores (its share of its GPU's NUMA node, tamd_cpu_share)
@@ -654,7 +717,8 @@ def main() -> int:
             "device_busy_frac": round((kernel_ms / 1e3) / (t1 - t0), 4),
         },
         "cpu_baseline": None,
-        "host_ms_per_step": host,
+        "host_ms_per_program": host,
+        "host_env": host_env,
         "checks": {"all_recovered": all_ok, "recovered": fin["recovered"], "lost_originals": fin["lost_originals"],
                    "lost_recoveries": fin["lost_recoveries"]},
     }

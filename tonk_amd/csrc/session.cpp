@@ -136,6 +136,51 @@ std::vector<int> device_local_cpus(int device) {
     return node_core_share(lists, (unsigned)device, out, getenv("TONK_AMD_CPU_SLOT"));
 }
 
+// Busy jiffies of each CPU so far (/proc/stat: every process on the host), indexed by CPU.
+std::vector<uint64_t> cpu_busy_jiffies() {
+    std::vector<uint64_t> busy;
+    FILE* f = fopen("/proc/stat", "r");
+    if (!f) return busy;
+    char line[512];
+    while (fgets(line, sizeof(line), f)) {
+        if (strncmp(line, "cpu", 3) != 0 || line[3] < '0' || line[3] > '9') continue;
+        unsigned c = 0;
+        unsigned long long v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (sscanf(line + 3, "%u %llu %llu %llu %llu %llu %llu %llu %llu", &c, &v[0], &v[1], &v[2], &v[3], &v[4],
+                   &v[5], &v[6], &v[7]) < 5)
+            continue;
+        if (c >= busy.size()) busy.resize(c + 1, 0);
+        busy[c] = v[0] + v[1] + v[2] + v[5] + v[6] + v[7];  // user nice system irq softirq steal
+    }
+    fclose(f);
+    return busy;
+}
+
+// The `want` least busy CPUs of `share` over a short sampling window (ties: lower CPU first),
+// in ascending order.  The GPU box's CPUs are shared with other jobs' threads; a pool thread
+// pinned to a core another job keeps busy is descheduled for milliseconds at a time, and the
+// step waits for it.  Pure selection in pick_idle(); the sampling reads /proc/stat.
+std::vector<int> pick_idle(const std::vector<int>& share, const std::vector<uint64_t>& busy_delta, size_t want) {
+    if (share.size() <= want) return share;
+    std::vector<int> order(share);
+    auto busy = [&](int c) { return (size_t)c < busy_delta.size() ? busy_delta[c] : 0; };
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return busy(a) < busy(b); });
+    order.resize(want);
+    std::sort(order.begin(), order.end());
+    return order;
+}
+
+std::vector<int> idle_cpus(const std::vector<int>& share, size_t want) {
+    static const bool off = getenv("TONK_AMD_NO_IDLE_PICK") != nullptr;  // A/B switch
+    if (off || share.size() <= want) return share.size() > want ? std::vector<int>(share.begin(), share.begin() + want) : share;
+    const std::vector<uint64_t> a = cpu_busy_jiffies();
+    std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    const std::vector<uint64_t> b = cpu_busy_jiffies();
+    std::vector<uint64_t> d(b.size(), 0);
+    for (size_t i = 0; i < b.size() && i < a.size(); ++i) d[i] = b[i] - a[i];
+    return pick_idle(share, d, want);
+}
+
 struct Stream;
 
 // Transcript in the oracle's format (record mode).  The digests of device rows are computed on
@@ -808,7 +853,7 @@ void* tamd_session_create(const tamd_session_params* p, char* err, size_t err_le
     s->deferred = pipe && getenv("TONK_AMD_NO_DEFER") == nullptr;
     Session* raw = s.get();
     if (nthreads > 1) {
-        raw->cpus = device_local_cpus((int)p->device);
+        raw->cpus = idle_cpus(device_local_cpus((int)p->device), nthreads);
         raw->threads_wanted = nthreads;
         for (uint32_t t = 0; t < nthreads; ++t) raw->threads.emplace_back([raw, t] { raw->pool_loop(t); });
     }

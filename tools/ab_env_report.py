@@ -6,7 +6,7 @@ rows = {}
 for f in sorted(glob.glob(f"gpurun_out/{tag}_*_[0-9]*.json")):
     m = re.match(rf"gpurun_out/{tag}_(.+)_(\d+)\.json", f)
     j = json.load(open(f))
-    h = j["host_ms_per_step"]
+    h = j.get("host_ms_per_program") or j["host_ms_per_step"]
     rows.setdefault(m.group(1), []).append(
         (j["value"], j["ms_per_step"], h["control_wall"], h["control_sum"], h["control_max"], h["fill"],
          j["roofline"]["avg_launch_us"]))

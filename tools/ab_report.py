@@ -7,6 +7,6 @@ tag = sys.argv[1]
 for side in ("A", "B"):
     for f in sorted(glob.glob(f"gpurun_out/{tag}_{side}_*.json")):
         j = json.load(open(f))
-        h = j["host_ms_per_step"]
+        h = j.get("host_ms_per_program") or j["host_ms_per_step"]
         print(side, j["value"], j["ms_per_step"], h["control_wall"], h["control_sum"], h["control_max"], h["fill"],
               j["roofline"]["avg_launch_us"])
