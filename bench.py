@@ -273,12 +273,14 @@ def single_stream(name: str, device: int, step: int, reps: int = 3) -> dict:
     end-of-stream flush and device sync timed), the median of `reps` fresh sessions, next to the
     reference codec on one host thread over the same stream."""
     wp = tonk_amd.WorkloadParams(payload=PAYLOAD, **SINGLE_STREAM[name])
-    times, payload, ok = [], 0, True
+    times, payload, ok, runs = [], 0, True, []
     for _ in range(reps):
         sess = tonk_amd.Session(wp, n_streams=1, device=device, threads=1, arena_bytes=(3 * wp.n * 1344) + (1 << 30))
         try:
             sess.generate()
             sess.wait()
+            sess.set_timing(True)
+            h0 = sess.host_ms()
             t0 = time.perf_counter()
             done = 0
             while done < wp.n:
@@ -286,19 +288,32 @@ def single_stream(name: str, device: int, step: int, reps: int = 3) -> dict:
                 done += step
             sess.finish()
             t1 = time.perf_counter()
+            sess.set_timing(False)
+            h1 = sess.host_ms()
+            kms, launches = sess.kernel_ms()
             summ = sess.summary()
         finally:
             sess.close()
         times.append(t1 - t0)
+        programs = summ["programs"]
+        runs.append((t1 - t0, {
+            "programs": programs, "launches": launches,
+            "wall_us_per_program": round((t1 - t0) * 1e6 / max(1, programs), 2),
+            "kernel_us_per_launch": round(kms * 1e3 / max(1, launches), 2),
+            "kernel_us_per_program": round(kms * 1e3 / max(1, programs), 2),
+            # host phases per program (tamd_session_host_ms): control planes, layout, fill, launch
+            "host_us_per_program": {k: round((h1[k] - h0[k]) * 1e3 / max(1, programs), 2)
+                                    for k in ("control_wall", "layout", "fill", "launch", "slot_wait")}}))
         payload = summ["payload_bytes"]
         ok = ok and summ["missing_at_end"] == 0 and summ["disabled_codecs"] == 0
     times.sort()
     dt = times[len(times) // 2]
+    breakdown = sorted(runs, key=lambda r: r[0])[len(runs) // 2][1]
     out = {"metric": METRIC, "value": round(payload / dt / 2**30, 4), "unit": "GiB/s", "n_gpus": 1,
            "ms_per_stream": round(dt * 1e3, 3), "higher_is_better": True, "dtype": "u8", "data": "synthetic",
            "config": {"workload": f"BASELINE.json {name}: 1 stream", **SINGLE_STREAM[name], "payload_bytes": PAYLOAD,
                       "originals_per_step": step},
-           "checks": {"all_recovered": ok}, "cpu_baseline": None}
+           "checks": {"all_recovered": ok}, "per_program": breakdown, "cpu_baseline": None}
     exe = os.path.join(ROOT, "oracle", "_ref", "golden_gen")
     if os.path.exists(exe):
         def run(r: int) -> dict | None:

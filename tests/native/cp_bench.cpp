@@ -8,6 +8,7 @@
 #include "../../tonk_amd/csrc/prof.h"
 
 #include <chrono>
+#include <x86intrin.h>
 #include <signal.h>
 #include <sys/time.h>
 #include <ucontext.h>
@@ -26,7 +27,7 @@ thread_local uint64_t calls[kSlots];
 const char* const names[kSlots] = {"enc_add", "enc_encode", "enc_ack", "dec_add_orig", "dec_add_rec", "dec_decode",
     "dec_ack", "dec_is_ready", "gen_matrix", "ge", "elim", "lower_tri", "back_sub", "chain_flush", "sym_merge",
     "prepare_flush", "finish_flush", "release", "enc_dense", "enc_light", "enc_emit", "elim_sums", "elim_pairs",
-    "elim_fold", "enc_cauchy", "enc_remove"};
+    "elim_fold", "enc_cauchy", "enc_remove", "elim_start"};
 } }
 #endif
 
@@ -189,7 +190,7 @@ int main(int argc, char** argv) {
     p.loss_thresh = 42949673;
     p.fec_rate_q16 = 1311;
     p.ack_every = 64;
-    uint32_t streams = 8, step = 4096, warm_steps = 0, expand = ~0u;  // warm: untimed, unsampled first steps
+    uint32_t streams = 8, step = 4096, warm_steps = 0, expand = ~0u, reps = 1;  // warm: untimed, unsampled first steps
     p.n_originals = 4096 * 6;
     for (int i = 1; i < argc; ++i) {
         const char* eq = strchr(argv[i], '=');
@@ -200,7 +201,8 @@ int main(int argc, char** argv) {
         if (k == "nobatch") { g_nobatch = atoi(eq + 1); continue; }
         if (k == "warm") { warm_steps = (uint32_t)atoi(eq + 1); continue; }
         if (k == "expand") { expand = (uint32_t)strtoul(eq + 1, nullptr, 0); continue; }
-        if (k == "pipe") { g_pipe = atoi(eq + 1); continue; }  // level pipelining as the session runs it
+        if (k == "pipe") { g_pipe = atoi(eq + 1); continue; }
+        if (k == "reps") { reps = (uint32_t)atoi(eq + 1); continue; }  // level pipelining as the session runs it
         const unsigned long long v = strtoull(eq + 1, nullptr, 0);
         if (k == "streams") streams = (uint32_t)v;
         else if (k == "n") p.n_originals = (uint32_t)v;
@@ -213,6 +215,22 @@ int main(int argc, char** argv) {
         else if (k == "bg") p.bg_thresh = (uint32_t)v;
         else if (k == "arq") p.arq_lag = (uint32_t)v;
     }
+    // reps=R: the whole run is repeated R times with fresh codecs; every (step, stream) segment
+    // is timed (TSC) and the sum over segments of each segment's minimum over the repetitions is
+    // reported (segmin_cyc_per_original): a host-load burst inflates one repetition's segment,
+    // not all of them.
+    std::vector<uint64_t> seg_min;
+    std::chrono::steady_clock::time_point t0;
+    double c0 = 0;
+    uint32_t timed_originals = 0;
+    uint64_t instrs = 0, ops = 0, acc_bytes = 0, store_bytes = 0;
+    auto cpu_now = []() {
+        timespec ts;
+        clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+        return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+    };
+    uint32_t last_enc_window = 0;
+    for (uint32_t rep = 0; rep < reps; ++rep) {
     // One Context per stream with each side's input rows contiguous, as the session lays them out
     // (tamd_session_generate), and steps of `step` originals per stream.
     std::vector<std::unique_ptr<Context>> ctxs(streams);
@@ -241,7 +259,8 @@ int main(int argc, char** argv) {
         for (uint32_t i = 0; i < p.n_originals; ++i) be[s]->dec_rows.push_back(ctx.rows.alloc(1302));
         run[s].reset(new wl::Runner<Null, NoTr>(ps[s], *be[s], tr));
     }
-    uint64_t instrs = 0, ops = 0, acc_bytes = 0, store_bytes = 0;
+    instrs = ops = acc_bytes = store_bytes = 0;
+    timed_originals = 0;
     auto start_sampling = [&]() {
         if (!sample_out) return;
         struct sigaction sa;
@@ -255,12 +274,14 @@ int main(int argc, char** argv) {
         tv.it_value = tv.it_interval;
         setitimer(ITIMER_PROF, &tv, nullptr);
     };
-    auto t0 = std::chrono::steady_clock::now();
-    uint32_t timed_originals = 0, step_no = 0;
+    t0 = std::chrono::steady_clock::now();
+    c0 = cpu_now();
+    uint32_t step_no = 0;
     if (!warm_steps) start_sampling();
     for (uint32_t done = 0; done < p.n_originals; done += step, ++step_no) {
         if (warm_steps && step_no == warm_steps) {
             t0 = std::chrono::steady_clock::now();
+            c0 = cpu_now();
 #ifdef TAMD_PROF
             memset(prof::cycles, 0, sizeof(prof::cycles));
             memset(prof::calls, 0, sizeof(prof::calls));
@@ -270,6 +291,7 @@ int main(int argc, char** argv) {
         if (step_no >= warm_steps) timed_originals += (done + step <= p.n_originals ? step : p.n_originals - done);
         for (uint32_t s = 0; s < streams; ++s) {
             Context& ctx = *ctxs[s];
+            const uint64_t seg0 = __rdtsc();
             run[s]->advance(step);
             const uint64_t e = ctx.epoch;
             {
@@ -289,9 +311,18 @@ int main(int argc, char** argv) {
                 TAMD_PROF_SCOPE(kRelease);
                 ctx.rows.release_up_to(e);
             }
+            if (step_no >= warm_steps) {
+                const uint64_t c = __rdtsc() - seg0;
+                const size_t si = (size_t)(step_no - warm_steps) * streams + s;
+                if (seg_min.size() <= si) seg_min.resize(si + 1, ~0ull);
+                if (c < seg_min[si]) seg_min[si] = c;
+            }
         }
     }
+    last_enc_window = (unsigned)(kMaxPackets - encs[0]->remaining_slots());
+    }  // rep
     const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    const double cpu_sec = cpu_now() - c0;
     if (sample_out) {
         itimerval off;
         memset(&off, 0, sizeof(off));
@@ -313,11 +344,13 @@ int main(int argc, char** argv) {
         if (in) fclose(in);
         if (out) fclose(out);
     }
-    if (getenv("CP_BENCH_WIN")) fprintf(stderr, "enc window %u\n", (unsigned)(kMaxPackets - encs[0]->remaining_slots()));
+    if (getenv("CP_BENCH_WIN")) fprintf(stderr, "enc window %u\n", last_enc_window);
     const double n = (double)streams * timed_originals;
-    printf("{\"ns_per_original\": %.1f, \"instrs_per_original\": %.2f, \"ops_per_original\": %.3f, "
+    uint64_t segsum = 0;
+    for (uint64_t c : seg_min) segsum += c;
+    printf("{\"segmin_cyc_per_original\": %.1f, \"cpu_ns_per_original\": %.1f, \"ns_per_original\": %.1f, \"instrs_per_original\": %.2f, \"ops_per_original\": %.3f, "
            "\"acc_bytes_per_original\": %.0f, \"store_bytes_per_original\": %.0f, \"seconds\": %.3f}\n",
-           sec * 1e9 / n, instrs / n, ops / n, acc_bytes / n, store_bytes / n, sec);
+           (double)segsum / n, cpu_sec * 1e9 / n, sec * 1e9 / n, instrs / n, ops / n, acc_bytes / n, store_bytes / n, sec);
 #ifdef TAMD_PROF
     const double ghz = 1.0 * 0 + 1;
     for (int i = 0; i < prof::kSlots; ++i)

@@ -130,19 +130,20 @@ bool SegmentPool::get(uint32_t min_units, uint64_t* base, uint32_t* units) {
     }
     const uint32_t n = min_units > seg_units ? min_units : seg_units;
     const uint64_t end_bytes = (bump_units + n) * TAMD_ROW_UNIT;
-    {
-        DevLock dl;  // lock order: pool, then device
-        if (end_bytes > g_rt->dev.arena_bytes() && !g_rt->dev.grow_arena(end_bytes)) {
-            static std::atomic<int> reported{0};
-            if (!reported.exchange(1))
-                fprintf(stderr, "tonk_amd: the arena cannot grow to %llu MB (mapped %llu MB)\n",
-                        (unsigned long long)(end_bytes >> 20), (unsigned long long)(g_rt->dev.arena_bytes() >> 20));
-            return false;
-        }
+    // Growth maps memory past everything in use: it takes no device lock, so other codecs'
+    // programs keep going (a growth costs ~170-190 ms); and it normally happened already, in the
+    // background, once three quarters of the mapped arena were handed out.
+    if (end_bytes > g_rt->dev.arena_bytes() && !g_rt->dev.grow_arena(end_bytes)) {
+        static std::atomic<int> reported{0};
+        if (!reported.exchange(1))
+            fprintf(stderr, "tonk_amd: the arena cannot grow to %llu MB (mapped %llu MB)\n",
+                    (unsigned long long)(end_bytes >> 20), (unsigned long long)(g_rt->dev.arena_bytes() >> 20));
+        return false;
     }
     *base = bump_units;
     *units = n;
     bump_units += n;
+    if (bump_units * TAMD_ROW_UNIT > g_rt->dev.arena_bytes() / 4 * 3) g_rt->dev.grow_arena_async();
     return true;
 }
 

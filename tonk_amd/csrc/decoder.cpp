@@ -8,6 +8,9 @@
 
 namespace tamd {
 
+// Term lists up to this length go to the device unmerged (see eliminate_original_data).
+static const size_t kMergeAbove = 48;
+
 static inline uint32_t popcount64(uint64_t x) { return (uint32_t)__builtin_popcountll(x); }
 
 // CustomBitSet<64> helpers (PacketAllocator.h:243-346)
@@ -57,11 +60,13 @@ void Decoder::pre_flush() {
 void Decoder::drop_original(StoredOriginal& o) {
     if (o.owned) ctx_->rows.free_deferred(o.row);
     if (o.host && release_) release_(o.host, user_);
-    // an empty slot is bytes == 0 (every add writes all the other fields)
+    // an empty slot is bytes == 0, run == 0, owned == 0 and host == null (every add writes all
+    // the other fields; a cleared subwindow is all zero)
     o.row = kNoRow;
     o.bytes = 0;
     o.owned = 0;
     o.host = nullptr;
+    o.run = 0;
 }
 
 void Decoder::free_recovery(Recovery* r) {
@@ -86,6 +91,22 @@ bool Decoder::mark_got(uint32_t column) {
     s->got_count++;
     s->got |= 1ull << (e % kSubwindow);
     return e == next_expected_;
+}
+
+// Run bookkeeping of input rows (Encoder::add_unchecked's StoredOriginal::run): the element
+// continues the run of the element before it when that one is a received input row of the same
+// length and the row offsets keep a fixed stride.  Recovered rows have run 0 and break runs
+// (their contents may still be in flight and their lengths are refined after readback).
+void Decoder::set_run(uint32_t e, StoredOriginal& o) {
+    o.run = 1;
+    o.stride = 0;
+    if (e == 0) return;
+    const StoredOriginal& p = elem(e - 1);
+    if (p.run && p.bytes == o.bytes && o.off > p.off && p.run < 0xffff &&
+        (p.run == 1 || o.off - p.off == p.stride)) {
+        o.run = (uint16_t)(p.run + 1);
+        o.stride = o.off - p.off;
+    }
 }
 
 // RangeLostPackets (:1279-1323)
@@ -189,6 +210,8 @@ Result Decoder::add_original(uint32_t packet_num, RowId row, uint32_t framed_byt
     o.header_bytes = (uint8_t)header_bytes;
     o.owned = borrowed ? 0 : 1;
     o.host = host;
+    if (o.owned || host) s->held++;
+    set_run(e, o);
     *took = !borrowed;
     s->got_count++;
     s->got |= 1ull << bit;
@@ -223,19 +246,42 @@ bool Decoder::add_run_inorder(uint32_t col0, const RowId* rows, uint32_t k, uint
     const uint8_t owned = borrowed ? 0 : 1;
     uint32_t column = col0;
     const RowId* r = rows;
+    // run state of the element before the run (set_run, kept in locals)
+    uint32_t prev_run = 0, prev_off = 0, prev_stride = 0, prev_bytes = 0;
+    if (e0 > 0) {
+        const StoredOriginal& p = elem(e0 - 1);
+        prev_run = p.run;
+        prev_off = p.off;
+        prev_stride = p.stride;
+        prev_bytes = p.bytes;
+    }
     for (uint32_t e = e0; e < e0 + k;) {  // a subwindow at a time: slots, then got bits
         const uint32_t bit = e % kSubwindow;
         const uint32_t n = std::min(kSubwindow - bit, e0 + k - e);
         Subwindow* s = subs_[e / kSubwindow];
         StoredOriginal* o = s->orig + bit;
+        if (owned) s->held += n;
         for (uint32_t t = 0; t < n; ++t, ++o, ++r) {
-            if (o->row != kNoRow || o->host) drop_original(*o);  // (slots past the window end are empty)
+            if (o->owned || o->host) drop_original(*o);  // (slots past the window end are empty)
+            const uint32_t off = rt.offset(*r);
+            uint32_t run = 1, stride = 0;
+            if (prev_run && prev_bytes == framed_bytes && off > prev_off && prev_run < 0xffff &&
+                (prev_run == 1 || off - prev_off == prev_stride)) {
+                run = prev_run + 1;
+                stride = off - prev_off;
+            }
             o->row = *r;
-            o->off = rt.offset(*r);
+            o->off = off;
             o->bytes = framed_bytes;
             o->column = column;
             o->header_bytes = (uint8_t)header_bytes;
             o->owned = owned;
+            o->run = (uint16_t)run;
+            o->stride = stride;
+            prev_run = run;
+            prev_off = off;
+            prev_stride = stride;
+            prev_bytes = framed_bytes;
             column = col_inc(column);
         }
         s->got |= (n == 64 ? ~0ull : ((1ull << n) - 1)) << bit;
@@ -303,8 +349,19 @@ LaneSums& Decoder::get_lane(uint32_t lane, uint32_t element_end) {
     LaneSum& sum = lanes_[lane];
     uint32_t e = sum.element_end;
     if (e >= element_end) return sum.sums;
+    // As Encoder::get_lane: when the run of received input packets ending at the lane's last
+    // element reaches back to e, the rest of the lane is one strided run.
+    const uint32_t last = e + ((element_end - 1 - e) / kLanes) * kLanes;
+    const StoredOriginal& ol = elem(last);
     do {
         const StoredOriginal& o = elem(e);
+        if (last > e && ol.run > last - e && o.column + (last - e) < kColumnPeriod) {
+            sum.sums.grow(o.bytes);
+            sum.sums.accumulate_run_level0(o.row, o.off, o.bytes, o.column, (last - e) / kLanes + 1,
+                                           ol.stride * kLanes);
+            e = last + kLanes;
+            break;
+        }
         if (o.bytes > 0) {
             sum.sums.grow(o.bytes);
             if (ctx_->rows.level(o.row) == 0) sum.sums.accumulate_level0(o.row, o.off, o.bytes, o.column);
@@ -383,9 +440,14 @@ void Decoder::remove_elements() {
 
     for (uint32_t i = 0; i < first_kept_sub; ++i) {
         Subwindow* s = subs_[i];
-        for (unsigned k = 0; k < kSubwindow; ++k) drop_original(s->orig[k]);
+        if (s->held) {
+            for (unsigned k = 0; k < kSubwindow; ++k) drop_original(s->orig[k]);
+        } else {
+            memset((void*)s->orig, 0, sizeof(s->orig));  // (nothing to release: borrowed rows)
+        }
         s->got = 0;
         s->got_count = 0;
+        s->held = 0;
     }
     std::rotate(subs_.begin(), subs_.begin() + first_kept_sub, subs_.end());
 
@@ -807,6 +869,9 @@ bool Decoder::add_single_recovery(RowId row, uint32_t data_bytes, const uint8_t*
     o.column = m.ColumnStart;
     o.header_bytes = (uint8_t)header;
     o.owned = 1;
+    o.run = 0;  // (not an input row: never part of a run, see set_run)
+    o.stride = 0;
+    subs_[e / kSubwindow]->held++;
     *took = true;
 
     if (!has_recovered_) {
@@ -969,8 +1034,8 @@ bool Decoder::eliminate_original_data() {
             }
         } else {
             const uint32_t rbytes = rec->bytes;
-            Sym& prod = prod_;
-            prod.clear();
+            {
+            TAMD_PROF_SCOPE(kElimStart);
             uint32_t sum_elem = to_element(m.ColumnStart);
             if (m.ColumnStart != sum_column_start_ || m.SumCount < sum_column_count_) {
                 if (invalid_element(sum_elem)) return false;
@@ -980,9 +1045,11 @@ bool Decoder::eliminate_original_data() {
                 if (invalid_element(sum_elem)) sum_elem = 0;
                 if (!start_sums(sum_elem, rbytes)) return false;
             }
+            }
             sum_column_count_ = m.SumCount;
 
             const uint8_t rx = row_value(m.Row);
+            {
             TAMD_PROF_SCOPE(kElimSums);
             for (unsigned l = 0; l < kLanes; ++l) {
                 const unsigned op = row_opcode(l, m.Row);
@@ -994,6 +1061,10 @@ bool Decoder::eliminate_original_data() {
                 opcode_coefs(op, rx, k);  // sums and RX * product sums in one read
                 c.read(ctx_->rows, ctx_->ex, buf, k, n);
             }
+            }
+            TAMD_PROF_SCOPE(kElimPairs);
+            // LDPC pairs; the product half takes its RX factor right away (the reference adds
+            // RX * product after the loop, SiameseDecoder.cpp:1029-1047: the same terms)
             Pcg32 prng;
             prng.seed(m.Row, m.LDPCCount);
             const uint32_t pairs = (m.LDPCCount + kPairRate - 1) / kPairRate;
@@ -1003,18 +1074,21 @@ bool Decoder::eliminate_original_data() {
                 if (o1.bytes > 0) read_original(o1, o1.bytes < rbytes ? o1.bytes : rbytes, 1, buf);
                 const uint32_t erx = es + prng.next() % m.LDPCCount;
                 const StoredOriginal& orx = elem(erx);
-                if (orx.bytes > 0) read_original(orx, orx.bytes < rbytes ? orx.bytes : rbytes, 1, prod);
+                if (orx.bytes > 0) read_original(orx, orx.bytes < rbytes ? orx.bytes : rbytes, rx, buf);
             }
-            sym_add(buf, prod, rbytes, row_value(m.Row));
         }
         if (ctx_->oom) return false;
+        // (every term is already clipped to rec->bytes: the row itself, lane reads at
+        // min(sum bytes, rbytes), originals at min(bytes, rbytes))
         // Fold everything already in memory into one partial row so the triangular solve and
         // any later reader in this program touch one row instead of the whole elimination.
         // A single unknown needs no triangular solve: back substitution scales the terms
-        // straight into the recovered row.
-        sym_clip(buf, rec->bytes);
+        // straight into the recovered row.  Short lists are not merged: a row named twice by
+        // the pairs is just read twice (GF(2^8) sums are linear).  Long ones are -- they come
+        // from inlined expansions of rows recovered in this program, which nest, and unmerged
+        // duplicates would compound from one recovery to the next.
         if (cr_.lost_count == 1) {
-            sym_merge(buf);
+            if (buf.size() > kMergeAbove) sym_merge(buf);
             continue;
         }
         TAMD_PROF_SCOPE(kElimFold);
@@ -1036,7 +1110,7 @@ bool Decoder::multiply_lower_triangle() {
     for (uint32_t i = 0; i < L; ++i) {
         tri_[(size_t)i * L + i] = 1;
         Recovery* r = mrows_[pivots_[i]].rec;
-        sym_merge(r->buf);
+        if (L > 1) sym_merge(r->buf);  // (one unknown: merged by eliminate_original_data)
         tri_b_[i] = r->bytes;
     }
     for (uint32_t ci = 0; ci + 1 < L; ++ci) {
@@ -1065,6 +1139,7 @@ bool Decoder::multiply_lower_triangle() {
 Result Decoder::back_substitution() {
     const uint32_t L = cr_.lost_count;
     recovered_.assign(L, RecoveredPacket());
+    if (L == 1) return back_substitution_one();
     tri_clips_.assign(tri_b_.begin(), tri_b_.end());
     std::sort(tri_clips_.begin(), tri_clips_.end());
     tri_clips_.erase(std::unique(tri_clips_.begin(), tri_clips_.end()), tri_clips_.end());
@@ -1082,7 +1157,6 @@ Result Decoder::back_substitution() {
     bool iterate = false;
     for (int ci = (int)L - 1; ci >= 0; --ci) {
         const uint32_t ri = pivots_[ci];
-        StoredOriginal* o = mcols_[ci].orig;
         const uint8_t y = mat(ri, (uint32_t)ci);
         if (y == 0) { disabled_ = true; return kDisabled; }
         const uint8_t inv_y = gf_inv(y);
@@ -1119,26 +1193,57 @@ Result Decoder::back_substitution() {
             sym_add(value, mrows_[pivots_[gr.k]].rec->buf, tri_clips_[gr.clip], gr.coef);
         }
         sym_merge(value);
-        const RowId out_row = ctx_->alloc(bytes);
-        if (out_row == kNoRow) { disabled_ = true; return kDisabled; }
-        ctx_->pb.combine(out_row, value.data(), value.size(), bytes);
-        ctx_->ex.set(out_row, value);
-
-        drop_original(*o);
-        o->row = out_row;
-        o->off = ctx_->rows.offset(out_row);
-        o->bytes = bytes;
-        o->column = mcols_[ci].column;
-        o->header_bytes = 0;
-        o->owned = 1;
-
-        RecoveredPacket& rp = recovered_[ci];
-        rp.packet_num = o->column;
-        rp.row = out_row;
-        rp.framed_upper = bytes;
-        recovered_columns_.push_back(o->column);
-        iterate |= mark_got(o->column);
+        if (!store_recovered((uint32_t)ci, value, bytes, iterate)) return kDisabled;
     }
+    return finish_solve(iterate);
+}
+
+// One unknown (the common case at low loss): the recovered value is inv(diag) times the single
+// eliminated row, whose terms eliminate_original_data clipped to the row's length -- the general
+// path's groups reduce to that list (merged there; duplicates are harmless reads here).
+Result Decoder::back_substitution_one() {
+    const uint32_t ri = pivots_[0];
+    const uint8_t y = mat(ri, 0);
+    if (y == 0) { disabled_ = true; return kDisabled; }
+    Recovery* rec = mrows_[ri].rec;
+    Sym& value = value_;
+    value.swap(rec->buf);  // (rec->buf is cleared below in any case)
+    sym_scale(value, gf_inv(y));
+    bool iterate = false;
+    if (!store_recovered(0, value, tri_b_[0], iterate)) return kDisabled;
+    return finish_solve(iterate);
+}
+
+// Materialize recovered column ci (one combine op) and put it into its window slot.
+bool Decoder::store_recovered(uint32_t ci, Sym& value, uint32_t bytes, bool& iterate) {
+    StoredOriginal* o = mcols_[ci].orig;
+    const RowId out_row = ctx_->alloc(bytes);
+    if (out_row == kNoRow) { disabled_ = true; return false; }
+    ctx_->pb.combine(out_row, value.data(), value.size(), bytes);
+    ctx_->ex.take(out_row, value);  // (value's storage is exchanged: not read again)
+
+    drop_original(*o);
+    o->row = out_row;
+    o->off = ctx_->rows.offset(out_row);
+    o->bytes = bytes;
+    o->column = mcols_[ci].column;
+    o->header_bytes = 0;
+    o->owned = 1;
+    o->run = 0;  // (a recovered row: never part of a run, see set_run)
+    o->stride = 0;
+    subs_[to_element(o->column) / kSubwindow]->held++;
+
+    RecoveredPacket& rp = recovered_[ci];
+    rp.packet_num = o->column;
+    rp.row = out_row;
+    rp.framed_upper = bytes;
+    recovered_columns_.push_back(o->column);
+    iterate |= mark_got(o->column);
+    return true;
+}
+
+Result Decoder::finish_solve(bool iterate) {
+    const uint32_t L = cr_.lost_count;
     for (uint32_t ci = 0; ci < L; ++ci) {
         Recovery* rec = mrows_[pivots_[ci]].rec;
         rec->buf.clear();

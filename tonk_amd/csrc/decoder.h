@@ -66,6 +66,9 @@ private:
         StoredOriginal orig[kSubwindow];
         uint64_t got = 0;
         uint32_t got_count = 0;
+        // slots written with something to release (an owned row or a host copy) since the
+        // subwindow was last cleared; 0: clearing is a plain memset (empty slot = all zero)
+        uint32_t held = 0;
     };
     struct Recovery {
         Recovery* next = nullptr;
@@ -132,7 +135,7 @@ private:
     uint32_t ge_resume_pivot_ = 0;
 
     uint32_t latest_column_ = 0;
-    Sym prod_, value_;  // scratch
+    Sym value_;  // scratch
     // Triangular solve in coefficient space (multiply_lower_triangle / back_substitution):
     // tri_[j * L + k] = coefficient of eliminated row k in row j after the lower triangle,
     // tri_b_[j] = row j's length; a recovered value is a list of groups (row k, clip, coef)
@@ -155,6 +158,7 @@ private:
 
     // window
     bool mark_got(uint32_t column);
+    void set_run(uint32_t e, StoredOriginal& o);
     uint32_t range_lost(uint32_t start, uint32_t end);
     uint32_t find_next_lost(uint32_t start);
     uint32_t find_next_got(uint32_t start);
@@ -192,6 +196,9 @@ private:
     bool eliminate_original_data();
     bool multiply_lower_triangle();
     Result back_substitution();
+    Result back_substitution_one();
+    bool store_recovered(uint32_t ci, Sym& value, uint32_t bytes, bool& iterate);
+    Result finish_solve(bool iterate);
 };
 
 } // namespace tamd

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 #include <chrono>
+#include <thread>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -261,15 +262,18 @@ static void report_slow(const char* what, std::chrono::steady_clock::time_point 
 
 bool Device::grow_arena(uint64_t min_bytes) {
     if (!reserved_bytes_) return min_bytes <= arena_bytes_;
+    std::lock_guard<std::mutex> g(grow_mu_);
+    if (arena_bytes_ >= min_bytes && min_bytes) return true;  // (another thread grew it meanwhile)
+    bind_thread();
     const auto t0 = std::chrono::steady_clock::now();
     struct Report {
         std::chrono::steady_clock::time_point t0;
-        const uint64_t* mapped;
-        ~Report() { report_slow("arena growth", t0, *mapped >> 20, 0); }
+        const std::atomic<uint64_t>* mapped;
+        ~Report() { report_slow("arena growth", t0, mapped->load() >> 20, 0); }
     } rep{t0, &arena_bytes_};
     // Physical 256 MiB chunks mapped back to back.  A growth maps at least half the size mapped so
-    // far: it runs under the C ABI's device lock, so a window-filling Tonk server should take a
-    // handful of growths, not one per 256 MiB.
+    // far, so a window-filling Tonk server takes a handful of growths, not one per 256 MiB (the C
+    // ABI starts them in the background ahead of need: SegmentPool::get).
     const uint64_t chunk = ((256ull << 20) + granule_ - 1) / granule_ * granule_;
     uint64_t target = arena_bytes_ + arena_bytes_ / 2;
     if (target < min_bytes) target = min_bytes;
@@ -278,6 +282,14 @@ bool Device::grow_arena(uint64_t min_bytes) {
         if (!map_chunk(chunk)) return arena_bytes_ >= min_bytes;
     }
     return true;
+}
+
+void Device::grow_arena_async() {
+    if (!reserved_bytes_ || arena_bytes_ >= reserved_bytes_ || growing_.exchange(true)) return;
+    std::thread([this] {
+        grow_arena(0);  // (a growth maps at least half the size mapped so far)
+        growing_.store(false);
+    }).detach();
 }
 
 bool Device::alloc_slots(size_t cap) {

@@ -5,7 +5,9 @@
 #include "engine.h"
 
 #include <stdint.h>
+#include <atomic>
 #include <deque>
+#include <mutex>
 #include <vector>
 #include <string>
 
@@ -32,7 +34,14 @@ public:
     // mapped now, grow_arena() maps more (HIP virtual memory management).  Falls back to a
     // fixed arena of `arena_bytes` where the device does not support it.
     bool init_growable(int device, uint64_t arena_bytes, uint64_t max_bytes);
-    bool grow_arena(uint64_t min_bytes);  // arena_bytes() >= min_bytes afterwards, or false
+    // arena_bytes() >= min_bytes afterwards, or false.  Thread safe, and independent of every
+    // other Device call (it maps memory into the reserved range past everything in use), so the
+    // C ABI grows without its device lock.
+    bool grow_arena(uint64_t min_bytes);
+    // Start growing the arena by half on a background thread (at most one growth at a time),
+    // so codecs find the memory mapped before they need it.
+    void grow_arena_async();
+    uint64_t reserved_bytes() const { return reserved_bytes_; }
     // Program staging: `count` pinned/device slot pairs of `bytes` each (grown on demand), used
     // round robin; a program waits only for the program `count` back.  Call before init.
     // Default 2 x 16 MB (the session's big step programs); the C ABI runs many small ones.
@@ -159,7 +168,9 @@ private:
     bool map_chunk(uint64_t bytes);
     int device_ = -1;
     uint8_t* arena_ = nullptr;
-    uint64_t arena_bytes_ = 0;
+    std::atomic<uint64_t> arena_bytes_{0};
+    std::mutex grow_mu_;
+    std::atomic<bool> growing_{false};
     uint32_t* d_gf_ = nullptr;
     uint8_t* d_zero_ = nullptr;
     uint32_t max_grid_ = 256;

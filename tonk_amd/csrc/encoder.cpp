@@ -37,6 +37,8 @@ Encoder::~Encoder() {
 }
 
 void Encoder::release_original(const StoredOriginal& o) {
+    if (!o.owned && !o.host) return;
+    --held_;
     if (o.owned) ctx_->rows.free_deferred(o.row);
     if (o.host && release_) release_(o.host, user_);
 }
@@ -113,6 +115,7 @@ bool Encoder::add_run(const RowId* rows, uint32_t k, uint32_t framed_bytes, uint
         column = col_inc(column);
     }
     win_.commit(k - 1);
+    if (owned) held_ += k - 1;
     count_ += k - 1;
     next_column_ = column;
     // every lane one of these columns fell on (all k - 1 have the same length)
@@ -162,6 +165,7 @@ inline void Encoder::add_unchecked(RowId row, uint32_t off, uint32_t framed_byte
     o.owned = borrowed ? 0 : 1;
     o.send_msec = (uint32_t)now_msec();
     o.host = host;
+    if (o.owned || host) ++held_;
     o.run = 1;
     o.stride = 0;
     if (element > 0) {
@@ -188,7 +192,8 @@ void Encoder::start_new_window(uint32_t column) {
     // Everything from the previous window is unreachable once Count reached zero (only the send
     // timestamps of its first elements stay visible to the RTT scan, see placeholder_msec_).
     for (uint32_t e = 0; e < kLanes; ++e) placeholder_msec_[e] = e < win_.size() ? win_[e].send_msec : placeholder_msec_[e];
-    for (size_t i = 0; i < win_.size(); ++i) drop_original(win_[i]);
+    if (held_)
+        for (size_t i = 0; i < win_.size(); ++i) drop_original(win_[i]);
     win_.clear();
     const uint32_t element = column % kLanes;
     column_start_ = column - element;
@@ -239,7 +244,8 @@ void Encoder::remove_elements() {
         sum_start_ = sum_start_ > removed ? sum_start_ - removed : 0;
     }
 
-    for (uint32_t i = 0; i < removed && i < win_.size(); ++i) release_original(win_[i]);
+    if (held_)  // (borrowed rows without host copies: nothing to release)
+        for (uint32_t i = 0; i < removed && i < win_.size(); ++i) release_original(win_[i]);
     win_.pop_front(removed);
     count_ -= removed;
     column_start_ = to_column(removed);
@@ -264,8 +270,21 @@ LaneSums& Encoder::get_lane(uint32_t lane_index, uint32_t element_end) {
     uint32_t element = lane.next_element;
     if (element < element_end) {
         if (lane.longest > 0) sums.grow(lane.longest);
+        // The lane's last element before element_end; when the run of equal, evenly spaced
+        // packets ending there (StoredOriginal::run) reaches back to `element`, the lane's
+        // packets from here on are one strided run (every kLanes-th packet of it).
+        const uint32_t last = element + ((element_end - 1 - element) / kLanes) * kLanes;
+        const StoredOriginal& ol = win_[last];
         do {
             const StoredOriginal& o = win_[element];
+            if (last > element && ol.run > last - element &&
+                o.column + (last - element) < kColumnPeriod) {
+                sums.grow(o.bytes);
+                sums.accumulate_run_level0(o.row, o.off, o.bytes, o.column, (last - element) / kLanes + 1,
+                                           ol.stride * kLanes);
+                element = last + kLanes;
+                break;
+            }
             sums.grow(o.bytes);
             sums.accumulate_level0(o.row, o.off, o.bytes, o.column);
             element += kLanes;
@@ -614,20 +633,27 @@ void Encoder::add_dense(uint32_t row, uint32_t recovery_bytes, Sym& rec) {
     sum_end_ = count_;
 }
 
-// Encoder::AddLightColumns (SiameseEncoder.cpp:1100-1144)
-void Encoder::add_light(uint32_t row, Sym& rec, Sym& prod) {
+// Encoder::AddLightColumns (SiameseEncoder.cpp:1100-1144).  The product half goes straight into
+// the row with its RX factor (the reference multiplies the product buffer by RX and adds it,
+// :1236-1240; both are clipped to the same length, and every window packet is at most
+// longest_ bytes, so no clipping is needed).
+void Encoder::add_light(uint32_t row, Sym& rec) {
     const uint32_t start = first_unremoved_;
     const uint32_t count = sum_end_ - start;
+    const uint8_t rx = row_value(row);
     Pcg32 prng;
     prng.seed(row, count);
     const uint32_t pairs = (count + kPairRate - 1) / kPairRate;
+    const size_t at = rec.size();
+    rec.resize(at + 2 * (size_t)pairs);
+    Term* t = rec.data() + at;
     for (uint32_t i = 0; i < pairs; ++i) {
         const uint32_t e1 = start + prng.next() % count;
         const uint32_t erx = start + prng.next() % count;
         const StoredOriginal& o1 = win_[e1];
         const StoredOriginal& orx = win_[erx];
-        rec.push_back(Term{o1.row, o1.bytes, 1});
-        prod.push_back(Term{orx.row, orx.bytes, 1});
+        t[2 * i] = Term{o1.row, o1.bytes, 1};
+        t[2 * i + 1] = Term{orx.row, orx.bytes, rx};
     }
 }
 
@@ -655,17 +681,14 @@ Result Encoder::encode(RecoveryOut& out) {
 
     const uint32_t recovery_bytes = longest_;
     Sym& rec = rec_;
-    Sym& prod = prod_;
     rec.clear();
-    prod.clear();
     {
         TAMD_PROF_SCOPE(kEncDense);
         add_dense(row, recovery_bytes, rec);
     }
     {
         TAMD_PROF_SCOPE(kEncLight);
-        add_light(row, rec, prod);
-        sym_add(rec, prod, recovery_bytes, row_value(row));
+        add_light(row, rec);
     }
 
     RecoveryMeta m;
@@ -673,8 +696,11 @@ Result Encoder::encode(RecoveryOut& out) {
     m.LDPCCount = un;
     m.ColumnStart = sum_column_start_;
     m.Row = row;
-    sym_clip(rec, recovery_bytes);
-    return emit(rec, recovery_bytes, m, out, false);
+    // Every term is within recovery_bytes already (lane reads clip to it, packets are at most
+    // longest_).  Terms are not merged: the lane snapshots are distinct rows, and a packet the
+    // LDPC pairs name twice just becomes two reads (GF(2^8) sums are linear), which costs the
+    // device less than a merge costs the host.
+    return emit(rec, recovery_bytes, m, out, true);
 }
 
 // Encoder::GetStatistics (SiameseEncoder.cpp:1445-1457)

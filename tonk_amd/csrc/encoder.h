@@ -39,8 +39,9 @@ struct StoredOriginal {
     uint32_t column = 0;
     uint32_t send_msec = 0;     // encoder only (retransmit timing)
     uint32_t off = 0;           // arena offset of `row` (64-B units), cached for program emission
-    uint32_t stride = 0;        // encoder: off - previous element's off when run > 1
-    uint16_t run = 0;           // encoder: packets of equal length at a fixed stride ending here
+    uint32_t stride = 0;        // off - previous element's off when run > 1
+    uint16_t run = 0;           // packets of equal length at a fixed stride ending here (decoder:
+                                // received input rows only; 0 for empty and recovered slots)
     uint8_t header_bytes = 0;
     uint8_t owned = 0;          // the codec frees `row` when the packet leaves the window
     void* host = nullptr;       // optional host mirror (C-ABI: siamese_encoder_get/retransmit)
@@ -106,6 +107,7 @@ private:
     // previous window's send time at that element, not zero.
     uint32_t placeholder_msec_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t next_column_ = 0, count_ = 0, column_start_ = 0, longest_ = 0;
+    uint32_t held_ = 0;  // window slots with something to release (an owned row or a host copy)
     uint32_t first_unremoved_ = 0;
     uint32_t sum_start_ = 0, sum_end_ = 0, sum_column_start_ = 0, sum_erased_ = 0;
     // The reference advances each of a lane's three sums lazily on its own; their values only
@@ -172,9 +174,9 @@ private:
     Result generate_single(RecoveryOut& out);
     Result generate_cauchy(RecoveryOut& out);
     void add_dense(uint32_t row, uint32_t recovery_bytes, Sym& rec);
-    void add_light(uint32_t row, Sym& rec, Sym& prod);
+    void add_light(uint32_t row, Sym& rec);
     Result emit(Sym& terms, uint32_t len, const RecoveryMeta& meta, RecoveryOut& out, bool distinct);
-    Sym scratch_, rec_, prod_;
+    Sym scratch_, rec_;
     struct Run { RowId row; uint32_t off, stride, count, len, col; };
     std::vector<Run> runs_;
 };

@@ -241,6 +241,37 @@ void ProgramBuilder::op_storec(RowId dst, uint32_t len, const uint8_t* c) {
     store_bytes_ += len;
 }
 
+void ProgramBuilder::op_storec_part(RowId dst, uint32_t units, uint32_t len, uint32_t cap, const uint8_t* c,
+                                    bool first) {
+    tamd_instr s;
+    cur_pure_ = false;
+    s.w0 = TAMD_I_STOREC | ((uint32_t)c[0] << 8) | ((uint32_t)c[1] << 16) | ((uint32_t)c[2] << 24);
+    s.row = rows_->offset(dst) + units;
+    s.len = len;
+    s.cap = cap;
+    instrs_.push_back(s);
+    if (cap > cur_span_) cur_span_ = cap;
+    if (len < cur_full_) cur_full_ = len;
+    if (first) written_.push_back(dst);
+    store_bytes_ += len;
+}
+
+void ProgramBuilder::op_acc_part(RowId src, uint32_t units, uint8_t coef, uint32_t len, uint32_t acc) {
+    if (!coef || !len) return;
+    tamd_instr in;
+    if (acc != 0) cur_pure_ = false;
+    in.w0 = tamd_w0(TAMD_I_ACC, coef, acc);
+    in.row = rows_->offset(src) + units;
+    in.len = len;
+    in.cap = 0;
+    instrs_.push_back(in);
+    if (len > cur_span_) cur_span_ = len;
+    if (len < cur_full_) cur_full_ = len;
+    const uint32_t l = rows_->level(src);
+    if (l > cur_level_in_) cur_level_in_ = l;
+    acc_bytes_ += len;
+}
+
 void ProgramBuilder::op_store(RowId dst, uint32_t len, uint32_t acc) {
     cur_pure_ = false;  // (pure combines end with finish_combine / combine only)
     const uint32_t cap = rows_->cap_bytes(dst);
@@ -392,6 +423,16 @@ void ExpansionTable::set(RowId r, const Sym& s) {
     used_.push_back(r);
 }
 
+void ExpansionTable::take(RowId r, Sym& s) {
+    if (r >= index_.size()) index_.resize((size_t)r + 1, -1);
+    if (index_[r] >= 0) { pool_[index_[r]].swap(s); return; }
+    index_[r] = (int32_t)n_pool_;
+    if (n_pool_ == pool_.size()) pool_.emplace_back();
+    pool_[n_pool_].swap(s);
+    ++n_pool_;
+    used_.push_back(r);
+}
+
 void ExpansionTable::clear() {
     for (RowId r : used_) index_[r] = -1;
     used_.clear();
@@ -531,9 +572,14 @@ void LaneSums::emit_scan(RowTable& rows, ProgramBuilder& pb, const RowId* base, 
         return;
     }
 
-    // chunk boundaries: every snapshot point, and at most kChunk packets apart
-    std::vector<uint32_t> cuts;
-    std::vector<RowId> deltas;
+    // chunk boundaries: every snapshot point, and at most kChunk packets apart.  A chunk's three
+    // partial sums go to one row of three parts (one allocation per chunk).
+    thread_local std::vector<uint32_t> cuts;
+    thread_local std::vector<RowId> deltas;
+    cuts.clear();
+    deltas.clear();
+    const uint32_t wunits = (width + TAMD_ROW_UNIT - 1) / TAMD_ROW_UNIT;
+    const uint32_t wcap = wunits * TAMD_ROW_UNIT;
     uint32_t pos = 0;
     size_t sj = 0;
     while (pos < n) {
@@ -544,11 +590,10 @@ void LaneSums::emit_scan(RowTable& rows, ProgramBuilder& pb, const RowId* base, 
         cuts.push_back(pos);
         pb.begin_op();
         emit_packets(pb, terms, ri, rdone, end - pos);
-        for (unsigned s = 0; s < 3; ++s) {
-            const RowId d = rows.alloc(width);
-            deltas.push_back(d);
-            if (d != kNoRow) pb.op_storec(d, rows.cap_bytes(d), unit[s]);
-        }
+        const RowId d = rows.alloc(3 * wcap);
+        deltas.push_back(d);
+        if (d != kNoRow)
+            for (unsigned s = 0; s < 3; ++s) pb.op_storec_part(d, s * wunits, wcap, wcap, unit[s], s == 0);
         pb.end_op(1);
         pos = end;
     }
@@ -557,10 +602,9 @@ void LaneSums::emit_scan(RowTable& rows, ProgramBuilder& pb, const RowId* base, 
         if (base[s] != kNoRow) pb.op_acc(base[s], 1, rows.cap_bytes(base[s]), s);
     for (size_t k = 0; k < cuts.size(); ++k) {
         snapshots(cuts[k]);
-        for (unsigned s = 0; s < 3; ++s) {
-            const RowId d = deltas[3 * k + s];
-            if (d != kNoRow) pb.op_acc(d, 1, rows.cap_bytes(d), s);
-        }
+        const RowId d = deltas[k];
+        if (d != kNoRow)
+            for (unsigned s = 0; s < 3; ++s) pb.op_acc_part(d, s * wunits, 1, wcap, s);
     }
     snapshots(n);
     if (final_rows)

@@ -141,6 +141,11 @@ public:
     uint32_t finish_combine(RowId dst, uint32_t len, const uint8_t* footer, uint32_t footer_len);
     void op_store(RowId dst, uint32_t len, uint32_t acc = 0);
     void op_storec(RowId dst, uint32_t len, const uint8_t* c);  // c0*acc_0 ^ c1*acc_1 ^ c2*acc_2
+    // The same into a part of row `dst` (`units` 64-B units from its start, `cap` bytes); the
+    // row is recorded as written once (`first`: the first part the op stores).
+    void op_storec_part(RowId dst, uint32_t units, uint32_t len, uint32_t cap, const uint8_t* c, bool first);
+    // ACC of a part of row `src` (its level is the row's).
+    void op_acc_part(RowId src, uint32_t units, uint8_t coef, uint32_t len, uint32_t acc);
     uint32_t end_op(uint32_t min_level = 1);  // returns level; rows stored get that level
 
     bool empty() const { return ops_.empty(); }
@@ -281,6 +286,34 @@ public:
         terms_.push_back(T{row, len, off, 0, 1, column});
         ++n_;
     }
+    // `count` level-0 lane packets at once: rows off + k * stride, columns column + 8k (the
+    // same packets accumulate_level0 would take one by one; the run must not wrap the column
+    // period).
+    void accumulate_run_level0(RowId row, uint32_t off, uint32_t len, uint32_t column, uint32_t count,
+                               uint32_t stride) {
+        if (!len || !count) return;
+        if (count == 1) {
+            accumulate_level0(row, off, len, column);
+            return;
+        }
+        if (len > content_) content_ = len;
+        n_ += count;
+        if (!terms_.empty()) {
+            T& b = terms_.back();
+            if (b.len == len && b.col + 8u * b.count == column) {
+                if (b.count == 1 && off > b.off && off - b.off == stride) {
+                    b.stride = stride;
+                    b.count = 1 + count;
+                    return;
+                }
+                if (b.count > 1 && b.stride == stride && off == b.off + b.stride * b.count) {
+                    b.count += count;
+                    return;
+                }
+            }
+        }
+        terms_.push_back(T{row, len, off, stride, count, column});
+    }
     // Append c[0]*sum_0 + c[1]*sum_1 + c[2]*sum_2 (current values, clipped to `limit` bytes).
     void read(RowTable& rows, const ExpansionTable& ex, Sym& out, const uint8_t* c, uint32_t limit);
     // Emit the scan (and fix-up) ops for the pending program and rebase the sums.
@@ -340,6 +373,8 @@ public:
     // inlining grows with the solves per program).
     uint32_t expand_limit = ~0u;
     void set(RowId r, const Sym& s);
+    // set() by exchanging storage: `s` is left with unspecified contents
+    void take(RowId r, Sym& s);
     bool has(RowId r) const { return r < index_.size() && index_[r] >= 0; }
     const Sym& get(RowId r) const { return pool_[index_[r]]; }
     void clear();

@@ -11,7 +11,7 @@ namespace prof {
 enum Slot {
     kEncAdd, kEncEncode, kEncAck, kDecAddOrig, kDecAddRec, kDecDecode, kDecAck, kDecIsReady,
     kGenMatrix, kGE, kElim, kLowerTri, kBackSub, kChainFlush, kSymMerge, kFlushAll, kFinish, kRelease,
-    kEncDense, kEncLight, kEncEmit, kElimSums, kElimPairs, kElimFold, kEncCauchy, kEncRemove, kSlots
+    kEncDense, kEncLight, kEncEmit, kElimSums, kElimPairs, kElimFold, kEncCauchy, kEncRemove, kElimStart, kSlots
 };
 extern thread_local uint64_t cycles[kSlots];
 extern thread_local uint64_t calls[kSlots];
