@@ -110,9 +110,10 @@ struct NoTr {
 // records the interrupted PC; `sample=FILE` writes them for addr2line.
 static uint64_t g_samples[1 << 20], g_callers[1 << 20], g_callers2[1 << 20];
 static volatile size_t g_nsamples = 0;
+static volatile int g_sampling = 0;  // samples are kept only inside timed loops
 static void on_prof(int, siginfo_t*, void* uc) {
     const size_t n = g_nsamples;
-    if (n < (1u << 20)) {
+    if (g_sampling && n < (1u << 20)) {
         g_samples[n] = (uint64_t)((ucontext_t*)uc)->uc_mcontext.gregs[REG_RIP];
         // top of stack: the return address when the sample lands in a frameless leaf (memmove)
         g_callers[n] = *(const uint64_t*)((ucontext_t*)uc)->uc_mcontext.gregs[REG_RSP];
@@ -273,6 +274,7 @@ int main(int argc, char** argv) {
         tv.it_interval.tv_usec = 100;
         tv.it_value = tv.it_interval;
         setitimer(ITIMER_PROF, &tv, nullptr);
+        g_sampling = 1;
     };
     t0 = std::chrono::steady_clock::now();
     c0 = cpu_now();
@@ -319,6 +321,7 @@ int main(int argc, char** argv) {
             }
         }
     }
+    g_sampling = 0;
     last_enc_window = (unsigned)(kMaxPackets - encs[0]->remaining_slots());
     }  // rep
     const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();

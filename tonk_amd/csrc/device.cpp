@@ -293,8 +293,16 @@ void Device::grow_arena_async() {
 }
 
 bool Device::alloc_slots(size_t cap) {
-    cap = (cap + 255) & ~(size_t)255;
-    if (cap * slots_.size() > 0xfffff000ull) return false;  // 32-bit program offsets
+    // parallel-assembly slots: the device half is larger than the pinned half (parts past the
+    // pinned record area are staged separately, close_program)
+    size_t hcap = cap, dcap = cap;
+    if (asm_items_) {
+        hcap = asm_items_ * 8 + asm_host_recs_ * 16;
+        dcap = asm_items_ * 8 + asm_dev_recs_ * 16;
+    }
+    hcap = (hcap + 255) & ~(size_t)255;
+    dcap = (dcap + 255) & ~(size_t)255;
+    if (dcap * slots_.size() > 0xfffff000ull) return false;  // 32-bit program offsets
     for (Slot& s : slots_) {
         s.host = nullptr;
         s.dev = nullptr;
@@ -305,16 +313,197 @@ bool Device::alloc_slots(size_t cap) {
     prog_dev_ = nullptr;
     slot_cap_ = 0;
     // one pinned and one device allocation, split into the slots
-    if (hipMalloc((void**)&prog_dev_, cap * slots_.size()) != hipSuccess) return false;
-    if (hipHostMalloc((void**)&prog_host_, cap * slots_.size(), hipHostMallocDefault) != hipSuccess) return false;
+    if (hipMalloc((void**)&prog_dev_, dcap * slots_.size()) != hipSuccess) return false;
+    if (hipHostMalloc((void**)&prog_host_, hcap * slots_.size(), hipHostMallocDefault) != hipSuccess) return false;
     for (size_t k = 0; k < slots_.size(); ++k) {
         Slot& s = slots_[k];
-        s.host = prog_host_ + k * cap;
-        s.dev_off = (uint32_t)(k * cap);
+        s.host = prog_host_ + k * hcap;
+        s.dev_off = (uint32_t)(k * dcap);
         s.dev = prog_dev_ + s.dev_off;
     }
-    slot_cap_ = cap;
+    slot_cap_ = hcap;
     return true;
+}
+
+void Device::set_assembly_slots(size_t count, size_t host_mb) {
+    slots_.assign(count < 2 ? 2 : count, Slot());
+    asm_items_ = 1u << 20;                  // 8 MB of work items per program
+    asm_host_recs_ = (host_mb << 20) / 16;  // pinned record area
+    asm_dev_recs_ = 4 * asm_host_recs_;
+    slot_bytes_ = 0;
+}
+
+int Device::open_program() {
+    const int h = next_slot_;
+    Slot& slot = slots_[h];
+    next_slot_ = (next_slot_ + 1) % (int)slots_.size();
+    for (const Inflight& p : progs_)
+        if (p.slot == &slot) { drain_programs(); break; }  // (the slot still holds a program in flight)
+    if (slot.ticket) {
+        const auto w0 = std::chrono::steady_clock::now();
+        HIPCHK(hipEventSynchronize((hipEvent_t)slot.done));
+        stats_.slot_wait_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
+        if (streams_.empty() && slot.ticket > completed_) completed_ = slot.ticket;
+        slot.ticket = 0;
+    }
+    slot.bump.store(0, std::memory_order_relaxed);
+    slot.failed = false;
+    return h;
+}
+
+bool Device::add_part(int h, const ProgramBuilder& pb, Part& out) {
+    Slot& slot = slots_[h];
+    const std::vector<tamd_instr>& ins = pb.instrs();
+    const std::vector<tamd_op>& ops = pb.ops();
+    const std::vector<uint32_t>& lv = pb.op_levels();
+    const std::vector<uint32_t>& li = pb.level_items();
+    const uint32_t ni = (uint32_t)ins.size(), no = (uint32_t)ops.size();
+    out.n_instr = ni;
+    out.n_ops = no;
+    out.acc_bytes = pb.acc_bytes();
+    out.store_bytes = pb.store_bytes();
+    out.bucket_start.assign(li.size() + 1, 0);
+    for (size_t b = 0; b < li.size(); ++b) out.bucket_start[b + 1] = out.bucket_start[b] + li[b];
+    out.items.resize(out.bucket_start.back());
+    if (!no) return true;
+    // the executor reads up to a batch past an op's last instruction: every part's instructions
+    // are followed by its ops, and the record area keeps 64 records of slack at its end
+    const uint32_t recs = ni + no;
+    const uint32_t base = slot.bump.fetch_add(recs, std::memory_order_relaxed);
+    if ((size_t)base + recs + 64 > asm_dev_recs_) {
+        slot.failed = true;
+        return false;
+    }
+    std::vector<uint8_t> spill;
+    tamd_instr* dst;
+    if ((size_t)base + recs <= asm_host_recs_) {
+        dst = (tamd_instr*)(slot.host + asm_items_ * 8) + base;
+    } else {
+        spill.resize((size_t)recs * 16);
+        dst = (tamd_instr*)spill.data();
+    }
+    memcpy(dst, ins.data(), (size_t)ni * sizeof(tamd_instr));
+    tamd_op* od = (tamd_op*)(dst + ni);
+    uint32_t cur_small[64];
+    std::vector<uint32_t> cur_big;
+    uint32_t* cur = cur_small;
+    if (li.size() > 64) {
+        cur_big.assign(out.bucket_start.begin(), out.bucket_start.end() - 1);
+        cur = cur_big.data();
+    } else {
+        for (size_t b = 0; b < li.size(); ++b) cur[b] = out.bucket_start[b];
+    }
+    const uint32_t sb = slice_bytes();
+    uint64_t* it = out.items.data();
+    for (uint32_t i = 0; i < no; ++i) {
+        tamd_op op = ops[i];
+        op.first += base;
+        od[i] = op;
+        const uint64_t rec = base + ni + i;
+        uint32_t slices = (op.span + sb - 1) / sb;
+        if (!slices) slices = 1;
+        uint32_t& c = cur[lv[i]];
+        for (uint32_t k = 0; k < slices; ++k) it[c++] = rec | ((uint64_t)k << 32);
+    }
+    if (!spill.empty()) {
+        std::lock_guard<std::mutex> g(spill_mu_);
+        spills_.push_back(Spill{base, std::move(spill)});
+        spill_slot_.push_back(h);
+    }
+    return true;
+}
+
+uint64_t Device::close_program(int h, Part* const* parts, size_t n) {
+    flush_uploads();
+    Slot& slot = slots_[h];
+    if (slot.failed) {
+        error_ = "a program exceeds its staging slot";
+        failed_ = true;
+    }
+    uint32_t B = 0;
+    size_t n_instr = 0, n_ops = 0;
+    std::vector<VerifyDesc> ver;
+    for (size_t i = 0; i < n; ++i) {
+        const Part& p = *parts[i];
+        if (p.bucket_start.size() > B + 1) B = (uint32_t)p.bucket_start.size() - 1;
+        n_instr += p.n_instr;
+        n_ops += p.n_ops;
+        stats_.acc_bytes += p.acc_bytes;
+        stats_.store_bytes += p.store_bytes;
+        ver.insert(ver.end(), p.verify.begin(), p.verify.end());
+    }
+    if (!ver.empty()) verify_next(ver);
+    B = (B + TAMD_COST_CLASSES - 1) / TAMD_COST_CLASSES * TAMD_COST_CLASSES;
+    const uint32_t L = B / TAMD_COST_CLASSES;
+    Inflight cur;
+    cur.levels = L;
+    cur.level_items.assign(L, 0);
+    cur.level_coop.assign(L, 0);
+    cur.item_base.assign(L + 1, 0);
+    // items of a level: cost class by cost class, each part's items of that class in part order
+    uint64_t* items = (uint64_t*)slot.host;
+    size_t at = 0;
+    for (uint32_t b = 0; b < B && !failed_; ++b) {
+        const uint32_t l = b / TAMD_COST_CLASSES;
+        if (b % TAMD_COST_CLASSES == 0) cur.item_base[l] = (uint32_t)at;
+        for (size_t i = 0; i < n; ++i) {
+            const Part& p = *parts[i];
+            if (b + 1 >= p.bucket_start.size()) continue;
+            const uint32_t c = p.bucket_start[b + 1] - p.bucket_start[b];
+            if (!c) continue;
+            if (at + c > asm_items_) {
+                error_ = "a program exceeds its work-item area";
+                failed_ = true;
+                break;
+            }
+            memcpy(items + at, p.items.data() + p.bucket_start[b], (size_t)c * 8);
+            at += c;
+            cur.level_items[l] += c;
+            if (b % TAMD_COST_CLASSES == 0) cur.level_coop[l] += c;
+        }
+    }
+    cur.item_base[L] = (uint32_t)at;
+    if (at == 0 || failed_) {  // nothing to run: complete once everything before it is done
+        const uint64_t ticket = ++ticket_;
+        drain_programs();
+        ticket_is_empty_ = true;
+        mark(ticket);
+        ticket_is_empty_ = false;
+        if (pending_verify_ >= 0) run_verify(pending_verify_);
+        pending_verify_ = -1;
+        return ticket;
+    }
+    hipStream_t st = (hipStream_t)stream_;
+    const size_t ibytes = asm_items_ * 8;
+    const uint32_t recs = slot.bump.load(std::memory_order_relaxed);
+    const size_t hrecs = recs < asm_host_recs_ ? recs : asm_host_recs_;
+    const auto u0 = std::chrono::steady_clock::now();
+    HIPCHK(hipMemcpyAsync(slot.dev, slot.host, at * 8, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(slot.dev + ibytes, slot.host + ibytes, hrecs * 16, hipMemcpyHostToDevice, st));
+    {
+        std::lock_guard<std::mutex> g(spill_mu_);
+        size_t keep = 0;
+        for (size_t i = 0; i < spills_.size(); ++i) {
+            if (spill_slot_[i] != h) {
+                spills_[keep] = std::move(spills_[i]);
+                spill_slot_[keep++] = spill_slot_[i];
+                continue;
+            }
+            // (rare: a program larger than the pinned area; a synchronous copy of the spilled part)
+            HIPCHK(hipStreamSynchronize(st));
+            HIPCHK(hipMemcpy(slot.dev + ibytes + (size_t)spills_[i].rec * 16, spills_[i].bytes.data(),
+                             spills_[i].bytes.size(), hipMemcpyHostToDevice));
+        }
+        spills_.resize(keep);
+        spill_slot_.resize(keep);
+    }
+    const double up_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - u0).count();
+    stats_.upload_enqueue_ms += up_ms;
+    if (up_ms > stats_.upload_enqueue_max_ms) stats_.upload_enqueue_max_ms = up_ms;
+    cur.instrs = cur.ops = slot.dev_off + (uint32_t)ibytes;
+    cur.items = slot.dev_off;
+    cur.slot = &slot;
+    return start_program(cur, n_instr, n_ops, at, at * 8 + (size_t)recs * 16);
 }
 
 bool Device::ensure_slot(Slot& s, size_t bytes) {
@@ -540,8 +729,8 @@ void Device::drain_programs() {
 uint64_t Device::launch() {
     flush_uploads();  // staged packets land before the program reads them
     Plan& P = plan_;
-    const uint64_t ticket = ++ticket_;
     if (P.empty) {
+        const uint64_t ticket = ++ticket_;
         drain_programs();
         ticket_is_empty_ = true;
         mark(ticket);  // done once everything enqueued before it is done
@@ -558,7 +747,7 @@ uint64_t Device::launch() {
     stats_.upload_enqueue_ms += up_ms;
     if (up_ms > 1.0 && getenv("TONK_AMD_TRACE_UPLOADS"))
         fprintf(stderr, "tonk_amd: program %llu: H2D enqueue of %zu bytes took %.3f ms\n",
-                (unsigned long long)ticket, P.total, up_ms);
+                (unsigned long long)(ticket_ + 1), P.total, up_ms);
     if (up_ms > stats_.upload_enqueue_max_ms) stats_.upload_enqueue_max_ms = up_ms;
     Inflight cur;
     cur.instrs = slot.dev_off;
@@ -569,6 +758,15 @@ uint64_t Device::launch() {
     cur.item_base = P.item_base;
     cur.level_coop = P.level_coop;
     cur.slot = &slot;
+    return start_program(cur, P.n_instr, P.n_ops, P.n_items, P.total);
+}
+
+// Enqueue a program whose memory is uploaded (launch, close_program): its first level now (with
+// the next level of every program in flight) when pipelined, all of its levels otherwise.
+uint64_t Device::start_program(Inflight& cur, size_t n_instr, size_t n_ops, size_t n_items, size_t bytes) {
+    hipStream_t st = (hipStream_t)stream_;
+    Slot& slot = *cur.slot;
+    const uint64_t ticket = ++ticket_;
     cur.ticket = ticket;
     cur.verify = pending_verify_;
     pending_verify_ = -1;
@@ -580,7 +778,7 @@ uint64_t Device::launch() {
     const bool stamp_this = stamp_env && (uint64_t)atoll(stamp_env) == stats_.programs;
     const bool pipe = pipelined_ && !stamp_this;
     if (!pipe) drain_programs();
-    if (stamp_this) HIPCHK(hipMalloc((void**)&stamps, P.n_items * 24 + 24));
+    if (stamp_this) HIPCHK(hipMalloc((void**)&stamps, n_items * 24 + 24));
     // a launch holds at most TAMD_MAX_SEGMENTS levels: the oldest programs finish first if needed
     while (progs_.size() + 1 > TAMD_MAX_SEGMENTS) {
         launch_step(nullptr, nullptr);
@@ -593,11 +791,11 @@ uint64_t Device::launch() {
         progs_.push_back(cur);
         retire_done();
     } else {
-        for (uint32_t l = 1; l < P.levels; ++l) {
+        for (uint32_t l = 1; l < cur.levels; ++l) {
             progs_.push_back(cur);  // (a single-program launch per level)
             progs_.back().next = l;
             progs_.back().levels = l + 1;
-            launch_step(nullptr, stamps ? stamps + 3 * P.item_base[l] : nullptr);
+            launch_step(nullptr, stamps ? stamps + 3 * cur.item_base[l] : nullptr);
             progs_.pop_back();
         }
         HIPCHK(hipEventRecord((hipEvent_t)slot.done, st));
@@ -607,7 +805,7 @@ uint64_t Device::launch() {
     }
     HIPCHK(hipGetLastError());
     if (stamp_this) {
-        std::vector<unsigned long long> h(P.n_items * 3);
+        std::vector<unsigned long long> h(n_items * 3);
         HIPCHK(hipMemcpyAsync(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         hipFree(stamps);
@@ -618,17 +816,18 @@ uint64_t Device::launch() {
         }
         f = fopen("tonk_amd_program.bin", "wb");
         if (f) {
-            fwrite(slot.host, 1, P.total, f);
+            fwrite(slot.host, 1, bytes, f);
             fclose(f);
         }
-        fprintf(stderr, "stamps: n_instr_bytes %zu n_ops_bytes %zu n_items %zu\n", P.bytes_instr, P.bytes_ops, P.n_items);
-        for (uint32_t k = 0; k <= P.levels; ++k) fprintf(stderr, "stamps level %u item_base %u\n", k, P.item_base[k]);
+        fprintf(stderr, "stamps: n_instr %zu n_ops %zu n_items %zu (instr/op/item offsets %u/%u/%u)\n", n_instr, n_ops,
+                n_items, cur.instrs - slot.dev_off, cur.ops - slot.dev_off, cur.items - slot.dev_off);
+        for (uint32_t k = 0; k <= cur.levels; ++k) fprintf(stderr, "stamps level %u item_base %u\n", k, cur.item_base[k]);
     }
     stats_.programs++;
-    stats_.ops += P.n_ops;
-    stats_.items += P.n_items;
-    stats_.instrs += P.n_instr;
-    stats_.upload_bytes += P.total;
+    stats_.ops += n_ops;
+    stats_.items += n_items;
+    stats_.instrs += n_instr;
+    stats_.upload_bytes += bytes;
     return ticket;
 }
 

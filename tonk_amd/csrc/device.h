@@ -83,6 +83,31 @@ public:
     void begin(Context* const* ctxs, size_t n, bool closed = false);
     void fill(size_t i);
     uint64_t launch();
+    // (verification descriptors, see verify_next below)
+    struct VerifyDesc { uint32_t row, len, mode, pad; };
+    struct VerifyOut { uint64_t hash; uint32_t len, ok; };
+
+    // Parallel assembly without a layout pass (the session's free-running schedule).  A program
+    // is opened (its staging slot: the slot's previous program must have completed), then any
+    // number of threads add parts concurrently -- one context's pending program each -- and the
+    // caller closes it: the parts' work items are merged level by level (cost class, then part),
+    // the program is uploaded and launched like launch().  A part reserves its instructions and
+    // ops with an atomic bump inside the slot, so no part waits for another; indices in the
+    // program are relative to the slot's record area.  open/close: the launching thread only;
+    // add_part: thread safe, no HIP call.
+    struct Part {
+        std::vector<uint32_t> bucket_start;  // buckets + 1 offsets into items
+        std::vector<uint64_t> items;         // op record index | slice << 32, by bucket
+        uint64_t acc_bytes = 0, store_bytes = 0;
+        uint32_t n_instr = 0, n_ops = 0;
+        std::vector<VerifyDesc> verify;      // rows to digest once the program completes
+    };
+    int open_program();
+    bool add_part(int h, const ProgramBuilder& pb, Part& out);
+    uint64_t close_program(int h, Part* const* parts, size_t n);
+    // Parallel-assembly slots: `count` slots of `host_mb` MB pinned staging (the record area a
+    // program can fill) and 4x that on the device, plus an item area; call before init.
+    void set_assembly_slots(size_t count, size_t host_mb);
     // Level pipelining across programs (the session; Context::kPipeDepth): a program's levels
     // above the depth are launched beside the next program's first levels.
     void set_pipelined(bool on) { pipelined_ = on; }
@@ -132,8 +157,6 @@ public:
     // FNV-1a over `len` bytes; 1: a length-prefixed original (`len` = its upper bound), FNV-1a
     // over the payload the header announces.  Results are read after synchronize(), in the
     // order the descriptors were given over all calls.
-    struct VerifyDesc { uint32_t row, len, mode, pad; };
-    struct VerifyOut { uint64_t hash; uint32_t len, ok; };
     void verify_next(const std::vector<VerifyDesc>& d);
     void verify_results(std::vector<VerifyOut>& out);  // all results so far (synchronizes)
     void verify_reset();                               // drop results read (after verify_results)
@@ -198,7 +221,24 @@ private:
         uint32_t dev_off = 0;
         void* done = nullptr;  // hipEvent_t
         uint64_t ticket = 0;
+        std::atomic<uint32_t> bump{0};  // parallel assembly: records reserved in the record area
+        bool failed = false;            // a part did not fit
+        Slot() {}
+        Slot(const Slot& o) : host(o.host), dev(o.dev), dev_off(o.dev_off), done(o.done), ticket(o.ticket) {}
+        Slot& operator=(const Slot& o) {
+            host = o.host; dev = o.dev; dev_off = o.dev_off; done = o.done; ticket = o.ticket;
+            return *this;
+        }
     };
+    // parallel assembly geometry (set_assembly_slots): per slot, the item area then the records
+    size_t asm_items_ = 0;        // item capacity (8 B each)
+    size_t asm_host_recs_ = 0;    // records (16 B) staged in pinned memory
+    size_t asm_dev_recs_ = 0;     // records the device slot holds (parts past the pinned area are
+                                  // staged in heap buffers and copied separately)
+    struct Spill { uint32_t rec; std::vector<uint8_t> bytes; };
+    std::mutex spill_mu_;
+    std::vector<Spill> spills_;   // parts of the open programs past their pinned area (rare)
+    std::vector<int> spill_slot_;
     std::vector<Slot> slots_ = std::vector<Slot>(2);
     size_t slot_bytes_ = 16u << 20;  // requested initial capacity
     size_t slot_cap_ = 0;            // current capacity of every slot
@@ -242,6 +282,7 @@ private:
     void run_verify(int batch);
     std::deque<Inflight> progs_;
     bool pipelined_ = false;
+    uint64_t start_program(Inflight& cur, size_t n_instr, size_t n_ops, size_t n_items, size_t bytes);
     // one launch: the next level of every program in progs_ (+ `fresh`'s level 1 when given)
     void launch_step(Inflight* fresh, unsigned long long* stamps);
     void retire_done();

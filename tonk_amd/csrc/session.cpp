@@ -345,6 +345,14 @@ struct Stream {
     }
 
     std::unique_ptr<wl::Runner<Stream, Stream>> runner;
+
+    // free-running schedule (Session::fr_*): the next step this stream runs, a claim flag (one
+    // thread at a time), the send clock of the step being run, and its part of each open program
+    std::atomic<uint32_t> next_step{0};
+    std::atomic<uint8_t> busy{0};
+    uint64_t clock = 0;
+    static const unsigned kParts = 8;
+    Device::Part parts[kParts];
 };
 
 // One stream = one Context (its own arena range and pending program), so host threads can take
@@ -384,6 +392,7 @@ struct Session {
     std::atomic<bool> quit{false};
 
     ~Session() {
+        if (fr_running) fr_drain();
         quit.store(true);
         {
             std::lock_guard<std::mutex> lk(mu);
@@ -490,7 +499,8 @@ struct Session {
             }
             seen = gen.load(std::memory_order_acquire);
             if (quit.load(std::memory_order_acquire)) return;
-            drain(*job, ti);
+            if (job_kind.load(std::memory_order_acquire) == 1) fr_loop(ti);
+            else drain(*job, ti);
             if (left.fetch_sub(1, std::memory_order_acq_rel) == 1 && main_sleeping.load()) {
                 std::lock_guard<std::mutex> lk(mu);
                 cv_done.notify_one();
@@ -511,15 +521,20 @@ struct Session {
             return;
         }
         job = &f;
+        job_kind.store(0, std::memory_order_relaxed);
         left.store(threads.size(), std::memory_order_relaxed);
         gen.fetch_add(1, std::memory_order_seq_cst);
         if (sleepers.load(std::memory_order_seq_cst) > 0) {
             std::lock_guard<std::mutex> lk(mu);
             cv_start.notify_all();
         }
-        // The caller blocks for the end of the pass (after a short spin): the workers already
-        // occupy the job's CPU share (cpu.max on the GPU box), a spinning 17th thread would
-        // push the process over its quota and get it throttled.
+        wait_pass_end();
+    }
+
+    // The caller blocks for the end of the pass (after a short spin): the workers already
+    // occupy the job's CPU share (cpu.max on the GPU box), a spinning 17th thread would push the
+    // process over its quota and get it throttled.
+    void wait_pass_end() {
         const auto until = std::chrono::steady_clock::now() + std::chrono::microseconds(20);
         unsigned k = 0;
         while (left.load(std::memory_order_acquire) != 0) {
@@ -532,6 +547,260 @@ struct Session {
                 break;
             }
         }
+    }
+
+    // ---- free-running schedule (sessions with worker threads, level pipelining) ----
+    // tamd_session_step publishes a step and returns; the workers run every stream through every
+    // published step, each stream's steps in order, a thread's own streams first (s % T == t: its
+    // state stays in that core's caches) and any other runnable stream when it has none, with no
+    // barrier between steps: a thread that finishes its streams of step k goes on with step k + 1
+    // while others finish k.  Right after a stream's control plane for step k, its thread adds
+    // the stream's part to program k (Device::add_part: an atomic reservation in the program's
+    // slot, no global layout); the caller launches program k once every stream has added its part
+    // (Device::close_program), programs in order.  Steps run at most fr_ahead ahead of the last
+    // launched program.  All HIP calls stay on the caller's thread.
+    struct FrProg {
+        uint32_t originals = 0;
+        bool finish = false;
+        int handle = -1;
+        uint64_t epoch = 0, clock = 0;
+        std::atomic<uint32_t> remaining{0};
+    };
+    static const unsigned kFrRing = Stream::kParts;
+    FrProg fr_progs[kFrRing];
+    bool fr_mode = false, fr_running = false;
+    std::atomic<int> job_kind{0};             // pool job: 0 run_all pass, 1 fr_loop
+    std::atomic<bool> fr_stop{false};
+    std::atomic<uint32_t> fr_published{0};
+    uint32_t fr_launched = 0, fr_ahead = 2;
+    uint64_t fr_next_epoch = 1;
+    std::atomic<uint64_t> fr_released{0};     // completed epoch (rows freed up to it are reusable)
+    std::mutex fr_mu;
+    std::condition_variable cv_fr, cv_main;
+    std::atomic<int> fr_sleepers{0};
+    std::atomic<bool> fr_main_waiting{false};
+    std::vector<std::vector<uint64_t>> fr_vbase;  // record mode: per program, per stream: first digest index
+
+    void start_fr() {
+        if (fr_running) return;
+        fr_stop.store(false);
+        job_kind.store(1, std::memory_order_relaxed);
+        left.store(threads.size(), std::memory_order_relaxed);
+        gen.fetch_add(1, std::memory_order_seq_cst);
+        if (sleepers.load(std::memory_order_seq_cst) > 0) {
+            std::lock_guard<std::mutex> lk(mu);
+            cv_start.notify_all();
+        }
+        fr_running = true;
+    }
+
+    void stop_fr() {
+        if (!fr_running) return;
+        fr_stop.store(true, std::memory_order_seq_cst);
+        {
+            std::lock_guard<std::mutex> lk(fr_mu);
+            cv_fr.notify_all();
+        }
+        wait_pass_end();
+        fr_running = false;
+        job_kind.store(0);
+        double sum = 0, mx = 0;
+        for (double b : busy_ms) {
+            sum += b;
+            if (b > mx) mx = b;
+        }
+        host_ms[1] += sum;
+        host_ms[5] += mx;
+        std::fill(busy_ms.begin(), busy_ms.end(), 0.0);
+        for (double f : fill_ms) host_ms[3] += f;  // stolen stream steps
+        std::fill(fill_ms.begin(), fill_ms.end(), 0.0);
+    }
+
+    // A runnable stream for thread ti (claimed), or -1: its own streams first, the one furthest
+    // behind; otherwise any other stream, again the one furthest behind (it holds up the oldest
+    // open program).
+    int fr_pick(size_t ti) {
+        const uint32_t pub = fr_published.load(std::memory_order_acquire);
+        const size_t T = threads.size(), n = streams.size();
+        for (int pass = 0; pass < 2; ++pass) {
+            int best = -1;
+            uint32_t bk = ~0u;
+            for (size_t s = pass ? 0 : ti; s < n; s += pass ? 1 : T) {
+                Stream& st = *streams[s];
+                const uint32_t k = st.next_step.load(std::memory_order_acquire);
+                if (k < pub && k < bk && !st.busy.load(std::memory_order_relaxed)) {
+                    best = (int)s;
+                    bk = k;
+                }
+            }
+            if (best < 0) continue;
+            Stream& st = *streams[best];
+            if (st.busy.exchange(1, std::memory_order_acq_rel)) return -2;  // raced: look again
+            if (st.next_step.load(std::memory_order_acquire) < pub) return best;
+            st.busy.store(0, std::memory_order_release);
+            return -2;
+        }
+        return -1;
+    }
+
+    void fr_loop(size_t ti) {
+        for (;;) {
+            if (fr_stop.load(std::memory_order_acquire)) return;
+            const int s = fr_pick(ti);
+            if (s >= 0) {
+                fr_run(s, ti);
+                continue;
+            }
+            if (s == -2) continue;
+            // idle: spin a while for the next step, then sleep until it is published
+            const uint32_t seen = fr_published.load(std::memory_order_acquire);
+            const auto until = std::chrono::steady_clock::now() + std::chrono::nanoseconds(spin_ns());
+            unsigned k = 0;
+            bool woke = false;
+            while (!fr_stop.load(std::memory_order_acquire)) {
+                if (fr_published.load(std::memory_order_acquire) != seen) { woke = true; break; }
+                __builtin_ia32_pause();
+                if ((++k & 255) == 0) {
+                    if (fr_pick_ready()) { woke = true; break; }
+                    if (std::chrono::steady_clock::now() > until) break;
+                }
+            }
+            if (woke || fr_stop.load(std::memory_order_acquire)) continue;
+            std::unique_lock<std::mutex> lk(fr_mu);
+            fr_sleepers.fetch_add(1);
+            cv_fr.wait(lk, [&] {
+                return fr_stop.load() || fr_published.load() != seen;
+            });
+            fr_sleepers.fetch_sub(1);
+        }
+    }
+    // some stream can run (a cheap check without claiming)
+    bool fr_pick_ready() {
+        const uint32_t pub = fr_published.load(std::memory_order_acquire);
+        for (auto& sp : streams)
+            if (sp->next_step.load(std::memory_order_relaxed) < pub && !sp->busy.load(std::memory_order_relaxed))
+                return true;
+        return false;
+    }
+
+    // Stream s's next step (claimed by the caller): control plane, then its part of the program.
+    void fr_run(int s, size_t ti) {
+        typedef std::chrono::steady_clock clk;
+        const auto w0 = clk::now();
+        Stream& st = *streams[s];
+        const uint32_t k = st.next_step.load(std::memory_order_relaxed);
+        FrProg& P = fr_progs[k % kFrRing];
+        Context& c = *ctxs[s];
+        c.rows.release_up_to(fr_released.load(std::memory_order_acquire));
+        st.clock = P.clock;
+        if (P.finish) st.runner->finish();
+        else st.runner->advance(P.originals);
+        c.prepare_flush();
+        Device::Part& part = st.parts[k % kFrRing];
+        dev.add_part(P.handle, c.pb, part);
+        part.verify.clear();
+        if (st.tr.on) {
+            // record mode: the digests of this step's rows, taken once program k completes;
+            // an entry's index is (program, position in this stream's part)
+            SessTranscript& t = st.tr;
+            uint64_t local = 0;
+            for (size_t e = t.reg_enc; e < t.pend_enc.size(); ++e) {
+                t.pend_enc[e].v = ((uint64_t)k << 32) | local++;
+                part.verify.push_back(Device::VerifyDesc{(uint32_t)c.rows.offset(t.pend_enc[e].row), t.pend_enc[e].total, 0, 0});
+            }
+            for (size_t e = t.reg_dec; e < t.pend_dec.size(); ++e) {
+                t.pend_dec[e].v = ((uint64_t)k << 32) | local++;
+                part.verify.push_back(Device::VerifyDesc{(uint32_t)c.rows.offset(t.pend_dec[e].row), t.pend_dec[e].upper, 1, 0});
+            }
+            t.reg_enc = t.pend_enc.size();
+            t.reg_dec = t.pend_dec.size();
+        }
+        c.finish_flush(false);
+        busy_ms[ti] += std::chrono::duration<double, std::milli>(clk::now() - w0).count();
+        if ((size_t)s % threads.size() != ti) fill_ms[ti] += 1.0;  // (fr: counts steps run by a thief)
+        st.next_step.store(k + 1, std::memory_order_release);
+        st.busy.store(0, std::memory_order_release);
+        if (P.remaining.fetch_sub(1, std::memory_order_acq_rel) == 1 && fr_main_waiting.load()) {
+            std::lock_guard<std::mutex> lk(fr_mu);
+            cv_main.notify_one();
+        }
+    }
+
+    // Launch every program whose parts are all in, in order.
+    void fr_launch_ready() {
+        typedef std::chrono::steady_clock clk;
+        const uint32_t pub = fr_published.load(std::memory_order_relaxed);
+        std::vector<Device::Part*> parts(streams.size());
+        while (fr_launched < pub) {
+            FrProg& P = fr_progs[fr_launched % kFrRing];
+            if (P.remaining.load(std::memory_order_acquire) != 0) break;
+            const auto t0 = clk::now();
+            for (size_t i = 0; i < streams.size(); ++i) parts[i] = &streams[i]->parts[fr_launched % kFrRing];
+            if (prm.record) {
+                std::vector<uint64_t> base(streams.size());
+                for (size_t i = 0; i < streams.size(); ++i) {
+                    base[i] = verify_count;
+                    verify_count += parts[i]->verify.size();
+                }
+                if (fr_vbase.size() <= fr_launched) fr_vbase.resize(fr_launched + 1);
+                fr_vbase[fr_launched].swap(base);
+            }
+            last_ticket = dev.close_program(P.handle, parts.data(), parts.size());
+            epoch_ticket.push_back(std::make_pair(P.epoch, last_ticket));
+            ++fr_launched;
+            fr_released.store(completed_epoch(), std::memory_order_release);
+            host_ms[4] += std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+        }
+    }
+
+    // Block until the oldest unlaunched program has all its parts, then launch what is ready.
+    void fr_wait_one() {
+        typedef std::chrono::steady_clock clk;
+        const auto t0 = clk::now();
+        FrProg& P = fr_progs[fr_launched % kFrRing];
+        const auto until = t0 + std::chrono::microseconds(20);
+        unsigned k = 0;
+        while (P.remaining.load(std::memory_order_acquire) != 0) {
+            __builtin_ia32_pause();
+            if ((++k & 255) == 0 && clk::now() > until) {
+                std::unique_lock<std::mutex> lk(fr_mu);
+                fr_main_waiting.store(true);
+                cv_main.wait(lk, [&] { return P.remaining.load() == 0; });
+                fr_main_waiting.store(false);
+                break;
+            }
+        }
+        host_ms[0] += std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+        fr_launch_ready();
+    }
+
+    void fr_step(uint32_t originals, bool finish) {
+        typedef std::chrono::steady_clock clk;
+        start_fr();
+        while (fr_published.load(std::memory_order_relaxed) - fr_launched >= fr_ahead) fr_wait_one();
+        const uint32_t k = fr_published.load(std::memory_order_relaxed);
+        FrProg& P = fr_progs[k % kFrRing];
+        P.originals = originals;
+        P.finish = finish;
+        P.clock = time_msec();
+        P.epoch = fr_next_epoch++;
+        const auto t0 = clk::now();
+        P.handle = dev.open_program();
+        host_ms[2] += std::chrono::duration<double, std::milli>(clk::now() - t0).count();
+        P.remaining.store((uint32_t)streams.size(), std::memory_order_relaxed);
+        fr_published.store(k + 1, std::memory_order_seq_cst);
+        if (fr_sleepers.load(std::memory_order_seq_cst) > 0) {
+            std::lock_guard<std::mutex> lk(fr_mu);
+            cv_fr.notify_all();
+        }
+        fr_launch_ready();
+    }
+
+    // Every published step run and launched; the workers leave their loop.
+    void fr_drain() {
+        if (!fr_mode) return;
+        while (fr_launched < fr_published.load(std::memory_order_relaxed)) fr_wait_one();
+        stop_fr();
     }
 
     // Highest epoch whose program has completed on the device (its freed rows are reusable).
@@ -562,6 +831,7 @@ struct Session {
     uint64_t closed_epoch = 0;
 
     void step(uint32_t originals, bool finish) {
+        if (fr_mode) { fr_step(originals, finish); return; }
         if (deferred) { step_deferred(originals, finish); return; }
         typedef std::chrono::steady_clock clk;
         auto ms = [](clk::time_point a, clk::time_point b) {
@@ -576,6 +846,7 @@ struct Session {
         run_all([this, originals, finish, rel, &ms](size_t i, size_t ti) {
             const auto w0 = clk::now();
             Context& c = *ctxs[i];
+            streams[i]->clock = clock_msec;
             c.rows.release_up_to(rel);
             if (finish) streams[i]->runner->finish();
             else streams[i]->runner->advance(originals);
@@ -661,6 +932,7 @@ struct Session {
                 if (early && fills_left.fetch_sub(1, std::memory_order_acq_rel) == 1) launch_closed();
             }
             c.rows.release_up_to(rel);
+            streams[i]->clock = clock_msec;
             if (finish) streams[i]->runner->finish();
             else streams[i]->runner->advance(originals);
             c.prepare_flush();
@@ -696,6 +968,7 @@ struct Session {
 
     // Fill and launch a closed program still waiting (end of a run: wait / finish).
     void flush_closed() {
+        fr_drain();
         if (!have_closed) return;
         run_all([this](size_t i, size_t) { dev.fill(i); });
         launch_closed();
@@ -786,14 +1059,19 @@ struct Session {
 
     // Fill the transcript lines from the device digests (end of a run: every program done).
     void resolve_transcripts() {
-        register_verify();  // (entries of a program never launched: none, unless the run failed)
+        if (!fr_mode) register_verify();  // (entries of a program never launched: none, unless the run failed)
         std::vector<Device::VerifyOut> res;
         dev.verify_results(res);
         if (verify_base + res.size() != verify_count) {
             error = "verification digests missing";
             return;
         }
-        auto get = [&](uint64_t v) -> const Device::VerifyOut& { return res[v - verify_base]; };
+        size_t si = 0;
+        auto get = [&](uint64_t v) -> const Device::VerifyOut& {
+            // free-running schedule: v = (program, position in the stream's part)
+            if (fr_mode) v = fr_vbase[v >> 32][si] + (v & 0xffffffffu);
+            return res[v - verify_base];
+        };
         for (auto& sp : streams) {
             Stream& s = *sp;
             char line[256];
@@ -817,6 +1095,7 @@ struct Session {
             s.tr.pend_enc.clear();
             s.tr.pend_dec.clear();
             s.tr.reg_enc = s.tr.reg_dec = 0;
+            ++si;
         }
         verify_base = verify_count;
         dev.verify_reset();
@@ -840,12 +1119,18 @@ void* tamd_session_create(const tamd_session_params* p, char* err, size_t err_le
     // (the D2H gather right after a program needs all of its levels) and for A/B runs.  A
     // program stays in flight for as many launches as it has levels: 6 staging slots.
     const bool pipe = !p->stage_host && getenv("TONK_AMD_NO_PIPELINE") == nullptr;
-    s->dev.set_program_slots(pipe ? 6 : 2, 16u << 20);
+    const uint32_t nthreads = p->n_threads ? (p->n_threads < p->n_streams ? p->n_threads : p->n_streams) : 1;
+    // The free-running schedule (worker threads, pipelined levels): programs assembled in
+    // parallel (Device::add_part) in 8 slots -- up to fr_ahead open, the rest in flight; otherwise
+    // one laid-out program per step in 6 slots (TONK_AMD_PASSES=1 keeps the pass schedule).
+    s->fr_mode = pipe && nthreads > 1 && getenv("TONK_AMD_NO_DEFER") == nullptr && getenv("TONK_AMD_PASSES") == nullptr;
+    if (const char* a = getenv("TONK_AMD_RUNAHEAD")) s->fr_ahead = (uint32_t)atoi(a) > 0 ? (uint32_t)atoi(a) : 1u;
+    if (s->fr_mode) s->dev.set_assembly_slots(8, 24);
+    else s->dev.set_program_slots(pipe ? 6 : 2, 16u << 20);
     if (!s->dev.init((int)p->device, p->arena_bytes)) return fail(s->dev.error());
     s->dev.set_pipelined(pipe);
     if (!s->dev.gf_selftest()) return fail("device GF(256) self test failed");
 
-    const uint32_t nthreads = p->n_threads ? (p->n_threads < p->n_streams ? p->n_threads : p->n_streams) : 1;
     const uint64_t range = (s->dev.arena_bytes() / p->n_streams) & ~(uint64_t)(TAMD_ROW_UNIT - 1);
     s->row_cap = ((p->payload_max + 4 + 63) / 64) * 64;
     s->busy_ms.assign(nthreads, 0.0);
@@ -896,7 +1181,7 @@ void* tamd_session_create(const tamd_session_params* p, char* err, size_t err_le
         q.seed_data = 1000 + q.stream_id;
         q.seed_loss = 2000 + q.stream_id;
         st->enc.reset(new Encoder(ctx.get(), raw->row_cap));
-        st->enc->set_clock(&raw->clock_msec);
+        st->enc->set_clock(&st->clock);
         st->dec.reset(new Decoder(ctx.get(), raw->row_cap));
         st->tr.on = p->record != 0;
         st->runner.reset(new wl::Runner<Stream, Stream>(st->p, *st, *st));

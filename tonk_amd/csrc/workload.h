@@ -198,6 +198,14 @@ public:
             int drawn = -1;  // loss draw of original next_ made by quiet_run (-1: not drawn)
             if (batching) {
                 const uint32_t k = quiet_run(end, drawn);
+                if (k >= 1 && next_ + k < end) {
+                    // the quiet run and the original after it (lost, or the one an event follows)
+                    // as one batch of adds, then that original's events
+                    if (drawn < 0) drawn = ch_.lost() ? 1 : 0;  // (its draw, as one() makes it)
+                    run_with_event(next_, k, drawn != 0);
+                    next_ += k + 1;
+                    continue;
+                }
                 if (k > 1) {
                     run_quiet(next_, k);
                     next_ += k;
@@ -350,6 +358,42 @@ private:
         if (p_.ack_every) ack_countdown_ -= k;
     }
 
+    // k quiet originals from i0 and original e = i0 + k after them (`lost`: its channel draw):
+    // the encoder adds all k + 1 in one batch and the decoder the delivered ones; then e's
+    // recovery tokens, acknowledgement and ARQ, exactly as one(e) does them.  The two codecs
+    // only meet through recovery packets and acknowledgements, which come after e in both orders,
+    // so adding e to the encoder before the run reaches the decoder changes no call's result.
+    void run_with_event(uint32_t i0, uint32_t k, bool lost) {
+        const uint32_t e = i0 + k;
+        const uint32_t len = payload_length(p_, i0);
+        uint32_t col0 = 0;
+        if (!be_.enc_add_run(i0, k + 1, len, &col0)) {
+            run_quiet(i0, k);
+            one(e, lost ? 1 : 0);
+            return;
+        }
+        for (uint32_t j = 0; j <= k; ++j) col_of_[i0 + j] = (col0 + j) & 0x3fffffu;
+        s_.originals += k + 1;
+        const uint32_t kd = lost ? k : k + 1;  // delivered
+        if (be_.dec_add_run(col0, i0, kd, len)) {
+            memset(&have_[i0], 1, kd);
+        } else {
+            for (uint32_t j = 0; j < kd; ++j) {
+                const int ro = be_.dec_add_original(col_of_[i0 + j], i0 + j, len);
+                tr_.on_event('O', ro, col_of_[i0 + j], 0);
+                have_[i0 + j] = 1;
+                decode_loop();
+            }
+        }
+        if (lost) {
+            ++s_.lost_originals;
+            pending_arq_.push_back(e);
+        }
+        tokens_ += k * p_.fec_rate_q16;
+        if (p_.ack_every) ack_countdown_ -= k;
+        events_after(e);
+    }
+
     // One original: add, channel, recovery tokens, acknowledgement, retransmission, ARQ.
     // `drawn`: its loss draw when already made (0 delivered, 1 lost), -1 to draw here.
     void one(uint32_t i, int drawn = -1) {
@@ -373,6 +417,11 @@ private:
             decode_loop();
         }
 
+        events_after(i);
+    }
+
+    // What follows original i: recovery tokens, acknowledgement, retransmission tick, ARQ.
+    void events_after(uint32_t i) {
         tokens_ += p_.fec_rate_q16;
         while (tokens_ >= 65536u) {
             tokens_ -= 65536u;
