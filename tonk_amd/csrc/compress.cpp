@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 
+#include <condition_variable>
 #include <mutex>
 #include <stdio.h>
 #include <stdlib.h>
@@ -15,6 +16,7 @@
 
 extern "C" __global__ void tamd_lz_compress(const tamd_lz_job*, const tamd_lz_msg*, const uint8_t*, uint8_t*,
                                             uint32_t*, unsigned long long*);
+extern "C" __global__ void tamd_lz_scatter_ring(const tamd_lz_scatter*, const uint8_t*);
 
 namespace tamd {
 namespace {
@@ -22,26 +24,27 @@ namespace {
 // History ring of PacketCompression.h:36-63 (kCompressionDictBytes = 24 * 1000).
 const uint32_t kDictBytes = 24 * 1000;
 
+// The FSE table blob on each device (uploaded once per device, kept for the process).
 struct DeviceTables {
     std::mutex mu;
-    int device = -1;
-    uint8_t* fse = nullptr;
+    std::vector<uint8_t*> fse;  // by device index
 };
 DeviceTables g_tables;
 
 const uint8_t* device_fse(int device) {
     std::lock_guard<std::mutex> g(g_tables.mu);
-    if (g_tables.fse && g_tables.device == device) return g_tables.fse;
+    if (device < 0) return nullptr;
+    if ((size_t)device < g_tables.fse.size() && g_tables.fse[device]) return g_tables.fse[device];
     std::vector<uint8_t> blob(TAMD_FSE_BYTES, 0);
     tamd_fse_blob(blob.data());
     uint8_t* d = nullptr;
-    if (hipMalloc((void**)&d, TAMD_FSE_BYTES) != hipSuccess) return nullptr;
+    if (hipSetDevice(device) != hipSuccess || hipMalloc((void**)&d, TAMD_FSE_BYTES) != hipSuccess) return nullptr;
     if (hipMemcpy(d, blob.data(), TAMD_FSE_BYTES, hipMemcpyHostToDevice) != hipSuccess) {
         hipFree(d);
         return nullptr;
     }
-    g_tables.fse = d;  // (kept for the process; one device per process in practice)
-    g_tables.device = device;
+    if ((size_t)device >= g_tables.fse.size()) g_tables.fse.resize(device + 1, nullptr);
+    g_tables.fse[device] = d;
     return d;
 }
 
@@ -95,65 +98,162 @@ struct RingTrack {
 struct Compressor {
     uint32_t max = 0;
     int device = 0;
-    const uint8_t* fse = nullptr;
-    uint8_t* ring = nullptr;  // 64 KB device ring of the stream's bytes (linear position & 0xffff)
-    tamd_lz_job* d_job = nullptr;
-    tamd_lz_msg* d_msg = nullptr;
-    uint8_t* d_out = nullptr;
-    uint32_t* d_written = nullptr;
-    uint8_t* h_stage = nullptr;  // pinned: message in, then {written, block} out
+    uint8_t* ring = nullptr;  // device ring of the stream's bytes (linear position & 0xffff) + mirror
     RingTrack ring_track;
     bool failed = false;
+    bool queued = false;      // a call of this compressor is in the current batch
 };
-
-static const uint32_t kRing = 1u << 16;
-static const uint32_t kMirror = 64;  // the ring's first bytes repeated after it (wide loads at its end)
-// pinned staging of the per-message path: [message | descriptor | written | compressed block]
-static size_t stage_msg(uint32_t max) { return ((size_t)max + 63u) & ~(size_t)63u; }
-static size_t stage_written(uint32_t max) { return stage_msg(max) + 64u; }
-static size_t stage_out(uint32_t max) { return stage_written(max) + 64u; }
-static size_t stage_bytes(uint32_t max) { return stage_out(max) + max + 64u; }
 
 }  // namespace tamd
 
 using namespace tamd;
 
-// Every compressor of the process enqueues on one stream (each call is a synchronous round trip);
-// Tonk creates a compressor per connection, most of which may never compress, so a compressor's
-// device buffers are made on its first message.
-static std::mutex g_lz_mu;
-static hipStream_t g_lz_stream = nullptr;
+// ---- the per-message drop-in: concurrent calls combined into one launch ----
+//
+// Tonk compresses each message on the connection's own thread and waits for the result
+// (PacketCompression.cpp:70-118).  One GPU round trip per message is slow next to zstd on the
+// calling thread, so calls from different connections are combined: a caller queues its
+// request; the first caller becomes the leader and runs every queued request as ONE batch (one
+// upload of all messages and descriptors, a scatter into the compressors' rings, one compression
+// launch with a wave per message, one download), then completes them and serves the requests
+// that queued meanwhile.  A batch costs about one round trip however many connections it serves.
+namespace {
+struct LzRequest {
+    Compressor* c;
+    const uint8_t* data;
+    uint32_t bytes;
+    uint8_t* dest;
+    unsigned* written;
+    int rc = 0;
+    bool done = false;
+};
+std::mutex g_req_mu;
+std::condition_variable g_req_cv;
+std::vector<LzRequest*> g_pending;
+bool g_leader = false;
 
-static bool ensure_device(Compressor* c) {
-    if (c->ring) return true;
-    bool ok = (c->fse = device_fse(c->device)) != nullptr;
-    if (ok && !g_lz_stream) ok = hipStreamCreateWithFlags(&g_lz_stream, hipStreamNonBlocking) == hipSuccess;
-    ok = ok && hipMalloc((void**)&c->d_job, sizeof(tamd_lz_job)) == hipSuccess;
-    ok = ok && hipMalloc((void**)&c->d_msg, sizeof(tamd_lz_msg)) == hipSuccess;
-    ok = ok && hipMalloc((void**)&c->d_out, c->max + 64) == hipSuccess;
-    ok = ok && hipMalloc((void**)&c->d_written, 64) == hipSuccess;
-    ok = ok && hipHostMalloc((void**)&c->h_stage, stage_bytes(c->max), hipHostMallocDefault) == hipSuccess;
-    uint8_t* ring = nullptr;
-    ok = ok && hipMalloc((void**)&ring, kRing + kMirror) == hipSuccess;
-    if (ok) {
-        tamd_lz_job job;
-        memset(&job, 0, sizeof(job));
-        job.buf = ring;
-        job.mask = kRing - 1;
-        job.first = 0;
-        job.count = 1;
-        ok = hipMemcpy(c->d_job, &job, sizeof(job), hipMemcpyHostToDevice) == hipSuccess;
-    }
-    if (!ok) {
-        if (ring) hipFree(ring);
+// leader-only launch state (grown on demand)
+struct LzBatchState {
+    int device = -1;
+    hipStream_t st = nullptr;
+    uint8_t* h_in = nullptr;   // pinned: scatter descs | msgs | jobs | message bytes
+    uint8_t* d_in = nullptr;
+    size_t in_cap = 0;
+    uint8_t* h_out = nullptr;  // pinned: written[] | compressed blocks
+    uint8_t* d_out = nullptr;
+    size_t out_cap = 0;
+} g_batch;
+
+size_t align16(size_t n) { return (n + 15) & ~(size_t)15; }
+
+bool grow(uint8_t*& h, uint8_t*& d, size_t& cap, size_t need) {
+    if (need <= cap) return true;
+    if (h) hipHostFree(h);
+    if (d) hipFree(d);
+    h = d = nullptr;
+    cap = need + need / 2;
+    if (hipHostMalloc((void**)&h, cap, hipHostMallocDefault) != hipSuccess || hipMalloc((void**)&d, cap) != hipSuccess) {
+        cap = 0;
         return false;
     }
-    c->ring = ring;
     return true;
 }
 
+// Runs one batch (leader, no lock held); every request of `b` belongs to device b[0]->c->device
+// and names a distinct compressor.
+void run_batch(const std::vector<LzRequest*>& b) {
+    LzBatchState& S = g_batch;
+    const int dev = b[0]->c->device;
+    bool ok = hipSetDevice(dev) == hipSuccess;
+    if (ok && S.device != dev) {  // (a process compresses on one device in practice)
+        if (S.st) hipStreamDestroy(S.st);
+        S.st = nullptr;
+        ok = hipStreamCreateWithFlags(&S.st, hipStreamNonBlocking) == hipSuccess;
+        S.device = ok ? dev : -1;
+    }
+    const uint8_t* fse = ok ? device_fse(dev) : nullptr;
+    ok = ok && fse;
+    const size_t n = b.size();
+    size_t data_bytes = 0, out_bytes = 0;
+    for (LzRequest* r : b) {
+        data_bytes += align16(r->bytes);
+        out_bytes += align16(r->c->max);
+        if (ok && !r->c->ring) {
+            uint8_t* ring = nullptr;
+            if (hipMalloc((void**)&ring, TAMD_LZ_RING + TAMD_LZ_MIRROR) != hipSuccess) r->c->failed = true;
+            else r->c->ring = ring;
+        }
+    }
+    const size_t o_msgs = align16(n * sizeof(tamd_lz_scatter));
+    const size_t o_jobs = o_msgs + align16(n * sizeof(tamd_lz_msg));
+    const size_t o_data = o_jobs + align16(n * sizeof(tamd_lz_job));
+    const size_t o_blocks = align16(n * 4);
+    ok = ok && grow(S.h_in, S.d_in, S.in_cap, o_data + data_bytes) && grow(S.h_out, S.d_out, S.out_cap, o_blocks + out_bytes);
+    if (ok) {
+        tamd_lz_scatter* sc = (tamd_lz_scatter*)S.h_in;
+        tamd_lz_msg* ms = (tamd_lz_msg*)(S.h_in + o_msgs);
+        tamd_lz_job* jb = (tamd_lz_job*)(S.h_in + o_jobs);
+        size_t din = 0, dout = o_blocks;
+        for (size_t i = 0; i < n; ++i) {
+            LzRequest* r = b[i];
+            Compressor* c = r->c;
+            uint64_t pos = 0, win = 0;
+            c->ring_track.place(r->bytes, &pos, &win);
+            // positions are rebased to a multiple of the ring size below the window (same ring
+            // slots, small numbers)
+            const uint64_t base = win & ~(uint64_t)(TAMD_LZ_RING - 1);
+            memcpy(S.h_in + o_data + din, r->data, r->bytes);
+            sc[i].ring = c->ring;
+            sc[i].slot = (uint32_t)(pos & (TAMD_LZ_RING - 1));
+            sc[i].bytes = r->bytes;
+            sc[i].src = (uint32_t)din;
+            sc[i].pad = 0;
+            memset(&ms[i], 0, sizeof(ms[i]));
+            ms[i].pos = (uint32_t)(pos - base);
+            ms[i].len = r->bytes;
+            ms[i].win = (uint32_t)(win - base);
+            ms[i].out = (uint32_t)(dout - o_blocks);
+            ms[i].cap = c->max;
+            memset(&jb[i], 0, sizeof(jb[i]));
+            jb[i].buf = c->ring;
+            jb[i].mask = TAMD_LZ_RING - 1;
+            jb[i].first = (uint32_t)i;
+            jb[i].count = 1;
+            din += align16(r->bytes);
+            dout += align16(c->max);
+        }
+        ok = hipMemcpyAsync(S.d_in, S.h_in, o_data + data_bytes, hipMemcpyHostToDevice, S.st) == hipSuccess;
+        if (ok) {
+            hipLaunchKernelGGL(tamd_lz_scatter_ring, dim3((uint32_t)n), dim3(256), 0, S.st,
+                               (const tamd_lz_scatter*)S.d_in, (const uint8_t*)(S.d_in + o_data));
+            hipLaunchKernelGGL(tamd_lz_compress, dim3((uint32_t)n), dim3(64), 0, S.st, (const tamd_lz_job*)(S.d_in + o_jobs),
+                               (const tamd_lz_msg*)(S.d_in + o_msgs), fse, S.d_out + o_blocks, (uint32_t*)S.d_out,
+                               (unsigned long long*)nullptr);
+            ok = hipGetLastError() == hipSuccess;
+        }
+        ok = ok && hipMemcpyAsync(S.h_out, S.d_out, o_blocks + out_bytes, hipMemcpyDeviceToHost, S.st) == hipSuccess;
+        ok = ok && hipStreamSynchronize(S.st) == hipSuccess;
+    }
+    size_t dout = o_blocks;
+    for (size_t i = 0; i < n; ++i) {
+        LzRequest* r = b[i];
+        Compressor* c = r->c;
+        const uint32_t w = ok ? ((const uint32_t*)S.h_out)[i] : 0;
+        if (!ok || c->failed || w > c->max) {
+            c->failed = true;
+            r->rc = -2;
+        } else {
+            if (w) memcpy(r->dest, S.h_out + dout, w);
+            *r->written = w;
+            r->rc = 0;
+        }
+        dout += align16(c->max);
+    }
+}
+}  // namespace
+
 extern "C" void* tamd_compressor_create(unsigned max_bytes) {
-    if (max_bytes == 0 || max_bytes + max_bytes > kRing || max_bytes > kDictBytes) return nullptr;
+    if (max_bytes == 0 || max_bytes + max_bytes > TAMD_LZ_RING || max_bytes > kDictBytes) return nullptr;
     if (!device_ok()) return nullptr;
     Compressor* c = new Compressor();
     c->max = max_bytes;
@@ -166,14 +266,14 @@ extern "C" void tamd_compressor_destroy(void* cp) {
     Compressor* c = (Compressor*)cp;
     if (!c) return;
     {
-        std::lock_guard<std::mutex> g(g_lz_mu);  // (no call of this compressor is in flight)
+        // (no call of this compressor is queued or in flight: its owner is not calling it)
+        std::unique_lock<std::mutex> g(g_req_mu);
+        g_req_cv.wait(g, [c] { return !c->queued; });
     }
-    if (c->ring) hipFree(c->ring);
-    if (c->d_job) hipFree(c->d_job);
-    if (c->d_msg) hipFree(c->d_msg);
-    if (c->d_out) hipFree(c->d_out);
-    if (c->d_written) hipFree(c->d_written);
-    if (c->h_stage) hipHostFree(c->h_stage);
+    if (c->ring) {
+        hipSetDevice(c->device);
+        hipFree(c->ring);
+    }
     delete c;
 }
 
@@ -183,65 +283,44 @@ extern "C" int tamd_compressor_compress(void* cp, const uint8_t* data, unsigned 
     if (written) *written = 0;
     if (!c || !data || !dest || !written || bytes == 0 || bytes > c->max) return -1;
     if (c->failed) return -2;
-    std::lock_guard<std::mutex> lock(g_lz_mu);
-    if (!ensure_device(c)) {
-        c->failed = true;
-        return -2;
+    LzRequest req;
+    req.c = c;
+    req.data = data;
+    req.bytes = bytes;
+    req.dest = dest;
+    req.written = written;
+    std::unique_lock<std::mutex> lk(g_req_mu);
+    g_pending.push_back(&req);
+    if (g_leader) {
+        g_req_cv.wait(lk, [&req] { return req.done; });
+        return req.rc;
     }
-    hipStream_t const stream = g_lz_stream;
-    uint64_t pos = 0, win = 0;
-    c->ring_track.place(bytes, &pos, &win);
-    // positions passed to the kernel are rebased to a multiple of the ring size below the window
-    // (same ring slots, small numbers)
-    const uint64_t base = win & ~(uint64_t)(kRing - 1);
-    tamd_lz_msg& m = *(tamd_lz_msg*)(c->h_stage + stage_msg(c->max));
-    memset(&m, 0, sizeof(m));
-    m.pos = (uint32_t)(pos - base);
-    m.len = bytes;
-    m.win = (uint32_t)(win - base);
-    m.out = 0;
-    m.cap = c->max;
-    memcpy(c->h_stage, data, bytes);
-    const uint32_t slot = (uint32_t)(pos & (kRing - 1));
-    const uint32_t first = bytes < kRing - slot ? bytes : kRing - slot;
-    bool ok = hipMemcpyAsync(c->ring + slot, c->h_stage, first, hipMemcpyHostToDevice, stream) == hipSuccess;
-    if (first < bytes)
-        ok = ok && hipMemcpyAsync(c->ring, c->h_stage + first, bytes - first, hipMemcpyHostToDevice, stream) ==
-                       hipSuccess;
-    // ring bytes [0, kMirror) also live at [kRing, kRing + kMirror)
-    if (first < bytes) {
-        const uint32_t k = bytes - first < kMirror ? bytes - first : kMirror;
-        ok = ok && hipMemcpyAsync(c->ring + kRing, c->h_stage + first, k, hipMemcpyHostToDevice, stream) ==
-                       hipSuccess;
+    g_leader = true;
+    std::vector<LzRequest*> batch, later;
+    while (!g_pending.empty()) {
+        // one request per compressor and one device per batch (a compressor's messages are
+        // placed in its ring in call order); the rest waits for the next batch
+        batch.clear();
+        later.clear();
+        for (LzRequest* r : g_pending) {
+            if (r->c->queued || r->c->device != g_pending[0]->c->device) later.push_back(r);
+            else {
+                r->c->queued = true;
+                batch.push_back(r);
+            }
+        }
+        g_pending.swap(later);
+        lk.unlock();
+        run_batch(batch);
+        lk.lock();
+        for (LzRequest* r : batch) {
+            r->c->queued = false;
+            r->done = true;
+        }
+        g_req_cv.notify_all();
     }
-    if (slot < kMirror) {
-        const uint32_t k = (kMirror - slot) < first ? kMirror - slot : first;
-        ok = ok && hipMemcpyAsync(c->ring + kRing + slot, c->h_stage, k, hipMemcpyHostToDevice, stream) ==
-                       hipSuccess;
-    }
-    ok = ok && hipMemcpyAsync(c->d_msg, &m, sizeof(m), hipMemcpyHostToDevice, stream) == hipSuccess;
-    if (ok) {
-        hipLaunchKernelGGL(tamd_lz_compress, dim3(1), dim3(64), 0, stream, c->d_job, c->d_msg, c->fse, c->d_out,
-                           c->d_written, (unsigned long long*)nullptr);
-        ok = hipGetLastError() == hipSuccess;
-    }
-    uint32_t* h_written = (uint32_t*)(c->h_stage + stage_written(c->max));
-    uint8_t* h_out = c->h_stage + stage_out(c->max);
-    ok = ok && hipMemcpyAsync(h_written, c->d_written, 4, hipMemcpyDeviceToHost, stream) == hipSuccess;
-    ok = ok && hipMemcpyAsync(h_out, c->d_out, c->max, hipMemcpyDeviceToHost, stream) == hipSuccess;
-    ok = ok && hipStreamSynchronize(stream) == hipSuccess;
-    if (!ok) {
-        c->failed = true;
-        return -2;
-    }
-    const uint32_t w = *h_written;
-    if (w > c->max) {
-        c->failed = true;
-        return -2;
-    }
-    if (w) memcpy(dest, h_out, w);
-    *written = w;
-    return 0;
+    g_leader = false;
+    return req.rc;
 }
 
 extern "C" int tamd_compress_batch(const void* dev_data, uint64_t stride, uint32_t n_streams, uint32_t n_msgs,

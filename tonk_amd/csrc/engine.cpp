@@ -531,6 +531,25 @@ static void emit_packets(ProgramBuilder& pb, const std::vector<LaneSums::T>& ter
     }
 }
 
+// Advance a run-list cursor past `count` packets without emitting them.
+static void skip_packets(const std::vector<LaneSums::T>& terms, size_t& ri, uint32_t& rdone, uint32_t count) {
+    while (count > 0 && ri < terms.size()) {
+        const uint32_t left = terms[ri].count - rdone;
+        if (left > count) {
+            rdone += count;
+            return;
+        }
+        count -= left;
+        ++ri;
+        rdone = 0;
+    }
+}
+
+uint32_t LaneSums::inline_max() {
+    static const uint32_t v = getenv("TONK_AMD_INLINE_SEG") ? (uint32_t)atoi(getenv("TONK_AMD_INLINE_SEG")) : 3u;  // A/B
+    return v;
+}
+
 // One scan = the lane's packets in order with snapshots (STOREC) at their read points.  A long
 // scan would be one wave walking hundreds of rows, so it is cut into chunks of at most kChunk
 // packets, split at every snapshot point: each chunk op (level 1) writes its three partial sums
@@ -572,14 +591,18 @@ void LaneSums::emit_scan(RowTable& rows, ProgramBuilder& pb, const RowId* base, 
         return;
     }
 
-    // chunk boundaries: every snapshot point, and at most kChunk packets apart.  A chunk's three
-    // partial sums go to one row of three parts (one allocation per chunk).
-    thread_local std::vector<uint32_t> cuts;
-    thread_local std::vector<RowId> deltas;
-    cuts.clear();
-    deltas.clear();
+    // Segments: cut at every snapshot point, and at most kChunk packets apart.  A segment of
+    // more than inline_max() packets is a chunk op (level 1) whose three partial sums go to one
+    // row of three parts; the chain op adds them.  A shorter one is walked by the chain op
+    // itself: its packets are read once, where a chunk would write three partial rows and the
+    // chain read them back (dense snapshots -- a recovery row every few lane packets -- made most
+    // chunks one to three packets long).
+    struct Seg { uint32_t pos, count; RowId delta; };
+    thread_local std::vector<Seg> segs;
+    segs.clear();
     const uint32_t wunits = (width + TAMD_ROW_UNIT - 1) / TAMD_ROW_UNIT;
     const uint32_t wcap = wunits * TAMD_ROW_UNIT;
+    const uint32_t imax = inline_max();
     uint32_t pos = 0;
     size_t sj = 0;
     while (pos < n) {
@@ -587,31 +610,41 @@ void LaneSums::emit_scan(RowTable& rows, ProgramBuilder& pb, const RowId* base, 
         uint32_t end = pos + kChunk;
         if (sj < snaps.size() && snaps[sj].after < end) end = snaps[sj].after;
         if (end > n) end = n;
-        cuts.push_back(pos);
-        pb.begin_op();
-        emit_packets(pb, terms, ri, rdone, end - pos);
-        const RowId d = rows.alloc(3 * wcap);
-        deltas.push_back(d);
-        if (d != kNoRow)
-            for (unsigned s = 0; s < 3; ++s) pb.op_storec_part(d, s * wunits, wcap, wcap, unit[s], s == 0);
-        pb.end_op(1);
+        Seg g{pos, end - pos, kNoRow};
+        if (g.count <= imax) {
+            skip_packets(terms, ri, rdone, g.count);
+        } else {
+            pb.begin_op();
+            emit_packets(pb, terms, ri, rdone, g.count);
+            g.delta = rows.alloc(3 * wcap);
+            if (g.delta != kNoRow)
+                for (unsigned s = 0; s < 3; ++s) pb.op_storec_part(g.delta, s * wunits, wcap, wcap, unit[s], s == 0);
+            pb.end_op(1);
+        }
+        segs.push_back(g);
         pos = end;
     }
+    ri = 0;
+    rdone = 0;
     pb.begin_op();
     for (unsigned s = 0; s < 3; ++s)
         if (base[s] != kNoRow) pb.op_acc(base[s], 1, rows.cap_bytes(base[s]), s);
-    for (size_t k = 0; k < cuts.size(); ++k) {
-        snapshots(cuts[k]);
-        const RowId d = deltas[k];
-        if (d != kNoRow)
-            for (unsigned s = 0; s < 3; ++s) pb.op_acc_part(d, s * wunits, 1, wcap, s);
+    for (const Seg& g : segs) {
+        snapshots(g.pos);
+        if (g.count <= imax) {
+            emit_packets(pb, terms, ri, rdone, g.count);
+        } else {
+            skip_packets(terms, ri, rdone, g.count);
+            if (g.delta != kNoRow)
+                for (unsigned s = 0; s < 3; ++s) pb.op_acc_part(g.delta, s * wunits, 1, wcap, s);
+        }
     }
     snapshots(n);
     if (final_rows)
         for (unsigned s = 0; s < 3; ++s)
             if (final_rows[s] != kNoRow) pb.op_storec(final_rows[s], rows.cap_bytes(final_rows[s]), unit[s]);
     pb.end_op(snap_level(rows, base));
-    for (RowId d : deltas) rows.free_deferred(d);  // read only inside this program
+    for (const Seg& g : segs) rows.free_deferred(g.delta);  // read only inside this program
 }
 
 void LaneSums::flush(RowTable& rows, ProgramBuilder& pb, const ExpansionTable& ex) {

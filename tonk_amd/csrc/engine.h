@@ -326,6 +326,7 @@ public:
     // a run of `count` lane packets: rows off + k*stride, columns col + 8k (count 1: a single row)
     struct T { RowId row; uint32_t len, off, stride, count, col; };
     static uint32_t chunk();  // longest packet walk of one scan op (see emit_scan)
+    static uint32_t inline_max();  // segments this short are walked by the chain op (emit_scan)
     // Level of snapshot rows: chunk ops run at level 1, the chain op that stores the snapshots at
     // level 2 (a short scan is one op, also placed at level 2).  Readers are assigned levels when
     // they read, before the scan is emitted, so the level is fixed up front.

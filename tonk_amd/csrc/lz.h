@@ -7,6 +7,14 @@
 
 #define TAMD_LZ_MAX_MESSAGE 2048u  // larger messages are stored uncompressed (written = 0)
 #define TAMD_LZ_WINDOW 32768u      // history bytes inserted into a job's hash table
+#define TAMD_LZ_RING 65536u        // per-compressor device ring of the stream's bytes (the drop-in)
+#define TAMD_LZ_MIRROR 64u         // the ring's first bytes repeated after it (wide loads at its end)
+
+// The drop-in's staging: message bytes land in their compressor's ring (one workgroup each).
+typedef struct tamd_lz_scatter {
+    uint8_t* ring;
+    uint32_t slot, bytes, src, pad;
+} tamd_lz_scatter;
 
 // A run of consecutive messages of one stream.  `buf` holds the stream's bytes at their linear
 // positions (masked by `mask`: a power-of-two ring, or ~0 for a linear array).

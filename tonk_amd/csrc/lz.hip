@@ -366,3 +366,17 @@ tamd_lz_compress(const tamd_lz_job* __restrict__ jobs, const tamd_lz_msg* __rest
 #pragma unroll
         for (uint32_t k = 0; k < 5; ++k) prof[5 * blockIdx.x + k] = ph[k];
 }
+
+// The per-message drop-in's staging (compress.cpp): each message of a combined batch is copied
+// from the batch upload into its compressor's ring at its slot, wrapping at the ring's end, with
+// the ring's first TAMD_LZ_MIRROR bytes mirrored after it.  One workgroup per message.
+extern "C" __global__ void __launch_bounds__(256)
+tamd_lz_scatter_ring(const tamd_lz_scatter* __restrict__ d, const uint8_t* __restrict__ src) {
+    const tamd_lz_scatter s = d[blockIdx.x];
+    for (uint32_t i = threadIdx.x; i < s.bytes; i += blockDim.x) {
+        const uint32_t p = (s.slot + i) & (TAMD_LZ_RING - 1u);
+        const uint8_t b = src[s.src + i];
+        s.ring[p] = b;
+        if (p < TAMD_LZ_MIRROR) s.ring[TAMD_LZ_RING + p] = b;
+    }
+}

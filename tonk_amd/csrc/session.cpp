@@ -616,29 +616,44 @@ struct Session {
         std::fill(fill_ms.begin(), fill_ms.end(), 0.0);
     }
 
-    // A runnable stream for thread ti (claimed), or -1: its own streams first, the one furthest
-    // behind; otherwise any other stream, again the one furthest behind (it holds up the oldest
-    // open program).
+    // A runnable stream for thread ti (claimed), or -1.  Its own streams first, the one furthest
+    // behind.  Otherwise a stream of a thread in its group of 8 (neighbouring cores: the stream's
+    // state is still in the shared L3), and beyond the group only a stream that holds up the
+    // oldest unlaunched program: a stolen stream's state moves to another core's caches, which
+    // costs more than it saves unless the launch waits for it (TONK_AMD_STEAL=0: steal anything).
+    std::atomic<uint32_t> fr_launched_pub{0};
     int fr_pick(size_t ti) {
+        const int best = fr_scan(ti);
+        if (best < 0) return -1;
         const uint32_t pub = fr_published.load(std::memory_order_acquire);
+        Stream& st = *streams[best];
+        if (st.busy.exchange(1, std::memory_order_acq_rel)) return -2;  // raced: look again
+        if (st.next_step.load(std::memory_order_acquire) < pub) return best;
+        st.busy.store(0, std::memory_order_release);
+        return -2;
+    }
+    // The stream fr_pick would take for thread ti (not claimed), or -1.
+    int fr_scan(size_t ti) {
+        static const int steal_mode = getenv("TONK_AMD_STEAL") ? atoi(getenv("TONK_AMD_STEAL")) : 1;  // A/B
+        const uint32_t pub = fr_published.load(std::memory_order_acquire);
+        const uint32_t oldest = fr_launched_pub.load(std::memory_order_acquire);
         const size_t T = threads.size(), n = streams.size();
-        for (int pass = 0; pass < 2; ++pass) {
+        const size_t group = ti / 8;
+        for (int pass = 0; pass < 3; ++pass) {
+            if (pass == 1 && steal_mode == 0) continue;
             int best = -1;
             uint32_t bk = ~0u;
             for (size_t s = pass ? 0 : ti; s < n; s += pass ? 1 : T) {
+                if (pass == 1 && (s % T) / 8 != group) continue;
                 Stream& st = *streams[s];
                 const uint32_t k = st.next_step.load(std::memory_order_acquire);
+                if (pass == 2 && steal_mode != 0 && k != oldest) continue;
                 if (k < pub && k < bk && !st.busy.load(std::memory_order_relaxed)) {
                     best = (int)s;
                     bk = k;
                 }
             }
-            if (best < 0) continue;
-            Stream& st = *streams[best];
-            if (st.busy.exchange(1, std::memory_order_acq_rel)) return -2;  // raced: look again
-            if (st.next_step.load(std::memory_order_acquire) < pub) return best;
-            st.busy.store(0, std::memory_order_release);
-            return -2;
+            if (best >= 0) return best;
         }
         return -1;
     }
@@ -652,35 +667,36 @@ struct Session {
                 continue;
             }
             if (s == -2) continue;
-            // idle: spin a while for the next step, then sleep until it is published
+            // idle: spin a while, then sleep until a step is published, a program is launched
+            // (its successor's streams become stealable) or a stolen stream is handed back
             const uint32_t seen = fr_published.load(std::memory_order_acquire);
+            const uint32_t seen_l = fr_launched_pub.load(std::memory_order_acquire);
+            const uint32_t seen_h = fr_handback.load(std::memory_order_acquire);
+            auto changed = [&] {
+                return fr_stop.load(std::memory_order_acquire) || fr_published.load(std::memory_order_acquire) != seen ||
+                       fr_launched_pub.load(std::memory_order_acquire) != seen_l ||
+                       fr_handback.load(std::memory_order_acquire) != seen_h;
+            };
             const auto until = std::chrono::steady_clock::now() + std::chrono::nanoseconds(spin_ns());
             unsigned k = 0;
             bool woke = false;
-            while (!fr_stop.load(std::memory_order_acquire)) {
-                if (fr_published.load(std::memory_order_acquire) != seen) { woke = true; break; }
+            while (!(woke = changed())) {
                 __builtin_ia32_pause();
-                if ((++k & 255) == 0) {
-                    if (fr_pick_ready()) { woke = true; break; }
-                    if (std::chrono::steady_clock::now() > until) break;
-                }
+                if ((++k & 255) == 0 && std::chrono::steady_clock::now() > until) break;
             }
-            if (woke || fr_stop.load(std::memory_order_acquire)) continue;
+            if (woke) continue;
             std::unique_lock<std::mutex> lk(fr_mu);
             fr_sleepers.fetch_add(1);
-            cv_fr.wait(lk, [&] {
-                return fr_stop.load() || fr_published.load() != seen;
-            });
+            cv_fr.wait(lk, [&] { return changed() || fr_scan(ti) >= 0; });
             fr_sleepers.fetch_sub(1);
         }
     }
-    // some stream can run (a cheap check without claiming)
-    bool fr_pick_ready() {
-        const uint32_t pub = fr_published.load(std::memory_order_acquire);
-        for (auto& sp : streams)
-            if (sp->next_step.load(std::memory_order_relaxed) < pub && !sp->busy.load(std::memory_order_relaxed))
-                return true;
-        return false;
+    std::atomic<uint32_t> fr_handback{0};  // bumped when a thief leaves a stream runnable
+    void fr_wake_workers() {
+        if (fr_sleepers.load(std::memory_order_seq_cst) > 0) {
+            std::lock_guard<std::mutex> lk(fr_mu);
+            cv_fr.notify_all();
+        }
     }
 
     // Stream s's next step (claimed by the caller): control plane, then its part of the program.
@@ -717,9 +733,14 @@ struct Session {
         }
         c.finish_flush(false);
         busy_ms[ti] += std::chrono::duration<double, std::milli>(clk::now() - w0).count();
-        if ((size_t)s % threads.size() != ti) fill_ms[ti] += 1.0;  // (fr: counts steps run by a thief)
+        const bool stolen = (size_t)s % threads.size() != ti;
+        if (stolen) fill_ms[ti] += 1.0;  // (fr: counts steps run by a thief)
         st.next_step.store(k + 1, std::memory_order_release);
         st.busy.store(0, std::memory_order_release);
+        if (stolen && k + 1 < fr_published.load(std::memory_order_acquire)) {
+            fr_handback.fetch_add(1, std::memory_order_seq_cst);  // its owner may be asleep
+            fr_wake_workers();
+        }
         if (P.remaining.fetch_sub(1, std::memory_order_acq_rel) == 1 && fr_main_waiting.load()) {
             std::lock_guard<std::mutex> lk(fr_mu);
             cv_main.notify_one();
@@ -748,6 +769,8 @@ struct Session {
             last_ticket = dev.close_program(P.handle, parts.data(), parts.size());
             epoch_ticket.push_back(std::make_pair(P.epoch, last_ticket));
             ++fr_launched;
+            fr_launched_pub.store(fr_launched, std::memory_order_seq_cst);
+            fr_wake_workers();  // (the next program's streams are now stealable)
             fr_released.store(completed_epoch(), std::memory_order_release);
             host_ms[4] += std::chrono::duration<double, std::milli>(clk::now() - t0).count();
         }
@@ -789,10 +812,7 @@ struct Session {
         host_ms[2] += std::chrono::duration<double, std::milli>(clk::now() - t0).count();
         P.remaining.store((uint32_t)streams.size(), std::memory_order_relaxed);
         fr_published.store(k + 1, std::memory_order_seq_cst);
-        if (fr_sleepers.load(std::memory_order_seq_cst) > 0) {
-            std::lock_guard<std::mutex> lk(fr_mu);
-            cv_fr.notify_all();
-        }
+        fr_wake_workers();
         fr_launch_ready();
     }
 
@@ -1126,7 +1146,11 @@ void* tamd_session_create(const tamd_session_params* p, char* err, size_t err_le
     s->fr_mode = pipe && nthreads > 1 && getenv("TONK_AMD_NO_DEFER") == nullptr && getenv("TONK_AMD_PASSES") == nullptr;
     if (const char* a = getenv("TONK_AMD_RUNAHEAD")) s->fr_ahead = (uint32_t)atoi(a) > 0 ? (uint32_t)atoi(a) : 1u;
     if (s->fr_mode) s->dev.set_assembly_slots(8, 24);
-    else s->dev.set_program_slots(pipe ? 6 : 2, 16u << 20);
+    else {
+        // (TONK_AMD_SLOTS: A/B knob for the slot count of the pass schedule)
+        const size_t slots = getenv("TONK_AMD_SLOTS") ? (size_t)atoi(getenv("TONK_AMD_SLOTS")) : (pipe ? 6 : 2);
+        s->dev.set_program_slots(slots, (p->n_streams <= 4 ? 2u : 16u) << 20);
+    }
     if (!s->dev.init((int)p->device, p->arena_bytes)) return fail(s->dev.error());
     s->dev.set_pipelined(pipe);
     if (!s->dev.gf_selftest()) return fail("device GF(256) self test failed");
