@@ -290,6 +290,7 @@ def single_stream(name: str, device: int, step: int, reps: int = 3) -> dict:
             t1 = time.perf_counter()
             sess.set_timing(False)
             h1 = sess.host_ms()
+            fr = sess.free_running()
             kms, launches = sess.kernel_ms()
             summ = sess.summary()
         finally:
@@ -302,8 +303,9 @@ def single_stream(name: str, device: int, step: int, reps: int = 3) -> dict:
             "kernel_us_per_launch": round(kms * 1e3 / max(1, launches), 2),
             "kernel_us_per_program": round(kms * 1e3 / max(1, programs), 2),
             # host phases per program (tamd_session_host_ms): control planes, layout, fill, launch
+            "schedule": "free-running" if fr else "passes",
             "host_us_per_program": {k: round((h1[k] - h0[k]) * 1e3 / max(1, programs), 2)
-                                    for k in ("control_wall", "layout", "fill", "launch", "slot_wait")}}))
+                                    for k in h1 if k not in ("slot_reallocs", "upload_enqueue_max")}}))
         payload = summ["payload_bytes"]
         ok = ok and summ["missing_at_end"] == 0 and summ["disabled_codecs"] == 0
     times.sort()

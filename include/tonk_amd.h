@@ -62,11 +62,15 @@ int   tamd_session_finish(void* s);                   /* end-of-stream flush, th
 int   tamd_session_summary(void* s, uint64_t* out, unsigned n);
 void  tamd_session_set_timing(void* s, int on);       /* HIP events around every launch */
 double tamd_session_kernel_ms(void* s, uint64_t* launches);
-/* Host time split of the steps so far, milliseconds (summed over steps):
+/* Host time split of the steps so far, milliseconds (summed over steps).  Pass schedule:
    [0] control planes (wall, all workers)   [1] sum over workers of their own control-plane time
    [2] program layout + staging-slot wait    [3] parallel program fill + epoch close
    [4] upload + launch enqueue               [5] max over workers of their control-plane time
-   [6] of [2]: wait for the staging slot      [7] of [4]: H2D copy enqueue
+   Free-running schedule (tamd_session_schedule = 1):
+   [0] caller waiting for a program's parts [1] sum over workers of control plane + part
+   [2] opening a program (its slot's wait)   [3] stream steps run by another thread (count)
+   [4] closing (item merge, upload) + launch [5] max over workers of [1]'s share
+   Both: [6] wait for the staging slot        [7] H2D copy enqueue
    [8] longest single H2D enqueue             [9] staging-slot reallocations (count) */
 void  tamd_session_host_ms(void* s, double out[10]);
 /* Transcript of one stream in the oracle's text format (record mode). Returns bytes needed. */
@@ -82,6 +86,10 @@ void  tamd_set_clock(uint64_t (*fn)(void));
 
 /* The CPUs the session's worker threads are pinned to (count returned; empty = not pinned). */
 unsigned tamd_session_cpus(void* s, int* out, unsigned cap);
+/* The session's host schedule: 1 = free-running streams with parallel program assembly (worker
+   threads beside the caller, level pipelining), 0 = one pass over the streams per step.  It
+   decides what tamd_session_host_ms's entries hold (tonk_amd.Session.host_phases). */
+int tamd_session_schedule(void* s);
 /* Host-core plan of one GPU's worker pool (pure, no device needed): `dev_cpulists` holds every
    device's NUMA local_cpulist separated by ';', `node_cores` the usable cores of `device`'s node
    (one CPU per core).  The devices sharing that node split its cores into equal contiguous

@@ -462,8 +462,9 @@ int oracle_recovery_row(const oracle_recovery_meta* m, oracle_get_row_fn get_row
    CPU interpreter for the device program (tonk_amd/csrc/program.h).  Word layouts are
    restated here (not included) so this file stays a stand-alone checker.
    ------------------------------------------------------------------------------------------ */
-enum { I_ACC = 1, I_STORE = 2, I_FOOTER = 3, I_CLEAR = 4, I_ACC3 = 5, I_STOREC = 6, I_ACCR = 7, I_RANGE = 8 };
-enum { R_LANE3 = 1, R_CAUCHY = 2, R_CONST = 3 };
+enum { I_ACC = 1, I_STORE = 2, I_FOOTER = 3, I_CLEAR = 4, I_ACC3 = 5, I_STOREC = 6, I_ACCR = 7, I_RANGE = 8,
+       I_TARGETS = 9 };
+enum { R_LANE3 = 1, R_CAUCHY = 2, R_CONST = 3, R_MULTI = 4 };
 
 /* Each op owns three accumulators of `span` bytes (program.h):
      ACC   w0 = 1 | coef << 8 | a << 16       acc_a ^= coef * row[0:len]
@@ -475,7 +476,10 @@ enum { R_LANE3 = 1, R_CAUCHY = 2, R_CONST = 3 };
      ACCR  w0 = 7 | mode << 8 | p << 16, row0, len, count; then RANGE w0 = 8, stride, col0, cstep:
            row_k = row0 + k*stride, col_k = (col0 + k*cstep) mod 2^22, k < count
            LANE3: as ACC3 with cx = CX(col_k); CAUCHY: acc_0 ^= CauchyElement(p, col_k mod 64)*row_k;
-           CONST: acc_0 ^= p*row_k */
+           CONST: acc_0 ^= p*row_k
+           MULTI: then TARGETS w0 = 9, t_0, t_1, t_2 with t_a = kind | p << 2 | lo << 10 | hi << 21: for
+           lo <= k < hi,
+           kind CAUCHY: acc_a ^= CauchyElement(p, col_k mod 64)*row_k, kind CONST: acc_a ^= row_k */
 int oracle_run_program(uint8_t* arena, size_t arena_bytes,
                        const uint32_t* ops, unsigned n_ops,
                        const uint32_t* instrs, unsigned n_instrs)
@@ -521,6 +525,12 @@ int oracle_run_program(uint8_t* arena, size_t arena_bytes,
                 const uint32_t mode = (w[0] >> 8) & 0xff, p = (w[0] >> 16) & 0xff;
                 const uint32_t len = w[2], n = w[3], stride = r[1], col0 = r[2], cstep = r[3];
                 if (len > span) { free(acc); return -12; }
+                const uint32_t* tg = NULL;
+                if (mode == R_MULTI) {
+                    if (k + 2 >= count) { free(acc); return -15; }
+                    tg = w + 8;
+                    if ((tg[0] & 0xff) != I_TARGETS) { free(acc); return -16; }
+                }
                 for (uint32_t e = 0; e < n; ++e) {
                     const size_t base = ((size_t)w[1] + (size_t)e * stride) * 64u;
                     const unsigned col = (unsigned)(((uint64_t)col0 + (uint64_t)e * cstep) % 0x400000u);
@@ -535,11 +545,20 @@ int oracle_run_program(uint8_t* arena, size_t arena_bytes,
                         oracle_muladd_mem(acc, oracle_cauchy_element(p, col % 64u), row, len);
                     } else if (mode == R_CONST) {
                         oracle_muladd_mem(acc, (uint8_t)p, row, len);
+                    } else if (mode == R_MULTI) {
+                        for (unsigned a = 0; a < 3; ++a) {
+                            const uint32_t t = tg[1 + a], kind = t & 3, tp = (t >> 2) & 0xff;
+                            if (e < ((t >> 10) & 0x7ff) || e >= (t >> 21)) continue;
+                            uint8_t* dst = acc + (size_t)a * span;
+                            if (kind == R_CONST) oracle_add_mem(dst, row, len);
+                            else if (kind == R_CAUCHY) oracle_muladd_mem(dst, oracle_cauchy_element(tp, col % 64u), row, len);
+                            else { free(acc); return -17; }
+                        }
                     } else {
                         free(acc); return -14;
                     }
                 }
-                ++k; /* consumed the RANGE word */
+                k += mode == R_MULTI ? 2 : 1; /* consumed the RANGE (and TARGETS) word */
             } else if (kind == I_STOREC) {
                 const uint8_t c[3] = { (uint8_t)(w[0] >> 8), (uint8_t)(w[0] >> 16), (uint8_t)(w[0] >> 24) };
                 const size_t base = (size_t)w[1] * 64u;

@@ -239,16 +239,17 @@ def test_gpu_compress_batch_streams():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("max_bytes", [1300, 4000])
+@pytest.mark.parametrize("max_bytes", [1300, 4000, 24000])
 def test_gpu_compressor_edge_cases(max_bytes):
     """Tiny messages (below the kernel's 8-byte floor: sent as is), runs of one byte (matches that
-    overlap their own output, distance 1), messages of exactly max bytes, messages above the
-    kernel's 2048-byte bound (max 4000: sent as is), and enough of them to restart the 24,000-byte
-    ring many times; every one restored by the reference decompressor."""
+    overlap their own output, distance 1), messages of exactly max bytes, messages above 2048
+    bytes (compressed through global scratch instead of LDS) up to the 24,000-byte history, and
+    enough of them to restart the ring many times; every one restored by the reference
+    decompressor."""
     from tonk_amd.compress import MessageCompressor
     L = ref_lib()
     rng = np.random.default_rng(max_bytes)
-    top = min(max_bytes, 2048)  # the kernel's message bound
+    top = max_bytes
     msgs = []
     for k in range(300):
         kind = k % 6
@@ -269,8 +270,52 @@ def test_gpu_compressor_edge_cases(max_bytes):
     for m in msgs:
         blk = comp.compress(m)
         assert len(blk) < len(m) or not blk
-        if len(m) < 8 or len(m) > 2048:
+        if len(m) < 8:
             assert blk == b""
         n_comp += bool(blk)
+        if len(m) > 2048 and len(set(m)) <= 3:
+            assert blk, len(m)  # (repetitive text and one-byte runs compress at any size)
         assert dec.feed(blk, m) == m
     assert n_comp > 100
+
+
+@pytest.mark.gpu
+def test_gpu_compress_batch_large_messages():
+    """The batch API with messages of 64 B .. 24,000 B (the history size) mixed in one launch:
+    the large ones go through global scratch; every stream restored by the reference."""
+    from tonk_amd.compress import compress_batch_host
+    L = ref_lib()
+    max_bytes, n_streams, n_msgs = 24000, 4, 24
+    rng = np.random.default_rng(11)
+    text = b"".join(rng.choice([b"siamese ", b"tonk ", b"window ", b"lane "], 6000))
+    streams = []
+    for s in range(n_streams):
+        ms = []
+        for k in range(n_msgs):
+            n = int(rng.integers(64, 2049)) if k % 3 else int(rng.integers(2049, max_bytes + 1))
+            if k % 4 == 3:
+                ms.append(bytes(rng.integers(0, 256, n, dtype=np.uint8)))
+            else:
+                o = int(rng.integers(0, len(text) - n))
+                ms.append(text[o:o + n])
+        streams.append(ms)
+    stride = max(sum(map(len, s)) for s in streams) + 64
+    host = np.zeros((n_streams, stride), dtype=np.uint8)
+    lens = []
+    for s, ms in enumerate(streams):
+        blob = b"".join(ms)
+        host[s, :len(blob)] = np.frombuffer(blob, dtype=np.uint8)
+        lens += [len(m) for m in ms]
+    raw, written, _ = compress_batch_host(host.tobytes(), stride, n_streams, n_msgs, lens, max_bytes, msgs_per_job=4)
+    out_h = np.frombuffer(raw, dtype=np.uint8)
+    big = 0
+    for s, msgs in enumerate(streams):
+        dec = RefDecompressor(L, max_bytes)
+        for k, m in enumerate(msgs):
+            i = s * n_msgs + k
+            w = written[i]
+            assert w < len(m)
+            big += bool(w) and len(m) > 2048
+            blk = out_h[i * max_bytes:i * max_bytes + w].tobytes() if w else b""
+            assert dec.feed(blk, m) == m, (s, k)
+    assert big >= n_streams * n_msgs // 6

@@ -61,6 +61,8 @@ def lib() -> ctypes.CDLL:
         L.tamd_session_error.argtypes = [vp]
         L.tamd_session_destroy.restype = None
         L.tamd_session_destroy.argtypes = [vp]
+        L.tamd_session_schedule.restype = ctypes.c_int
+        L.tamd_session_schedule.argtypes = [vp]
         L.tamd_session_cpus.restype = ctypes.c_uint
         L.tamd_session_cpus.argtypes = [vp, ctypes.POINTER(ctypes.c_int), ctypes.c_uint]
         L.tamd_cpu_share.restype = ctypes.c_uint
@@ -213,10 +215,18 @@ class Session:
     HOST_PHASES = ("control_wall", "control_sum", "layout", "fill", "launch", "control_max", "slot_wait",
                    "upload_enqueue", "upload_enqueue_max", "slot_reallocs")
 
+    # the same entries under the free-running schedule (include/tonk_amd.h)
+    HOST_PHASES_FR = ("parts_wait", "control_sum", "open_wait", "stolen_steps", "close_launch", "control_max",
+                      "slot_wait", "upload_enqueue", "upload_enqueue_max", "slot_reallocs")
+
+    def free_running(self) -> bool:
+        return lib().tamd_session_schedule(self._h) == 1
+
     def host_ms(self) -> dict:
         out = (ctypes.c_double * 10)()
         lib().tamd_session_host_ms(self._h, out)
-        return dict(zip(self.HOST_PHASES, [float(v) for v in out]))
+        names = self.HOST_PHASES_FR if self.free_running() else self.HOST_PHASES
+        return dict(zip(names, [float(v) for v in out]))
 
     def cpus(self) -> list[int]:
         """CPUs the worker threads are pinned to (empty: not pinned)."""

@@ -14,8 +14,10 @@
 #include <string.h>
 #include <vector>
 
-extern "C" __global__ void tamd_lz_compress(const tamd_lz_job*, const tamd_lz_msg*, const uint8_t*, uint8_t*,
-                                            uint32_t*, unsigned long long*);
+extern "C" __global__ void tamd_lz_compress(const tamd_lz_job*, uint32_t, const tamd_lz_msg*, const uint8_t*,
+                                            uint8_t*, uint32_t*, uint8_t*, unsigned long long*);
+// (lz.hip: two jobs per 128-thread workgroup)
+static const uint32_t kLzJobsPerGroup = 2;
 extern "C" __global__ void tamd_lz_scatter_ring(const tamd_lz_scatter*, const uint8_t*);
 
 namespace tamd {
@@ -142,6 +144,8 @@ struct LzBatchState {
     uint8_t* h_out = nullptr;  // pinned: written[] | compressed blocks
     uint8_t* d_out = nullptr;
     size_t out_cap = 0;
+    uint8_t* d_scratch = nullptr;  // messages above TAMD_LZ_MAX_MESSAGE
+    size_t scratch_cap = 0;
 } g_batch;
 
 size_t align16(size_t n) { return (n + 15) & ~(size_t)15; }
@@ -174,10 +178,11 @@ void run_batch(const std::vector<LzRequest*>& b) {
     const uint8_t* fse = ok ? device_fse(dev) : nullptr;
     ok = ok && fse;
     const size_t n = b.size();
-    size_t data_bytes = 0, out_bytes = 0;
+    size_t data_bytes = 0, out_bytes = 0, scratch_bytes = 0;
     for (LzRequest* r : b) {
         data_bytes += align16(r->bytes);
         out_bytes += align16(r->c->max);
+        if (r->bytes > TAMD_LZ_MAX_MESSAGE) scratch_bytes += tamd_lz_scratch_bytes(r->bytes);
         if (ok && !r->c->ring) {
             uint8_t* ring = nullptr;
             if (hipMalloc((void**)&ring, TAMD_LZ_RING + TAMD_LZ_MIRROR) != hipSuccess) r->c->failed = true;
@@ -189,7 +194,17 @@ void run_batch(const std::vector<LzRequest*>& b) {
     const size_t o_data = o_jobs + align16(n * sizeof(tamd_lz_job));
     const size_t o_blocks = align16(n * 4);
     ok = ok && grow(S.h_in, S.d_in, S.in_cap, o_data + data_bytes) && grow(S.h_out, S.d_out, S.out_cap, o_blocks + out_bytes);
+    if (ok && scratch_bytes > S.scratch_cap) {
+        if (S.d_scratch) hipFree(S.d_scratch);
+        S.d_scratch = nullptr;
+        S.scratch_cap = scratch_bytes + scratch_bytes / 2;
+        if (hipMalloc((void**)&S.d_scratch, S.scratch_cap) != hipSuccess) {
+            S.scratch_cap = 0;
+            ok = false;
+        }
+    }
     if (ok) {
+        size_t scr = 0;
         tamd_lz_scatter* sc = (tamd_lz_scatter*)S.h_in;
         tamd_lz_msg* ms = (tamd_lz_msg*)(S.h_in + o_msgs);
         tamd_lz_job* jb = (tamd_lz_job*)(S.h_in + o_jobs);
@@ -214,6 +229,11 @@ void run_batch(const std::vector<LzRequest*>& b) {
             ms[i].win = (uint32_t)(win - base);
             ms[i].out = (uint32_t)(dout - o_blocks);
             ms[i].cap = c->max;
+            ms[i].scratch = TAMD_LZ_NO_SCRATCH;
+            if (r->bytes > TAMD_LZ_MAX_MESSAGE) {
+                ms[i].scratch = (uint32_t)scr;
+                scr += tamd_lz_scratch_bytes(r->bytes);
+            }
             memset(&jb[i], 0, sizeof(jb[i]));
             jb[i].buf = c->ring;
             jb[i].mask = TAMD_LZ_RING - 1;
@@ -226,9 +246,10 @@ void run_batch(const std::vector<LzRequest*>& b) {
         if (ok) {
             hipLaunchKernelGGL(tamd_lz_scatter_ring, dim3((uint32_t)n), dim3(256), 0, S.st,
                                (const tamd_lz_scatter*)S.d_in, (const uint8_t*)(S.d_in + o_data));
-            hipLaunchKernelGGL(tamd_lz_compress, dim3((uint32_t)n), dim3(64), 0, S.st, (const tamd_lz_job*)(S.d_in + o_jobs),
+            hipLaunchKernelGGL(tamd_lz_compress, dim3((uint32_t)((n + kLzJobsPerGroup - 1) / kLzJobsPerGroup)),
+                               dim3(64 * kLzJobsPerGroup), 0, S.st, (const tamd_lz_job*)(S.d_in + o_jobs), (uint32_t)n,
                                (const tamd_lz_msg*)(S.d_in + o_msgs), fse, S.d_out + o_blocks, (uint32_t*)S.d_out,
-                               (unsigned long long*)nullptr);
+                               S.d_scratch, (unsigned long long*)nullptr);
             ok = hipGetLastError() == hipSuccess;
         }
         ok = ok && hipMemcpyAsync(S.h_out, S.d_out, o_blocks + out_bytes, hipMemcpyDeviceToHost, S.st) == hipSuccess;
@@ -339,6 +360,7 @@ extern "C" int tamd_compress_batch(const void* dev_data, uint64_t stride, uint32
     const uint64_t total = (uint64_t)n_streams * n_msgs;
     std::vector<tamd_lz_msg> msgs(total);
     std::vector<tamd_lz_job> jobs;
+    uint64_t scratch_bytes = 0;
     for (uint32_t s = 0; s < n_streams; ++s) {
         RingTrack rt;
         rt.max = max_bytes;
@@ -355,6 +377,11 @@ extern "C" int tamd_compress_batch(const void* dev_data, uint64_t stride, uint32
             m.win = (uint32_t)win;
             m.out = 0;  // (set below: out is a 32-bit offset per stream chunk)
             m.cap = max_bytes;
+            m.scratch = TAMD_LZ_NO_SCRATCH;
+            if (n > TAMD_LZ_MAX_MESSAGE) {
+                m.scratch = (uint32_t)scratch_bytes;
+                scratch_bytes += tamd_lz_scratch_bytes(n);
+            }
         }
         for (uint32_t k = 0; k < n_msgs; k += msgs_per_job) {
             tamd_lz_job j;
@@ -366,7 +393,7 @@ extern "C" int tamd_compress_batch(const void* dev_data, uint64_t stride, uint32
             jobs.push_back(j);
         }
     }
-    if (total * max_bytes > 0xffffffffull) return -1;  // output offsets are 32-bit
+    if (total * max_bytes > 0xffffffffull || scratch_bytes > 0xffffffffull) return -1;  // 32-bit offsets
     for (uint64_t i = 0; i < total; ++i) msgs[i].out = (uint32_t)(i * max_bytes);
     // persistent launch state (grown on demand): stream, descriptor and result buffers, events
     static std::mutex mu;
@@ -376,9 +403,18 @@ extern "C" int tamd_compress_batch(const void* dev_data, uint64_t stride, uint32
     static uint32_t* d_written = nullptr;
     static size_t cap_jobs = 0, cap_msgs = 0;
     static hipEvent_t e0 = nullptr, e1 = nullptr;
+    static uint8_t* d_scratch = nullptr;
+    static size_t cap_scratch = 0;
     std::lock_guard<std::mutex> g(mu);
     bool ok = true;
-    if (!st) ok = hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess &&
+    if (scratch_bytes > cap_scratch) {
+        if (d_scratch) hipFree(d_scratch);
+        d_scratch = nullptr;
+        cap_scratch = scratch_bytes + scratch_bytes / 2;
+        ok = hipMalloc((void**)&d_scratch, cap_scratch) == hipSuccess;
+        if (!ok) cap_scratch = 0;
+    }
+    if (ok && !st) ok = hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess &&
                   hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess;
     if (ok && jobs.size() > cap_jobs) {
         if (d_jobs) hipFree(d_jobs);
@@ -406,8 +442,10 @@ extern "C" int tamd_compress_batch(const void* dev_data, uint64_t stride, uint32
     unsigned long long* d_prof = nullptr;
     if (ok && prof_on) ok = hipMalloc((void**)&d_prof, jobs.size() * 5 * 8) == hipSuccess;
     if (ok) {
-        hipExtLaunchKernelGGL(tamd_lz_compress, dim3((uint32_t)jobs.size()), dim3(64), 0, st, e0, e1, 0, d_jobs,
-                              d_msgs, fse, (uint8_t*)dev_out, d_written, d_prof);
+        const uint32_t nj = (uint32_t)jobs.size();
+        hipExtLaunchKernelGGL(tamd_lz_compress, dim3((nj + kLzJobsPerGroup - 1) / kLzJobsPerGroup),
+                              dim3(64 * kLzJobsPerGroup), 0, st, e0, e1, 0, d_jobs, nj, d_msgs, fse, (uint8_t*)dev_out,
+                              d_written, d_scratch, d_prof);
         ok = hipGetLastError() == hipSuccess;
     }
     if (ok && d_prof) {

@@ -3,6 +3,7 @@
 #include "encoder.h"
 #include "prof.h"
 
+#include <stdlib.h>
 #include <string.h>
 #include <time.h>
 
@@ -49,6 +50,7 @@ void Encoder::drop_original(StoredOriginal& o) {
 }
 
 void Encoder::pre_flush() {
+    emit_cauchy_group();
     for (unsigned l = 0; l < kLanes; ++l) lanes_[l].sums.flush(ctx_->rows, ctx_->pb, ctx_->ex);
 }
 
@@ -192,6 +194,7 @@ void Encoder::start_new_window(uint32_t column) {
     // Everything from the previous window is unreachable once Count reached zero (only the send
     // timestamps of its first elements stay visible to the RTT scan, see placeholder_msec_).
     for (uint32_t e = 0; e < kLanes; ++e) placeholder_msec_[e] = e < win_.size() ? win_[e].send_msec : placeholder_msec_[e];
+    ++window_gen_;  // (a pending Cauchy group does not extend into the new window)
     if (held_)
         for (size_t i = 0; i < win_.size(); ++i) drop_original(win_[i]);
     win_.clear();
@@ -599,20 +602,80 @@ Result Encoder::generate_cauchy(RecoveryOut& out) {
     out.data_len = used;
     out.row = ctx_->alloc(used + out.footer_len);
     if (out.row == kNoRow) { disabled_ = true; return kDisabled; }
-    ProgramBuilder& pb = ctx_->pb;
-    pb.begin_op();
-    for (const Run& r : runs) {
-        if (r.count == 1) {
-            const uint8_t c = mode == TAMD_R_CONST ? 1 : cauchy_element(crow, r.col % kCauchyMaxColumns);
-            pb.op_acc(r.row, c, r.len);
-        } else {
-            pb.op_accr(mode, mode == TAMD_R_CONST ? 1 : crow, r.off, r.stride, r.count, r.len, r.col, 1);
-        }
-    }
-    pb.finish_combine(out.row, used, out.footer, out.footer_len);
+    // The row's op is emitted with the group (at the latest by pre_flush, so within this
+    // program); its readers must already see the level it will be written at.
+    ctx_->rows.set_level(out.row, 1);
+    static const uint32_t max_group = getenv("TONK_AMD_NO_MULTI") ? 1u : 3u;
+    const uint32_t end_col = to_column(count_);
+    // A row over a long window stays a pure combine of its own (the executor shares those across
+    // a workgroup); a group is one wave's chain, and a long one would set the launch's tail.
+    const bool alone = count_ - first >= kGroupSpan;
+    if (grp_n_ && (alone || grp_n_ >= max_group || grp_gen_ != window_gen_ ||
+                   col_sub(end_col, grp_[0].first_col) >= kGroupSpan))
+        emit_cauchy_group();
+    grp_gen_ = window_gen_;
+    CauchyTarget& t = grp_[grp_n_++];
+    t.row = out.row;
+    t.used = used;
+    t.first_col = m.ColumnStart;
+    t.end_col = end_col;
+    t.kind = mode;
+    t.param = mode == TAMD_R_CONST ? 1 : crow;
+    t.flen = out.footer_len;
+    memcpy(t.footer, out.footer, sizeof(t.footer));
+    t.runs.swap(runs);
+    if (alone) emit_cauchy_group();
     stats_[2]++;
     stats_[3] += out.total();
     return kSuccess;
+}
+
+void Encoder::emit_cauchy_group() {
+    const uint32_t n = grp_n_;
+    if (!n) return;
+    grp_n_ = 0;
+    ProgramBuilder& pb = ctx_->pb;
+    pb.begin_op();
+    if (n == 1) {  // a lone row: a pure combine (the executor may share it across a workgroup)
+        const CauchyTarget& t = grp_[0];
+        for (const Run& r : t.runs) {
+            if (r.count == 1) {
+                const uint8_t c = t.kind == TAMD_R_CONST ? 1 : cauchy_element(t.param, r.col % kCauchyMaxColumns);
+                pb.op_acc(r.row, c, r.len);
+            } else {
+                pb.op_accr(t.kind, t.param, r.off, r.stride, r.count, r.len, r.col, 1);
+            }
+        }
+        pb.finish_combine(t.row, t.used, t.footer, t.flen);
+        return;
+    }
+    // The union of the windows in runs: row a's runs below the next row's first column.
+    const uint32_t base = grp_[0].first_col;
+    std::vector<Run>& u = grp_union_;
+    u.clear();
+    for (uint32_t a = 0; a < n; ++a) {
+        const uint32_t stop = a + 1 < n ? col_sub(grp_[a + 1].first_col, base) : ~0u;
+        for (const Run& r : grp_[a].runs) {
+            const uint32_t at = col_sub(r.col, base);
+            if (at >= stop) continue;
+            Run c = r;
+            if (at + c.count > stop) c.count = stop - at;
+            u.push_back(c);
+        }
+    }
+    for (const Run& r : u) {
+        const uint32_t at = col_sub(r.col, base);
+        uint32_t tw[3] = {0, 0, 0};
+        for (uint32_t a = 0; a < n; ++a) {
+            const uint32_t f = col_sub(grp_[a].first_col, base), e = col_sub(grp_[a].end_col, base);
+            const uint32_t lo = f > at ? f - at : 0u;
+            const uint32_t hi = e - at < r.count ? e - at : r.count;  // (e > at: within the union)
+            if (e > at && lo < hi) tw[a] = grp_[a].kind | grp_[a].param << 2 | lo << 10 | hi << 21;
+        }
+        if (tw[0] | tw[1] | tw[2]) pb.op_accr_multi(r.off, r.stride, r.count, r.len, r.col, 1, tw);
+    }
+    for (uint32_t a = 0; a < n; ++a) pb.op_store(grp_[a].row, grp_[a].used, a, grp_[a].footer, grp_[a].flen);
+    pb.end_op(1);
 }
 
 // Encoder::AddDenseColumns (SiameseEncoder.cpp:1046-1098)

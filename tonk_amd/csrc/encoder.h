@@ -179,6 +179,23 @@ private:
     Sym scratch_, rec_;
     struct Run { RowId row; uint32_t off, stride, count, len, col; };
     std::vector<Run> runs_;
+    // Up to three consecutive Cauchy / parity rows of one window generation are emitted together
+    // as one op (MULTI runs, program.h): each packet of their windows' union is read once.
+    // Windows only move forward (first and end columns never decrease), so the union is each
+    // row's runs up to where the next row's window starts.
+    struct CauchyTarget {
+        RowId row = kNoRow;
+        uint32_t used = 0, first_col = 0, end_col = 0, kind = 0, param = 0, flen = 0;
+        uint8_t footer[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        std::vector<Run> runs;
+    };
+    // Union of a group's windows, in packets (within the 11-bit run indices of TARGETS, and short
+    // enough that the group stays below the executor's shared-combine class).
+    static const uint32_t kGroupSpan = 32;
+    CauchyTarget grp_[3];
+    uint32_t grp_n_ = 0, grp_gen_ = 0, window_gen_ = 0;
+    std::vector<Run> grp_union_;
+    void emit_cauchy_group();
 };
 
 uint64_t time_msec();

@@ -181,6 +181,32 @@ void ProgramBuilder::op_accr(uint32_t mode, uint32_t param, uint32_t row0, uint3
     acc_bytes_ += (uint64_t)len * count;
 }
 
+void ProgramBuilder::op_accr_multi(uint32_t row0, uint32_t stride, uint32_t count, uint32_t len, uint32_t col0,
+                                   uint32_t cstep, const uint32_t t[3]) {
+    if (!len || !count) return;
+    tamd_instr a, r, g;
+    a.w0 = tamd_w0(TAMD_I_ACCR, TAMD_R_MULTI, 0);
+    a.row = row0;
+    a.len = len;
+    a.cap = count;
+    r.w0 = TAMD_I_RANGE;
+    r.row = stride;
+    r.len = col0;
+    r.cap = cstep;
+    g.w0 = TAMD_I_TARGETS;
+    g.row = t[0];
+    g.len = t[1];
+    g.cap = t[2];
+    instrs_.push_back(a);
+    instrs_.push_back(r);
+    instrs_.push_back(g);
+    ++cur_runs_;
+    cur_pure_ = false;
+    if (len > cur_span_) cur_span_ = len;
+    if (len < cur_full_) cur_full_ = len;
+    acc_bytes_ += (uint64_t)len * count;
+}
+
 uint32_t ProgramBuilder::finish_combine(RowId dst, uint32_t len, const uint8_t* footer, uint32_t footer_len) {
     const uint32_t cap = rows_->cap_bytes(dst);
     push_store(instrs_, rows_->offset(dst), len, cap, footer, footer_len);
@@ -272,14 +298,15 @@ void ProgramBuilder::op_acc_part(RowId src, uint32_t units, uint8_t coef, uint32
     acc_bytes_ += len;
 }
 
-void ProgramBuilder::op_store(RowId dst, uint32_t len, uint32_t acc) {
+void ProgramBuilder::op_store(RowId dst, uint32_t len, uint32_t acc, const uint8_t* footer, uint32_t footer_len) {
     cur_pure_ = false;  // (pure combines end with finish_combine / combine only)
     const uint32_t cap = rows_->cap_bytes(dst);
-    push_store(instrs_, rows_->offset(dst), len, cap, nullptr, 0, acc);
+    push_store(instrs_, rows_->offset(dst), len, cap, footer, footer_len, acc);
     if (cap > cur_span_) cur_span_ = cap;
+    if (len > cur_span_) cur_span_ = len;
     if (len < cur_full_) cur_full_ = len;
     written_.push_back(dst);
-    store_bytes_ += len;
+    store_bytes_ += len + footer_len;
 }
 
 uint32_t ProgramBuilder::end_op(uint32_t min_level) {

@@ -137,9 +137,12 @@ public:
     // A strided run of level-0 rows (program.h ACCR); row0/stride in 64-B units.
     void op_accr(uint32_t mode, uint32_t param, uint32_t row0, uint32_t stride, uint32_t count, uint32_t len,
                  uint32_t col0, uint32_t cstep);
+    // MULTI run: targets t[a] = kind | p << 8 | hi << 16 accumulate into acc_a (program.h).
+    void op_accr_multi(uint32_t row0, uint32_t stride, uint32_t count, uint32_t len, uint32_t col0, uint32_t cstep,
+                       const uint32_t t[3]);
     // STORE (+FOOTER) of acc_0 into dst and close the op (the tail of combine()).
     uint32_t finish_combine(RowId dst, uint32_t len, const uint8_t* footer, uint32_t footer_len);
-    void op_store(RowId dst, uint32_t len, uint32_t acc = 0);
+    void op_store(RowId dst, uint32_t len, uint32_t acc = 0, const uint8_t* footer = nullptr, uint32_t footer_len = 0);
     void op_storec(RowId dst, uint32_t len, const uint8_t* c);  // c0*acc_0 ^ c1*acc_1 ^ c2*acc_2
     // The same into a part of row `dst` (`units` 64-B units from its start, `cap` bytes); the
     // row is recorded as written once (`first`: the first part the op stores).

@@ -227,7 +227,7 @@ __device__ __forceinline__ void lv_store_row(uint8_t* __restrict__ arena, uint32
 // wave combines only the batches with unit mod nw == wid (the coefficient stepping still walks
 // every row).
 template <bool FULL, int NH, uint32_t TAMD_RBATCH>
-__device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& r, uint32_t o,
+__device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& r, const tamd_instr& tg, uint32_t o,
                                          const uint8_t* __restrict__ arena, const uint32_t* __restrict__ lds,
                                          uint32_t& unit, uint32_t nw, uint32_t wid, LV<NH>& a0, LV<NH>& a1,
                                          LV<NH>& a2) {
@@ -298,6 +298,52 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
                 }
             }
         }
+    } else if (mode == TAMD_R_MULTI) {
+        // Up to three Cauchy / parity rows over overlapping windows: row i of the run goes to
+        // every target a with lo_a <= i < hi_a, loaded once (the op is never shared: nw == 1).
+        uint32_t col = vgpr(col0);
+        const uint32_t cs = vgpr(cstep);
+        const uint8_t* inv = (const uint8_t*)(lds + TAMD_LDS_INV);
+        const uint32_t w0 = tg.row, w1 = tg.len, w2 = tg.cap;
+        // target a takes rows lo_a <= i < hi_a: (i - lo_a) < n_a, unsigned
+        const uint32_t l0 = (w0 >> 10) & 0x7ffu, l1 = (w1 >> 10) & 0x7ffu, l2 = (w2 >> 10) & 0x7ffu;
+        const uint32_t h0 = (w0 >> 21) - l0, h1 = (w1 >> 21) - l1, h2 = (w2 >> 21) - l2;
+        const uint32_t x0 = ((w0 >> 2) & 0xffu) + 64u, x1 = ((w1 >> 2) & 0xffu) + 64u, x2 = ((w2 >> 2) & 0xffu) + 64u;
+        const bool k0 = (w0 & 3u) == TAMD_R_CONST, k1 = (w1 & 3u) == TAMD_R_CONST, k2 = (w2 & 3u) == TAMD_R_CONST;
+        constexpr uint32_t H = TAMD_RBATCH / 2;
+        LV<NH> d[TAMD_RBATCH];
+#pragma unroll
+        for (uint32_t q = 0; q < TAMD_RBATCH; ++q) d[q] = lv_load<NH>(src + (size_t)min(q, count - 1u) * step);
+#define TAMD_MULTI_TARGET(l, h, k, x, acc)                                                 \
+    if (i - l < h) {                                                                       \
+        if (k) acc ^= v;                                                                   \
+        else acc ^= lv_mul<NH>(v, perm_at(lds, inv[(col & 63u) ^ x] * 8u));                \
+    }
+        for (uint32_t e = 0; e < count; e += TAMD_RBATCH) {
+            const bool more = e + TAMD_RBATCH < count;
+#pragma unroll
+            for (uint32_t h = 0; h < 2; ++h) {
+#pragma unroll
+                for (uint32_t q = h * H; q < h * H + H; ++q) {
+                    const uint32_t i = e + q;
+                    if (i < count) {
+                        const LV<NH> v = lv_keep<FULL, NH>(d[q], o, len);
+                        TAMD_MULTI_TARGET(l0, h0, k0, x0, a0)
+                        TAMD_MULTI_TARGET(l1, h1, k1, x1, a1)
+                        TAMD_MULTI_TARGET(l2, h2, k2, x2, a2)
+                    }
+                    col += cs;
+                }
+                if (more) {
+#pragma unroll
+                    for (uint32_t q = h * H; q < h * H + H; ++q)
+                        d[q] = lv_load<NH>(src + (size_t)min(e + TAMD_RBATCH + q, count - 1u) * step);
+                }
+            }
+        }
+#undef TAMD_MULTI_TARGET
+        unit += (count + TAMD_RBATCH - 1) / TAMD_RBATCH;
+        return;
     } else if (mode == TAMD_R_CAUCHY) {
         // CauchyElement(p, col mod 64) = inv((col mod 64) ^ (p + 64)) (SiameseCommon.h:212-218)
         uint32_t col = vgpr(col0);
@@ -386,8 +432,9 @@ __device__ __forceinline__ LV<NH> run_item(const tamd_instr* __restrict__ instrs
         for (uint32_t j = TAMD_BATCH; j-- > 0;)
             if ((in[j].w0 & 0xffu) == TAMD_I_ACCR && j < nb) nb = j;
         if (nb == 0) {
-            run_accr<FULL, NH, TAMD_BATCH>(in[0], in[1], o, arena, lds, unit, nw, wid, a0, a1, a2);  // in[1]: RANGE word
-            k += 2;
+            // in[1]: the RANGE word, in[2]: TARGETS (MULTI runs)
+            run_accr<FULL, NH, TAMD_BATCH>(in[0], in[1], in[2], o, arena, lds, unit, nw, wid, a0, a1, a2);
+            k += ((in[0].w0 >> 8) & 0xffu) == TAMD_R_MULTI ? 3u : 2u;
             continue;
         }
         if ((unit++ & (nw - 1u)) != wid) {  // another wave's batch (shared ops only)

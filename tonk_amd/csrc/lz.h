@@ -5,7 +5,9 @@
 #pragma once
 #include <stdint.h>
 
-#define TAMD_LZ_MAX_MESSAGE 2048u  // larger messages are stored uncompressed (written = 0)
+#define TAMD_LZ_MAX_MESSAGE 2048u  // messages up to this size are compressed entirely in LDS
+#define TAMD_LZ_MAX_BLOCK 131071u  // larger ones (up to zstd's block limit, 128 KB) use global scratch
+#define TAMD_LZ_NO_SCRATCH 0xffffffffu
 #define TAMD_LZ_WINDOW 32768u      // history bytes inserted into a job's hash table
 #define TAMD_LZ_RING 65536u        // per-compressor device ring of the stream's bytes (the drop-in)
 #define TAMD_LZ_MIRROR 64u         // the ring's first bytes repeated after it (wide loads at its end)
@@ -24,10 +26,30 @@ typedef struct tamd_lz_job {
 } tamd_lz_job;
 
 // One message: linear position and length, the start of the bytes the decompressor holds when it
-// decodes it (previous history segment start), and its output slot.
+// decodes it (previous history segment start), its output slot, and for a message above
+// TAMD_LZ_MAX_MESSAGE the byte offset of its scratch area (tamd_lz_scratch_bytes, 16-byte
+// aligned; TAMD_LZ_NO_SCRATCH: none, the message is stored uncompressed).
 typedef struct tamd_lz_msg {
-    uint32_t pos, len, win, out, cap, pad[3];
+    uint32_t pos, len, win, out, cap, scratch, pad[2];
 } tamd_lz_msg;
+
+// Sequences of a message of n bytes: at most n / 4 (every match is at least 4 bytes).
+static inline
+#ifdef __HIPCC__
+__host__ __device__
+#endif
+uint32_t tamd_lz_big_seqs(uint32_t n) { return n / 4u + 1u; }
+// Scratch of a message above TAMD_LZ_MAX_MESSAGE (lz.hip lz_message<true>): sequences, offsets,
+// literal starts, codes (4 x S words), the bit stream ((n + 64) / 4 + 4 words) and three chains
+// of state updates (3 x S halfwords).
+static inline
+#ifdef __HIPCC__
+__host__ __device__
+#endif
+uint32_t tamd_lz_scratch_bytes(uint32_t n) {
+    const uint32_t S = tamd_lz_big_seqs(n);
+    return (16u * S + 4u * ((n + 64u) / 4u + 4u) + 6u * S + 15u) & ~15u;
+}
 
 // FSE tables of the predefined distributions, one blob:
 //   *_ENC[symbol][next_state] = the state of `symbol` whose bit range holds next_state

@@ -21,11 +21,18 @@
 
 #include "lz.h"
 
+#include <type_traits>
+
 #define LZ_HASH_LOG 12
 #define LZ_HASH (1u << LZ_HASH_LOG)
 #define LZ_MIN_MATCH 4u
 #define LZ_PROBE 16u  // bytes a lane compares per candidate; a chosen match is extended by the wave
 #define LZ_MAX_SEQS (TAMD_LZ_MAX_MESSAGE / LZ_MIN_MATCH)
+// Candidates are found and parsed LZ_CH positions at a time; after the parse the same words
+// hold the sequences' codes (LZ_MAX_SEQS words) and the three state-update chains (3 x
+// LZ_MAX_SEQS halfwords).
+#define LZ_CH (LZ_MAX_SEQS + 3u * LZ_MAX_SEQS / 2u)
+#define LZ_WAVES 2  // jobs per workgroup: the waves share the FSE maps (2 workgroups per CU)
 
 // Byte loads of a stream: `buf` at linear position p & mask.  Multi-byte loads are unaligned
 // global loads; the buffers carry readable slack past their end (a linear stream: 8 bytes past its
@@ -43,40 +50,355 @@ static __device__ __forceinline__ uint64_t lz_dword(const uint8_t* __restrict__ 
 
 static __device__ __forceinline__ uint32_t lz_hash(uint32_t w) { return (w * 2654435761u) >> (32 - LZ_HASH_LOG); }
 
-extern "C" __global__ void __launch_bounds__(64)
-tamd_lz_compress(const tamd_lz_job* __restrict__ jobs, const tamd_lz_msg* __restrict__ msgs,
-                 const uint8_t* __restrict__ fse, uint8_t* __restrict__ out, uint32_t* __restrict__ written,
-                 unsigned long long* __restrict__ prof) {
-    __shared__ uint32_t htab[LZ_HASH];                       // (position + 1), 0 = empty
-    // per message byte: the match found there, length | distance << 16 (length 0: none)
-    __shared__ __attribute__((aligned(16))) uint32_t mword[TAMD_LZ_MAX_MESSAGE];
-    __shared__ uint32_t seq_lo[LZ_MAX_SEQS];                 // literal length | match length << 16
-    __shared__ uint32_t seq_off[LZ_MAX_SEQS];                // offset
-    __shared__ uint32_t bitw[(TAMD_LZ_MAX_MESSAGE + 64) / 4];  // backward FSE bit stream
-    uint8_t* const bits = (uint8_t*)bitw;
-    __shared__ uint32_t sh_init[3];
-    __shared__ __attribute__((aligned(16))) uint8_t mbuf[TAMD_LZ_MAX_MESSAGE + LZ_PROBE + 16];  // the message
-    __shared__ uint16_t seq_pos[LZ_MAX_SEQS];                // where each sequence's literals start
-    __shared__ uint16_t e16[TAMD_FSE_E16_WORDS];             // FSE encode maps with decode info (lz.h)
-    __shared__ uint32_t sh_bytes, sh_ok;
+// The waves of a workgroup run unrelated jobs: they synchronise only with themselves (LDS and
+// scratch writes complete before any lane reads them).
+#define LZ_SYNC()                                                \
+    do {                                                         \
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");   \
+        __builtin_amdgcn_wave_barrier();                         \
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");   \
+    } while (0)
 
-    const uint32_t lane = threadIdx.x;
-    const tamd_lz_job job = jobs[blockIdx.x];
-    // profiling only (TONK_AMD_LZ_PROF): per job, 100 MHz ticks spent in each phase
-    unsigned long long ph[5] = {0, 0, 0, 0, 0}, t_ph = prof ? __builtin_amdgcn_s_memrealtime() : 0;
+// One wave's LDS.
+struct LzWave {
+    uint32_t htab[LZ_HASH];                                   // (position + 1), 0 = empty
+    uint32_t mword[LZ_CH];  // per chunk position: the match there, length | distance << 16
+    uint32_t seq_lo[LZ_MAX_SEQS];                             // literal length | match length << 16
+    uint32_t seq_off[LZ_MAX_SEQS];                            // offset
+    uint32_t bitw[(TAMD_LZ_MAX_MESSAGE + 64) / 4];            // backward FSE bit stream
+    __attribute__((aligned(16))) uint8_t mbuf[TAMD_LZ_MAX_MESSAGE + LZ_PROBE + 16];  // the message
+    uint16_t seq_pos[LZ_MAX_SEQS];                            // where each sequence's literals start
+    uint32_t sh_init[3], sh_bytes, sh_ok;
+};
+
+
+// One message.  BIG: the message is read from the stream buffer and its per-sequence arrays live
+// in global scratch; otherwise all of it is in the wave's LDS.
+template <bool BIG>
+static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __restrict__ e16, const tamd_lz_msg m,
+                                                  const uint8_t* __restrict__ buf, uint32_t mask,
+                                                  uint8_t* __restrict__ scratch, uint8_t* __restrict__ out,
+                                                  uint32_t* __restrict__ written, uint32_t mi, uint32_t lane,
+                                                  unsigned long long* ph, unsigned long long& t_ph, bool prof) {
 #define LZ_PHASE(k)                                                          \
     if (prof) {                                                              \
         const unsigned long long t_now = __builtin_amdgcn_s_memrealtime();   \
         ph[k] += t_now - t_ph;                                               \
         t_ph = t_now;                                                        \
     }
+    const uint32_t n = m.len;
+    const uint32_t S = BIG ? tamd_lz_big_seqs(n) : LZ_MAX_SEQS;
+    uint32_t *seq_lo, *seq_off, *code, *bitw;
+    uint16_t* upd;
+    typedef typename std::conditional<BIG, uint32_t, uint16_t>::type pos_t;
+    pos_t* seq_pos;
+    uint32_t bw_cap;  // bit-stream words
+    if constexpr (BIG) {
+        uint32_t* w = (uint32_t*)(scratch + m.scratch);
+        seq_lo = w;
+        seq_off = w + S;
+        seq_pos = w + 2 * S;
+        code = w + 3 * S;
+        bitw = w + 4 * S;
+        bw_cap = (n + 64u) / 4u;
+        upd = (uint16_t*)(bitw + bw_cap + 4u);
+    } else {
+        seq_lo = L.seq_lo;
+        seq_off = L.seq_off;
+        seq_pos = L.seq_pos;
+        code = L.mword;                        // (free after the parse)
+        upd = (uint16_t*)(L.mword + LZ_MAX_SEQS);
+        bitw = L.bitw;
+        bw_cap = (TAMD_LZ_MAX_MESSAGE + 64u) / 4u;
+    }
+    const uint8_t* mb = L.mbuf;
+    // the message's bytes at offset i (LDS copy, or the stream buffer for BIG messages)
+    auto msg_word = [&](uint32_t i) -> uint32_t {
+        if constexpr (BIG) return lz_word(buf, mask, m.pos + i);
+        else return *(const lz_u32u*)(mb + i);
+    };
+    auto msg_dword = [&](uint32_t i) -> uint64_t {
+        if constexpr (BIG) return lz_dword(buf, mask, m.pos + i);
+        else return *(const lz_u64u*)(mb + i);
+    };
+    auto msg_byte = [&](uint32_t i) -> uint8_t {
+        if constexpr (BIG) return buf[(m.pos + i) & mask];
+        else return mb[i];
+    };
+    if constexpr (!BIG) {
+        // the message into LDS (16 bytes per lane per step; the slack past it is readable)
+        for (uint32_t k = 16u * lane; k < n; k += 1024) {
+            const uint64_t a = lz_dword(buf, mask, m.pos + k), b = lz_dword(buf, mask, m.pos + k + 8);
+            *(uint64_t*)(L.mbuf + k) = a;
+            *(uint64_t*)(L.mbuf + k + 8) = b;
+        }
+        LZ_SYNC();
+    }
+    // Chunks of LZ_CH positions: (1)+(2) candidates and match lengths, 64 positions at a time (a
+    // group's positions are inserted after it is scanned: matches reach back to earlier groups),
+    // then (3) the greedy parse of the chunk: from p, the first position with a match starts the
+    // next sequence.  The wave holds the match words of 64 positions from `wb` in registers; the
+    // window moves only when p leaves it.  Sequences collect in registers (lane j keeps sequence
+    // j of each group of 64) and are stored a group at a time.
+    uint32_t p = 0, lit_start = 0, nseq = 0, lits = 0;
+    uint32_t my_lo = 0, my_off = 0, my_pos = 0;
+    for (uint32_t c0 = 0; c0 < n; c0 += LZ_CH) {
+        const uint32_t cend = n - c0 < LZ_CH ? n : c0 + LZ_CH;
+        for (uint32_t c = c0; c < cend; c += 64) {
+            const uint32_t i = c + lane;
+            uint32_t len = 0, src = 0;
+            if (i + LZ_MIN_MATCH <= n) {
+                const uint32_t pp = m.pos + i;
+                const uint32_t e = L.htab[lz_hash(msg_word(i))];
+                if (e) {
+                    src = e - 1;
+                    if (src >= m.win && src < pp) {
+                        const uint32_t lim = n - i < LZ_PROBE ? n - i : LZ_PROBE;
+                        // the probe's loads all go out together
+                        uint64_t xs[LZ_PROBE / 8];
+#pragma unroll
+                        for (uint32_t k = 0; k < LZ_PROBE / 8; ++k)  // (no load past the message)
+                            xs[k] = 8 * k < lim ? lz_dword(buf, mask, src + 8 * k) ^ msg_dword(i + 8 * k) : 0ull;
+                        len = LZ_PROBE;
+#pragma unroll
+                        for (uint32_t k = LZ_PROBE / 8; k-- > 0;)
+                            if (xs[k]) len = 8 * k + ((uint32_t)__builtin_ctzll(xs[k]) >> 3);
+                        if (len > lim) len = lim;
+                        if (len < LZ_MIN_MATCH) len = 0;
+                    }
+                }
+            }
+            if (i < cend) L.mword[i - c0] = len ? len | ((m.pos + i - src) << 16) : 0u;
+            LZ_SYNC();
+            if (i + 3 < n && i < cend) atomicMax(&L.htab[lz_hash(msg_word(i))], m.pos + i + 1);
+            LZ_SYNC();
+        }
+        LZ_PHASE(1)
+        if (p < cend) {
+            uint32_t wb = p > c0 ? p : c0;  // (positions in [p, c0) were scanned with the last chunk)
+            uint32_t mine = wb + lane < cend ? L.mword[wb + lane - c0] : 0u;
+            for (;;) {
+                const uint64_t b = __ballot((mine & 0xffffu) != 0 && wb + lane >= p);
+                if (!b) {
+                    wb = __builtin_amdgcn_readfirstlane(wb + 64);
+                    if (wb >= cend) break;
+                    if (p < wb) p = wb;
+                    mine = wb + lane < cend ? L.mword[wb + lane - c0] : 0u;
+                    continue;
+                }
+                const uint32_t first = (uint32_t)__builtin_ctzll(b);
+                const uint32_t at = __builtin_amdgcn_readfirstlane(wb + first);
+                const uint32_t word = (uint32_t)__builtin_amdgcn_readlane((int)mine, (int)first);
+                const uint32_t dist = word >> 16;
+                uint32_t ml = word & 0xffffu;
+                if (ml == LZ_PROBE && at + ml < n) {
+                    // the probe matched in full: the wave extends the match 512 bytes per step
+                    const uint32_t q = m.pos + at;
+                    for (;;) {
+                        const uint32_t k = ml + 8u * lane;
+                        uint64_t x = 0;
+                        if (k < n - at) x = lz_dword(buf, mask, q - dist + k) ^ lz_dword(buf, mask, q + k);
+                        const uint64_t bad = __ballot(k >= n - at || x != 0);
+                        if (!bad) {
+                            ml += 512;
+                            continue;
+                        }
+                        const uint32_t fb = (uint32_t)__builtin_ctzll(bad);
+                        const uint64_t xf = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, (int)fb) |
+                                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(x >> 32), (int)fb) << 32);
+                        const uint32_t kf = ml + 8u * fb;
+                        ml = kf < n - at ? kf + ((uint32_t)__builtin_ctzll(xf) >> 3) : n - at;
+                        break;
+                    }
+                    if (ml > n - at) ml = n - at;
+                    ml = __builtin_amdgcn_readfirstlane(ml);
+                }
+                if (lane == (nseq & 63u)) {
+                    my_lo = (at - lit_start) | (ml << 16);
+                    my_off = dist;
+                    my_pos = lit_start;
+                }
+                lits += at - lit_start;
+                ++nseq;
+                if ((nseq & 63u) == 0) {
+                    seq_lo[nseq - 64 + lane] = my_lo;
+                    seq_off[nseq - 64 + lane] = my_off;
+                    seq_pos[nseq - 64 + lane] = (pos_t)my_pos;
+                }
+                p = __builtin_amdgcn_readfirstlane(at + ml);
+                lit_start = p;
+                if (p >= cend) break;
+                if (p >= wb + 64) {
+                    wb = p;
+                    mine = wb + lane < cend ? L.mword[wb + lane - c0] : 0u;
+                }
+            }
+        }
+        LZ_SYNC();  // (the next chunk rewrites mword)
+        LZ_PHASE(2)
+    }
+    if ((nseq & 63u) != 0 && lane < (nseq & 63u)) {
+        const uint32_t g = nseq & ~63u;
+        seq_lo[g + lane] = my_lo;
+        seq_off[g + lane] = my_off;
+        seq_pos[g + lane] = (pos_t)my_pos;
+    }
+    const uint32_t last_lits = n - lit_start;  // literals after the last sequence
+    lits += last_lits;
+    LZ_SYNC();
+
+    // (4) the sequence bit stream, as tamd_fse_sequences (lz.h) writes it, built in parallel:
+    // codes per sequence (all lanes), the three FSE state chains (lanes 0-2, one chain each,
+    // from the last sequence back), then every sequence's bit fields placed at their offsets
+    // (a prefix sum of the field widths in stream order: the last sequence first).
+    uint32_t lh = 0, shb = 0;
+    const uint32_t lits_word = tamd_lits_header_word(lits, &lh);
+    const uint32_t seq_word = tamd_seq_header_word(nseq, &shb);
+    const uint32_t limit = n - 1u < m.cap ? n - 1u : m.cap;  // smaller than the message, fits
+    const uint32_t head = lh + lits + shb;
+    bool ok = head < limit && nseq > 0;
+    uint32_t total = 0;
+    if (ok) {
+        for (uint32_t sq = lane; sq < nseq; sq += 64)
+            code[sq] = tamd_ll_code(seq_lo[sq] & 0xffffu) | (tamd_ml_code(seq_lo[sq] >> 16) << 8) |
+                       ((31u - (uint32_t)__builtin_clz(seq_off[sq] + 3u)) << 16);
+        LZ_SYNC();
+        if (lane < 3) {
+            const uint32_t shift = 8u * lane, size = lane == 2 ? 32u : 64u;
+            const uint16_t* enc = e16 + (lane == 0 ? TAMD_FSE_LL_E16 : lane == 1 ? TAMD_FSE_ML_E16 : TAMD_FSE_OF_E16);
+            uint16_t* u_out = upd + S * lane;
+            uint32_t st = enc[((code[nseq - 1] >> shift) & 0xffu) * size] & 63u;
+            for (uint32_t sq = nseq - 1; sq-- > 0;) {
+                const uint32_t e = enc[((code[sq] >> shift) & 0xffu) * size + st];
+                u_out[sq] = (uint16_t)((e >> 10) | (((e >> 6) & 15u) << 8));
+                st = e & 63u;
+            }
+            L.sh_init[lane] = st;
+        }
+        // zero the bit buffer words the stream can use
+        const uint32_t cap_words = (limit - head + 3u) / 4u + 1u;
+        const uint32_t wcap = cap_words < bw_cap ? cap_words : bw_cap;
+        for (uint32_t k = lane; k < wcap; k += 64) bitw[k] = 0;
+        LZ_SYNC();
+        uint32_t carry = 0;
+        for (uint32_t base = 0; base < nseq; base += 64) {
+            const uint32_t r = base + lane;  // stream order: sequence nseq - 1 - r
+            uint64_t v = 0;
+            uint32_t nbits = 0;
+            if (r < nseq) {
+                const uint32_t sq = nseq - 1u - r;
+                const uint32_t cd = code[sq], llc = cd & 0xffu, mlc = (cd >> 8) & 0xffu, ofc = cd >> 16;
+                auto put = [&](uint32_t val, uint32_t nb) {
+                    v |= (uint64_t)(val & ((1u << nb) - 1u)) << nbits;
+                    nbits += nb;
+                };
+                if (sq != nseq - 1u) {
+                    const uint32_t o = upd[2u * S + sq], ml_u = upd[S + sq], l_u = upd[sq];
+                    put(o & 0xffu, o >> 8);
+                    put(ml_u & 0xffu, ml_u >> 8);
+                    put(l_u & 0xffu, l_u >> 8);
+                }
+                put((seq_lo[sq] & 0xffffu) - tamd_ll_base(llc), tamd_ll_bits(llc));
+                put((seq_lo[sq] >> 16) - tamd_ml_base(mlc), tamd_ml_bits(mlc));
+                put(seq_off[sq] + 3u, ofc);
+            }
+            uint32_t x = nbits;
+#pragma unroll
+            for (uint32_t d = 1; d < 64; d <<= 1) {
+                const uint32_t y = __shfl_up(x, d);
+                if (lane >= d) x += y;
+            }
+            const uint32_t at = carry + x - nbits;
+            if (nbits && (at + nbits + 31u) / 32u < wcap) {
+                const uint32_t w0 = at / 32u, sh = at % 32u;
+                atomicOr(&bitw[w0], (uint32_t)(v << sh));
+                if (sh + nbits > 32u) atomicOr(&bitw[w0 + 1], (uint32_t)(v >> (32u - sh)));
+                if (sh + nbits > 64u) atomicOr(&bitw[w0 + 2], (uint32_t)(v >> (64u - sh)));
+            }
+            carry += __shfl(x, 63);
+        }
+        LZ_SYNC();
+        // the initial states (ML, OF, LL: the decoder reads LL first) and the end mark
+        const uint64_t tail = (uint64_t)L.sh_init[1] | ((uint64_t)L.sh_init[2] << 6) | ((uint64_t)L.sh_init[0] << 11) |
+                              (1ull << 17);
+        const uint32_t bits_total = carry + 18u;
+        total = head + (bits_total + 7u) / 8u;
+        ok = total <= limit;
+        if (ok && lane == 0) {
+            const uint32_t w0 = carry / 32u, sh = carry % 32u;
+            bitw[w0] |= (uint32_t)(tail << sh);
+            if (sh + 18u > 32u) bitw[w0 + 1] |= (uint32_t)(tail >> (32u - sh));
+        }
+    }
+    if (lane == 0) {
+        L.sh_bytes = ok ? total : 0;
+        L.sh_ok = ok;
+        written[mi] = ok ? total : 0;
+    }
+    LZ_SYNC();
+    LZ_PHASE(3)
+    // (5) the block: literals section header, literals, sequences header, bit stream
+    if (L.sh_ok) {
+        uint8_t* o = out + m.out;
+        uint32_t w = lh;
+        if (lane < w) o[lane] = (uint8_t)(lits_word >> (8u * lane));
+        // literals: lane j copies the literal run of sequences j, j + 64, ... (and the final run)
+        // to its place, found by a wave prefix sum of the run lengths
+        uint32_t carry = 0;
+        for (uint32_t base = 0; base <= nseq; base += 64) {
+            const uint32_t sq = base + lane;
+            uint32_t ll = 0, from = 0;
+            if (sq < nseq) {
+                ll = seq_lo[sq] & 0xffffu;
+                from = seq_pos[sq];
+            } else if (sq == nseq) {
+                ll = last_lits;
+                from = n - last_lits;
+            }
+            uint32_t x = ll;
+#pragma unroll
+            for (uint32_t d = 1; d < 64; d <<= 1) {
+                const uint32_t y = __shfl_up(x, d);
+                if (lane >= d) x += y;
+            }
+            const uint32_t at = w + carry + x - ll;
+            for (uint32_t k = 0; k < ll; ++k) o[at + k] = msg_byte(from + k);
+            carry += __shfl(x, 63);
+        }
+        w += lits;
+        const uint32_t hs = shb;
+        if (lane < hs) o[w + lane] = (uint8_t)(seq_word >> (8u * lane));
+        w += hs;
+        const uint32_t nb = L.sh_bytes - w;
+        const uint8_t* bits = (const uint8_t*)bitw;
+        for (uint32_t k = lane; k < nb; k += 64) o[w + k] = bits[k];
+    }
+    LZ_SYNC();
+    LZ_PHASE(4)
+#undef LZ_PHASE
+}
+
+extern "C" __global__ void __launch_bounds__(64 * LZ_WAVES)
+tamd_lz_compress(const tamd_lz_job* __restrict__ jobs, uint32_t n_jobs, const tamd_lz_msg* __restrict__ msgs,
+                 const uint8_t* __restrict__ fse, uint8_t* __restrict__ out, uint32_t* __restrict__ written,
+                 uint8_t* __restrict__ scratch, unsigned long long* __restrict__ prof) {
+    __shared__ LzWave W[LZ_WAVES];
+    __shared__ uint16_t e16[TAMD_FSE_E16_WORDS];  // FSE encode maps with decode info (lz.h)
+    for (uint32_t i = threadIdx.x; i < TAMD_FSE_E16_WORDS / 2; i += blockDim.x)
+        ((uint32_t*)e16)[i] = ((const uint32_t*)(fse + TAMD_FSE_E16))[i];
+    __syncthreads();  // (the only workgroup barrier: from here on the waves are independent)
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t ji = blockIdx.x * LZ_WAVES + wave;
+    if (ji >= n_jobs) return;
+    LzWave& L = W[wave];
+    const tamd_lz_job job = jobs[ji];
+    // profiling only (TONK_AMD_LZ_PROF): per job, 100 MHz ticks spent in each phase
+    unsigned long long ph[5] = {0, 0, 0, 0, 0}, t_ph = prof ? __builtin_amdgcn_s_memrealtime() : 0;
     const uint8_t* __restrict__ buf = job.buf;
     const uint32_t mask = job.mask;
-
-    for (uint32_t i = lane; i < TAMD_FSE_E16_WORDS / 2; i += 64)
-        ((uint32_t*)e16)[i] = ((const uint32_t*)(fse + TAMD_FSE_E16))[i];
-    for (uint32_t i = lane; i < LZ_HASH; i += 64) htab[i] = 0;
-    __syncthreads();
+    for (uint32_t i = lane; i < LZ_HASH; i += 64) L.htab[i] = 0;
+    LZ_SYNC();
 
     // The job's window: the positions before its first message, last TAMD_LZ_WINDOW bytes of it.
     {
@@ -96,275 +418,38 @@ tamd_lz_compress(const tamd_lz_job* __restrict__ jobs, const tamd_lz_msg* __rest
                     else if (k < 8) w = (uint32_t)(a >> (8 * k)) | (k > 4 ? (uint32_t)(b << (64 - 8 * k)) : 0u);
                     else if (k == 8) w = (uint32_t)b;
                     else w = (uint32_t)(b >> (8 * (k - 8))) | (k > 12 ? c << (32 - 8 * (k - 12)) : 0u);
-                    if (p0 + k < m0.pos) atomicMax(&htab[lz_hash(w)], p0 + k + 1);
+                    if (p0 + k < m0.pos) atomicMax(&L.htab[lz_hash(w)], p0 + k + 1);
                 }
             }
         }
-        __syncthreads();
+        LZ_SYNC();
     }
-    LZ_PHASE(0)
+    if (prof) {
+        const unsigned long long t_now = __builtin_amdgcn_s_memrealtime();
+        ph[0] += t_now - t_ph;
+        t_ph = t_now;
+    }
 
     for (uint32_t mi = job.first; mi < job.first + job.count; ++mi) {
         const tamd_lz_msg m = msgs[mi];
         const uint32_t n = m.len;
-        if (n > TAMD_LZ_MAX_MESSAGE || n < 8) {  // (outside the kernel's bounds: stored uncompressed)
+        const bool big = n > TAMD_LZ_MAX_MESSAGE;
+        if (n < 8 || n > TAMD_LZ_MAX_BLOCK || (big && m.scratch == TAMD_LZ_NO_SCRATCH)) {
+            // (outside the kernel's bounds: stored uncompressed; its positions still enter the table)
             if (lane == 0) written[mi] = 0;
             for (uint32_t q = m.pos; q + 3 < m.pos + n; q += 64) {
-                const uint32_t p = q + lane;
-                if (p + 3 < m.pos + n) atomicMax(&htab[lz_hash(lz_word(buf, mask, p))], p + 1);
+                const uint32_t pp = q + lane;
+                if (pp + 3 < m.pos + n) atomicMax(&L.htab[lz_hash(lz_word(buf, mask, pp))], pp + 1);
             }
-            __syncthreads();
+            LZ_SYNC();
             continue;
         }
-        // the message into LDS (16 bytes per lane per step; the slack past it is readable)
-        for (uint32_t k = 16u * lane; k < n; k += 1024) {
-            const uint64_t a = lz_dword(buf, mask, m.pos + k), b = lz_dword(buf, mask, m.pos + k + 8);
-            *(uint64_t*)(mbuf + k) = a;
-            *(uint64_t*)(mbuf + k + 8) = b;
-        }
-        __syncthreads();
-        // (1)+(2) candidates and match lengths, 64 positions at a time; a chunk's positions are
-        // inserted after the chunk is scanned (matches reach back to the previous chunks)
-        for (uint32_t c = 0; c < n; c += 64) {
-            const uint32_t i = c + lane;
-            uint32_t len = 0, src = 0;
-            if (i + LZ_MIN_MATCH <= n) {
-                const uint32_t p = m.pos + i;
-                const uint32_t e = htab[lz_hash(*(const lz_u32u*)(mbuf + i))];
-                if (e) {
-                    src = e - 1;
-                    if (src >= m.win && src < p) {
-                        const uint32_t lim = n - i < LZ_PROBE ? n - i : LZ_PROBE;
-                        // the probe's loads all go out together; the message side is in LDS
-                        uint64_t xs[LZ_PROBE / 8];
-#pragma unroll
-                        for (uint32_t k = 0; k < LZ_PROBE / 8; ++k)  // (no load past the message)
-                            xs[k] = 8 * k < lim ? lz_dword(buf, mask, src + 8 * k) ^ *(const lz_u64u*)(mbuf + i + 8 * k)
-                                                : 0ull;
-                        len = LZ_PROBE;
-#pragma unroll
-                        for (uint32_t k = LZ_PROBE / 8; k-- > 0;)
-                            if (xs[k]) len = 8 * k + ((uint32_t)__builtin_ctzll(xs[k]) >> 3);
-                        if (len > lim) len = lim;
-                        if (len < LZ_MIN_MATCH) len = 0;
-                    }
-                }
-            }
-            if (i < n) mword[i] = len ? len | ((m.pos + i - src) << 16) : 0u;
-            __syncthreads();
-            if (i + 3 < n) atomicMax(&htab[lz_hash(*(const lz_u32u*)(mbuf + i))], m.pos + i + 1);
-            __syncthreads();
-        }
-        LZ_PHASE(1)
-        // (3) greedy parse: from p, the first position with a match starts the next sequence
-        // The wave holds the match words of 64 positions from `wb` in registers; the next sequence
-        // starts at the first of them at or after p; the window moves only when p leaves it.
-        // Sequences collect in registers (lane j keeps sequence j of each group of 64) and reach
-        // LDS a group at a time, so no iteration waits on an LDS write.
-        uint32_t p = 0, lit_start = 0, nseq = 0, lits = 0, wb = 0;
-        uint32_t mine = lane < n ? mword[lane] : 0u;
-        uint32_t my_lo = 0, my_off = 0, my_pos = 0;
-        for (;;) {
-            const uint64_t b = __ballot((mine & 0xffffu) != 0 && wb + lane >= p);
-            if (!b) {
-                wb = __builtin_amdgcn_readfirstlane(wb + 64);
-                if (wb >= n) break;
-                if (p < wb) p = wb;
-                mine = wb + lane < n ? mword[wb + lane] : 0u;
-                continue;
-            }
-            const uint32_t first = (uint32_t)__builtin_ctzll(b);
-            const uint32_t at = __builtin_amdgcn_readfirstlane(wb + first);
-            const uint32_t word = (uint32_t)__builtin_amdgcn_readlane((int)mine, (int)first);
-            const uint32_t dist = word >> 16;
-            uint32_t ml = word & 0xffffu;
-            if (ml == LZ_PROBE && at + ml < n) {
-                // the probe matched in full: the wave extends the match 512 bytes per step
-                const uint32_t q = m.pos + at;
-                for (;;) {
-                    const uint32_t k = ml + 8u * lane;
-                    uint64_t x = 0;
-                    if (k < n - at) x = lz_dword(buf, mask, q - dist + k) ^ lz_dword(buf, mask, q + k);
-                    const uint64_t bad = __ballot(k >= n - at || x != 0);
-                    if (!bad) {
-                        ml += 512;
-                        continue;
-                    }
-                    const uint32_t fb = (uint32_t)__builtin_ctzll(bad);
-                    const uint64_t xf = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)x, (int)fb) |
-                                        ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(x >> 32), (int)fb) << 32);
-                    const uint32_t kf = ml + 8u * fb;
-                    ml = kf < n - at ? kf + ((uint32_t)__builtin_ctzll(xf) >> 3) : n - at;
-                    break;
-                }
-                if (ml > n - at) ml = n - at;
-                ml = __builtin_amdgcn_readfirstlane(ml);
-            }
-            if (lane == (nseq & 63u)) {
-                my_lo = (at - lit_start) | (ml << 16);
-                my_off = dist;
-                my_pos = lit_start;
-            }
-            lits += at - lit_start;
-            ++nseq;
-            if ((nseq & 63u) == 0) {
-                seq_lo[nseq - 64 + lane] = my_lo;
-                seq_off[nseq - 64 + lane] = my_off;
-                seq_pos[nseq - 64 + lane] = (uint16_t)my_pos;
-            }
-            p = __builtin_amdgcn_readfirstlane(at + ml);
-            lit_start = p;
-            if (p >= n) break;
-            if (p >= wb + 64) {
-                wb = p;
-                mine = wb + lane < n ? mword[wb + lane] : 0u;
-            }
-        }
-        if ((nseq & 63u) != 0 && lane < (nseq & 63u)) {
-            const uint32_t g = nseq & ~63u;
-            seq_lo[g + lane] = my_lo;
-            seq_off[g + lane] = my_off;
-            seq_pos[g + lane] = (uint16_t)my_pos;
-        }
-        const uint32_t last_lits = n - lit_start;  // literals after the last sequence
-        lits += last_lits;
-        __syncthreads();
-
-        LZ_PHASE(2)
-        // (4) the sequence bit stream, as tamd_fse_sequences (lz.h) writes it, built in parallel:
-        // codes per sequence (all lanes), the three FSE state chains (lanes 0-2, one chain each,
-        // from the last sequence back), then every sequence's bit fields placed at their offsets
-        // (a prefix sum of the field widths in stream order: the last sequence first).
-        uint32_t lh = 0, shb = 0;
-        const uint32_t lits_word = tamd_lits_header_word(lits, &lh);
-        const uint32_t seq_word = tamd_seq_header_word(nseq, &shb);
-        const uint32_t limit = n - 1u < m.cap ? n - 1u : m.cap;  // smaller than the message, fits
-        const uint32_t head = lh + lits + shb;
-        bool ok = head < limit && nseq > 0;
-        uint32_t total = 0;
-        if (ok) {
-            uint32_t* code = mword;                      // (free after the parse) llc | mlc << 8 | ofc << 16
-            uint16_t* upd = (uint16_t*)(mword + 512);    // state transition bits per chain: value | nb << 8
-            for (uint32_t sq = lane; sq < nseq; sq += 64)
-                code[sq] = tamd_ll_code(seq_lo[sq] & 0xffffu) | (tamd_ml_code(seq_lo[sq] >> 16) << 8) |
-                           ((31u - (uint32_t)__builtin_clz(seq_off[sq] + 3u)) << 16);
-            __syncthreads();
-            if (lane < 3) {
-                const uint32_t shift = 8u * lane, size = lane == 2 ? 32u : 64u;
-                const uint16_t* enc = e16 + (lane == 0 ? TAMD_FSE_LL_E16 : lane == 1 ? TAMD_FSE_ML_E16 : TAMD_FSE_OF_E16);
-                uint16_t* u_out = upd + 512u * lane;
-                uint32_t st = enc[((code[nseq - 1] >> shift) & 0xffu) * size] & 63u;
-                for (uint32_t sq = nseq - 1; sq-- > 0;) {
-                    const uint32_t e = enc[((code[sq] >> shift) & 0xffu) * size + st];
-                    u_out[sq] = (uint16_t)((e >> 10) | (((e >> 6) & 15u) << 8));
-                    st = e & 63u;
-                }
-                sh_init[lane] = st;
-            }
-            // zero the bit buffer words the stream can use
-            const uint32_t cap_words = (limit - head + 3u) / 4u + 1u;
-            for (uint32_t k = lane; k < cap_words && k < (TAMD_LZ_MAX_MESSAGE + 64u) / 4u; k += 64) bitw[k] = 0;
-            __syncthreads();
-            uint32_t carry = 0;
-            for (uint32_t base = 0; base < nseq; base += 64) {
-                const uint32_t r = base + lane;  // stream order: sequence nseq - 1 - r
-                uint64_t v = 0;
-                uint32_t nbits = 0;
-                if (r < nseq) {
-                    const uint32_t sq = nseq - 1u - r;
-                    const uint32_t cd = code[sq], llc = cd & 0xffu, mlc = (cd >> 8) & 0xffu, ofc = cd >> 16;
-                    auto put = [&](uint32_t val, uint32_t nb) {
-                        v |= (uint64_t)(val & ((1u << nb) - 1u)) << nbits;
-                        nbits += nb;
-                    };
-                    if (sq != nseq - 1u) {
-                        const uint32_t o = upd[1024u + sq], ml_u = upd[512u + sq], l_u = upd[sq];
-                        put(o & 0xffu, o >> 8);
-                        put(ml_u & 0xffu, ml_u >> 8);
-                        put(l_u & 0xffu, l_u >> 8);
-                    }
-                    put((seq_lo[sq] & 0xffffu) - tamd_ll_base(llc), tamd_ll_bits(llc));
-                    put((seq_lo[sq] >> 16) - tamd_ml_base(mlc), tamd_ml_bits(mlc));
-                    put(seq_off[sq] + 3u, ofc);
-                }
-                uint32_t x = nbits;
-#pragma unroll
-                for (uint32_t d = 1; d < 64; d <<= 1) {
-                    const uint32_t y = __shfl_up(x, d);
-                    if (lane >= d) x += y;
-                }
-                const uint32_t at = carry + x - nbits;
-                const uint32_t wcap = cap_words < (TAMD_LZ_MAX_MESSAGE + 64u) / 4u ? cap_words
-                                                                                   : (TAMD_LZ_MAX_MESSAGE + 64u) / 4u;
-                if (nbits && (at + nbits + 31u) / 32u < wcap) {
-                    const uint32_t w0 = at / 32u, sh = at % 32u;
-                    atomicOr(&bitw[w0], (uint32_t)(v << sh));
-                    if (sh + nbits > 32u) atomicOr(&bitw[w0 + 1], (uint32_t)(v >> (32u - sh)));
-                    if (sh + nbits > 64u) atomicOr(&bitw[w0 + 2], (uint32_t)(v >> (64u - sh)));
-                }
-                carry += __shfl(x, 63);
-            }
-            __syncthreads();
-            // the initial states (ML, OF, LL: the decoder reads LL first) and the end mark
-            const uint64_t tail = (uint64_t)sh_init[1] | ((uint64_t)sh_init[2] << 6) | ((uint64_t)sh_init[0] << 11) |
-                                  (1ull << 17);
-            const uint32_t bits_total = carry + 18u;
-            total = head + (bits_total + 7u) / 8u;
-            ok = total <= limit;
-            if (ok && lane == 0) {
-                const uint32_t w0 = carry / 32u, sh = carry % 32u;
-                bitw[w0] |= (uint32_t)(tail << sh);
-                if (sh + 18u > 32u) bitw[w0 + 1] |= (uint32_t)(tail >> (32u - sh));
-            }
-        }
-        if (lane == 0) {
-            sh_bytes = ok ? total : 0;
-            sh_ok = ok;
-            written[mi] = ok ? total : 0;
-        }
-        __syncthreads();
-        LZ_PHASE(3)
-        // (5) the block: literals section header, literals, sequences header, bit stream
-        if (sh_ok) {
-            uint8_t* o = out + m.out;
-            uint32_t w = lh;
-            if (lane < w) o[lane] = (uint8_t)(lits_word >> (8u * lane));
-            // literals: lane j copies the literal run of sequences j, j + 64, ... (and the final run)
-            // from LDS to its place, found by a wave prefix sum of the run lengths
-            uint32_t carry = 0;
-            for (uint32_t base = 0; base <= nseq; base += 64) {
-                const uint32_t sq = base + lane;
-                uint32_t ll = 0, from = 0;
-                if (sq < nseq) {
-                    ll = seq_lo[sq] & 0xffffu;
-                    from = seq_pos[sq];
-                } else if (sq == nseq) {
-                    ll = last_lits;
-                    from = n - last_lits;
-                }
-                uint32_t x = ll;
-#pragma unroll
-                for (uint32_t d = 1; d < 64; d <<= 1) {
-                    const uint32_t y = __shfl_up(x, d);
-                    if (lane >= d) x += y;
-                }
-                const uint32_t at = w + carry + x - ll;
-                for (uint32_t k = 0; k < ll; ++k) o[at + k] = mbuf[from + k];
-                carry += __shfl(x, 63);
-            }
-            w += lits;
-            const uint32_t hs = shb;
-            if (lane < hs) o[w + lane] = (uint8_t)(seq_word >> (8u * lane));
-            w += hs;
-            const uint32_t nb = sh_bytes - w;
-            for (uint32_t k = lane; k < nb; k += 64) o[w + k] = bits[k];
-        }
-        __syncthreads();
-        LZ_PHASE(4)
+        if (big) lz_message<true>(L, e16, m, buf, mask, scratch, out, written, mi, lane, ph, t_ph, prof != nullptr);
+        else lz_message<false>(L, e16, m, buf, mask, scratch, out, written, mi, lane, ph, t_ph, prof != nullptr);
     }
     if (prof && lane == 0)
 #pragma unroll
-        for (uint32_t k = 0; k < 5; ++k) prof[5 * blockIdx.x + k] = ph[k];
+        for (uint32_t k = 0; k < 5; ++k) prof[5 * ji + k] = ph[k];
 }
 
 // The per-message drop-in's staging (compress.cpp): each message of a combined batch is copied

@@ -18,6 +18,11 @@
 //         LANE3:  acc_0 ^= row_k, acc_1 ^= cx*row_k, acc_2 ^= cx^2*row_k, cx = 3 + (199*col_k mod 253)
 //         CAUCHY: acc_0 ^= inv((col_k mod 64) ^ (p + 64)) * row_k
 //         CONST:  acc_0 ^= p * row_k
+//         MULTI:  + TARGETS (t_0, t_1, t_2), t_a = kind | p << 2 | lo << 10 | hi << 21 (kind 0:
+//                 unused): for lo <= k < hi: CAUCHY: acc_a ^= inv((col_k mod 64) ^ (p + 64)) * row_k,
+//                                            CONST:  acc_a ^= row_k
+//                 (up to three Cauchy / parity rows over overlapping windows: each row of the
+//                 run is read once for all of them)
 //         (runs of equally long packets stored at a fixed stride: the window's originals, whose
 //         rows sit in a contiguous ring in HBM, become one instruction per run)
 //
@@ -45,12 +50,14 @@ enum tamd_instr_kind {
     TAMD_I_STOREC = 6,  // w0 = kind | c0 << 8 | c1 << 16 | c2 << 24
     TAMD_I_ACCR   = 7,  // w0 = kind | mode << 8 | p << 16; row = row0, len, cap = count
     TAMD_I_RANGE  = 8,  // payload word after ACCR: row = stride (units), len = col0, cap = cstep
+    TAMD_I_TARGETS = 9, // payload word after the RANGE of a MULTI ACCR: row, len, cap = t_0, t_1, t_2
 };
 
 enum tamd_range_mode {
     TAMD_R_LANE3  = 1,
     TAMD_R_CAUCHY = 2,
     TAMD_R_CONST  = 3,
+    TAMD_R_MULTI  = 4,
 };
 
 // Ops of a level are grouped into classes: class 0 holds the long pure combines (ACC into acc_0,

@@ -1143,9 +1143,16 @@ void* tamd_session_create(const tamd_session_params* p, char* err, size_t err_le
     // The free-running schedule (worker threads, pipelined levels): programs assembled in
     // parallel (Device::add_part) in 8 slots -- up to fr_ahead open, the rest in flight; otherwise
     // one laid-out program per step in 6 slots (TONK_AMD_PASSES=1 keeps the pass schedule).
-    s->fr_mode = pipe && nthreads > 1 && getenv("TONK_AMD_NO_DEFER") == nullptr && getenv("TONK_AMD_PASSES") == nullptr;
+    // TONK_AMD_FR_SINGLE=1 runs it for one-thread sessions too (one worker beside the caller:
+    // the worker's control plane of step k + 1 overlaps the caller's assembly and launch of
+    // program k).  Off by default: on the decoder-stress stream the worker's control plane ran
+    // 25-40 % slower than the caller's own (configs[4]: 2.8 vs 3.6 GiB/s at 512 originals per
+    // program, 3.6 vs 4.2 at 1024), which costs more than the overlap gains.
+    static const bool fr_single = getenv("TONK_AMD_FR_SINGLE") != nullptr;
+    s->fr_mode = pipe && (nthreads > 1 || fr_single) && getenv("TONK_AMD_NO_DEFER") == nullptr &&
+                 getenv("TONK_AMD_PASSES") == nullptr;
     if (const char* a = getenv("TONK_AMD_RUNAHEAD")) s->fr_ahead = (uint32_t)atoi(a) > 0 ? (uint32_t)atoi(a) : 1u;
-    if (s->fr_mode) s->dev.set_assembly_slots(8, 24);
+    if (s->fr_mode) s->dev.set_assembly_slots(8, p->n_streams <= 4 ? 8 : 24);
     else {
         // (TONK_AMD_SLOTS: A/B knob for the slot count of the pass schedule)
         const size_t slots = getenv("TONK_AMD_SLOTS") ? (size_t)atoi(getenv("TONK_AMD_SLOTS")) : (pipe ? 6 : 2);
@@ -1161,7 +1168,7 @@ void* tamd_session_create(const tamd_session_params* p, char* err, size_t err_le
     s->fill_ms.assign(nthreads, 0.0);
     s->deferred = pipe && getenv("TONK_AMD_NO_DEFER") == nullptr;
     Session* raw = s.get();
-    if (nthreads > 1) {
+    if (nthreads > 1 || s->fr_mode) {
         raw->cpus = idle_cpus(device_local_cpus((int)p->device), nthreads);
         raw->threads_wanted = nthreads;
         for (uint32_t t = 0; t < nthreads; ++t) raw->threads.emplace_back([raw, t] { raw->pool_loop(t); });
@@ -1381,6 +1388,8 @@ const char* tamd_session_error(void* sp) {
 }
 
 void tamd_set_clock(uint64_t (*fn)(void)) { set_clock_source(fn); }
+
+int tamd_session_schedule(void* sp) { return ((Session*)sp)->fr_mode ? 1 : 0; }
 
 unsigned tamd_session_cpus(void* sp, int* out, unsigned cap) {
     Session* s = (Session*)sp;

@@ -8,7 +8,8 @@ for f in sorted(glob.glob(f"gpurun_out/{tag}_*_[0-9]*.json")):
     j = json.load(open(f))
     h = j.get("host_ms_per_program") or j["host_ms_per_step"]
     rows.setdefault(m.group(1), []).append(
-        (j["value"], j["ms_per_step"], h["control_wall"], h["control_sum"], h["control_max"], h["fill"],
+        (j["value"], j["ms_per_step"], h.get("control_wall", h.get("parts_wait")), h["control_sum"], h["control_max"],
+              h.get("fill", h.get("stolen_steps")),
          j["roofline"]["avg_launch_us"]))
 for v, rs in rows.items():
     for r in rs:
