@@ -614,7 +614,7 @@ def main() -> int:
         if world > 1:
             print("bench.py: single-stream workloads run on one GPU (replicas only)", file=sys.stderr)
             return 2
-        step = a.step or (512 if a.workload == "cfg4" else ORIGINALS_PER_STEP)
+        step = a.step or ORIGINALS_PER_STEP
         print(json.dumps(single_stream(a.workload, local_rank, step)), flush=True)
         return 0
 

@@ -5,10 +5,9 @@ built from the reference sources with the Siamese codec replaced by libtonk_amd.
 the drop-in check of SURVEY.md s8(f)1.
 
 unit_tests_amd_lz additionally replaces PacketCompression.cpp with the GPU MessageCompressor
-(integration/tonk/PacketCompressionAmd.cpp).  Its TestCompression passes, but a
-synchronous GPU round trip per datagram is too slow for the bandwidth tests' time limits (a Tonk
-server compresses every reliable datagram), so it runs only on request:
-TONK_AMD_TONK_BINARY=unit_tests_amd_lz.  The compressor's parity is tests/test_compress.py."""
+(integration/tonk/PacketCompressionAmd.cpp): every reliable datagram Tonk sends is
+compressed on the GPU, concurrent connections' calls combined into one launch (compress.cpp).
+Both binaries run in the default -m gpu pass.  The compressor's parity is tests/test_compress.py."""
 from __future__ import annotations
 
 import os
@@ -18,23 +17,27 @@ import pytest
 
 from conftest import ROOT
 
-EXE = os.path.join(ROOT, "oracle", "_ref", "tonk", os.environ.get("TONK_AMD_TONK_BINARY", "unit_tests_amd"))
+BINARIES = ["unit_tests_amd", "unit_tests_amd_lz"]
+if os.environ.get("TONK_AMD_TONK_BINARY"):
+    BINARIES = [os.environ["TONK_AMD_TONK_BINARY"]]
 
 
 @pytest.mark.gpu
 @pytest.mark.timeout(840)
-def test_tonk_unit_tests_with_mi355x_codec():
-    if not os.path.exists(EXE):
-        pytest.skip("oracle/_ref/tonk/unit_tests_amd not built (needs /root/reference at build time)")
+@pytest.mark.parametrize("binary", BINARIES)
+def test_tonk_unit_tests_with_mi355x_codec(binary):
+    exe = os.path.join(ROOT, "oracle", "_ref", "tonk", binary)
+    if not os.path.exists(exe):
+        pytest.skip(f"oracle/_ref/tonk/{binary} not built (needs /root/reference at build time)")
     # the C ABI watchdog prints call/wait counts to stderr every 5 s (Tonk's own log is buffered)
     # The log streams to gpurun_out/ while the test runs (a run that writes nothing for minutes
     # looks hung to the GPU-box harness).
     env = dict(os.environ, TONK_AMD_CAPI_WATCH="5")
     out_dir = os.path.join(ROOT, "gpurun_out")
     os.makedirs(out_dir, exist_ok=True)
-    path = os.path.join(out_dir, "tonk_unit_tests.log")
+    path = os.path.join(out_dir, f"tonk_{binary}.log")
     with open(path, "w") as f:
-        r = subprocess.run([EXE], stdin=subprocess.DEVNULL, stdout=f, stderr=subprocess.STDOUT, timeout=800, env=env)
+        r = subprocess.run([exe], stdin=subprocess.DEVNULL, stdout=f, stderr=subprocess.STDOUT, timeout=800, env=env)
     with open(path) as f:
         log = f.read()
     assert r.returncode == 0, log[-3000:]

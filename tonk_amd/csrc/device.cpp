@@ -353,7 +353,7 @@ int Device::open_program() {
 
 bool Device::add_part(int h, const ProgramBuilder& pb, Part& out) {
     Slot& slot = slots_[h];
-    const std::vector<tamd_instr>& ins = pb.instrs();
+    const InstrVec& ins = pb.instrs();
     const std::vector<tamd_op>& ops = pb.ops();
     const std::vector<uint32_t>& lv = pb.op_levels();
     const std::vector<uint32_t>& li = pb.level_items();

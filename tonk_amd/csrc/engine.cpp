@@ -122,7 +122,7 @@ void RowTable::release_up_to(uint64_t completed) {
 // ---------------------------------------------------------------------------------------------
 // ProgramBuilder
 // ---------------------------------------------------------------------------------------------
-static void push_store(std::vector<tamd_instr>& v, uint32_t off, uint32_t len, uint32_t cap,
+static void push_store(InstrVec& v, uint32_t off, uint32_t len, uint32_t cap,
                        const uint8_t* footer, uint32_t flen, uint32_t acc = 0);
 void ProgramBuilder::clear() {
     ops_.clear();
@@ -234,7 +234,7 @@ void ProgramBuilder::op_acc(RowId src, uint8_t coef, uint32_t len, uint32_t acc)
     acc_bytes_ += len;
 }
 
-static void push_store(std::vector<tamd_instr>& v, uint32_t off, uint32_t len, uint32_t cap,
+static void push_store(InstrVec& v, uint32_t off, uint32_t len, uint32_t cap,
                        const uint8_t* footer, uint32_t flen, uint32_t acc) {
     tamd_instr s;
     s.w0 = tamd_w0(TAMD_I_STORE, flen, acc);

@@ -30,6 +30,8 @@
 #include <stdint.h>
 #include <vector>
 #include <algorithm>
+#include <memory>
+#include <utility>
 
 namespace tamd {
 
@@ -42,8 +44,24 @@ struct Term {
     uint8_t coef;
 };
 
+// Allocator whose value-initialisation leaves PODs uninitialised: growing a term list or an
+// instruction list by resize() and then writing every new element skips a zero fill.
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+    template <class U>
+    struct rebind { typedef NoInitAlloc<U> other; };
+    NoInitAlloc() = default;
+    template <class U>
+    NoInitAlloc(const NoInitAlloc<U>&) noexcept {}
+    template <class U>
+    void construct(U* p) noexcept { ::new ((void*)p) U; }
+    template <class U, class... A>
+    void construct(U* p, A&&... a) { ::new ((void*)p) U(std::forward<A>(a)...); }
+};
+
 // A symbolic buffer.  `terms` may contain duplicates; they are merged when materialized.
-typedef std::vector<Term> Sym;
+typedef std::vector<Term, NoInitAlloc<Term>> Sym;
+typedef std::vector<tamd_instr, NoInitAlloc<tamd_instr>> InstrVec;
 
 // Bytes of an op one device work item covers (program.h TAMD_SLICE_BYTES, tamd_exec16).
 inline uint32_t slice_bytes() { return TAMD_SLICE_BYTES; }
@@ -168,7 +186,7 @@ public:
     uint32_t max_level() const { return max_level_; }
 
     const std::vector<tamd_op>& ops() const { return ops_; }
-    const std::vector<tamd_instr>& instrs() const { return instrs_; }
+    const InstrVec& instrs() const { return instrs_; }
     // Per op: its bucket, TAMD_COST_CLASSES * level + cost class (0 = most expensive).
     const std::vector<uint32_t>& op_levels() const { return levels_; }
     const std::vector<RowId>& written_rows() const { return written_; }
@@ -182,7 +200,7 @@ public:
 private:
     RowTable* rows_;
     std::vector<tamd_op> ops_;
-    std::vector<tamd_instr> instrs_;
+    InstrVec instrs_;
     std::vector<uint32_t> levels_;
     std::vector<RowId> written_;
     std::vector<uint32_t> level_ops_, level_items_;
