@@ -193,6 +193,7 @@ def verify_schedule(threads: int, device: int) -> dict:
                             arena_bytes=2 * wp.n * n_streams * 1344 + (4 << 30), record=True)
     try:
         sess.generate()
+        fr = sess.free_running()
         done = 0
         while done < wp.n:
             sess.step(min(ORIGINALS_PER_STEP, wp.n - done))
@@ -208,7 +209,9 @@ def verify_schedule(threads: int, device: int) -> dict:
         sess.close()
     return {"digests_match": not bad, "streams_differing": bad, "streams": n_streams, "originals_per_stream": wp.n,
             "seconds": round(time.perf_counter() - t0, 2),
-            "schedule": f"{threads} host threads, deferred fill, early launch, release at completion"}
+            "schedule": (f"{threads} host threads, free-running streams, parallel program assembly, "
+                         "pipelined levels, release at completion" if fr else
+                         f"{threads} host threads, one pass per step")}
 
 
 def end_to_end(threads: int, device: int, loss: float, steps: int = 3, warmup: int = 1) -> dict | None:

@@ -18,4 +18,5 @@ timeout -k 10 300 python bench.py --workload cfg4 > "$OUT/bench_cfg4_$TAG.json" 
 timeout -k 10 300 python bench.py --workload compress > "$OUT/bench_compress_$TAG.json" 2> "$OUT/bench_compress_$TAG.err" &&
 cd /tmp && export TMPDIR=/tmp &&
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$TAG" -o run -- python3 "$R/bench.py" --no-cpu-baseline --no-end-to-end --no-verify --no-pmc > "$OUT/bench_prof_$TAG.json" 2> "$OUT/bench_prof_$TAG.err" &&
-python3 "$R/tools/trace_region.py" "$OUT/prof_$TAG/run_kernel_trace.csv" > "$OUT/trace_region_$TAG.json"
+python3 "$R/tools/trace_region.py" "$OUT/prof_$TAG/run_kernel_trace.csv" > "$OUT/trace_region_$TAG.json" &&
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_lz_$TAG" -o run -- python3 "$R/bench.py" --workload compress --no-cpu-baseline > "$OUT/bench_compress_prof_$TAG.json" 2> "$OUT/bench_compress_prof_$TAG.err"
