@@ -4,12 +4,15 @@
 #include "prof.h"
 
 #include <algorithm>
+#include <stdlib.h>
 #include <string.h>
 
 namespace tamd {
 
 // Term lists up to this length go to the device unmerged (see eliminate_original_data).
 static const size_t kMergeAbove = 48;
+// Unknowns from which back substitution combines materialized eliminated rows (back_substitution).
+static const uint32_t kBackSubRows = 2;
 
 static inline uint32_t popcount64(uint64_t x) { return (uint32_t)__builtin_popcountll(x); }
 
@@ -1154,6 +1157,23 @@ Result Decoder::back_substitution() {
     std::vector<uint32_t>& gpos = tri_gstart_;
     std::vector<uint32_t> gend(L, 0);
     tri_acc_.resize((size_t)L * D);
+    // Every recovered value is a combination of up to L eliminated rows.  From kBackSubRows
+    // unknowns on, each eliminated row with more than one term is first materialized (one op
+    // reading its terms once) and the values combine those rows: Sum|buf| + L^2 row reads on
+    // the device and term copies on the host, instead of up to L * Sum|buf| of both.
+    static const uint32_t mat_from = getenv("TONK_AMD_BACKSUB_ROWS") ? (uint32_t)atoi(getenv("TONK_AMD_BACKSUB_ROWS"))
+                                                                      : kBackSubRows;
+    if (L >= mat_from) {
+        for (uint32_t k = 0; k < L; ++k) {
+            Recovery* r = mrows_[pivots_[k]].rec;
+            if (r->buf.size() <= 1) continue;
+            const RowId row = ctx_->alloc_temp(r->bytes);
+            if (row == kNoRow) { disabled_ = true; return kDisabled; }
+            ctx_->pb.combine(row, r->buf.data(), r->buf.size(), r->bytes);
+            r->buf.clear();
+            r->buf.push_back(Term{row, r->bytes, 1});
+        }
+    }
     bool iterate = false;
     for (int ci = (int)L - 1; ci >= 0; --ci) {
         const uint32_t ri = pivots_[ci];

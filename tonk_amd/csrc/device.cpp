@@ -146,8 +146,8 @@ bool Device::init(int device, uint64_t arena_bytes) {
     HIPCHK(hipMemsetAsync(arena_, 0, arena_bytes_, s));
     if (!gf_init()) { error_ = "gf self test failed"; return false; }
     // kernels.hip TAMD_GF_DWORDS: perm tables, inv[256], sqr[256], then the lane table: for
-    // i = 0..252 (column value cx = 3 + i) the perm dwords of cx and of cx^2
-    std::vector<uint8_t> tables(sizeof(g_gf.perm) + 512 + 253 * 12 * 4);
+    // i = 0..252 (column value cx = 3 + i) the perm dwords of cx and of cx^2, then the Cauchy table
+    std::vector<uint8_t> tables(sizeof(g_gf.perm) + 512 + 253 * 12 * 4 + 192 * 32);
     memcpy(tables.data(), g_gf.perm, sizeof(g_gf.perm));
     memcpy(tables.data() + sizeof(g_gf.perm), g_gf.inv, 256);
     memcpy(tables.data() + sizeof(g_gf.perm) + 256, g_gf.sqr, 256);
@@ -157,6 +157,9 @@ bool Device::init(int device, uint64_t arena_bytes) {
         memcpy(dst, g_gf.perm[cx], 24);
         memcpy(dst + 24, g_gf.perm[gf_sqr(cx)], 24);
     }
+    // then the Cauchy table: for x = 64..255 the perm tables of inv(x), 32 bytes each
+    for (unsigned x = 64; x < 256; ++x)
+        memcpy(tables.data() + sizeof(g_gf.perm) + 512 + 253 * 48 + (x - 64) * 32, g_gf.perm[gf_inv((uint8_t)x)], 32);
     HIPCHK(hipMalloc((void**)&d_zero_, 4096));  // the executor's dummy-load target (kernels.hip)
     HIPCHK(hipMemsetAsync(d_zero_, 0, 4096, s));
     HIPCHK(hipMalloc((void**)&d_gf_, tables.size()));
@@ -809,18 +812,23 @@ uint64_t Device::start_program(Inflight& cur, size_t n_instr, size_t n_ops, size
         HIPCHK(hipMemcpyAsync(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
         hipFree(stamps);
-        FILE* f = fopen("tonk_amd_stamps.bin", "wb");
-        if (f) {
-            fwrite(h.data(), 8, h.size(), f);
-            fclose(f);
-        }
-        f = fopen("tonk_amd_program.bin", "wb");
-        if (f) {
-            fwrite(slot.host, 1, bytes, f);
-            fclose(f);
-        }
-        fprintf(stderr, "stamps: n_instr %zu n_ops %zu n_items %zu (instr/op/item offsets %u/%u/%u)\n", n_instr, n_ops,
-                n_items, cur.instrs - slot.dev_off, cur.ops - slot.dev_off, cur.items - slot.dev_off);
+        // items (op record, slice), the table item.x indexes (op records) and the one op.first
+        // indexes (instructions); with parallel assembly both are the slot's record area
+        const size_t io = cur.instrs - slot.dev_off, oo = cur.ops - slot.dev_off, it = cur.items - slot.dev_off;
+        const bool merged = io == oo;
+        const size_t rec_bytes = merged ? bytes - n_items * 8 : 0;
+        auto dump = [](const char* name, const void* p, size_t n) {
+            FILE* f = fopen(name, "wb");
+            if (f) {
+                fwrite(p, 1, n, f);
+                fclose(f);
+            }
+        };
+        dump("tonk_amd_stamps.bin", h.data(), h.size() * 8);
+        dump("tonk_amd_items.bin", slot.host + it, n_items * 8);
+        dump("tonk_amd_ops.bin", slot.host + oo, merged ? rec_bytes : n_ops * 16);
+        dump("tonk_amd_instrs.bin", slot.host + io, merged ? rec_bytes : n_instr * 16);
+        fprintf(stderr, "stamps: n_instr %zu n_ops %zu n_items %zu\n", n_instr, n_ops, n_items);
         for (uint32_t k = 0; k <= cur.levels; ++k) fprintf(stderr, "stamps level %u item_base %u\n", k, cur.item_base[k]);
     }
     stats_.programs++;

@@ -85,9 +85,12 @@ __device__ __forceinline__ void store_slice(uint8_t* __restrict__ arena, uint32_
 //   [2048, 2112)     inv[256] as bytes
 //   [2112, 2176)     sqr[256] as bytes
 //   [2176, +253*12)  lane table: for i = 0..252 (cx = 3 + i) the 6 perm dwords of cx, then of cx^2
+//   [5212, +192*8)   Cauchy table: for x = 64..255 the perm tables of inv(x) (CauchyElement(p, c)
+//                    = inv(c ^ (p + 64)) in one lookup instead of two dependent ones)
 #define TAMD_LDS_INV 2048
 #define TAMD_LDS_LANE 2176
-#define TAMD_GF_DWORDS (TAMD_LDS_LANE + 253 * 12)  // 5212, a multiple of 4
+#define TAMD_LDS_CINV (TAMD_LDS_LANE + 253 * 12)  // 5212, a multiple of 4
+#define TAMD_GF_DWORDS (TAMD_LDS_CINV + 192 * 8)  // 6748
 
 // v_perm product tables of one coefficient from LDS (6 dwords at a 16-byte aligned address).
 struct PermT { uint32_t t[6]; };
@@ -303,7 +306,6 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
         // every target a with lo_a <= i < hi_a, loaded once (the op is never shared: nw == 1).
         uint32_t col = vgpr(col0);
         const uint32_t cs = vgpr(cstep);
-        const uint8_t* inv = (const uint8_t*)(lds + TAMD_LDS_INV);
         const uint32_t w0 = tg.row, w1 = tg.len, w2 = tg.cap;
         // target a takes rows lo_a <= i < hi_a: (i - lo_a) < n_a, unsigned
         const uint32_t l0 = (w0 >> 10) & 0x7ffu, l1 = (w1 >> 10) & 0x7ffu, l2 = (w2 >> 10) & 0x7ffu;
@@ -317,7 +319,7 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
 #define TAMD_MULTI_TARGET(l, h, k, x, acc)                                                 \
     if (i - l < h) {                                                                       \
         if (k) acc ^= v;                                                                   \
-        else acc ^= lv_mul<NH>(v, perm_at(lds, inv[(col & 63u) ^ x] * 8u));                \
+        else acc ^= lv_mul<NH>(v, perm_at(lds, TAMD_LDS_CINV - 512u + (((col & 63u) ^ x) << 3)));  \
     }
         for (uint32_t e = 0; e < count; e += TAMD_RBATCH) {
             const bool more = e + TAMD_RBATCH < count;
@@ -360,9 +362,10 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
                 for (uint32_t h = 0; h < 2; ++h) {
 #pragma unroll
                     for (uint32_t q = h * H; q < h * H + H; ++q) {
-                        const uint32_t c = inv[(col & 63u) ^ px];
+                        // the perm tables of inv((col mod 64) ^ (p + 64)), one LDS lookup
+                        const uint32_t ti = TAMD_LDS_CINV - 512u + (((col & 63u) ^ px) << 3);
                         col += cs;
-                        if (e + q < count) a0 ^= lv_mul<NH>(lv_keep<FULL, NH>(d[q], o, len), perm_at(lds, c * 8u));
+                        if (e + q < count) a0 ^= lv_mul<NH>(lv_keep<FULL, NH>(d[q], o, len), perm_at(lds, ti));
                     }
                     if (more) {
 #pragma unroll
@@ -394,6 +397,32 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
     } else {
         const bool plain = p == 1u;
         const PermT cp = perm_at(lds, p * 8u);
+        if (TAMD_ROLL && nw == 1u) {
+            // rolling loads (as for LANE3 runs): the rows are summed as they arrive and the sum
+            // multiplied once (a parity row: p = 1, no multiply at all)
+            constexpr uint32_t H = TAMD_RBATCH / 2;
+            LV<NH> d[TAMD_RBATCH];
+            LV<NH> x = lv_zero<NH>();
+#pragma unroll
+            for (uint32_t q = 0; q < TAMD_RBATCH; ++q) d[q] = lv_load<NH>(src + (size_t)min(q, count - 1u) * step);
+            for (uint32_t e = 0; e < count; e += TAMD_RBATCH) {
+                const bool more = e + TAMD_RBATCH < count;
+#pragma unroll
+                for (uint32_t h = 0; h < 2; ++h) {
+#pragma unroll
+                    for (uint32_t q = h * H; q < h * H + H; ++q)
+                        if (e + q < count) x ^= lv_keep<FULL, NH>(d[q], o, len);
+                    if (more) {
+#pragma unroll
+                        for (uint32_t q = h * H; q < h * H + H; ++q)
+                            d[q] = lv_load<NH>(src + (size_t)min(e + TAMD_RBATCH + q, count - 1u) * step);
+                    }
+                }
+            }
+            a0 ^= plain ? x : lv_mul<NH>(x, cp);
+            unit += (count + TAMD_RBATCH - 1) / TAMD_RBATCH;
+            return;
+        }
         for (uint32_t e = 0; e < count; e += TAMD_RBATCH) {
             if ((unit++ & (nw - 1u)) != wid) continue;
             LV<NH> d[TAMD_RBATCH];

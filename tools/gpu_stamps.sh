@@ -6,10 +6,7 @@ OUT=$R/gpurun_out
 TAG=${1:-st}
 PROG=${2:-8}
 mkdir -p "$OUT/$TAG" && cd "$OUT/$TAG" || exit 1
-TONK_AMD_STAMPS=$PROG timeout -k 10 300 python "$R/bench.py" --no-cpu-baseline --no-end-to-end --steps 10 --warmup 3 > bench.json 2> stamps.err || exit 1
-ib=$(grep -o "n_instr_bytes [0-9]*" stamps.err | awk '{print $2}')
-ob=$(grep -o "n_ops_bytes [0-9]*" stamps.err | awk '{print $2}')
-ni=$(grep -o "n_items [0-9]*" stamps.err | awk '{print $2}')
+TONK_AMD_STAMPS=$PROG timeout -k 10 300 python "$R/bench.py" ${ARGS:-} --no-cpu-baseline --no-end-to-end --no-verify --no-pmc --steps 4 --warmup 2 > bench.json 2> stamps.err || exit 1
 bases=$(grep "item_base" stamps.err | awk '{print $NF}' | paste -sd,)
-python "$R/tools/stamps_report.py" "$ib" "$ob" "$ni" "$bases" > report.txt 2>&1
-rm -f tonk_amd_program.bin tonk_amd_stamps.bin
+python "$R/tools/stamps_report.py" "$bases" > report.txt 2>&1
+rm -f tonk_amd_*.bin

@@ -1,12 +1,13 @@
 """Per-item timing from TONK_AMD_STAMPS dumps (profiling only): per level, item duration vs op
 composition, wave busy time and the level's span."""
+import functools
 import numpy as np, sys
-ibytes, obytes, nitems = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
-bases = [int(x) for x in sys.argv[4].split(',')]
-prog = np.fromfile('tonk_amd_program.bin', dtype=np.uint32)
-instr = prog[:ibytes // 4].reshape(-1, 4)
-ops = prog[ibytes // 4:(ibytes + obytes) // 4].reshape(-1, 4)
-items = prog[(ibytes + obytes) // 4:(ibytes + obytes) // 4 + 2 * nitems].reshape(-1, 2)
+print = functools.partial(print, flush=True)  # (progress reaches the file as it is made)
+bases = [int(x) for x in sys.argv[1].split(',')]
+# tables as Device::start_program dumps them: items index op records, ops index instructions
+items = np.fromfile('tonk_amd_items.bin', dtype=np.uint32).reshape(-1, 2)
+ops = np.fromfile('tonk_amd_ops.bin', dtype=np.uint32).reshape(-1, 4)
+instr = np.fromfile('tonk_amd_instrs.bin', dtype=np.uint32).reshape(-1, 4)
 st = np.fromfile('tonk_amd_stamps.bin', dtype=np.uint64).reshape(-1, 3)
 kinds = instr[:, 0] & 0xff
 for l in range(len(bases) - 1):
