@@ -191,7 +191,7 @@ int main(int argc, char** argv) {
     p.loss_thresh = 42949673;
     p.fec_rate_q16 = 1311;
     p.ack_every = 64;
-    uint32_t streams = 8, step = 4096, warm_steps = 0, expand = ~0u, reps = 1;  // warm: untimed, unsampled first steps
+    uint32_t streams = 8, step = 4096, warm_steps = 0, expand = ~0u, backsub = ~0u, reps = 1;  // warm: untimed, unsampled first steps
     p.n_originals = 4096 * 6;
     for (int i = 1; i < argc; ++i) {
         const char* eq = strchr(argv[i], '=');
@@ -202,6 +202,7 @@ int main(int argc, char** argv) {
         if (k == "nobatch") { g_nobatch = atoi(eq + 1); continue; }
         if (k == "warm") { warm_steps = (uint32_t)atoi(eq + 1); continue; }
         if (k == "expand") { expand = (uint32_t)strtoul(eq + 1, nullptr, 0); continue; }
+        if (k == "backsub") { backsub = (uint32_t)strtoul(eq + 1, nullptr, 0); continue; }
         if (k == "pipe") { g_pipe = atoi(eq + 1); continue; }
         if (k == "reps") { reps = (uint32_t)atoi(eq + 1); continue; }  // level pipelining as the session runs it
         const unsigned long long v = strtoull(eq + 1, nullptr, 0);
@@ -247,6 +248,7 @@ int main(int argc, char** argv) {
         ctxs[s].reset(new Context());
         Context& ctx = *ctxs[s];
         ctx.ex.expand_limit = expand;
+        ctx.backsub_rows = backsub;
         ctx.pipeline = g_pipe != 0;
         ctx.rows.init(4ull * p.n_originals * 1344 + (256u << 20));
         encs[s].reset(new Encoder(&ctx, 1344));

@@ -30,6 +30,7 @@ static bool g_nobatch = false;  // nobatch=1: the runner's single-add path only
 // hazards (no segment reads or writes a row another writes) before the programs run in order.
 static bool g_pipeline = false;
 static uint32_t g_expand = ~0u;  // expand=<terms>: the session's expansion limit
+static uint32_t g_backsub = ~0u;  // backsub=<unknowns>: back substitution over materialized rows
 static uint32_t g_drain = 0;  // pipelined: complete every in-flight program after every g_drain-th (session record mode: 2)
 #include <map>
 #include <set>
@@ -165,6 +166,7 @@ struct Harness {
         ctx.track_dirty = g_dirty;
         ctx.pipeline = g_pipeline;
         ctx.ex.expand_limit = g_expand;
+        ctx.backsub_rows = g_backsub;
         arena.assign(g_arena_bytes, 0);
         enc = new Encoder(&ctx, row_bytes);
         dec = new Decoder(&ctx, row_bytes);
@@ -421,6 +423,7 @@ int main(int argc, char** argv) {
         else if (k == "pipeline") g_pipeline = v != 0;
         else if (k == "drain") g_drain = (uint32_t)v;
         else if (k == "expand") g_expand = (uint32_t)v;
+        else if (k == "backsub") g_backsub = (uint32_t)v;
         else if (parse_param(p, k, v)) {}
         else { fprintf(stderr, "bad key %s\n", k.c_str()); return 2; }
     }

@@ -48,11 +48,14 @@ def test_control_plane_matches_reference(harness, golden_index, tmp_path, name, 
     # also completes all in-flight ones (the session's record mode), so rows are reused sooner
     base, dirty = mode.split("-")[0], int(mode.endswith("-dirty"))
     # "-pipeexp": also the few-stream session's expansion limit (expansions over 16 terms are
-    # read as rows, one level up)
+    # read as rows, one level up) and its back substitution over materialized rows (from 2
+    # unknowns)
     pipe, drain = int("-pipe" in mode), 2 * int(mode.endswith("-pipedrain"))
-    expand = 16 if mode.endswith("-pipeexp") else 0xFFFFFFFF
+    few = mode.endswith("-pipeexp")
+    expand = 16 if few else 0xFFFFFFFF
+    backsub = 2 if few else 0xFFFFFFFF
     args = [harness, str(out), f"mode={base}", f"batch={batch}", f"dirty={dirty}", f"pipeline={pipe}",
-            f"drain={drain}", f"expand={expand}"] + sc["args"] + [
+            f"drain={drain}", f"expand={expand}", f"backsub={backsub}"] + sc["args"] + [
         f"seed_data={1000 + sid}", f"seed_loss={2000 + sid}"]
     r = subprocess.run(args, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]

@@ -11,8 +11,6 @@ namespace tamd {
 
 // Term lists up to this length go to the device unmerged (see eliminate_original_data).
 static const size_t kMergeAbove = 48;
-// Unknowns from which back substitution combines materialized eliminated rows (back_substitution).
-static const uint32_t kBackSubRows = 2;
 
 static inline uint32_t popcount64(uint64_t x) { return (uint32_t)__builtin_popcountll(x); }
 
@@ -1157,13 +1155,12 @@ Result Decoder::back_substitution() {
     std::vector<uint32_t>& gpos = tri_gstart_;
     std::vector<uint32_t> gend(L, 0);
     tri_acc_.resize((size_t)L * D);
-    // Every recovered value is a combination of up to L eliminated rows.  From kBackSubRows
-    // unknowns on, each eliminated row with more than one term is first materialized (one op
-    // reading its terms once) and the values combine those rows: Sum|buf| + L^2 row reads on
-    // the device and term copies on the host, instead of up to L * Sum|buf| of both.
-    static const uint32_t mat_from = getenv("TONK_AMD_BACKSUB_ROWS") ? (uint32_t)atoi(getenv("TONK_AMD_BACKSUB_ROWS"))
-                                                                      : kBackSubRows;
-    if (L >= mat_from) {
+    // Every recovered value is a combination of up to L eliminated rows.  From
+    // Context::backsub_rows unknowns on, each eliminated row with more than one term is first
+    // materialized (one op reading its terms once) and the values combine those rows: Sum|buf| +
+    // L^2 row reads on the device and term copies on the host, instead of up to L * Sum|buf| of
+    // both, for one more level.
+    if (L >= ctx_->backsub_rows) {
         for (uint32_t k = 0; k < L; ++k) {
             Recovery* r = mrows_[pivots_[k]].rec;
             if (r->buf.size() <= 1) continue;

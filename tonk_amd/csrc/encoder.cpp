@@ -606,12 +606,14 @@ Result Encoder::generate_cauchy(RecoveryOut& out) {
     // program); its readers must already see the level it will be written at.
     ctx_->rows.set_level(out.row, 1);
     static const uint32_t max_group = getenv("TONK_AMD_NO_MULTI") ? 1u : 3u;
+    static const uint32_t span = getenv("TONK_AMD_MULTI_SPAN") ? (uint32_t)atoi(getenv("TONK_AMD_MULTI_SPAN"))
+                                                                : kGroupSpan;  // (A/B knob, <= 2047)
     const uint32_t end_col = to_column(count_);
     // A row over a long window stays a pure combine of its own (the executor shares those across
     // a workgroup); a group is one wave's chain, and a long one would set the launch's tail.
-    const bool alone = count_ - first >= kGroupSpan;
+    const bool alone = count_ - first >= span;
     if (grp_n_ && (alone || grp_n_ >= max_group || grp_gen_ != window_gen_ ||
-                   col_sub(end_col, grp_[0].first_col) >= kGroupSpan))
+                   col_sub(end_col, grp_[0].first_col) >= span))
         emit_cauchy_group();
     grp_gen_ = window_gen_;
     CauchyTarget& t = grp_[grp_n_++];

@@ -441,6 +441,10 @@ struct Context {
     uint64_t epoch = 1;                // id of the pending program
     uint64_t arena_base_units = 0;     // offset of this context's range in the device arena
     bool oom = false;                  // arena exhausted (codecs go to Disabled)
+    // Decoder back substitution over materialized eliminated rows from this many unknowns on
+    // (Decoder::back_substitution; ~0u: never).  Few-stream sessions use it; in batched ones the
+    // extra level costs launches and saves no device bytes.
+    uint32_t backsub_rows = ~0u;
     // Level pipelining (the session, Device::set_pipelined): every launch runs level 1 of the
     // newest program beside the next level of each older program still in flight, so level d
     // of a program runs with level 1 of the program d - 1 later.  A row written at level d is

@@ -1189,6 +1189,11 @@ void* tamd_session_create(const tamd_session_params* p, char* err, size_t err_le
         static const char* expand_env = getenv("TONK_AMD_EXPAND");
         const uint32_t expand = expand_env ? (uint32_t)atoi(expand_env) : (p->n_streams <= 4 ? 16u : ~0u);
         if (pipe) ctx->ex.expand_limit = expand;
+        // The same split for back substitution over materialized rows (configs[4]: host time per
+        // program -12 %, device -6 %; configs[2]/[3]: +1 level, +20 % launches, no fewer bytes).
+        // TONK_AMD_BACKSUB_ROWS=<unknowns> overrides (A/B knob).
+        static const char* bs_env = getenv("TONK_AMD_BACKSUB_ROWS");
+        ctx->backsub_rows = bs_env ? (uint32_t)atoi(bs_env) : (p->n_streams <= 4 ? 2u : ~0u);
         std::unique_ptr<Stream> st(new Stream());
         st->ctx = ctx.get();
         wl::Params& q = st->p;
