@@ -245,7 +245,6 @@ bool Decoder::add_run_inorder(uint32_t col0, const RowId* rows, uint32_t k, uint
     grow_window(e0 + k);
     const RowTable& rt = ctx_->rows;
     const uint8_t owned = borrowed ? 0 : 1;
-    const uint64_t w_hdr = (uint64_t)(uint8_t)header_bytes << 16 | (uint64_t)owned << 24;
     uint32_t column = col0;
     const RowId* r = rows;
     // run state of the element before the run (set_run, kept in locals)
@@ -272,13 +271,14 @@ bool Decoder::add_run_inorder(uint32_t col0, const RowId* rows, uint32_t k, uint
                 run = prev_run + 1;
                 stride = off - prev_off;
             }
-            // 8-byte words in the StoredOriginal layout (encoder.h); send_msec and host stay
-            const uint64_t w0 = (uint64_t)*r | (uint64_t)framed_bytes << 32;  // row, bytes
-            const uint64_t w2[2] = {(uint64_t)off | (uint64_t)stride << 32,  // off, stride
-                                    (uint64_t)run | w_hdr};                  // run, header, owned (+pad)
-            memcpy((void*)o, &w0, 8);
-            memcpy((char*)(void*)o + 16, w2, 16);
+            o->row = *r;
+            o->off = off;
+            o->bytes = framed_bytes;
             o->column = column;
+            o->header_bytes = (uint8_t)header_bytes;
+            o->owned = owned;
+            o->run = (uint16_t)run;
+            o->stride = stride;
             prev_run = run;
             prev_off = off;
             prev_stride = stride;

@@ -90,11 +90,9 @@ bool Encoder::add_run(const RowId* rows, uint32_t k, uint32_t framed_bytes, uint
     uint32_t column = next_column_;
     const uint32_t now = (uint32_t)now_msec();
     const uint8_t owned = borrowed ? 0 : 1;
-    // Each slot is written as five 8-byte words (the StoredOriginal layout, checked in
-    // encoder.h): half the stores of field-by-field writes, nothing read back.
-    const uint64_t w_hdr = (uint64_t)(uint8_t)header_bytes << 16 | (uint64_t)owned << 24;
     for (uint32_t j = 1; j < k; ++j) {
         idx = (idx + 1) & mask;
+        StoredOriginal& o = base[idx];
         const uint32_t off = rt.offset(rows[j]);
         uint32_t run = 1, stride = 0;
         if (prev_bytes == framed_bytes && off > prev_off && prev_run < 0xffff &&
@@ -102,12 +100,16 @@ bool Encoder::add_run(const RowId* rows, uint32_t k, uint32_t framed_bytes, uint
             run = prev_run + 1;
             stride = off - prev_off;
         }
-        const uint64_t w[5] = {(uint64_t)rows[j] | (uint64_t)framed_bytes << 32,  // row, bytes
-                               (uint64_t)column | (uint64_t)now << 32,             // column, send_msec
-                               (uint64_t)off | (uint64_t)stride << 32,             // off, stride
-                               (uint64_t)run | w_hdr,                              // run, header, owned
-                               0};                                                 // host
-        memcpy((void*)&base[idx], w, sizeof(w));
+        o.row = rows[j];
+        o.bytes = framed_bytes;
+        o.column = column;
+        o.send_msec = now;
+        o.off = off;
+        o.stride = stride;
+        o.run = (uint16_t)run;
+        o.header_bytes = (uint8_t)header_bytes;
+        o.owned = owned;
+        o.host = nullptr;
         prev_off = off;
         prev_stride = stride;
         prev_bytes = framed_bytes;

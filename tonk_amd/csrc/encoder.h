@@ -8,7 +8,6 @@
 // combine op (plus running-sum scans) in the context's device program.
 #pragma once
 
-#include <stddef.h>
 #include <stdio.h>
 
 #include "engine.h"
@@ -47,14 +46,6 @@ struct StoredOriginal {
     uint8_t owned = 0;          // the codec frees `row` when the packet leaves the window
     void* host = nullptr;       // optional host mirror (C-ABI: siamese_encoder_get/retransmit)
 };
-
-// Encoder::add_run and Decoder::add_run_inorder write slots as 8-byte words in this layout.
-static_assert(sizeof(StoredOriginal) == 40 && offsetof(StoredOriginal, bytes) == 4 &&
-                  offsetof(StoredOriginal, column) == 8 && offsetof(StoredOriginal, send_msec) == 12 &&
-                  offsetof(StoredOriginal, off) == 16 && offsetof(StoredOriginal, stride) == 20 &&
-                  offsetof(StoredOriginal, run) == 24 && offsetof(StoredOriginal, header_bytes) == 26 &&
-                  offsetof(StoredOriginal, owned) == 27 && offsetof(StoredOriginal, host) == 32,
-              "StoredOriginal word layout");
 
 typedef void (*HostRelease)(void* host, void* user);
 
