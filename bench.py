@@ -13,7 +13,7 @@ work runs as one merged launch sequence on the GPU, pipelined with the host buil
 payload GiB/s over all ranks; the timed region is bracketed by a barrier and a device sync.
 
 roofline: algorithmic HBM bytes (SURVEY.md s8(d) B_alg, counted exactly per step) divided by
-the summed duration of the executor (tamd_exec16) launches of the timed steps (HIP events on the launch
+the summed duration of the executor (tamd_exec24; tamd_exec16 under TONK_AMD_SLICE=1024) launches of the timed steps (HIP events on the launch
 stream), against the 8.0 TB/s HBM3E peak.  cpu_baseline: the reference codec (compiled from
 /root/reference by oracle/Makefile, shipped prebuilt in oracle/_ref) on a sample of the same
 workload, on rank 0 after the timed region, with the host cores the job owns (16 per GPU).
@@ -101,7 +101,12 @@ def host_cpus() -> int:
         return os.cpu_count() or 8
 
 
-def _timed_counter_values(csv_dir: str, counter: str, kernel: str = "tamd_exec16") -> list[float]:
+# The executor kernel the library launches (engine.cpp slice_from_env: 1536-byte slices unless
+# TONK_AMD_SLICE=1024).
+EXEC_KERNEL = "tamd_exec16" if os.environ.get("TONK_AMD_SLICE", "").strip() == "1024" else "tamd_exec24"
+
+
+def _timed_counter_values(csv_dir: str, counter: str, kernel: str = EXEC_KERNEL) -> list[float]:
     """Per-dispatch values of `counter` for `kernel`'s dispatches inside the timed region (between
     the two tamd_timed_region markers Device::set_timing launches), in dispatch order."""
     import csv
@@ -124,8 +129,9 @@ def pmc_traffic(workload: str, steps: int, warmup: int, timeout_s: int = 240) ->
     passes (FETCH_SIZE, then WRITE_SIZE: they do not fit one TCC pass) over a rerun of the same
     workload with the same steps (child processes), restricted to the dispatches between the
     timed-region markers, so the launches counted are the ones the line's roofline averages.  gfx950 corrections (MI355X_MICROARCH.md, HBM): FETCH_SIZE counts half
-    the bytes of 16-B-per-lane reads (the executor's width), so it is doubled; WRITE_SIZE is exact
-    for 16-B stores.  Both counters are KiB and count L2 fabric requests (Infinity-Cache hits
+    the bytes of 16-B-per-lane reads, so it is doubled; tools/pmc_calib.hip measures the same
+    factor 2 for tamd_exec24's row pattern (16 B + 8 B per lane over 1344-byte rows:
+    profiles/r03_pmc_calib.txt); WRITE_SIZE is exact for both store patterns.  Both counters are KiB and count L2 fabric requests (Infinity-Cache hits
     included).  Returns None when rocprofv3 is unavailable or a pass fails."""
     import shutil
     import signal
@@ -158,7 +164,7 @@ def pmc_traffic(workload: str, steps: int, warmup: int, timeout_s: int = 240) ->
         vals[counter] = _timed_counter_values(d, counter)
         shutil.rmtree(d, ignore_errors=True)
         if not vals[counter]:
-            return {"error": f"{counter}: no timed tamd_exec16 dispatches in the counter csv"}
+            return {"error": f"{counter}: no timed {EXEC_KERNEL} dispatches in the counter csv"}
     f, w = vals["FETCH_SIZE"], vals["WRITE_SIZE"]
     per = [(a * 2.0 + b) * 1024.0 for a, b in zip(f, w)]
     mean = sum(per) / len(per)
@@ -727,7 +733,7 @@ def main() -> int:
             "traffic": round(traffic, 1) if traffic else None,
             "traffic_over_alg": pmc.get("traffic_over_alg") if pmc else None,
             "pmc": pmc,
-            "kernel": "tamd_exec16",
+            "kernel": EXEC_KERNEL,
             "launches": launches,
             "avg_launch_us": round(kernel_ms * 1e3 / launches, 3) if launches else None,
             "alg_bytes_per_launch": round(alg / launches, 1) if launches else None,

@@ -9,6 +9,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+extern "C" __global__ void tamd_exec24(tamd_segments, const uint8_t*, uint32_t, uint8_t*, const uint32_t*,
+                                        const uint8_t*, unsigned long long*);
 extern "C" __global__ void tamd_exec16(tamd_segments, const uint8_t*, uint32_t, uint8_t*, const uint32_t*,
                                        const uint8_t*, unsigned long long*);
 typedef void (*ExecFn)(tamd_segments, const uint8_t*, uint32_t, uint8_t*, const uint32_t*, const uint8_t*,
@@ -127,7 +129,7 @@ bool Device::init(int device, uint64_t arena_bytes) {
     // Persistent grid: exactly the workgroups that are resident at once (occupancy x CUs), so
     // every workgroup stages the GF tables once and no workgroup starts late (kernels.hip).
     int per_cu = 0;
-    exec_kernel_ = (const void*)tamd_exec16;
+    exec_kernel_ = slice_bytes() == TAMD_SLICE_BYTES ? (const void*)tamd_exec16 : (const void*)tamd_exec24;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, exec_kernel_, 256, 0) != hipSuccess ||
         per_cu < 1)
         per_cu = 1;

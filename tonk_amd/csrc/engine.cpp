@@ -7,6 +7,12 @@
 
 namespace tamd {
 
+static uint32_t slice_from_env() {
+    const char* e = getenv("TONK_AMD_SLICE");
+    return e && atoi(e) == (int)TAMD_SLICE_BYTES ? TAMD_SLICE_BYTES : TAMD_SLICE_BYTES_X;
+}
+const uint32_t g_slice_bytes = slice_from_env();
+
 // ---------------------------------------------------------------------------------------------
 // RowTable
 // ---------------------------------------------------------------------------------------------

@@ -63,8 +63,10 @@ struct NoInitAlloc : std::allocator<T> {
 typedef std::vector<Term, NoInitAlloc<Term>> Sym;
 typedef std::vector<tamd_instr, NoInitAlloc<tamd_instr>> InstrVec;
 
-// Bytes of an op one device work item covers (program.h TAMD_SLICE_BYTES, tamd_exec16).
-inline uint32_t slice_bytes() { return TAMD_SLICE_BYTES; }
+// Bytes of an op one device work item covers (program.h): TAMD_SLICE_BYTES_X (tamd_exec24) unless
+// TONK_AMD_SLICE=1024 selects TAMD_SLICE_BYTES (tamd_exec16); fixed for the process.
+extern const uint32_t g_slice_bytes;
+inline uint32_t slice_bytes() { return g_slice_bytes; }
 
 // ---------------------------------------------------------------------------------------------
 // Arena bookkeeping: rows are contiguous ranges of 64-byte units in one device allocation.

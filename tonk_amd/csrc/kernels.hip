@@ -159,8 +159,13 @@ __device__ __forceinline__ LV<NH> lv_zero() {
     for (int i = 0; i < NH; ++i) r.h[i] = 0;
     return r;
 }
+// NH = 3: a 1536-byte slice, 16 B per lane at `o` (the slice's first 1024 bytes) and 8 B per lane
+// at `ox` = slice + 1024 + 8 * lane (its last 512): one wave covers a whole 1302-byte packet row,
+// one dwordx4 and one dwordx2 load per row, instead of a 1024-byte item plus a tail item that
+// repeats the instruction walk and memory round trips for 278 bytes.  `px` is the row's address
+// at ox (unused for NH < 3).
 template <int NH>
-__device__ __forceinline__ LV<NH> lv_load(const uint8_t* p) {
+__device__ __forceinline__ LV<NH> lv_load(const uint8_t* p, const uint8_t* px = nullptr) {
     LV<NH> r;
     if constexpr (NH == 1) {
         r.h[0] = *(const u64*)p;
@@ -168,6 +173,7 @@ __device__ __forceinline__ LV<NH> lv_load(const uint8_t* p) {
         const u64x2 t = *(const u64x2*)p;
         r.h[0] = t.x;
         r.h[1] = t.y;
+        if constexpr (NH == 3) r.h[2] = *(const u64*)px;
     }
     return r;
 }
@@ -183,12 +189,14 @@ __device__ __forceinline__ void lv_store(uint8_t* p, const LV<NH>& v) {
     }
 }
 // x with the bytes at or past `len` cleared (lane bytes start at offset o)
+// (NH = 3: FULL covers the 16-byte part only; the extension word is always masked)
 template <bool FULL, int NH>
-__device__ __forceinline__ LV<NH> lv_keep(LV<NH> x, uint32_t o, uint32_t len) {
+__device__ __forceinline__ LV<NH> lv_keep(LV<NH> x, uint32_t o, uint32_t len, uint32_t ox = 0) {
     if (!FULL) {
 #pragma unroll
-        for (int i = 0; i < NH; ++i) x.h[i] &= keep_mask<false>(o + 8u * i, len);
+        for (int i = 0; i < (NH < 3 ? NH : 2); ++i) x.h[i] &= keep_mask<false>(o + 8u * i, len);
     }
+    if constexpr (NH == 3) x.h[2] &= keep_mask<false>(ox, len);
     return x;
 }
 template <int NH>
@@ -212,13 +220,22 @@ __device__ __forceinline__ void lv_acc3(const LV<NH>& x, const PermT& c1, const 
 }
 template <bool FULL, int NH>
 __device__ __forceinline__ void lv_store_row(uint8_t* __restrict__ arena, uint32_t row, uint32_t len, uint32_t cap,
-                                             u64 footer, uint32_t o, const LV<NH>& x) {
+                                             u64 footer, uint32_t o, const LV<NH>& x, uint32_t ox = 0) {
+    constexpr int NM = NH < 3 ? NH : 2;
     if (FULL) {
-        lv_store<NH>(arena + (size_t)row * TAMD_ROW_UNIT + o, x);
+        if constexpr (NH == 3) {
+            u64x2 t;
+            t.x = x.h[0];
+            t.y = x.h[1];
+            *(u64x2*)(arena + (size_t)row * TAMD_ROW_UNIT + o) = t;
+        } else {
+            lv_store<NH>(arena + (size_t)row * TAMD_ROW_UNIT + o, x);
+        }
     } else {
 #pragma unroll
-        for (int i = 0; i < NH; ++i) store_slice(arena, row, len, cap, footer, o + 8u * i, x.h[i]);
+        for (int i = 0; i < NM; ++i) store_slice(arena, row, len, cap, footer, o + 8u * i, x.h[i]);
     }
+    if constexpr (NH == 3) store_slice(arena, row, len, cap, footer, ox, x.h[2]);
 }
 
 // ACCR: a strided run of equally long rows (program.h).  TAMD_RBATCH row loads are issued
@@ -230,7 +247,7 @@ __device__ __forceinline__ void lv_store_row(uint8_t* __restrict__ arena, uint32
 // wave combines only the batches with unit mod nw == wid (the coefficient stepping still walks
 // every row).
 template <bool FULL, int NH, uint32_t TAMD_RBATCH>
-__device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& r, const tamd_instr& tg, uint32_t o,
+__device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& r, const tamd_instr& tg, uint32_t o, uint32_t ox,
                                          const uint8_t* __restrict__ arena, const uint32_t* __restrict__ lds,
                                          uint32_t& unit, uint32_t nw, uint32_t wid, LV<NH>& a0, LV<NH>& a1,
                                          LV<NH>& a2) {
@@ -238,9 +255,10 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
     const uint32_t row0 = a.row, len = a.len, count = a.cap;
     const uint32_t stride = r.row, col0 = r.len, cstep = r.cap;
     const uint8_t* src = arena + (size_t)row0 * TAMD_ROW_UNIT + load_off<FULL>(o, len);
+    const uint8_t* srcx = arena + (size_t)row0 * TAMD_ROW_UNIT + (NH == 3 ? load_off<false>(ox, len) : 0u);
     const size_t step = (size_t)stride * TAMD_ROW_UNIT;
     // loads past the run's end re-read its last row (never consumed)
-#define TAMD_RUN_ROW(q) lv_load<NH>(src + (size_t)min(e + (q), count - 1u) * step)
+#define TAMD_RUN_ROW(q) lv_load<NH>(src + (size_t)min(e + (q), count - 1u) * step, srcx + (size_t)min(e + (q), count - 1u) * step)
     if (mode == TAMD_R_LANE3) {
         // byte offset of the (cx, cx^2) tables in the lane table: 48 bytes per column value index
         const uint32_t W = 253u * 48u;
@@ -253,25 +271,25 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
             constexpr uint32_t H = TAMD_RBATCH / 2;
             LV<NH> d[TAMD_RBATCH];
 #pragma unroll
-            for (uint32_t q = 0; q < TAMD_RBATCH; ++q) d[q] = lv_load<NH>(src + (size_t)min(q, count - 1u) * step);
+            for (uint32_t q = 0; q < TAMD_RBATCH; ++q) d[q] = lv_load<NH>(src + (size_t)min(q, count - 1u) * step, srcx + (size_t)min(q, count - 1u) * step);
             for (uint32_t e = 0; e < count; e += TAMD_RBATCH) {
                 const bool more = e + TAMD_RBATCH < count;
 #pragma unroll
                 for (uint32_t h = 0; h < 2; ++h) {
 #pragma unroll
-                    for (uint32_t q = h * H; q < h * H + H; ++q) {
+                    for (uint32_t q = h * H; q < (h ? TAMD_RBATCH : H); ++q) {
                         if (e + q < count) {
                             const uint32_t ti = TAMD_LDS_LANE + (t >> 2);
                             const PermT c1 = perm_at(lds, ti), c2 = perm_at_hi(lds, ti + 6u);
-                            lv_acc3<NH>(lv_keep<FULL, NH>(d[q], o, len), c1, c2, a0, a1, a2);
+                            lv_acc3<NH>(lv_keep<FULL, NH>(d[q], o, len, ox), c1, c2, a0, a1, a2);
                             t += tstep;
                             t = min(t, t - W);
                         }
                     }
                     if (more) {
 #pragma unroll
-                        for (uint32_t q = h * H; q < h * H + H; ++q)
-                            d[q] = lv_load<NH>(src + (size_t)min(e + TAMD_RBATCH + q, count - 1u) * step);
+                        for (uint32_t q = h * H; q < (h ? TAMD_RBATCH : H); ++q)
+                            d[q] = lv_load<NH>(src + (size_t)min(e + TAMD_RBATCH + q, count - 1u) * step, srcx + (size_t)min(e + TAMD_RBATCH + q, count - 1u) * step);
                     }
                 }
             }
@@ -295,7 +313,7 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
                 if (e + q < count) {
                     const uint32_t ti = TAMD_LDS_LANE + (t >> 2);
                     const PermT c1 = perm_at(lds, ti), c2 = perm_at_hi(lds, ti + 6u);
-                    lv_acc3<NH>(lv_keep<FULL, NH>(d[q], o, len), c1, c2, a0, a1, a2);
+                    lv_acc3<NH>(lv_keep<FULL, NH>(d[q], o, len, ox), c1, c2, a0, a1, a2);
                     t += tstep;
                     t = min(t, t - W);  // t - W wraps above t while t < W
                 }
@@ -315,7 +333,7 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
         constexpr uint32_t H = TAMD_RBATCH / 2;
         LV<NH> d[TAMD_RBATCH];
 #pragma unroll
-        for (uint32_t q = 0; q < TAMD_RBATCH; ++q) d[q] = lv_load<NH>(src + (size_t)min(q, count - 1u) * step);
+        for (uint32_t q = 0; q < TAMD_RBATCH; ++q) d[q] = lv_load<NH>(src + (size_t)min(q, count - 1u) * step, srcx + (size_t)min(q, count - 1u) * step);
 #define TAMD_MULTI_TARGET(l, h, k, x, acc)                                                 \
     if (i - l < h) {                                                                       \
         if (k) acc ^= v;                                                                   \
@@ -326,10 +344,10 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
 #pragma unroll
             for (uint32_t h = 0; h < 2; ++h) {
 #pragma unroll
-                for (uint32_t q = h * H; q < h * H + H; ++q) {
+                for (uint32_t q = h * H; q < (h ? TAMD_RBATCH : H); ++q) {
                     const uint32_t i = e + q;
                     if (i < count) {
-                        const LV<NH> v = lv_keep<FULL, NH>(d[q], o, len);
+                        const LV<NH> v = lv_keep<FULL, NH>(d[q], o, len, ox);
                         TAMD_MULTI_TARGET(l0, h0, k0, x0, a0)
                         TAMD_MULTI_TARGET(l1, h1, k1, x1, a1)
                         TAMD_MULTI_TARGET(l2, h2, k2, x2, a2)
@@ -338,8 +356,8 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
                 }
                 if (more) {
 #pragma unroll
-                    for (uint32_t q = h * H; q < h * H + H; ++q)
-                        d[q] = lv_load<NH>(src + (size_t)min(e + TAMD_RBATCH + q, count - 1u) * step);
+                    for (uint32_t q = h * H; q < (h ? TAMD_RBATCH : H); ++q)
+                        d[q] = lv_load<NH>(src + (size_t)min(e + TAMD_RBATCH + q, count - 1u) * step, srcx + (size_t)min(e + TAMD_RBATCH + q, count - 1u) * step);
                 }
             }
         }
@@ -355,22 +373,22 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
             constexpr uint32_t H = TAMD_RBATCH / 2;
             LV<NH> d[TAMD_RBATCH];
 #pragma unroll
-            for (uint32_t q = 0; q < TAMD_RBATCH; ++q) d[q] = lv_load<NH>(src + (size_t)min(q, count - 1u) * step);
+            for (uint32_t q = 0; q < TAMD_RBATCH; ++q) d[q] = lv_load<NH>(src + (size_t)min(q, count - 1u) * step, srcx + (size_t)min(q, count - 1u) * step);
             for (uint32_t e = 0; e < count; e += TAMD_RBATCH) {
                 const bool more = e + TAMD_RBATCH < count;
 #pragma unroll
                 for (uint32_t h = 0; h < 2; ++h) {
 #pragma unroll
-                    for (uint32_t q = h * H; q < h * H + H; ++q) {
+                    for (uint32_t q = h * H; q < (h ? TAMD_RBATCH : H); ++q) {
                         // the perm tables of inv((col mod 64) ^ (p + 64)), one LDS lookup
                         const uint32_t ti = TAMD_LDS_CINV - 512u + (((col & 63u) ^ px) << 3);
                         col += cs;
-                        if (e + q < count) a0 ^= lv_mul<NH>(lv_keep<FULL, NH>(d[q], o, len), perm_at(lds, ti));
+                        if (e + q < count) a0 ^= lv_mul<NH>(lv_keep<FULL, NH>(d[q], o, len, ox), perm_at(lds, ti));
                     }
                     if (more) {
 #pragma unroll
-                        for (uint32_t q = h * H; q < h * H + H; ++q)
-                            d[q] = lv_load<NH>(src + (size_t)min(e + TAMD_RBATCH + q, count - 1u) * step);
+                        for (uint32_t q = h * H; q < (h ? TAMD_RBATCH : H); ++q)
+                            d[q] = lv_load<NH>(src + (size_t)min(e + TAMD_RBATCH + q, count - 1u) * step, srcx + (size_t)min(e + TAMD_RBATCH + q, count - 1u) * step);
                     }
                 }
             }
@@ -392,7 +410,7 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
             }
 #pragma unroll
             for (uint32_t q = 0; q < TAMD_RBATCH; ++q)
-                if (e + q < count) a0 ^= lv_mul<NH>(lv_keep<FULL, NH>(d[q], o, len), perm_at(lds, c[q] * 8u));
+                if (e + q < count) a0 ^= lv_mul<NH>(lv_keep<FULL, NH>(d[q], o, len, ox), perm_at(lds, c[q] * 8u));
         }
     } else {
         const bool plain = p == 1u;
@@ -404,18 +422,18 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
             LV<NH> d[TAMD_RBATCH];
             LV<NH> x = lv_zero<NH>();
 #pragma unroll
-            for (uint32_t q = 0; q < TAMD_RBATCH; ++q) d[q] = lv_load<NH>(src + (size_t)min(q, count - 1u) * step);
+            for (uint32_t q = 0; q < TAMD_RBATCH; ++q) d[q] = lv_load<NH>(src + (size_t)min(q, count - 1u) * step, srcx + (size_t)min(q, count - 1u) * step);
             for (uint32_t e = 0; e < count; e += TAMD_RBATCH) {
                 const bool more = e + TAMD_RBATCH < count;
 #pragma unroll
                 for (uint32_t h = 0; h < 2; ++h) {
 #pragma unroll
-                    for (uint32_t q = h * H; q < h * H + H; ++q)
-                        if (e + q < count) x ^= lv_keep<FULL, NH>(d[q], o, len);
+                    for (uint32_t q = h * H; q < (h ? TAMD_RBATCH : H); ++q)
+                        if (e + q < count) x ^= lv_keep<FULL, NH>(d[q], o, len, ox);
                     if (more) {
 #pragma unroll
-                        for (uint32_t q = h * H; q < h * H + H; ++q)
-                            d[q] = lv_load<NH>(src + (size_t)min(e + TAMD_RBATCH + q, count - 1u) * step);
+                        for (uint32_t q = h * H; q < (h ? TAMD_RBATCH : H); ++q)
+                            d[q] = lv_load<NH>(src + (size_t)min(e + TAMD_RBATCH + q, count - 1u) * step, srcx + (size_t)min(e + TAMD_RBATCH + q, count - 1u) * step);
                     }
                 }
             }
@@ -431,7 +449,7 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
             LV<NH> x = lv_zero<NH>();
 #pragma unroll
             for (uint32_t q = 0; q < TAMD_RBATCH; ++q)
-                if (e + q < count) x ^= lv_keep<FULL, NH>(d[q], o, len);
+                if (e + q < count) x ^= lv_keep<FULL, NH>(d[q], o, len, ox);
             a0 ^= plain ? x : lv_mul<NH>(x, cp);  // one coefficient: sum the batch's rows, one product
         }
     }
@@ -446,7 +464,7 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
 // acc_0 through LDS and stores.  Returns acc_0.
 template <bool FULL, int NH, uint32_t TAMD_BATCH>
 __device__ __forceinline__ LV<NH> run_item(const tamd_instr* __restrict__ instrs, uint32_t first, uint32_t end,
-                                           uint32_t o, uint32_t laneb, uint8_t* __restrict__ arena,
+                                           uint32_t o, uint32_t ox, uint32_t laneb, uint8_t* __restrict__ arena,
                                            const uint8_t* __restrict__ zrow, const uint32_t* __restrict__ lds,
                                            uint32_t nw, uint32_t wid) {
     LV<NH> a0 = lv_zero<NH>(), a1 = lv_zero<NH>(), a2 = lv_zero<NH>();  // the op's accumulators (program.h)
@@ -462,7 +480,7 @@ __device__ __forceinline__ LV<NH> run_item(const tamd_instr* __restrict__ instrs
             if ((in[j].w0 & 0xffu) == TAMD_I_ACCR && j < nb) nb = j;
         if (nb == 0) {
             // in[1]: the RANGE word, in[2]: TARGETS (MULTI runs)
-            run_accr<FULL, NH, TAMD_BATCH>(in[0], in[1], in[2], o, arena, lds, unit, nw, wid, a0, a1, a2);
+            run_accr<FULL, NH, TAMD_BATCH>(in[0], in[1], in[2], o, ox, arena, lds, unit, nw, wid, a0, a1, a2);
             k += ((in[0].w0 >> 8) & 0xffu) == TAMD_R_MULTI ? 3u : 2u;
             continue;
         }
@@ -477,15 +495,16 @@ __device__ __forceinline__ LV<NH> run_item(const tamd_instr* __restrict__ instrs
         for (uint32_t j = 0; j < TAMD_BATCH; ++j) {
             const uint32_t kind = in[j].w0 & 0xffu;
             const bool ld = j < nb && (kind == TAMD_I_ACC || kind == TAMD_I_ACC3);
-            const uint8_t* p = ld ? arena + (size_t)in[j].row * TAMD_ROW_UNIT + load_off<FULL>(o, in[j].len)
-                                  : zrow + laneb;
-            v[j] = lv_load<NH>(p);
+            const uint8_t* rp = arena + (size_t)in[j].row * TAMD_ROW_UNIT;
+            const uint8_t* p = ld ? rp + load_off<FULL>(o, in[j].len) : zrow + laneb;
+            const uint8_t* px = NH < 3 ? p : ld ? rp + load_off<false>(ox, in[j].len) : zrow + (laneb >> 1);
+            v[j] = lv_load<NH>(p, px);
         }
 #pragma unroll
         for (uint32_t j = 0; j < TAMD_BATCH; ++j) {
             const uint32_t w = in[j].w0, kind = j < nb ? (w & 0xffu) : 0u;
             if (kind == TAMD_I_ACC) {
-                LV<NH> x = lv_keep<FULL, NH>(v[j], o, in[j].len);
+                LV<NH> x = lv_keep<FULL, NH>(v[j], o, in[j].len, ox);
                 const uint32_t coef = (w >> 8) & 0xffu;
                 if (coef != 1u) x = lv_mul<NH>(x, perm_at(lds, coef * 8u));
                 const uint32_t a = (w >> 16) & 0xffu;
@@ -498,20 +517,20 @@ __device__ __forceinline__ LV<NH> run_item(const tamd_instr* __restrict__ instrs
                 if (c0 == 1u) x = a0; else if (c0) x = lv_mul<NH>(a0, perm_at(lds, c0 * 8u));
                 if (c1 == 1u) x ^= a1; else if (c1) x ^= lv_mul<NH>(a1, perm_at(lds, c1 * 8u));
                 if (c2 == 1u) x ^= a2; else if (c2) x ^= lv_mul<NH>(a2, perm_at(lds, c2 * 8u));
-                lv_store_row<FULL, NH>(arena, in[j].row, in[j].len, in[j].cap, 0, o, x);
+                lv_store_row<FULL, NH>(arena, in[j].row, in[j].len, in[j].cap, 0, o, x, ox);
             } else if (kind == TAMD_I_ACC3) {
-                const LV<NH> x = lv_keep<FULL, NH>(v[j], o, in[j].len);
+                const LV<NH> x = lv_keep<FULL, NH>(v[j], o, in[j].len, ox);
                 const PermT c1 = perm_at(lds, ((w >> 8) & 0xffu) * 8u), c2 = perm_at(lds, ((w >> 16) & 0xffu) * 8u);
                 lv_acc3<NH>(x, c1, c2, a0, a1, a2);
             } else if (kind == TAMD_I_STORE && nw == 1u) {
                 const uint32_t a = (w >> 16) & 0xffu;
                 const LV<NH> x = a == 0 ? a0 : (a == 1 ? a1 : a2);
-                if (FULL) {
+                if (FULL && NH < 3) {
                     lv_store<NH>(arena + (size_t)in[j].row * TAMD_ROW_UNIT + o, x);
                 } else {
                     // the FOOTER word follows the STORE (possibly past this batch)
                     const tamd_instr f = instrs[k + j + 1];
-                    lv_store_row<false, NH>(arena, in[j].row, in[j].len, in[j].cap, ((u64)f.len << 32) | f.row, o, x);
+                    lv_store_row<FULL, NH>(arena, in[j].row, in[j].len, in[j].cap, ((u64)f.len << 32) | f.row, o, x, ox);
                 }
             } else if (kind == TAMD_I_CLEAR) {
                 a0 = a1 = a2 = lv_zero<NH>();
@@ -536,6 +555,8 @@ __device__ __forceinline__ void exec_level(const tamd_segments& sg, const uint8_
                                            const uint32_t* __restrict__ gf_perm, const uint8_t* __restrict__ zrow,
                                            unsigned long long* __restrict__ stamps) {
     constexpr uint32_t SLICE = 64u * 8u * NH;
+    // bytes of a slice at the lanes' 16-byte offsets (NH = 3: the first 1024, FULL's extent)
+    constexpr uint32_t MAIN = NH == 3 ? 1024u : SLICE;
     __shared__ __attribute__((aligned(16))) uint32_t lds_perm[TAMD_GF_DWORDS];
     __shared__ LV<NH> partial[TAMD_WAVES_PER_WG][64];  // shared ops: the waves' acc_0
     __shared__ uint32_t claim, shared_claim, shared_item;
@@ -559,7 +580,8 @@ __device__ __forceinline__ void exec_level(const tamd_segments& sg, const uint8_
 
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t wave = uniform(threadIdx.x >> 6);
-    const uint32_t laneb = lane * 8u * NH;
+    const uint32_t laneb = lane * 8u * (NH < 3 ? NH : 2);
+    const uint32_t laneb_x = MAIN + lane * 8u;  // (NH = 3) the extension word's offset in the slice
 
     // Items [0, n_shared) are class-0 pure combines: the workgroup takes them one at a time
     // (items g, g + G, ...), each wave combining every fourth batch of rows; wave 0 reduces the
@@ -573,12 +595,12 @@ __device__ __forceinline__ void exec_level(const tamd_segments& sg, const uint8_
         const uint2 item = items[it];
         const tamd_op op = ops[uniform(item.x)];
         const uint32_t s0 = uniform(item.y) * SLICE;
-        const uint32_t o = s0 + laneb;
+        const uint32_t o = s0 + laneb, ox = s0 + laneb_x;
         const uint32_t first = uniform(op.first), end = uniform(op.first + op.count);
-        const bool full = s0 + SLICE <= uniform(op.full);
+        const bool full = s0 + MAIN <= uniform(op.full);
         const u64 t0 = stamps ? __builtin_amdgcn_s_memrealtime() : 0;
-        const LV<NH> x = full ? run_item<true, NH, B>(instrs, first, end, o, laneb, arena, zrow, lds_perm, TAMD_WAVES_PER_WG, wave)
-                              : run_item<false, NH, B>(instrs, first, end, o, laneb, arena, zrow, lds_perm, TAMD_WAVES_PER_WG, wave);
+        const LV<NH> x = full ? run_item<true, NH, B>(instrs, first, end, o, ox, laneb, arena, zrow, lds_perm, TAMD_WAVES_PER_WG, wave)
+                              : run_item<false, NH, B>(instrs, first, end, o, ox, laneb, arena, zrow, lds_perm, TAMD_WAVES_PER_WG, wave);
         partial[wave][lane] = x;
         __syncthreads();
         if (wave == 0) {
@@ -587,8 +609,9 @@ __device__ __forceinline__ void exec_level(const tamd_segments& sg, const uint8_
             sum ^= partial[2][lane];
             sum ^= partial[3][lane];
             const tamd_instr st = instrs[end - 2u], f = instrs[end - 1u];  // STORE (acc_0) + FOOTER
-            if (full) lv_store<NH>(arena + (size_t)st.row * TAMD_ROW_UNIT + o, sum);
-            else lv_store_row<false, NH>(arena, st.row, st.len, st.cap, ((u64)f.len << 32) | f.row, o, sum);
+            const u64 foot = ((u64)f.len << 32) | f.row;
+            if (full) lv_store_row<true, NH>(arena, st.row, st.len, st.cap, foot, o, sum, ox);
+            else lv_store_row<false, NH>(arena, st.row, st.len, st.cap, foot, o, sum, ox);
             if (stamps && lane == 0) {
                 __atomic_signal_fence(__ATOMIC_SEQ_CST);
                 stamps[3 * it] = t0;
@@ -619,13 +642,13 @@ __device__ __forceinline__ void exec_level(const tamd_segments& sg, const uint8_
         const uint2 item = ((const uint2*)(pbase + uniform(sd.items)))[uniform(rel)];
         const tamd_op op = sops[uniform(item.x)];
         const uint32_t s0 = uniform(item.y) * SLICE;
-        const uint32_t o = s0 + laneb;
+        const uint32_t o = s0 + laneb, ox = s0 + laneb_x;
         const uint32_t first = uniform(op.first), end = uniform(op.first + op.count);
         const u64 t0 = stamps ? __builtin_amdgcn_s_memrealtime() : 0;
-        if (s0 + SLICE <= uniform(op.full))
-            run_item<true, NH, B>(ins, first, end, o, laneb, arena, zrow, lds_perm, 1u, 0u);
+        if (s0 + MAIN <= uniform(op.full))
+            run_item<true, NH, B>(ins, first, end, o, ox, laneb, arena, zrow, lds_perm, 1u, 0u);
         else
-            run_item<false, NH, B>(ins, first, end, o, laneb, arena, zrow, lds_perm, 1u, 0u);
+            run_item<false, NH, B>(ins, first, end, o, ox, laneb, arena, zrow, lds_perm, 1u, 0u);
         if (stamps && lane == 0) {  // profiling only (TONK_AMD_STAMPS): vector stores of 100 MHz stamps
             __atomic_signal_fence(__ATOMIC_SEQ_CST);
             const u64 t1 = __builtin_amdgcn_s_memrealtime();
@@ -649,6 +672,9 @@ __device__ __forceinline__ void exec_level(const tamd_segments& sg, const uint8_
         exec_level<NH, B>(segments, prog, n_shared, arena, gf_perm, zrow, stamps);                    \
     }
 TAMD_EXEC_KERNEL(tamd_exec16, 2, 6)
+// tamd_exec24: 1536-byte slices (16 + 8 B per lane), so a 1302-byte packet row is one work item
+// (program.h TAMD_SLICE_BYTES_X; chosen by Device::init, tonk_amd::slice_bytes()).
+TAMD_EXEC_KERNEL(tamd_exec24, 3, 5)
 
 // GF self test: out[y * 256 + x] = x * y through the same v_perm path the executor uses.
 extern "C" __global__ void tamd_gf_selftest(const uint32_t* __restrict__ gf_perm, uint8_t* __restrict__ out) {

@@ -38,8 +38,11 @@
 #include <stdint.h>
 
 #define TAMD_ROW_UNIT 64u
-/* A work item (one wave) covers one 1024-byte slice of an op (16 B per lane, tamd_exec16). */
+/* A work item (one wave) covers one slice of an op: 1536 bytes (16 + 8 B per lane, tamd_exec24,
+   the default: a packet row of up to 1536 bytes is one item) or 1024 bytes (16 B per lane,
+   tamd_exec16; TONK_AMD_SLICE=1024). */
 #define TAMD_SLICE_BYTES 1024u
+#define TAMD_SLICE_BYTES_X 1536u
 
 enum tamd_instr_kind {
     TAMD_I_ACC    = 1,

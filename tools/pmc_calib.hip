@@ -41,6 +41,34 @@ extern "C" __global__ void calib_write16(u64x2* __restrict__ dst, size_t n_pairs
     }
 }
 
+// tamd_exec24's pattern: one wave per 1344-byte row, 16 B per lane over its first 1024 bytes and
+// 8 B per lane over bytes 1024..1535 (lanes past the row's 1302 bytes re-read its first bytes).
+extern "C" __global__ void calib_read_row24(const unsigned char* __restrict__ src, size_t n_rows, u64* __restrict__ sink) {
+    const uint32_t lane = threadIdx.x & 63u;
+    u64 acc = 0;
+    for (size_t r = (size_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64; r < n_rows; r += (size_t)gridDim.x * (blockDim.x / 64)) {
+        const unsigned char* row = src + r * 1344;
+        const u64x2 v = *(const u64x2*)(row + lane * 16u);
+        const uint32_t ox = 1024u + lane * 8u;
+        const u64 w = *(const u64*)(row + (ox < 1302u ? ox : 0u));
+        acc ^= v.x ^ v.y ^ w;
+    }
+    if (acc == 0x123456789abcdefull) sink[0] = acc;
+}
+
+extern "C" __global__ void calib_write_row24(unsigned char* __restrict__ dst, size_t n_rows) {
+    const uint32_t lane = threadIdx.x & 63u;
+    for (size_t r = (size_t)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64; r < n_rows; r += (size_t)gridDim.x * (blockDim.x / 64)) {
+        unsigned char* row = dst + r * 1344;
+        u64x2 v;
+        v.x = r;
+        v.y = ~r;
+        *(u64x2*)(row + lane * 16u) = v;
+        const uint32_t ox = 1024u + lane * 8u;
+        if (ox < 1344u) *(u64*)(row + ox) = r ^ lane;
+    }
+}
+
 int main() {
     const size_t read_bytes = 2ull << 30, write_bytes = 1ull << 30;
     u64 *src = nullptr, *dst = nullptr, *sink = nullptr;
@@ -55,9 +83,12 @@ int main() {
         hipLaunchKernelGGL(calib_write8, dim3(4096), dim3(256), 0, 0, dst, write_bytes / 8);
         hipLaunchKernelGGL(calib_read16, dim3(4096), dim3(256), 0, 0, (const u64x2*)src, read_bytes / 16, sink);
         hipLaunchKernelGGL(calib_write16, dim3(4096), dim3(256), 0, 0, (u64x2*)dst, write_bytes / 16);
+        hipLaunchKernelGGL(calib_read_row24, dim3(4096), dim3(256), 0, 0, (const unsigned char*)src, read_bytes / 1344, sink);
+        hipLaunchKernelGGL(calib_write_row24, dim3(4096), dim3(256), 0, 0, (unsigned char*)dst, write_bytes / 1344);
     }
     (void)hipDeviceSynchronize();
-    printf("{\"calib_read_bytes\": %zu, \"calib_write_bytes\": %zu}\n", read_bytes, write_bytes);
+    printf("{\"calib_read_bytes\": %zu, \"calib_write_bytes\": %zu, \"row24_read_bytes\": %zu, \"row24_write_bytes\": %zu}\n",
+           read_bytes, write_bytes, (read_bytes / 1344) * 1302, (write_bytes / 1344) * 1344);
     (void)hipFree(src);
     (void)hipFree(dst);
     (void)hipFree(sink);

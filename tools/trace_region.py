@@ -3,13 +3,13 @@ kernel trace (--kernel-trace --output-format csv).  The region is delimited by t
 tamd_timed_region dispatches that Device::set_timing launches, so the figure covers the same
 launches as the bench's own event timing (roofline.avg_launch_us).
 
-usage: python tools/trace_region.py run_kernel_trace.csv [kernel=tamd_exec16]"""
+usage: python tools/trace_region.py run_kernel_trace.csv [kernel=tamd_exec24]"""
 import csv
 import json
 import sys
 
 
-def region_stats(path: str, kernel: str = "tamd_exec16") -> dict:
+def region_stats(path: str, kernel: str = "tamd_exec24") -> dict:
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     marks = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith("tamd_timed_region")]
     if len(marks) < 2:
@@ -22,4 +22,4 @@ def region_stats(path: str, kernel: str = "tamd_exec16") -> dict:
 
 
 if __name__ == "__main__":
-    print(json.dumps(region_stats(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "tamd_exec16")))
+    print(json.dumps(region_stats(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "tamd_exec24")))
