@@ -177,6 +177,15 @@ __device__ __forceinline__ LV<NH> lv_load(const uint8_t* p, const uint8_t* px = 
     }
     return r;
 }
+// The same from a wave-uniform row base and the lane's offsets (scalar-base addressing).
+template <int NH>
+__device__ __forceinline__ LV<NH> lv_load_at(const uint8_t* base, uint32_t off, uint32_t offx) {
+    // (the empty asm keeps the 32-bit offsets from being widened once outside the loop, which
+    // would turn every load into a 64-bit per-lane address add)
+    asm volatile("" : "+v"(off));
+    if constexpr (NH == 3) asm volatile("" : "+v"(offx));
+    return lv_load<NH>(base + off, base + offx);
+}
 template <int NH>
 __device__ __forceinline__ void lv_store(uint8_t* p, const LV<NH>& v) {
     if constexpr (NH == 1) {
@@ -254,11 +263,14 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
     const uint32_t mode = (a.w0 >> 8) & 0xffu, p = (a.w0 >> 16) & 0xffu;
     const uint32_t row0 = a.row, len = a.len, count = a.cap;
     const uint32_t stride = r.row, col0 = r.len, cstep = r.cap;
-    const uint8_t* src = arena + (size_t)row0 * TAMD_ROW_UNIT + load_off<FULL>(o, len);
-    const uint8_t* srcx = arena + (size_t)row0 * TAMD_ROW_UNIT + (NH == 3 ? load_off<false>(ox, len) : 0u);
+    // a row's address: a wave-uniform base (SGPRs) plus the lane's 32-bit offsets, so the loads
+    // use the scalar-base addressing mode and no 64-bit per-lane address math per row
+    const uint8_t* rbase = arena + (size_t)row0 * TAMD_ROW_UNIT;
+    const uint32_t lo = load_off<FULL>(o, len), lox = NH == 3 ? load_off<false>(ox, len) : 0u;
     const size_t step = (size_t)stride * TAMD_ROW_UNIT;
+#define TAMD_RUN_LD(idx) lv_load_at<NH>(rbase + (size_t)(idx) * step, lo, lox)
     // loads past the run's end re-read its last row (never consumed)
-#define TAMD_RUN_ROW(q) lv_load<NH>(src + (size_t)min(e + (q), count - 1u) * step, srcx + (size_t)min(e + (q), count - 1u) * step)
+#define TAMD_RUN_ROW(q) TAMD_RUN_LD(min(e + (q), count - 1u))
     if (mode == TAMD_R_LANE3) {
         // byte offset of the (cx, cx^2) tables in the lane table: 48 bytes per column value index
         const uint32_t W = 253u * 48u;
@@ -271,7 +283,7 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
             constexpr uint32_t H = TAMD_RBATCH / 2;
             LV<NH> d[TAMD_RBATCH];
 #pragma unroll
-            for (uint32_t q = 0; q < TAMD_RBATCH; ++q) d[q] = lv_load<NH>(src + (size_t)min(q, count - 1u) * step, srcx + (size_t)min(q, count - 1u) * step);
+            for (uint32_t q = 0; q < TAMD_RBATCH; ++q) d[q] = TAMD_RUN_LD(min(q, count - 1u));
             for (uint32_t e = 0; e < count; e += TAMD_RBATCH) {
                 const bool more = e + TAMD_RBATCH < count;
 #pragma unroll
@@ -289,7 +301,7 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
                     if (more) {
 #pragma unroll
                         for (uint32_t q = h * H; q < (h ? TAMD_RBATCH : H); ++q)
-                            d[q] = lv_load<NH>(src + (size_t)min(e + TAMD_RBATCH + q, count - 1u) * step, srcx + (size_t)min(e + TAMD_RBATCH + q, count - 1u) * step);
+                            d[q] = TAMD_RUN_LD(min(e + TAMD_RBATCH + q, count - 1u));
                     }
                 }
             }
@@ -333,7 +345,7 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
         constexpr uint32_t H = TAMD_RBATCH / 2;
         LV<NH> d[TAMD_RBATCH];
 #pragma unroll
-        for (uint32_t q = 0; q < TAMD_RBATCH; ++q) d[q] = lv_load<NH>(src + (size_t)min(q, count - 1u) * step, srcx + (size_t)min(q, count - 1u) * step);
+        for (uint32_t q = 0; q < TAMD_RBATCH; ++q) d[q] = TAMD_RUN_LD(min(q, count - 1u));
 #define TAMD_MULTI_TARGET(l, h, k, x, acc)                                                 \
     if (i - l < h) {                                                                       \
         if (k) acc ^= v;                                                                   \
@@ -357,7 +369,7 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
                 if (more) {
 #pragma unroll
                     for (uint32_t q = h * H; q < (h ? TAMD_RBATCH : H); ++q)
-                        d[q] = lv_load<NH>(src + (size_t)min(e + TAMD_RBATCH + q, count - 1u) * step, srcx + (size_t)min(e + TAMD_RBATCH + q, count - 1u) * step);
+                        d[q] = TAMD_RUN_LD(min(e + TAMD_RBATCH + q, count - 1u));
                 }
             }
         }
@@ -373,7 +385,7 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
             constexpr uint32_t H = TAMD_RBATCH / 2;
             LV<NH> d[TAMD_RBATCH];
 #pragma unroll
-            for (uint32_t q = 0; q < TAMD_RBATCH; ++q) d[q] = lv_load<NH>(src + (size_t)min(q, count - 1u) * step, srcx + (size_t)min(q, count - 1u) * step);
+            for (uint32_t q = 0; q < TAMD_RBATCH; ++q) d[q] = TAMD_RUN_LD(min(q, count - 1u));
             for (uint32_t e = 0; e < count; e += TAMD_RBATCH) {
                 const bool more = e + TAMD_RBATCH < count;
 #pragma unroll
@@ -388,7 +400,7 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
                     if (more) {
 #pragma unroll
                         for (uint32_t q = h * H; q < (h ? TAMD_RBATCH : H); ++q)
-                            d[q] = lv_load<NH>(src + (size_t)min(e + TAMD_RBATCH + q, count - 1u) * step, srcx + (size_t)min(e + TAMD_RBATCH + q, count - 1u) * step);
+                            d[q] = TAMD_RUN_LD(min(e + TAMD_RBATCH + q, count - 1u));
                     }
                 }
             }
@@ -422,7 +434,7 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
             LV<NH> d[TAMD_RBATCH];
             LV<NH> x = lv_zero<NH>();
 #pragma unroll
-            for (uint32_t q = 0; q < TAMD_RBATCH; ++q) d[q] = lv_load<NH>(src + (size_t)min(q, count - 1u) * step, srcx + (size_t)min(q, count - 1u) * step);
+            for (uint32_t q = 0; q < TAMD_RBATCH; ++q) d[q] = TAMD_RUN_LD(min(q, count - 1u));
             for (uint32_t e = 0; e < count; e += TAMD_RBATCH) {
                 const bool more = e + TAMD_RBATCH < count;
 #pragma unroll
@@ -433,7 +445,7 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
                     if (more) {
 #pragma unroll
                         for (uint32_t q = h * H; q < (h ? TAMD_RBATCH : H); ++q)
-                            d[q] = lv_load<NH>(src + (size_t)min(e + TAMD_RBATCH + q, count - 1u) * step, srcx + (size_t)min(e + TAMD_RBATCH + q, count - 1u) * step);
+                            d[q] = TAMD_RUN_LD(min(e + TAMD_RBATCH + q, count - 1u));
                     }
                 }
             }
@@ -454,6 +466,7 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
         }
     }
 #undef TAMD_RUN_ROW
+#undef TAMD_RUN_LD
 }
 
 // One work item: the op's instruction list over this wave's slice.  FULL items lie below every
@@ -495,10 +508,10 @@ __device__ __forceinline__ LV<NH> run_item(const tamd_instr* __restrict__ instrs
         for (uint32_t j = 0; j < TAMD_BATCH; ++j) {
             const uint32_t kind = in[j].w0 & 0xffu;
             const bool ld = j < nb && (kind == TAMD_I_ACC || kind == TAMD_I_ACC3);
-            const uint8_t* rp = arena + (size_t)in[j].row * TAMD_ROW_UNIT;
-            const uint8_t* p = ld ? rp + load_off<FULL>(o, in[j].len) : zrow + laneb;
-            const uint8_t* px = NH < 3 ? p : ld ? rp + load_off<false>(ox, in[j].len) : zrow + (laneb >> 1);
-            v[j] = lv_load<NH>(p, px);
+            const uint8_t* rp = ld ? arena + (size_t)in[j].row * TAMD_ROW_UNIT : zrow;  // wave-uniform
+            const uint32_t lo = ld ? load_off<FULL>(o, in[j].len) : laneb;
+            const uint32_t lox = NH < 3 ? 0u : ld ? load_off<false>(ox, in[j].len) : (laneb >> 1);
+            v[j] = lv_load_at<NH>(rp, lo, lox);
         }
 #pragma unroll
         for (uint32_t j = 0; j < TAMD_BATCH; ++j) {
