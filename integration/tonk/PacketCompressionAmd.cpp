@@ -11,7 +11,7 @@
 // oracle/tonk.mk links Tonk's unit_tests with this file (unit_tests_amd_lz).
 #include "PacketCompression.h"
 
-#include "../../include/tonk_compress.h"
+#include "tonk_compress.h"  // include/ (oracle/tonk.mk: -I../include)
 
 #include <string.h>
 
