@@ -610,6 +610,13 @@ def main() -> int:
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    # With several ranks, gloo's connection messages go to stdout from C++ (fd 1); the bench line
+    # keeps the real stdout to itself and everything else that writes to fd 1 goes to stderr.
+    line_out = sys.stdout
+    if world > 1:
+        sys.stdout.flush()
+        line_out = os.fdopen(os.dup(1), "w")
+        os.dup2(2, 1)
 
     if a.workload == "compress":  # SURVEY s8(f)4 side line (not the headline)
         if world > 1:
@@ -642,7 +649,8 @@ def main() -> int:
         if rank == 0:
             print(json.dumps({"dry_run": True, "n_gpus": world, "streams_per_gpu": STREAMS_PER_GPU,
                               "ranks": [{"rank": int(v[1]), "local_rank": int(v[2]), "stream_base": int(v[0]),
-                                         "host_cores": unpad_cores(v[3:])} for v in bases]}), flush=True)
+                                         "host_cores": unpad_cores(v[3:])} for v in bases]}), file=line_out,
+                  flush=True)
         d.close()
         return 0
 
@@ -650,7 +658,12 @@ def main() -> int:
     total_steps = a.warmup + a.steps
     n_orig = total_steps * ORIGINALS_PER_STEP * PROGRAMS_PER_STEP
     wp = tonk_amd.WorkloadParams(n=n_orig, payload=PAYLOAD, loss=loss, ack=ACK)
-    sess = tonk_amd.Session(wp, n_streams=STREAMS_PER_GPU, device=local_rank,
+    # TONK_AMD_BENCH_DEVICE: every rank on this device -- a rehearsal of the N-rank path on a
+    # one-GPU box (the ranks then share one GPU and its host cores: not a scaling measurement)
+    device = int(os.environ.get("TONK_AMD_BENCH_DEVICE", local_rank))
+    if "TONK_AMD_BENCH_DEVICE" in os.environ and local_world > 1 and "TONK_AMD_CPU_SLOT" not in os.environ:
+        os.environ["TONK_AMD_CPU_SLOT"] = f"{local_rank}/{local_world}"  # (disjoint cores all the same)
+    sess = tonk_amd.Session(wp, n_streams=STREAMS_PER_GPU, device=device,
                             stream_base=stream_base(rank), threads=threads,
                             arena_bytes=(2 * n_orig * STREAMS_PER_GPU * 1344) + (4 << 30))
     sess.generate()
@@ -753,14 +766,14 @@ def main() -> int:
     if rank == 0 and not a.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(min(host_cpus(), threads * local_world))
     if rank == 0 and world == 1 and not a.no_end_to_end:
-        out["end_to_end"] = end_to_end(threads, local_rank, loss)
+        out["end_to_end"] = end_to_end(threads, device, loss)
     if rank == 0 and a.workload == "cfg3" and not a.no_verify:
-        v = verify_schedule(threads, local_rank)
+        v = verify_schedule(threads, device)
         out["checks"]["digests_match"] = v["digests_match"]
         out["checks"]["verify"] = v
     d.barrier()
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        print(json.dumps(out), file=line_out, flush=True)
     d.close()
     return 0 if all_ok and out["checks"].get("digests_match") is not False else 1
 

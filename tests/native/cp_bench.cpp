@@ -13,6 +13,7 @@
 #include <sys/time.h>
 #include <ucontext.h>
 #include <memory>
+#include <malloc.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -205,6 +206,15 @@ int main(int argc, char** argv) {
         if (k == "backsub") { backsub = (uint32_t)strtoul(eq + 1, nullptr, 0); continue; }
         if (k == "pipe") { g_pipe = atoi(eq + 1); continue; }
         if (k == "reps") { reps = (uint32_t)atoi(eq + 1); continue; }  // level pipelining as the session runs it
+        if (k == "prefault") {  // MB of heap faulted in and kept before the run (cold-start studies)
+            const size_t mb = (size_t)atoi(eq + 1);
+            mallopt(M_MMAP_THRESHOLD, 512 << 20);
+            mallopt(M_TRIM_THRESHOLD, 1 << 30);
+            void* m = malloc(mb << 20);
+            if (m) memset(m, 1, mb << 20);
+            free(m);
+            continue;
+        }
         const unsigned long long v = strtoull(eq + 1, nullptr, 0);
         if (k == "streams") streams = (uint32_t)v;
         else if (k == "n") p.n_originals = (uint32_t)v;

@@ -64,9 +64,9 @@ def test_bench_gpus_flag_spawns_ranks():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
                        capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
-    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1, r.stdout          # rank 0 prints the one line
-    j = json.loads(lines[0])
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, r.stdout          # rank 0 prints the one line, and nothing else reaches stdout
+    j = json.loads(lines[0])                  # (gloo's connection messages go to stderr)
     assert j["n_gpus"] == 2
     ranks = j["ranks"]
     assert [x["rank"] for x in ranks] == [0, 1] and [x["local_rank"] for x in ranks] == [0, 1]
