@@ -667,15 +667,16 @@ bool Decoder::generate_matrix() {
         prng.seed(m.Row, m.LDPCCount);
         const uint32_t es = rec->element_start;
         const uint32_t pairs = (m.LDPCCount + kPairRate - 1) / kPairRate;
+        const FastMod ldpc_mod(m.LDPCCount);
         for (uint32_t k = 0; k < pairs; ++k) {
-            const uint32_t e1 = es + prng.next() % m.LDPCCount;
+            const uint32_t e1 = es + ldpc_mod(prng.next());
             const StoredOriginal& o1 = elem(e1);
             if (o1.bytes <= 0) {
                 const uint32_t mc = o1.column;
                 if (mc >= columns) { disabled_ = true; return false; }
                 if (mc >= start_col) mat(i, mc) ^= 1;
             }
-            const uint32_t erx = es + prng.next() % m.LDPCCount;
+            const uint32_t erx = es + ldpc_mod(prng.next());
             const StoredOriginal& orx = elem(erx);
             if (orx.bytes <= 0) {
                 const uint32_t mc = orx.column;
@@ -1069,11 +1070,12 @@ bool Decoder::eliminate_original_data() {
             Pcg32 prng;
             prng.seed(m.Row, m.LDPCCount);
             const uint32_t pairs = (m.LDPCCount + kPairRate - 1) / kPairRate;
+            const FastMod ldpc_mod(m.LDPCCount);
             for (uint32_t i = 0; i < pairs; ++i) {
-                const uint32_t e1 = es + prng.next() % m.LDPCCount;
+                const uint32_t e1 = es + ldpc_mod(prng.next());
                 const StoredOriginal& o1 = elem(e1);
                 if (o1.bytes > 0) read_original(o1, o1.bytes < rbytes ? o1.bytes : rbytes, 1, buf);
-                const uint32_t erx = es + prng.next() % m.LDPCCount;
+                const uint32_t erx = es + ldpc_mod(prng.next());
                 const StoredOriginal& orx = elem(erx);
                 if (orx.bytes > 0) read_original(orx, orx.bytes < rbytes ? orx.bytes : rbytes, rx, buf);
             }

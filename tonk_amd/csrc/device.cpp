@@ -398,15 +398,13 @@ bool Device::add_part(int h, const ProgramBuilder& pb, Part& out) {
     } else {
         for (size_t b = 0; b < li.size(); ++b) cur[b] = out.bucket_start[b];
     }
-    const uint32_t sb = slice_bytes();
     uint64_t* it = out.items.data();
     for (uint32_t i = 0; i < no; ++i) {
         tamd_op op = ops[i];
         op.first += base;
         od[i] = op;
         const uint64_t rec = base + ni + i;
-        uint32_t slices = (op.span + sb - 1) / sb;
-        if (!slices) slices = 1;
+        const uint32_t slices = op_slices(op.span);
         uint32_t& c = cur[lv[i]];
         for (uint32_t k = 0; k < slices; ++k) it[c++] = rec | ((uint64_t)k << 32);
     }
@@ -637,15 +635,13 @@ void Device::fill(size_t c) {
     }
     const std::vector<tamd_op>& ops = pb.ops();
     const std::vector<uint32_t>& lv = pb.op_levels();
-    const uint32_t sb = slice_bytes();
     for (size_t i = 0; i < ops.size(); ++i) {
         const uint32_t l = lv[i];
         tamd_op op = ops[i];
         op.first += ibase;
         const uint32_t oi = of[l]++;
         ho[oi] = op;
-        uint32_t slices = (op.span + sb - 1) / sb;
-        if (!slices) slices = 1;
+        const uint32_t slices = op_slices(op.span);
         uint32_t ii = itf[l];
         itf[l] += slices;
         for (uint32_t s = 0; s < slices; ++s, ++ii) {

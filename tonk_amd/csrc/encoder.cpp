@@ -712,9 +712,10 @@ void Encoder::add_light(uint32_t row, Sym& rec) {
     const size_t at = rec.size();
     rec.resize(at + 2 * (size_t)pairs);
     Term* t = rec.data() + at;
+    const FastMod mod(count);
     for (uint32_t i = 0; i < pairs; ++i) {
-        const uint32_t e1 = start + prng.next() % count;
-        const uint32_t erx = start + prng.next() % count;
+        const uint32_t e1 = start + mod(prng.next());
+        const uint32_t erx = start + mod(prng.next());
         const StoredOriginal& o1 = win_[e1];
         const StoredOriginal& orx = win_[erx];
         t[2 * i] = Term{o1.row, o1.bytes, 1};

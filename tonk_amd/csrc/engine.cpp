@@ -335,10 +335,8 @@ uint32_t ProgramBuilder::end_op(uint32_t min_level) {
         level_ops_.resize(TAMD_COST_CLASSES * (level + 1), 0);
         level_items_.resize(TAMD_COST_CLASSES * (level + 1), 0);
     }
-    const uint32_t sb = slice_bytes();
-    const uint32_t slices = (op.span + sb - 1) / sb;
     level_ops_[bucket]++;
-    level_items_[bucket] += slices ? slices : 1;
+    level_items_[bucket] += op_slices(op.span);
     for (size_t i = cur_written_begin_; i < written_.size(); ++i) rows_->set_level(written_[i], level);
     if (level > max_level_) max_level_ = level;
     return level;

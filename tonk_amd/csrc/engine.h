@@ -67,6 +67,12 @@ typedef std::vector<tamd_instr, NoInitAlloc<tamd_instr>> InstrVec;
 // TONK_AMD_SLICE=1024 selects TAMD_SLICE_BYTES (tamd_exec16); fixed for the process.
 extern const uint32_t g_slice_bytes;
 inline uint32_t slice_bytes() { return g_slice_bytes; }
+// Work items of an op spanning `span` bytes (at least one): constant divisors, no division.
+inline uint32_t op_slices(uint32_t span) {
+    const uint32_t n = g_slice_bytes == TAMD_SLICE_BYTES_X ? (span + TAMD_SLICE_BYTES_X - 1) / TAMD_SLICE_BYTES_X
+                                                            : (span + TAMD_SLICE_BYTES - 1) / TAMD_SLICE_BYTES;
+    return n ? n : 1u;
+}
 
 // ---------------------------------------------------------------------------------------------
 // Arena bookkeeping: rows are contiguous ranges of 64-byte units in one device allocation.

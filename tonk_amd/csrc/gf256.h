@@ -91,4 +91,14 @@ struct Pcg32 {
     }
 };
 
+// x mod d for a divisor fixed over many draws (the LDPC pair columns, `next() % count`): two
+// multiplications instead of a division, exact for every 32-bit x and d > 0 (Lemire, Kaser &
+// Kurz, "Faster remainder by direct computation", 2019).
+struct FastMod {
+    uint64_t m;
+    uint32_t d;
+    explicit FastMod(uint32_t divisor) : m(divisor ? ~0ull / divisor + 1 : 0), d(divisor) {}  // (d = 0: never called)
+    uint32_t operator()(uint32_t x) const { return (uint32_t)(((unsigned __int128)(m * x) * d) >> 64); }
+};
+
 } // namespace tamd
