@@ -35,6 +35,44 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+
+def _hugepage_heap_relaunch() -> None:
+    """Run the bench in a child process whose glibc heap uses transparent huge pages
+    (GLIBC_TUNABLES=glibc.malloc.hugetlb=1: madvise(MADV_HUGEPAGE) on malloc's arenas; the
+    GPU boxes run THP in "madvise" mode).  The host control plane walks per-stream windows,
+    row tables and term lists spread over the heap; with 2 MB pages it costs 9 % less CPU per
+    original on one core of the box (profiles/r03e_cp_hugetlb_ab.txt).  A tunable is read only
+    at process start, hence the child; it dies with this process (PR_SET_PDEATHSIG), and this
+    process touches no GPU and exits with the child's code.  TONK_AMD_HUGEPAGE_HEAP=0 runs
+    in-process as before; a process under a profiler (rocprofv3's preload) is never relaunched."""
+    if os.environ.get("TONK_AMD_HUGEPAGE_HEAP", "1") == "0" or not sys.platform.startswith("linux"):
+        return
+    tun = os.environ.get("GLIBC_TUNABLES", "")
+    if "glibc.malloc.hugetlb" in tun or "rocprof" in os.environ.get("LD_PRELOAD", "") or \
+            any(k.startswith("ROCPROF") for k in os.environ):
+        return
+    import ctypes
+    import signal
+    libc = ctypes.CDLL(None, use_errno=True)
+
+    def die_with_parent() -> None:
+        libc.prctl(1, int(signal.SIGKILL))  # PR_SET_PDEATHSIG
+
+    env = dict(os.environ, GLIBC_TUNABLES=(tun + ":" if tun else "") + "glibc.malloc.hugetlb=1")
+    child = subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                             preexec_fn=die_with_parent)
+    while True:
+        try:
+            rc = child.wait()
+            break
+        except KeyboardInterrupt:
+            child.send_signal(signal.SIGINT)
+    sys.exit(rc if rc >= 0 else 128 - rc)
+
+
+if __name__ == "__main__":
+    _hugepage_heap_relaunch()
+
 import tonk_amd  # noqa: E402
 
 METRIC = "Siamese FEC encode+decode GiB/s (device-resident), 1/2/4/8 MI355X"
