@@ -657,22 +657,48 @@ void Device::launch_step(Inflight* fresh, unsigned long long* stamps) {
     tamd_segments sg;
     memset(&sg, 0, sizeof(sg));
     uint32_t cnt = 0, coop = 0;
+    uint32_t seg_level[TAMD_MAX_SEGMENTS], seg_coop[TAMD_MAX_SEGMENTS];
     auto add = [&](Inflight& p) {
         if (p.done()) return;
         const uint32_t l = p.next++;
         const uint32_t c = p.level_items[l];
         if (!c) return;
+        seg_level[sg.n] = l;
+        seg_coop[sg.n] = p.level_coop[l];
         tamd_segment& g = sg.s[sg.n++];
         g.ops = p.ops;
         g.instrs = p.instrs;
         g.items = p.items + 8u * p.item_base[l];
         g.count = c;
-        if (sg.n == 1) coop = p.level_coop[l];
         cnt += c;
     };
     for (Inflight& p : progs_) add(p);
     if (fresh) add(*fresh);
     if (!cnt) return;
+    // Segment order = the order waves claim items in (A/B, TONK_AMD_SEG_ORDER): 0 programs
+    // oldest first (deepest level first, the new program's level 1 last); 1 level 2, level 1,
+    // then the rest; 2 level 1, level 2, then the rest; 3 the rest, then level 1, then level 2.
+    static const int seg_order = getenv("TONK_AMD_SEG_ORDER") ? atoi(getenv("TONK_AMD_SEG_ORDER")) : 0;
+    if (seg_order && sg.n > 1) {
+        static const uint32_t rank_of[4][3] = {{0, 0, 0}, {1, 0, 2}, {0, 1, 2}, {1, 2, 0}};  // [order][L1, L2, rest]
+        tamd_segment tmp[TAMD_MAX_SEGMENTS];
+        uint32_t tl[TAMD_MAX_SEGMENTS], tc[TAMD_MAX_SEGMENTS], m = 0;
+        for (uint32_t pass = 0; pass < 3; ++pass)
+            for (uint32_t k = 0; k < sg.n; ++k) {
+                const uint32_t cls = seg_level[k] == 1 ? 0u : seg_level[k] == 2 ? 1u : 2u;
+                if (rank_of[seg_order & 3][cls] != pass) continue;
+                tmp[m] = sg.s[k];
+                tl[m] = seg_level[k];
+                tc[m] = seg_coop[k];
+                ++m;
+            }
+        for (uint32_t k = 0; k < sg.n; ++k) {
+            sg.s[k] = tmp[k];
+            seg_level[k] = tl[k];
+            seg_coop[k] = tc[k];
+        }
+    }
+    coop = seg_coop[0];
     hipStream_t st = (hipStream_t)stream_;
     uint32_t grid = (cnt + 3) / 4;
     if (grid > max_grid_) grid = max_grid_;
