@@ -721,6 +721,8 @@ def main() -> int:
     sess.wait()
     t1 = time.perf_counter()
     host_env = env.report()
+    host_env["heap"] = "glibc hugetlb (THP)" if "glibc.malloc.hugetlb=1" in os.environ.get("GLIBC_TUNABLES", "") \
+        else "glibc default"
     d.barrier()
     sess.set_timing(False)
     kernel_ms, launches = sess.kernel_ms()
