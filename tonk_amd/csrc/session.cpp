@@ -1236,6 +1236,7 @@ int tamd_session_generate(void* sp) {
         Stream& st = *s->streams[si];
         std::vector<Device::GenDesc>& d = per[si];
         const uint32_t n = st.p.n_originals;
+        st.runner->pregenerate();  // the stream's loss draws (scenario generation, untimed)
         st.enc_rows.assign(n, kNoRow);
         st.dec_rows.assign(n, kNoRow);
         d.reserve(2 * (size_t)n);

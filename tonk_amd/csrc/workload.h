@@ -125,12 +125,67 @@ inline uint64_t fnv1a(const uint8_t* d, size_t n, uint64_t h = 14695981039346656
     return h;
 }
 
+// The loss process is a fixed sequence of draws (one per packet sent through the channel, in
+// send order).  The draws are generated ahead, as a bitmap (bit i: draw i is a loss), so that
+// scenario generation stays outside a timed region ("timer around the API calls
+// only") and a run of delivered originals is found a 64-bit word at a time.  Draws past the
+// generated ones are produced on demand, continuing the same PCG sequence: the channel's answers
+// never depend on how far ahead it was generated.
 struct LossChannel {
     Pcg rng;
     bool bad = false;
     const Params* p = nullptr;
-    void init(const Params& prm) { p = &prm; rng.seed(prm.seed_loss, 0); bad = false; }
+    std::vector<uint64_t> bits;
+    uint64_t pos = 0, avail = 0;  // next draw; draws generated
+    void init(const Params& prm) {
+        p = &prm;
+        rng.seed(prm.seed_loss, 0);
+        bad = false;
+        bits.clear();
+        pos = avail = 0;
+    }
+    // Generate draws up to `n` (at least).
+    void generate(uint64_t n) {
+        n = (n + 63) & ~63ull;
+        if (n <= avail) return;
+        bits.resize(n / 64, 0);
+        for (uint64_t i = avail; i < n; i += 64) {
+            uint64_t w = 0;
+            for (unsigned b = 0; b < 64; ++b) w |= (uint64_t)draw() << b;
+            bits[i / 64] = w;
+        }
+        avail = n;
+    }
     bool lost() {
+        if (pos >= avail) generate(avail + 4096);
+        const bool l = (bits[pos >> 6] >> (pos & 63)) & 1u;
+        ++pos;
+        return l;
+    }
+    // Consume the next draws up to and including the first loss among the next `kmax`: returns
+    // its index (< kmax), or kmax when all kmax are deliveries (kmax draws consumed).
+    uint32_t first_lost(uint32_t kmax) {
+        if (pos + kmax > avail) generate(pos + kmax + 4096);
+        uint64_t at = pos;
+        const uint64_t end = pos + kmax;
+        while (at < end) {
+            const uint64_t w = bits[at >> 6] >> (at & 63);
+            if (w) {
+                const uint64_t hit = at + (uint64_t)__builtin_ctzll(w);
+                if (hit < end) {
+                    pos = hit + 1;
+                    return (uint32_t)(hit - (end - kmax));
+                }
+                break;
+            }
+            at = (at | 63) + 1;
+        }
+        pos = end;
+        return kmax;
+    }
+
+private:
+    bool draw() {
         const uint32_t u = rng.next();
         if (!p->ge_enable) return u < p->loss_thresh;
         if (bad) { if (u < p->bg_thresh) bad = false; }
@@ -187,6 +242,12 @@ public:
 
     uint32_t position() const { return next_; }
     const Summary& summary() const { return s_; }
+    // Scenario generation, done before any timed region: the loss draws of the originals and of
+    // the recovery packets sent with them (the channel continues the sequence on demand past it).
+    void pregenerate() {
+        const uint64_t rec = (uint64_t)p_.n_originals * p_.fec_rate_q16 / 65536u;
+        ch_.generate((uint64_t)p_.n_originals + 2 * rec + 1024);
+    }
 
     // Feed the next `n` originals (and everything they trigger).  Runs of originals that trigger
     // nothing (delivered, no recovery packet, acknowledgement, retransmission or ARQ due after
@@ -325,13 +386,9 @@ private:
             const uint32_t room = due > next_ ? due - next_ : 0;
             if (room < kmax) kmax = room;
         }
-        for (uint32_t j = 0; j < kmax; ++j) {
-            if (ch_.lost()) {
-                drawn_next = 1;
-                return j;
-            }
-        }
-        return kmax;
+        const uint32_t j = ch_.first_lost(kmax);
+        if (j < kmax) drawn_next = 1;
+        return j;
     }
 
     // k quiet originals from index i0 (every channel draw already made: all delivered).
