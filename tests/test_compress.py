@@ -319,3 +319,38 @@ def test_gpu_compress_batch_large_messages():
             blk = out_h[i * max_bytes:i * max_bytes + w].tobytes() if w else b""
             assert dec.feed(blk, m) == m, (s, k)
     assert big >= n_streams * n_msgs // 6
+
+
+@pytest.mark.gpu
+def test_gpu_compressor_concurrent_callers():
+    """Several threads, each with its own compressor, call the synchronous per-message API at the
+    same time (Tonk's connection threads): the calls are combined into shared launches, a leader
+    hands leadership on once its own message is done, and every stream is restored in order by
+    its own reference decompressor."""
+    import threading
+    from tonk_amd.compress import MessageCompressor
+    L = ref_lib()
+    n_threads, n_msgs = 8, 150
+    streams = [mixed_messages(n_msgs, 300 + t) for t in range(n_threads)]
+    blocks = [[None] * n_msgs for _ in range(n_threads)]
+    errors = []
+
+    def worker(t):
+        try:
+            comp = MessageCompressor(MAX)
+            for k, m in enumerate(streams[t]):
+                blocks[t][k] = comp.compress(m)
+        except Exception as e:  # (surfaced below)
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(n_threads)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=120)
+    assert not any(x.is_alive() for x in th), "a compressor call did not return"
+    assert not errors, errors
+    for t in range(n_threads):
+        dec = RefDecompressor(L)
+        for k, m in enumerate(streams[t]):
+            assert dec.feed(blocks[t][k], m) == m, (t, k)

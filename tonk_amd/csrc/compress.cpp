@@ -165,9 +165,9 @@ bool grow(uint8_t*& h, uint8_t*& d, size_t& cap, size_t need) {
 
 // Runs one batch (leader, no lock held); every request of `b` belongs to device b[0]->c->device
 // and names a distinct compressor.
-void run_batch(const std::vector<LzRequest*>& b) {
+void run_batch(const std::vector<LzRequest*>& in) {
     LzBatchState& S = g_batch;
-    const int dev = b[0]->c->device;
+    const int dev = in[0]->c->device;
     bool ok = hipSetDevice(dev) == hipSuccess;
     if (ok && S.device != dev) {  // (a process compresses on one device in practice)
         if (S.st) hipStreamDestroy(S.st);
@@ -177,17 +177,31 @@ void run_batch(const std::vector<LzRequest*>& b) {
     }
     const uint8_t* fse = ok ? device_fse(dev) : nullptr;
     ok = ok && fse;
+    // A compressor whose device ring cannot be allocated fails on its own (rc -2, sticky) and is
+    // left out of the launch: nothing is ever placed into a null ring.
+    std::vector<LzRequest*> live;
+    live.reserve(in.size());
+    for (LzRequest* r : in) {
+        if (ok && !r->c->ring && !r->c->failed) {
+            uint8_t* ring = nullptr;
+            if (hipMalloc((void**)&ring, TAMD_LZ_RING + TAMD_LZ_MIRROR) != hipSuccess) r->c->failed = true;
+            else r->c->ring = ring;
+        }
+        if (ok && r->c->ring && !r->c->failed) {
+            live.push_back(r);
+        } else {
+            if (ok) r->c->failed = true;
+            r->rc = -2;
+        }
+    }
+    if (ok && live.empty()) return;
+    const std::vector<LzRequest*>& b = ok ? live : in;
     const size_t n = b.size();
     size_t data_bytes = 0, out_bytes = 0, scratch_bytes = 0;
     for (LzRequest* r : b) {
         data_bytes += align16(r->bytes);
         out_bytes += align16(r->c->max);
         if (r->bytes > TAMD_LZ_MAX_MESSAGE) scratch_bytes += tamd_lz_scratch_bytes(r->bytes);
-        if (ok && !r->c->ring) {
-            uint8_t* ring = nullptr;
-            if (hipMalloc((void**)&ring, TAMD_LZ_RING + TAMD_LZ_MIRROR) != hipSuccess) r->c->failed = true;
-            else r->c->ring = ring;
-        }
     }
     const size_t o_msgs = align16(n * sizeof(tamd_lz_scatter));
     const size_t o_jobs = o_msgs + align16(n * sizeof(tamd_lz_msg));
@@ -312,13 +326,14 @@ extern "C" int tamd_compressor_compress(void* cp, const uint8_t* data, unsigned 
     req.written = written;
     std::unique_lock<std::mutex> lk(g_req_mu);
     g_pending.push_back(&req);
-    if (g_leader) {
-        g_req_cv.wait(lk, [&req] { return req.done; });
-        return req.rc;
-    }
+    // Wait while another caller leads; take over when it steps down with this request unserved.
+    g_req_cv.wait(lk, [&req] { return req.done || !g_leader; });
+    if (req.done) return req.rc;
     g_leader = true;
     std::vector<LzRequest*> batch, later;
-    while (!g_pending.empty()) {
+    // The leader serves batches only until its own request is done, then hands leadership to a
+    // waiting caller: its own send path is never held by other connections' traffic.
+    while (!req.done) {
         // one request per compressor and one device per batch (a compressor's messages are
         // placed in its ring in call order); the rest waits for the next batch
         batch.clear();
@@ -341,6 +356,7 @@ extern "C" int tamd_compressor_compress(void* cp, const uint8_t* data, unsigned 
         g_req_cv.notify_all();
     }
     g_leader = false;
+    g_req_cv.notify_all();  // a caller whose request is still queued becomes the next leader
     return req.rc;
 }
 

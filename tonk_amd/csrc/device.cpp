@@ -338,6 +338,33 @@ void Device::set_assembly_slots(size_t count, size_t host_mb) {
     slot_bytes_ = 0;
 }
 
+bool Device::assembly_fits(size_t recs, size_t items) const {
+    return recs + 64 <= asm_dev_recs_ && items <= asm_items_;
+}
+
+bool Device::ensure_assembly(size_t recs, size_t items) {
+    if (assembly_fits(recs, items)) return true;
+    stats_.slot_reallocs++;
+    const auto t0 = std::chrono::steady_clock::now();
+    drain_programs();
+    sync_all_streams();  // a program on any stream may still read its slot
+    for (Slot& sl : slots_) sl.ticket = 0;
+    if (items > asm_items_) asm_items_ = items + items / 4;
+    if (recs + 64 > asm_dev_recs_) asm_dev_recs_ = (recs + 64) + (recs + 64) / 4;
+    // (every slot lies within 4 GB of the program base: 32-bit offsets; a bound above that is
+    // clamped -- the callers' bounds are generous, and a real overflow still fails loudly)
+    const size_t per_slot = (0xfffff000ull / slots_.size()) & ~(size_t)255;
+    const size_t max_recs = per_slot > asm_items_ * 8 + 4096 ? (per_slot - asm_items_ * 8 - 4096) / 16 : 0;
+    if (asm_dev_recs_ > max_recs) asm_dev_recs_ = max_recs;
+    const bool ok = alloc_slots(0);
+    if (!ok) {
+        error_ = "program staging allocation failed (assembly slots)";
+        failed_ = true;
+    }
+    report_slow("assembly slot growth", t0, asm_dev_recs_ >> 6, recs >> 6);
+    return ok;
+}
+
 int Device::open_program() {
     const int h = next_slot_;
     Slot& slot = slots_[h];

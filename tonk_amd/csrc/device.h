@@ -108,6 +108,10 @@ public:
     // Parallel-assembly slots: `count` slots of `host_mb` MB pinned staging (the record area a
     // program can fill) and 4x that on the device, plus an item area; call before init.
     void set_assembly_slots(size_t count, size_t host_mb);
+    // Whether a program of `recs` records (instructions + ops) and `items` work items fits a slot;
+    // ensure_assembly grows every slot to fit (drains the device first: no program may be open).
+    bool assembly_fits(size_t recs, size_t items) const;
+    bool ensure_assembly(size_t recs, size_t items);
     // Level pipelining across programs (the session; Context::kPipeDepth): a program's levels
     // above the depth are launched beside the next program's first levels.
     void set_pipelined(bool on) { pipelined_ = on; }

@@ -3,6 +3,7 @@
 #include "encoder.h"
 #include "prof.h"
 
+#include <algorithm>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
@@ -606,8 +607,10 @@ Result Encoder::generate_cauchy(RecoveryOut& out) {
     // program); its readers must already see the level it will be written at.
     ctx_->rows.set_level(out.row, 1);
     static const uint32_t max_group = getenv("TONK_AMD_NO_MULTI") ? 1u : 3u;
-    static const uint32_t span = getenv("TONK_AMD_MULTI_SPAN") ? (uint32_t)atoi(getenv("TONK_AMD_MULTI_SPAN"))
-                                                                : kGroupSpan;  // (A/B knob, <= 2047)
+    // (A/B knob; at most 2047: the run indices of a TARGETS word are 11-bit)
+    static const uint32_t span = getenv("TONK_AMD_MULTI_SPAN")
+                                     ? std::min<uint32_t>(2047u, std::max(1, atoi(getenv("TONK_AMD_MULTI_SPAN"))))
+                                     : kGroupSpan;
     const uint32_t end_col = to_column(count_);
     // A row over a long window stays a pure combine of its own (the executor shares those across
     // a workgroup); a group is one wave's chain, and a long one would set the launch's tail.

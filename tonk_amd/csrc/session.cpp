@@ -509,6 +509,7 @@ struct Session {
     }
 
     void run_all(const std::function<void(size_t, size_t)>& f) {
+        if (fr_running) fr_drain();  // (the pool leaves the free-running loop first)
         static const bool sticky = getenv("TONK_AMD_NO_STICKY") == nullptr;  // A/B switch (profiling)
         next_item = 0;
         sticky_job = sticky && !threads.empty();
@@ -797,8 +798,32 @@ struct Session {
         fr_launch_ready();
     }
 
+    // Upper bounds of one stream's program for a step of `originals` (records = instructions +
+    // ops; measured up to ~12 records per original on the decoder-stress stream and ~1.5 on the
+    // batched ones) and the end-of-stream flush (remaining originals + flush_max recoveries).
+    void fr_bounds(uint32_t originals, bool finish, size_t* recs, size_t* items) const {
+        uint64_t n = originals;
+        if (finish) {
+            n = 0;
+            for (const auto& sp : streams) {
+                const uint64_t left = sp->p.n_originals - sp->runner->position() + sp->p.flush_max;
+                if (left > n) n = left;
+            }
+        }
+        *recs = streams.size() * (size_t)(16 * n + 8192);
+        *items = streams.size() * (size_t)(n / 2 + 2048);
+    }
+
     void fr_step(uint32_t originals, bool finish) {
         typedef std::chrono::steady_clock clk;
+        size_t recs = 0, items = 0;
+        fr_bounds(originals, finish, &recs, &items);
+        if (!dev.assembly_fits(recs, items)) {
+            // A step larger than the staging slots were sized for: launch what is published, then
+            // grow every slot (nothing in flight) before this step's program is opened.
+            fr_drain();
+            if (!dev.ensure_assembly(recs, items)) error = dev.error();
+        }
         start_fr();
         while (fr_published.load(std::memory_order_relaxed) - fr_launched >= fr_ahead) fr_wait_one();
         const uint32_t k = fr_published.load(std::memory_order_relaxed);
@@ -1151,7 +1176,11 @@ void* tamd_session_create(const tamd_session_params* p, char* err, size_t err_le
     static const bool fr_single = getenv("TONK_AMD_FR_SINGLE") != nullptr;
     s->fr_mode = pipe && (nthreads > 1 || fr_single) && getenv("TONK_AMD_NO_DEFER") == nullptr &&
                  getenv("TONK_AMD_PASSES") == nullptr;
-    if (const char* a = getenv("TONK_AMD_RUNAHEAD")) s->fr_ahead = (uint32_t)atoi(a) > 0 ? (uint32_t)atoi(a) : 1u;
+    if (const char* a = getenv("TONK_AMD_RUNAHEAD")) {
+        // (programs k .. k + fr_ahead are open at once: each needs its own FrProg, Part and slot)
+        const int v = atoi(a);
+        s->fr_ahead = v < 1 ? 1u : v > (int)Session::kFrRing - 1 ? Session::kFrRing - 1 : (uint32_t)v;
+    }
     if (s->fr_mode) s->dev.set_assembly_slots(8, p->n_streams <= 4 ? 8 : 24);
     else {
         // (TONK_AMD_SLOTS: A/B knob for the slot count of the pass schedule)
