@@ -351,8 +351,9 @@ struct Harness {
         vclock = ms;
     }
     int enc_retransmit(uint32_t* num, uint32_t* bytes, const uint8_t** data) {
-        const StoredOriginal* o = nullptr;
-        const Result rc = E()->retransmit(&o);
+        StoredOriginal ov;
+        const StoredOriginal* o = &ov;
+        const Result rc = E()->retransmit(&ov);
         if (rc == kSuccess) {
             *num = o->column;
             *bytes = o->bytes - o->header_bytes;

@@ -527,8 +527,9 @@ SIAMESE_EXPORT SiameseResult siamese_encoder_get(SiameseEncoder encoder_t, Siame
     CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
     if (!e || !packet || packet->PacketNum > SIAMESE_PACKET_NUM_MAX) return Siamese_InvalidInput;
     API_CALL();
-    const StoredOriginal* o = nullptr;
-    const Result r = e->enc->get(packet->PacketNum, &o);
+    StoredOriginal ov;
+    const StoredOriginal* o = &ov;
+    const Result r = e->enc->get(packet->PacketNum, &ov);
     if (r != kSuccess) {
         packet->Data = nullptr;
         packet->DataBytes = 0;
@@ -564,8 +565,9 @@ SIAMESE_EXPORT SiameseResult siamese_encoder_retransmit(SiameseEncoder encoder_t
     API_CALL();
     original->Data = nullptr;
     original->DataBytes = 0;
-    const StoredOriginal* o = nullptr;
-    const Result r = e->enc->retransmit(&o);
+    StoredOriginal ov;
+    const StoredOriginal* o = &ov;
+    const Result r = e->enc->retransmit(&ov);
     if (r != kSuccess) API_RC(r);
     original->PacketNum = o->column;
     original->Data = (const unsigned char*)o->host + o->header_bytes;

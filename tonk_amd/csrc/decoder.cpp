@@ -43,6 +43,8 @@ Decoder::~Decoder() {
         delete s;
     }
     subs_.clear();
+    for (size_t i = 0; i < segs_.size(); ++i) release_segment(segs_[i], 0, segs_[i].count);
+    segs_.clear();
     Recovery* r = head_;
     while (r) { Recovery* n = r->next; free_recovery(r); r = n; }
     for (Recovery* g : graveyard_) delete g;
@@ -76,8 +78,101 @@ void Decoder::free_recovery(Recovery* r) {
     graveyard_.push_back(r);
 }
 
-void Decoder::read_original(const StoredOriginal& o, uint32_t len, uint8_t coef, Sym& out) const {
-    ctx_->ex.append(ctx_->rows, o.row, len, coef, out);
+void Decoder::read_original(RowId row, uint32_t len, uint8_t coef, Sym& out) const {
+    ctx_->ex.append(ctx_->rows, row, len, coef, out);
+}
+
+void Decoder::release_segment(const Segment& s, uint32_t from, uint32_t n) {
+    if (s.owned)
+        for (uint32_t j = from; j < from + n; ++j) ctx_->rows.free_deferred(s.row(j));
+}
+
+void Decoder::append(uint32_t e0, const RowId* rows, uint32_t k, uint32_t framed_bytes, uint32_t header_bytes,
+                     uint8_t owned) {
+    const RowTable& rt = ctx_->rows;
+    uint32_t e = e0, col = to_column(e0);
+    // Fast path: the k packets are consecutive handles at one offset stride with no column wrap
+    // inside (a stretch of a session's inputs): they continue the last segment or open one, and
+    // only the elements' segment numbers are filled.
+    if (k >= 2 && col + k - 1 < kColumnPeriod && col != 0 && consecutive_handles(rows, k)) {
+        const uint32_t o0 = rt.offset(rows[0]), o1 = rt.offset(rows[1]);
+        const uint32_t stride = o1 - o0;
+        if (o1 > o0 && rt.affine(rows[0], k, stride)) {
+            Segment* last = segs_.empty() ? nullptr : &segs_.back();
+            const bool cont = last && last->end() == e0 + base_ && last->bytes == framed_bytes &&
+                              last->header_bytes == header_bytes && last->owned == owned &&
+                              rows[0] == last->row0 + last->count && o0 > last->off0 &&
+                              (last->count == 1 ? o0 - last->off0 == stride
+                                                : last->stride == stride && o0 == last->off(last->count));
+            if (cont) {
+                last->stride = stride;
+                last->count += k;
+            } else {
+                Segment sg;
+                sg.first = e0 + base_;
+                sg.count = k;
+                sg.row0 = rows[0];
+                sg.off0 = o0;
+                sg.stride = stride;
+                sg.bytes = framed_bytes;
+                sg.column0 = col;
+                sg.header_bytes = (uint8_t)header_bytes;
+                sg.owned = owned;
+                segs_.push_back(sg);
+            }
+            const uint32_t id = seg_base_ + (uint32_t)segs_.size() - 1;
+            for (uint32_t x = e0; x < e0 + k;) {
+                const uint32_t bit = x % kSubwindow;
+                const uint32_t n = std::min(kSubwindow - bit, e0 + k - x);
+                std::fill_n(subs_[x / kSubwindow]->seg + bit, n, id);
+                x += n;
+            }
+            return;
+        }
+    }
+    uint32_t j = 0;
+    while (j < k) {
+        Segment* last = segs_.empty() ? nullptr : &segs_.back();
+        const uint32_t e_abs = e + base_;
+        const RowId r = rows[j];
+        const uint32_t off = rt.offset(r);
+        const bool cont = last && last->end() == e_abs && last->bytes == framed_bytes &&
+                          last->header_bytes == header_bytes && last->owned == owned && r == last->row0 + last->count &&
+                          off > last->off0 && col != 0 && (last->count == 1 || off == last->off(last->count));
+        if (cont) {
+            if (last->count == 1) last->stride = off - last->off0;
+            ++last->count;
+        } else {
+            Segment sg;
+            sg.first = e_abs;
+            sg.count = 1;
+            sg.row0 = r;
+            sg.off0 = off;
+            sg.bytes = framed_bytes;
+            sg.column0 = col;
+            sg.header_bytes = (uint8_t)header_bytes;
+            sg.owned = owned;
+            segs_.push_back(sg);
+            last = &segs_.back();
+        }
+        const uint32_t id = seg_base_ + (uint32_t)segs_.size() - 1;
+        subs_[e / kSubwindow]->seg[e % kSubwindow] = id;
+        ++e;
+        ++j;
+        col = col_inc(col);
+        // the rest of the run while rows keep both strides: only the element's segment number
+        if (last->count >= 2) {
+            uint32_t n = last->count;
+            while (j < k && rows[j] == last->row0 + n && col != 0 && rt.offset(rows[j]) == last->off(n)) {
+                subs_[e / kSubwindow]->seg[e % kSubwindow] = id;
+                ++e;
+                ++j;
+                ++n;
+                col = col_inc(col);
+            }
+            last->count = n;
+        }
+    }
 }
 
 // ============================================================================================
@@ -92,22 +187,6 @@ bool Decoder::mark_got(uint32_t column) {
     s->got_count++;
     s->got |= 1ull << (e % kSubwindow);
     return e == next_expected_;
-}
-
-// Run bookkeeping of input rows (Encoder::add_unchecked's StoredOriginal::run): the element
-// continues the run of the element before it when that one is a received input row of the same
-// length and the row offsets keep a fixed stride.  Recovered rows have run 0 and break runs
-// (their contents may still be in flight and their lengths are refined after readback).
-void Decoder::set_run(uint32_t e, StoredOriginal& o) {
-    o.run = 1;
-    o.stride = 0;
-    if (e == 0) return;
-    const StoredOriginal& p = elem(e - 1);
-    if (p.run && p.bytes == o.bytes && o.off > p.off && p.run < 0xffff &&
-        (p.run == 1 || o.off - p.off == p.stride)) {
-        o.run = (uint16_t)(p.run + 1);
-        o.stride = o.off - p.off;
-    }
 }
 
 // RangeLostPackets (:1279-1323)
@@ -195,24 +274,31 @@ Result Decoder::add_original(uint32_t packet_num, RowId row, uint32_t framed_byt
         stats_[6]++;
         return kDuplicateData;
     }
+    const bool at_end = e >= count_;  // (beyond every element so far: may continue a segment)
     grow_window(e + 1);
     Subwindow* s = subs_[e / kSubwindow];
     const uint32_t bit = e % kSubwindow;
-    StoredOriginal& o = s->orig[bit];
-    if (o.bytes > 0) {
+    if ((s->got >> bit) & 1u) {
         stats_[6]++;
         return kDuplicateData;
     }
-    drop_original(o);
-    o.row = row;
-    o.off = ctx_->rows.offset(row);
-    o.bytes = framed_bytes;
-    o.column = packet_num;
-    o.header_bytes = (uint8_t)header_bytes;
-    o.owned = borrowed ? 0 : 1;
-    o.host = host;
-    if (o.owned || host) s->held++;
-    set_run(e, o);
+    if (at_end && !host) {
+        append(e, &row, 1, framed_bytes, header_bytes, borrowed ? 0 : 1);
+    } else {
+        StoredOriginal& o = s->orig[bit];
+        drop_original(o);
+        o.row = row;
+        o.off = ctx_->rows.offset(row);
+        o.bytes = framed_bytes;
+        o.column = packet_num;
+        o.header_bytes = (uint8_t)header_bytes;
+        o.owned = borrowed ? 0 : 1;
+        o.host = host;
+        o.run = 0;
+        o.stride = 0;
+        if (o.owned || host) s->held++;
+        s->singles++;
+    }
     *took = !borrowed;
     s->got_count++;
     s->got |= 1ull << bit;
@@ -243,48 +329,11 @@ bool Decoder::add_run_inorder(uint32_t col0, const RowId* rows, uint32_t k, uint
     // would repeat this answer without changing any state.
     if (head_ && (next_expected_ >= e0 || check_recovery_possible())) return false;
     grow_window(e0 + k);
-    const RowTable& rt = ctx_->rows;
-    const uint8_t owned = borrowed ? 0 : 1;
-    uint32_t column = col0;
-    const RowId* r = rows;
-    // run state of the element before the run (set_run, kept in locals)
-    uint32_t prev_run = 0, prev_off = 0, prev_stride = 0, prev_bytes = 0;
-    if (e0 > 0) {
-        const StoredOriginal& p = elem(e0 - 1);
-        prev_run = p.run;
-        prev_off = p.off;
-        prev_stride = p.stride;
-        prev_bytes = p.bytes;
-    }
-    for (uint32_t e = e0; e < e0 + k;) {  // a subwindow at a time: slots, then got bits
+    append(e0, rows, k, framed_bytes, header_bytes, borrowed ? 0 : 1);
+    for (uint32_t e = e0; e < e0 + k;) {  // got bits a subwindow at a time
         const uint32_t bit = e % kSubwindow;
         const uint32_t n = std::min(kSubwindow - bit, e0 + k - e);
         Subwindow* s = subs_[e / kSubwindow];
-        StoredOriginal* o = s->orig + bit;
-        if (owned) s->held += n;
-        for (uint32_t t = 0; t < n; ++t, ++o, ++r) {
-            if (o->owned || o->host) drop_original(*o);  // (slots past the window end are empty)
-            const uint32_t off = rt.offset(*r);
-            uint32_t run = 1, stride = 0;
-            if (prev_run && prev_bytes == framed_bytes && off > prev_off && prev_run < 0xffff &&
-                (prev_run == 1 || off - prev_off == prev_stride)) {
-                run = prev_run + 1;
-                stride = off - prev_off;
-            }
-            o->row = *r;
-            o->off = off;
-            o->bytes = framed_bytes;
-            o->column = column;
-            o->header_bytes = (uint8_t)header_bytes;
-            o->owned = owned;
-            o->run = (uint16_t)run;
-            o->stride = stride;
-            prev_run = run;
-            prev_off = off;
-            prev_stride = stride;
-            prev_bytes = framed_bytes;
-            column = col_inc(column);
-        }
         s->got |= (n == 64 ? ~0ull : ((1ull << n) - 1)) << bit;
         s->got_count += n;
         e += n;
@@ -345,27 +394,29 @@ bool Decoder::start_sums(uint32_t element_start, uint32_t buffer_bytes) {
     return true;
 }
 
-// DecoderPacketWindow::GetSum (:1680-1739), for the lane's three sums at once
+// DecoderPacketWindow::GetSum (:1680-1739), for the lane's three sums at once.  The lane's
+// packets inside a segment are every kLanes-th of it: one strided run per segment.
 LaneSums& Decoder::get_lane(uint32_t lane, uint32_t element_end) {
     LaneSum& sum = lanes_[lane];
     uint32_t e = sum.element_end;
     if (e >= element_end) return sum.sums;
-    // As Encoder::get_lane: when the run of received input packets ending at the lane's last
-    // element reaches back to e, the rest of the lane is one strided run.
-    const uint32_t last = e + ((element_end - 1 - e) / kLanes) * kLanes;
-    const StoredOriginal& ol = elem(last);
     do {
-        const StoredOriginal& o = elem(e);
-        if (last > e && ol.run > last - e && o.column + (last - e) < kColumnPeriod) {
-            sum.sums.grow(o.bytes);
-            sum.sums.accumulate_run_level0(o.row, o.off, o.bytes, o.column, (last - e) / kLanes + 1,
-                                           ol.stride * kLanes);
-            e = last + kLanes;
-            break;
+        const uint32_t id = seg_id(e);
+        if (id != kSingle) {
+            const Segment& sg = segs_[id - seg_base_];
+            const uint32_t j = e + base_ - sg.first;
+            uint32_t stop = sg.end() - base_;
+            if (stop > element_end) stop = element_end;
+            const uint32_t n = (stop - 1 - e) / kLanes + 1;
+            sum.sums.grow(sg.bytes);
+            sum.sums.accumulate_run_level0(sg.row(j), sg.off(j), sg.bytes, col_add(sg.column0, j), n, sg.stride * kLanes);
+            e += n * kLanes;
+            continue;
         }
+        const StoredOriginal& o = elem(e);
         if (o.bytes > 0) {
             sum.sums.grow(o.bytes);
-            if (ctx_->rows.level(o.row) == 0) sum.sums.accumulate_level0(o.row, o.off, o.bytes, o.column);
+            if (ctx_->rows.level(o.row) == 0) sum.sums.accumulate_level0(o.row, ctx_->rows.offset(o.row), o.bytes, o.column);
             else sum.sums.accumulate(ctx_->rows, o.row, o.bytes, o.column);
         }
         e += kLanes;
@@ -443,14 +494,34 @@ void Decoder::remove_elements() {
         Subwindow* s = subs_[i];
         if (s->held) {
             for (unsigned k = 0; k < kSubwindow; ++k) drop_original(s->orig[k]);
-        } else {
+        } else if (s->singles) {
             memset((void*)s->orig, 0, sizeof(s->orig));  // (nothing to release: borrowed rows)
         }
+        memset(s->seg, 0xff, sizeof(s->seg));
         s->got = 0;
         s->got_count = 0;
         s->held = 0;
+        s->singles = 0;
     }
     std::rotate(subs_.begin(), subs_.begin() + first_kept_sub, subs_.end());
+    // segments below the new window start leave; one that straddles it keeps its later packets
+    const uint32_t cut = base_ + removed;
+    while (!segs_.empty() && segs_.front().end() <= cut) {
+        release_segment(segs_.front(), 0, segs_.front().count);
+        segs_.pop_front(1);
+        ++seg_base_;
+    }
+    if (!segs_.empty() && segs_.front().first < cut) {
+        Segment& f = segs_.front();
+        const uint32_t d = cut - f.first;
+        release_segment(f, 0, d);
+        f.first = cut;
+        f.count -= d;
+        f.row0 += d;
+        f.off0 += d * f.stride;
+        f.column0 = col_add(f.column0, d);
+    }
+    base_ = cut;
 
     count_ -= removed;
     column_start_ = to_column(removed);
@@ -591,6 +662,7 @@ void Decoder::populate_columns(uint32_t old_cols, uint32_t new_cols) {
                 c.orig = &s->orig[bit];
                 c.cx = column_value(c.column);
                 c.orig->column = column;  // lost slot remembers its matrix column
+                s->singles++;
                 if (++column >= new_cols) return;
             } while (++bit < kSubwindow);
         }
@@ -670,16 +742,14 @@ bool Decoder::generate_matrix() {
         const FastMod ldpc_mod(m.LDPCCount);
         for (uint32_t k = 0; k < pairs; ++k) {
             const uint32_t e1 = es + ldpc_mod(prng.next());
-            const StoredOriginal& o1 = elem(e1);
-            if (o1.bytes <= 0) {
-                const uint32_t mc = o1.column;
+            if (!got(e1)) {  // a lost element: its slot holds its matrix column (populate_columns)
+                const uint32_t mc = elem(e1).column;
                 if (mc >= columns) { disabled_ = true; return false; }
                 if (mc >= start_col) mat(i, mc) ^= 1;
             }
             const uint32_t erx = es + ldpc_mod(prng.next());
-            const StoredOriginal& orx = elem(erx);
-            if (orx.bytes <= 0) {
-                const uint32_t mc = orx.column;
+            if (!got(erx)) {
+                const uint32_t mc = elem(erx).column;
                 if (mc >= columns) { disabled_ = true; return false; }
                 if (mc >= start_col) mat(i, mc) ^= rx;
             }
@@ -853,8 +923,8 @@ bool Decoder::add_single_recovery(RowId row, uint32_t data_bytes, const uint8_t*
                                   const RecoveryMeta& m, bool* took) {
     const uint32_t e = to_element(m.ColumnStart);
     if (invalid_element(e)) return false;
+    if (got(e)) return true;
     StoredOriginal& o = elem(e);
-    if (o.bytes != 0) return true;
 
     uint32_t header = 0, payload = 0;
     if (host) {
@@ -871,9 +941,10 @@ bool Decoder::add_single_recovery(RowId row, uint32_t data_bytes, const uint8_t*
     o.column = m.ColumnStart;
     o.header_bytes = (uint8_t)header;
     o.owned = 1;
-    o.run = 0;  // (not an input row: never part of a run, see set_run)
+    o.run = 0;
     o.stride = 0;
     subs_[e / kSubwindow]->held++;
+    subs_[e / kSubwindow]->singles++;
     *took = true;
 
     if (!has_recovered_) {
@@ -1026,13 +1097,12 @@ bool Decoder::eliminate_original_data() {
 
         if (m.SumCount <= kCauchyThreshold) {
             for (uint32_t j = es; j < ee; ++j) {
-                const StoredOriginal& o = elem(j);
-                uint32_t add = o.bytes;
-                if (add > 0) {
-                    if (add > rec->bytes) add = rec->bytes;
-                    const uint8_t y = m.Row == 0 ? 1 : cauchy_element(m.Row - 1, o.column % kCauchyMaxColumns);
-                    read_original(o, add, y, buf);
-                }
+                RowId row;
+                uint32_t add;
+                if (!packet(j, row, add)) continue;
+                if (add > rec->bytes) add = rec->bytes;
+                const uint8_t y = m.Row == 0 ? 1 : cauchy_element(m.Row - 1, to_column(j) % kCauchyMaxColumns);
+                read_original(row, add, y, buf);
             }
         } else {
             const uint32_t rbytes = rec->bytes;
@@ -1072,12 +1142,12 @@ bool Decoder::eliminate_original_data() {
             const uint32_t pairs = (m.LDPCCount + kPairRate - 1) / kPairRate;
             const FastMod ldpc_mod(m.LDPCCount);
             for (uint32_t i = 0; i < pairs; ++i) {
+                RowId row;
+                uint32_t b;
                 const uint32_t e1 = es + ldpc_mod(prng.next());
-                const StoredOriginal& o1 = elem(e1);
-                if (o1.bytes > 0) read_original(o1, o1.bytes < rbytes ? o1.bytes : rbytes, 1, buf);
+                if (packet(e1, row, b)) read_original(row, b < rbytes ? b : rbytes, 1, buf);
                 const uint32_t erx = es + ldpc_mod(prng.next());
-                const StoredOriginal& orx = elem(erx);
-                if (orx.bytes > 0) read_original(orx, orx.bytes < rbytes ? orx.bytes : rbytes, rx, buf);
+                if (packet(erx, row, b)) read_original(row, b < rbytes ? b : rbytes, rx, buf);
             }
         }
         if (ctx_->oom) return false;
@@ -1248,9 +1318,10 @@ bool Decoder::store_recovered(uint32_t ci, Sym& value, uint32_t bytes, bool& ite
     o->column = mcols_[ci].column;
     o->header_bytes = 0;
     o->owned = 1;
-    o->run = 0;  // (a recovered row: never part of a run, see set_run)
+    o->run = 0;
     o->stride = 0;
     subs_[to_element(o->column) / kSubwindow]->held++;
+    subs_[to_element(o->column) / kSubwindow]->singles++;
 
     RecoveredPacket& rp = recovered_[ci];
     rp.packet_num = o->column;
@@ -1278,7 +1349,7 @@ Result Decoder::finish_solve(bool iterate) {
 
 void Decoder::set_recovered_length(uint32_t packet_num, uint32_t framed_bytes, uint32_t header_bytes, void* host) {
     const uint32_t e = to_element(packet_num);
-    if (invalid_element(e)) { if (host && release_) release_(host, user_); return; }
+    if (invalid_element(e) || seg_id(e) != kSingle) { if (host && release_) release_(host, user_); return; }
     StoredOriginal& o = elem(e);
     if (o.column != packet_num || o.bytes == 0) { if (host && release_) release_(host, user_); return; }
     o.bytes = framed_bytes;
@@ -1293,6 +1364,19 @@ Result Decoder::get(uint32_t packet_num, StoredOriginal** out) {
     if (disabled_) return kDisabled;
     const uint32_t e = to_element(packet_num);
     if (invalid_element(e)) return kNeedMoreData;
+    const uint32_t id = seg_id(e);
+    if (id != kSingle) {  // (a segment's packet, as a value: no host copy)
+        const Segment& sg = segs_[id - seg_base_];
+        const uint32_t j = e + base_ - sg.first;
+        view_ = StoredOriginal();
+        view_.row = sg.row(j);
+        view_.off = sg.off(j);
+        view_.bytes = sg.bytes;
+        view_.column = packet_num;
+        view_.header_bytes = sg.header_bytes;
+        *out = &view_;
+        return kSuccess;
+    }
     StoredOriginal& o = elem(e);
     if (o.bytes <= 0) return kNeedMoreData;
     *out = &o;

@@ -11,6 +11,7 @@
 #include "encoder.h"
 
 #include <stdint.h>
+#include <string.h>
 #include <vector>
 
 namespace tamd {
@@ -62,13 +63,21 @@ public:
     void post_flush() override {}
 
 private:
+    // Received originals are stored as segments (encoder.h Segment: runs of equally long packets
+    // at fixed row strides, added in order); seg[bit] names the element's segment, or kSingle
+    // when the element is described by orig[bit] instead -- a recovered original, one delivered
+    // out of order into a hole, a C-ABI add with a host copy -- or is not received (bytes 0).
+    static const uint32_t kSingle = 0xffffffffu;
     struct Subwindow {
-        StoredOriginal orig[kSubwindow];
         uint64_t got = 0;
         uint32_t got_count = 0;
-        // slots written with something to release (an owned row or a host copy) since the
+        // orig[] slots written with something to release (an owned row or a host copy) since the
         // subwindow was last cleared; 0: clearing is a plain memset (empty slot = all zero)
         uint32_t held = 0;
+        uint32_t singles = 0;  // orig[] slots written since the last clear (0: nothing to clear)
+        uint32_t seg[kSubwindow];
+        StoredOriginal orig[kSubwindow];
+        Subwindow() { memset(seg, 0xff, sizeof(seg)); }
     };
     struct Recovery {
         Recovery* next = nullptr;
@@ -99,6 +108,10 @@ private:
     // ---- DecoderPacketWindow (SiameseDecoder.h:288-419) ----
     uint32_t count_ = 0, column_start_ = 0, next_expected_ = 0;
     std::vector<Subwindow*> subs_;
+    Ring<Segment> segs_;      // run segments in element order; segs_[i] is number seg_base_ + i
+    uint32_t seg_base_ = 0;
+    uint32_t base_ = 0;       // absolute element number of window element 0
+    StoredOriginal view_;     // get() of an element inside a segment
     LaneSum lanes_[kLanes];
     uint32_t sum_column_start_ = 0, sum_column_count_ = 0;
     std::vector<RecoveredPacket> recovered_;
@@ -148,7 +161,29 @@ private:
     uint32_t to_element(uint32_t column) const { return col_sub(column, column_start_); }
     uint32_t to_column(uint32_t element) const { return col_add(element, column_start_); }
     bool invalid_element(uint32_t e) const { return e >= count_; }
-    StoredOriginal& elem(uint32_t e) { return subs_[e / kSubwindow]->orig[e % kSubwindow]; }
+    StoredOriginal& elem(uint32_t e) { return subs_[e / kSubwindow]->orig[e % kSubwindow]; }  // its single slot
+    uint32_t seg_id(uint32_t e) const { return subs_[e / kSubwindow]->seg[e % kSubwindow]; }
+    bool got(uint32_t e) const { return (subs_[e / kSubwindow]->got >> (e % kSubwindow)) & 1u; }
+    // The packet of a received or recovered element: row and framed bytes (false: none).
+    bool packet(uint32_t e, RowId& row, uint32_t& bytes) const {
+        const Subwindow* s = subs_[e / kSubwindow];
+        const uint32_t id = s->seg[e % kSubwindow];
+        if (id != kSingle) {
+            const Segment& sg = segs_[id - seg_base_];
+            row = sg.row(e + base_ - sg.first);
+            bytes = sg.bytes;
+            return true;
+        }
+        const StoredOriginal& o = s->orig[e % kSubwindow];
+        row = o.row;
+        bytes = o.bytes;
+        return o.bytes > 0;
+    }
+    // Append received packets rows[0..k) (equally long, no host copy) as elements e0 .. e0 + k - 1
+    // at the window end (beyond every segment), extending the last segment while they continue it.
+    void append(uint32_t e0, const RowId* rows, uint32_t k, uint32_t framed_bytes, uint32_t header_bytes,
+                uint8_t owned);
+    void release_segment(const Segment& s, uint32_t from, uint32_t n);
     uint32_t next_lane_element(uint32_t element, uint32_t lane) const {
         uint32_t n = element - (element % kLanes) + lane;
         if (n < element) n += kLanes;
@@ -158,7 +193,6 @@ private:
 
     // window
     bool mark_got(uint32_t column);
-    void set_run(uint32_t e, StoredOriginal& o);
     uint32_t range_lost(uint32_t start, uint32_t end);
     uint32_t find_next_lost(uint32_t start);
     uint32_t find_next_got(uint32_t start);
@@ -170,7 +204,7 @@ private:
     bool plug_sum_holes(uint32_t element_start);
     void remove_elements();
     void drop_original(StoredOriginal& o);
-    void read_original(const StoredOriginal& o, uint32_t len, uint8_t coef, Sym& out) const;
+    void read_original(RowId row, uint32_t len, uint8_t coef, Sym& out) const;
 
     // recovery list / checked region / matrix
     void list_insert(Recovery* r, bool out_of_order);

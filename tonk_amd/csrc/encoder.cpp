@@ -32,22 +32,40 @@ Encoder::Encoder(Context* ctx, uint32_t row_bytes, HostRelease release, void* us
 
 Encoder::~Encoder() {
     pre_flush();  // snapshots already referenced by the pending program must still be written
-    for (size_t i = 0; i < win_.size(); ++i) drop_original(win_[i]);
-    win_.clear();
+    drop_all();
     for (unsigned l = 0; l < kLanes; ++l) lanes_[l].sums.release(ctx_->rows);
     ctx_->detach(this);
 }
 
-void Encoder::release_original(const StoredOriginal& o) {
-    if (!o.owned && !o.host) return;
-    --held_;
-    if (o.owned) ctx_->rows.free_deferred(o.row);
-    if (o.host && release_) release_(o.host, user_);
+void Encoder::release_segment(const Segment& s, uint32_t from, uint32_t n) {
+    if (s.owned)
+        for (uint32_t j = from; j < from + n; ++j) ctx_->rows.free_deferred(s.row(j));
+    if (s.host && release_ && from == 0 && n == s.count) release_(s.host, user_);
 }
 
-void Encoder::drop_original(StoredOriginal& o) {
-    release_original(o);
-    o = StoredOriginal();
+void Encoder::drop_all() {
+    if (held_)
+        for (size_t i = 0; i < segs_.size(); ++i) release_segment(segs_[i], 0, segs_[i].count);
+    held_ = 0;
+    seg_base_ += (uint32_t)segs_.size();
+    segs_.clear();
+    win_.clear();
+    base_ = 0;
+}
+
+StoredOriginal Encoder::view(uint32_t e) const {
+    const Segment& s = seg_of(e);
+    const uint32_t j = e + base_ - s.first;
+    StoredOriginal o;
+    o.row = s.row(j);
+    o.bytes = s.bytes;
+    o.column = to_column(e);
+    o.send_msec = win_[e].send_msec;
+    o.off = s.off(j);
+    o.header_bytes = s.header_bytes;
+    o.owned = s.owned;
+    o.host = s.host;
+    return o;
 }
 
 void Encoder::pre_flush() {
@@ -55,72 +73,154 @@ void Encoder::pre_flush() {
     for (unsigned l = 0; l < kLanes; ++l) lanes_[l].sums.flush(ctx_->rows, ctx_->pb, ctx_->ex);
 }
 
+void Encoder::append(const RowId* rows, uint32_t k, uint32_t framed_bytes, uint32_t header_bytes, uint8_t owned,
+                     void* host, uint32_t now) {
+    const RowTable& rt = ctx_->rows;
+    uint32_t e_abs = base_ + (uint32_t)win_.size();
+    uint32_t col = next_column_;
+    win_.reserve_more(k);
+    Slot* wb = win_.slot_base();
+    const size_t mask = win_.slot_mask();
+    size_t idx = win_.slot_index(win_.size());
+    // Fast path: the k packets are consecutive handles at one offset stride with no column wrap
+    // inside (a stretch of a session's inputs): they continue the last segment or open one, and
+    // only the element slots are filled.
+    if (k >= 2 && !host && col + k - 1 < kColumnPeriod && col != 0 && consecutive_handles(rows, k)) {
+        const uint32_t o0 = rt.offset(rows[0]), o1 = rt.offset(rows[1]);
+        const uint32_t stride = o1 - o0;
+        if (o1 > o0 && rt.affine(rows[0], k, stride)) {
+            Segment* last = segs_.empty() ? nullptr : &segs_.back();
+            const bool cont = last && !last->host && last->row0 != kNoRow && last->end() == e_abs &&
+                              last->bytes == framed_bytes && last->header_bytes == header_bytes &&
+                              last->owned == owned && rows[0] == last->row0 + last->count && o0 > last->off0 &&
+                              (last->count == 1 ? o0 - last->off0 == stride
+                                                : last->stride == stride && o0 == last->off(last->count));
+            if (cont) {
+                last->stride = stride;
+                last->count += k;
+            } else {
+                Segment sg;
+                sg.first = e_abs;
+                sg.count = k;
+                sg.row0 = rows[0];
+                sg.off0 = o0;
+                sg.stride = stride;
+                sg.bytes = framed_bytes;
+                sg.column0 = col;
+                sg.header_bytes = (uint8_t)header_bytes;
+                sg.owned = owned;
+                segs_.push_back(sg);
+                if (owned) ++held_;
+            }
+            const Slot v{seg_base_ + (uint32_t)segs_.size() - 1, now};
+            for (uint32_t x = 0; x < k; ++x) wb[(idx + x) & mask] = v;
+            win_.commit(k);
+            return;
+        }
+    }
+    uint32_t j = 0;
+    while (j < k) {
+        // extend the last segment when this packet continues it, else open one
+        Segment* last = segs_.empty() ? nullptr : &segs_.back();
+        const RowId r = rows[j];
+        const uint32_t off = rt.offset(r);
+        const bool cont = last && !host && !last->host && last->row0 != kNoRow && last->end() == e_abs &&
+                          last->bytes == framed_bytes && last->header_bytes == header_bytes && last->owned == owned &&
+                          r == last->row0 + last->count && off > last->off0 && col != 0 &&
+                          (last->count == 1 || off == last->off(last->count));
+        if (cont) {
+            if (last->count == 1) last->stride = off - last->off0;
+            ++last->count;
+        } else {
+            Segment sg;
+            sg.first = e_abs;
+            sg.count = 1;
+            sg.row0 = r;
+            sg.off0 = off;
+            sg.bytes = framed_bytes;
+            sg.column0 = col;
+            sg.header_bytes = (uint8_t)header_bytes;
+            sg.owned = owned;
+            sg.host = host;
+            segs_.push_back(sg);
+            if (owned || host) ++held_;
+            last = &segs_.back();
+        }
+        const uint32_t id = seg_base_ + (uint32_t)segs_.size() - 1;
+        wb[idx] = Slot{id, now};
+        idx = (idx + 1) & mask;
+        ++e_abs;
+        col = col_inc(col);
+        ++j;
+        // the rest of the run while rows keep both strides (one contiguous scan of the handles'
+        // offsets): only the per-element slot is written
+        if (last->count >= 2) {
+            uint32_t n = last->count;
+            while (j < k && rows[j] == last->row0 + n && col != 0 && rt.offset(rows[j]) == last->off(n)) {
+                wb[idx] = Slot{id, now};
+                idx = (idx + 1) & mask;
+                ++n;
+                ++j;
+                col = col_inc(col);
+            }
+            e_abs += n - last->count;
+            last->count = n;
+        }
+    }
+    win_.commit(k);
+}
+
 // EncoderPacketWindow::Add (SiameseEncoder.cpp:85-161)
 Result Encoder::add(RowId row, uint32_t framed_bytes, uint32_t header_bytes, uint32_t payload_bytes,
                     void* host, uint32_t* packet_num, bool borrowed) {
     if (disabled_) return kDisabled;
     if (remaining_slots() <= 0) return kMaxPacketsReached;
-    add_unchecked(row, ctx_->rows.offset(row), framed_bytes, header_bytes, payload_bytes, host, packet_num, borrowed);
+    *packet_num = add_first(row, framed_bytes, header_bytes, payload_bytes, host, borrowed);
     return kSuccess;
+}
+
+// The window part of Add for one packet: a new window when the previous one is empty (elements
+// below column % kLanes of a fresh window are placeholders: only the RTT scan reads them, and only
+// their send timestamps), then the packet at the window end.
+uint32_t Encoder::add_first(RowId row, uint32_t framed_bytes, uint32_t header_bytes, uint32_t payload_bytes,
+                            void* host, bool borrowed) {
+    const uint32_t column = next_column_;
+    const uint32_t now = (uint32_t)now_msec();
+    if (count_ > 0) {
+        ++count_;
+    } else {
+        start_new_window(column);
+        const uint32_t element = column % kLanes;
+        if (element) {
+            Segment ph;
+            ph.first = base_;
+            ph.count = element;
+            ph.column0 = column - element;
+            segs_.push_back(ph);
+            for (uint32_t e = 0; e < element; ++e)
+                win_.push_back(Slot{seg_base_ + (uint32_t)segs_.size() - 1, placeholder_msec_[e]});
+        }
+    }
+    append(&row, 1, framed_bytes, header_bytes, borrowed ? 0 : 1, host, now);
+    next_column_ = col_inc(next_column_);
+    Lane& lane = lanes_[column % kLanes];
+    if (lane.longest < framed_bytes) lane.longest = framed_bytes;
+    if (longest_ < framed_bytes) longest_ = framed_bytes;
+    stats_[0]++;
+    stats_[1] += payload_bytes;
+    return column;
 }
 
 // k consecutive add() calls that all succeed.
 bool Encoder::add_run(const RowId* rows, uint32_t k, uint32_t framed_bytes, uint32_t header_bytes,
                       uint32_t payload_bytes, bool borrowed, uint32_t* first_col) {
     if (disabled_ || remaining_slots() < k || !k) return false;
-    *first_col = next_column_;
-    uint32_t col = 0;
-    const RowTable& rt = ctx_->rows;
     // the first add may start a window; the rest append to it (count_ > 0, element == count_)
-    add_unchecked(rows[0], rt.offset(rows[0]), framed_bytes, header_bytes, payload_bytes, nullptr, &col, borrowed);
+    *first_col = add_first(rows[0], framed_bytes, header_bytes, payload_bytes, nullptr, borrowed);
     if (k == 1) return true;
-    // k - 1 more appends, as add_unchecked would do them, with the window state in locals
-    uint32_t element = count_;
-    if (win_.size() != element) {  // (placeholder slots would be overwritten: the general path)
-        for (uint32_t j = 1; j < k; ++j)
-            add_unchecked(rows[j], rt.offset(rows[j]), framed_bytes, header_bytes, payload_bytes, nullptr, &col,
-                          borrowed);
-        return true;
-    }
-    win_.reserve_more(k - 1);
-    StoredOriginal* base = win_.slot_base();
-    const size_t mask = win_.slot_mask();
-    size_t idx = win_.slot_index(element - 1);
-    uint32_t prev_off = base[idx].off, prev_stride = base[idx].stride, prev_bytes = base[idx].bytes;
-    uint32_t prev_run = base[idx].run;
-    uint32_t column = next_column_;
-    const uint32_t now = (uint32_t)now_msec();
-    const uint8_t owned = borrowed ? 0 : 1;
-    for (uint32_t j = 1; j < k; ++j) {
-        idx = (idx + 1) & mask;
-        StoredOriginal& o = base[idx];
-        const uint32_t off = rt.offset(rows[j]);
-        uint32_t run = 1, stride = 0;
-        if (prev_bytes == framed_bytes && off > prev_off && prev_run < 0xffff &&
-            (prev_run == 1 || off - prev_off == prev_stride)) {
-            run = prev_run + 1;
-            stride = off - prev_off;
-        }
-        o.row = rows[j];
-        o.bytes = framed_bytes;
-        o.column = column;
-        o.send_msec = now;
-        o.off = off;
-        o.stride = stride;
-        o.run = (uint16_t)run;
-        o.header_bytes = (uint8_t)header_bytes;
-        o.owned = owned;
-        o.host = nullptr;
-        prev_off = off;
-        prev_stride = stride;
-        prev_bytes = framed_bytes;
-        prev_run = run;
-        column = col_inc(column);
-    }
-    win_.commit(k - 1);
-    if (owned) held_ += k - 1;
+    append(rows + 1, k - 1, framed_bytes, header_bytes, borrowed ? 0 : 1, nullptr, (uint32_t)now_msec());
     count_ += k - 1;
-    next_column_ = column;
+    next_column_ = col_add(next_column_, k - 1);
     // every lane one of these columns fell on (all k - 1 have the same length)
     const uint32_t first = col_inc(*first_col);
     for (uint32_t j = 0; j < k - 1 && j < kLanes; ++j) {
@@ -133,72 +233,13 @@ bool Encoder::add_run(const RowId* rows, uint32_t k, uint32_t framed_bytes, uint
     return true;
 }
 
-inline void Encoder::add_unchecked(RowId row, uint32_t off, uint32_t framed_bytes, uint32_t header_bytes,
-                                   uint32_t payload_bytes, void* host, uint32_t* packet_num, bool borrowed) {
-    const uint32_t column = next_column_;
-    uint32_t element = count_;
-    *packet_num = column;
-
-    if (count_ > 0) {
-        ++count_;
-    } else {
-        element = column % kLanes;
-        start_new_window(column);
-    }
-    // Elements below `element` in a fresh window are placeholders: only the RTT scan reads them,
-    // and only their send timestamps.
-    while (win_.size() < element) {
-        StoredOriginal p;
-        p.send_msec = placeholder_msec_[win_.size() % kLanes];
-        win_.push_back(p);
-    }
-    StoredOriginal* slot;
-    if (win_.size() == element) {
-        slot = &win_.push_slot();
-    } else {
-        slot = &win_[element];
-        drop_original(*slot);
-    }
-    StoredOriginal& o = *slot;
-    o.row = row;
-    o.off = off;
-    o.bytes = framed_bytes;
-    o.column = column;
-    o.header_bytes = (uint8_t)header_bytes;
-    o.owned = borrowed ? 0 : 1;
-    o.send_msec = (uint32_t)now_msec();
-    o.host = host;
-    if (o.owned || host) ++held_;
-    o.run = 1;
-    o.stride = 0;
-    if (element > 0) {
-        const StoredOriginal& p = win_[element - 1];
-        if (p.bytes == framed_bytes && o.off > p.off && p.run < 0xffff &&
-            (p.run == 1 || o.off - p.off == p.stride)) {
-            o.run = (uint16_t)(p.run + 1);
-            o.stride = o.off - p.off;
-        }
-    }
-
-    next_column_ = col_inc(next_column_);
-
-    Lane& lane = lanes_[column % kLanes];
-    if (lane.longest < framed_bytes) lane.longest = framed_bytes;
-    if (longest_ < framed_bytes) longest_ = framed_bytes;
-
-    stats_[0]++;
-    stats_[1] += payload_bytes;
-}
-
 // EncoderPacketWindow::StartNewWindow (SiameseEncoder.cpp:163-181)
 void Encoder::start_new_window(uint32_t column) {
     // Everything from the previous window is unreachable once Count reached zero (only the send
     // timestamps of its first elements stay visible to the RTT scan, see placeholder_msec_).
     for (uint32_t e = 0; e < kLanes; ++e) placeholder_msec_[e] = e < win_.size() ? win_[e].send_msec : placeholder_msec_[e];
     ++window_gen_;  // (a pending Cauchy group does not extend into the new window)
-    if (held_)
-        for (size_t i = 0; i < win_.size(); ++i) drop_original(win_[i]);
-    win_.clear();
+    drop_all();
     const uint32_t element = column % kLanes;
     column_start_ = column - element;
     sum_start_ = element;
@@ -248,18 +289,49 @@ void Encoder::remove_elements() {
         sum_start_ = sum_start_ > removed ? sum_start_ - removed : 0;
     }
 
-    if (held_)  // (borrowed rows without host copies: nothing to release)
-        for (uint32_t i = 0; i < removed && i < win_.size(); ++i) release_original(win_[i]);
+    // segments below the new window start leave (what they own is released); one that straddles
+    // it keeps its remaining packets
+    const uint32_t cut = base_ + removed;
+    while (!segs_.empty() && segs_.front().end() <= cut) {
+        const Segment& f = segs_.front();
+        if (f.owned || f.host) {
+            release_segment(f, 0, f.count);
+            --held_;
+        }
+        segs_.pop_front(1);
+        ++seg_base_;
+    }
+    if (!segs_.empty() && segs_.front().first < cut) {
+        Segment& f = segs_.front();
+        const uint32_t d = cut - f.first;
+        release_segment(f, 0, d);  // (a straddling segment holds no host copy: count > 1)
+        f.first = cut;
+        f.count -= d;
+        if (f.row0 != kNoRow) f.row0 += d;
+        f.off0 += d * f.stride;
+        f.column0 = col_add(f.column0, d);
+    }
     win_.pop_front(removed);
+    base_ = cut;
     count_ -= removed;
     column_start_ = to_column(removed);
     first_unremoved_ -= removed;
 
+    // longest packet of the unacknowledged elements, overall and per lane (segment by segment)
     uint32_t longest = 0, lane_longest[kLanes] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (uint32_t i = first_unremoved_; i < count_; ++i) {
-        const uint32_t b = win_[i].bytes;
-        if (longest < b) longest = b;
-        if (lane_longest[i % kLanes] < b) lane_longest[i % kLanes] = b;
+    if (first_unremoved_ < count_) {
+        const uint32_t lo = base_ + first_unremoved_, hi = base_ + count_;
+        for (uint32_t i = win_[first_unremoved_].seg - seg_base_; i < segs_.size(); ++i) {
+            const Segment& sg = segs_[i];
+            if (sg.first >= hi) break;
+            const uint32_t a = sg.first > lo ? sg.first : lo, b = sg.end() < hi ? sg.end() : hi;
+            if (a >= b || !sg.bytes) continue;
+            if (longest < sg.bytes) longest = sg.bytes;
+            for (uint32_t x = a; x < b && x < a + kLanes; ++x) {
+                const uint32_t l = (x - base_) % kLanes;
+                if (lane_longest[l] < sg.bytes) lane_longest[l] = sg.bytes;
+            }
+        }
     }
     longest_ = longest;
     for (unsigned l = 0; l < kLanes; ++l) lanes_[l].longest = lane_longest[l];
@@ -267,31 +339,26 @@ void Encoder::remove_elements() {
     if (sum_end_ <= sum_start_) reset_sums(first_unremoved_);
 }
 
-// EncoderPacketWindow::GetSum (SiameseEncoder.cpp:359-418), for the lane's three sums at once
+// EncoderPacketWindow::GetSum (SiameseEncoder.cpp:359-418), for the lane's three sums at once.
+// The lane's packets in a segment are every kLanes-th of it: one strided run per segment.
 LaneSums& Encoder::get_lane(uint32_t lane_index, uint32_t element_end) {
     Lane& lane = lanes_[lane_index];
     LaneSums& sums = lane.sums;
     uint32_t element = lane.next_element;
     if (element < element_end) {
         if (lane.longest > 0) sums.grow(lane.longest);
-        // The lane's last element before element_end; when the run of equal, evenly spaced
-        // packets ending there (StoredOriginal::run) reaches back to `element`, the lane's
-        // packets from here on are one strided run (every kLanes-th packet of it).
-        const uint32_t last = element + ((element_end - 1 - element) / kLanes) * kLanes;
-        const StoredOriginal& ol = win_[last];
         do {
-            const StoredOriginal& o = win_[element];
-            if (last > element && ol.run > last - element &&
-                o.column + (last - element) < kColumnPeriod) {
-                sums.grow(o.bytes);
-                sums.accumulate_run_level0(o.row, o.off, o.bytes, o.column, (last - element) / kLanes + 1,
-                                           ol.stride * kLanes);
-                element = last + kLanes;
-                break;
+            const Segment& sg = seg_of(element);
+            const uint32_t j = element + base_ - sg.first;
+            uint32_t stop = sg.end() - base_;  // window element past the segment
+            if (stop > element_end) stop = element_end;
+            const uint32_t n = (stop - 1 - element) / kLanes + 1;  // lane packets in [element, stop)
+            if (sg.bytes) {
+                sums.grow(sg.bytes);
+                sums.accumulate_run_level0(sg.row(j), sg.off(j), sg.bytes, col_add(sg.column0, j), n,
+                                           sg.stride * kLanes);
             }
-            sums.grow(o.bytes);
-            sums.accumulate_level0(o.row, o.off, o.bytes, o.column);
-            element += kLanes;
+            element += n * kLanes;
         } while (element < element_end);
         lane.next_element = element;
     }
@@ -444,17 +511,17 @@ Result Encoder::acknowledge(const uint8_t* data, uint32_t bytes, uint32_t* next_
     return kSuccess;
 }
 
-Result Encoder::attempt_retransmit(const StoredOriginal* o, const StoredOriginal** out) {
-    if (o->header_bytes == 0 || o->bytes <= o->header_bytes) { disabled_ = true; return kDisabled; }
+Result Encoder::attempt_retransmit(uint32_t e, StoredOriginal* out) {
+    const StoredOriginal o = view(e);
+    if (o.header_bytes == 0 || o.bytes <= o.header_bytes) { disabled_ = true; return kDisabled; }
     *out = o;
     stats_[4]++;
-    stats_[5] += o->bytes - o->header_bytes;
+    stats_[5] += o.bytes - o.header_bytes;
     return kSuccess;
 }
 
 // Encoder::Retransmit (SiameseEncoder.cpp:877-1044)
-Result Encoder::retransmit(const StoredOriginal** out) {
-    *out = nullptr;
+Result Encoder::retransmit(StoredOriginal* out) {
     if (disabled_) return kDisabled;
     if (unacked() == 0) {
         ack_.found_oldest = false;
@@ -470,20 +537,20 @@ Result Encoder::retransmit(const StoredOriginal** out) {
     if (ack_.found_oldest) {
         const uint32_t e = col_sub(ack_.oldest_column, column_start_);
         if (!col_delta_negative(e) && e >= first && e < count) {
-            StoredOriginal& o = win_[e];
+            Slot& o = win_[e];
             if ((uint32_t)(now - o.send_msec) < rto) return kNeedMoreData;
             o.send_msec = now;
             ack_.found_oldest = false;
-            return attempt_retransmit(&o, out);
+            return attempt_retransmit(e, out);
         }
         ack_.found_oldest = false;
     }
 
     uint32_t nack_element = first;
-    StoredOriginal* oldest = &win_[nack_element];
-    uint32_t oldest_msec = oldest->send_msec;
+    uint32_t oldest = nack_element;
+    uint32_t oldest_msec = win_[oldest].send_msec;
     if ((uint32_t)(now - oldest_msec) >= rto) {
-        oldest->send_msec = now;
+        win_[oldest].send_msec = now;
         return attempt_retransmit(oldest, out);
     }
 
@@ -493,40 +560,39 @@ Result Encoder::retransmit(const StoredOriginal** out) {
         while (next_loss_column(column)) {
             nack_element = to_element(column);
             if (nack_element >= count) break;
-            StoredOriginal& o = win_[nack_element];
+            Slot& o = win_[nack_element];
             const uint32_t last = o.send_msec;
             if ((uint32_t)(now - last) >= rto) {
                 o.send_msec = now;
-                return attempt_retransmit(&o, out);
+                return attempt_retransmit(nack_element, out);
             }
-            if ((int32_t)(oldest_msec - last) > 0) { oldest = &o; oldest_msec = last; }
+            if ((int32_t)(oldest_msec - last) > 0) { oldest = nack_element; oldest_msec = last; }
         }
     }
 
     for (uint32_t e = nack_element + 1; e < count; ++e) {
-        StoredOriginal& o = win_[e];
+        Slot& o = win_[e];
         const uint32_t last = o.send_msec;
         if ((uint32_t)(now - last) >= rto) {
             o.send_msec = now;
-            return attempt_retransmit(&o, out);
+            return attempt_retransmit(e, out);
         }
-        if ((int32_t)(oldest_msec - last) > 0) { oldest = &o; oldest_msec = last; }
+        if ((int32_t)(oldest_msec - last) > 0) { oldest = e; oldest_msec = last; }
     }
     ack_.found_oldest = true;
-    ack_.oldest_column = oldest->column;
+    ack_.oldest_column = to_column(oldest);
     return kNeedMoreData;
 }
 
 // Encoder::Get (SiameseEncoder.cpp:1256-1294)
-Result Encoder::get(uint32_t packet_num, const StoredOriginal** out) {
-    *out = nullptr;
+Result Encoder::get(uint32_t packet_num, StoredOriginal* out) {
     if (disabled_) return kDisabled;
     const uint32_t e = to_element(packet_num);
     if (e >= count_) return kNeedMoreData;
-    const StoredOriginal& o = win_[e];
+    const StoredOriginal o = view(e);
     if (o.bytes == 0) return kNeedMoreData;
     if (o.header_bytes == 0 || o.bytes <= o.header_bytes) { disabled_ = true; return kDisabled; }
-    *out = &o;
+    *out = o;
     return kSuccess;
 }
 
@@ -550,7 +616,7 @@ Result Encoder::emit(Sym& terms, uint32_t len, const RecoveryMeta& meta, Recover
 
 // Encoder::GenerateSinglePacket (SiameseEncoder.cpp:1296-1329)
 Result Encoder::generate_single(RecoveryOut& out) {
-    const StoredOriginal& o = win_[first_unremoved_];
+    const StoredOriginal o = view(first_unremoved_);
     RecoveryMeta m;
     m.SumCount = 1;
     m.LDPCCount = 1;
@@ -583,19 +649,22 @@ Result Encoder::generate_cauchy(RecoveryOut& out) {
         mode = TAMD_R_CAUCHY;  // CauchyElement(crow, column mod 64)
     }
 
-    // The window's originals (level-0 rows) in runs of equal length at a fixed row stride,
-    // tracked at add time: one ACCR per run, found by walking the window back run by run.
+    // The window's originals (level-0 rows): one ACCR per segment (a run of equally long packets
+    // at a fixed row stride), clipped to the unacknowledged range.
     std::vector<Run>& runs = runs_;
     runs.clear();
     uint32_t used = 0;
-    for (uint32_t e = count_; e > first;) {
-        const StoredOriginal& last = win_[e - 1];
-        uint32_t r = last.run;
-        if (r > e - first) r = e - first;
-        const StoredOriginal& head = win_[e - r];
-        if (used < last.bytes) used = last.bytes;
-        runs.push_back(Run{head.row, head.off, last.stride, r, last.bytes, head.column});
-        e -= r;
+    {
+        const uint32_t lo = base_ + first, hi = base_ + count_;
+        for (uint32_t i = win_[first].seg - seg_base_; i < segs_.size(); ++i) {
+            const Segment& sg = segs_[i];
+            if (sg.first >= hi) break;
+            const uint32_t a = sg.first > lo ? sg.first : lo, b = sg.end() < hi ? sg.end() : hi;
+            if (a >= b || !sg.bytes) continue;
+            const uint32_t j = a - sg.first;
+            if (used < sg.bytes) used = sg.bytes;
+            runs.push_back(Run{sg.row(j), sg.off(j), sg.stride, b - a, sg.bytes, col_add(sg.column0, j)});
+        }
     }
 
     out.meta = m;
@@ -719,10 +788,10 @@ void Encoder::add_light(uint32_t row, Sym& rec) {
     for (uint32_t i = 0; i < pairs; ++i) {
         const uint32_t e1 = start + mod(prng.next());
         const uint32_t erx = start + mod(prng.next());
-        const StoredOriginal& o1 = win_[e1];
-        const StoredOriginal& orx = win_[erx];
-        t[2 * i] = Term{o1.row, o1.bytes, 1};
-        t[2 * i + 1] = Term{orx.row, orx.bytes, rx};
+        const Segment& s1 = seg_of(e1);
+        const Segment& srx = seg_of(erx);
+        t[2 * i] = Term{s1.row(e1 + base_ - s1.first), s1.bytes, 1};
+        t[2 * i + 1] = Term{srx.row(erx + base_ - srx.first), srx.bytes, rx};
     }
 }
 

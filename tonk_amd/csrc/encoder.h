@@ -49,6 +49,33 @@ struct StoredOriginal {
 
 typedef void (*HostRelease)(void* host, void* user);
 
+// Whether rows[0..k) are consecutive handles (rows[j] == rows[0] + j).
+inline bool consecutive_handles(const RowId* rows, uint32_t k) {
+    uint32_t bad = 0;
+    for (uint32_t j = 0; j < k; ++j) bad |= rows[j] ^ (rows[0] + j);
+    return bad == 0;
+}
+
+// A run of consecutive window elements stored as one record ("segment"): equally long framed
+// packets whose rows sit at fixed handle and arena strides (row0 + j, off0 + j * stride), none of
+// them with a host copy -- a stream's originals added in batches are one segment per stretch
+// between events, so adding k of them is O(1) records instead of k.  Any other element (a host
+// copy, the C ABI's single adds, placeholders of a restarted window) is a segment of one.
+struct Segment {
+    uint32_t first = 0;   // absolute element number of the first packet (window element + base)
+    uint32_t count = 0;
+    RowId row0 = kNoRow;  // kNoRow: placeholders (no packet)
+    uint32_t off0 = 0, stride = 0;  // arena offsets in 64-B units; stride 0 when count is 1
+    uint32_t bytes = 0;   // framed bytes of every packet (0: placeholder)
+    uint32_t column0 = 0; // packet number of the first packet (a segment never wraps the period)
+    uint8_t header_bytes = 0;
+    uint8_t owned = 0;    // the codec frees the rows when they leave the window
+    void* host = nullptr; // count 1 only
+    uint32_t end() const { return first + count; }
+    RowId row(uint32_t j) const { return row0 == kNoRow ? kNoRow : row0 + j; }
+    uint32_t off(uint32_t j) const { return off0 + j * stride; }
+};
+
 class Encoder : public FlushClient {
 public:
     Encoder(Context* ctx, uint32_t row_bytes, HostRelease release = nullptr, void* user = nullptr);
@@ -66,10 +93,11 @@ public:
     // add() calls.  Returns false, with nothing done, when one of those calls would not succeed.
     bool add_run(const RowId* rows, uint32_t k, uint32_t framed_bytes, uint32_t header_bytes,
                  uint32_t payload_bytes, bool borrowed, uint32_t* first_col);
-    Result get(uint32_t packet_num, const StoredOriginal** out);
+    // siamese_encoder_get / _retransmit: the packet as a value (row, lengths, column, host copy)
+    Result get(uint32_t packet_num, StoredOriginal* out);
     void remove_before(uint32_t first_kept_column);
     Result acknowledge(const uint8_t* data, uint32_t bytes, uint32_t* next_expected);
-    Result retransmit(const StoredOriginal** out);
+    Result retransmit(StoredOriginal* out);
     // siamese_encode.  On success `out.row` is owned by the caller (free it with
     // ctx->rows.free_deferred once nothing reads it).
     Result encode(RecoveryOut& out);
@@ -96,10 +124,27 @@ private:
     bool disabled_ = false;
     const uint64_t* clock_ = nullptr;
     uint64_t now_msec() const;
-    void release_original(const StoredOriginal& o);  // frees what the slot owns (slot left as is)
 
     // ---- EncoderPacketWindow (SiameseEncoder.h:104-232) ----
-    Ring<StoredOriginal> win_;
+    // Elements are stored as segments (Segment, above); per element only its segment number and
+    // its send time (retransmit moves single elements' send times).
+    struct Slot { uint32_t seg, send_msec; };
+    Ring<Slot> win_;
+    Ring<Segment> segs_;       // in element order; segs_[i] is segment number seg_base_ + i
+    uint32_t seg_base_ = 0;    // number of the segment at segs_[0]
+    uint32_t base_ = 0;        // absolute element number of window element 0
+    const Segment& seg_of(uint32_t e) const { return segs_[win_[e].seg - seg_base_]; }
+    RowId row_of(uint32_t e) const {
+        const Segment& s = seg_of(e);
+        return s.row(e + base_ - s.first);
+    }
+    StoredOriginal view(uint32_t e) const;  // element e as a value (get / retransmit)
+    // Append k packets (rows[0..k), equally long) at the window end, extending the last segment
+    // while the rows continue its strides; `now` is their send time.
+    void append(const RowId* rows, uint32_t k, uint32_t framed_bytes, uint32_t header_bytes, uint8_t owned,
+                void* host, uint32_t now);
+    void release_segment(const Segment& s, uint32_t from, uint32_t n);  // rows [from, from + n) of s
+    void drop_all();                                // release every segment, empty window
     // Send timestamps the placeholder elements of a restarted window read: the reference keeps
     // them in its subwindows' LastSendMsec arrays (SiameseEncoder.h:96), which a window restart
     // (StartNewWindow, SiameseEncoder.cpp:163) does not clear, so an RTT scan that starts on a
@@ -107,7 +152,7 @@ private:
     // previous window's send time at that element, not zero.
     uint32_t placeholder_msec_[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t next_column_ = 0, count_ = 0, column_start_ = 0, longest_ = 0;
-    uint32_t held_ = 0;  // window slots with something to release (an owned row or a host copy)
+    uint32_t held_ = 0;  // segments with something to release (owned rows or a host copy)
     uint32_t first_unremoved_ = 0;
     uint32_t sum_start_ = 0, sum_end_ = 0, sum_column_start_ = 0, sum_erased_ = 0;
     // The reference advances each of a lane's three sums lazily on its own; their values only
@@ -135,7 +180,6 @@ private:
     uint32_t to_element(uint32_t column) const { return col_sub(column, column_start_); }
     uint32_t to_column(uint32_t element) const { return col_add(element, column_start_); }
     uint32_t unacked() const { return count_ - first_unremoved_; }
-    StoredOriginal& elem(uint32_t e) { return win_[e]; }
 public:
     // Diagnostics (the C ABI watchdog): window and acknowledgement state in one line.
     int debug_state(char* buf, size_t n) const {
@@ -155,9 +199,9 @@ private:
         return n;
     }
 
-    void drop_original(StoredOriginal& o);
-    void add_unchecked(RowId row, uint32_t off, uint32_t framed_bytes, uint32_t header_bytes, uint32_t payload_bytes,
-                       void* host, uint32_t* packet_num, bool borrowed);
+    // The first packet of an add (starts a window when it is empty); returns its column.
+    uint32_t add_first(RowId row, uint32_t framed_bytes, uint32_t header_bytes, uint32_t payload_bytes, void* host,
+                       bool borrowed);
     void start_new_window(uint32_t column);
     void reset_sums(uint32_t element_start);
     void remove_elements();
@@ -169,7 +213,7 @@ private:
     bool on_ack_data(const uint8_t* data, uint32_t bytes);
     void update_rto();
     void rtt_update(uint32_t value, uint64_t now, uint64_t window);
-    Result attempt_retransmit(const StoredOriginal* o, const StoredOriginal** out);
+    Result attempt_retransmit(uint32_t e, StoredOriginal* out);
 
     Result generate_single(RecoveryOut& out);
     Result generate_cauchy(RecoveryOut& out);

@@ -46,6 +46,7 @@ void RowTable::init(uint64_t arena_bytes, uint64_t base_units) {
 }
 
 RowId RowTable::alloc(uint32_t bytes) {
+    TAMD_PROF_SCOPE(kAlloc);
     uint32_t units = (bytes + TAMD_ROW_UNIT - 1) / TAMD_ROW_UNIT;
     if (units == 0) units = 1;
     uint32_t off = 0xffffffffu;
@@ -344,6 +345,7 @@ uint32_t ProgramBuilder::end_op(uint32_t min_level) {
 
 uint32_t ProgramBuilder::combine(RowId dst, const Term* terms, size_t n, uint32_t len,
                                  const uint8_t* footer, uint32_t footer_len) {
+    TAMD_PROF_SCOPE(kCombine);
     begin_op();
     // inline op_acc over the term list: one resize, then straight stores
     const size_t at = instrs_.size();
@@ -514,6 +516,7 @@ static inline bool same_coefs(const uint8_t* a, const uint8_t* b) {
 
 void LaneSums::read(RowTable& rows, const ExpansionTable& ex, Sym& out, const uint8_t* c, uint32_t limit) {
     if (!limit || (!c[0] && !c[1] && !c[2])) return;
+    TAMD_PROF_SCOPE(kLaneRead);
     const uint32_t clip = content_ < limit ? content_ : limit;
     if (!terms_.empty()) {
         const uint32_t at = n_;
@@ -531,6 +534,7 @@ void LaneSums::read(RowTable& rows, const ExpansionTable& ex, Sym& out, const ui
         for (unsigned s = 0; s < 3; ++s)
             if (base_[s] != kNoRow && c[s]) out.push_back(Term{base_[s], clip, c[s]});
     }
+    TAMD_PROF_SCOPE(kLaneDyn);
     for (const T& d : dyn_) {
         const uint32_t l = d.len < limit ? d.len : limit;
         const uint8_t cx = column_value(d.col);

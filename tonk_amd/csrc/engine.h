@@ -109,6 +109,16 @@ public:
     void seal_epoch(uint64_t epoch);  // rows freed so far belong to `epoch`
 
     uint32_t offset(RowId r) const { return off_[r]; }  // 64-B units from the arena base
+    // Whether rows r0 .. r0 + k - 1 are live handles at offsets off(r0) + j * stride (a run of
+    // rows laid out in order, as a session's inputs are): one contiguous scan of the offsets.
+    bool affine(RowId r0, uint32_t k, uint32_t stride) const {
+        if ((size_t)r0 + k > off_.size()) return false;
+        const uint32_t* o = off_.data() + r0;
+        const uint32_t o0 = o[0];
+        uint32_t bad = 0;
+        for (uint32_t j = 0; j < k; ++j) bad |= o[j] ^ (o0 + j * stride);
+        return bad == 0;
+    }
     uint32_t cap_bytes(RowId r) const { return units_[r] * TAMD_ROW_UNIT; }
     uint32_t units(RowId r) const { return units_[r]; }
     // Only rows written by the pending program have a level; a bitmap keeps the common case

@@ -11,7 +11,7 @@ namespace prof {
 enum Slot {
     kEncAdd, kEncEncode, kEncAck, kDecAddOrig, kDecAddRec, kDecDecode, kDecAck, kDecIsReady,
     kGenMatrix, kGE, kElim, kLowerTri, kBackSub, kChainFlush, kSymMerge, kFlushAll, kFinish, kRelease,
-    kEncDense, kEncLight, kEncEmit, kElimSums, kElimPairs, kElimFold, kEncCauchy, kEncRemove, kElimStart, kSlots
+    kEncDense, kEncLight, kEncEmit, kElimSums, kElimPairs, kElimFold, kEncCauchy, kEncRemove, kElimStart, kLaneRead, kLaneDyn, kCombine, kFoldMerge, kAlloc, kSlots
 };
 extern thread_local uint64_t cycles[kSlots];
 extern thread_local uint64_t calls[kSlots];
@@ -24,7 +24,9 @@ struct Scope {
 };
 }  // namespace prof
 }  // namespace tamd
-#define TAMD_PROF_SCOPE(slot) ::tamd::prof::Scope tamd_prof_scope_##__LINE__(::tamd::prof::slot)
+#define TAMD_PROF_CAT2(a, b) a##b
+#define TAMD_PROF_CAT(a, b) TAMD_PROF_CAT2(a, b)
+#define TAMD_PROF_SCOPE(slot) ::tamd::prof::Scope TAMD_PROF_CAT(tamd_prof_scope_, __LINE__)(::tamd::prof::slot)
 #else
 #define TAMD_PROF_SCOPE(slot) do {} while (0)
 #endif

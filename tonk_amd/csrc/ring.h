@@ -9,6 +9,10 @@ template <class T>
 class Ring {
 public:
     size_t size() const { return n_; }
+    bool empty() const { return n_ == 0; }
+    T& back() { return buf_[(head_ + n_ - 1) & mask_]; }
+    const T& back() const { return buf_[(head_ + n_ - 1) & mask_]; }
+    T& front() { return buf_[head_]; }
     T& operator[](size_t i) { return buf_[(head_ + i) & mask_]; }
     const T& operator[](size_t i) const { return buf_[(head_ + i) & mask_]; }
     void push_back(const T& v) {
