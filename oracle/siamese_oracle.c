@@ -463,8 +463,8 @@ int oracle_recovery_row(const oracle_recovery_meta* m, oracle_get_row_fn get_row
    restated here (not included) so this file stays a stand-alone checker.
    ------------------------------------------------------------------------------------------ */
 enum { I_ACC = 1, I_STORE = 2, I_FOOTER = 3, I_CLEAR = 4, I_ACC3 = 5, I_STOREC = 6, I_ACCR = 7, I_RANGE = 8,
-       I_TARGETS = 9 };
-enum { R_LANE3 = 1, R_CAUCHY = 2, R_CONST = 3, R_MULTI = 4 };
+       I_TARGETS = 9, I_COEFS = 10 };
+enum { R_LANE3 = 1, R_CAUCHY = 2, R_CONST = 3, R_MULTI = 4, R_DENSE = 5 };
 
 /* Each op owns three accumulators of `span` bytes (program.h):
      ACC   w0 = 1 | coef << 8 | a << 16       acc_a ^= coef * row[0:len]
@@ -479,7 +479,10 @@ enum { R_LANE3 = 1, R_CAUCHY = 2, R_CONST = 3, R_MULTI = 4 };
            CONST: acc_0 ^= p*row_k
            MULTI: then TARGETS w0 = 9, t_0, t_1, t_2 with t_a = kind | p << 2 | lo << 10 | hi << 21: for
            lo <= k < hi,
-           kind CAUCHY: acc_a ^= CauchyElement(p, col_k mod 64)*row_k, kind CONST: acc_a ^= row_k */
+           kind CAUCHY: acc_a ^= CauchyElement(p, col_k mod 64)*row_k, kind CONST: acc_a ^= row_k
+           DENSE: then COEFS w0 = 10, o[0:32], o[32:48] | rx << 16: with b = (o >> 6*(col_k mod 8)) & 63
+           and cx = CX(col_k), acc_0 ^= (b0 ^ b1 cx ^ b2 cx^2 ^ rx (b3 ^ b4 cx ^ b5 cx^2)) * row_k, the
+           lane-sum combination of a Siamese row (SiameseEncoder.cpp:1046-1098) packet by packet */
 int oracle_run_program(uint8_t* arena, size_t arena_bytes,
                        const uint32_t* ops, unsigned n_ops,
                        const uint32_t* instrs, unsigned n_instrs)
@@ -526,10 +529,10 @@ int oracle_run_program(uint8_t* arena, size_t arena_bytes,
                 const uint32_t len = w[2], n = w[3], stride = r[1], col0 = r[2], cstep = r[3];
                 if (len > span) { free(acc); return -12; }
                 const uint32_t* tg = NULL;
-                if (mode == R_MULTI) {
+                if (mode == R_MULTI || mode == R_DENSE) {
                     if (k + 2 >= count) { free(acc); return -15; }
                     tg = w + 8;
-                    if ((tg[0] & 0xff) != I_TARGETS) { free(acc); return -16; }
+                    if ((tg[0] & 0xff) != (mode == R_MULTI ? I_TARGETS : I_COEFS)) { free(acc); return -16; }
                 }
                 for (uint32_t e = 0; e < n; ++e) {
                     const size_t base = ((size_t)w[1] + (size_t)e * stride) * 64u;
@@ -545,6 +548,15 @@ int oracle_run_program(uint8_t* arena, size_t arena_bytes,
                         oracle_muladd_mem(acc, oracle_cauchy_element(p, col % 64u), row, len);
                     } else if (mode == R_CONST) {
                         oracle_muladd_mem(acc, (uint8_t)p, row, len);
+                    } else if (mode == R_DENSE) {
+                        const uint64_t ow = (uint64_t)tg[1] | ((uint64_t)(tg[2] & 0xffffu) << 32);
+                        const uint8_t rx = (uint8_t)(tg[2] >> 16);
+                        const unsigned b = (unsigned)(ow >> (6u * (col % 8u))) & 63u;
+                        const uint8_t cx = oracle_column_value(col), cx2 = oracle_gf_sqr(cx);
+                        const uint8_t sdir = (uint8_t)((b & 1u) ^ ((b & 2u) ? cx : 0u) ^ ((b & 4u) ? cx2 : 0u));
+                        const uint8_t tprod = (uint8_t)(((b >> 3) & 1u) ^ ((b & 16u) ? cx : 0u) ^ ((b & 32u) ? cx2 : 0u));
+                        const uint8_t g = (uint8_t)(sdir ^ oracle_gf_mul(rx, tprod));
+                        if (g) oracle_muladd_mem(acc, g, row, len);
                     } else if (mode == R_MULTI) {
                         for (unsigned a = 0; a < 3; ++a) {
                             const uint32_t t = tg[1 + a], kind = t & 3, tp = (t >> 2) & 0xff;
@@ -558,7 +570,7 @@ int oracle_run_program(uint8_t* arena, size_t arena_bytes,
                         free(acc); return -14;
                     }
                 }
-                k += mode == R_MULTI ? 2 : 1; /* consumed the RANGE (and TARGETS) word */
+                k += (mode == R_MULTI || mode == R_DENSE) ? 2 : 1; /* consumed RANGE (and TARGETS / COEFS) */
             } else if (kind == I_STOREC) {
                 const uint8_t c[3] = { (uint8_t)(w[0] >> 8), (uint8_t)(w[0] >> 16), (uint8_t)(w[0] >> 24) };
                 const size_t base = (size_t)w[1] * 64u;

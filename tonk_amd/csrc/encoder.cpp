@@ -26,7 +26,7 @@ uint64_t time_msec() {
 Encoder::Encoder(Context* ctx, uint32_t row_bytes, HostRelease release, void* user)
     : ctx_(ctx), row_bytes_(row_bytes), release_(release), user_(user) {
     // ClearWindow (SiameseEncoder.cpp:64-83)
-    for (unsigned l = 0; l < kLanes; ++l) lanes_[l].next_element = l;
+    for (unsigned l = 0; l < kLanes; ++l) lanes_[l].next_abs = l;
     ctx_->attach(this);
 }
 
@@ -264,35 +264,18 @@ void Encoder::remove_before(uint32_t first_kept_column) {
 // EncoderPacketWindow::ResetSums (SiameseEncoder.cpp:218-237)
 void Encoder::reset_sums(uint32_t element_start) {
     for (unsigned l = 0; l < kLanes; ++l) {
-        lanes_[l].next_element = next_lane_element(element_start, l);
+        lanes_[l].next_abs = base_ + next_lane_element(element_start, l);
         lanes_[l].sums.reset(ctx_->rows);
     }
     sum_start_ = element_start;
     sum_end_ = element_start;
     sum_column_start_ = to_column(element_start);
     sum_erased_ = 0;
+    drop_segments_below(base_);  // (segments kept for the previous sums)
 }
 
-// EncoderPacketWindow::RemoveElements (SiameseEncoder.cpp:239-357)
-void Encoder::remove_elements() {
-    TAMD_PROF_SCOPE(kEncRemove);
-    const uint32_t first_kept_sub = first_unremoved_ / kSubwindow;
-    const uint32_t removed = first_kept_sub * kSubwindow;
-
-    if (sum_end_ > sum_start_) {
-        for (unsigned l = 0; l < kLanes; ++l) {
-            get_lane(l, removed);
-            lanes_[l].next_element -= removed;
-        }
-        if (removed > sum_start_) sum_erased_ += removed - sum_start_;
-        sum_end_ = sum_end_ > removed ? sum_end_ - removed : 0;
-        sum_start_ = sum_start_ > removed ? sum_start_ - removed : 0;
-    }
-
-    // segments below the new window start leave (what they own is released); one that straddles
-    // it keeps its remaining packets
-    const uint32_t cut = base_ + removed;
-    while (!segs_.empty() && segs_.front().end() <= cut) {
+void Encoder::drop_segments_below(uint32_t drop) {
+    while (!segs_.empty() && (int32_t)(segs_.front().end() - drop) <= 0) {
         const Segment& f = segs_.front();
         if (f.owned || f.host) {
             release_segment(f, 0, f.count);
@@ -301,16 +284,41 @@ void Encoder::remove_elements() {
         segs_.pop_front(1);
         ++seg_base_;
     }
-    if (!segs_.empty() && segs_.front().first < cut) {
+    if (!segs_.empty() && (int32_t)(segs_.front().first - drop) < 0) {
         Segment& f = segs_.front();
-        const uint32_t d = cut - f.first;
+        const uint32_t d = drop - f.first;
         release_segment(f, 0, d);  // (a straddling segment holds no host copy: count > 1)
-        f.first = cut;
+        f.first = drop;
         f.count -= d;
         if (f.row0 != kNoRow) f.row0 += d;
         f.off0 += d * f.stride;
         f.column0 = col_add(f.column0, d);
     }
+}
+
+// EncoderPacketWindow::RemoveElements (SiameseEncoder.cpp:239-357)
+void Encoder::remove_elements() {
+    TAMD_PROF_SCOPE(kEncRemove);
+    const uint32_t first_kept_sub = first_unremoved_ / kSubwindow;
+    const uint32_t removed = first_kept_sub * kSubwindow;
+
+    // While the running sums are active, the lanes accumulate lazily (the reference advances them
+    // here, GetSum up to the removed elements): the segments of the sum range are kept -- with the
+    // rows they own -- until the sums reset, so a later lane read (or a direct dense read) still
+    // finds every packet of the range.
+    const uint32_t cut = base_ + removed;
+    uint32_t drop = cut;
+    if (sum_end_ > sum_start_) {
+        const uint32_t keep = sum_abs_start();
+        if ((int32_t)(keep - drop) < 0) drop = keep;
+        if (removed > sum_start_) sum_erased_ += removed - sum_start_;
+        sum_end_ = sum_end_ > removed ? sum_end_ - removed : 0;
+        sum_start_ = sum_start_ > removed ? sum_start_ - removed : 0;
+    }
+
+    // segments below `drop` leave (what they own is released); one that straddles it keeps its
+    // later packets
+    drop_segments_below(drop);
     win_.pop_front(removed);
     base_ = cut;
     count_ -= removed;
@@ -340,27 +348,30 @@ void Encoder::remove_elements() {
 }
 
 // EncoderPacketWindow::GetSum (SiameseEncoder.cpp:359-418), for the lane's three sums at once.
-// The lane's packets in a segment are every kLanes-th of it: one strided run per segment.
+// The lane's packets in a segment are every kLanes-th of it: one strided run per segment.  The
+// lane may start before the window (segments kept for the sums, remove_elements).
 LaneSums& Encoder::get_lane(uint32_t lane_index, uint32_t element_end) {
     Lane& lane = lanes_[lane_index];
     LaneSums& sums = lane.sums;
-    uint32_t element = lane.next_element;
-    if (element < element_end) {
+    uint32_t a = lane.next_abs;
+    const uint32_t end = base_ + element_end;
+    if ((int32_t)(end - a) > 0) {
         if (lane.longest > 0) sums.grow(lane.longest);
+        size_t si = seg_index_at(a);
         do {
-            const Segment& sg = seg_of(element);
-            const uint32_t j = element + base_ - sg.first;
-            uint32_t stop = sg.end() - base_;  // window element past the segment
-            if (stop > element_end) stop = element_end;
-            const uint32_t n = (stop - 1 - element) / kLanes + 1;  // lane packets in [element, stop)
+            const Segment& sg = segs_[si];
+            const uint32_t j = a - sg.first;
+            const uint32_t stop = (int32_t)(sg.end() - end) < 0 ? sg.end() : end;
+            const uint32_t n = (stop - 1 - a) / kLanes + 1;  // lane packets in [a, stop)
             if (sg.bytes) {
                 sums.grow(sg.bytes);
                 sums.accumulate_run_level0(sg.row(j), sg.off(j), sg.bytes, col_add(sg.column0, j), n,
                                            sg.stride * kLanes);
             }
-            element += n * kLanes;
-        } while (element < element_end);
-        lane.next_element = element;
+            a += n * kLanes;
+            while (si + 1 < segs_.size() && (int32_t)(segs_[si].end() - a) <= 0) ++si;
+        } while ((int32_t)(end - a) > 0);
+        lane.next_abs = a;
     }
     return sums;
 }
@@ -770,6 +781,30 @@ void Encoder::add_dense(uint32_t row, uint32_t recovery_bytes, Sym& rec) {
     sum_end_ = count_;
 }
 
+// AddDenseColumns straight from the packets: the lane sums a Siamese row reads are sums over the
+// packets of its sum range, so the row's dense part is one DENSE run per segment of that range
+// (program.h), each packet weighted by its lane's opcode combination -- no lane walk, snapshot
+// or carried sum.  Bytes are the same: a lane sum is its packets zero-padded to the longest, and
+// each packet is clipped to the recovery length as the sum would be.
+void Encoder::add_dense_direct(uint32_t row, uint32_t recovery_bytes) {
+    uint64_t ops = 0;
+    for (unsigned l = 0; l < kLanes; ++l) ops |= (uint64_t)row_opcode(l, row) << (6 * l);
+    const uint8_t rx = row_value(row);
+    const uint32_t lo = sum_abs_start(), hi = base_ + count_;
+    ProgramBuilder& pb = ctx_->pb;
+    for (size_t i = seg_index_at(lo); i < segs_.size(); ++i) {
+        const Segment& sg = segs_[i];
+        if ((int32_t)(sg.first - hi) >= 0) break;
+        const uint32_t a = (int32_t)(sg.first - lo) > 0 ? sg.first : lo;
+        const uint32_t b = (int32_t)(sg.end() - hi) < 0 ? sg.end() : hi;
+        if ((int32_t)(b - a) <= 0 || !sg.bytes) continue;
+        const uint32_t j = a - sg.first;
+        const uint32_t len = sg.bytes < recovery_bytes ? sg.bytes : recovery_bytes;
+        pb.op_accr_dense(sg.off(j), sg.stride, b - a, len, col_add(sg.column0, j), ops, rx);
+    }
+    sum_end_ = count_;
+}
+
 // Encoder::AddLightColumns (SiameseEncoder.cpp:1100-1144).  The product half goes straight into
 // the row with its RX factor (the reference multiplies the product buffer by RX and adds it,
 // :1236-1240; both are clipped to the same length, and every window packet is at most
@@ -820,9 +855,19 @@ Result Encoder::encode(RecoveryOut& out) {
     const uint32_t recovery_bytes = longest_;
     Sym& rec = rec_;
     rec.clear();
-    {
+    // Short sum ranges (the usual case with acknowledgements: each Siamese row follows a sum
+    // reset) are read straight from the packets; long ones through the running lane sums.
+    static const uint32_t direct_max = getenv("TONK_AMD_DIRECT") ? (uint32_t)atoi(getenv("TONK_AMD_DIRECT"))
+                                                                  : kDirectMax;
+    static const int direct_mode = getenv("TONK_AMD_DIRECT_MODE") ? atoi(getenv("TONK_AMD_DIRECT_MODE")) : 0;
+    const uint32_t range = count_ + sum_erased_ - sum_start_;
+    const bool fresh = sum_end_ == sum_start_;
+    const bool direct = range <= direct_max && (direct_mode == 0 || fresh || (direct_mode == 2 && range <= 128));
+    if (!direct) {
         TAMD_PROF_SCOPE(kEncDense);
         add_dense(row, recovery_bytes, rec);
+    } else {
+        sum_end_ = count_;
     }
     {
         TAMD_PROF_SCOPE(kEncLight);
@@ -834,6 +879,22 @@ Result Encoder::encode(RecoveryOut& out) {
     m.LDPCCount = un;
     m.ColumnStart = sum_column_start_;
     m.Row = row;
+    if (direct) {
+        // one op: the dense runs, the LDPC pairs, the store
+        out.meta = m;
+        out.footer_len = put_recovery_footer(m, out.footer);
+        out.data_len = recovery_bytes;
+        out.row = ctx_->alloc(recovery_bytes + out.footer_len);
+        if (out.row == kNoRow) { disabled_ = true; return kDisabled; }
+        ProgramBuilder& pb = ctx_->pb;
+        pb.begin_op();
+        add_dense_direct(row, recovery_bytes);
+        for (const Term& t : rec) pb.op_acc(t.row, t.coef, t.len);
+        pb.finish_combine(out.row, recovery_bytes, out.footer, out.footer_len);
+        stats_[2]++;
+        stats_[3] += out.total();
+        return kSuccess;
+    }
     // Every term is within recovery_bytes already (lane reads clip to it, packets are at most
     // longest_).  Terms are not merged: the lane snapshots are distinct rows, and a packet the
     // LDPC pairs name twice just becomes two reads (GF(2^8) sums are linear), which costs the

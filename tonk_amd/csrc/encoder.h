@@ -139,12 +139,22 @@ private:
         return s.row(e + base_ - s.first);
     }
     StoredOriginal view(uint32_t e) const;  // element e as a value (get / retransmit)
+    // Index in segs_ of the segment holding absolute element `a` (segments below the window are
+    // kept while the running sums may still need them, see remove_elements).
+    size_t seg_index_at(uint32_t a) const {
+        if ((int32_t)(a - base_) >= 0) return win_[a - base_].seg - seg_base_;
+        size_t i = 0;
+        while (i + 1 < segs_.size() && (int32_t)(segs_[i].end() - a) <= 0) ++i;
+        return i;
+    }
+    uint32_t sum_abs_start() const { return base_ + sum_start_ - sum_erased_; }  // first element of the sums
     // Append k packets (rows[0..k), equally long) at the window end, extending the last segment
     // while the rows continue its strides; `now` is their send time.
     void append(const RowId* rows, uint32_t k, uint32_t framed_bytes, uint32_t header_bytes, uint8_t owned,
                 void* host, uint32_t now);
     void release_segment(const Segment& s, uint32_t from, uint32_t n);  // rows [from, from + n) of s
     void drop_all();                                // release every segment, empty window
+    void drop_segments_below(uint32_t drop);        // release segments (parts) below absolute `drop`
     // Send timestamps the placeholder elements of a restarted window read: the reference keeps
     // them in its subwindows' LastSendMsec arrays (SiameseEncoder.h:96), which a window restart
     // (StartNewWindow, SiameseEncoder.cpp:163) does not clear, so an RTT scan that starts on a
@@ -158,7 +168,7 @@ private:
     // The reference advances each of a lane's three sums lazily on its own; their values only
     // depend on the element they are read at (always Count), so one position per lane suffices.
     struct Lane {
-        uint32_t next_element = 0;
+        uint32_t next_abs = 0;  // absolute element number of the lane's next packet to accumulate
         LaneSums sums;
         uint32_t longest = 0;
     } lanes_[kLanes];
@@ -218,6 +228,7 @@ private:
     Result generate_single(RecoveryOut& out);
     Result generate_cauchy(RecoveryOut& out);
     void add_dense(uint32_t row, uint32_t recovery_bytes, Sym& rec);
+    void add_dense_direct(uint32_t row, uint32_t recovery_bytes);  // (into the op under construction)
     void add_light(uint32_t row, Sym& rec);
     Result emit(Sym& terms, uint32_t len, const RecoveryMeta& meta, RecoveryOut& out, bool distinct);
     Sym scratch_, rec_;
@@ -236,6 +247,9 @@ private:
     // Union of a group's windows, in packets (within the 11-bit run indices of TARGETS, and short
     // enough that the group stays below the executor's shared-combine class).
     static const uint32_t kGroupSpan = 32;
+    // Siamese rows whose sum range is at most this many packets read it straight from the packets
+    // (add_dense_direct); longer ones through the running lane sums (TONK_AMD_DIRECT overrides).
+    static const uint32_t kDirectMax = 512;
     CauchyTarget grp_[3];
     uint32_t grp_n_ = 0, grp_gen_ = 0, window_gen_ = 0;
     std::vector<Run> grp_union_;

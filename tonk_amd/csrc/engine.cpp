@@ -214,6 +214,32 @@ void ProgramBuilder::op_accr_multi(uint32_t row0, uint32_t stride, uint32_t coun
     acc_bytes_ += (uint64_t)len * count;
 }
 
+void ProgramBuilder::op_accr_dense(uint32_t row0, uint32_t stride, uint32_t count, uint32_t len, uint32_t col0,
+                                   uint64_t ops, uint8_t rx) {
+    if (!len || !count) return;
+    tamd_instr a, r, g;
+    a.w0 = tamd_w0(TAMD_I_ACCR, TAMD_R_DENSE, 0);
+    a.row = row0;
+    a.len = len;
+    a.cap = count;
+    r.w0 = TAMD_I_RANGE;
+    r.row = stride;
+    r.len = col0;
+    r.cap = 1;
+    g.w0 = TAMD_I_COEFS;
+    g.row = (uint32_t)ops;
+    g.len = (uint32_t)(ops >> 32) & 0xffffu;
+    g.len |= (uint32_t)rx << 16;
+    g.cap = 0;
+    instrs_.push_back(a);
+    instrs_.push_back(r);
+    instrs_.push_back(g);
+    ++cur_runs_;  // (acc_0 only: the op stays a pure combine)
+    if (len > cur_span_) cur_span_ = len;
+    if (len < cur_full_) cur_full_ = len;
+    acc_bytes_ += (uint64_t)len * count;
+}
+
 uint32_t ProgramBuilder::finish_combine(RowId dst, uint32_t len, const uint8_t* footer, uint32_t footer_len) {
     const uint32_t cap = rows_->cap_bytes(dst);
     push_store(instrs_, rows_->offset(dst), len, cap, footer, footer_len);

@@ -176,6 +176,10 @@ public:
     // MULTI run: targets t[a] = kind | p << 8 | hi << 16 accumulate into acc_a (program.h).
     void op_accr_multi(uint32_t row0, uint32_t stride, uint32_t count, uint32_t len, uint32_t col0, uint32_t cstep,
                        const uint32_t t[3]);
+    // DENSE run: a Siamese row's dense part over a run of level-0 packets (program.h); `ops` holds
+    // the row's 8 lane opcodes, 6 bits each.
+    void op_accr_dense(uint32_t row0, uint32_t stride, uint32_t count, uint32_t len, uint32_t col0, uint64_t ops,
+                       uint8_t rx);
     // STORE (+FOOTER) of acc_0 into dst and close the op (the tail of combine()).
     uint32_t finish_combine(RowId dst, uint32_t len, const uint8_t* footer, uint32_t footer_len);
     void op_store(RowId dst, uint32_t len, uint32_t acc = 0, const uint8_t* footer = nullptr, uint32_t footer_len = 0);

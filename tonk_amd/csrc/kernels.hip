@@ -376,6 +376,64 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
 #undef TAMD_MULTI_TARGET
         unit += (count + TAMD_RBATCH - 1) / TAMD_RBATCH;
         return;
+    } else if (mode == TAMD_R_DENSE) {
+        // A Siamese row's dense part packet by packet (program.h DENSE): row k's coefficient is the
+        // lane-sum combination the recovery row reads, from its lane's opcode bits, cx and rx --
+        // wave-uniform scalar work per row, then one product per byte as in a Cauchy run.
+        const u64 opw = (u64)tg.row | ((u64)(tg.len & 0xffffu) << 32);
+        const PermT prx = perm_at(lds, ((tg.len >> 16) & 0xffu) * 8u);
+        const uint8_t* sqr = (const uint8_t*)(lds + TAMD_LDS_INV + 64u);
+        uint32_t col = col0;
+        const uint32_t cs = cstep;
+        auto coef = [&](uint32_t c) -> uint32_t {
+            const uint32_t b = (uint32_t)(opw >> (6u * (c & 7u))) & 63u;
+            const uint32_t cx = 3u + (199u * (c % 253u)) % 253u, cx2 = sqr[cx];
+            const uint32_t sd = (b & 1u) ^ ((b & 2u) ? cx : 0u) ^ ((b & 4u) ? cx2 : 0u);
+            const uint32_t tp = ((b >> 3) & 1u) ^ ((b & 16u) ? cx : 0u) ^ ((b & 32u) ? cx2 : 0u);
+            return (sd ^ mul_sel(sel4(tp), prx)) & 0xffu;
+        };
+        if (TAMD_ROLL && nw == 1u) {  // rolling loads, as for LANE3 runs
+            constexpr uint32_t H = TAMD_RBATCH / 2;
+            LV<NH> d[TAMD_RBATCH];
+#pragma unroll
+            for (uint32_t q = 0; q < TAMD_RBATCH; ++q) d[q] = TAMD_RUN_LD(min(q, count - 1u));
+            for (uint32_t e = 0; e < count; e += TAMD_RBATCH) {
+                const bool more = e + TAMD_RBATCH < count;
+#pragma unroll
+                for (uint32_t h = 0; h < 2; ++h) {
+#pragma unroll
+                    for (uint32_t q = h * H; q < (h ? TAMD_RBATCH : H); ++q) {
+                        const uint32_t g = coef(col);
+                        col = (col + cs) & (TAMD_COLUMN_PERIOD - 1u);
+                        if (e + q < count) a0 ^= lv_mul<NH>(lv_keep<FULL, NH>(d[q], o, len, ox), perm_at(lds, g * 8u));
+                    }
+                    if (more) {
+#pragma unroll
+                        for (uint32_t q = h * H; q < (h ? TAMD_RBATCH : H); ++q)
+                            d[q] = TAMD_RUN_LD(min(e + TAMD_RBATCH + q, count - 1u));
+                    }
+                }
+            }
+            unit += (count + TAMD_RBATCH - 1) / TAMD_RBATCH;
+            return;
+        }
+        for (uint32_t e = 0; e < count; e += TAMD_RBATCH) {
+            if ((unit++ & (nw - 1u)) != wid) {
+                col = (col + cs * TAMD_RBATCH) & (TAMD_COLUMN_PERIOD - 1u);
+                continue;
+            }
+            LV<NH> d[TAMD_RBATCH];
+            uint32_t c[TAMD_RBATCH];
+#pragma unroll
+            for (uint32_t q = 0; q < TAMD_RBATCH; ++q) {
+                d[q] = TAMD_RUN_ROW(q);
+                c[q] = coef(col);
+                col = (col + cs) & (TAMD_COLUMN_PERIOD - 1u);
+            }
+#pragma unroll
+            for (uint32_t q = 0; q < TAMD_RBATCH; ++q)
+                if (e + q < count) a0 ^= lv_mul<NH>(lv_keep<FULL, NH>(d[q], o, len, ox), perm_at(lds, c[q] * 8u));
+        }
     } else if (mode == TAMD_R_CAUCHY) {
         // CauchyElement(p, col mod 64) = inv((col mod 64) ^ (p + 64)) (SiameseCommon.h:212-218)
         uint32_t col = vgpr(col0);
@@ -492,9 +550,10 @@ __device__ __forceinline__ LV<NH> run_item(const tamd_instr* __restrict__ instrs
         for (uint32_t j = TAMD_BATCH; j-- > 0;)
             if ((in[j].w0 & 0xffu) == TAMD_I_ACCR && j < nb) nb = j;
         if (nb == 0) {
-            // in[1]: the RANGE word, in[2]: TARGETS (MULTI runs)
+            // in[1]: the RANGE word, in[2]: TARGETS (MULTI runs) or COEFS (DENSE runs)
             run_accr<FULL, NH, TAMD_BATCH>(in[0], in[1], in[2], o, ox, arena, lds, unit, nw, wid, a0, a1, a2);
-            k += ((in[0].w0 >> 8) & 0xffu) == TAMD_R_MULTI ? 3u : 2u;
+            const uint32_t rmode = (in[0].w0 >> 8) & 0xffu;
+            k += (rmode == TAMD_R_MULTI || rmode == TAMD_R_DENSE) ? 3u : 2u;
             continue;
         }
         if ((unit++ & (nw - 1u)) != wid) {  // another wave's batch (shared ops only)

@@ -23,6 +23,12 @@
 //                                            CONST:  acc_a ^= row_k
 //                 (up to three Cauchy / parity rows over overlapping windows: each row of the
 //                 run is read once for all of them)
+//         DENSE:  + COEFS (row = o bits 0..31, len = o bits 32..47 | rx << 16): o holds the 6-bit
+//                 opcode of each lane (bits 6l .. 6l + 5, SiameseCommon.h:160 GetRowOpcode); row k
+//                 (lane l = col_k mod 8, opcode b, cx = CX(col_k)) adds
+//                 acc_0 ^= (b0 ^ b1*cx ^ b2*cx^2  ^  rx * (b3 ^ b4*cx ^ b5*cx^2)) * row_k
+//                 -- a Siamese row's dense part straight from the packets of its sum range: the
+//                 lane-sum combination the row reads (SiameseEncoder.cpp:1046-1098), without sums
 //         (runs of equally long packets stored at a fixed stride: the window's originals, whose
 //         rows sit in a contiguous ring in HBM, become one instruction per run)
 //
@@ -54,6 +60,7 @@ enum tamd_instr_kind {
     TAMD_I_ACCR   = 7,  // w0 = kind | mode << 8 | p << 16; row = row0, len, cap = count
     TAMD_I_RANGE  = 8,  // payload word after ACCR: row = stride (units), len = col0, cap = cstep
     TAMD_I_TARGETS = 9, // payload word after the RANGE of a MULTI ACCR: row, len, cap = t_0, t_1, t_2
+    TAMD_I_COEFS  = 10, // payload word after the RANGE of a DENSE ACCR: lane opcodes and rx
 };
 
 enum tamd_range_mode {
@@ -61,6 +68,7 @@ enum tamd_range_mode {
     TAMD_R_CAUCHY = 2,
     TAMD_R_CONST  = 3,
     TAMD_R_MULTI  = 4,
+    TAMD_R_DENSE  = 5,
 };
 
 // Ops of a level are grouped into classes: class 0 holds the long pure combines (ACC into acc_0,
