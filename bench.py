@@ -97,39 +97,33 @@ def host_threads(local_world: int) -> int:
     return max(1, min(16, per, env))
 
 
-def cpu_baseline(threads: int, target_s: float = 12.0, reps_runs: int = 3) -> dict | None:
-    """The reference codec (oracle/_ref, compiled from /root/reference sources) on a bounded
-    sample of the same workload: 64 streams x 16384 originals per repetition (fresh codecs),
-    repeated to about target_s / reps_runs seconds per run on `threads` host threads; the run is
-    done `reps_runs` times and the median reported with the spread (min, max)."""
+def cpu_baseline(threads: int, n_orig: int, runs: int = 5, pool: int = 16384) -> dict | None:
+    """The reference codec (oracle/_ref, compiled from /root/reference sources) on the bench's own
+    workload: the same 64 streams, each over the bench's full stream length (`n_orig` originals,
+    fresh codecs), on `threads` host threads; `runs` timed passes, median reported with the spread.
+    Scenario generation -- payloads and loss draws -- happens before each pass's clock (SURVEY.md
+    s8(d)); the payload bytes come from a pool of `pool` packets per stream, reused cyclically
+    (the codec's work does not depend on the bytes; recovered packets are still checked)."""
     exe = os.path.join(ROOT, "oracle", "_ref", "golden_gen")
     if not os.path.exists(exe):
         return None
-    n = 4 * ORIGINALS_PER_STEP
-    wp = tonk_amd.WorkloadParams(n=n, payload=PAYLOAD, loss=LOSS, ack=ACK)
-
-    def run(reps: int) -> dict | None:
-        args = [exe, "time", f"threads={threads}", f"streams={STREAMS_PER_GPU}", f"reps={reps}"] + wp.args()
-        r = subprocess.run(args, capture_output=True, text=True, timeout=900)
-        if r.returncode != 0:
-            return None
-        return json.loads(r.stdout.strip().splitlines()[-1])
-
-    probe = run(max(1, threads // 8))
-    if probe is None:
+    wp = tonk_amd.WorkloadParams(n=n_orig, payload=PAYLOAD, loss=LOSS, ack=ACK)
+    args = [exe, "time", f"threads={threads}", f"streams={STREAMS_PER_GPU}", "reps=1", f"runs={runs}",
+            f"pool={pool}"] + wp.args()
+    r = subprocess.run(args, capture_output=True, text=True, timeout=900)
+    if r.returncode != 0:
         return None
-    per_rep = max(probe["seconds"] / max(1, threads // 8), 1e-3)
-    reps = int(min(4000, max(2, round(target_s / reps_runs / per_rep))))
-    runs = [run(reps) for _ in range(reps_runs)]
-    if any(j is None for j in runs):
+    passes = [json.loads(l) for l in r.stdout.strip().splitlines() if l.startswith("{")]
+    if len(passes) != runs:
         return None
-    vals = sorted(j["gib_per_s"] for j in runs)
-    secs = sum(j["seconds"] for j in runs)
+    vals = sorted(j["gib_per_s"] for j in passes)
+    secs = sum(j["seconds"] for j in passes)
     return {"value": round(vals[len(vals) // 2], 4), "unit": "GiB/s", "cores": threads, "kind": "reference",
             "spread": [round(vals[0], 4), round(vals[-1], 4)],
-            "sample": f"{STREAMS_PER_GPU} streams x {n} originals x {PAYLOAD} B x {reps} repetitions "
-                      f"(same loss/FEC/ack workload, fresh codecs per repetition), {threads} host threads, "
-                      f"median of {reps_runs} runs, {secs:.2f} s in total"}
+            "sample": f"the bench's workload: {STREAMS_PER_GPU} streams x {n_orig} originals (its full stream "
+                      f"length) x {PAYLOAD} B, same loss/FEC/ack, steady state, fresh codecs per pass, loss draws "
+                      f"and payloads generated before the clock (payload pool of {pool} packets per stream), "
+                      f"{threads} host threads, median of {runs} passes, {secs:.2f} s timed in total"}
 
 
 def host_cpus() -> int:
@@ -477,6 +471,16 @@ def compress_bench(device: int, steps: int, warmup: int, cpu: bool) -> dict:
     return line
 
 
+def per_gpu_entries(rows: list[list[float]]) -> list[dict]:
+    """The line's per_gpu list from every rank's gathered [rank, GiB/s, roofline frac, device busy
+    frac, ms per step, executor us per launch] (None entries: a --dry-run, nothing measured)."""
+    def r(x, nd):
+        return None if x is None or x != x else round(x, nd)
+    return [{"rank": int(v[0]), "stream_base": stream_base(int(v[0])), "value": r(v[1], 4), "unit": "GiB/s",
+             "roofline_frac": r(v[2], 4), "device_busy_frac": r(v[3], 4), "ms_per_step": r(v[4], 4),
+             "avg_launch_us": r(v[5], 3)} for v in rows]
+
+
 def stream_base(rank: int) -> int:
     """Weak scaling: rank r owns streams [64 r, 64 r + 64) -- disjoint, no data-path exchange."""
     return rank * STREAMS_PER_GPU
@@ -684,11 +688,13 @@ def main() -> int:
             lists = topo.split(";")
             cores = tonk_amd.cpu_share(lists, local_rank, lists[local_rank], os.environ.get("TONK_AMD_CPU_SLOT"))
         bases = d.gather([float(stream_base(rank)), float(rank), float(local_rank)] + pad_cores(cores))
+        nan = float("nan")
+        per_rank = d.gather([float(rank), nan, nan, nan, nan, nan])  # (the same gather as a measured run)
         if rank == 0:
             print(json.dumps({"dry_run": True, "n_gpus": world, "streams_per_gpu": STREAMS_PER_GPU,
                               "ranks": [{"rank": int(v[1]), "local_rank": int(v[2]), "stream_base": int(v[0]),
-                                         "host_cores": unpad_cores(v[3:])} for v in bases]}), file=line_out,
-                  flush=True)
+                                         "host_cores": unpad_cores(v[3:])} for v in bases],
+                              "per_gpu": per_gpu_entries(per_rank)}), file=line_out, flush=True)
         d.close()
         return 0
 
@@ -747,6 +753,12 @@ def main() -> int:
     all_ok = d.allsum(0.0 if ok else 1.0) == 0.0
 
     achieved = alg / (kernel_ms / 1e3) / 1e9 if kernel_ms > 0 else 0.0
+    # Every rank's own figures (BASELINE.json configs[3]: per-GPU GiB/s beside the aggregate): its
+    # payload over its own timed region, its executor's roofline fraction and busy share.
+    own_ms = (t1 - t0) * 1e3 / a.steps
+    per_rank = d.gather([float(rank), payload / (t1 - t0) / 2**30, achieved / HBM_PEAK_GBS,
+                         (kernel_ms / 1e3) / (t1 - t0), own_ms,
+                         kernel_ms * 1e3 / launches if launches else 0.0])
     pmc = pmc_traffic(a.workload, a.steps, a.warmup) if (rank == 0 and world == 1 and not a.no_pmc) else None
     traffic = pmc.get("traffic_per_timed_launch") if pmc else None
     workload = {
@@ -794,9 +806,12 @@ def main() -> int:
             # gap to alg_bytes is what L2 / Infinity Cache serve
             "op_trace_bytes_per_launch": round(op_trace / launches, 1) if launches else None,
             "device_busy_frac": round((kernel_ms / 1e3) / (t1 - t0), 4),
+            # (with several ranks this object is rank 0's executor; per_gpu holds every rank's)
+            "scope": "rank 0" if world > 1 else "the one GPU",
         },
+        "per_gpu": per_gpu_entries(per_rank),
         "cpu_baseline": None,
-        "host_ms_per_program": host,
+        "host_ms_per_program": host,  # (rank 0's, as host_env)
         "host_env": host_env,
         "checks": {"all_recovered": all_ok, "recovered": fin["recovered"], "lost_originals": fin["lost_originals"],
                    "lost_recoveries": fin["lost_recoveries"]},
@@ -804,7 +819,7 @@ def main() -> int:
     # The CPU leg runs after every rank's timed region: the reference codec on the host cores the
     # job owns (16 per GPU, so N x 16 at N GPUs, capped by this process's CPU set).
     if rank == 0 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(min(host_cpus(), threads * local_world))
+        out["cpu_baseline"] = cpu_baseline(min(host_cpus(), threads * local_world), n_orig)
     if rank == 0 and world == 1 and not a.no_end_to_end:
         out["end_to_end"] = end_to_end(threads, device, loss)
     if rank == 0 and a.workload == "cfg3" and not a.no_verify:

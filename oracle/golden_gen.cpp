@@ -18,6 +18,7 @@
 
 #include <chrono>
 #include <dlfcn.h>
+#include <functional>
 #include <thread>
 #include <atomic>
 #include <memory>
@@ -56,17 +57,25 @@ struct RefBackend {
     uint32_t stride = 0;
     uint64_t bad_recoveries = 0;
 
-    explicit RefBackend(const Params& prm) : p(prm) {
+    // `pool` > 0 (timing only): payloads of the first `pool` indices, reused cyclically (original
+    // i carries the bytes of i mod pool), so a long stream does not need its whole payload set in
+    // host memory; the codec's work does not depend on the bytes, and recovered packets are
+    // still checked against what was sent.
+    uint32_t pool = 0;
+    explicit RefBackend(const Params& prm, uint32_t pool_n = 0) : p(prm) {
         enc = siamese_encoder_create();
         dec = siamese_decoder_create();
         stride = prm.payload_max;
-        payloads.resize((size_t)stride * prm.n_originals);
-        lens.resize(prm.n_originals);
-        for (uint32_t i = 0; i < prm.n_originals; ++i) {
+        // (equal lengths only: the runner passes payload_length(i) with every packet)
+        pool = pool_n && pool_n < prm.n_originals && prm.payload_min == prm.payload_max ? pool_n : prm.n_originals;
+        payloads.resize((size_t)stride * pool);
+        lens.resize(pool);
+        for (uint32_t i = 0; i < pool; ++i) {
             lens[i] = payload_length(prm, i);
             payload_bytes(prm, i, payloads.data() + (size_t)i * stride, lens[i]);
         }
     }
+    uint32_t len_of(uint32_t i) const { return lens[i % pool]; }
     ~RefBackend() {
         siamese_encoder_free(enc);
         siamese_decoder_free(dec);
@@ -78,7 +87,7 @@ struct RefBackend {
         enc = siamese_encoder_create();
         dec = siamese_decoder_create();
     }
-    const uint8_t* pay(uint32_t i) const { return payloads.data() + (size_t)i * stride; }
+    const uint8_t* pay(uint32_t i) const { return payloads.data() + (size_t)(i % pool) * stride; }
 
     int enc_add(uint32_t index, uint32_t len, uint32_t* col) {
         SiameseOriginalPacket o;
@@ -124,7 +133,7 @@ struct RefBackend {
                 nums.push_back(pk[k].PacketNum);
                 out.data.emplace_back(pk[k].Data, pk[k].Data + pk[k].DataBytes);
                 const uint32_t idx = pk[k].PacketNum;
-                if (idx >= p.n_originals || lens[idx] != pk[k].DataBytes ||
+                if (idx >= p.n_originals || len_of(idx) != pk[k].DataBytes ||
                     memcmp(pay(idx), pk[k].Data, pk[k].DataBytes) != 0)
                     ++bad_recoveries;
             }
@@ -215,12 +224,16 @@ struct RefTranscript {
     }
 };
 
+static uint32_t g_pool = 0;  // time mode: payload pool per stream (RefBackend::pool)
+static int g_runs = 1;        // time mode: timed passes
 static bool parse_kv(Params& p, int& threads, int& streams, int& reps, const char* kv) {
     const char* eq = strchr(kv, '=');
     if (!eq) return false;
     std::string k(kv, eq - kv);
     const unsigned long long v = strtoull(eq + 1, nullptr, 0);
-    if (k == "threads") threads = (int)v;
+    if (k == "pool") g_pool = (uint32_t)v;
+    else if (k == "runs") g_runs = (int)v;
+    else if (k == "threads") threads = (int)v;
     else if (k == "streams") streams = (int)v;
     else if (k == "reps") reps = (int)v;
     else return parse_param(p, k, v);
@@ -300,47 +313,57 @@ int main(int argc, char** argv) {
     // Scenario generation -- payloads and every run's loss draws -- happens before the clock
     // starts; the timed region is the siamese.h calls and the runner's
     // bookkeeping between them.
+    // `runs=R` repeats the whole timed pass R times (fresh codecs and pregenerated runners each
+    // time) and prints one line per pass.
     typedef Runner<RefBackend, RefTranscript> RefRunner;
-    std::atomic<int> next{0};
-    std::atomic<unsigned long long> bytes{0}, bad{0};
-    std::vector<std::thread> pool;
+    std::atomic<unsigned long long> bad{0};
     std::vector<std::unique_ptr<RefBackend>> bes(streams);
     std::vector<Params> ps(streams, base);
     RefTranscript quiet;
     quiet.enabled = false;
-    std::vector<std::vector<std::unique_ptr<RefRunner>>> runs(streams);
-    for (int s = 0; s < streams; ++s) {
+    // setup on the worker threads too (the payload pools are the bulk of it)
+    auto parallel = [&](const std::function<void(int)>& f) {
+        std::atomic<int> at{0};
+        std::vector<std::thread> pool;
+        for (int t = 0; t < threads; ++t)
+            pool.emplace_back([&]() {
+                for (int s; (s = at++) < streams;) f(s);
+            });
+        for (auto& th : pool) th.join();
+    };
+    parallel([&](int s) {
         ps[s].stream_id = base.stream_id + s;
         ps[s].seed_data = 1000 + ps[s].stream_id;
         ps[s].seed_loss = 2000 + ps[s].stream_id;
-        bes[s].reset(new RefBackend(ps[s]));
-        for (int r = 0; r < reps; ++r) {
-            runs[s].emplace_back(new RefRunner(ps[s], *bes[s], quiet));
-            runs[s].back()->pregenerate();
-        }
-    }
-    const auto t0 = std::chrono::steady_clock::now();
-    for (int t = 0; t < threads; ++t) {
-        pool.emplace_back([&]() {
-            for (;;) {
-                const int s = next++;
-                if (s >= streams) break;
-                unsigned long long b = 0;
-                for (uint32_t i = 0; i < ps[s].n_originals; ++i) b += bes[s]->lens[i];
-                for (int r = 0; r < reps; ++r) {
-                    if (r) bes[s]->reset_codecs();
-                    runs[s][r]->finish();
-                    bytes += b;
-                }
-                bad += bes[s]->bad_recoveries;
+        bes[s].reset(new RefBackend(ps[s], g_pool));
+    });
+    for (int pass = 0; pass < g_runs; ++pass) {
+        std::vector<std::vector<std::unique_ptr<RefRunner>>> runs(streams);
+        parallel([&](int s) {
+            if (pass) bes[s]->reset_codecs();
+            for (int r = 0; r < reps; ++r) {
+                runs[s].emplace_back(new RefRunner(ps[s], *bes[s], quiet));
+                runs[s].back()->pregenerate();
             }
         });
+        std::atomic<unsigned long long> bytes{0};
+        const auto t0 = std::chrono::steady_clock::now();
+        parallel([&](int s) {
+            unsigned long long b = 0;
+            for (uint32_t i = 0; i < ps[s].n_originals; ++i) b += bes[s]->len_of(i);
+            for (int r = 0; r < reps; ++r) {
+                if (r) bes[s]->reset_codecs();
+                runs[s][r]->finish();
+                bytes += b;
+            }
+        });
+        const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        for (int s = 0; s < streams; ++s) bad += bes[s]->bad_recoveries;
+        printf("{\"seconds\": %.6f, \"payload_bytes\": %llu, \"gib_per_s\": %.6f, \"threads\": %d, "
+               "\"streams\": %d, \"reps\": %d, \"bad\": %llu}\n",
+               sec, (unsigned long long)bytes.load(), bytes.load() / sec / (1024.0 * 1024 * 1024),
+               threads, streams, reps, (unsigned long long)bad.load());
+        fflush(stdout);
     }
-    for (auto& th : pool) th.join();
-    const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    printf("{\"seconds\": %.6f, \"payload_bytes\": %llu, \"gib_per_s\": %.6f, \"threads\": %d, "
-           "\"streams\": %d, \"reps\": %d, \"bad\": %llu}\n",
-           sec, (unsigned long long)bytes.load(), bytes.load() / sec / (1024.0 * 1024 * 1024),
-           threads, streams, reps, (unsigned long long)bad.load());
     return bad.load() ? 5 : 0;
 }

@@ -73,6 +73,11 @@ def test_bench_gpus_flag_spawns_ranks():
     per = j["streams_per_gpu"]
     shards = [set(range(x["stream_base"], x["stream_base"] + per)) for x in ranks]
     assert not (shards[0] & shards[1]) and ranks[1]["stream_base"] == per
+    # per-GPU entries (BASELINE.json configs[3]: per-GPU GiB/s beside the aggregate), one per rank
+    pg = j["per_gpu"]
+    assert len(pg) == j["n_gpus"] == 2
+    assert [x["rank"] for x in pg] == [0, 1] and [x["stream_base"] for x in pg] == [0, per]
+    assert all(set(x) >= {"value", "roofline_frac", "device_busy_frac", "ms_per_step"} for x in pg)
 
 
 # A 2-socket 8-GPU node as the MI355X platform lays it out: GPUs 0-3 on socket 0 (cores 0-63,

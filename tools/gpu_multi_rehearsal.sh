@@ -7,4 +7,4 @@ R=${GRAFT_REPO_ROOT:-$PWD}; OUT=$R/gpurun_out; mkdir -p $OUT; cd $R
 export TONK_AMD_BENCH_DEVICE=0 TONK_AMD_HOST_THREADS=8
 timeout -k 10 300 python bench.py --gpus 2 --steps 10 --no-cpu-baseline --no-end-to-end --no-pmc > $OUT/multi_spawn.json 2> $OUT/multi_spawn.err &&
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 \
-    bench.py --gpus 2 --steps 10 --no-cpu-baseline --no-end-to-end --no-pmc --no-verify > $OUT/multi_torchrun.json 2> $OUT/multi_torchrun.err
+    bench.py --gpus 2 --steps 10 --no-cpu-baseline --no-end-to-end --no-pmc > $OUT/multi_torchrun.json 2> $OUT/multi_torchrun.err
