@@ -373,6 +373,48 @@ def single_stream(name: str, device: int, step: int, reps: int = 3) -> dict:
     return out
 
 
+def capi_bench(threads: int, runs: int = 3) -> dict:
+    """`--workload capi`: the drop-in path Tonk actually links -- libtonk_amd.so through the
+    siamese.h C ABI (every siamese_encode / siamese_decode is one synchronous program on the GPU
+    and a readback; siamese.cpp:158-167 / TonkineseOutgoing.cpp:1284-1328 call it inline) -- on
+    BASELINE.json configs[2] (64 streams x 4096 originals, 2% loss, f = 4%, ack every 64), each
+    stream's codec pair driven by the same workload loop on `threads` host threads
+    (tests/native/_build/capi_gen: oracle/golden_gen.cpp linked against our library), beside the
+    reference codec with the same arguments (oracle/_ref/golden_gen).  Reports GiB/s and the per-call
+    latency percentiles of siamese_encode and siamese_decode for both."""
+    n, loss = 4096, 0.02
+    wp = tonk_amd.WorkloadParams(n=n, payload=PAYLOAD, loss=loss, ack=ACK)
+    common = ["time", f"threads={threads}", f"streams={STREAMS_PER_GPU}", "reps=1", f"runs={runs}", "lat=1"] + wp.args()
+
+    def leg(exe: str) -> dict | None:
+        if not os.path.exists(exe):
+            return None
+        r = subprocess.run([exe] + common, capture_output=True, text=True, timeout=900)
+        if r.returncode != 0:
+            return {"error": f"exit {r.returncode}: {r.stderr[-300:]}"}
+        passes = [json.loads(l) for l in r.stdout.strip().splitlines() if l.startswith("{")]
+        passes.sort(key=lambda j: j["gib_per_s"])
+        med = passes[len(passes) // 2]
+        return {"value": round(med["gib_per_s"], 4), "unit": "GiB/s",
+                "spread": [round(passes[0]["gib_per_s"], 4), round(passes[-1]["gib_per_s"], 4)],
+                "encode_us": med.get("encode_us"), "decode_us": med.get("decode_us"), "bad": med["bad"]}
+
+    ours = leg(os.path.join(ROOT, "tests", "native", "_build", "capi_gen"))
+    ref = leg(os.path.join(ROOT, "oracle", "_ref", "golden_gen"))
+    line = {"metric": "Siamese FEC encode+decode GiB/s through the siamese.h C ABI (host buffers, per-call programs)",
+            "value": ours.get("value") if ours else None, "unit": "GiB/s", "n_gpus": 1, "higher_is_better": True,
+            "dtype": "u8", "data": "synthetic",
+            "config": {"workload": "BASELINE.json configs[2] through siamese.h: 64 streams x 4096 originals, 1300 B, "
+                                   "2% loss, f=4%, ack every 64; one codec pair per stream, "
+                                   f"{threads} host threads, median of {runs} passes",
+                       "streams": STREAMS_PER_GPU, "originals_per_stream": n, "host_threads": threads},
+            "capi": ours,
+            "cpu_baseline": dict(ref, cores=threads, kind="reference",
+                                 sample="the same streams through the reference codec's siamese.h, same threads")
+            if ref else None}
+    return line
+
+
 def compress_messages(n_streams: int, n_msgs: int, seed: int = 7):
     """Synthetic reliable-message streams for the compression step: per stream, messages of
     64..1300 bytes mixing word runs (compressible), random bytes (not) and repeats of earlier
@@ -632,7 +674,7 @@ def main() -> int:
     ap.add_argument("--no-end-to-end", action="store_true", help="skip the PCIe-inclusive side measurement")
     ap.add_argument("--no-verify", action="store_true", help="skip the untimed byte check of the timed schedule")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 HBM-traffic passes (roofline.traffic)")
-    ap.add_argument("--workload", choices=sorted(BATCHED) + sorted(SINGLE_STREAM) + ["compress"], default="cfg3",
+    ap.add_argument("--workload", choices=sorted(BATCHED) + sorted(SINGLE_STREAM) + ["compress", "capi"], default="cfg3",
                     help="BASELINE.json configs[] index: cfg3 (the headline, 64 streams per GPU), cfg2 (64 "
                          "streams, 2%% loss), cfg1 / cfg4 (one stream, start to finish)")
     ap.add_argument("--step", type=int, default=0,
@@ -666,6 +708,13 @@ def main() -> int:
             return 2
         print(json.dumps(compress_bench(local_rank, min(a.steps, 10), min(a.warmup, 2), not a.no_cpu_baseline)),
               flush=True)
+        return 0
+
+    if a.workload == "capi":  # the siamese.h drop-in path (side line, not the headline)
+        if world > 1:
+            print("bench.py: the capi workload runs on one GPU", file=sys.stderr)
+            return 2
+        print(json.dumps(capi_bench(host_threads(1))), flush=True)
         return 0
 
     if a.workload in SINGLE_STREAM:

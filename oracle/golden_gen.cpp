@@ -16,6 +16,7 @@
 #include "../tonk_amd/csrc/workload.h"
 #include "../tonk_amd/csrc/transcript.h"
 
+#include <algorithm>
 #include <chrono>
 #include <dlfcn.h>
 #include <functional>
@@ -44,6 +45,16 @@ namespace siamese {
 uint64_t GetTimeUsec() { return g_vclock_on ? g_vclock_ms * 1000 : real_usec(); }
 uint64_t GetTimeMsec() { return vclock_msec(); }
 }  // namespace siamese
+
+// `lat=1` (time mode): the duration of every siamese_encode and siamese_decode call, per thread
+// (the drop-in's per-call latency: TonkineseOutgoing.cpp:1284-1328 calls siamese_encode inline).
+static bool g_lat = false;
+struct LatLog { std::vector<uint32_t> enc_ns, dec_ns; };
+static thread_local LatLog* g_latlog = nullptr;
+static inline uint64_t now_ns() {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 
 struct RefBackend {
     struct RecRef { std::vector<uint8_t> bytes; };
@@ -102,7 +113,9 @@ struct RefBackend {
         SiameseRecoveryPacket rp;
         rp.Data = nullptr;
         rp.DataBytes = 0;
+        const uint64_t t0 = g_latlog ? now_ns() : 0;
         const int rc = siamese_encode(enc, &rp);
+        if (g_latlog) g_latlog->enc_ns.push_back((uint32_t)std::min<uint64_t>(now_ns() - t0, 0xffffffffu));
         if (rc == 0) r.bytes.assign(rp.Data, rp.Data + rp.DataBytes);
         return rc;
     }
@@ -127,7 +140,9 @@ struct RefBackend {
     int dec_decode(std::vector<uint32_t>& nums, DecRef& out) {
         SiameseOriginalPacket* pk = nullptr;
         unsigned count = 0;
+        const uint64_t t0 = g_latlog ? now_ns() : 0;
         const int rc = siamese_decode(dec, &pk, &count);
+        if (g_latlog) g_latlog->dec_ns.push_back((uint32_t)std::min<uint64_t>(now_ns() - t0, 0xffffffffu));
         if (rc == 0) {
             for (unsigned k = 0; k < count; ++k) {
                 nums.push_back(pk[k].PacketNum);
@@ -232,6 +247,7 @@ static bool parse_kv(Params& p, int& threads, int& streams, int& reps, const cha
     std::string k(kv, eq - kv);
     const unsigned long long v = strtoull(eq + 1, nullptr, 0);
     if (k == "pool") g_pool = (uint32_t)v;
+    else if (k == "lat") g_lat = v != 0;
     else if (k == "runs") g_runs = (int)v;
     else if (k == "threads") threads = (int)v;
     else if (k == "streams") streams = (int)v;
@@ -347,8 +363,10 @@ int main(int argc, char** argv) {
             }
         });
         std::atomic<unsigned long long> bytes{0};
+        std::vector<LatLog> logs(streams);
         const auto t0 = std::chrono::steady_clock::now();
         parallel([&](int s) {
+            if (g_lat) g_latlog = &logs[s];
             unsigned long long b = 0;
             for (uint32_t i = 0; i < ps[s].n_originals; ++i) b += bes[s]->len_of(i);
             for (int r = 0; r < reps; ++r) {
@@ -356,13 +374,34 @@ int main(int argc, char** argv) {
                 runs[s][r]->finish();
                 bytes += b;
             }
+            g_latlog = nullptr;
         });
         const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         for (int s = 0; s < streams; ++s) bad += bes[s]->bad_recoveries;
+        std::string lat;
+        if (g_lat) {
+            auto pct = [&](bool enc) {
+                std::vector<uint32_t> all;
+                for (const LatLog& l : logs) {
+                    const std::vector<uint32_t>& v = enc ? l.enc_ns : l.dec_ns;
+                    all.insert(all.end(), v.begin(), v.end());
+                }
+                if (all.empty()) return std::string("null");
+                std::sort(all.begin(), all.end());
+                auto at = [&](double q) { return all[std::min(all.size() - 1, (size_t)(q * (double)all.size()))] / 1e3; };
+                double sum = 0;
+                for (uint32_t x : all) sum += x;
+                char b[200];
+                snprintf(b, sizeof(b), "{\"calls\": %zu, \"mean\": %.2f, \"p50\": %.2f, \"p90\": %.2f, \"p99\": %.2f, \"max\": %.2f}",
+                         all.size(), sum / all.size() / 1e3, at(0.5), at(0.9), at(0.99), all.back() / 1e3);
+                return std::string(b);
+            };
+            lat = ", \"encode_us\": " + pct(true) + ", \"decode_us\": " + pct(false);
+        }
         printf("{\"seconds\": %.6f, \"payload_bytes\": %llu, \"gib_per_s\": %.6f, \"threads\": %d, "
-               "\"streams\": %d, \"reps\": %d, \"bad\": %llu}\n",
+               "\"streams\": %d, \"reps\": %d, \"bad\": %llu%s}\n",
                sec, (unsigned long long)bytes.load(), bytes.load() / sec / (1024.0 * 1024 * 1024),
-               threads, streams, reps, (unsigned long long)bad.load());
+               threads, streams, reps, (unsigned long long)bad.load(), lat.c_str());
         fflush(stdout);
     }
     return bad.load() ? 5 : 0;
