@@ -21,6 +21,8 @@
 
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
 #include <mutex>
 #include <thread>
 #include <stdio.h>
@@ -43,6 +45,7 @@ int64_t now_ns() {
 // stuck one under a real caller (Tonk).  Everything it reads is an atomic.
 std::atomic<uint64_t> g_calls{0}, g_waits{0}, g_wait_ns{0}, g_lock_wait_max_ns{0}, g_lock_hold_max_ns{0};
 std::atomic<uint64_t> g_programs{0}, g_launches{0}, g_prepare_ns{0}, g_run_ns{0};
+std::atomic<uint64_t> g_batches{0}, g_batched{0};  // combined launches and the calls they served
 std::atomic<int> g_in_wait{0};
 std::atomic<int64_t> g_in_wait_since{0};  // start of the current run of overlapping waits
 bool g_watch = false;
@@ -173,9 +176,10 @@ void watch_loop(double period_s) {
                 (now_ns() - start) * 1e-9, (unsigned long long)g_calls.load(), (unsigned long long)g_waits.load(),
                 g_wait_ns.load() * 1e-6, g_lock_wait_max_ns.exchange(0) * 1e-6, g_lock_hold_max_ns.exchange(0) * 1e-6,
                 w.c_str());
-        fprintf(stderr, "[tonk_amd capi]   flush: prepare_ms=%.1f launch_ms=%.1f programs=%llu launches=%llu\n",
+        fprintf(stderr, "[tonk_amd capi]   flush: prepare_ms=%.1f launch_ms=%.1f programs=%llu launches=%llu batches=%llu calls_batched=%llu\n",
                 g_prepare_ns.load() * 1e-6, g_run_ns.load() * 1e-6, (unsigned long long)g_programs.load(),
-                (unsigned long long)g_launches.load());
+                (unsigned long long)g_launches.load(), (unsigned long long)g_batches.load(),
+                (unsigned long long)g_batched.load());
         for (Site* st = g_sites.load(); st; st = st->next) {
             const uint64_t c = st->calls.load();
             if (!c) continue;
@@ -202,6 +206,8 @@ void report_disable(const char* where) {
     fprintf(stderr, "tonk_amd: codec disabled in %s%s\n", where, g_rt && g_rt->dev.failed() ? " (device failure)" : "");
 }
 #define DISABLE(codec) (report_disable(__func__), (codec)->set_disabled())
+
+bool capi_combine();
 
 // Packets added to a codec wait in the codec's own pinned staging (two halves) and reach the
 // arena in one H2D copy + one scatter launch: before the codec's next program, or when a half
@@ -296,7 +302,7 @@ struct Codec {
     Codec() {
         ctx.rows.init_segmented(&g_rt->pool);
         static std::atomic<unsigned> next{0};
-        staging.stream = next.fetch_add(1) % g_rt->dev.stream_count();
+        staging.stream = capi_combine() ? 0u : next.fetch_add(1) % g_rt->dev.stream_count();
     }
     uint64_t byte_offset(RowId r) const { return (uint64_t)ctx.rows.offset(r) * TAMD_ROW_UNIT; }
     // The pinned buffer holds at least n bytes (no copy can be landing in it: every read into it
@@ -343,6 +349,55 @@ struct CDecoder : Codec {
     std::vector<SiameseOriginalPacket> out;
 };
 
+// Combined launches (TONK_AMD_CAPI_COMBINE=0 turns them off).  Codecs of different connections
+// call siamese_encode / siamese_decode concurrently, and each call needs its program run and read
+// back before it returns (siamese.cpp:158-167; TonkineseOutgoing.cpp:1284-1328 sends the result
+// at once).  A caller whose program is ready queues it; the first caller to find no leader
+// becomes the leader and launches every queued program as ONE merged program (Device::run over
+// their contexts: one executor launch per level for all of them), with each caller's reads and
+// event behind it; it hands leadership on once its own program is launched, so no connection's
+// send path serves the others for long (the compressor's pattern, compress.cpp).  Every caller
+// then waits for its own event without a lock.  All codecs use one launch stream then: a
+// codec's staged uploads, its programs and its reads stay in order.
+bool capi_combine() {
+    static const bool on = !(getenv("TONK_AMD_CAPI_COMBINE") && atoi(getenv("TONK_AMD_CAPI_COMBINE")) == 0);
+    return on;
+}
+struct RunReq {
+    Codec* c = nullptr;
+    const std::function<void(Device&)>* reads = nullptr;
+    void* ev = nullptr;
+    bool launched = false, ok = true;
+};
+std::mutex g_run_mu;
+std::condition_variable g_run_cv;
+std::vector<RunReq*> g_run_q;
+bool g_run_leader = false;
+
+void launch_batch(const std::vector<RunReq*>& b) {
+    DevLock dl;
+    Device& dev = g_rt->dev;
+    dev.select_stream(0);
+    std::vector<Context*> ctxs;
+    const uint64_t launches = dev.stats().launches;
+    for (RunReq* r : b) {
+        r->c->staging.send_locked(dev);  // packets added since the codec's last program land first
+        if (!r->c->ctx.pb.empty()) ctxs.push_back(&r->c->ctx);
+    }
+    if (!ctxs.empty()) {
+        dev.run(ctxs.data(), ctxs.size());
+        g_programs.fetch_add(ctxs.size(), std::memory_order_relaxed);
+        g_launches.fetch_add(dev.stats().launches - launches, std::memory_order_relaxed);
+    }
+    g_batches.fetch_add(1, std::memory_order_relaxed);
+    g_batched.fetch_add(b.size(), std::memory_order_relaxed);
+    for (RunReq* r : b) {
+        (*r->reads)(dev);
+        r->ev = dev.record_event();
+        r->ok = !dev.failed();
+    }
+}
+
 // Close the codec's pending program and enqueue it with the reads `enqueue_reads` adds behind
 // it, then wait for all of it without any lock.  Returns false on a device failure.
 template <class Reads>
@@ -353,7 +408,34 @@ bool run_and_read(Codec& c, Reads enqueue_reads) {
     const int64_t t1 = g_watch ? now_ns() : 0;
     void* ev = nullptr;
     bool ok = true;
-    {
+    if (capi_combine()) {
+        const std::function<void(Device&)> f(enqueue_reads);
+        RunReq req;
+        req.c = &c;
+        req.reads = &f;
+        {
+            std::unique_lock<std::mutex> lk(g_run_mu);
+            g_run_q.push_back(&req);
+            g_run_cv.wait(lk, [&req] { return req.launched || !g_run_leader; });
+            if (!req.launched) {
+                g_run_leader = true;
+                std::vector<RunReq*> b;
+                while (!req.launched) {
+                    b.clear();
+                    b.swap(g_run_q);
+                    lk.unlock();
+                    launch_batch(b);
+                    lk.lock();
+                    for (RunReq* r : b) r->launched = true;
+                    g_run_cv.notify_all();
+                }
+                g_run_leader = false;
+                g_run_cv.notify_all();  // a caller still queued becomes the next leader
+            }
+        }
+        ev = req.ev;
+        ok = req.ok;
+    } else {
         DevLock dl;
         Device& dev = g_rt->dev;
         dev.select_stream(c.staging.stream);
