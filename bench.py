@@ -254,41 +254,55 @@ def verify_schedule(threads: int, device: int) -> dict:
 
 def end_to_end(threads: int, device: int, loss: float, steps: int = 3, warmup: int = 1) -> dict | None:
     """The PCIe-inclusive rate (north_star): the same workload with packets starting
-    and ending in pinned host memory -- every step copies its originals H2D for both codec
-    sides, its recovery packets and recovered originals D2H (packed by a gather kernel) and the
-    received recovery packets H2D again, on copy streams overlapped with the codec work.
-    Reported beside `value`, never as it."""
+    and ending in pinned host memory -- copies on their own streams, overlapped with the codec
+    work.  Measured three ways: both ends of every connection on this GPU (each original crosses
+    PCIe twice: into the encoder and into the decoder), the sender's end only (originals H2D,
+    recovery packets D2H: what a sending host's GPU moves) and the receiver's end only (originals
+    and received recovery packets H2D, recovered originals D2H).  D2H is timed on its own copies
+    (HIP events): `d2h_copy_gb_per_s` is the rate while a copy runs, `d2h_gb_per_s` its bytes over
+    the step time.  Reported beside `value`, never as it."""
     n_orig = (warmup + steps) * ORIGINALS_PER_STEP
     wp = tonk_amd.WorkloadParams(n=n_orig, payload=PAYLOAD, loss=loss, ack=ACK)
-    try:
-        sess = tonk_amd.Session(wp, n_streams=STREAMS_PER_GPU, device=device, threads=threads,
-                                arena_bytes=(2 * n_orig * STREAMS_PER_GPU * 1344) + (4 << 30), stage_host=True)
-    except RuntimeError as e:
-        return {"error": str(e)}
-    try:
-        sess.generate()
-        for _ in range(warmup):
-            sess.step(ORIGINALS_PER_STEP)
-        sess.wait()
-        s0 = sess.summary()
-        t0 = time.perf_counter()
-        for _ in range(steps):
-            sess.step(ORIGINALS_PER_STEP)
-        sess.wait()
-        t1 = time.perf_counter()
-        s1 = sess.summary()
-    finally:
-        sess.close()
-    payload = s1["payload_bytes"] - s0["payload_bytes"]
-    h2d = s1["h2d_bytes"] - s0["h2d_bytes"]
-    d2h = s1["d2h_bytes"] - s0["d2h_bytes"]
-    dt = t1 - t0
-    return {"value": round(payload / dt / 2**30, 4), "unit": "GiB/s", "steps": steps,
-            "ms_per_step": round(dt * 1e3 / steps, 4),
-            "h2d_gb_per_s": round(h2d / dt / 1e9, 2), "d2h_gb_per_s": round(d2h / dt / 1e9, 2),
-            "h2d_bytes_per_step": h2d // steps, "d2h_bytes_per_step": d2h // steps,
-            "note": "pinned hipMemcpyAsync H2D of every original (encoder and decoder copies), D2H of "
-                    "recovery packets and recovered originals, H2D of received recovery packets"}
+
+    def run(mask: int) -> dict:
+        try:
+            sess = tonk_amd.Session(wp, n_streams=STREAMS_PER_GPU, device=device, threads=threads,
+                                    arena_bytes=(2 * n_orig * STREAMS_PER_GPU * 1344) + (4 << 30), stage_host=mask)
+        except RuntimeError as e:
+            return {"error": str(e)}
+        try:
+            sess.generate()
+            for _ in range(warmup):
+                sess.step(ORIGINALS_PER_STEP)
+            sess.wait()
+            s0 = sess.summary()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                sess.step(ORIGINALS_PER_STEP)
+            sess.wait()
+            t1 = time.perf_counter()
+            s1 = sess.summary()
+        finally:
+            sess.close()
+        payload = s1["payload_bytes"] - s0["payload_bytes"]
+        h2d = s1["h2d_bytes"] - s0["h2d_bytes"]
+        d2h = s1["d2h_bytes"] - s0["d2h_bytes"]
+        d2h_s = (s1["d2h_copy_us"] - s0["d2h_copy_us"]) / 1e6
+        dt = t1 - t0
+        return {"value": round(payload / dt / 2**30, 4), "unit": "GiB/s", "ms_per_step": round(dt * 1e3 / steps, 4),
+                "h2d_gb_per_s": round(h2d / dt / 1e9, 2), "d2h_gb_per_s": round(d2h / dt / 1e9, 2),
+                "d2h_copy_gb_per_s": round(d2h / d2h_s / 1e9, 2) if d2h_s > 0 else None,
+                "d2h_copy_ms_per_step": round(d2h_s * 1e3 / steps, 4),
+                "h2d_bytes_per_step": h2d // steps, "d2h_bytes_per_step": d2h // steps}
+
+    both = run(3)
+    out = dict(both)
+    out.update({"steps": steps, "per_side": {"sender": run(1), "receiver": run(2)},
+                "note": "pinned hipMemcpyAsync on copy streams: H2D of the originals into the encoder (sender) "
+                        "and the decoder (receiver), D2H of recovery packets (sender) and recovered originals "
+                        "(receiver, packed by a gather kernel), H2D of the received recovery packets (receiver); "
+                        "`value` here has both ends on this GPU"})
+    return out
 
 
 # Workload names follow BASELINE.json's 0-based configs[] index.

@@ -30,10 +30,11 @@ typedef struct tamd_session_params {
                                   schedule is the timed one (early launch, rows released at their
                                   program's completion); the rows are digested on the launch
                                   stream right after the launch that completes their program. */
-    uint32_t stage_host;       /* 1: packets start and end in pinned host memory: every step copies
-                                  its originals H2D (both codec sides), its recovery packets and
-                                  recovered originals D2H and the received recovery packets H2D
-                                  (the PCIe-inclusive rate) */
+    uint32_t stage_host;       /* packets start and end in pinned host memory (the PCIe-inclusive
+                                  rate), a bit mask of the connection's two ends:
+                                  1 the sender (originals H2D into the encoder, recovery packets
+                                  D2H), 2 the receiver (originals and received recovery packets
+                                  H2D into the decoder, recovered originals D2H); 3 both */
     uint64_t arena_bytes;
     uint32_t rtx_every;        /* retransmission tick every rtx_every originals (0: off) under a
                                   virtual clock advancing rtx_msec per original (workload.h) */
@@ -51,6 +52,7 @@ enum {
     TAMD_SUM_DISABLED_CODECS,
     TAMD_SUM_H2D_BYTES,        /* stage_host: bytes copied host -> device */
     TAMD_SUM_D2H_BYTES,        /* stage_host: bytes copied device -> host */
+    TAMD_SUM_D2H_COPY_US,      /* stage_host: duration of the D2H copies themselves (HIP events) */
     TAMD_SUM_COUNT
 };
 

@@ -84,15 +84,18 @@ def test_session_matches_reference(golden_index, name):
     assert summ["disabled_codecs"] == 0
 
 
-@pytest.mark.parametrize("name", ["c2_4096_p1_ack64", "c3_4096_p2_ack64_s1", "burst8_p5"])
-def test_session_host_staged_matches_reference(golden_index, name):
+@pytest.mark.parametrize("name,mask", [("c2_4096_p1_ack64", 3), ("c3_4096_p2_ack64_s1", 3), ("burst8_p5", 3),
+                                       ("c3_4096_p2_ack64_s1", 1), ("c3_4096_p2_ack64_s1", 2)])
+def test_session_host_staged_matches_reference(golden_index, name, mask):
     """Packets staged through pinned host memory (the PCIe-inclusive path: H2D of the inputs
-    before every step's program, D2H of its outputs) give the same transcript."""
-    got, summ = _session_transcript(golden_index, name, stage_host=True)
+    before every step's program, D2H of its outputs) give the same transcript -- with both ends
+    of the connection staged (3), the sender's only (1) or the receiver's only (2)."""
+    got, summ = _session_transcript(golden_index, name, stage_host=mask)
     want = golden_text(name)
     want = "\n".join(l for l in want.splitlines() if not l.startswith("Z ")) + "\n"
     assert got == want, first_diff(want, got)
     assert summ["h2d_bytes"] > 0 and summ["d2h_bytes"] > 0
+    assert summ["d2h_copy_us"] > 0
 
 
 def _batch_digests(entry, threads=16, step=4096):

@@ -83,7 +83,8 @@ class _SessionParams(ctypes.Structure):
 
 SUMMARY_FIELDS = ["originals", "lost_originals", "recoveries", "lost_recoveries", "recovered", "arq",
                   "missing_at_end", "payload_bytes", "alg_bytes", "acc_bytes", "store_bytes", "programs",
-                  "launches", "ops", "instrs", "upload_bytes", "disabled_codecs", "h2d_bytes", "d2h_bytes"]
+                  "launches", "ops", "instrs", "upload_bytes", "disabled_codecs", "h2d_bytes", "d2h_bytes",
+                  "d2h_copy_us"]
 
 
 def loss_threshold(p: float) -> int:
@@ -174,7 +175,8 @@ class Session:
         p.loss_thresh, p.ge_enable, p.gb_thresh, p.bg_thresh = wp.loss, wp.ge, wp.gb, wp.bg
         p.loss_on_recovery, p.fec_rate_q16, p.ack_every, p.ack_bytes = wp.lossrec, wp.fec, wp.ack, wp.ackbytes
         p.arq_lag, p.flush_max, p.record, p.arena_bytes = wp.arq, wp.flush, 1 if record else 0, arena_bytes
-        p.stage_host = 1 if stage_host else 0
+        # stage_host: True (both ends), or the tonk_amd.h mask (1 sender end, 2 receiver end)
+        p.stage_host = 3 if stage_host is True else int(stage_host or 0)
         p.rtx_every, p.rtx_msec = wp.rtx, wp.rtxms
         self.n_streams = n_streams
         err = ctypes.create_string_buffer(512)

@@ -1148,7 +1148,12 @@ void Device::d2h_gather(const std::vector<GatherDesc>& d, size_t bytes, void* ds
     HIPCHK(hipEventRecord((hipEvent_t)gather_done_, st));
     hipStream_t ds = (hipStream_t)d2h_stream_;
     HIPCHK(hipStreamWaitEvent(ds, (hipEvent_t)gather_done_, 0));
+    void* ta = timing_event();
+    void* tb = timing_event();
+    HIPCHK(hipEventRecord((hipEvent_t)ta, ds));  // (the copy's own duration: D2H effective rate)
     HIPCHK(hipMemcpyAsync(dst, gather_dev_, bytes, hipMemcpyDeviceToHost, ds));
+    HIPCHK(hipEventRecord((hipEvent_t)tb, ds));
+    d2h_timing_.push_back(std::make_pair(ta, tb));
     HIPCHK(hipEventRecord((hipEvent_t)d2h_done_, ds));
 }
 
@@ -1168,6 +1173,13 @@ void Device::h2d_after_d2h(const void* src, size_t n) {
 void Device::sync_staging() {
     if (h2d_stream_) HIPCHK(hipStreamSynchronize((hipStream_t)h2d_stream_));
     if (d2h_stream_) HIPCHK(hipStreamSynchronize((hipStream_t)d2h_stream_));
+    for (auto& p : d2h_timing_) {
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, (hipEvent_t)p.first, (hipEvent_t)p.second) == hipSuccess) stats_.d2h_copy_ms += ms;
+        timing_pool_.push_back(p.first);
+        timing_pool_.push_back(p.second);
+    }
+    d2h_timing_.clear();
 }
 
 void Device::generate_rows(const std::vector<GenDesc>& d, uint32_t row_cap) {

@@ -22,6 +22,7 @@ struct DeviceStats {
     double upload_enqueue_max_ms = 0;
     uint64_t slot_reallocs = 0;
     uint64_t timed_launches = 0;
+    double d2h_copy_ms = 0;  // stage_host: duration of the D2H copies (events around each copy)
 };
 
 class Device {
@@ -212,6 +213,7 @@ private:
     size_t gather_cap_ = 0;
     uint8_t* recv_dev_ = nullptr;    // received-recovery landing area
     size_t recv_cap_ = 0;
+    std::vector<std::pair<void*, void*>> d2h_timing_;  // (start, end) events of D2H copies not yet read
     GatherDesc* gdesc_host_ = nullptr;
     GatherDesc* gdesc_dev_ = nullptr;
     size_t gdesc_cap_ = 0;

@@ -210,7 +210,7 @@ struct Stream {
     uint64_t alg_bytes = 0, payload_bytes = 0;
     // stage_host: rows this step produced that leave through PCIe (recovery packets, recovered
     // originals) and the recovery bytes the decoder received (which arrived through PCIe)
-    bool stage = false;
+    uint32_t stage = 0;  // stage_host mask: 1 sender side staged, 2 receiver side
     std::vector<std::pair<RowId, uint32_t>> out_rows;
     uint64_t recv_bytes = 0;
 
@@ -245,7 +245,7 @@ struct Stream {
         const Result rc = enc->encode(r.out);
         if (rc == kSuccess) {
             alg_bytes += r.out.total();
-            if (stage) out_rows.push_back(std::make_pair(r.out.row, r.out.total()));
+            if (stage & 1u) out_rows.push_back(std::make_pair(r.out.row, r.out.total()));
         }
         return rc;
     }
@@ -266,7 +266,7 @@ struct Stream {
         const Result rc = dec->add_recovery(r.out.row, r.out.total(), tail, nullptr, &took);
         if (!took) ctx->rows.free_deferred(r.out.row);
         alg_bytes += r.out.total();
-        recv_bytes += r.out.total();
+        if (stage & 2u) recv_bytes += r.out.total();
         return rc;
     }
     int dec_is_ready() { return dec->is_ready(); }
@@ -278,7 +278,7 @@ struct Stream {
             for (RecoveredPacket* rp : got_) {
                 nums.push_back(rp->packet_num);
                 alg_bytes += rp->framed_upper;
-                if (stage) out_rows.push_back(std::make_pair(rp->row, rp->framed_upper));
+                if (stage & 2u) out_rows.push_back(std::make_pair(rp->row, rp->framed_upper));
                 if (tr.on) tr.pend_dec.push_back(SessTranscript::PendDec{rp->row, rp->framed_upper, tr.lines.size(), 0});
             }
         }
@@ -1030,6 +1030,7 @@ struct Session {
             const uint32_t n = next + originals <= st.p.n_originals ? originals : st.p.n_originals - next;
             if (!n) continue;
             for (int side = 0; side < 2; ++side) {
+                if (!((prm.stage_host >> side) & 1u)) continue;  // (that end's packets are resident)
                 const RowId r = (side ? st.dec_rows : st.enc_rows)[next];
                 const uint8_t* src = host_in + (2 * i + side) * side_bytes + (size_t)next * row_cap;
                 dev.h2d((uint64_t)st.ctx->rows.offset(r) * TAMD_ROW_UNIT, src, (size_t)n * row_cap);
@@ -1311,7 +1312,7 @@ int tamd_session_generate(void* sp) {
         }
         for (size_t i = 0; i < s->streams.size(); ++i) {
             Stream& st = *s->streams[i];
-            st.stage = true;
+            st.stage = s->prm.stage_host & 3u;
             for (int side = 0; side < 2; ++side) {
                 const std::vector<RowId>& rows = side ? st.dec_rows : st.enc_rows;
                 const uint64_t base = st.ctx->rows.offset(rows[0]);
@@ -1379,6 +1380,7 @@ int tamd_session_summary(void* sp, uint64_t* out, unsigned n) {
     v[TAMD_SUM_STORE_BYTES] = ds.store_bytes;
     v[TAMD_SUM_H2D_BYTES] = s->h2d_bytes;
     v[TAMD_SUM_D2H_BYTES] = s->d2h_bytes;
+    v[TAMD_SUM_D2H_COPY_US] = (uint64_t)(ds.d2h_copy_ms * 1e3);
     if (n > TAMD_SUM_COUNT) n = TAMD_SUM_COUNT;
     for (unsigned i = 0; i < n; ++i) out[i] = v[i];
     return s->error.empty() ? 0 : -1;
