@@ -545,7 +545,9 @@ int oracle_run_program(uint8_t* arena, size_t arena_bytes,
                         oracle_muladd_mem(acc + span, cx, row, len);
                         oracle_muladd_mem(acc + 2 * (size_t)span, oracle_gf_sqr(cx), row, len);
                     } else if (mode == R_CAUCHY) {
-                        oracle_muladd_mem(acc, oracle_cauchy_element(p, col % 64u), row, len);
+                        /* w0 bits 24..31: scale s (0 or 1: none) -- decoder elimination runs */
+                        const uint8_t s = (uint8_t)(w[0] >> 24), ce = oracle_cauchy_element(p, col % 64u);
+                        oracle_muladd_mem(acc, s > 1 ? oracle_gf_mul(s, ce) : ce, row, len);
                     } else if (mode == R_CONST) {
                         oracle_muladd_mem(acc, (uint8_t)p, row, len);
                     } else if (mode == R_DENSE) {

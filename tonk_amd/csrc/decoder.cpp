@@ -1096,7 +1096,23 @@ bool Decoder::eliminate_original_data() {
         Sym& buf = rec->buf;
 
         if (m.SumCount <= kCauchyThreshold) {
+            // Received originals inside a segment (a run of equally long level-0 packets at one
+            // row stride) enter as one run term: one ACCR run on the device, one term here.
+            const uint32_t mode = m.Row == 0 ? TAMD_R_CONST : TAMD_R_CAUCHY;
+            const uint32_t param = m.Row == 0 ? 1u : m.Row - 1;
             for (uint32_t j = es; j < ee; ++j) {
+                const uint32_t id = seg_id(j);
+                if (id != kSingle) {
+                    const Segment& sg = segs_[id - seg_base_];
+                    const uint32_t k = j + base_ - sg.first;
+                    const uint32_t n = std::min(sg.end() - base_, ee) - j;
+                    if (n >= 2) {
+                        const uint32_t add = std::min(sg.bytes, rec->bytes);
+                        buf.push_back(ctx_->pb.run_term(mode, param, sg.off(k), sg.stride, n, to_column(j), add));
+                        j += n - 1;
+                        continue;
+                    }
+                }
                 RowId row;
                 uint32_t add;
                 if (!packet(j, row, add)) continue;

@@ -138,6 +138,7 @@ void ProgramBuilder::clear() {
     written_.clear();
     level_ops_.clear();
     level_items_.clear();
+    runs_.clear();
     max_level_ = 0;
     acc_bytes_ = store_bytes_ = 0;
 }
@@ -379,10 +380,14 @@ uint32_t ProgramBuilder::combine(RowId dst, const Term* terms, size_t n, uint32_
     tamd_instr* w = instrs_.data() + at;
     uint32_t span = cur_span_, lvl = cur_level_in_, full = cur_full_;
     uint64_t acc = 0;
-    size_t k = 0;
+    size_t k = 0, nrun = 0;
     for (size_t i = 0; i < n; ++i) {
         const Term& t = terms[i];
         if (!t.coef || !t.len) continue;
+        if (is_run(t.row)) {
+            ++nrun;
+            continue;
+        }
         w[k].w0 = tamd_w0(TAMD_I_ACC, t.coef);
         w[k].row = rows_->offset(t.row);
         w[k].len = t.len;
@@ -399,6 +404,15 @@ uint32_t ProgramBuilder::combine(RowId dst, const Term* terms, size_t n, uint32_
     cur_full_ = full;
     cur_level_in_ = lvl;
     acc_bytes_ += acc;
+    for (size_t i = 0; nrun && i < n; ++i) {
+        const Term& t = terms[i];
+        if (!t.coef || !t.len || !is_run(t.row)) continue;
+        const RunRef& r = runs_[t.row & ~kRunFlag];
+        // a CONST run's constant is the coefficient itself; a CAUCHY run carries it as its scale
+        const uint32_t param = r.mode == TAMD_R_CONST ? gf_mul((uint8_t)r.p, t.coef) : r.p | (uint32_t)t.coef << 8;
+        op_accr(r.mode, param, r.off0, r.stride, r.count, t.len, r.col0, 1);
+        --nrun;
+    }
     const uint32_t cap = rows_->cap_bytes(dst);
     push_store(instrs_, rows_->offset(dst), len, cap, footer, footer_len);
     if (cap > cur_span_) cur_span_ = cap;
@@ -789,7 +803,7 @@ RowId fold_low_levels(RowTable& rows, ProgramBuilder& pb, Sym& s, uint32_t keep_
     low.clear();
     high.clear();
     for (const Term& t : s) {
-        if (rows.level(t.row) < keep_level) low.push_back(t);
+        if (is_run(t.row) || rows.level(t.row) < keep_level) low.push_back(t);
         else high.push_back(t);
     }
     sym_merge(low);

@@ -43,6 +43,10 @@ struct Term {
     uint32_t len;
     uint8_t coef;
 };
+// A term whose row has this bit set names a run of level-0 rows registered with the pending
+// program (ProgramBuilder::run_term) instead of one row: coef * sum_k c_k * row_k[0:len].
+static const RowId kRunFlag = 0x80000000u;
+inline bool is_run(RowId r) { return (r & kRunFlag) != 0; }
 
 // Allocator whose value-initialisation leaves PODs uninitialised: growing a term list or an
 // instruction list by resize() and then writing every new element skips a zero fill.
@@ -180,6 +184,15 @@ public:
     // the row's 8 lane opcodes, 6 bits each.
     void op_accr_dense(uint32_t row0, uint32_t stride, uint32_t count, uint32_t len, uint32_t col0, uint64_t ops,
                        uint8_t rx);
+    // Register a run of level-0 rows at offsets off0 + k * stride (k < count), columns col0 + k,
+    // with per-row coefficients CauchyElement(p, column mod 64) (mode TAMD_R_CAUCHY) or 1
+    // (TAMD_R_CONST), as one symbolic term (kRunFlag) of length len; combine() emits it as one
+    // ACCR run scaled by the term's coefficient.  Valid until clear().
+    Term run_term(uint32_t mode, uint32_t p, uint32_t off0, uint32_t stride, uint32_t count, uint32_t col0,
+                  uint32_t len) {
+        runs_.push_back(RunRef{mode, p, off0, stride, count, col0});
+        return Term{kRunFlag | (uint32_t)(runs_.size() - 1), len, 1};
+    }
     // STORE (+FOOTER) of acc_0 into dst and close the op (the tail of combine()).
     uint32_t finish_combine(RowId dst, uint32_t len, const uint8_t* footer, uint32_t footer_len);
     void op_store(RowId dst, uint32_t len, uint32_t acc = 0, const uint8_t* footer = nullptr, uint32_t footer_len = 0);
@@ -230,6 +243,8 @@ private:
     // op under construction
     uint32_t cur_first_ = 0, cur_span_ = 0, cur_level_in_ = 0, cur_full_ = ~0u, cur_runs_ = 0;
     bool cur_pure_ = true;  // only acc_0 sums and CONST/CAUCHY runs so far (see TAMD_COST_CLASSES)
+    struct RunRef { uint32_t mode, p, off0, stride, count, col0; };
+    std::vector<RunRef> runs_;  // run terms of the pending program
     size_t cur_written_begin_ = 0;
     uint64_t acc_bytes_ = 0, store_bytes_ = 0, cur_acc_begin_ = 0;
 };

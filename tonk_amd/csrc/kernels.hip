@@ -376,16 +376,23 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
 #undef TAMD_MULTI_TARGET
         unit += (count + TAMD_RBATCH - 1) / TAMD_RBATCH;
         return;
-    } else if (mode == TAMD_R_DENSE) {
-        // A Siamese row's dense part packet by packet (program.h DENSE): row k's coefficient is the
-        // lane-sum combination the recovery row reads, from its lane's opcode bits, cx and rx --
-        // wave-uniform scalar work per row, then one product per byte as in a Cauchy run.
+    } else if (mode == TAMD_R_DENSE || (mode == TAMD_R_CAUCHY && (a.w0 >> 24) > 1u)) {
+        // Rows with a per-row coefficient computed by wave-uniform scalar work, then one product
+        // per byte:
+        //  - DENSE: a Siamese row's dense part packet by packet (program.h); row k's coefficient
+        //    is the lane-sum combination the recovery row reads, from its lane's opcode bits, cx
+        //    and rx;
+        //  - scaled CAUCHY (a decoder elimination run): s * CauchyElement(p, col mod 64).
+        const bool dense = mode == TAMD_R_DENSE;
         const u64 opw = (u64)tg.row | ((u64)(tg.len & 0xffffu) << 32);
-        const PermT prx = perm_at(lds, ((tg.len >> 16) & 0xffu) * 8u);
+        const PermT prx = perm_at(lds, (dense ? (tg.len >> 16) & 0xffu : a.w0 >> 24) * 8u);
         const uint8_t* sqr = (const uint8_t*)(lds + TAMD_LDS_INV + 64u);
+        const uint8_t* inv = (const uint8_t*)(lds + TAMD_LDS_INV);
+        const uint32_t px = p + 64u;
         uint32_t col = col0;
         const uint32_t cs = cstep;
         auto coef = [&](uint32_t c) -> uint32_t {
+            if (!dense) return mul_sel(sel4(inv[(c & 63u) ^ px]), prx) & 0xffu;
             const uint32_t b = (uint32_t)(opw >> (6u * (c & 7u))) & 63u;
             const uint32_t cx = 3u + (199u * (c % 253u)) % 253u, cx2 = sqr[cx];
             const uint32_t sd = (b & 1u) ^ ((b & 2u) ? cx : 0u) ^ ((b & 4u) ? cx2 : 0u);

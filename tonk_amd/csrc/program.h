@@ -57,7 +57,7 @@ enum tamd_instr_kind {
     TAMD_I_CLEAR  = 4,
     TAMD_I_ACC3   = 5,
     TAMD_I_STOREC = 6,  // w0 = kind | c0 << 8 | c1 << 16 | c2 << 24
-    TAMD_I_ACCR   = 7,  // w0 = kind | mode << 8 | p << 16; row = row0, len, cap = count
+    TAMD_I_ACCR   = 7,  // w0 = kind | mode << 8 | p << 16 (| s << 24: CAUCHY scale); row = row0, len, cap = count
     TAMD_I_RANGE  = 8,  // payload word after ACCR: row = stride (units), len = col0, cap = cstep
     TAMD_I_TARGETS = 9, // payload word after the RANGE of a MULTI ACCR: row, len, cap = t_0, t_1, t_2
     TAMD_I_COEFS  = 10, // payload word after the RANGE of a DENSE ACCR: lane opcodes and rx
