@@ -32,7 +32,7 @@ void  tamd_compressor_destroy(void* c);
 
 /* The device-resident batch (bench.py --workload compress): n_streams independent compressor
    streams, stream s's messages back to back at dev_data + s * stride (device memory, with at
-   least 8 readable bytes after a stream's last message), message k of stream s is
+   least 32 readable bytes after a stream's last message), message k of stream s is
    lens[s * n_msgs + k] bytes (1..max_bytes).  Every stream starts fresh (history
    empty) and applies MessageCompressor's Allocate(max)/Commit ring rule.  Outputs: message
    (s, k) compressed at dev_out + (s * n_msgs + k) * max_bytes, written_host[s * n_msgs + k]

@@ -385,7 +385,8 @@ extern "C" int tamd_compress_batch(const void* dev_data, uint64_t stride, uint32
             if (n == 0 || n > max_bytes) return -1;
             uint64_t pos = 0, win = 0;
             rt.place(n, &pos, &win);
-            if (pos + n + 8 > stride) return -1;  // (8 readable bytes past the last message)
+            if (pos + n + 32 > stride) return -1;  // (32 readable bytes past the last message: the
+                                                   // kernel's wide loads, lz.hip)
             tamd_lz_msg& m = msgs[(uint64_t)s * n_msgs + k];
             memset(&m, 0, sizeof(m));
             m.pos = (uint32_t)pos;

@@ -10,7 +10,7 @@
 // distributions for literal lengths, match lengths and offsets (no repeat offsets, so no state
 // carries from block to block).
 //
-// Per message: (1) candidate positions from a 4-byte hash table in LDS (the window's positions
+// Per message: (1) candidate positions from a hash table of 8-byte keys in LDS (the window's positions
 // are inserted once per job, each message's after it is scanned, 64 at a time), (2) every lane
 // extends its own candidate, (3) a ballot-driven greedy parse, (4) lane 0 writes the backward
 // FSE bit stream of the sequences into LDS, (5) the wave copies header, literals and bit stream
@@ -35,20 +35,21 @@
 #define LZ_WAVES 2  // jobs per workgroup: the waves share the FSE maps (2 workgroups per CU)
 
 // Byte loads of a stream: `buf` at linear position p & mask.  Multi-byte loads are unaligned
-// global loads; the buffers carry readable slack past their end (a linear stream: 8 bytes past its
-// last message, tamd_compress_batch; the 64 KB ring: its first 64 bytes mirrored after it).
-typedef uint32_t lz_u32u __attribute__((aligned(1)));
+// global loads; the buffers carry readable slack past their end (a linear stream: 32 bytes past
+// its last message, tamd_compress_batch; the 64 KB ring: its first 64 bytes mirrored after it).
 typedef uint64_t lz_u64u __attribute__((aligned(1)));
-
-static __device__ __forceinline__ uint32_t lz_word(const uint8_t* __restrict__ buf, uint32_t mask, uint32_t p) {
-    return *(const lz_u32u*)(buf + (p & mask));
-}
 
 static __device__ __forceinline__ uint64_t lz_dword(const uint8_t* __restrict__ buf, uint32_t mask, uint32_t p) {
     return *(const lz_u64u*)(buf + (p & mask));
 }
 
-static __device__ __forceinline__ uint32_t lz_hash(uint32_t w) { return (w * 2654435761u) >> (32 - LZ_HASH_LOG); }
+// Candidates are keyed by the 8 bytes at a position (a match still needs only LZ_MIN_MATCH equal
+// bytes): on text a 4-byte key's most recent occurrence is mostly a short match inside a common
+// word, an 8-byte key's mostly the long one (fewer, longer sequences: the ratio of zstd level 1).
+// Bytes past the message end may enter a key; the probe compares only the message's bytes.
+static __device__ __forceinline__ uint32_t lz_hash(uint64_t w) {
+    return (uint32_t)((w * 0x9E3779B185EBCA87ull) >> (64 - LZ_HASH_LOG));
+}
 
 // The waves of a workgroup run unrelated jobs: they synchronise only with themselves (LDS and
 // scratch writes complete before any lane reads them).
@@ -113,10 +114,6 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
     }
     const uint8_t* mb = L.mbuf;
     // the message's bytes at offset i (LDS copy, or the stream buffer for BIG messages)
-    auto msg_word = [&](uint32_t i) -> uint32_t {
-        if constexpr (BIG) return lz_word(buf, mask, m.pos + i);
-        else return *(const lz_u32u*)(mb + i);
-    };
     auto msg_dword = [&](uint32_t i) -> uint64_t {
         if constexpr (BIG) return lz_dword(buf, mask, m.pos + i);
         else return *(const lz_u64u*)(mb + i);
@@ -149,7 +146,7 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
             uint32_t len = 0, src = 0;
             if (i + LZ_MIN_MATCH <= n) {
                 const uint32_t pp = m.pos + i;
-                const uint32_t e = L.htab[lz_hash(msg_word(i))];
+                const uint32_t e = L.htab[lz_hash(msg_dword(i))];
                 if (e) {
                     src = e - 1;
                     if (src >= m.win && src < pp) {
@@ -170,7 +167,7 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
             }
             if (i < cend) L.mword[i - c0] = len ? len | ((m.pos + i - src) << 16) : 0u;
             LZ_SYNC();
-            if (i + 3 < n && i < cend) atomicMax(&L.htab[lz_hash(msg_word(i))], m.pos + i + 1);
+            if (i + 3 < n && i < cend) atomicMax(&L.htab[lz_hash(msg_dword(i))], m.pos + i + 1);
             LZ_SYNC();
         }
         LZ_PHASE(1)
@@ -405,19 +402,19 @@ tamd_lz_compress(const tamd_lz_job* __restrict__ jobs, uint32_t n_jobs, const ta
         const tamd_lz_msg m0 = msgs[job.first];
         uint32_t w0 = m0.win;
         if (m0.pos - w0 > TAMD_LZ_WINDOW) w0 = m0.pos - TAMD_LZ_WINDOW;
-        // 16 consecutive positions per lane: 19 bytes loaded once, 16 hashes from registers
+        // 16 consecutive positions per lane: 24 bytes loaded once, 16 keys from registers
         for (uint32_t q = w0; q < m0.pos; q += 1024) {
             const uint32_t p0 = q + 16u * lane;
             if (p0 < m0.pos) {
-                const uint64_t a = lz_dword(buf, mask, p0), b = lz_dword(buf, mask, p0 + 8);
-                const uint32_t c = lz_word(buf, mask, p0 + 16);
+                const uint64_t a = lz_dword(buf, mask, p0), b = lz_dword(buf, mask, p0 + 8),
+                               c = lz_dword(buf, mask, p0 + 16);
 #pragma unroll
                 for (uint32_t k = 0; k < 16; ++k) {
-                    uint32_t w;
-                    if (k == 0) w = (uint32_t)a;
-                    else if (k < 8) w = (uint32_t)(a >> (8 * k)) | (k > 4 ? (uint32_t)(b << (64 - 8 * k)) : 0u);
-                    else if (k == 8) w = (uint32_t)b;
-                    else w = (uint32_t)(b >> (8 * (k - 8))) | (k > 12 ? c << (32 - 8 * (k - 12)) : 0u);
+                    uint64_t w;
+                    if (k == 0) w = a;
+                    else if (k < 8) w = (a >> (8 * k)) | (b << (64 - 8 * k));
+                    else if (k == 8) w = b;
+                    else w = (b >> (8 * (k - 8))) | (c << (64 - 8 * (k - 8)));
                     if (p0 + k < m0.pos) atomicMax(&L.htab[lz_hash(w)], p0 + k + 1);
                 }
             }
@@ -439,7 +436,7 @@ tamd_lz_compress(const tamd_lz_job* __restrict__ jobs, uint32_t n_jobs, const ta
             if (lane == 0) written[mi] = 0;
             for (uint32_t q = m.pos; q + 3 < m.pos + n; q += 64) {
                 const uint32_t pp = q + lane;
-                if (pp + 3 < m.pos + n) atomicMax(&L.htab[lz_hash(lz_word(buf, mask, pp))], pp + 1);
+                if (pp + 3 < m.pos + n) atomicMax(&L.htab[lz_hash(lz_dword(buf, mask, pp))], pp + 1);
             }
             LZ_SYNC();
             continue;
