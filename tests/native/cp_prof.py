@@ -17,6 +17,8 @@ for a in sys.argv[1:]:
         args.append(a)
 if not args:
     args = ["streams=16", "n=49152", "step=4096", "warm=2"]
+# (the binary is not part of the Makefile's default target: rebuild it from the current sources)
+subprocess.run(["make", "-s", "-C", here, "_build/cp_bench_prof"], check=True)
 best, ns = {}, []
 for _ in range(runs):
     r = subprocess.run([os.path.join(here, "_build", "cp_bench_prof")] + args, capture_output=True, text=True)
