@@ -377,20 +377,22 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
         unit += (count + TAMD_RBATCH - 1) / TAMD_RBATCH;
         return;
     } else if (mode == TAMD_R_DENSE || (mode == TAMD_R_CAUCHY && (a.w0 >> 24) > 1u)) {
-        // Rows with a per-row coefficient computed by wave-uniform scalar work, then one product
-        // per byte:
+        // Rows with a per-row coefficient, then one product per byte:
         //  - DENSE: a Siamese row's dense part packet by packet (program.h); row k's coefficient
         //    is the lane-sum combination the recovery row reads, from its lane's opcode bits, cx
         //    and rx;
         //  - scaled CAUCHY (a decoder elimination run): s * CauchyElement(p, col mod 64).
+        // The coefficients of 64 rows are computed at once, lane j taking row base + j (the table
+        // lookups of one row depend on each other; across rows they do not); each row then reads
+        // its product table at the index broadcast from its lane, so no row waits on the LDS
+        // round trips of its own coefficient.
         const bool dense = mode == TAMD_R_DENSE;
         const u64 opw = (u64)tg.row | ((u64)(tg.len & 0xffffu) << 32);
         const PermT prx = perm_at(lds, (dense ? (tg.len >> 16) & 0xffu : a.w0 >> 24) * 8u);
         const uint8_t* sqr = (const uint8_t*)(lds + TAMD_LDS_INV + 64u);
         const uint8_t* inv = (const uint8_t*)(lds + TAMD_LDS_INV);
         const uint32_t px = p + 64u;
-        uint32_t col = col0;
-        const uint32_t cs = cstep;
+        const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
         auto coef = [&](uint32_t c) -> uint32_t {
             if (!dense) return mul_sel(sel4(inv[(c & 63u) ^ px]), prx) & 0xffu;
             const uint32_t b = (uint32_t)(opw >> (6u * (c & 7u))) & 63u;
@@ -398,6 +400,14 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
             const uint32_t sd = (b & 1u) ^ ((b & 2u) ? cx : 0u) ^ ((b & 4u) ? cx2 : 0u);
             const uint32_t tp = ((b >> 3) & 1u) ^ ((b & 16u) ? cx : 0u) ^ ((b & 32u) ? cx2 : 0u);
             return (sd ^ mul_sel(sel4(tp), prx)) & 0xffu;
+        };
+        uint32_t gv = 0, gblk = ~0u;  // gv: lane j's table index for row 64 * gblk + j
+        auto row_tab = [&](uint32_t i) -> PermT {
+            if ((i >> 6) != gblk) {
+                gblk = i >> 6;
+                gv = coef((col0 + ((i & ~63u) + lane) * cstep) & (TAMD_COLUMN_PERIOD - 1u)) * 8u;
+            }
+            return perm_at(lds, (uint32_t)__builtin_amdgcn_readlane((int)gv, (int)(i & 63u)));
         };
         if (TAMD_ROLL && nw == 1u) {  // rolling loads, as for LANE3 runs
             constexpr uint32_t H = TAMD_RBATCH / 2;
@@ -409,11 +419,8 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
 #pragma unroll
                 for (uint32_t h = 0; h < 2; ++h) {
 #pragma unroll
-                    for (uint32_t q = h * H; q < (h ? TAMD_RBATCH : H); ++q) {
-                        const uint32_t g = coef(col);
-                        col = (col + cs) & (TAMD_COLUMN_PERIOD - 1u);
-                        if (e + q < count) a0 ^= lv_mul<NH>(lv_keep<FULL, NH>(d[q], o, len, ox), perm_at(lds, g * 8u));
-                    }
+                    for (uint32_t q = h * H; q < (h ? TAMD_RBATCH : H); ++q)
+                        if (e + q < count) a0 ^= lv_mul<NH>(lv_keep<FULL, NH>(d[q], o, len, ox), row_tab(e + q));
                     if (more) {
 #pragma unroll
                         for (uint32_t q = h * H; q < (h ? TAMD_RBATCH : H); ++q)
@@ -425,21 +432,13 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
             return;
         }
         for (uint32_t e = 0; e < count; e += TAMD_RBATCH) {
-            if ((unit++ & (nw - 1u)) != wid) {
-                col = (col + cs * TAMD_RBATCH) & (TAMD_COLUMN_PERIOD - 1u);
-                continue;
-            }
+            if ((unit++ & (nw - 1u)) != wid) continue;
             LV<NH> d[TAMD_RBATCH];
-            uint32_t c[TAMD_RBATCH];
 #pragma unroll
-            for (uint32_t q = 0; q < TAMD_RBATCH; ++q) {
-                d[q] = TAMD_RUN_ROW(q);
-                c[q] = coef(col);
-                col = (col + cs) & (TAMD_COLUMN_PERIOD - 1u);
-            }
+            for (uint32_t q = 0; q < TAMD_RBATCH; ++q) d[q] = TAMD_RUN_ROW(q);
 #pragma unroll
             for (uint32_t q = 0; q < TAMD_RBATCH; ++q)
-                if (e + q < count) a0 ^= lv_mul<NH>(lv_keep<FULL, NH>(d[q], o, len, ox), perm_at(lds, c[q] * 8u));
+                if (e + q < count) a0 ^= lv_mul<NH>(lv_keep<FULL, NH>(d[q], o, len, ox), row_tab(e + q));
         }
     } else if (mode == TAMD_R_CAUCHY) {
         // CauchyElement(p, col mod 64) = inv((col mod 64) ^ (p + 64)) (SiameseCommon.h:212-218)
