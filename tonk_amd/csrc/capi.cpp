@@ -223,6 +223,15 @@ struct Staging {
     std::vector<Device::ScatterIn> descs;
 
     size_t need(size_t bytes, size_t n_desc) const { return ((bytes + 15) & ~(size_t)15) + n_desc * 16 + 16; }
+    // The current half's packets as zero-copy sources of one batched host_copy (combined
+    // launches): the half is reused by the codec's next adds, which cannot come before the batch
+    // has completed (the codec's caller waits for it).
+    void take_uploads(std::vector<Device::HostCopy>& out) {
+        for (const Device::ScatterIn& d : descs)
+            out.push_back(Device::HostCopy{half[cur] + d.src, (uint64_t)d.row * TAMD_ROW_UNIT, d.len});
+        descs.clear();
+        used = 0;
+    }
     // Enqueue the current half (caller holds the device lock).
     void send_locked(Device& dev) {
         if (descs.empty()) return;
@@ -363,10 +372,15 @@ bool capi_combine() {
     static const bool on = !(getenv("TONK_AMD_CAPI_COMBINE") && atoi(getenv("TONK_AMD_CAPI_COMBINE")) == 0);
     return on;
 }
+// The event behind a combined batch, released by the last of its callers to finish waiting.
+struct BatchDone {
+    void* ev = nullptr;
+    std::atomic<int> left{0};
+};
 struct RunReq {
     Codec* c = nullptr;
     const std::function<void(Device&)>* reads = nullptr;
-    void* ev = nullptr;
+    BatchDone* done = nullptr;
     bool launched = false, ok = true;
 };
 std::mutex g_run_mu;
@@ -374,16 +388,23 @@ std::condition_variable g_run_cv;
 std::vector<RunReq*> g_run_q;
 bool g_run_leader = false;
 
+// One batch = one zero-copy upload launch for every codec's staged packets, the merged program's
+// level launches, one zero-copy read-back launch for every caller's reads and one event: a fixed
+// handful of commands however many callers it serves (per-codec copies would queue one H2D and
+// one D2H command per caller on the stream).
 void launch_batch(const std::vector<RunReq*>& b) {
     DevLock dl;
     Device& dev = g_rt->dev;
     dev.select_stream(0);
     std::vector<Context*> ctxs;
+    thread_local std::vector<Device::HostCopy> up;
+    up.clear();
     const uint64_t launches = dev.stats().launches;
     for (RunReq* r : b) {
-        r->c->staging.send_locked(dev);  // packets added since the codec's last program land first
+        r->c->staging.take_uploads(up);  // packets added since the codec's last program land first
         if (!r->c->ctx.pb.empty()) ctxs.push_back(&r->c->ctx);
     }
+    dev.host_copy(up.data(), (uint32_t)up.size(), false);
     if (!ctxs.empty()) {
         dev.run(ctxs.data(), ctxs.size());
         g_programs.fetch_add(ctxs.size(), std::memory_order_relaxed);
@@ -391,10 +412,17 @@ void launch_batch(const std::vector<RunReq*>& b) {
     }
     g_batches.fetch_add(1, std::memory_order_relaxed);
     g_batched.fetch_add(b.size(), std::memory_order_relaxed);
+    dev.collect_host_reads(true);
+    for (RunReq* r : b) (*r->reads)(dev);
+    dev.collect_host_reads(false);
+    dev.flush_host_reads();
+    BatchDone* done = new BatchDone();
+    done->ev = dev.record_event();
+    done->left.store((int)b.size());
+    const bool ok = !dev.failed();
     for (RunReq* r : b) {
-        (*r->reads)(dev);
-        r->ev = dev.record_event();
-        r->ok = !dev.failed();
+        r->done = done;
+        r->ok = ok;
     }
 }
 
@@ -407,6 +435,7 @@ bool run_and_read(Codec& c, Reads enqueue_reads) {
     ctx.prepare_flush();
     const int64_t t1 = g_watch ? now_ns() : 0;
     void* ev = nullptr;
+    BatchDone* batch = nullptr;
     bool ok = true;
     if (capi_combine()) {
         const std::function<void(Device&)> f(enqueue_reads);
@@ -433,8 +462,8 @@ bool run_and_read(Codec& c, Reads enqueue_reads) {
                 g_run_cv.notify_all();  // a caller still queued becomes the next leader
             }
         }
-        ev = req.ev;
         ok = req.ok;
+        batch = req.done;
     } else {
         DevLock dl;
         Device& dev = g_rt->dev;
@@ -458,13 +487,16 @@ bool run_and_read(Codec& c, Reads enqueue_reads) {
     ctx.finish_flush();
     const int64_t w0 = now_ns();
     if (g_in_wait.fetch_add(1) == 0) g_in_wait_since.store(w0);
-    ok = Device::event_wait(ev) && ok;
+    ok = Device::event_wait(batch ? batch->ev : ev) && ok;
     if (g_in_wait.fetch_sub(1) == 1) g_in_wait_since.store(0);
     g_waits.fetch_add(1, std::memory_order_relaxed);
     g_wait_ns.fetch_add((uint64_t)(now_ns() - w0), std::memory_order_relaxed);
-    {
+    if (!batch || batch->left.fetch_sub(1) == 1) {
         DevLock dl;
-        g_rt->dev.event_release(ev);
+        g_rt->dev.event_release(batch ? batch->ev : ev);
+        ok = ok && !g_rt->dev.failed();
+        delete batch;
+    } else {
         ok = ok && !g_rt->dev.failed();
     }
     c.staging.all_settled();         // every staged copy was enqueued before `ev`

@@ -20,6 +20,8 @@ extern "C" __global__ void tamd_timed_region();
 extern "C" __global__ void tamd_gather_rows(const tamd::Device::GatherDesc*, uint32_t, const uint8_t*, uint8_t*);
 struct ScatterDescDev { uint32_t row, len, src, pad; };
 extern "C" __global__ void tamd_scatter_rows(const ScatterDescDev*, uint32_t, const uint8_t*, uint8_t*);
+struct HostCopyDev { uint64_t host; uint32_t unit, len; };
+extern "C" __global__ void tamd_host_copy(const HostCopyDev*, uint32_t, uint8_t*, uint32_t);
 
 struct GenDescDev { uint32_t row, index, len, pad; unsigned long long seed; };
 struct DigestDescDev { uint32_t row, skip, len, pad; };
@@ -70,6 +72,10 @@ Device::~Device() {
     if (sc_dev_ && sc_per_stream_.empty()) hipFree(sc_dev_);
     if (rb_host_) hipHostFree(rb_host_);
     if (up_event_) hipEventDestroy((hipEvent_t)up_event_);
+    for (HcBuf& b : hc_) {
+        if (b.ev) hipEventDestroy((hipEvent_t)b.ev);
+        if (b.p) hipHostFree(b.p);
+    }
     if (d_gf_) hipFree(d_gf_);
     if (d_zero_) hipFree(d_zero_);
     for (VerifyBatch& b : vbatches_)
@@ -1056,8 +1062,56 @@ void Device::download_async(void* dst, uint64_t off, size_t n) {
 }
 
 void Device::download_pinned(void* dst, uint64_t off, size_t n) {
+    if (collect_reads_) {
+        if (n) reads_.push_back(HostCopy{dst, off, (uint32_t)n});
+        return;
+    }
     flush_uploads();
     if (n) HIPCHK(hipMemcpyAsync(dst, arena_ + off, n, hipMemcpyDeviceToHost, (hipStream_t)stream_));
+}
+
+void Device::flush_host_reads() {
+    if (!reads_.empty()) host_copy(reads_.data(), (uint32_t)reads_.size(), true);
+    reads_.clear();
+}
+
+void Device::host_copy(const HostCopy* d, uint32_t n, bool to_host) {
+    if (!n) return;
+    flush_uploads();
+    hipStream_t st = (hipStream_t)stream_;
+    HcBuf& b = hc_[hc_next_++ % (sizeof(hc_) / sizeof(hc_[0]))];
+    if (b.ev) HIPCHK(hipEventSynchronize((hipEvent_t)b.ev));  // (its previous launch has read it)
+    const size_t need = (size_t)n * sizeof(HostCopyDev);
+    if (need > b.cap) {
+        if (b.p) hipHostFree(b.p);
+        b.cap = need + need / 2 + 4096;
+        if (hipHostMalloc(&b.p, b.cap, hipHostMallocDefault) != hipSuccess) {
+            b.p = nullptr;
+            b.cap = 0;
+            error_ = "host copy descriptor allocation failed";
+            failed_ = true;
+            return;
+        }
+    }
+    HostCopyDev* hd = (HostCopyDev*)b.p;
+    for (uint32_t k = 0; k < n; ++k) {
+        if (((uintptr_t)d[k].host & 15u) || (d[k].arena_off & 63u) || d[k].arena_off / 64 > 0xffffffffull) {
+            error_ = "host copy: unaligned host buffer or arena offset";
+            failed_ = true;
+            return;
+        }
+        hd[k].host = (uint64_t)(uintptr_t)d[k].host;
+        hd[k].unit = (uint32_t)(d[k].arena_off / 64);
+        hd[k].len = d[k].len;
+    }
+    hipLaunchKernelGGL(tamd_host_copy, dim3(n), dim3(128), 0, st, (const HostCopyDev*)b.p, n, arena_, to_host ? 1u : 0u);
+    HIPCHK(hipGetLastError());
+    if (!b.ev) {
+        hipEvent_t he;
+        HIPCHK(hipEventCreateWithFlags(&he, hipEventDisableTiming));
+        b.ev = he;
+    }
+    HIPCHK(hipEventRecord((hipEvent_t)b.ev, st));
 }
 
 void* Device::record_event() {

@@ -143,6 +143,17 @@ public:
     // caller's pinned buffer, then an event recorded behind it.  event_wait() may run without
     // any lock; record/release must hold the same lock as every other Device call.
     void download_pinned(void* pinned_dst, uint64_t arena_offset, size_t n);
+    // Zero-copy transfers between pinned host memory and the arena: one tamd_host_copy launch
+    // moves every listed packet (the kernel reads or writes the host pages over the link), instead
+    // of a copy command per packet.  Host addresses must be pinned (host_alloc) and 16-B aligned;
+    // arena offsets 64-B aligned.  to_host = false: the host bytes must stay untouched until an
+    // event recorded after this call has completed; true: they are valid once it has.
+    struct HostCopy { void* host; uint64_t arena_off; uint32_t len; };
+    void host_copy(const HostCopy* d, uint32_t n, bool to_host);
+    // While collecting, download_pinned() only lists its copy; flush_host_reads() then runs every
+    // listed copy as one host_copy(to_host) launch (the C ABI's combined batches).
+    void collect_host_reads(bool on) { collect_reads_ = on; }
+    void flush_host_reads();
     void* record_event();
     static bool event_wait(void* ev);  // false when the wait failed
     void event_release(void* ev) { free_events_.push_back(ev); }
@@ -303,6 +314,13 @@ private:
     uint8_t* up_host_ = nullptr;
     uint8_t* up_dev_ = nullptr;
     uint8_t* sc_dev_ = nullptr;  // scatter_upload landing area (of the current stream)
+    // host_copy: descriptor buffers (pinned, read by the kernel over the link), used in turn; each
+    // is reused once the event recorded behind its launch has completed
+    struct HcBuf { void* p = nullptr; size_t cap = 0; void* ev = nullptr; };
+    HcBuf hc_[8];
+    unsigned hc_next_ = 0;
+    bool collect_reads_ = false;
+    std::vector<HostCopy> reads_;
     size_t sc_cap_ = 0;
     std::vector<void*> streams_;  // all launch streams (add_streams), streams_[0] = the first
     std::vector<std::pair<uint8_t*, size_t>> sc_per_stream_;  // landing areas of the others

@@ -846,6 +846,23 @@ extern "C" __global__ void tamd_scatter_rows(const ScatterDesc* __restrict__ d, 
     for (uint32_t i = n16 * 16u + threadIdx.x; i < g.len; i += blockDim.x) dst[i] = src[i];
 }
 
+// Zero-copy transfers between pinned host memory and the arena (Device::host_copy): one
+// workgroup per packet reads (to_host = 0) or writes (1) the host bytes over the link directly.
+// Host addresses are 16-B aligned, arena rows 64-B aligned.
+struct HostCopyDesc { u64 host; uint32_t unit, len; };
+
+extern "C" __global__ void __launch_bounds__(128)
+tamd_host_copy(const HostCopyDesc* __restrict__ d, uint32_t n, uint8_t* __restrict__ arena, uint32_t to_host) {
+    const HostCopyDesc c = d[blockIdx.x];
+    uint8_t* a = arena + (size_t)c.unit * TAMD_ROW_UNIT;
+    uint8_t* h = (uint8_t*)c.host;
+    uint8_t* dst = to_host ? h : a;
+    const uint8_t* src = to_host ? a : h;
+    const uint32_t n16 = c.len / 16u;
+    for (uint32_t i = threadIdx.x; i < n16; i += blockDim.x) ((uint4*)dst)[i] = ((const uint4*)src)[i];
+    for (uint32_t i = n16 * 16u + threadIdx.x; i < c.len; i += blockDim.x) dst[i] = src[i];
+}
+
 // Digest of rows (FNV-1a 64 over `len` bytes starting `skip` bytes into the row): one thread
 // per row, for output verification after a timed run (not on the timed path).
 struct DigestDesc { uint32_t row, skip, len, pad; };
