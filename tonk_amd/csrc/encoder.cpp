@@ -786,12 +786,65 @@ void Encoder::add_dense(uint32_t row, uint32_t recovery_bytes, Sym& rec) {
 // (program.h), each packet weighted by its lane's opcode combination -- no lane walk, snapshot
 // or carried sum.  Bytes are the same: a lane sum is its packets zero-padded to the longest, and
 // each packet is clipped to the recovery length as the sum would be.
+uint32_t Encoder::dense_direct_rows() const {
+    const uint32_t lo = sum_abs_start(), hi = base_ + count_;
+    uint32_t n = 0;
+    for (size_t i = seg_index_at(lo); i < segs_.size(); ++i) {
+        const Segment& sg = segs_[i];
+        if ((int32_t)(sg.first - hi) >= 0) break;
+        const uint32_t a = (int32_t)(sg.first - lo) > 0 ? sg.first : lo;
+        const uint32_t b = (int32_t)(sg.end() - hi) < 0 ? sg.end() : hi;
+        if ((int32_t)(b - a) > 0 && sg.bytes) n += b - a;
+    }
+    return n;
+}
+
 void Encoder::add_dense_direct(uint32_t row, uint32_t recovery_bytes) {
     uint64_t ops = 0;
     for (unsigned l = 0; l < kLanes; ++l) ops |= (uint64_t)row_opcode(l, row) << (6 * l);
     const uint8_t rx = row_value(row);
     const uint32_t lo = sum_abs_start(), hi = base_ + count_;
     ProgramBuilder& pb = ctx_->pb;
+    static const uint32_t split = getenv("TONK_AMD_DENSE_SPLIT") ? (uint32_t)atoi(getenv("TONK_AMD_DENSE_SPLIT"))
+                                                                  : kDenseSplit;
+    const uint32_t total = split ? dense_direct_rows() : 0;
+    if (split && total > split) {
+        // Partial sums of at most `split` packets each, closed before the row's own op: the
+        // caller's op (begun already, still empty) is set aside and reopened after them.
+        const uint32_t parts = (total + split - 1) / split, per = (total + parts - 1) / parts;
+        thread_local std::vector<RowId> partial;
+        partial.clear();
+        uint32_t left = 0;  // packets the current partial still takes
+        for (size_t i = seg_index_at(lo); i < segs_.size(); ++i) {
+            const Segment& sg = segs_[i];
+            if ((int32_t)(sg.first - hi) >= 0) break;
+            uint32_t a = (int32_t)(sg.first - lo) > 0 ? sg.first : lo;
+            const uint32_t b = (int32_t)(sg.end() - hi) < 0 ? sg.end() : hi;
+            if ((int32_t)(b - a) <= 0 || !sg.bytes) continue;
+            const uint32_t len = sg.bytes < recovery_bytes ? sg.bytes : recovery_bytes;
+            while (a != b) {
+                if (!left) {
+                    if (!partial.empty()) pb.finish_combine(partial.back(), recovery_bytes, nullptr, 0);
+                    const RowId t = ctx_->alloc_temp(recovery_bytes);
+                    if (t == kNoRow) { disabled_ = true; break; }
+                    partial.push_back(t);
+                    pb.begin_op();
+                    left = per;
+                }
+                const uint32_t k = std::min(b - a, left);
+                const uint32_t j = a - sg.first;
+                pb.op_accr_dense(sg.off(j), sg.stride, k, len, col_add(sg.column0, j), ops, rx);
+                a += k;
+                left -= k;
+            }
+            if (disabled_) break;
+        }
+        if (!partial.empty()) pb.finish_combine(partial.back(), recovery_bytes, nullptr, 0);
+        pb.begin_op();  // the row's op again: the partials, then the caller's terms
+        for (RowId t : partial) pb.op_acc(t, 1, recovery_bytes);
+        sum_end_ = count_;
+        return;
+    }
     for (size_t i = seg_index_at(lo); i < segs_.size(); ++i) {
         const Segment& sg = segs_[i];
         if ((int32_t)(sg.first - hi) >= 0) break;

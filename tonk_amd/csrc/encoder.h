@@ -229,6 +229,12 @@ private:
     Result generate_cauchy(RecoveryOut& out);
     void add_dense(uint32_t row, uint32_t recovery_bytes, Sym& rec);
     void add_dense_direct(uint32_t row, uint32_t recovery_bytes);  // (into the op under construction)
+    // Packets of the direct dense range (add_dense_direct's rows).
+    uint32_t dense_direct_rows() const;
+    // Longer direct dense ranges are split: partial sums of at most this many packets, one pure
+    // combine each (level 1), added by the row's op (level 2), so no single work item walks
+    // hundreds of packets (a level's tail).  TONK_AMD_DENSE_SPLIT overrides (A/B knob; 0: never).
+    static const uint32_t kDenseSplit = 192;
     void add_light(uint32_t row, Sym& rec);
     Result emit(Sym& terms, uint32_t len, const RecoveryMeta& meta, RecoveryOut& out, bool distinct);
     Sym scratch_, rec_;
