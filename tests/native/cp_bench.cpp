@@ -126,6 +126,31 @@ static void on_prof(int, siginfo_t*, void* uc) {
     }
 }
 
+// Rows read per program by instruction kind: ACC/ACC3 rows and ACCR runs by mode (CAUCHY split
+// into plain -- encoder windows -- and scaled -- decoder run terms), in row loads and bytes.
+static void dump_reads(Context& ctx) {
+    const auto& ins = ctx.pb.instrs();
+    const char* names[8] = {"acc", "lane3", "cauchy", "const", "multi", "dense", "cauchy_scaled", "acc3"};
+    uint64_t rows[8] = {0}, bytes[8] = {0};
+    for (size_t k = 0; k < ins.size(); ++k) {
+        const uint32_t kind = ins[k].w0 & 0xff;
+        int m = -1;
+        uint64_t n = 1;
+        if (kind == TAMD_I_ACC) m = 0;
+        else if (kind == TAMD_I_ACC3) m = 7;
+        else if (kind == TAMD_I_ACCR) {
+            const uint32_t mode = (ins[k].w0 >> 8) & 0xff;
+            m = mode == TAMD_R_CAUCHY && (ins[k].w0 >> 24) > 1 ? 6 : (int)mode;
+            n = ins[k].cap;
+        }
+        if (m < 0 || m > 7) continue;
+        rows[m] += n;
+        bytes[m] += n * ins[k].len;
+    }
+    for (int m = 0; m < 8; ++m)
+        if (rows[m]) fprintf(stderr, "reads %-14s rows %8llu  MB %8.2f\n", names[m], (unsigned long long)rows[m], bytes[m] / 1e6);
+}
+
 static void dump_levels(Context& ctx) {
             for (size_t b = 0; b < ctx.pb.level_ops().size(); ++b)
                 fprintf(stderr, "bucket %zu (level %zu class %zu): ops %u items %u\n", b, b / TAMD_COST_CLASSES, b % TAMD_COST_CLASSES,
@@ -314,6 +339,7 @@ int main(int argc, char** argv) {
                 ctx.prepare_flush();
             }
             if (getenv("CP_BENCH_LEVELS") && done == step && s == 0) dump_levels(ctx);
+            if (getenv("CP_BENCH_READS") && done == step && s == 0) dump_reads(ctx);
             instrs += ctx.pb.instrs().size();
             ops += ctx.pb.ops().size();
             acc_bytes += ctx.pb.acc_bytes();
