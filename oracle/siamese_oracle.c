@@ -533,6 +533,7 @@ int oracle_run_program(uint8_t* arena, size_t arena_bytes,
                     if (k + 2 >= count) { free(acc); return -15; }
                     tg = w + 8;
                     if ((tg[0] & 0xff) != (mode == R_MULTI ? I_TARGETS : I_COEFS)) { free(acc); return -16; }
+                    if (mode == R_DENSE && k + 2 + tg[3] >= count) { free(acc); return -18; }
                 }
                 for (uint32_t e = 0; e < n; ++e) {
                     const size_t base = ((size_t)w[1] + (size_t)e * stride) * 64u;
@@ -557,7 +558,13 @@ int oracle_run_program(uint8_t* arena, size_t arena_bytes,
                         const uint8_t cx = oracle_column_value(col), cx2 = oracle_gf_sqr(cx);
                         const uint8_t sdir = (uint8_t)((b & 1u) ^ ((b & 2u) ? cx : 0u) ^ ((b & 4u) ? cx2 : 0u));
                         const uint8_t tprod = (uint8_t)(((b >> 3) & 1u) ^ ((b & 16u) ? cx : 0u) ^ ((b & 32u) ? cx2 : 0u));
-                        const uint8_t g = (uint8_t)(sdir ^ oracle_gf_mul(rx, tprod));
+                        uint8_t g = (uint8_t)(sdir ^ oracle_gf_mul(rx, tprod));
+                        /* ADJ words (COEFS.cap of them): idx << 16 | delta << 8 additions */
+                        for (uint32_t w = 0; w < tg[3]; ++w)
+                            for (unsigned q = 0; q < 4; ++q) {
+                                const uint32_t d = tg[4 + 4 * w + q];
+                                if ((d >> 16) == e) g ^= (uint8_t)(d >> 8);
+                            }
                         if (g) oracle_muladd_mem(acc, g, row, len);
                     } else if (mode == R_MULTI) {
                         for (unsigned a = 0; a < 3; ++a) {
@@ -572,7 +579,7 @@ int oracle_run_program(uint8_t* arena, size_t arena_bytes,
                         free(acc); return -14;
                     }
                 }
-                k += (mode == R_MULTI || mode == R_DENSE) ? 2 : 1; /* consumed RANGE (and TARGETS / COEFS) */
+                k += mode == R_DENSE ? 2 + tg[3] : mode == R_MULTI ? 2 : 1; /* RANGE (+ TARGETS / COEFS + ADJ) */
             } else if (kind == I_STOREC) {
                 const uint8_t c[3] = { (uint8_t)(w[0] >> 8), (uint8_t)(w[0] >> 16), (uint8_t)(w[0] >> 24) };
                 const size_t base = (size_t)w[1] * 64u;

@@ -799,12 +799,29 @@ uint32_t Encoder::dense_direct_rows() const {
     return n;
 }
 
-void Encoder::add_dense_direct(uint32_t row, uint32_t recovery_bytes) {
+void Encoder::add_dense_direct(uint32_t row, uint32_t recovery_bytes, const std::vector<uint64_t>& pairs) {
     uint64_t ops = 0;
     for (unsigned l = 0; l < kLanes; ++l) ops |= (uint64_t)row_opcode(l, row) << (6 * l);
     const uint8_t rx = row_value(row);
     const uint32_t lo = sum_abs_start(), hi = base_ + count_;
     ProgramBuilder& pb = ctx_->pb;
+    // A DENSE run over absolute elements [e0, e0 + k), with the pair columns that fall in it
+    // (pairs are sorted, runs come in element order: one cursor)
+    size_t pi = 0;
+    std::vector<uint32_t>& adj = adj_;
+    thread_local std::vector<uint64_t> loose;  // pair columns outside every run (read as rows)
+    loose.clear();
+    auto dense = [&](const Segment& sg, uint32_t j, uint32_t k, uint32_t len) {
+        const uint32_t e0 = sg.first + j;
+        adj.clear();
+        while (pi < pairs.size() && (int32_t)((uint32_t)(pairs[pi] >> 8) - e0) < 0) loose.push_back(pairs[pi++]);
+        while (pi < pairs.size() && (int32_t)((uint32_t)(pairs[pi] >> 8) - (e0 + k)) < 0) {
+            adj.push_back(((uint32_t)(pairs[pi] >> 8) - e0) << 16 | (uint32_t)(pairs[pi] & 0xffu) << 8);
+            ++pi;
+        }
+        pb.op_accr_dense(sg.off(j), sg.stride, k, len, col_add(sg.column0, j), ops, rx, adj.data(),
+                         (uint32_t)adj.size());
+    };
     static const uint32_t split = getenv("TONK_AMD_DENSE_SPLIT") ? (uint32_t)atoi(getenv("TONK_AMD_DENSE_SPLIT"))
                                                                   : kDenseSplit;
     const uint32_t total = split ? dense_direct_rows() : 0;
@@ -832,8 +849,7 @@ void Encoder::add_dense_direct(uint32_t row, uint32_t recovery_bytes) {
                     left = per;
                 }
                 const uint32_t k = std::min(b - a, left);
-                const uint32_t j = a - sg.first;
-                pb.op_accr_dense(sg.off(j), sg.stride, k, len, col_add(sg.column0, j), ops, rx);
+                dense(sg, a - sg.first, k, len);
                 a += k;
                 left -= k;
             }
@@ -842,6 +858,7 @@ void Encoder::add_dense_direct(uint32_t row, uint32_t recovery_bytes) {
         if (!partial.empty()) pb.finish_combine(partial.back(), recovery_bytes, nullptr, 0);
         pb.begin_op();  // the row's op again: the partials, then the caller's terms
         for (RowId t : partial) pb.op_acc(t, 1, recovery_bytes);
+        add_loose_pairs(pairs, pi, loose);
         sum_end_ = count_;
         return;
     }
@@ -851,11 +868,22 @@ void Encoder::add_dense_direct(uint32_t row, uint32_t recovery_bytes) {
         const uint32_t a = (int32_t)(sg.first - lo) > 0 ? sg.first : lo;
         const uint32_t b = (int32_t)(sg.end() - hi) < 0 ? sg.end() : hi;
         if ((int32_t)(b - a) <= 0 || !sg.bytes) continue;
-        const uint32_t j = a - sg.first;
         const uint32_t len = sg.bytes < recovery_bytes ? sg.bytes : recovery_bytes;
-        pb.op_accr_dense(sg.off(j), sg.stride, b - a, len, col_add(sg.column0, j), ops, rx);
+        dense(sg, a - sg.first, b - a, len);
     }
+    add_loose_pairs(pairs, pi, loose);
     sum_end_ = count_;
+}
+
+// Pair columns no dense run covered (pairs[from..) and `loose`): plain row reads, as add_light.
+void Encoder::add_loose_pairs(const std::vector<uint64_t>& pairs, size_t from, const std::vector<uint64_t>& loose) {
+    auto one = [&](uint64_t p) {
+        const uint32_t e = (uint32_t)(p >> 8) - base_;
+        const Segment& sg = seg_of(e);
+        ctx_->pb.op_acc(sg.row(e + base_ - sg.first), (uint8_t)(p & 0xffu), sg.bytes);
+    };
+    for (uint64_t p : loose) one(p);
+    for (size_t i = from; i < pairs.size(); ++i) one(pairs[i]);
 }
 
 // Encoder::AddLightColumns (SiameseEncoder.cpp:1100-1144).  The product half goes straight into
@@ -881,6 +909,24 @@ void Encoder::add_light(uint32_t row, Sym& rec) {
         t[2 * i] = Term{s1.row(e1 + base_ - s1.first), s1.bytes, 1};
         t[2 * i + 1] = Term{srx.row(erx + base_ - srx.first), srx.bytes, rx};
     }
+}
+
+void Encoder::light_pairs(uint32_t row, std::vector<uint64_t>& out) {
+    const uint32_t start = first_unremoved_;
+    const uint32_t count = sum_end_ - start;
+    const uint8_t rx = row_value(row);
+    Pcg32 prng;
+    prng.seed(row, count);
+    const uint32_t pairs = (count + kPairRate - 1) / kPairRate;
+    out.resize(2 * (size_t)pairs);
+    const FastMod mod(count);
+    for (uint32_t i = 0; i < pairs; ++i) {
+        const uint32_t e1 = start + mod(prng.next());
+        const uint32_t erx = start + mod(prng.next());
+        out[2 * i] = (uint64_t)(base_ + e1) << 8 | 1u;
+        out[2 * i + 1] = (uint64_t)(base_ + erx) << 8 | rx;
+    }
+    std::sort(out.begin(), out.end());
 }
 
 // Encoder::Encode (SiameseEncoder.cpp:1146-1254)
@@ -924,7 +970,8 @@ Result Encoder::encode(RecoveryOut& out) {
     }
     {
         TAMD_PROF_SCOPE(kEncLight);
-        add_light(row, rec);
+        if (direct) light_pairs(row, pairs_);  // (folded into the dense runs' coefficients)
+        else add_light(row, rec);
     }
 
     RecoveryMeta m;
@@ -941,8 +988,7 @@ Result Encoder::encode(RecoveryOut& out) {
         if (out.row == kNoRow) { disabled_ = true; return kDisabled; }
         ProgramBuilder& pb = ctx_->pb;
         pb.begin_op();
-        add_dense_direct(row, recovery_bytes);
-        for (const Term& t : rec) pb.op_acc(t.row, t.coef, t.len);
+        add_dense_direct(row, recovery_bytes, pairs_);
         pb.finish_combine(out.row, recovery_bytes, out.footer, out.footer_len);
         stats_[2]++;
         stats_[3] += out.total();

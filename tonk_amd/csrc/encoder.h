@@ -228,7 +228,9 @@ private:
     Result generate_single(RecoveryOut& out);
     Result generate_cauchy(RecoveryOut& out);
     void add_dense(uint32_t row, uint32_t recovery_bytes, Sym& rec);
-    void add_dense_direct(uint32_t row, uint32_t recovery_bytes);  // (into the op under construction)
+    // (into the op under construction) the dense range's runs with the row's LDPC pair columns
+    // `pairs` (light_pairs) folded into their coefficients
+    void add_dense_direct(uint32_t row, uint32_t recovery_bytes, const std::vector<uint64_t>& pairs);
     // Packets of the direct dense range (add_dense_direct's rows).
     uint32_t dense_direct_rows() const;
     // Longer direct dense ranges are split: partial sums of at most this many packets, one pure
@@ -236,6 +238,11 @@ private:
     // hundreds of packets (a level's tail).  TONK_AMD_DENSE_SPLIT overrides (A/B knob; 0: never).
     static const uint32_t kDenseSplit = 192;
     void add_light(uint32_t row, Sym& rec);
+    // The same pair columns as (absolute element << 8 | coefficient), sorted by element.
+    void light_pairs(uint32_t row, std::vector<uint64_t>& out);
+    void add_loose_pairs(const std::vector<uint64_t>& pairs, size_t from, const std::vector<uint64_t>& loose);
+    std::vector<uint64_t> pairs_;
+    std::vector<uint32_t> adj_;
     Result emit(Sym& terms, uint32_t len, const RecoveryMeta& meta, RecoveryOut& out, bool distinct);
     Sym scratch_, rec_;
     struct Run { RowId row; uint32_t off, stride, count, len, col; };

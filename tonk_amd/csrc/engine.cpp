@@ -216,8 +216,9 @@ void ProgramBuilder::op_accr_multi(uint32_t row0, uint32_t stride, uint32_t coun
 }
 
 void ProgramBuilder::op_accr_dense(uint32_t row0, uint32_t stride, uint32_t count, uint32_t len, uint32_t col0,
-                                   uint64_t ops, uint8_t rx) {
+                                   uint64_t ops, uint8_t rx, const uint32_t* adj, uint32_t nadj) {
     if (!len || !count) return;
+    const uint32_t nwords = (nadj + 3) / 4;
     tamd_instr a, r, g;
     a.w0 = tamd_w0(TAMD_I_ACCR, TAMD_R_DENSE, 0);
     a.row = row0;
@@ -231,10 +232,20 @@ void ProgramBuilder::op_accr_dense(uint32_t row0, uint32_t stride, uint32_t coun
     g.row = (uint32_t)ops;
     g.len = (uint32_t)(ops >> 32) & 0xffffu;
     g.len |= (uint32_t)rx << 16;
-    g.cap = 0;
+    g.cap = nwords;
     instrs_.push_back(a);
     instrs_.push_back(r);
     instrs_.push_back(g);
+    for (uint32_t w = 0; w < nwords; ++w) {
+        uint32_t d[4] = {0, 0, 0, 0};
+        for (uint32_t q = 0; q < 4 && 4 * w + q < nadj; ++q) d[q] = adj[4 * w + q];
+        tamd_instr x;
+        x.w0 = (d[0] & ~0xffu) | TAMD_I_ADJ;
+        x.row = d[1];
+        x.len = d[2];
+        x.cap = d[3];
+        instrs_.push_back(x);
+    }
     ++cur_runs_;  // (acc_0 only: the op stays a pure combine)
     if (len > cur_span_) cur_span_ = len;
     if (len < cur_full_) cur_full_ = len;

@@ -181,9 +181,10 @@ public:
     void op_accr_multi(uint32_t row0, uint32_t stride, uint32_t count, uint32_t len, uint32_t col0, uint32_t cstep,
                        const uint32_t t[3]);
     // DENSE run: a Siamese row's dense part over a run of level-0 packets (program.h); `ops` holds
-    // the row's 8 lane opcodes, 6 bits each.
+    // the row's 8 lane opcodes, 6 bits each; adj[0..nadj) = (index in the run) << 16 | delta << 8
+    // coefficient additions (ADJ words).
     void op_accr_dense(uint32_t row0, uint32_t stride, uint32_t count, uint32_t len, uint32_t col0, uint64_t ops,
-                       uint8_t rx);
+                       uint8_t rx, const uint32_t* adj = nullptr, uint32_t nadj = 0);
     // Register a run of level-0 rows at offsets off0 + k * stride (k < count), columns col0 + k,
     // with per-row coefficients CauchyElement(p, column mod 64) (mode TAMD_R_CAUCHY) or 1
     // (TAMD_R_CONST), as one symbolic term (kRunFlag) of length len; combine() emits it as one

@@ -256,7 +256,8 @@ __device__ __forceinline__ void lv_store_row(uint8_t* __restrict__ arena, uint32
 // wave combines only the batches with unit mod nw == wid (the coefficient stepping still walks
 // every row).
 template <bool FULL, int NH, uint32_t TAMD_RBATCH>
-__device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& r, const tamd_instr& tg, uint32_t o, uint32_t ox,
+__device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& r, const tamd_instr& tg,
+                                         const tamd_instr* __restrict__ adj, uint32_t o, uint32_t ox,
                                          const uint8_t* __restrict__ arena, const uint32_t* __restrict__ lds,
                                          uint32_t& unit, uint32_t nw, uint32_t wid, LV<NH>& a0, LV<NH>& a1,
                                          LV<NH>& a2) {
@@ -401,11 +402,23 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
             const uint32_t tp = ((b >> 3) & 1u) ^ ((b & 16u) ? cx : 0u) ^ ((b & 32u) ? cx2 : 0u);
             return (sd ^ mul_sel(sel4(tp), prx)) & 0xffu;
         };
+        // DENSE: COEFS.cap ADJ words follow, coefficient additions for single rows (the LDPC pair
+        // columns of the recovery row, SiameseEncoder.cpp:1100-1144, folded into the run)
+        const uint32_t nadj = dense ? tg.cap : 0u;
         uint32_t gv = 0, gblk = ~0u;  // gv: lane j's table index for row 64 * gblk + j
         auto row_tab = [&](uint32_t i) -> PermT {
             if ((i >> 6) != gblk) {
                 gblk = i >> 6;
-                gv = coef((col0 + ((i & ~63u) + lane) * cstep) & (TAMD_COLUMN_PERIOD - 1u)) * 8u;
+                const uint32_t mine = (i & ~63u) + lane;
+                uint32_t g = coef((col0 + mine * cstep) & (TAMD_COLUMN_PERIOD - 1u));
+                for (uint32_t w = 0; w < nadj; ++w) {
+                    const tamd_instr x = adj[w];
+                    const uint32_t d[4] = {x.w0, x.row, x.len, x.cap};
+#pragma unroll
+                    for (uint32_t q = 0; q < 4; ++q)
+                        if ((d[q] >> 16) == mine) g ^= (d[q] >> 8) & 0xffu;
+                }
+                gv = g * 8u;
             }
             return perm_at(lds, (uint32_t)__builtin_amdgcn_readlane((int)gv, (int)(i & 63u)));
         };
@@ -556,10 +569,12 @@ __device__ __forceinline__ LV<NH> run_item(const tamd_instr* __restrict__ instrs
         for (uint32_t j = TAMD_BATCH; j-- > 0;)
             if ((in[j].w0 & 0xffu) == TAMD_I_ACCR && j < nb) nb = j;
         if (nb == 0) {
-            // in[1]: the RANGE word, in[2]: TARGETS (MULTI runs) or COEFS (DENSE runs)
-            run_accr<FULL, NH, TAMD_BATCH>(in[0], in[1], in[2], o, ox, arena, lds, unit, nw, wid, a0, a1, a2);
+            // in[1]: the RANGE word, in[2]: TARGETS (MULTI runs) or COEFS (DENSE runs, followed by
+            // COEFS.cap ADJ words)
+            run_accr<FULL, NH, TAMD_BATCH>(in[0], in[1], in[2], instrs + k + 3, o, ox, arena, lds, unit, nw, wid, a0,
+                                           a1, a2);
             const uint32_t rmode = (in[0].w0 >> 8) & 0xffu;
-            k += (rmode == TAMD_R_MULTI || rmode == TAMD_R_DENSE) ? 3u : 2u;
+            k += rmode == TAMD_R_DENSE ? 3u + in[2].cap : rmode == TAMD_R_MULTI ? 3u : 2u;
             continue;
         }
         if ((unit++ & (nw - 1u)) != wid) {  // another wave's batch (shared ops only)

@@ -60,7 +60,11 @@ enum tamd_instr_kind {
     TAMD_I_ACCR   = 7,  // w0 = kind | mode << 8 | p << 16 (| s << 24: CAUCHY scale); row = row0, len, cap = count
     TAMD_I_RANGE  = 8,  // payload word after ACCR: row = stride (units), len = col0, cap = cstep
     TAMD_I_TARGETS = 9, // payload word after the RANGE of a MULTI ACCR: row, len, cap = t_0, t_1, t_2
-    TAMD_I_COEFS  = 10, // payload word after the RANGE of a DENSE ACCR: lane opcodes and rx
+    TAMD_I_COEFS  = 10, // payload word after the RANGE of a DENSE ACCR: lane opcodes and rx; cap =
+                        // the number of ADJ words that follow it
+    TAMD_I_ADJ    = 11, // payload of a DENSE ACCR: four coefficient additions, each dword
+                        // idx << 16 | delta << 8 (| kind in dword 0): row idx of the run gets
+                        // coefficient ^ delta (delta 0: an empty entry)
 };
 
 enum tamd_range_mode {
