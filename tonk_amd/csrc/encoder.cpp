@@ -926,7 +926,16 @@ void Encoder::light_pairs(uint32_t row, std::vector<uint64_t>& out) {
         out[2 * i] = (uint64_t)(base_ + e1) << 8 | 1u;
         out[2 * i + 1] = (uint64_t)(base_ + erx) << 8 | rx;
     }
-    std::sort(out.begin(), out.end());
+    // (a few dozen entries: insertion sort)
+    for (size_t i = 1; i < out.size(); ++i) {
+        const uint64_t x = out[i];
+        size_t j = i;
+        while (j > 0 && out[j - 1] > x) {
+            out[j] = out[j - 1];
+            --j;
+        }
+        out[j] = x;
+    }
 }
 
 // Encoder::Encode (SiameseEncoder.cpp:1146-1254)
