@@ -284,6 +284,8 @@ int main(int argc, char** argv) {
         Context& ctx = *ctxs[s];
         ctx.ex.expand_limit = expand;
         ctx.backsub_rows = backsub;
+        ctx.dense_split = getenv("TONK_AMD_DENSE_SPLIT") ? (uint32_t)atoi(getenv("TONK_AMD_DENSE_SPLIT"))
+                                                        : (streams > 4 ? Encoder::kDenseSplit : 0u);
         ctx.pipeline = g_pipe != 0;
         ctx.rows.init(4ull * p.n_originals * 1344 + (256u << 20));
         encs[s].reset(new Encoder(&ctx, 1344));

@@ -31,6 +31,7 @@ static bool g_nobatch = false;  // nobatch=1: the runner's single-add path only
 static bool g_pipeline = false;
 static uint32_t g_expand = ~0u;  // expand=<terms>: the session's expansion limit
 static uint32_t g_backsub = ~0u;  // backsub=<unknowns>: back substitution over materialized rows
+static uint32_t g_split = 0;      // split=<packets>: the batched session's dense-range split
 static uint32_t g_drain = 0;  // pipelined: complete every in-flight program after every g_drain-th (session record mode: 2)
 #include <map>
 #include <set>
@@ -167,6 +168,7 @@ struct Harness {
         ctx.pipeline = g_pipeline;
         ctx.ex.expand_limit = g_expand;
         ctx.backsub_rows = g_backsub;
+        ctx.dense_split = g_split;
         arena.assign(g_arena_bytes, 0);
         enc = new Encoder(&ctx, row_bytes);
         dec = new Decoder(&ctx, row_bytes);
@@ -425,6 +427,7 @@ int main(int argc, char** argv) {
         else if (k == "drain") g_drain = (uint32_t)v;
         else if (k == "expand") g_expand = (uint32_t)v;
         else if (k == "backsub") g_backsub = (uint32_t)v;
+        else if (k == "split") g_split = (uint32_t)v;
         else if (parse_param(p, k, v)) {}
         else { fprintf(stderr, "bad key %s\n", k.c_str()); return 2; }
     }

@@ -27,7 +27,8 @@ SCENARIOS = ["c1_256_p3", "c2_4096_p1_ack64", "c2_4096_p1_noack", "c3_4096_p2_ac
              "norecloss_p5_arq", "single_p0", "burst8_p5", "rtx_p2_ack64", "rtx_p5_ack32", "rtx_p3_noack",
              "rtx_restart_p1_ack4", "rtx_restart_p2_ack2"]
 MODES = [("sync", 0), ("batch", 1000), ("batch", 4096), ("sync-dirty", 0), ("batch-dirty", 1000),
-         ("batch-pipe", 1000), ("batch-pipe", 4096), ("batch-pipedrain", 1000), ("batch-pipeexp", 512)]
+         ("batch-pipe", 1000), ("batch-pipe", 4096), ("batch-pipedrain", 1000), ("batch-pipeexp", 512),
+         ("batch-pipesplit", 1000)]
 
 
 @pytest.fixture(scope="module")
@@ -54,8 +55,11 @@ def test_control_plane_matches_reference(harness, golden_index, tmp_path, name, 
     few = mode.endswith("-pipeexp")
     expand = 16 if few else 0xFFFFFFFF
     backsub = 2 if few else 0xFFFFFFFF
+    # the batched session splits direct dense ranges over 192 packets (Context::dense_split);
+    # "-pipesplit" splits every range over 16, so most Siamese rows take the two-level form
+    split = 16 if mode.endswith("-pipesplit") else 192 if mode in ("batch-pipe", "batch-pipedrain") else 0
     args = [harness, str(out), f"mode={base}", f"batch={batch}", f"dirty={dirty}", f"pipeline={pipe}",
-            f"drain={drain}", f"expand={expand}", f"backsub={backsub}"] + sc["args"] + [
+            f"drain={drain}", f"expand={expand}", f"backsub={backsub}", f"split={split}"] + sc["args"] + [
         f"seed_data={1000 + sid}", f"seed_loss={2000 + sid}"]
     r = subprocess.run(args, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
@@ -74,7 +78,7 @@ def test_control_plane_batch_streams(harness, golden_index, tmp_path, batch_name
     import hashlib
     entry = golden_index["batches"][batch_name]
     out = tmp_path / "t.txt"
-    args = [harness, str(out), "mode=batch", "batch=4096", "dirty=0", "pipeline=1", "drain=2"] + entry["args"] + [
+    args = [harness, str(out), "mode=batch", "batch=4096", "dirty=0", "pipeline=1", "drain=2", "split=192"] + entry["args"] + [
         f"seed_data={1000 + sid}", f"seed_loss={2000 + sid}"]
     r = subprocess.run(args, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]

@@ -822,8 +822,7 @@ void Encoder::add_dense_direct(uint32_t row, uint32_t recovery_bytes, const std:
         pb.op_accr_dense(sg.off(j), sg.stride, k, len, col_add(sg.column0, j), ops, rx, adj.data(),
                          (uint32_t)adj.size());
     };
-    static const uint32_t split = getenv("TONK_AMD_DENSE_SPLIT") ? (uint32_t)atoi(getenv("TONK_AMD_DENSE_SPLIT"))
-                                                                  : kDenseSplit;
+    const uint32_t split = ctx_->dense_split;
     const uint32_t total = split ? dense_direct_rows() : 0;
     if (split && total > split) {
         // Partial sums of at most `split` packets each, closed before the row's own op: the

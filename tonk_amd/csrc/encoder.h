@@ -78,6 +78,10 @@ struct Segment {
 
 class Encoder : public FlushClient {
 public:
+    // Longer direct dense ranges are split (in contexts that ask for it, Context::dense_split):
+    // partial sums of at most this many packets, one pure combine each (level 1), added by the
+    // row's op (level 2), so no single work item walks hundreds of packets (a level's tail).
+    static const uint32_t kDenseSplit = 192;
     Encoder(Context* ctx, uint32_t row_bytes, HostRelease release = nullptr, void* user = nullptr);
     ~Encoder();
 
@@ -233,10 +237,6 @@ private:
     void add_dense_direct(uint32_t row, uint32_t recovery_bytes, const std::vector<uint64_t>& pairs);
     // Packets of the direct dense range (add_dense_direct's rows).
     uint32_t dense_direct_rows() const;
-    // Longer direct dense ranges are split: partial sums of at most this many packets, one pure
-    // combine each (level 1), added by the row's op (level 2), so no single work item walks
-    // hundreds of packets (a level's tail).  TONK_AMD_DENSE_SPLIT overrides (A/B knob; 0: never).
-    static const uint32_t kDenseSplit = 192;
     void add_light(uint32_t row, Sym& rec);
     // The same pair columns as (absolute element << 8 | coefficient), sorted by element.
     void light_pairs(uint32_t row, std::vector<uint64_t>& out);

@@ -483,6 +483,11 @@ struct Context {
     // (Decoder::back_substitution; ~0u: never).  Few-stream sessions use it; in batched ones the
     // extra level costs launches and saves no device bytes.
     uint32_t backsub_rows = ~0u;
+    // Direct dense ranges longer than this are split into partial sums over two levels
+    // (Encoder::add_dense_direct; 0: never).  Only batched sessions split: there a long op is a
+    // launch's tail, while per-call programs (the C ABI) and single streams pay an extra level
+    // launch in latency and already share a long op across a workgroup.
+    uint32_t dense_split = 0;
     // Level pipelining (the session, Device::set_pipelined): every launch runs level 1 of the
     // newest program beside the next level of each older program still in flight, so level d
     // of a program runs with level 1 of the program d - 1 later.  A row written at level d is

@@ -1225,6 +1225,9 @@ void* tamd_session_create(const tamd_session_params* p, char* err, size_t err_le
         // TONK_AMD_BACKSUB_ROWS=<unknowns> overrides (A/B knob).
         static const char* bs_env = getenv("TONK_AMD_BACKSUB_ROWS");
         ctx->backsub_rows = bs_env ? (uint32_t)atoi(bs_env) : (p->n_streams <= 4 ? 2u : ~0u);
+        // (TONK_AMD_DENSE_SPLIT=<packets> overrides: A/B knob)
+        static const char* split_env = getenv("TONK_AMD_DENSE_SPLIT");
+        ctx->dense_split = split_env ? (uint32_t)atoi(split_env) : (p->n_streams <= 4 ? 0u : Encoder::kDenseSplit);
         std::unique_ptr<Stream> st(new Stream());
         st->ctx = ctx.get();
         wl::Params& q = st->p;
