@@ -694,7 +694,9 @@ Result Encoder::generate_cauchy(RecoveryOut& out) {
     const uint32_t end_col = to_column(count_);
     // A row over a long window stays a pure combine of its own (the executor shares those across
     // a workgroup); a group is one wave's chain, and a long one would set the launch's tail.
-    const bool alone = count_ - first >= span;
+    // (and rows over windows of short runs -- the C ABI's one-packet segments -- stay alone too:
+    // a MULTI run per packet is an unbatched load each, a lone row's single packets are batched)
+    const bool alone = count_ - first >= span || runs.size() * 4 > count_ - first;
     if (grp_n_ && (alone || grp_n_ >= max_group || grp_gen_ != window_gen_ ||
                    col_sub(end_col, grp_[0].first_col) >= span))
         emit_cauchy_group();
@@ -969,7 +971,11 @@ Result Encoder::encode(RecoveryOut& out) {
     static const int direct_mode = getenv("TONK_AMD_DIRECT_MODE") ? atoi(getenv("TONK_AMD_DIRECT_MODE")) : 0;
     const uint32_t range = count_ + sum_erased_ - sum_start_;
     const bool fresh = sum_end_ == sum_start_;
-    const bool direct = range <= direct_max && (direct_mode == 0 || fresh || (direct_mode == 2 && range <= 128));
+    // Direct reads pay per run (a DENSE run's coefficient setup and first row loads); packets
+    // added one by one with host copies (the C ABI) are runs of one, where the lane sums' batched
+    // single-row reads are far cheaper: direct only while the range's runs average kDirectMinRun.
+    bool direct = range <= direct_max && (direct_mode == 0 || fresh || (direct_mode == 2 && range <= 128));
+    if (direct && range) direct = (segs_.size() - seg_index_at(sum_abs_start())) * kDirectMinRun <= range;
     if (!direct) {
         TAMD_PROF_SCOPE(kEncDense);
         add_dense(row, recovery_bytes, rec);

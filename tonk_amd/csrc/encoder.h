@@ -266,6 +266,7 @@ private:
     // Siamese rows whose sum range is at most this many packets read it straight from the packets
     // (add_dense_direct); longer ones through the running lane sums (TONK_AMD_DIRECT overrides).
     static const uint32_t kDirectMax = 512;
+    static const uint32_t kDirectMinRun = 8;  // packets per run the direct reads need on average
     CauchyTarget grp_[3];
     uint32_t grp_n_ = 0, grp_gen_ = 0, window_gen_ = 0;
     std::vector<Run> grp_union_;
