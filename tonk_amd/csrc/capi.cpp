@@ -311,7 +311,7 @@ struct Codec {
     Codec() {
         ctx.rows.init_segmented(&g_rt->pool);
         static std::atomic<unsigned> next{0};
-        staging.stream = capi_combine() ? 0u : next.fetch_add(1) % g_rt->dev.stream_count();
+        staging.stream = next.fetch_add(1) % g_rt->dev.stream_count();
     }
     uint64_t byte_offset(RowId r) const { return (uint64_t)ctx.rows.offset(r) * TAMD_ROW_UNIT; }
     // The pinned buffer holds at least n bytes (no copy can be landing in it: every read into it
@@ -366,8 +366,9 @@ struct CDecoder : Codec {
 // their contexts: one executor launch per level for all of them), with each caller's reads and
 // event behind it; it hands leadership on once its own program is launched, so no connection's
 // send path serves the others for long (the compressor's pattern, compress.cpp).  Every caller
-// then waits for its own event without a lock.  All codecs use one launch stream then: a
-// codec's staged uploads, its programs and its reads stay in order.
+// then waits for its own event without a lock.  There is one such queue per launch stream and a
+// codec keeps its stream, so its staged uploads, programs and reads stay in order while the
+// streams' batches overlap on the device.
 bool capi_combine() {
     static const bool on = !(getenv("TONK_AMD_CAPI_COMBINE") && atoi(getenv("TONK_AMD_CAPI_COMBINE")) == 0);
     return on;
@@ -383,19 +384,24 @@ struct RunReq {
     BatchDone* done = nullptr;
     bool launched = false, ok = true;
 };
+// One combining queue per launch stream: a codec keeps its stream, so its uploads, programs and
+// reads stay in order, and the streams' batches run side by side.
 std::mutex g_run_mu;
 std::condition_variable g_run_cv;
-std::vector<RunReq*> g_run_q;
-bool g_run_leader = false;
+struct RunQueue {
+    std::vector<RunReq*> q;
+    bool leader = false;
+};
+RunQueue g_run[Device::kMaxStreams];
 
 // One batch = one zero-copy upload launch for every codec's staged packets, the merged program's
 // level launches, one zero-copy read-back launch for every caller's reads and one event: a fixed
 // handful of commands however many callers it serves (per-codec copies would queue one H2D and
 // one D2H command per caller on the stream).
-void launch_batch(const std::vector<RunReq*>& b) {
+void launch_batch(const std::vector<RunReq*>& b, unsigned stream) {
     DevLock dl;
     Device& dev = g_rt->dev;
-    dev.select_stream(0);
+    dev.select_stream(stream);
     std::vector<Context*> ctxs;
     thread_local std::vector<Device::HostCopy> up;
     up.clear();
@@ -443,22 +449,24 @@ bool run_and_read(Codec& c, Reads enqueue_reads) {
         req.c = &c;
         req.reads = &f;
         {
+            const unsigned st = c.staging.stream;
+            RunQueue& rq = g_run[st];
             std::unique_lock<std::mutex> lk(g_run_mu);
-            g_run_q.push_back(&req);
-            g_run_cv.wait(lk, [&req] { return req.launched || !g_run_leader; });
+            rq.q.push_back(&req);
+            g_run_cv.wait(lk, [&req, &rq] { return req.launched || !rq.leader; });
             if (!req.launched) {
-                g_run_leader = true;
+                rq.leader = true;
                 std::vector<RunReq*> b;
                 while (!req.launched) {
                     b.clear();
-                    b.swap(g_run_q);
+                    b.swap(rq.q);
                     lk.unlock();
-                    launch_batch(b);
+                    launch_batch(b, st);
                     lk.lock();
                     for (RunReq* r : b) r->launched = true;
                     g_run_cv.notify_all();
                 }
-                g_run_leader = false;
+                rq.leader = false;
                 g_run_cv.notify_all();  // a caller still queued becomes the next leader
             }
         }

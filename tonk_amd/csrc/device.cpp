@@ -101,6 +101,7 @@ void Device::bind_thread() const {
 }
 
 void Device::add_streams(unsigned k) {
+    if (k > kMaxStreams) k = kMaxStreams;
     if (!stream_ || !streams_.empty() || k < 2) return;
     streams_.push_back(stream_);
     for (unsigned i = 1; i < k; ++i) {
