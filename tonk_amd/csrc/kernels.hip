@@ -404,19 +404,21 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
         };
         // DENSE: COEFS.cap ADJ words follow, coefficient additions for single rows (the LDPC pair
         // columns of the recovery row, SiameseEncoder.cpp:1100-1144, folded into the run)
-        const uint32_t nadj = dense ? tg.cap : 0u;
+        // The additions come sorted by row (empty entries, row 0, only at the end): a cursor walks
+        // them once per run, each block taking the ones below its end.
+        const uint32_t nadj = dense ? 4u * tg.cap : 0u;
+        const uint32_t* __restrict__ adw = (const uint32_t*)adj;
+        uint32_t acur = 0;
         uint32_t gv = 0, gblk = ~0u;  // gv: lane j's table index for row 64 * gblk + j
         auto row_tab = [&](uint32_t i) -> PermT {
             if ((i >> 6) != gblk) {
                 gblk = i >> 6;
-                const uint32_t mine = (i & ~63u) + lane;
+                const uint32_t base = i & ~63u, mine = base + lane;
                 uint32_t g = coef((col0 + mine * cstep) & (TAMD_COLUMN_PERIOD - 1u));
-                for (uint32_t w = 0; w < nadj; ++w) {
-                    const tamd_instr x = adj[w];
-                    const uint32_t d[4] = {x.w0, x.row, x.len, x.cap};
-#pragma unroll
-                    for (uint32_t q = 0; q < 4; ++q)
-                        if ((d[q] >> 16) == mine) g ^= (d[q] >> 8) & 0xffu;
+                for (; acur < nadj; ++acur) {
+                    const uint32_t d = adw[acur];
+                    if ((d >> 16) >= base + 64u) break;
+                    if ((d >> 16) == mine) g ^= (d >> 8) & 0xffu;
                 }
                 gv = g * 8u;
             }
