@@ -411,8 +411,22 @@ void launch_batch(const std::vector<RunReq*>& b, unsigned stream) {
         if (!r->c->ctx.pb.empty()) ctxs.push_back(&r->c->ctx);
     }
     dev.host_copy(up.data(), (uint32_t)up.size(), false);
+    // the merged program, in parts that fit a staging slot as it is (a part of one codec's
+    // program may still need a larger slot)
+    const size_t cap = dev.slot_capacity(), pad = 64 * 16;
+    size_t at = 0;
+    while (at < ctxs.size()) {
+        size_t end = at + 1, bytes = Device::program_bytes(ctxs[at]->pb) + pad;
+        while (end < ctxs.size()) {
+            const size_t more = Device::program_bytes(ctxs[end]->pb);
+            if (bytes + more > cap) break;
+            bytes += more;
+            ++end;
+        }
+        dev.run(ctxs.data() + at, end - at);
+        at = end;
+    }
     if (!ctxs.empty()) {
-        dev.run(ctxs.data(), ctxs.size());
         g_programs.fetch_add(ctxs.size(), std::memory_order_relaxed);
         g_launches.fetch_add(dev.stats().launches - launches, std::memory_order_relaxed);
     }
@@ -559,8 +573,11 @@ SIAMESE_EXPORT int siamese_init_(int version) {
     g_rt->pool.seg_units = (uint32_t)(seg_kb * 1024 / TAMD_ROW_UNIT);
     // Many slots of modest size: a codec waits for its own program before its next one, so with
     // hundreds of codecs (a Tonk server) hundreds of programs are in flight, and a slot still in
-    // use is waited for under the device lock, which stalls every codec behind it.
-    g_rt->dev.set_program_slots(128, 1u << 20);
+    // use is waited for under the device lock, which stalls every codec behind it.  4 MB each
+    // (512 MB pinned): combined batches are split to fit a slot, and a growth of all 128 slots
+    // (drain + reallocation, 0.1-0.5 s with every codec waiting) inflates the round trips Tonk
+    // measures for its retransmission timeouts.
+    g_rt->dev.set_program_slots(128, 4u << 20);
     if (!g_rt->dev.init_growable(device, arena_mb << 20, max_mb << 20)) {
         fprintf(stderr, "%s\n", g_rt->dev.error().c_str());
         return Siamese_Disabled;

@@ -50,6 +50,15 @@ public:
         slots_.assign(count < 2 ? 2 : count, Slot());
         slot_bytes_ = bytes;
     }
+    // Staging bytes a program of these builders needs (Device::begin's layout) and the slots'
+    // current capacity: a caller merging programs (the C ABI's batches) keeps a merge within it,
+    // since growing the slots drains the device and reallocates every slot.
+    static size_t program_bytes(const ProgramBuilder& pb) {
+        size_t items = 0;
+        for (uint32_t c : pb.level_items()) items += c;
+        return (pb.instrs().size() + pb.ops().size()) * 16 + items * 8;
+    }
+    size_t slot_capacity() const { return slot_cap_ ? slot_cap_ : slot_bytes_; }
     const std::string& error() const { return error_; }
     bool failed() const { return failed_; }  // any HIP call failed (sticky; safe to read unlocked)
     uint64_t arena_bytes() const { return arena_bytes_; }
