@@ -28,7 +28,7 @@ SCENARIOS = ["c1_256_p3", "c2_4096_p1_ack64", "c2_4096_p1_noack", "c3_4096_p2_ac
              "rtx_restart_p1_ack4", "rtx_restart_p2_ack2"]
 MODES = [("sync", 0), ("batch", 1000), ("batch", 4096), ("sync-dirty", 0), ("batch-dirty", 1000),
          ("batch-pipe", 1000), ("batch-pipe", 4096), ("batch-pipedrain", 1000), ("batch-pipeexp", 512),
-         ("batch-pipesplit", 1000)]
+         ("batch-pipesplit", 1000), ("sync-exp", 0)]
 
 
 @pytest.fixture(scope="module")
@@ -52,7 +52,8 @@ def test_control_plane_matches_reference(harness, golden_index, tmp_path, name, 
     # read as rows, one level up) and its back substitution over materialized rows (from 2
     # unknowns)
     pipe, drain = int("-pipe" in mode), 2 * int(mode.endswith("-pipedrain"))
-    few = mode.endswith("-pipeexp")
+    # "-exp" alone: the same limits on per-call programs (the siamese.h C ABI's contexts)
+    few = mode.endswith("exp")
     expand = 16 if few else 0xFFFFFFFF
     backsub = 2 if few else 0xFFFFFFFF
     # the batched session splits direct dense ranges over 192 packets (Context::dense_split);

@@ -310,6 +310,13 @@ struct Codec {
     // other on one stream).
     Codec() {
         ctx.rows.init_segmented(&g_rt->pool);
+        // Per-call programs stay small (the few-stream session's policies, Context): a decode of L
+        // unknowns solves over materialized eliminated rows from L = 2 on, and expansions of more
+        // than 16 terms are read as rows -- inlining both grows a program quadratically with L
+        // (a burst of losses under Tonk made single programs of 8 MB, and the slot growth that
+        // follows stalls every codec).
+        ctx.backsub_rows = 2;
+        ctx.ex.expand_limit = 16;
         static std::atomic<unsigned> next{0};
         staging.stream = next.fetch_add(1) % g_rt->dev.stream_count();
     }
