@@ -186,6 +186,23 @@ def test_capi_arena_growth(golden_index, name):
     assert out.stdout.decode() == want, first_diff(want, out.stdout.decode())
 
 
+def test_capi_oversize_programs(golden_index, tmp_path):
+    """Programs larger than a C ABI staging slot run in the oversize slot (here: 64 KB slots, a
+    256 KB oversize slot that must also grow once), with eight threads of codecs sharing the
+    device: every stream's transcript still equals the reference codec's."""
+    import hashlib
+    exe = os.path.join(NATIVE, "_build", "capi_gen")
+    entry = golden_index["batches"]["cfg2_64x4096_p2_ack64"]
+    prefix = str(tmp_path / "s")
+    env = dict(os.environ, TONK_AMD_CAPI_SLOT_KB="64", TONK_AMD_CAPI_OVERSIZE_KB="256")
+    out = subprocess.run([exe, "transcripts", prefix, "threads=8", "streams=8", "stream=0"] + entry["args"],
+                         capture_output=True, timeout=600, env=env)
+    assert out.returncode == 0, out.stderr.decode()[-2000:]
+    bad = [s for s in range(8)
+           if hashlib.sha256(open(f"{prefix}{s}.txt", "rb").read()).hexdigest() != entry["streams"][str(s)]["sha256"]]
+    assert not bad, f"streams differing from the reference: {bad}"
+
+
 def test_capi_device_failure_disables_codec(golden_index):
     """A device failure (injected: every program after the 20th fails to stage) must surface as
     Siamese_Disabled from siamese_encode / siamese_decode -- never as Success with stale bytes:

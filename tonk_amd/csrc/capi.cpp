@@ -419,7 +419,7 @@ void launch_batch(const std::vector<RunReq*>& b, unsigned stream) {
     }
     dev.host_copy(up.data(), (uint32_t)up.size(), false);
     // the merged program, in parts that fit a staging slot as it is (a part of one codec's
-    // program may still need a larger slot)
+    // program may still need the oversize slot)
     const size_t cap = dev.slot_capacity(), pad = 64 * 16;
     size_t at = 0;
     while (at < ctxs.size()) {
@@ -583,8 +583,14 @@ SIAMESE_EXPORT int siamese_init_(int version) {
     // use is waited for under the device lock, which stalls every codec behind it.  4 MB each
     // (512 MB pinned): combined batches are split to fit a slot, and a growth of all 128 slots
     // (drain + reallocation, 0.1-0.5 s with every codec waiting) inflates the round trips Tonk
-    // measures for its retransmission timeouts.
-    g_rt->dev.set_program_slots(128, 4u << 20);
+    // measures for its retransmission timeouts.  A single program above 4 MB (a decode solving
+    // hundreds of unknowns) takes the 32 MB oversize slot instead of growing them all: one such
+    // growth stalled every codec of a Tonk test for 317 ms, and the losses the peers piled up
+    // meanwhile made an acknowledgement too long for a Tonk datagram.
+    size_t slot_kb = 4096, big_kb = 32768;  // (test hooks: small slots send programs to the oversize one)
+    if (const char* a = getenv("TONK_AMD_CAPI_SLOT_KB")) slot_kb = strtoull(a, nullptr, 10);
+    if (const char* a = getenv("TONK_AMD_CAPI_OVERSIZE_KB")) big_kb = strtoull(a, nullptr, 10);
+    g_rt->dev.set_program_slots(128, slot_kb << 10, big_kb << 10);
     if (!g_rt->dev.init_growable(device, arena_mb << 20, max_mb << 20)) {
         fprintf(stderr, "%s\n", g_rt->dev.error().c_str());
         return Siamese_Disabled;

@@ -51,6 +51,7 @@ Device::~Device() {
     else for (void* st : streams_) hipStreamSynchronize((hipStream_t)st);
     for (Slot& s : slots_)
         if (s.done) hipEventDestroy((hipEvent_t)s.done);
+    if (big_.done) hipEventDestroy((hipEvent_t)big_.done);
     if (prog_host_) hipHostFree(prog_host_);
     if (prog_dev_) hipFree(prog_dev_);
     for (auto& p : inflight_) hipEventDestroy((hipEvent_t)p.second);
@@ -177,6 +178,11 @@ bool Device::init(int device, uint64_t arena_bytes) {
         hipEvent_t e;
         HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
         sl.done = e;
+    }
+    if (big_cap_) {
+        hipEvent_t e;
+        HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        big_.done = e;
     }
     hipEvent_t ue;
     HIPCHK(hipEventCreateWithFlags(&ue, hipEventDisableTiming));
@@ -314,24 +320,31 @@ bool Device::alloc_slots(size_t cap) {
     }
     hcap = (hcap + 255) & ~(size_t)255;
     dcap = (dcap + 255) & ~(size_t)255;
-    if (dcap * slots_.size() > 0xfffff000ull) return false;  // 32-bit program offsets
+    const size_t big = asm_items_ ? 0 : (big_cap_ + 255) & ~(size_t)255;  // (after the regular slots)
+    if (dcap * slots_.size() + big > 0xfffff000ull) return false;  // 32-bit program offsets
     for (Slot& s : slots_) {
         s.host = nullptr;
         s.dev = nullptr;
     }
+    big_.host = big_.dev = nullptr;
     if (prog_host_) hipHostFree(prog_host_);
     if (prog_dev_) hipFree(prog_dev_);
     prog_host_ = nullptr;
     prog_dev_ = nullptr;
     slot_cap_ = 0;
     // one pinned and one device allocation, split into the slots
-    if (hipMalloc((void**)&prog_dev_, dcap * slots_.size()) != hipSuccess) return false;
-    if (hipHostMalloc((void**)&prog_host_, hcap * slots_.size(), hipHostMallocDefault) != hipSuccess) return false;
+    if (hipMalloc((void**)&prog_dev_, dcap * slots_.size() + big) != hipSuccess) return false;
+    if (hipHostMalloc((void**)&prog_host_, hcap * slots_.size() + big, hipHostMallocDefault) != hipSuccess) return false;
     for (size_t k = 0; k < slots_.size(); ++k) {
         Slot& s = slots_[k];
         s.host = prog_host_ + k * hcap;
         s.dev_off = (uint32_t)(k * dcap);
         s.dev = prog_dev_ + s.dev_off;
+    }
+    if (big) {
+        big_.host = prog_host_ + slots_.size() * hcap;
+        big_.dev_off = (uint32_t)(slots_.size() * dcap);
+        big_.dev = prog_dev_ + big_.dev_off;
     }
     slot_cap_ = hcap;
     return true;
@@ -544,18 +557,23 @@ uint64_t Device::close_program(int h, Part* const* parts, size_t n) {
 }
 
 bool Device::ensure_slot(Slot& s, size_t bytes) {
-    (void)s;
-    if (slot_cap_ >= bytes) return true;
+    const bool big = &s == &big_;
+    if ((big ? big_cap_ : slot_cap_) >= bytes) return true;
     stats_.slot_reallocs++;
     // a bench step's program is ~8 MB: avoid reallocating mid-run
     size_t cap = slot_cap_ ? slot_cap_ : slot_bytes_;
-    while (cap < bytes) cap *= 2;
+    if (big) {
+        while (big_cap_ < bytes) big_cap_ *= 2;
+    } else {
+        while (cap < bytes) cap *= 2;
+    }
     const auto t0 = std::chrono::steady_clock::now();
     drain_programs();
     sync_all_streams();  // a program on any stream may still read its slot
     for (Slot& sl : slots_) sl.ticket = 0;
+    big_.ticket = 0;
     const bool ok = alloc_slots(cap);
-    report_slow("program slot growth", t0, cap >> 10, bytes >> 10);
+    report_slow(big ? "oversize slot growth" : "program slot growth", t0, (big ? big_cap_ : cap) >> 10, bytes >> 10);
     return ok;
 }
 
@@ -619,8 +637,10 @@ void Device::begin(Context* const* ctxs, size_t n, bool closed) {
     P.bytes_ops = P.n_ops * sizeof(tamd_op);
     P.total = P.bytes_instr + P.bytes_ops + P.n_items * sizeof(uint32_t) * 2;
 
-    Slot& slot = slots_[next_slot_];
-    next_slot_ = (next_slot_ + 1) % (int)slots_.size();
+    // (a program larger than a regular slot takes the oversize slot when there is one)
+    const bool big = big_.dev && P.total > slot_capacity();
+    Slot& slot = big ? big_ : slots_[next_slot_];
+    if (!big) next_slot_ = (next_slot_ + 1) % (int)slots_.size();
     for (const Inflight& p : progs_)
         if (p.slot == &slot) { drain_programs(); break; }  // (the slot still holds a program in flight)
     if (slot.ticket) {

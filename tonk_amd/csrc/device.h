@@ -46,9 +46,13 @@ public:
     // Program staging: `count` pinned/device slot pairs of `bytes` each (grown on demand), used
     // round robin; a program waits only for the program `count` back.  Call before init.
     // Default 2 x 16 MB (the session's big step programs); the C ABI runs many small ones.
-    void set_program_slots(size_t count, size_t bytes) {
+    // `oversize` > 0 adds one more slot of that size for the rare program larger than a regular
+    // slot (the C ABI: a decode that solves hundreds of unknowns in one call), so such a program
+    // waits only for the previous oversize one instead of draining the device to grow every slot.
+    void set_program_slots(size_t count, size_t bytes, size_t oversize = 0) {
         slots_.assign(count < 2 ? 2 : count, Slot());
         slot_bytes_ = bytes;
+        big_cap_ = oversize;
     }
     // Staging bytes a program of these builders needs (Device::begin's layout) and the slots'
     // current capacity: a caller merging programs (the C ABI's batches) keeps a merge within it,
@@ -59,6 +63,7 @@ public:
         return (pb.instrs().size() + pb.ops().size()) * 16 + items * 8;
     }
     size_t slot_capacity() const { return slot_cap_ ? slot_cap_ : slot_bytes_; }
+    size_t oversize_capacity() const { return big_cap_; }
     const std::string& error() const { return error_; }
     bool failed() const { return failed_; }  // any HIP call failed (sticky; safe to read unlocked)
     uint64_t arena_bytes() const { return arena_bytes_; }
@@ -269,6 +274,8 @@ private:
     std::vector<Slot> slots_ = std::vector<Slot>(2);
     size_t slot_bytes_ = 16u << 20;  // requested initial capacity
     size_t slot_cap_ = 0;            // current capacity of every slot
+    Slot big_;                       // the oversize slot (set_program_slots), after the regular ones
+    size_t big_cap_ = 0;
     uint8_t* prog_dev_ = nullptr;
     uint8_t* prog_host_ = nullptr;   // pinned twin of prog_dev_
     bool alloc_slots(size_t cap);    // (re)allocate every slot; nothing may be in flight
