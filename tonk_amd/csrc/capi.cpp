@@ -405,8 +405,18 @@ RunQueue g_run[Device::kMaxStreams];
 // level launches, one zero-copy read-back launch for every caller's reads and one event: a fixed
 // handful of commands however many callers it serves (per-codec copies would queue one H2D and
 // one D2H command per caller on the stream).
-void launch_batch(const std::vector<RunReq*>& b, unsigned stream) {
+// The batch is taken from the stream's queue only once the device lock is held: the lock is
+// shared by every stream's leader, and callers that queue while a leader waits for it join that
+// leader's batch instead of forming batches of one behind it (under a Tonk server's load the lock
+// is busy most of the time, and batches of ~1.3 calls made every call pay a launch of its own).
+void launch_batch(std::vector<RunReq*>& b, unsigned stream) {
     DevLock dl;
+    {
+        std::lock_guard<std::mutex> g(g_run_mu);
+        b.clear();
+        b.swap(g_run[stream].q);
+    }
+    if (b.empty()) return;
     Device& dev = g_rt->dev;
     dev.select_stream(stream);
     std::vector<Context*> ctxs;
@@ -479,10 +489,8 @@ bool run_and_read(Codec& c, Reads enqueue_reads) {
                 rq.leader = true;
                 std::vector<RunReq*> b;
                 while (!req.launched) {
-                    b.clear();
-                    b.swap(rq.q);
                     lk.unlock();
-                    launch_batch(b, st);
+                    launch_batch(b, st);  // (takes the queue under the device lock)
                     lk.lock();
                     for (RunReq* r : b) r->launched = true;
                     g_run_cv.notify_all();
