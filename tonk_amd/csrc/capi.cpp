@@ -101,7 +101,8 @@ struct Runtime {
 struct DevLock {
     std::unique_lock<std::mutex> lk;
     int64_t held_since = 0;
-    DevLock() : lk(g_rt->dev_mu, std::defer_lock) {
+    const char* site;
+    explicit DevLock(const char* where = __builtin_FUNCTION()) : lk(g_rt->dev_mu, std::defer_lock), site(where) {
         if (!lk.try_lock()) {
             const int64_t t0 = now_ns();
             lk.lock();
@@ -117,6 +118,7 @@ struct DevLock {
         const uint64_t h = (uint64_t)(now_ns() - held_since);
         uint64_t m = g_lock_hold_max_ns.load(std::memory_order_relaxed);
         while (h > m && !g_lock_hold_max_ns.compare_exchange_weak(m, h)) {}
+        if (h >= 10000000) fprintf(stderr, "tonk_amd: device lock held %.1f ms in %s\n", h * 1e-6, site);
     }
 };
 
@@ -315,8 +317,10 @@ struct Codec {
         // than 16 terms are read as rows -- inlining both grows a program quadratically with L
         // (a burst of losses under Tonk made single programs of 8 MB, and the slot growth that
         // follows stalls every codec).
-        ctx.backsub_rows = 2;
-        ctx.ex.expand_limit = 16;
+        static const uint32_t bs = getenv("TONK_AMD_CAPI_BACKSUB") ? (uint32_t)atoi(getenv("TONK_AMD_CAPI_BACKSUB")) : 2u;
+        static const uint32_t ex = getenv("TONK_AMD_CAPI_EXPAND") ? (uint32_t)atoi(getenv("TONK_AMD_CAPI_EXPAND")) : 16u;
+        ctx.backsub_rows = bs ? bs : ~0u;  // (0: never materialize / always inline)
+        ctx.ex.expand_limit = ex ? ex : ~0u;
         static std::atomic<unsigned> next{0};
         staging.stream = next.fetch_add(1) % g_rt->dev.stream_count();
     }
@@ -427,7 +431,9 @@ void launch_batch(std::vector<RunReq*>& b, unsigned stream) {
         r->c->staging.take_uploads(up);  // packets added since the codec's last program land first
         if (!r->c->ctx.pb.empty()) ctxs.push_back(&r->c->ctx);
     }
+    const int64_t p0 = g_watch ? now_ns() : 0;
     dev.host_copy(up.data(), (uint32_t)up.size(), false);
+    const int64_t p1 = g_watch ? now_ns() : 0;
     // the merged program, in parts that fit a staging slot as it is (a part of one codec's
     // program may still need the oversize slot)
     const size_t cap = dev.slot_capacity(), pad = 64 * 16;
@@ -443,6 +449,7 @@ void launch_batch(std::vector<RunReq*>& b, unsigned stream) {
         dev.run(ctxs.data() + at, end - at);
         at = end;
     }
+    const int64_t p2 = g_watch ? now_ns() : 0;
     if (!ctxs.empty()) {
         g_programs.fetch_add(ctxs.size(), std::memory_order_relaxed);
         g_launches.fetch_add(dev.stats().launches - launches, std::memory_order_relaxed);
@@ -455,6 +462,12 @@ void launch_batch(std::vector<RunReq*>& b, unsigned stream) {
     dev.flush_host_reads();
     BatchDone* done = new BatchDone();
     done->ev = dev.record_event();
+    if (g_watch && now_ns() - p0 >= 10000000) {
+        size_t bytes = 0;
+        for (Context* c : ctxs) bytes += Device::program_bytes(c->pb);
+        fprintf(stderr, "tonk_amd: slow batch: uploads %.1f ms (%zu), programs %.1f ms (%zu, %zu KB), reads %.1f ms\n",
+                (p1 - p0) * 1e-6, up.size(), (p2 - p1) * 1e-6, ctxs.size(), bytes >> 10, (now_ns() - p2) * 1e-6);
+    }
     done->left.store((int)b.size());
     const bool ok = !dev.failed();
     for (RunReq* r : b) {

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 #include <chrono>
+#include <unordered_map>
 #include <thread>
 #include <stdio.h>
 #include <stdlib.h>
@@ -75,7 +76,7 @@ Device::~Device() {
     if (up_event_) hipEventDestroy((hipEvent_t)up_event_);
     for (HcBuf& b : hc_) {
         if (b.ev) hipEventDestroy((hipEvent_t)b.ev);
-        if (b.p) hipHostFree(b.p);
+        host_free(b.p);
     }
     if (d_gf_) hipFree(d_gf_);
     if (d_zero_) hipFree(d_zero_);
@@ -1103,11 +1104,10 @@ void Device::host_copy(const HostCopy* d, uint32_t n, bool to_host) {
     HcBuf& b = hc_[hc_next_++ % (sizeof(hc_) / sizeof(hc_[0]))];
     if (b.ev) HIPCHK(hipEventSynchronize((hipEvent_t)b.ev));  // (its previous launch has read it)
     const size_t need = (size_t)n * sizeof(HostCopyDev);
-    if (need > b.cap) {
-        if (b.p) hipHostFree(b.p);
+    if (need > b.cap) {  // (pooled: hipHostFree would wait for the whole device)
+        host_free(b.p);
         b.cap = need + need / 2 + 4096;
-        if (hipHostMalloc(&b.p, b.cap, hipHostMallocDefault) != hipSuccess) {
-            b.p = nullptr;
+        if (!(b.p = host_alloc(b.cap))) {
             b.cap = 0;
             error_ = "host copy descriptor allocation failed";
             failed_ = true;
@@ -1155,14 +1155,41 @@ bool Device::event_wait(void* ev) {
     return e == hipSuccess;
 }
 
+// Pinned buffers (the C ABI's per-codec staging and landing buffers) come from power-of-two
+// free lists and go back to them, never to HIP while the process runs: hipHostFree waits for the
+// whole device, so a codec growing its buffer (or a connection closing) would stall every other
+// codec's work behind it -- under a Tonk server's connection churn, seconds at a time.
+namespace {
+std::mutex g_pin_mu;
+std::vector<void*> g_pin_free[64];
+std::unordered_map<void*, unsigned> g_pin_class;
+}  // namespace
+
 void* Device::host_alloc(size_t n) {
+    unsigned c = 12;
+    while (((size_t)1 << c) < n) ++c;
+    {
+        std::lock_guard<std::mutex> g(g_pin_mu);
+        if (!g_pin_free[c].empty()) {
+            void* p = g_pin_free[c].back();
+            g_pin_free[c].pop_back();
+            return p;
+        }
+    }
     void* p = nullptr;
-    if (hipHostMalloc(&p, n, hipHostMallocDefault) != hipSuccess) return nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    if (hipHostMalloc(&p, (size_t)1 << c, hipHostMallocDefault) != hipSuccess) return nullptr;
+    report_slow("pinned allocation", t0, ((size_t)1 << c) >> 10, 0);
+    std::lock_guard<std::mutex> g(g_pin_mu);
+    g_pin_class[p] = c;
     return p;
 }
 
 void Device::host_free(void* p) {
-    if (p) hipHostFree(p);
+    if (!p) return;
+    std::lock_guard<std::mutex> g(g_pin_mu);
+    auto it = g_pin_class.find(p);
+    if (it != g_pin_class.end()) g_pin_free[it->second].push_back(p);
 }
 
 bool Device::enable_staging() {
