@@ -46,6 +46,7 @@ int64_t now_ns() {
 std::atomic<uint64_t> g_calls{0}, g_waits{0}, g_wait_ns{0}, g_lock_wait_max_ns{0}, g_lock_hold_max_ns{0};
 std::atomic<uint64_t> g_programs{0}, g_launches{0}, g_prepare_ns{0}, g_run_ns{0};
 std::atomic<uint64_t> g_batches{0}, g_batched{0};  // combined launches and the calls they served
+std::atomic<uint64_t> g_ph_up_ns{0}, g_ph_run_ns{0}, g_ph_read_ns{0}, g_ph_lock_ns{0};  // batch phases (watch)
 std::atomic<int> g_in_wait{0};
 std::atomic<int64_t> g_in_wait_since{0};  // start of the current run of overlapping waits
 bool g_watch = false;
@@ -182,6 +183,12 @@ void watch_loop(double period_s) {
                 g_prepare_ns.load() * 1e-6, g_run_ns.load() * 1e-6, (unsigned long long)g_programs.load(),
                 (unsigned long long)g_launches.load(), (unsigned long long)g_batches.load(),
                 (unsigned long long)g_batched.load());
+        {
+            DeviceStats& ds = g_rt->dev.stats();  // (read unlocked: diagnostics)
+            fprintf(stderr, "[tonk_amd capi]   batch phases (device lock held): bind+take_ms=%.1f uploads_ms=%.1f programs_ms=%.1f reads_ms=%.1f; slot_wait_ms=%.1f program_h2d_enqueue_ms=%.1f\n",
+                    g_ph_lock_ns.load() * 1e-6, g_ph_up_ns.load() * 1e-6, g_ph_run_ns.load() * 1e-6,
+                    g_ph_read_ns.load() * 1e-6, ds.slot_wait_ms, ds.upload_enqueue_ms);
+        }
         for (Site* st = g_sites.load(); st; st = st->next) {
             const uint64_t c = st->calls.load();
             if (!c) continue;
@@ -462,6 +469,12 @@ void launch_batch(std::vector<RunReq*>& b, unsigned stream) {
     dev.flush_host_reads();
     BatchDone* done = new BatchDone();
     done->ev = dev.record_event();
+    if (g_watch) {
+        g_ph_lock_ns.fetch_add((uint64_t)(p0 - dl.held_since), std::memory_order_relaxed);
+        g_ph_up_ns.fetch_add((uint64_t)(p1 - p0), std::memory_order_relaxed);
+        g_ph_run_ns.fetch_add((uint64_t)(p2 - p1), std::memory_order_relaxed);
+        g_ph_read_ns.fetch_add((uint64_t)(now_ns() - p2), std::memory_order_relaxed);
+    }
     if (g_watch && now_ns() - p0 >= 10000000) {
         size_t bytes = 0;
         for (Context* c : ctxs) bytes += Device::program_bytes(c->pb);
@@ -614,6 +627,11 @@ SIAMESE_EXPORT int siamese_init_(int version) {
     g_rt->dev.set_program_slots(128, slot_kb << 10, big_kb << 10);
     if (!g_rt->dev.init_growable(device, arena_mb << 20, max_mb << 20)) {
         fprintf(stderr, "%s\n", g_rt->dev.error().c_str());
+        return Siamese_Disabled;
+    }
+    // pinned staging for the codecs to come, mapped now (Device::host_alloc)
+    if (!Device::host_reserve(1)) {
+        fprintf(stderr, "tonk_amd: pinned host memory unavailable\n");
         return Siamese_Disabled;
     }
     if (!g_rt->dev.gf_selftest()) {

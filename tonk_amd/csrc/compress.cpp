@@ -150,6 +150,23 @@ struct LzBatchState {
 
 size_t align16(size_t n) { return (n + 15) & ~(size_t)15; }
 
+// Device rings of destroyed compressors are kept for the next ones: hipFree waits for the whole
+// device (every stream of the process, the Siamese codecs' too), and Tonk destroys a compressor
+// with every connection it closes.
+std::mutex g_ring_mu;
+std::vector<std::pair<int, uint8_t*>> g_free_rings;  // (device, ring)
+uint8_t* take_ring(int device) {
+    std::lock_guard<std::mutex> g(g_ring_mu);
+    for (size_t i = 0; i < g_free_rings.size(); ++i)
+        if (g_free_rings[i].first == device) {
+            uint8_t* r = g_free_rings[i].second;
+            g_free_rings[i] = g_free_rings.back();
+            g_free_rings.pop_back();
+            return r;
+        }
+    return nullptr;
+}
+
 bool grow(uint8_t*& h, uint8_t*& d, size_t& cap, size_t need) {
     if (need <= cap) return true;
     if (h) hipHostFree(h);
@@ -183,8 +200,8 @@ void run_batch(const std::vector<LzRequest*>& in) {
     live.reserve(in.size());
     for (LzRequest* r : in) {
         if (ok && !r->c->ring && !r->c->failed) {
-            uint8_t* ring = nullptr;
-            if (hipMalloc((void**)&ring, TAMD_LZ_RING + TAMD_LZ_MIRROR) != hipSuccess) r->c->failed = true;
+            uint8_t* ring = take_ring(dev);
+            if (!ring && hipMalloc((void**)&ring, TAMD_LZ_RING + TAMD_LZ_MIRROR) != hipSuccess) r->c->failed = true;
             else r->c->ring = ring;
         }
         if (ok && r->c->ring && !r->c->failed) {
@@ -305,9 +322,9 @@ extern "C" void tamd_compressor_destroy(void* cp) {
         std::unique_lock<std::mutex> g(g_req_mu);
         g_req_cv.wait(g, [c] { return !c->queued; });
     }
-    if (c->ring) {
-        hipSetDevice(c->device);
-        hipFree(c->ring);
+    if (c->ring) {  // (no launch reads it any more: its last call was waited for)
+        std::lock_guard<std::mutex> g(g_ring_mu);
+        g_free_rings.push_back(std::make_pair(c->device, c->ring));
     }
     delete c;
 }

@@ -1155,19 +1155,47 @@ bool Device::event_wait(void* ev) {
     return e == hipSuccess;
 }
 
-// Pinned buffers (the C ABI's per-codec staging and landing buffers) come from power-of-two
-// free lists and go back to them, never to HIP while the process runs: hipHostFree waits for the
-// whole device, so a codec growing its buffer (or a connection closing) would stall every other
-// codec's work behind it -- under a Tonk server's connection churn, seconds at a time.
+// Pinned buffers (the C ABI's per-codec staging and landing buffers) are power-of-two blocks cut
+// from pinned slabs of 64 MB, and go back to per-size free lists, never to HIP while the process
+// runs: hipHostFree waits for the whole device, so a codec growing its buffer (or a connection
+// closing) would stall every other codec's work behind it; and on some hosts every hipHostMalloc
+// takes 10+ ms while blocking other HIP calls -- hundreds of codecs starting together (a Tonk test
+// opening 100 connections) then spent seconds in allocations.  host_reserve() maps slabs up front.
 namespace {
+const size_t kPinSlab = 64u << 20;
 std::mutex g_pin_mu;
 std::vector<void*> g_pin_free[64];
 std::unordered_map<void*, unsigned> g_pin_class;
+uint8_t* g_slab = nullptr;  // the slab blocks are cut from
+size_t g_slab_used = kPinSlab;
 }  // namespace
+
+bool Device::host_reserve(size_t bytes) {
+    std::lock_guard<std::mutex> g(g_pin_mu);
+    // (one slab at a time: the current one is only replaced once used up)
+    if (g_slab && g_slab_used + bytes <= kPinSlab) return true;
+    void* p = nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    if (hipHostMalloc(&p, kPinSlab, hipHostMallocDefault) != hipSuccess) return false;
+    report_slow("pinned slab", t0, kPinSlab >> 20, 0);
+    if (g_slab) {  // the rest of the old slab becomes free blocks
+        for (unsigned c = 63; c >= 12; --c)
+            while (g_slab_used + ((size_t)1 << c) <= kPinSlab) {
+                void* b = g_slab + g_slab_used;
+                g_pin_class[b] = c;
+                g_pin_free[c].push_back(b);
+                g_slab_used += (size_t)1 << c;
+            }
+    }
+    g_slab = (uint8_t*)p;
+    g_slab_used = 0;
+    return true;
+}
 
 void* Device::host_alloc(size_t n) {
     unsigned c = 12;
     while (((size_t)1 << c) < n) ++c;
+    const size_t sz = (size_t)1 << c;
     {
         std::lock_guard<std::mutex> g(g_pin_mu);
         if (!g_pin_free[c].empty()) {
@@ -1176,13 +1204,27 @@ void* Device::host_alloc(size_t n) {
             return p;
         }
     }
-    void* p = nullptr;
-    const auto t0 = std::chrono::steady_clock::now();
-    if (hipHostMalloc(&p, (size_t)1 << c, hipHostMallocDefault) != hipSuccess) return nullptr;
-    report_slow("pinned allocation", t0, ((size_t)1 << c) >> 10, 0);
-    std::lock_guard<std::mutex> g(g_pin_mu);
-    g_pin_class[p] = c;
-    return p;
+    if (sz > kPinSlab / 4) {  // (large blocks: their own allocation)
+        void* p = nullptr;
+        const auto t0 = std::chrono::steady_clock::now();
+        if (hipHostMalloc(&p, sz, hipHostMallocDefault) != hipSuccess) return nullptr;
+        report_slow("pinned allocation", t0, sz >> 10, 0);
+        std::lock_guard<std::mutex> g(g_pin_mu);
+        g_pin_class[p] = c;
+        return p;
+    }
+    for (;;) {
+        {
+            std::lock_guard<std::mutex> g(g_pin_mu);
+            if (g_slab && g_slab_used + sz <= kPinSlab) {  // (4 KB aligned: every size is a multiple)
+                void* p = g_slab + g_slab_used;
+                g_slab_used += sz;
+                g_pin_class[p] = c;
+                return p;
+            }
+        }
+        if (!host_reserve(sz)) return nullptr;
+    }
 }
 
 void Device::host_free(void* p) {

@@ -172,7 +172,8 @@ public:
     void* record_event();
     static bool event_wait(void* ev);  // false when the wait failed
     void event_release(void* ev) { free_events_.push_back(ev); }
-    static void* host_alloc(size_t n);  // pinned
+    static void* host_alloc(size_t n);  // pinned (pooled; see device.cpp)
+    static bool host_reserve(size_t n);  // map a pinned slab now if fewer than n bytes are left in it
     static void host_free(void* p);
 
     // Bench helpers (kernels.hip).
