@@ -104,6 +104,10 @@ struct DevLock {
     int64_t held_since = 0;
     const char* site;
     explicit DevLock(const char* where = __builtin_FUNCTION()) : lk(g_rt->dev_mu, std::defer_lock), site(where) {
+        // Tonk calls from many threads; every Device call targets this GPU.  Bound outside the lock:
+        // a thread's first hipSetDevice can take tens of ms while the driver is busy (e.g. right
+        // after another GPU process exited), which under the lock stalls every codec.
+        g_rt->dev.bind_thread();
         if (!lk.try_lock()) {
             const int64_t t0 = now_ns();
             lk.lock();
@@ -112,7 +116,6 @@ struct DevLock {
             while (w > m && !g_lock_wait_max_ns.compare_exchange_weak(m, w)) {}
         }
         if (g_watch) held_since = now_ns();
-        g_rt->dev.bind_thread();  // Tonk calls from many threads; every Device call targets its GPU
     }
     ~DevLock() {
         if (!g_watch) return;
@@ -629,7 +632,9 @@ SIAMESE_EXPORT int siamese_init_(int version) {
         fprintf(stderr, "%s\n", g_rt->dev.error().c_str());
         return Siamese_Disabled;
     }
-    // pinned staging for the codecs to come, mapped now (Device::host_alloc)
+    // events and pinned staging for the codecs to come, created now: creating either later makes
+    // a driver call that can block for milliseconds, and it would happen under the device lock
+    g_rt->dev.reserve_events(1024);
     if (!Device::host_reserve(1)) {
         fprintf(stderr, "tonk_amd: pinned host memory unavailable\n");
         return Siamese_Disabled;

@@ -1149,6 +1149,14 @@ void* Device::record_event() {
     return e;
 }
 
+void Device::reserve_events(size_t n) {
+    while (free_events_.size() < n) {
+        hipEvent_t he;
+        if (hipEventCreateWithFlags(&he, hipEventDisableTiming) != hipSuccess) return;
+        free_events_.push_back(he);
+    }
+}
+
 bool Device::event_wait(void* ev) {
     const hipError_t e = hipEventSynchronize((hipEvent_t)ev);
     if (e != hipSuccess) fprintf(stderr, "tonk_amd: hipEventSynchronize failed: %s\n", hipGetErrorString(e));

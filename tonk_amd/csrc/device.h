@@ -170,6 +170,7 @@ public:
     void collect_host_reads(bool on) { collect_reads_ = on; }
     void flush_host_reads();
     void* record_event();
+    void reserve_events(size_t n);  // pre-create events for record_event (no creation later)
     static bool event_wait(void* ev);  // false when the wait failed
     void event_release(void* ev) { free_events_.push_back(ev); }
     static void* host_alloc(size_t n);  // pinned (pooled; see device.cpp)
