@@ -404,12 +404,12 @@ struct RunReq {
     const std::function<void(Device&)>* reads = nullptr;
     BatchDone* done = nullptr;
     bool launched = false, ok = true;
+    std::condition_variable cv;  // its caller waits here (woken alone: no herd of hundreds of threads)
 };
 // One combining queue per launch stream: a codec keeps its stream, so its uploads, programs and
 // reads stay in order, and the streams' batches run side by side.
-std::mutex g_run_mu;
-std::condition_variable g_run_cv;
 struct RunQueue {
+    std::mutex mu;
     std::vector<RunReq*> q;
     bool leader = false;
 };
@@ -426,7 +426,7 @@ RunQueue g_run[Device::kMaxStreams];
 void launch_batch(std::vector<RunReq*>& b, unsigned stream) {
     DevLock dl;
     {
-        std::lock_guard<std::mutex> g(g_run_mu);
+        std::lock_guard<std::mutex> g(g_run[stream].mu);
         b.clear();
         b.swap(g_run[stream].q);
     }
@@ -511,9 +511,9 @@ bool run_and_read(Codec& c, Reads enqueue_reads) {
         {
             const unsigned st = c.staging.stream;
             RunQueue& rq = g_run[st];
-            std::unique_lock<std::mutex> lk(g_run_mu);
+            std::unique_lock<std::mutex> lk(rq.mu);
             rq.q.push_back(&req);
-            g_run_cv.wait(lk, [&req, &rq] { return req.launched || !rq.leader; });
+            req.cv.wait(lk, [&req, &rq] { return req.launched || !rq.leader; });
             if (!req.launched) {
                 rq.leader = true;
                 std::vector<RunReq*> b;
@@ -521,11 +521,13 @@ bool run_and_read(Codec& c, Reads enqueue_reads) {
                     lk.unlock();
                     launch_batch(b, st);  // (takes the queue under the device lock)
                     lk.lock();
-                    for (RunReq* r : b) r->launched = true;
-                    g_run_cv.notify_all();
+                    for (RunReq* r : b) {
+                        r->launched = true;
+                        if (r != &req) r->cv.notify_one();
+                    }
                 }
                 rq.leader = false;
-                g_run_cv.notify_all();  // a caller still queued becomes the next leader
+                if (!rq.q.empty()) rq.q.front()->cv.notify_one();  // the next caller queued leads
             }
         }
         ok = req.ok;

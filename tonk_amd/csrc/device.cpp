@@ -1101,7 +1101,17 @@ void Device::host_copy(const HostCopy* d, uint32_t n, bool to_host) {
     if (!n) return;
     flush_uploads();
     hipStream_t st = (hipStream_t)stream_;
-    HcBuf& b = hc_[hc_next_++ % (sizeof(hc_) / sizeof(hc_[0]))];
+    // a descriptor buffer whose previous launch has read it: the next one in turn that is free,
+    // or (all busy) the next one in turn once it is (the ring is shared by every stream, and a
+    // buffer's last launch may be queued behind another stream's work)
+    const unsigned nb = (unsigned)(sizeof(hc_) / sizeof(hc_[0]));
+    unsigned pick = hc_next_ % nb;
+    for (unsigned k = 0; k < nb; ++k) {
+        const unsigned i = (hc_next_ + k) % nb;
+        if (!hc_[i].ev || hipEventQuery((hipEvent_t)hc_[i].ev) == hipSuccess) { pick = i; break; }
+    }
+    hc_next_ = pick + 1;
+    HcBuf& b = hc_[pick];
     if (b.ev) HIPCHK(hipEventSynchronize((hipEvent_t)b.ev));  // (its previous launch has read it)
     const size_t need = (size_t)n * sizeof(HostCopyDev);
     if (need > b.cap) {  // (pooled: hipHostFree would wait for the whole device)

@@ -336,7 +336,7 @@ private:
     // host_copy: descriptor buffers (pinned, read by the kernel over the link), used in turn; each
     // is reused once the event recorded behind its launch has completed
     struct HcBuf { void* p = nullptr; size_t cap = 0; void* ev = nullptr; };
-    HcBuf hc_[8];
+    HcBuf hc_[32];
     unsigned hc_next_ = 0;
     bool collect_reads_ = false;
     std::vector<HostCopy> reads_;
