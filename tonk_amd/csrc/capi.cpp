@@ -650,6 +650,7 @@ SIAMESE_EXPORT int siamese_init_(int version) {
     unsigned nstreams = 4;
     if (const char* a = getenv("TONK_AMD_CAPI_STREAMS")) nstreams = (unsigned)atoi(a);
     if (nstreams > 1) g_rt->dev.add_streams(nstreams);
+    g_rt->dev.warm_streams();
     g_rt->ok = true;
     if (const char* w = getenv("TONK_AMD_CAPI_WATCH")) {
         const double period = atof(w) > 0 ? atof(w) : 5.0;

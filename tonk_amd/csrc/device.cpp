@@ -114,6 +114,27 @@ void Device::add_streams(unsigned k) {
     sc_per_stream_.assign(k, std::make_pair((uint8_t*)nullptr, (size_t)0));
 }
 
+void Device::warm_streams() {
+    // The runtime creates a stream's hardware queues on its first kernel and its first copy
+    // (~80 ms each, blocking); do both on every launch stream now instead of under the device
+    // lock of the first codecs to use them.
+    uint8_t* h = (uint8_t*)host_alloc(4096);
+    uint8_t* d = nullptr;
+    HIPCHK(hipMalloc((void**)&d, 4096));
+    if (!h || !d) return;
+    std::vector<void*> all = streams_;
+    if (all.empty()) all.push_back(stream_);
+    for (void* s : all) {
+        hipStream_t st = (hipStream_t)s;
+        hipLaunchKernelGGL(tamd_timed_region, dim3(1), dim3(64), 0, st);
+        HIPCHK(hipMemcpyAsync(d, h, 64, hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(h, d, 64, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+    }
+    HIPCHK(hipFree(d));
+    host_free(h);
+}
+
 void Device::sync_all_streams() {
     if (streams_.empty()) {
         HIPCHK(hipStreamSynchronize((hipStream_t)stream_));

@@ -84,6 +84,7 @@ public:
         if (i < streams_.size()) { stream_ = streams_[i]; cur_stream_ = i; }
     }
     unsigned stream_count() const { return streams_.empty() ? 1u : (unsigned)streams_.size(); }
+    void warm_streams();  // first kernel and copies on every launch stream now (queue creation)
     static const unsigned kMaxStreams = 16;  // add_streams clamps to it
 
     // Enqueue the pending programs of `ctxs` as one merged program (asynchronous).  Returns the
