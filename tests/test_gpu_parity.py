@@ -219,13 +219,13 @@ def test_capi_device_failure_disables_codec(golden_index):
 
 def test_capi_arena_grows_past_many_chunks(golden_index, tmp_path):
     """32 codec pairs alive at once with 48 MB segments each need about 3 GB: the C ABI arena
-    (256 MB to start) maps chunk after chunk of its reserved range, and every stream still
+    (256 MB to start here) maps chunk after chunk of its reserved range, and every stream still
     matches the reference."""
     import hashlib
     exe = os.path.join(NATIVE, "_build", "capi_gen")
     entry = golden_index["batches"]["cfg2_64x4096_p2_ack64"]
     prefix = str(tmp_path / "s")
-    env = dict(os.environ, TONK_AMD_SEGMENT_KB=str(48 << 10))
+    env = dict(os.environ, TONK_AMD_SEGMENT_KB=str(48 << 10), TONK_AMD_ARENA_MB="256")
     out = subprocess.run([exe, "transcripts", prefix, "threads=32", "streams=32", "stream=0"] + entry["args"],
                          capture_output=True, timeout=600, env=env)
     assert out.returncode == 0, out.stderr.decode()[-2000:]

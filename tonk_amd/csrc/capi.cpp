@@ -610,7 +610,8 @@ SIAMESE_EXPORT int siamese_init_(int version) {
     if (const char* d = getenv("TONK_AMD_DEVICE")) device = atoi(d);
     // Initial arena (grown on demand up to TONK_AMD_ARENA_MAX_MB of reserved address space) and
     // the size of the ranges codecs take from it.
-    uint64_t arena_mb = 256, max_mb = 64 << 10, seg_kb = 4096;
+    // (4 GB mapped up front: every growth remaps device memory while codecs run; 288 GB per GPU)
+    uint64_t arena_mb = 4096, max_mb = 64 << 10, seg_kb = 4096;
     if (const char* a = getenv("TONK_AMD_ARENA_MB")) arena_mb = strtoull(a, nullptr, 10);
     if (const char* a = getenv("TONK_AMD_ARENA_MAX_MB")) max_mb = strtoull(a, nullptr, 10);
     if (const char* a = getenv("TONK_AMD_SEGMENT_KB")) seg_kb = strtoull(a, nullptr, 10);
@@ -637,6 +638,7 @@ SIAMESE_EXPORT int siamese_init_(int version) {
     // events and pinned staging for the codecs to come, created now: creating either later makes
     // a driver call that can block for milliseconds, and it would happen under the device lock
     g_rt->dev.reserve_events(1024);
+    Device::host_prefill(4);  // (a Tonk process with 100 connections uses ~250 MB of staging)
     if (!Device::host_reserve(1)) {
         fprintf(stderr, "tonk_amd: pinned host memory unavailable\n");
         return Siamese_Disabled;

@@ -1207,16 +1207,45 @@ std::vector<void*> g_pin_free[64];
 std::unordered_map<void*, unsigned> g_pin_class;
 uint8_t* g_slab = nullptr;  // the slab blocks are cut from
 size_t g_slab_used = kPinSlab;
+std::vector<void*> g_spare_slabs;  // mapped and warmed ahead (host_prefill)
+
+// A new slab, and one small copy out of it and back: the first transfer touching a new pinned
+// allocation has been seen to block for ~80 ms, which should not happen under the device lock.
+void* new_slab() {
+    void* p = nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    if (hipHostMalloc(&p, kPinSlab, hipHostMallocDefault) != hipSuccess) return nullptr;
+    static uint8_t* d = nullptr;
+    if (!d && hipMalloc((void**)&d, 4096) != hipSuccess) d = nullptr;
+    if (d) {
+        memset(p, 0, 4096);
+        hipMemcpy(d, p, 4096, hipMemcpyHostToDevice);
+        hipMemcpy(p, d, 4096, hipMemcpyDeviceToHost);
+    }
+    report_slow("pinned slab", t0, kPinSlab >> 20, 0);
+    return p;
+}
 }  // namespace
+
+void Device::host_prefill(unsigned slabs) {
+    std::vector<void*> got;
+    for (unsigned i = 0; i < slabs; ++i)
+        if (void* p = new_slab()) got.push_back(p);
+    std::lock_guard<std::mutex> g(g_pin_mu);
+    g_spare_slabs.insert(g_spare_slabs.end(), got.begin(), got.end());
+}
 
 bool Device::host_reserve(size_t bytes) {
     std::lock_guard<std::mutex> g(g_pin_mu);
     // (one slab at a time: the current one is only replaced once used up)
     if (g_slab && g_slab_used + bytes <= kPinSlab) return true;
     void* p = nullptr;
-    const auto t0 = std::chrono::steady_clock::now();
-    if (hipHostMalloc(&p, kPinSlab, hipHostMallocDefault) != hipSuccess) return false;
-    report_slow("pinned slab", t0, kPinSlab >> 20, 0);
+    if (!g_spare_slabs.empty()) {
+        p = g_spare_slabs.back();
+        g_spare_slabs.pop_back();
+    } else if (!(p = new_slab())) {
+        return false;
+    }
     if (g_slab) {  // the rest of the old slab becomes free blocks
         for (unsigned c = 63; c >= 12; --c)
             while (g_slab_used + ((size_t)1 << c) <= kPinSlab) {

@@ -176,6 +176,7 @@ public:
     void event_release(void* ev) { free_events_.push_back(ev); }
     static void* host_alloc(size_t n);  // pinned (pooled; see device.cpp)
     static bool host_reserve(size_t n);  // map a pinned slab now if fewer than n bytes are left in it
+    static void host_prefill(unsigned slabs);  // map (and warm) that many 64 MB slabs ahead of use
     static void host_free(void* p);
 
     // Bench helpers (kernels.hip).
