@@ -18,6 +18,7 @@ typedef void (*ExecFn)(tamd_segments, const uint8_t*, uint32_t, uint8_t*, const 
                        unsigned long long*);
 extern "C" __global__ void tamd_gf_selftest(const uint32_t*, uint8_t*);
 extern "C" __global__ void tamd_timed_region();
+extern "C" __global__ void tamd_nop();
 extern "C" __global__ void tamd_gather_rows(const tamd::Device::GatherDesc*, uint32_t, const uint8_t*, uint8_t*);
 struct ScatterDescDev { uint32_t row, len, src, pad; };
 extern "C" __global__ void tamd_scatter_rows(const ScatterDescDev*, uint32_t, const uint8_t*, uint8_t*);
@@ -124,13 +125,22 @@ void Device::warm_streams() {
     if (!h || !d) return;
     std::vector<void*> all = streams_;
     if (all.empty()) all.push_back(stream_);
-    for (void* s : all) {
-        hipStream_t st = (hipStream_t)s;
-        hipLaunchKernelGGL(tamd_timed_region, dim3(1), dim3(64), 0, st);
-        HIPCHK(hipMemcpyAsync(d, h, 64, hipMemcpyHostToDevice, st));
-        HIPCHK(hipMemcpyAsync(h, d, 64, hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
-    }
+    // Then many commands in flight at once, so the runtime's per-queue pools (kernel arguments,
+    // completion signals) grow to a working size now: under load each growth blocked ~80 ms.
+    for (int round = 0; round < 2; ++round)
+        for (void* s : all) {
+            hipStream_t st = (hipStream_t)s;
+            const int n = round ? 1024 : 1;
+            for (int i = 0; i < n; ++i) {
+                hipLaunchKernelGGL(tamd_nop, dim3(1), dim3(64), 0, st);
+                if (i % 8 == 0) {
+                    HIPCHK(hipMemcpyAsync(d, h, 64, hipMemcpyHostToDevice, st));
+                    HIPCHK(hipMemcpyAsync(h, d, 64, hipMemcpyDeviceToHost, st));
+                }
+            }
+            if (!round) HIPCHK(hipStreamSynchronize(st));
+        }
+    sync_all_streams();
     HIPCHK(hipFree(d));
     host_free(h);
 }

@@ -934,3 +934,5 @@ extern "C" __global__ void tamd_verify_rows(const VerifyDesc* __restrict__ d, ui
 
 // Marks the start and end of a bench's timed region in kernel traces (Device::set_timing).
 extern "C" __global__ void tamd_timed_region() {}
+// Empty kernel of the C ABI's start-up warming (Device::warm_streams): not a trace marker.
+extern "C" __global__ void tamd_nop() {}
