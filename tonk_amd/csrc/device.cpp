@@ -143,6 +143,21 @@ void Device::warm_streams() {
     sync_all_streams();
     HIPCHK(hipFree(d));
     host_free(h);
+    // scatter_upload's landing areas at their working size (a staged half: up to 1 MB of packets
+    // and its descriptors), so none grows -- hipFree + hipMalloc -- while codecs run
+    const size_t land = 2u << 20;
+    if (!sc_per_stream_.empty()) {
+        for (auto& a : sc_per_stream_)
+            if (a.second < land) {
+                if (a.first) HIPCHK(hipFree(a.first));
+                HIPCHK(hipMalloc((void**)&a.first, land));
+                a.second = land;
+            }
+    } else if (sc_cap_ < land) {
+        if (sc_dev_) HIPCHK(hipFree(sc_dev_));
+        HIPCHK(hipMalloc((void**)&sc_dev_, land));
+        sc_cap_ = land;
+    }
 }
 
 void Device::sync_all_streams() {
