@@ -35,8 +35,30 @@ extern "C" __global__ void tamd_verify_rows(const VerifyDescDev*, uint32_t, cons
 
 namespace tamd {
 
+// With the C ABI watchdog on (TONK_AMD_CAPI_WATCH), every runtime call through HIPCHK / HIPT
+// that blocks for 10 ms or more is named on stderr.
+static bool hip_watch() {
+    static const bool on = getenv("TONK_AMD_CAPI_WATCH") != nullptr;
+    return on;
+}
+struct HipTimer {
+    const char* what;
+    std::chrono::steady_clock::time_point t0;
+    explicit HipTimer(const char* w) : what(w) { if (hip_watch()) t0 = std::chrono::steady_clock::now(); }
+    ~HipTimer() {
+        if (!hip_watch()) return;
+        const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        if (ms >= 10.0) fprintf(stderr, "tonk_amd: slow HIP call %.1f ms: %.60s\n", ms, what);
+    }
+};
+#define HIPT(x)                  \
+    do {                         \
+        HipTimer ht_(#x);        \
+        x;                       \
+    } while (0)
 #define HIPCHK(x)                                                                        \
     do {                                                                                 \
+        HipTimer ht_(#x);                                                                \
         hipError_t e_ = (x);                                                             \
         if (e_ != hipSuccess) {                                                          \
             fprintf(stderr, "tonk_amd: %s failed: %s\n", #x, hipGetErrorString(e_));     \
@@ -817,11 +839,11 @@ void Device::launch_step(Inflight* fresh, unsigned long long* stamps) {
     // Timed: the events carry the dispatch's own start and end (hipExtLaunchKernelGGL), as a
     // kernel trace does; events recorded around the launch would add the dispatch latency.
     if (timing_)
-        hipExtLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, st, e0, e1, 0, sg, (const uint8_t*)prog_dev_, shared,
-                              arena_, d_gf_, d_zero_, stamps);
+        HIPT(hipExtLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, st, e0, e1, 0, sg, (const uint8_t*)prog_dev_, shared,
+                              arena_, d_gf_, d_zero_, stamps));
     else
-        hipLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, st, sg, (const uint8_t*)prog_dev_, shared, arena_, d_gf_,
-                           d_zero_, stamps);
+        HIPT(hipLaunchKernelGGL(fn, dim3(grid), dim3(256), 0, st, sg, (const uint8_t*)prog_dev_, shared, arena_, d_gf_,
+                           d_zero_, stamps));
     if (timing_) {
         timing_events_.push_back(std::make_pair((void*)e0, (void*)e1));
     }
@@ -1054,8 +1076,8 @@ void Device::flush_uploads() {
     const size_t end = up_used_ + dbytes;
     HIPCHK(hipMemcpyAsync(up_dev_ + begin, up_host_ + begin, end - begin, hipMemcpyHostToDevice, st));
     // descriptor sources are offsets into up_dev_ (the same offsets as in up_host_)
-    hipLaunchKernelGGL(tamd_scatter_rows, dim3(cnt), dim3(64), 0, st, (const ScatterDescDev*)(up_dev_ + up_used_), cnt,
-                       (const uint8_t*)up_dev_, arena_);
+    HIPT(hipLaunchKernelGGL(tamd_scatter_rows, dim3(cnt), dim3(64), 0, st, (const ScatterDescDev*)(up_dev_ + up_used_), cnt,
+                       (const uint8_t*)up_dev_, arena_));
     HIPCHK(hipGetLastError());
     up_used_ = (end + 15) & ~(size_t)15;
     up_flushed_ = up_used_;
@@ -1089,8 +1111,8 @@ void Device::scatter_upload(uint8_t* src, size_t bytes, const ScatterIn* d, uint
     }
     // (the landing area is reused batch after batch: copies and scatters are stream ordered)
     HIPCHK(hipMemcpyAsync(sc_dev_, src, total, hipMemcpyHostToDevice, st));
-    hipLaunchKernelGGL(tamd_scatter_rows, dim3(n), dim3(64), 0, st, (const ScatterDescDev*)(sc_dev_ + at), n,
-                       (const uint8_t*)sc_dev_, arena_);
+    HIPT(hipLaunchKernelGGL(tamd_scatter_rows, dim3(n), dim3(64), 0, st, (const ScatterDescDev*)(sc_dev_ + at), n,
+                       (const uint8_t*)sc_dev_, arena_));
     HIPCHK(hipGetLastError());
     stats_.upload_bytes += total;
 }
@@ -1181,7 +1203,7 @@ void Device::host_copy(const HostCopy* d, uint32_t n, bool to_host) {
         hd[k].unit = (uint32_t)(d[k].arena_off / 64);
         hd[k].len = d[k].len;
     }
-    hipLaunchKernelGGL(tamd_host_copy, dim3(n), dim3(128), 0, st, (const HostCopyDev*)b.p, n, arena_, to_host ? 1u : 0u);
+    HIPT(hipLaunchKernelGGL(tamd_host_copy, dim3(n), dim3(128), 0, st, (const HostCopyDev*)b.p, n, arena_, to_host ? 1u : 0u));
     HIPCHK(hipGetLastError());
     if (!b.ev) {
         hipEvent_t he;

@@ -5,6 +5,7 @@
 #   PART=b  the configs[2] / [1] / [4] and compression lines, rocprofv3 kernel traces of the
 #           default bench and of the compressor (+ the timed-region average)
 #   PART=c  the siamese.h C ABI line and the two-rank rehearsal
+#   PART=d  part a without the tests (smoke and the default bench line)
 # (no PART: all three in one go).  Every GPU step has its own time limit; a part stops at its first
 # failure.
 set -o pipefail
@@ -15,6 +16,10 @@ PART=${PART:-abc}
 mkdir -p "$OUT" && cd "$R" || exit 1
 if [[ $PART == *a* ]]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread > "$OUT/gpu_tests_$TAG.log" 2>&1 &&
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke_$TAG.log" 2>&1 &&
+  timeout -k 10 900 python bench.py > "$OUT/bench_$TAG.json" 2> "$OUT/bench_$TAG.err" || exit 1
+fi
+if [[ $PART == *d* ]]; then
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke_$TAG.log" 2>&1 &&
   timeout -k 10 900 python bench.py > "$OUT/bench_$TAG.json" 2> "$OUT/bench_$TAG.err" || exit 1
 fi
