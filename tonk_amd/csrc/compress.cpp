@@ -128,9 +128,10 @@ struct LzRequest {
     unsigned* written;
     int rc = 0;
     bool done = false;
+    std::condition_variable cv;  // its caller waits here: a batch wakes only its own callers
 };
 std::mutex g_req_mu;
-std::condition_variable g_req_cv;
+std::condition_variable g_req_cv;  // tamd_compressor_destroy waits here for its last call
 std::vector<LzRequest*> g_pending;
 bool g_leader = false;
 
@@ -344,7 +345,7 @@ extern "C" int tamd_compressor_compress(void* cp, const uint8_t* data, unsigned 
     std::unique_lock<std::mutex> lk(g_req_mu);
     g_pending.push_back(&req);
     // Wait while another caller leads; take over when it steps down with this request unserved.
-    g_req_cv.wait(lk, [&req] { return req.done || !g_leader; });
+    req.cv.wait(lk, [&req] { return req.done || !g_leader; });
     if (req.done) return req.rc;
     g_leader = true;
     std::vector<LzRequest*> batch, later;
@@ -369,11 +370,12 @@ extern "C" int tamd_compressor_compress(void* cp, const uint8_t* data, unsigned 
         for (LzRequest* r : batch) {
             r->c->queued = false;
             r->done = true;
+            if (r != &req) r->cv.notify_one();
         }
         g_req_cv.notify_all();
     }
     g_leader = false;
-    g_req_cv.notify_all();  // a caller whose request is still queued becomes the next leader
+    if (!g_pending.empty()) g_pending.front()->cv.notify_one();  // the next queued caller leads
     return req.rc;
 }
 
