@@ -7,7 +7,7 @@ rank*64 .. rank*64+63), 1300-byte payloads, 1% uniform loss on originals and rec
 recovery rate f = max(2p, 1%) = 2%, acknowledgements every 64 originals.  Payloads are
 synthetic (PCG, seed 1000 + stream id) and already resident in HBM when timing starts.
 
-A step = 16384 originals per stream, in 4 device programs of 4096: the host control planes (16
+A step = 65536 originals per stream, in 16 device programs of 4096: the host control planes (16
 worker threads per GPU) turn every add/encode/ack/decode into device ops and each program's byte
 work runs as one merged launch sequence on the GPU, pipelined with the host building the next.  `value` is whole-job
 payload GiB/s over all ranks; the timed region is bracketed by a barrier and a device sync.
@@ -79,7 +79,11 @@ METRIC = "Siamese FEC encode+decode GiB/s (device-resident), 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0
 STREAMS_PER_GPU = 64
 ORIGINALS_PER_STEP = 4096   # per stream per device program (tamd_session_step)
-PROGRAMS_PER_STEP = 4       # a bench step: 4 programs, 16384 originals per stream
+# A bench step: 16 programs, 65536 originals per stream (round 5; 4 before): the driver's
+# `--steps 20` then times ~110 ms instead of ~28 ms.  The inputs are a pool of INPUT_POOL rows per
+# side per stream that original i reads as row i mod INPUT_POOL (tonk_amd.h input_pool).
+PROGRAMS_PER_STEP = 16
+INPUT_POOL = 65536
 LOSS = 0.01
 ACK = 64
 PAYLOAD = 1300
@@ -682,7 +686,7 @@ def spawn_ranks(n: int, argv: list[str]) -> int:
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=40)
+    ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-end-to-end", action="store_true", help="skip the PCIe-inclusive side measurement")
@@ -770,9 +774,10 @@ def main() -> int:
     device = int(os.environ.get("TONK_AMD_BENCH_DEVICE", local_rank))
     if "TONK_AMD_BENCH_DEVICE" in os.environ and local_world > 1 and "TONK_AMD_CPU_SLOT" not in os.environ:
         os.environ["TONK_AMD_CPU_SLOT"] = f"{local_rank}/{local_world}"  # (disjoint cores all the same)
+    pool = min(INPUT_POOL, n_orig)
     sess = tonk_amd.Session(wp, n_streams=STREAMS_PER_GPU, device=device,
                             stream_base=stream_base(rank), threads=threads,
-                            arena_bytes=(2 * n_orig * STREAMS_PER_GPU * 1344) + (4 << 30))
+                            arena_bytes=(2 * pool * STREAMS_PER_GPU * 1344) + (4 << 30), input_pool=pool)
     sess.generate()
     rank_cores = d.gather(pad_cores(sess.cpus()))
 
@@ -825,9 +830,9 @@ def main() -> int:
     pmc = pmc_traffic(a.workload, a.steps, a.warmup) if (rank == 0 and world == 1 and not a.no_pmc) else None
     traffic = pmc.get("traffic_per_timed_launch") if pmc else None
     workload = {
-        "cfg3": "configs[3] per-GPU shard: 64 independent streams/GPU, 16384 originals per stream per step (4 programs), "
+        "cfg3": "configs[3] per-GPU shard: 64 independent streams/GPU, 65536 originals per stream per step (16 programs), "
                 "1300 B payloads, 1% uniform loss, f=2%, ack every 64",
-        "cfg2": "configs[2]: 64 independent streams/GPU, 16384 originals per stream per step (4 programs), 1300 B payloads, "
+        "cfg2": "configs[2]: 64 independent streams/GPU, 65536 originals per stream per step (16 programs), 1300 B payloads, "
                 "2% uniform loss, f=4%, ack every 64",
     }[a.workload]
     out = {
@@ -846,7 +851,7 @@ def main() -> int:
         "config": {
             "workload": workload,
             "streams_per_gpu": STREAMS_PER_GPU, "originals_per_step": ORIGINALS_PER_STEP * PROGRAMS_PER_STEP,
-            "originals_per_program": ORIGINALS_PER_STEP, "payload_bytes": PAYLOAD,
+            "originals_per_program": ORIGINALS_PER_STEP, "payload_bytes": PAYLOAD, "input_pool_per_stream": pool,
             "loss": loss, "ack_every": ACK, "host_threads_per_gpu": threads,
             "parallelism": f"streams sharded {STREAMS_PER_GPU}/GPU x {world} GPU, no collective",
             # each rank's pinned worker cores (its share of its GPU's NUMA node, tamd_cpu_share)

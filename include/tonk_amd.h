@@ -39,6 +39,10 @@ typedef struct tamd_session_params {
     uint32_t rtx_every;        /* retransmission tick every rtx_every originals (0: off) under a
                                   virtual clock advancing rtx_msec per original (workload.h) */
     uint32_t rtx_msec;
+    uint32_t input_pool;       /* > 0: only this many input rows per side are generated and original
+                                  i reads row i mod input_pool (the bench's long streams: the codecs'
+                                  work does not depend on the payload bytes, as the reference
+                                  timing leg's payload pool).  Ignored with record or stage_host. */
 } tamd_session_params;
 
 /* Summary counters (tamd_session_summary indices). */

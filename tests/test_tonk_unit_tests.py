@@ -26,11 +26,11 @@ if os.environ.get("TONK_AMD_TONK_BINARY"):
 @pytest.mark.timeout(1500)
 @pytest.mark.parametrize("binary", BINARIES)
 def test_tonk_unit_tests_with_mi355x_codec(binary):
-    """Every Tonk unit test must pass.  TestBandwidthControl is a wall-clock simulation (100
-    lossy connections through the Mau proxy, 300 s limit) whose outcome depends on how fast the
-    first seconds of codec calls are; when it -- and only it -- fails, the binary runs once more
-    and must then pass (DESIGN.md s5.4 records how often and why: driver calls that block for
-    ~80 ms right after start).  Both logs are kept."""
+    """Every Tonk unit test must pass, on the binary's one and only run.  TestBandwidthControl is
+    a wall-clock simulation (100 lossy connections through the Mau proxy, 300 s limit) whose
+    outcome depends on how fast the codec calls are from the first second on: the C ABI's calls
+    go through the launch-free persistent executor (server.h), so no runtime enqueue under a
+    process-wide lock can stall every connection."""
     exe = os.path.join(ROOT, "oracle", "_ref", "tonk", binary)
     if not os.path.exists(exe):
         pytest.skip(f"oracle/_ref/tonk/{binary} not built (needs /root/reference at build time)")
@@ -40,19 +40,10 @@ def test_tonk_unit_tests_with_mi355x_codec(binary):
     env = dict(os.environ, TONK_AMD_CAPI_WATCH="5")
     out_dir = os.path.join(ROOT, "gpurun_out")
     os.makedirs(out_dir, exist_ok=True)
-
-    def run(path):
-        with open(path, "w") as f:
-            r = subprocess.run([exe], stdin=subprocess.DEVNULL, stdout=f, stderr=subprocess.STDOUT, timeout=700, env=env)
-        with open(path) as f:
-            return r.returncode, f.read()
-
     path = os.path.join(out_dir, f"tonk_{binary}.log")
-    rc, log = run(path)
-    failures = [l for l in log.splitlines() if "Failure:" in l]
-    if rc != 0 and failures and all("TestBandwidthControl" in l for l in failures):
-        os.replace(path, os.path.join(out_dir, f"tonk_{binary}_try1.log"))
-        print(f"{binary}: TestBandwidthControl failed once (log tonk_{binary}_try1.log); running again")
-        rc, log = run(path)
-    assert rc == 0, log[-3000:]
+    with open(path, "w") as f:
+        r = subprocess.run([exe], stdin=subprocess.DEVNULL, stdout=f, stderr=subprocess.STDOUT, timeout=700, env=env)
+    with open(path) as f:
+        log = f.read()
+    assert r.returncode == 0, log[-3000:]
     assert "SUCCESS" in log, log[-3000:]

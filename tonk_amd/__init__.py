@@ -78,7 +78,8 @@ class _SessionParams(ctypes.Structure):
         "device", "n_streams", "stream_base", "n_threads", "n_originals", "payload_min", "payload_max",
         "loss_thresh", "ge_enable", "gb_thresh", "bg_thresh", "loss_on_recovery", "fec_rate_q16",
         "ack_every", "ack_bytes", "arq_lag", "flush_max", "record", "stage_host")] + [
-            ("arena_bytes", ctypes.c_uint64), ("rtx_every", ctypes.c_uint32), ("rtx_msec", ctypes.c_uint32)]
+            ("arena_bytes", ctypes.c_uint64), ("rtx_every", ctypes.c_uint32), ("rtx_msec", ctypes.c_uint32),
+            ("input_pool", ctypes.c_uint32)]
 
 
 SUMMARY_FIELDS = ["originals", "lost_originals", "recoveries", "lost_recoveries", "recovered", "arq",
@@ -168,7 +169,8 @@ class Session:
     """Batched device-resident Siamese streams on one MI355X (include/tonk_amd.h)."""
 
     def __init__(self, wp: WorkloadParams, n_streams: int, device: int = 0, stream_base: int = 0,
-                 threads: int = 1, arena_bytes: int = 4 << 30, record: bool = False, stage_host: bool = False):
+                 threads: int = 1, arena_bytes: int = 4 << 30, record: bool = False, stage_host: bool = False,
+                 input_pool: int = 0):
         p = _SessionParams()
         p.device, p.n_streams, p.stream_base, p.n_threads = device, n_streams, stream_base, threads
         p.n_originals, p.payload_min, p.payload_max = wp.n, wp.pmin, wp.pmax
@@ -178,6 +180,7 @@ class Session:
         # stage_host: True (both ends), or the tonk_amd.h mask (1 sender end, 2 receiver end)
         p.stage_host = 3 if stage_host is True else int(stage_host or 0)
         p.rtx_every, p.rtx_msec = wp.rtx, wp.rtxms
+        p.input_pool = input_pool
         self.n_streams = n_streams
         err = ctypes.create_string_buffer(512)
         self._h = lib().tamd_session_create(ctypes.byref(p), err, len(err))

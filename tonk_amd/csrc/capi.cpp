@@ -18,6 +18,7 @@
 
 #include "decoder.h"
 #include "device.h"
+#include "server.h"
 
 #include <atomic>
 #include <chrono>
@@ -98,6 +99,8 @@ struct Runtime {
     SegmentPool pool;
     bool ok = false;
 };
+// The launch-free path (server.h): null when off (TONK_AMD_SERVE=0) or when it failed its checks.
+Server* g_srv = nullptr;
 
 struct DevLock {
     std::unique_lock<std::mutex> lk;
@@ -201,6 +204,10 @@ void watch_loop(double period_s) {
             fprintf(stderr, "[tonk_amd capi]   %-28s calls=%llu ms=%.1f%s\n", st->name, (unsigned long long)c,
                     st->ns.load() * 1e-6, h.c_str());
         }
+        if (g_srv)
+            fprintf(stderr, "[tonk_amd capi]   server: posted=%llu launches=%llu slow_waits=%llu gpu_ms=%.1f\n",
+                    (unsigned long long)g_srv->posted.load(), (unsigned long long)g_srv->launches.load(),
+                    (unsigned long long)g_srv->waits_slow.load(), g_srv->gpu_ns_sum * 1e-6);
         dump_encoders();
     }
 }
@@ -233,16 +240,28 @@ struct Staging {
     int cur = 0;
     size_t used = 0;                 // packet bytes in the current half (16-B aligned)
     std::vector<Device::ScatterIn> descs;
+    // The launch-free path: one command buffer per half.  A half that fills up goes out as an
+    // upload-only command from its buffer; a program's command is built in the current half's.
+    CmdBuf cmd[2];
 
     size_t need(size_t bytes, size_t n_desc) const { return ((bytes + 15) & ~(size_t)15) + n_desc * 16 + 16; }
     // The current half's packets as zero-copy sources of one batched host_copy (combined
     // launches): the half is reused by the codec's next adds, which cannot come before the batch
     // has completed (the codec's caller waits for it).
     void take_uploads(std::vector<Device::HostCopy>& out) {
-        for (const Device::ScatterIn& d : descs)
-            out.push_back(Device::HostCopy{half[cur] + d.src, (uint64_t)d.row * TAMD_ROW_UNIT, d.len});
+        peek_uploads(out);
         descs.clear();
         used = 0;
+    }
+    void peek_uploads(std::vector<Device::HostCopy>& out) const {
+        for (const Device::ScatterIn& d : descs)
+            out.push_back(Device::HostCopy{half[cur] + d.src, (uint64_t)d.row * TAMD_ROW_UNIT, d.len});
+    }
+    // Every command of this codec's halves has completed (launch-free path).
+    bool settle_cmds() {
+        bool ok = true;
+        for (CmdBuf& b : cmd) ok = g_srv->settle(b) && ok;
+        return ok;
     }
     // Enqueue the current half (caller holds the device lock).
     void send_locked(Device& dev) {
@@ -271,6 +290,7 @@ struct Staging {
     bool grow(size_t want) {
         settle(sent[0]);
         settle(sent[1]);
+        if (g_srv && !settle_cmds()) return false;
         for (uint8_t*& h : half) {
             Device::host_free(h);
             h = nullptr;
@@ -282,6 +302,20 @@ struct Staging {
     }
     // Copy a packet into the staging for arena unit offset `row`.
     bool stage(uint32_t row, const uint8_t* data, uint32_t n) {
+        if (used && (used + n > kFlushBytes || need(used + n, descs.size() + 1) > cap) && g_srv) {
+            // launch-free: the full half lands by an upload-only command; the other half is
+            // reused once its own command has completed
+            thread_local std::vector<Device::HostCopy> ups, none;
+            ups.clear();
+            peek_uploads(ups);
+            if (g_srv->settle(cmd[cur]) && Server::build(cmd[cur], ups, nullptr, none)) {
+                g_srv->post(cmd[cur]);
+                descs.clear();
+                used = 0;
+                cur ^= 1;
+                if (!g_srv->settle(cmd[cur])) return false;
+            }
+        }
         if (used && (used + n > kFlushBytes || need(used + n, descs.size() + 1) > cap)) {
             {
                 DevLock dl;
@@ -308,6 +342,7 @@ struct Staging {
     }
     ~Staging() {
         for (uint8_t* h : half) Device::host_free(h);
+        for (CmdBuf& b : cmd) Device::host_free(b.mem);
     }
 };
 
@@ -346,7 +381,10 @@ struct Codec {
         return pinned != nullptr;
     }
     // Before the codec's rows go back to the pool: nothing of its may still be in flight.
+    bool used_launch = false;  // a program of this codec went through the launch path
     void quiesce() {
+        if (g_srv) staging.settle_cmds();
+        if (g_srv && !used_launch && !staging.sent[0] && !staging.sent[1]) return;
         DevLock dl;
         g_rt->dev.synchronize();
         for (void*& ev : staging.sent)
@@ -401,7 +439,7 @@ struct BatchDone {
 };
 struct RunReq {
     Codec* c = nullptr;
-    const std::function<void(Device&)>* reads = nullptr;
+    const std::vector<Device::HostCopy>* reads = nullptr;
     BatchDone* done = nullptr;
     bool launched = false, ok = true;
     std::condition_variable cv;  // its caller waits here (woken alone: no herd of hundreds of threads)
@@ -467,7 +505,8 @@ void launch_batch(std::vector<RunReq*>& b, unsigned stream) {
     g_batches.fetch_add(1, std::memory_order_relaxed);
     g_batched.fetch_add(b.size(), std::memory_order_relaxed);
     dev.collect_host_reads(true);
-    for (RunReq* r : b) (*r->reads)(dev);
+    for (RunReq* r : b)
+        for (const Device::HostCopy& x : *r->reads) dev.download_pinned(x.host, x.arena_off, x.len);
     dev.collect_host_reads(false);
     dev.flush_host_reads();
     BatchDone* done = new BatchDone();
@@ -492,22 +531,57 @@ void launch_batch(std::vector<RunReq*>& b, unsigned stream) {
     }
 }
 
-// Close the codec's pending program and enqueue it with the reads `enqueue_reads` adds behind
-// it, then wait for all of it without any lock.  Returns false on a device failure.
-template <class Reads>
-bool run_and_read(Codec& c, Reads enqueue_reads) {
+// Close the codec's pending program and run it with `reads` (arena rows into the caller's
+// pinned buffer) behind it, then wait for all of it without any lock.  Returns false on a device
+// failure.  Launch-free when the command fits a worker of the persistent executor (server.h);
+// otherwise, or with the server off, through kernel launches on the codec's launch stream.
+bool run_and_read(Codec& c, const std::vector<Device::HostCopy>& reads) {
     Context& ctx = c.ctx;
     const int64_t t0 = g_watch ? now_ns() : 0;
     ctx.prepare_flush();
     const int64_t t1 = g_watch ? now_ns() : 0;
+    if (g_srv) {
+        Staging& sg = c.staging;
+        // (upload-only commands of full halves -- or launch-path scatters of halves whose command
+        // did not fit -- landed before this program reads their rows)
+        if (!sg.settle_cmds()) return false;
+        Staging::settle(sg.sent[0]);
+        Staging::settle(sg.sent[1]);
+        thread_local std::vector<Device::HostCopy> ups;
+        ups.clear();
+        sg.peek_uploads(ups);
+        CmdBuf& b = sg.cmd[sg.cur];
+        // Test hook (as Device::begin's): every program after the n-th fails like a device failure.
+        static const long long fail_after =
+            getenv("TONK_AMD_FAIL_AFTER_PROGRAMS") ? atoll(getenv("TONK_AMD_FAIL_AFTER_PROGRAMS")) : -1;
+        if (fail_after >= 0 && !ctx.pb.empty() && (long long)g_programs.load() >= fail_after) {
+            ctx.finish_flush();
+            return false;
+        }
+        if (Server::build(b, ups, &ctx.pb, reads)) {
+            sg.descs.clear();
+            sg.used = 0;
+            g_srv->post(b);
+            g_programs.fetch_add(ctx.pb.empty() ? 0 : 1, std::memory_order_relaxed);
+            const uint64_t done = ctx.epoch;
+            ctx.finish_flush();
+            const int64_t w0 = now_ns();
+            const bool ok = g_srv->wait(b);
+            g_waits.fetch_add(1, std::memory_order_relaxed);
+            g_wait_ns.fetch_add((uint64_t)(now_ns() - w0), std::memory_order_relaxed);
+            if (g_watch) g_prepare_ns.fetch_add((uint64_t)(t1 - t0), std::memory_order_relaxed);
+            ctx.rows.release_up_to(done);
+            return ok;
+        }
+        c.used_launch = true;
+    }
     void* ev = nullptr;
     BatchDone* batch = nullptr;
     bool ok = true;
     if (capi_combine()) {
-        const std::function<void(Device&)> f(enqueue_reads);
         RunReq req;
         req.c = &c;
-        req.reads = &f;
+        req.reads = &reads;
         {
             const unsigned st = c.staging.stream;
             RunQueue& rq = g_run[st];
@@ -543,7 +617,7 @@ bool run_and_read(Codec& c, Reads enqueue_reads) {
             g_programs.fetch_add(1, std::memory_order_relaxed);
             g_launches.fetch_add(dev.stats().launches - launches, std::memory_order_relaxed);
         }
-        enqueue_reads(dev);
+        for (const Device::HostCopy& x : reads) dev.download_pinned(x.host, x.arena_off, x.len);
         ev = dev.record_event();
         ok = !dev.failed();
     }
@@ -654,6 +728,30 @@ SIAMESE_EXPORT int siamese_init_(int version) {
     if (nstreams > 1) g_rt->dev.add_streams(nstreams);
     g_rt->dev.warm_streams();
     g_rt->ok = true;
+    // The launch-free path (TONK_AMD_SERVE=0: kernel launches for every call): the persistent
+    // executor on TONK_AMD_SERVE_WORKERS CUs (default 64), ending after TONK_AMD_SERVE_IDLE_MS
+    // (default 50) without a command and relaunched on demand.
+    if (!(getenv("TONK_AMD_SERVE") && atoi(getenv("TONK_AMD_SERVE")) == 0)) {
+        unsigned workers = 64;
+        double idle_ms = 50;
+        if (const char* a = getenv("TONK_AMD_SERVE_WORKERS")) workers = (unsigned)atoi(a);
+        if (const char* a = getenv("TONK_AMD_SERVE_IDLE_MS")) idle_ms = atof(a);
+        Server* srv = new Server();
+        if (srv->init(g_rt->dev, workers, 4096, idle_ms)) {
+            // the launch streams must not queue behind the resident kernel (a shared hardware
+            // queue): each completes an empty kernel while it runs
+            const double worst = g_rt->dev.probe_streams();
+            if (worst > 20.0) {
+                fprintf(stderr, "tonk_amd: launch streams wait %.1f ms behind the persistent executor; using kernel launches\n", worst);
+                srv->stop();
+            } else {
+                g_srv = srv;
+                atexit([] { if (g_srv) g_srv->stop(); });
+            }
+        } else {
+            srv->stop();
+        }
+    }
     if (const char* w = getenv("TONK_AMD_CAPI_WATCH")) {
         const double period = atof(w) > 0 ? atof(w) : 5.0;
         g_watch = true;
@@ -790,8 +888,11 @@ SIAMESE_EXPORT SiameseResult siamese_encode(SiameseEncoder encoder_t, SiameseRec
     const uint32_t total = out.total();
     bool ok = e->ensure_pinned(total);
     // the program and the read of the recovery row behind it, waited for without a lock
-    if (ok)
-        ok = run_and_read(*e, [&](Device& dev) { dev.download_pinned(e->pinned, e->byte_offset(out.row), total); });
+    if (ok) {
+        thread_local std::vector<Device::HostCopy> rd;
+        rd.assign(1, Device::HostCopy{e->pinned, e->byte_offset(out.row), total});
+        ok = run_and_read(*e, rd);
+    }
     e->ctx.rows.free_deferred(out.row);  // released once the codec's next program completes
     if (!ok) {
         DISABLE(e->enc);
@@ -889,9 +990,11 @@ bool read_back(CDecoder& d, const std::vector<std::pair<StoredOriginal*, RowId>>
         total += (upper[i] + 63) & ~(size_t)63;
     }
     if (!d.ensure_pinned(total ? total : 64)) return false;
-    const bool ok = run_and_read(d, [&](Device& dev) {
-        for (size_t i = 0; i < rows.size(); ++i) dev.download_pinned(d.pinned + at[i], d.byte_offset(rows[i].second), upper[i]);
-    });
+    thread_local std::vector<Device::HostCopy> rd;
+    rd.clear();
+    for (size_t i = 0; i < rows.size(); ++i)
+        rd.push_back(Device::HostCopy{d.pinned + at[i], d.byte_offset(rows[i].second), upper[i]});
+    const bool ok = run_and_read(d, rd);
     if (!ok) return false;
     for (size_t i = 0; i < rows.size(); ++i) {
         StoredOriginal* o = rows[i].first;

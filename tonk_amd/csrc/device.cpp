@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
+#include <algorithm>
 #include <chrono>
 #include <unordered_map>
 #include <thread>
@@ -180,6 +181,23 @@ void Device::warm_streams() {
         HIPCHK(hipMalloc((void**)&sc_dev_, land));
         sc_cap_ = land;
     }
+}
+
+double Device::probe_streams() {
+    std::vector<void*> all = streams_;
+    if (all.empty()) all.push_back(stream_);
+    const auto t0 = std::chrono::steady_clock::now();
+    auto ms = [&] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
+    for (void* s : all) hipLaunchKernelGGL(tamd_nop, dim3(1), dim3(64), 0, (hipStream_t)s);
+    double worst = 0;
+    for (void* s : all) {
+        while (hipStreamQuery((hipStream_t)s) == hipErrorNotReady) {
+            if (ms() > 2000.0) return ms();
+            std::this_thread::sleep_for(std::chrono::microseconds(50));
+        }
+        worst = std::max(worst, ms());
+    }
+    return worst;
 }
 
 void Device::sync_all_streams() {
@@ -1261,7 +1279,9 @@ std::vector<void*> g_spare_slabs;  // mapped and warmed ahead (host_prefill)
 void* new_slab() {
     void* p = nullptr;
     const auto t0 = std::chrono::steady_clock::now();
-    if (hipHostMalloc(&p, kPinSlab, hipHostMallocDefault) != hipSuccess) return nullptr;
+    // (coherent: the persistent executor reads staged packets and commands, and writes results and
+    // completion words, while the host works on the same pages -- server.h)
+    if (hipHostMalloc(&p, kPinSlab, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return nullptr;
     static uint8_t* d = nullptr;
     if (!d && hipMalloc((void**)&d, 4096) != hipSuccess) d = nullptr;
     if (d) {
@@ -1322,7 +1342,7 @@ void* Device::host_alloc(size_t n) {
     if (sz > kPinSlab / 4) {  // (large blocks: their own allocation)
         void* p = nullptr;
         const auto t0 = std::chrono::steady_clock::now();
-        if (hipHostMalloc(&p, sz, hipHostMallocDefault) != hipSuccess) return nullptr;
+        if (hipHostMalloc(&p, sz, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return nullptr;
         report_slow("pinned allocation", t0, sz >> 10, 0);
         std::lock_guard<std::mutex> g(g_pin_mu);
         g_pin_class[p] = c;

@@ -72,6 +72,11 @@ public:
     // per thread, and events, streams and allocations of a call belong to the current one.
     void bind_thread() const;
     uint8_t* arena() const { return arena_; }
+    const uint32_t* gf_tables() const { return d_gf_; }  // the executor's LDS table image (kernels.hip)
+    const uint8_t* zero_row() const { return d_zero_; }
+    // An empty kernel on every launch stream; returns the longest any took to complete (ms,
+    // capped near 2000): a stream that shares a hardware queue with a resident kernel waits.
+    double probe_streams();
     void* stream() const { return stream_; }
     // Several launch streams (the C ABI): add_streams(k) creates k - 1 more streams beside the
     // first; select_stream(i) makes stream i the one every following enqueue uses (the caller

@@ -1004,6 +1004,11 @@ Result Encoder::encode(RecoveryOut& out) {
         pb.begin_op();
         add_dense_direct(row, recovery_bytes, pairs_);
         pb.finish_combine(out.row, recovery_bytes, out.footer, out.footer_len);
+        if (disabled_) {  // a partial sum found no arena room: the row lacks dense runs, never emit it
+            ctx_->rows.free_deferred(out.row);
+            out = RecoveryOut();
+            return kDisabled;
+        }
         stats_[2]++;
         stats_[3] += out.total();
         return kSuccess;

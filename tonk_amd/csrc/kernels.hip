@@ -11,6 +11,7 @@
 #include <stdint.h>
 
 #include "program.h"
+#include "serve.h"
 
 #define TAMD_WAVES_PER_WG 4
 #ifndef TAMD_BITOP3
@@ -38,6 +39,24 @@ __device__ __forceinline__ u64 byte_mask(uint32_t nbytes) {  // low `nbytes` byt
 __device__ __forceinline__ uint32_t uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t lane) { return __builtin_amdgcn_readlane(v, lane); }
 __device__ __forceinline__ u64 ballot(bool p) { return __builtin_amdgcn_uicmp((uint32_t)p, 0u, 33 /*ne*/); }
+
+// An instruction word of the op's list.  LDSI: the list sits in LDS (the persistent C-ABI
+// executor, tamd_serve, copies each command's program there); its fields are wave uniform, so
+// they move to SGPRs and every row address keeps its scalar base.  Otherwise a scalar load.
+template <bool LDSI>
+__device__ __forceinline__ tamd_instr fetch_instr(const tamd_instr* __restrict__ p, uint32_t i) {
+    if constexpr (!LDSI) {
+        return p[i];
+    } else {
+        const uint4 v = *(const uint4*)(p + i);
+        tamd_instr r;
+        r.w0 = uniform(v.x);
+        r.row = uniform(v.y);
+        r.len = uniform(v.z);
+        r.cap = uniform(v.w);
+        return r;
+    }
+}
 
 // A wave-uniform value moved into a VGPR: LDS addresses built from it need no v_readfirstlane /
 // v_mov round trip.
@@ -255,7 +274,7 @@ __device__ __forceinline__ void lv_store_row(uint8_t* __restrict__ arena, uint32
 // Batches of rows are numbered across the op (`unit`); with nw > 1 waves sharing the op, a
 // wave combines only the batches with unit mod nw == wid (the coefficient stepping still walks
 // every row).
-template <bool FULL, int NH, uint32_t TAMD_RBATCH>
+template <bool FULL, int NH, uint32_t TAMD_RBATCH, bool LDSI = false>
 __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& r, const tamd_instr& tg,
                                          const tamd_instr* __restrict__ adj, uint32_t o, uint32_t ox,
                                          const uint8_t* __restrict__ arena, const uint32_t* __restrict__ lds,
@@ -416,7 +435,7 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
                 const uint32_t base = i & ~63u, mine = base + lane;
                 uint32_t g = coef((col0 + mine * cstep) & (TAMD_COLUMN_PERIOD - 1u));
                 for (; acur < nadj; ++acur) {
-                    const uint32_t d = adw[acur];
+                    const uint32_t d = LDSI ? uniform(adw[acur]) : adw[acur];
                     if ((d >> 16) >= base + 64u) break;
                     if ((d >> 16) == mine) g ^= (d >> 8) & 0xffu;
                 }
@@ -554,7 +573,7 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
 // Shared ops (nw = 4, the class-0 pure combines): every wave walks the instruction list, combines
 // only its share of the row batches and skips the final STORE; the caller reduces the waves'
 // acc_0 through LDS and stores.  Returns acc_0.
-template <bool FULL, int NH, uint32_t TAMD_BATCH>
+template <bool FULL, int NH, uint32_t TAMD_BATCH, bool LDSI = false>
 __device__ __forceinline__ LV<NH> run_item(const tamd_instr* __restrict__ instrs, uint32_t first, uint32_t end,
                                            uint32_t o, uint32_t ox, uint32_t laneb, uint8_t* __restrict__ arena,
                                            const uint8_t* __restrict__ zrow, const uint32_t* __restrict__ lds,
@@ -564,7 +583,7 @@ __device__ __forceinline__ LV<NH> run_item(const tamd_instr* __restrict__ instrs
     for (uint32_t k = first; k < end;) {
         tamd_instr in[TAMD_BATCH];
 #pragma unroll
-        for (uint32_t j = 0; j < TAMD_BATCH; ++j) in[j] = instrs[k + j];  // region padded by 64 words
+        for (uint32_t j = 0; j < TAMD_BATCH; ++j) in[j] = fetch_instr<LDSI>(instrs, k + j);  // region padded
         // A batch runs up to (not including) the next ACCR; an ACCR at the head runs alone.
         uint32_t nb = end - k < TAMD_BATCH ? end - k : TAMD_BATCH;
 #pragma unroll
@@ -573,7 +592,7 @@ __device__ __forceinline__ LV<NH> run_item(const tamd_instr* __restrict__ instrs
         if (nb == 0) {
             // in[1]: the RANGE word, in[2]: TARGETS (MULTI runs) or COEFS (DENSE runs, followed by
             // COEFS.cap ADJ words)
-            run_accr<FULL, NH, TAMD_BATCH>(in[0], in[1], in[2], instrs + k + 3, o, ox, arena, lds, unit, nw, wid, a0,
+            run_accr<FULL, NH, TAMD_BATCH, LDSI>(in[0], in[1], in[2], instrs + k + 3, o, ox, arena, lds, unit, nw, wid, a0,
                                            a1, a2);
             const uint32_t rmode = (in[0].w0 >> 8) & 0xffu;
             k += rmode == TAMD_R_DENSE ? 3u + in[2].cap : rmode == TAMD_R_MULTI ? 3u : 2u;
@@ -624,7 +643,7 @@ __device__ __forceinline__ LV<NH> run_item(const tamd_instr* __restrict__ instrs
                     lv_store<NH>(arena + (size_t)in[j].row * TAMD_ROW_UNIT + o, x);
                 } else {
                     // the FOOTER word follows the STORE (possibly past this batch)
-                    const tamd_instr f = instrs[k + j + 1];
+                    const tamd_instr f = fetch_instr<LDSI>(instrs, k + j + 1);
                     lv_store_row<FULL, NH>(arena, in[j].row, in[j].len, in[j].cap, ((u64)f.len << 32) | f.row, o, x, ox);
                 }
             } else if (kind == TAMD_I_CLEAR) {
@@ -770,6 +789,251 @@ TAMD_EXEC_KERNEL(tamd_exec16, 2, 6)
 // tamd_exec24: 1536-byte slices (16 + 8 B per lane), so a 1302-byte packet row is one work item
 // (program.h TAMD_SLICE_BYTES_X; chosen by Device::init, tonk_amd::slice_bytes()).
 TAMD_EXEC_KERNEL(tamd_exec24, 3, 5)
+
+
+// ---------------------------------------------------------------------------------------------
+// tamd_serve: the persistent executor of the siamese.h C ABI (serve.h; host side serve.cpp).
+// Block 0 is the dispatcher: one lane polls the host ring in order and publishes each command in
+// the device work list.  Every other block is a worker (16 waves, one per CU): it claims the next
+// work-list index, waits for it, and runs the command -- copy it into LDS, land its packets in
+// the arena, run the program's levels (waves claim items through an LDS counter; a workgroup
+// barrier between levels: an op only reads rows of lower levels), write the reads to the host
+// and store the completion word.  Memory: the worker's system-scope acquire at the start of a
+// command (this CU's L1, and host data the L2 may hold) and release at its end (the XCD's L2
+// written back before the completion word) make a codec's rows visible to its next command on
+// any CU or XCD, and to the ordinary executor launches.  The dispatcher ends after
+// `idle_ticks` without a command (or when the host sets `stop`); the workers drain every
+// published command and end too, so the grid always empties; the host relaunches on demand.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ u64 ld_sys(const uint64_t* p) {
+    return __hip_atomic_load((uint64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_sys(uint64_t* p, u64 v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ u64 ld_agent(const uint64_t* p) {
+    return __hip_atomic_load((uint64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Copy `len` bytes between host memory (16-B aligned) and an arena row, one wave: 16 B per lane
+// per chunk, four chunks in flight per lane, the tail (len mod 16) byte by byte.
+template <bool TO_HOST>
+__device__ __forceinline__ void serve_xfer(uint8_t* __restrict__ arena, u64 host, uint32_t unit, uint32_t len,
+                                           uint32_t lane) {
+    uint8_t* a = arena + (size_t)unit * TAMD_ROW_UNIT;
+    uint8_t* h = (uint8_t*)host;
+    const uint8_t* src = TO_HOST ? a : h;
+    uint8_t* dst = TO_HOST ? h : a;
+    const uint32_t n16 = len >> 4;
+    // (every lane loads -- a clamped chunk when past the end -- and only in-range lanes store:
+    // four loads in flight, no exec-masked loads, no private array)
+    for (uint32_t b = 0; b < n16; b += 256u) {
+        const uint32_t c0 = b + lane, c1 = c0 + 64u, c2 = c0 + 128u, c3 = c0 + 192u, m = n16 - 1u;
+        const uint4 v0 = *(const uint4*)(src + 16u * min(c0, m));
+        const uint4 v1 = *(const uint4*)(src + 16u * min(c1, m));
+        const uint4 v2 = *(const uint4*)(src + 16u * min(c2, m));
+        const uint4 v3 = *(const uint4*)(src + 16u * min(c3, m));
+        if (c0 < n16) *(uint4*)(dst + 16u * c0) = v0;
+        if (c1 < n16) *(uint4*)(dst + 16u * c1) = v1;
+        if (c2 < n16) *(uint4*)(dst + 16u * c2) = v2;
+        if (c3 < n16) *(uint4*)(dst + 16u * c3) = v3;
+    }
+    const uint32_t tail = len & 15u;
+    if (lane < tail) dst[16u * n16 + lane] = src[16u * n16 + lane];
+}
+
+__device__ __forceinline__ tamd_xfer lds_xfer(const uint8_t* base, uint32_t i) {
+    const uint4 v = ((const uint4*)base)[i];
+    tamd_xfer x;
+    x.host = ((u64)uniform(v.y) << 32) | uniform(v.x);
+    x.unit = uniform(v.z);
+    x.len = uniform(v.w);
+    return x;
+}
+
+extern "C" __global__ void __launch_bounds__(TAMD_SERVE_THREADS) tamd_serve(const tamd_serve_args a) {
+    uint64_t* ready = (uint64_t*)(a.dev + 1);
+    tamd_serve_entry* wl = (tamd_serve_entry*)(ready + a.wl_mask + 1);
+    if (blockIdx.x == 0) {
+        // ---- the dispatcher: one lane ----
+        if (threadIdx.x != 0) return;
+        u64 t = a.tail0;
+        u64 last = __builtin_amdgcn_s_memrealtime();
+        st_sys(&a.host->dbg[0], last);
+        for (uint32_t polls = 0;; ++polls) {
+            if ((polls & 1023u) == 0) {
+                st_sys(&a.host->dbg[1], polls >> 10);
+                st_sys(&a.host->dbg[2], t);
+            }
+            const tamd_serve_slot* s = a.ring + (t & a.ring_mask);
+            if (ld_sys(&s->seq) == t + 1) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the slot's fields after its seq
+                tamd_serve_entry e;
+                e.cmd = ld_sys(&s->cmd);
+                e.done = ld_sys(&s->done);
+                e.done_val = ld_sys(&s->done_val);
+                e.cmd_bytes = (uint32_t)ld_sys((const uint64_t*)&s->cmd_bytes);
+                e.pad = 0;
+                wl[t & a.wl_mask] = e;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                vm_drain();
+                __hip_atomic_store(&ready[t & a.wl_mask], t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ++t;
+                st_sys(&a.host->consumed, t);
+                last = __builtin_amdgcn_s_memrealtime();
+                continue;
+            }
+            if (__builtin_amdgcn_s_memrealtime() - last > a.idle_ticks || ld_sys(&a.host->stop)) break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+        // End: the workers drain what was published, then end; the host learns where the next
+        // instance starts (exit_tail) before it learns that this one ended (exited_gen).
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        vm_drain();
+        __hip_atomic_store(&a.dev->quit, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        st_sys(&a.host->exit_tail, t);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        vm_drain();
+        st_sys(&a.host->exited_gen, a.gen);
+        return;
+    }
+
+    // ---- a worker ----
+    constexpr int NH = 3;
+    constexpr uint32_t SLICE = 64u * 8u * NH, MAIN = 1024u;
+    __shared__ __attribute__((aligned(16))) uint32_t lds_perm[TAMD_GF_DWORDS];
+    __shared__ __attribute__((aligned(16))) uint4 cbuf[TAMD_SERVE_CMD_BYTES / 16];
+    __shared__ tamd_serve_entry sh_e;
+    __shared__ uint32_t sh_state, sh_item;
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = uniform(tid >> 6);
+    for (uint32_t i = tid; i < TAMD_GF_DWORDS / 4; i += TAMD_SERVE_THREADS)
+        ((uint4*)lds_perm)[i] = ((const uint4*)a.gf)[i];
+    const uint32_t laneb = lane * 16u, laneb_x = MAIN + lane * 8u;
+    const uint8_t* cb = (const uint8_t*)cbuf;
+    // Lane 0 of wave 0 completes the previous command (its completion words) and claims the next
+    // one in ONE divergent region at the top of the loop, right before the barrier: a divergent
+    // region at the end of the body, before the back edge, was rotated by the compiler so that
+    // the other lanes of wave 0 looped through the barrier without lane 0 (a hang).
+    u64 prev_done = 0, prev_val = 0, prev_start = 0;
+    uint32_t prev_dbg = 0;
+    for (;;) {
+        if (tid == 0) {
+            if (prev_done) {
+                uint64_t* done = (uint64_t*)prev_done;
+                st_sys(done + 1, prev_start);
+                st_sys(done + 2, __builtin_amdgcn_s_memrealtime());
+                // everything the command wrote -- its rows, for the next command on any CU or XCD;
+                // its reads, for the host -- before its completion word
+                if (!(a.pad & 2u)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+                vm_drain();
+                st_sys(done, prev_val);
+                if (prev_dbg) st_sys(&a.host->dbg[3], 7);
+                prev_done = 0;
+            }
+            const u64 k = __hip_atomic_fetch_add(&a.dev->claim, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const u64 idx = a.tail0 + k;
+            const uint64_t* rp = &ready[idx & a.wl_mask];
+            if (idx == 0) {  // (diagnostics: the first command, the server's start-up probe)
+                st_sys(&a.host->dbg[3], 1);
+                st_sys(&a.host->dbg[4], blockIdx.x);
+            }
+            uint32_t st = 0;
+            for (;;) {
+                if (ld_agent(rp) == idx + 1) { st = 1; break; }
+                if (ld_agent(&a.dev->quit)) {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+                    st = ld_agent(rp) == idx + 1;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            if (st) {
+                // this CU's L1 and the host data the L2 may hold are refreshed before any load of
+                // the command, its packets or the codec's rows
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+                const tamd_serve_entry e = wl[idx & a.wl_mask];
+                sh_e = e;
+                prev_done = e.done;
+                prev_val = e.done_val;
+                prev_start = __builtin_amdgcn_s_memrealtime();
+                prev_dbg = idx == 0;
+            }
+            sh_state = st ? (idx == 0 ? 2u : 1u) : 0u;
+        }
+        __syncthreads();
+        // (read through readfirstlane: a loop exit the compiler sees as divergent would put the
+        // workgroup barriers below under divergent control flow)
+        const uint32_t state = uniform(sh_state);
+        if (!state) break;
+        const bool dbg = state == 2u && tid == 0;
+        if (dbg) st_sys(&a.host->dbg[3], 2);
+        const u64 cmd_addr = ((u64)uniform((uint32_t)(sh_e.cmd >> 32)) << 32) | uniform((uint32_t)sh_e.cmd);
+        const uint32_t cmd_bytes = uniform(sh_e.cmd_bytes);
+        // 1. the command into LDS
+        {
+            const uint32_t n16 = (cmd_bytes + 15u) >> 4, m = n16 - 1u;
+            const uint4* src = (const uint4*)cmd_addr;
+            constexpr uint32_t T = TAMD_SERVE_THREADS;
+            for (uint32_t b = tid; b < n16; b += 4u * T) {
+                const uint4 v0 = src[min(b, m)], v1 = src[min(b + T, m)], v2 = src[min(b + 2u * T, m)],
+                            v3 = src[min(b + 3u * T, m)];
+                cbuf[b] = v0;
+                if (b + T < n16) cbuf[b + T] = v1;
+                if (b + 2u * T < n16) cbuf[b + 2u * T] = v2;
+                if (b + 3u * T < n16) cbuf[b + 3u * T] = v3;
+            }
+        }
+        __syncthreads();
+        if (dbg) st_sys(&a.host->dbg[3], 3);
+        const tamd_cmd* c = (const tamd_cmd*)cb;
+        const uint32_t n_up = uniform(c->n_up), n_rd = uniform(c->n_rd), levels = uniform(c->levels);
+        // 2. packets staged since the codec's last program land in their rows
+        for (uint32_t u = wave; u < n_up; u += TAMD_SERVE_WAVES) {
+            const tamd_xfer x = lds_xfer(cb + uniform(c->off_up), u);
+            serve_xfer<false>(a.arena, x.host, x.unit, x.len, lane);
+        }
+        vm_drain();
+        __syncthreads();
+        if (dbg) st_sys(&a.host->dbg[3], 4);
+        // 3. the program, level by level
+        const tamd_instr* ins = (const tamd_instr*)(cb + uniform(c->off_instr));
+        const uint4* ops = (const uint4*)(cb + uniform(c->off_ops));
+        const uint2* items = (const uint2*)(cb + uniform(c->off_items));
+        for (uint32_t l = 0; l < levels; ++l) {
+            const uint32_t b1 = uniform(c->level_base[l + 1]);
+            if (tid == 0) sh_item = c->level_base[l];
+            __syncthreads();
+            for (;;) {
+                uint32_t it = 0;
+                if (lane == 0) it = atomicAdd(&sh_item, 1u);
+                it = uniform(rdl(it, 0));
+                if (it >= b1) break;
+                const uint2 item = items[it];
+                const uint4 op = ops[uniform(item.x)];
+                const uint32_t s0 = uniform(item.y) * SLICE;
+                const uint32_t o = s0 + laneb, ox = s0 + laneb_x;
+                const uint32_t first = uniform(op.x), end = first + uniform(op.y);
+                if (s0 + MAIN <= uniform(op.w))
+                    run_item<true, NH, 5, true>(ins, first, end, o, ox, laneb, a.arena, a.zrow, lds_perm, 1u, 0u);
+                else
+                    run_item<false, NH, 5, true>(ins, first, end, o, ox, laneb, a.arena, a.zrow, lds_perm, 1u, 0u);
+            }
+            vm_drain();
+            __syncthreads();
+        }
+        if (dbg) st_sys(&a.host->dbg[3], 5);
+        // 4. the reads into the caller's pinned buffer
+        for (uint32_t r = wave; r < n_rd; r += TAMD_SERVE_WAVES) {
+            const tamd_xfer x = lds_xfer(cb + uniform(c->off_rd), r);
+            serve_xfer<true>(a.arena, x.host, x.unit, x.len, lane);
+        }
+        vm_drain();
+        __syncthreads();
+        if (dbg) st_sys(&a.host->dbg[3], 6);
+        // 5. completion: at the top of the next iteration (lane 0 of wave 0)
+    }
+}
 
 // GF self test: out[y * 256 + x] = x * y through the same v_perm path the executor uses.
 extern "C" __global__ void tamd_gf_selftest(const uint32_t* __restrict__ gf_perm, uint8_t* __restrict__ out) {

@@ -1,0 +1,277 @@
+// server.cpp -- host side of the launch-free submission path (server.h, serve.h).
+#include "server.h"
+
+#include <hip/hip_runtime.h>
+#include <chrono>
+#include <sched.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <thread>
+#include <immintrin.h>
+
+extern "C" __global__ void tamd_serve(const tamd_serve_args);
+
+namespace tamd {
+
+namespace {
+double now_us() {
+    return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+void* coherent_alloc(size_t n) {
+    void* p = nullptr;
+    if (hipHostMalloc(&p, n, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return nullptr;
+    memset(p, 0, n);
+    return p;
+}
+}  // namespace
+
+bool Server::init(Device& dev, unsigned workers, unsigned ring_size, double idle_ms) {
+    dev_ = &dev;
+    dev.bind_thread();
+    ring_size_ = 1;
+    while (ring_size_ < ring_size) ring_size_ <<= 1;
+    workers_ = workers ? workers : 1;
+    idle_ticks_ = (uint64_t)(idle_ms * 1e5);  // s_memrealtime: 100 MHz
+    if (const char* e = getenv("TONK_AMD_SERVE_DEBUG")) debug_ = (uint32_t)atoi(e);
+    ring_ = (tamd_serve_slot*)coherent_alloc((size_t)ring_size_ * sizeof(tamd_serve_slot));
+    host_ = (volatile tamd_serve_host*)coherent_alloc(sizeof(tamd_serve_host));
+    if (!ring_ || !host_) return false;
+    const size_t dbytes = sizeof(tamd_serve_dev) + (size_t)ring_size_ * (8 + sizeof(tamd_serve_entry));
+    if (hipMalloc((void**)&dstate_, dbytes) != hipSuccess) return false;
+    int least = 0, greatest = 0;
+    hipDeviceGetStreamPriorityRange(&least, &greatest);
+    hipStream_t st = nullptr;
+    if (hipStreamCreateWithPriority(&st, hipStreamNonBlocking, greatest) != hipSuccess) return false;
+    stream_ = st;
+    if (hipMemsetAsync(dstate_, 0, dbytes, st) != hipSuccess) return false;
+    {
+        std::lock_guard<std::mutex> lk(launch_mu_);
+        if (!launch_locked(0)) return false;
+    }
+    ok_ = true;
+    // An empty command through the ring must come back.
+    CmdBuf probe;
+    if (debug_ & 1u) {
+        dbg_done_ = (uint64_t*)coherent_alloc(4096);
+        probe.done_at = dbg_done_;
+    }
+    std::vector<Device::HostCopy> none;
+    if (!build(probe, none, nullptr, none)) return false;
+    post(probe);
+    const bool answered = wait(probe);
+    Device::host_free(probe.mem);
+    if (!answered) {
+        fprintf(stderr, "tonk_amd: the persistent executor did not answer; using kernel launches\n");
+        ok_ = false;
+        return false;
+    }
+    return true;
+}
+
+bool Server::launch_locked(uint64_t tail0) {
+    hipStream_t st = (hipStream_t)stream_;
+    tamd_serve_args a;
+    memset(&a, 0, sizeof(a));
+    a.ring = ring_;
+    a.host = (tamd_serve_host*)host_;
+    a.dev = dstate_;
+    a.arena = dev_->arena();
+    a.gf = dev_->gf_tables();
+    a.zrow = dev_->zero_row();
+    a.tail0 = tail0;
+    a.idle_ticks = idle_ticks_;
+    a.ring_mask = ring_size_ - 1;
+    a.wl_mask = ring_size_ - 1;
+    a.gen = gen_.load() + 1;
+    a.pad = debug_;
+    // the instance's claim counter and quit flag start from zero (stream order: after the
+    // previous instance has ended)
+    if (hipMemsetAsync(dstate_, 0, sizeof(tamd_serve_dev), st) != hipSuccess) return false;
+    hipLaunchKernelGGL(tamd_serve, dim3(1 + workers_), dim3(TAMD_SERVE_THREADS), 0, st, a);
+    if (hipGetLastError() != hipSuccess) return false;
+    gen_.store(a.gen);
+    launches.fetch_add(1, std::memory_order_relaxed);
+    return true;
+}
+
+void Server::ensure_running() {
+    std::lock_guard<std::mutex> lk(launch_mu_);
+    if (host_->exited_gen != gen_.load()) return;  // the current instance runs (or a relaunch won)
+    dev_->bind_thread();
+    const uint64_t tail = host_->exit_tail;
+    if (!launch_locked(tail)) fprintf(stderr, "tonk_amd: relaunching the persistent executor failed\n");
+}
+
+bool Server::build(CmdBuf& b, const std::vector<Device::HostCopy>& up, const ProgramBuilder* pb,
+                   const std::vector<Device::HostCopy>& rd) {
+    uint32_t levels = 0, n_items = 0, n_instr = 0, n_ops = 0, B = 0;
+    if (pb && !pb->empty()) {
+        B = (uint32_t)pb->level_ops().size();
+        B = (B + TAMD_COST_CLASSES - 1) / TAMD_COST_CLASSES * TAMD_COST_CLASSES;
+        levels = B / TAMD_COST_CLASSES;
+        for (uint32_t c : pb->level_items()) n_items += c;
+        n_instr = (uint32_t)pb->instrs().size();
+        n_ops = (uint32_t)pb->ops().size();
+    }
+    if (levels > TAMD_SERVE_MAX_LEVELS) return false;
+    for (const Device::HostCopy& x : up)
+        if (((uintptr_t)x.host & 15u) || (x.arena_off & 63u) || x.arena_off / 64 > 0xffffffffull) return false;
+    for (const Device::HostCopy& x : rd)
+        if (((uintptr_t)x.host & 15u) || (x.arena_off & 63u) || x.arena_off / 64 > 0xffffffffull) return false;
+    const uint32_t off_up = (uint32_t)((sizeof(tamd_cmd) + 15) & ~(size_t)15);
+    const uint32_t off_rd = off_up + 16u * (uint32_t)up.size();
+    const uint32_t off_instr = off_rd + 16u * (uint32_t)rd.size();
+    const uint32_t off_ops = off_instr + 16u * (n_instr + 8u);  // (the executor reads a batch past the end)
+    const uint32_t off_items = off_ops + 16u * n_ops;
+    const uint32_t bytes = (off_items + 8u * n_items + 15u) & ~15u;
+    if ((size_t)bytes + 256 > TAMD_SERVE_CMD_BYTES) return false;
+    if (CmdBuf::kHead + bytes > b.cap) {
+        Device::host_free(b.mem);
+        b.cap = 4096;
+        while (b.cap < CmdBuf::kHead + bytes) b.cap <<= 1;
+        b.mem = (uint8_t*)Device::host_alloc(b.cap);
+        if (!b.mem) {
+            b.cap = 0;
+            return false;
+        }
+        memset(b.mem, 0, CmdBuf::kHead);
+    }
+    uint8_t* base = (uint8_t*)b.cmd();
+    tamd_cmd* c = b.cmd();
+    memset(c, 0, sizeof(tamd_cmd));
+    c->bytes = bytes;
+    c->n_up = (uint32_t)up.size();
+    c->n_rd = (uint32_t)rd.size();
+    c->levels = levels;
+    c->off_up = off_up;
+    c->off_rd = off_rd;
+    c->off_instr = off_instr;
+    c->off_ops = off_ops;
+    c->off_items = off_items;
+    c->n_items = n_items;
+    c->n_instr = n_instr;
+    c->n_ops = n_ops;
+    tamd_xfer* xu = (tamd_xfer*)(base + off_up);
+    for (size_t i = 0; i < up.size(); ++i)
+        xu[i] = tamd_xfer{(uint64_t)(uintptr_t)up[i].host, (uint32_t)(up[i].arena_off / 64), up[i].len};
+    tamd_xfer* xr = (tamd_xfer*)(base + off_rd);
+    for (size_t i = 0; i < rd.size(); ++i)
+        xr[i] = tamd_xfer{(uint64_t)(uintptr_t)rd[i].host, (uint32_t)(rd[i].arena_off / 64), rd[i].len};
+    if (!levels) return true;
+    // The program as Device::begin / fill lay out one context's: ops grouped by bucket (level,
+    // then cost class, most expensive first), each op's work items (op, slice) in that order.
+    memcpy(base + off_instr, pb->instrs().data(), (size_t)n_instr * sizeof(tamd_instr));
+    memset(base + off_instr + 16u * n_instr, 0, 16u * 8u);
+    uint32_t op_fill[TAMD_SERVE_MAX_LEVELS * TAMD_COST_CLASSES], item_fill[TAMD_SERVE_MAX_LEVELS * TAMD_COST_CLASSES];
+    uint32_t op_at = 0, item_at = 0;
+    const std::vector<uint32_t>& lo = pb->level_ops();
+    const std::vector<uint32_t>& li = pb->level_items();
+    for (uint32_t k = 0; k < B; ++k) {
+        if (k % TAMD_COST_CLASSES == 0) c->level_base[k / TAMD_COST_CLASSES] = item_at;
+        op_fill[k] = op_at;
+        item_fill[k] = item_at;
+        if (k < lo.size()) {
+            op_at += lo[k];
+            item_at += li[k];
+        }
+    }
+    c->level_base[levels] = item_at;
+    tamd_op* ho = (tamd_op*)(base + off_ops);
+    uint32_t* hi = (uint32_t*)(base + off_items);
+    const std::vector<tamd_op>& ops = pb->ops();
+    const std::vector<uint32_t>& lv = pb->op_levels();
+    for (size_t i = 0; i < ops.size(); ++i) {
+        const uint32_t k = lv[i];
+        const uint32_t oi = op_fill[k]++;
+        ho[oi] = ops[i];
+        const uint32_t slices = op_slices(ops[i].span);
+        uint32_t ii = item_fill[k];
+        item_fill[k] += slices;
+        for (uint32_t s = 0; s < slices; ++s, ++ii) {
+            hi[2 * ii] = oi;
+            hi[2 * ii + 1] = s;
+        }
+    }
+    return true;
+}
+
+void Server::post(CmdBuf& b) {
+    const uint64_t idx = head_.fetch_add(1, std::memory_order_relaxed);
+    tamd_serve_slot* s = &ring_[idx & (ring_size_ - 1)];
+    // the slot's previous command (idx - ring size) must have been handed on
+    for (uint32_t spin = 0; idx >= host_->consumed + ring_size_; ++spin) {
+        if ((spin & 255) == 255) {
+            if (host_->exited_gen == gen_.load()) ensure_running();
+            sched_yield();
+        }
+        _mm_pause();
+    }
+    s->cmd = (uint64_t)(uintptr_t)b.cmd();
+    s->done = (uint64_t)(uintptr_t)b.done();
+    s->done_val = idx + 1;
+    s->cmd_bytes = b.cmd()->bytes;
+    __atomic_store_n(&s->seq, idx + 1, __ATOMIC_RELEASE);
+    b.ticket = idx;
+    b.busy = true;
+    posted.fetch_add(1, std::memory_order_relaxed);
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    if (host_->exited_gen == gen_.load()) ensure_running();
+}
+
+bool Server::wait(CmdBuf& b) {
+    const uint64_t want = b.ticket + 1;
+    volatile uint64_t* d = b.done();
+    if (*d == want) {
+        b.busy = false;
+        std::atomic_thread_fence(std::memory_order_acquire);
+        return true;
+    }
+    const double t0 = now_us();
+    for (uint32_t spin = 1;; ++spin) {
+        if (*d == want) break;
+        if ((spin & 63) == 0) {
+            const double t = now_us() - t0;
+            // the executor ended on an idle spell without taking this command: start the next one
+            if (host_->exited_gen == gen_.load() && host_->exit_tail <= b.ticket) ensure_running();
+            if (t > 3e6) {
+                fprintf(stderr, "tonk_amd: command %llu not completed after 3 s (done word %llu); dispatcher: start %llu "
+                        "polls/1024 %llu waits for %llu; command 0: stage %llu block %llu; consumed %llu exited_gen %llu "
+                        "(launched %u) exit_tail %llu\n",
+                        (unsigned long long)b.ticket, (unsigned long long)*d, (unsigned long long)host_->dbg[0],
+                        (unsigned long long)host_->dbg[1], (unsigned long long)host_->dbg[2],
+                        (unsigned long long)host_->dbg[3], (unsigned long long)host_->dbg[4],
+                        (unsigned long long)host_->consumed, (unsigned long long)host_->exited_gen, gen_.load(),
+                        (unsigned long long)host_->exit_tail);
+                return false;
+            }
+            // a short spin, then give the core to other threads between polls (a Tonk process
+            // has hundreds of threads on a few cores)
+            if (t > 30.0) {
+                if (t > 2000.0) {
+                    waits_slow.fetch_add(1, std::memory_order_relaxed);
+                    std::this_thread::sleep_for(std::chrono::microseconds(20));
+                } else {
+                    sched_yield();
+                }
+            }
+        }
+        _mm_pause();
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    b.busy = false;
+    gpu_ns_sum += (d[2] - d[1]) * 10;
+    return true;
+}
+
+void Server::stop() {
+    if (!ring_) return;
+    host_->stop = 1;
+    std::atomic_thread_fence(std::memory_order_seq_cst);
+    hipStream_t st = (hipStream_t)stream_;
+    for (int i = 0; i < 2000 && hipStreamQuery(st) == hipErrorNotReady; ++i)
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
+    ok_ = false;
+}
+
+}  // namespace tamd

@@ -1,0 +1,76 @@
+// server.h -- host side of the launch-free submission path (serve.h): the command ring, the
+// persistent executor's life cycle and the completion waits of the siamese.h C ABI.
+//
+// Calls never launch, record or wait on HIP objects: a call writes its command into its codec's
+// pinned buffer, stores the command's address into the ring (a release store of the slot's
+// sequence word) and spins on the command's completion word.  The only HIP calls left are the
+// executor's (re)launches -- at start, and after it ended on an idle spell -- made under the
+// server's own mutex, never under the device lock.
+#pragma once
+
+#include "device.h"
+#include "serve.h"
+
+#include <atomic>
+#include <mutex>
+#include <stdint.h>
+#include <vector>
+
+namespace tamd {
+
+// A codec's command buffer: [0, 128) completion words (done, start, end), then the command.
+struct CmdBuf {
+    uint8_t* mem = nullptr;
+    size_t cap = 0;
+    uint64_t ticket = 0;   // ring index of the command in flight from this buffer
+    bool busy = false;     // posted and not yet waited for
+    static const size_t kHead = 128;
+    volatile uint64_t* done_at = nullptr;  // completion words (null: the buffer's head)
+    volatile uint64_t* done() const { return done_at ? done_at : (volatile uint64_t*)mem; }
+    tamd_cmd* cmd() const { return (tamd_cmd*)(mem + kHead); }
+};
+
+class Server {
+public:
+    // Ring, control words and device state; the executor's first instance is launched on a
+    // stream of its own (high priority, non-blocking: it must not share a hardware queue with
+    // the launch streams, whose work would queue behind a resident kernel).  False: no server,
+    // the C ABI keeps its launch path.
+    bool init(Device& dev, unsigned workers, unsigned ring_size, double idle_ms);
+    bool ok() const { return ok_; }
+    // Build a command into `b` (grown as needed): `up` packets to land, the program of `pb`
+    // (may be null or empty), `rd` rows to read back.  False when it does not fit the worker's
+    // LDS (TAMD_SERVE_CMD_BYTES) or has too many levels: the caller takes the launch path.
+    static bool build(CmdBuf& b, const std::vector<Device::HostCopy>& up, const ProgramBuilder* pb,
+                      const std::vector<Device::HostCopy>& rd);
+    // Post the command in `b` (after build); wait for it.  wait() returns false on a timeout
+    // (the executor stopped answering: the codec is disabled).
+    void post(CmdBuf& b);
+    bool wait(CmdBuf& b);
+    bool settle(CmdBuf& b) { return b.busy ? wait(b) : true; }
+    void stop();  // process exit: the executor ends and the stream drains (bounded wait)
+
+    // counters for the C ABI's watchdog
+    std::atomic<uint64_t> posted{0}, launches{0}, waits_slow{0};
+    uint64_t gpu_ns_sum = 0;  // (unsynchronised: diagnostics)
+
+private:
+    bool ok_ = false;
+    Device* dev_ = nullptr;
+    void* stream_ = nullptr;
+    tamd_serve_slot* ring_ = nullptr;
+    volatile tamd_serve_host* host_ = nullptr;
+    tamd_serve_dev* dstate_ = nullptr;
+    uint32_t ring_size_ = 0, workers_ = 0;
+    uint64_t idle_ticks_ = 0;
+    std::atomic<uint64_t> head_{0};
+    std::mutex launch_mu_;
+    std::atomic<uint32_t> gen_{0};  // generation of the instance launched last
+    void ensure_running();
+    uint32_t debug_ = 0;  // TONK_AMD_SERVE_DEBUG bits (diagnostics): 1 probe's completion words in
+                          // the server's own coherent page, 2 no release fence before them
+    uint64_t* dbg_done_ = nullptr;
+    bool launch_locked(uint64_t tail0);
+};
+
+}  // namespace tamd

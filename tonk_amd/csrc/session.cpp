@@ -1273,11 +1273,16 @@ int tamd_session_generate(void* sp) {
         st.runner->pregenerate();  // the stream's loss draws (scenario generation, untimed)
         st.enc_rows.assign(n, kNoRow);
         st.dec_rows.assign(n, kNoRow);
-        d.reserve(2 * (size_t)n);
+        // (an input pool: rows for the first `pool` originals; original i reads row i mod pool)
+        // (equal payload lengths only: a pooled row's length header must be original i's)
+        const uint32_t pool = s->prm.input_pool && s->prm.input_pool < n && !s->prm.record &&
+                                      !s->prm.stage_host && st.p.payload_min == st.p.payload_max
+                                  ? s->prm.input_pool : n;
+        d.reserve(2 * (size_t)pool);
         // Each side's inputs are an array of equal slots (row_cap bytes) in packet order, so runs of
         // a window's packets sit at a fixed stride (one ACCR instruction per run).
         for (int side = 0; side < 2; ++side) {
-            for (uint32_t i = 0; i < n; ++i) {
+            for (uint32_t i = 0; i < pool; ++i) {
                 const uint32_t len = wl::payload_length(st.p, i);
                 const RowId r = st.ctx->alloc(s->row_cap);
                 if (r == kNoRow) { full = true; return; }
@@ -1290,6 +1295,8 @@ int tamd_session_generate(void* sp) {
                 g.seed = st.p.seed_data;
                 d.push_back(g);
             }
+            std::vector<RowId>& rows = side ? st.dec_rows : st.enc_rows;
+            for (uint32_t i = pool; i < n; ++i) rows[i] = rows[i - pool];
         }
     });
     if (full) { s->error = "arena too small for the session inputs"; return -1; }
