@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <chrono>
 #include <dlfcn.h>
+#include <sys/resource.h>
 #include <functional>
 #include <thread>
 #include <atomic>
@@ -55,6 +56,17 @@ static inline uint64_t now_ns() {
     return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
                std::chrono::steady_clock::now().time_since_epoch()).count();
 }
+// `prof=1` (time mode): nanoseconds spent in each kind of siamese.h call, summed per thread, and
+// each thread's busy time -- where a pass's time goes (diagnostics; adds two clock reads per call).
+enum { P_ADD, P_ENCODE, P_EACK, P_DADD, P_DREC, P_READY, P_DECODE, P_DACK, P_N };
+static bool g_prof = false;
+static thread_local uint64_t* g_profv = nullptr;
+struct ProfScope {
+    int k;
+    uint64_t t0;
+    explicit ProfScope(int kind) : k(kind), t0(g_profv ? now_ns() : 0) {}
+    ~ProfScope() { if (g_profv) g_profv[k] += now_ns() - t0; }
+};
 
 struct RefBackend {
     struct RecRef { std::vector<uint8_t> bytes; };
@@ -105,6 +117,7 @@ struct RefBackend {
         o.PacketNum = 0;
         o.Data = pay(index);
         o.DataBytes = len;
+        ProfScope ps(P_ADD);
         const int rc = siamese_encoder_add(enc, &o);
         *col = o.PacketNum;
         return rc;
@@ -114,12 +127,14 @@ struct RefBackend {
         rp.Data = nullptr;
         rp.DataBytes = 0;
         const uint64_t t0 = g_latlog ? now_ns() : 0;
+        ProfScope ps(P_ENCODE);
         const int rc = siamese_encode(enc, &rp);
         if (g_latlog) g_latlog->enc_ns.push_back((uint32_t)std::min<uint64_t>(now_ns() - t0, 0xffffffffu));
         if (rc == 0) r.bytes.assign(rp.Data, rp.Data + rp.DataBytes);
         return rc;
     }
     int enc_ack(const uint8_t* buf, uint32_t n, uint32_t* next) {
+        ProfScope ps(P_EACK);
         return siamese_encoder_ack(enc, buf, n, next);
     }
     int dec_add_original(uint32_t col, uint32_t index, uint32_t len) {
@@ -127,20 +142,26 @@ struct RefBackend {
         o.PacketNum = col;
         o.Data = pay(index);
         o.DataBytes = len;
+        ProfScope ps(P_DADD);
         return siamese_decoder_add_original(dec, &o);
     }
     int dec_add_recovery(const RecRef& r) {
         SiameseRecoveryPacket rp;
         rp.Data = r.bytes.data();
         rp.DataBytes = (unsigned)r.bytes.size();
+        ProfScope ps(P_DREC);
         return siamese_decoder_add_recovery(dec, &rp);
     }
     void recovery_lost(const RecRef&) {}
-    int dec_is_ready() { return siamese_decoder_is_ready(dec); }
+    int dec_is_ready() {
+        ProfScope ps(P_READY);
+        return siamese_decoder_is_ready(dec);
+    }
     int dec_decode(std::vector<uint32_t>& nums, DecRef& out) {
         SiameseOriginalPacket* pk = nullptr;
         unsigned count = 0;
         const uint64_t t0 = g_latlog ? now_ns() : 0;
+        ProfScope ps(P_DECODE);
         const int rc = siamese_decode(dec, &pk, &count);
         if (g_latlog) g_latlog->dec_ns.push_back((uint32_t)std::min<uint64_t>(now_ns() - t0, 0xffffffffu));
         if (rc == 0) {
@@ -156,6 +177,7 @@ struct RefBackend {
         return rc;
     }
     int dec_ack(uint8_t* buf, uint32_t limit, uint32_t* used) {
+        ProfScope ps(P_DACK);
         return siamese_decoder_ack(dec, buf, limit, used);
     }
     // the reference is always driven one call at a time
@@ -248,6 +270,7 @@ static bool parse_kv(Params& p, int& threads, int& streams, int& reps, const cha
     const unsigned long long v = strtoull(eq + 1, nullptr, 0);
     if (k == "pool") g_pool = (uint32_t)v;
     else if (k == "lat") g_lat = v != 0;
+    else if (k == "prof") g_prof = v != 0;
     else if (k == "runs") g_runs = (int)v;
     else if (k == "threads") threads = (int)v;
     else if (k == "streams") streams = (int)v;
@@ -338,12 +361,17 @@ int main(int argc, char** argv) {
     RefTranscript quiet;
     quiet.enabled = false;
     // setup on the worker threads too (the payload pools are the bulk of it)
+    // (prof=1: each thread's first and last stream start / end, ns after the pass started)
+    std::vector<uint64_t> th_first(threads), th_end(threads);
+    uint64_t pass_t0 = 0;
     auto parallel = [&](const std::function<void(int)>& f) {
         std::atomic<int> at{0};
         std::vector<std::thread> pool;
         for (int t = 0; t < threads; ++t)
-            pool.emplace_back([&]() {
+            pool.emplace_back([&, t]() {
+                th_first[t] = now_ns() - pass_t0;
                 for (int s; (s = at++) < streams;) f(s);
+                th_end[t] = now_ns() - pass_t0;
             });
         for (auto& th : pool) th.join();
     };
@@ -364,9 +392,15 @@ int main(int argc, char** argv) {
         });
         std::atomic<unsigned long long> bytes{0};
         std::vector<LatLog> logs(streams);
+        std::vector<std::vector<uint64_t>> prof(streams, std::vector<uint64_t>(P_N + 1, 0));
+        struct rusage ru0, ru1;
+        getrusage(RUSAGE_SELF, &ru0);
+        pass_t0 = now_ns();
         const auto t0 = std::chrono::steady_clock::now();
         parallel([&](int s) {
             if (g_lat) g_latlog = &logs[s];
+            if (g_prof) g_profv = prof[s].data();
+            const uint64_t s0 = g_prof ? now_ns() : 0;
             unsigned long long b = 0;
             for (uint32_t i = 0; i < ps[s].n_originals; ++i) b += bes[s]->len_of(i);
             for (int r = 0; r < reps; ++r) {
@@ -375,6 +409,8 @@ int main(int argc, char** argv) {
                 bytes += b;
             }
             g_latlog = nullptr;
+            if (g_prof) prof[s][P_N] += now_ns() - s0;
+            g_profv = nullptr;
         });
         const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
         for (int s = 0; s < streams; ++s) bad += bes[s]->bad_recoveries;
@@ -397,6 +433,45 @@ int main(int argc, char** argv) {
                 return std::string(b);
             };
             lat = ", \"encode_us\": " + pct(true) + ", \"decode_us\": " + pct(false);
+        }
+        if (g_prof) {
+            getrusage(RUSAGE_SELF, &ru1);
+            char rb[256];
+            snprintf(rb, sizeof(rb), ", \"rusage\": {\"minflt\": %ld, \"majflt\": %ld, \"nvcsw\": %ld, \"nivcsw\": %ld, "
+                     "\"utime_s\": %.3f, \"stime_s\": %.3f}", ru1.ru_minflt - ru0.ru_minflt, ru1.ru_majflt - ru0.ru_majflt,
+                     ru1.ru_nvcsw - ru0.ru_nvcsw, ru1.ru_nivcsw - ru0.ru_nivcsw,
+                     (ru1.ru_utime.tv_sec - ru0.ru_utime.tv_sec) + 1e-6 * (ru1.ru_utime.tv_usec - ru0.ru_utime.tv_usec),
+                     (ru1.ru_stime.tv_sec - ru0.ru_stime.tv_sec) + 1e-6 * (ru1.ru_stime.tv_usec - ru0.ru_stime.tv_usec));
+            lat += rb;
+            const uint64_t fmax = *std::max_element(th_first.begin(), th_first.end());
+            const uint64_t emin = *std::min_element(th_end.begin(), th_end.end());
+            const uint64_t emax = *std::max_element(th_end.begin(), th_end.end());
+            snprintf(rb, sizeof(rb), ", \"threads_ms\": {\"last_start\": %.2f, \"first_end\": %.2f, \"last_end\": %.2f}",
+                     fmax / 1e6, emin / 1e6, emax / 1e6);
+            lat += rb;
+            static const char* names[P_N + 1] = {"enc_add", "encode", "enc_ack", "dec_add", "dec_recovery", "is_ready",
+                                                 "decode", "dec_ack", "stream_total"};
+            // the slowest stream (it sets the pass time): its id, ms per call kind, call counts
+            int worst = 0;
+            for (int s = 1; s < streams; ++s)
+                if (prof[s][P_N] > prof[worst][P_N]) worst = s;
+            lat += ", \"slowest_stream\": {\"stream\": " + std::to_string(ps[worst].stream_id) + ", \"encodes\": " +
+                   std::to_string(logs[worst].enc_ns.size()) + ", \"decodes\": " + std::to_string(logs[worst].dec_ns.size());
+            for (int k = 0; k <= P_N; ++k) {
+                char b[96];
+                snprintf(b, sizeof(b), ", \"%s\": %.2f", names[k], prof[worst][k] / 1e6);
+                lat += b;
+            }
+            lat += "}";
+            lat += ", \"call_ms\": {";
+            for (int k = 0; k <= P_N; ++k) {
+                uint64_t t = 0;
+                for (int s = 0; s < streams; ++s) t += prof[s][k];
+                char b[96];
+                snprintf(b, sizeof(b), "%s\"%s\": %.1f", k ? ", " : "", names[k], t / 1e6);
+                lat += b;
+            }
+            lat += "}";
         }
         printf("{\"seconds\": %.6f, \"payload_bytes\": %llu, \"gib_per_s\": %.6f, \"threads\": %d, "
                "\"streams\": %d, \"reps\": %d, \"bad\": %llu%s}\n",

@@ -12,6 +12,7 @@
 #include "../../tonk_amd/csrc/transcript.h"
 #include "../../oracle/siamese_oracle.h"
 
+#include <chrono>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -218,6 +219,24 @@ struct Harness {
                     sorted.push_back(o.first); sorted.push_back(o.count);
                     sorted.push_back(o.span); sorted.push_back(o.full);
                 }
+        static const bool dump = getenv("CP_DUMP_OPS") != nullptr;
+        if (dump && !ops_v.empty()) {  // (diagnostics) every op: level, instructions, rows read, stores
+            const auto& in = ctx.pb.instrs();
+            fprintf(stderr, "program %llu: %zu ops, %u levels\n", (unsigned long long)programs, ops_v.size(), maxl);
+            for (size_t i = 0; i < ops_v.size(); ++i) {
+                const tamd_op& o = ops_v[i];
+                uint32_t rows = 0, runs = 0, acc3 = 0, stores = 0;
+                for (uint32_t k = o.first; k < o.first + o.count; ++k) {
+                    const uint32_t kind = in[k].w0 & 0xff;
+                    if (kind == TAMD_I_ACC) ++rows;
+                    else if (kind == TAMD_I_ACC3) { ++rows; ++acc3; }
+                    else if (kind == TAMD_I_ACCR) { rows += in[k].cap; ++runs; }
+                    else if (kind == TAMD_I_STORE || kind == TAMD_I_STOREC) ++stores;
+                }
+                fprintf(stderr, "  op L%u c%u: %u instrs, %u rows (%u acc3, %u runs), %u stores, span %u\n",
+                        lv[i] / TAMD_COST_CLASSES, lv[i] % TAMD_COST_CLASSES, o.count, rows, acc3, runs, stores, o.span);
+            }
+        }
         if (!ops_v.empty()) {
             const int rc = oracle_run_program(arena.data(), arena.size(), sorted.data(),
                                               (unsigned)(sorted.size() / 4),
@@ -308,7 +327,23 @@ struct Harness {
         }
         return true;
     }
-    int enc_encode(RecRef& r) { return E()->encode(r.out); }
+    // CP_TIME=1 (diagnostics): host nanoseconds in encode / add_recovery / is_ready / decode
+    uint64_t t_ns[4] = {0, 0, 0, 0}, t_n[4] = {0, 0, 0, 0};
+    static uint64_t tnow() {
+        return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                   std::chrono::steady_clock::now().time_since_epoch()).count();
+    }
+    struct TScope {
+        Harness& h;
+        int k;
+        uint64_t t0;
+        TScope(Harness& hh, int kk) : h(hh), k(kk), t0(tnow()) {}
+        ~TScope() { h.t_ns[k] += tnow() - t0; h.t_n[k]++; }
+    };
+    int enc_encode(RecRef& r) {
+        TScope ts(*this, 0);
+        return E()->encode(r.out);
+    }
     int enc_ack(const uint8_t* buf, uint32_t n, uint32_t* next) { return E()->acknowledge(buf, n, next); }
     int dec_add_original(uint32_t col, uint32_t index, uint32_t len) {
         uint32_t framed = 0, header = 0;
@@ -328,14 +363,22 @@ struct Harness {
         uint8_t tail[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         const uint32_t tl = r.out.total() < 8 ? r.out.total() : 8;
         memcpy(tail + tl - r.out.footer_len, r.out.footer, r.out.footer_len);
+        TScope ts(*this, 1);
         const Result rc = D()->add_recovery(r.out.row, r.out.total(), tail, nullptr, &took);
         if (!took) ctx.rows.free_deferred(r.out.row);
         return rc;
     }
-    int dec_is_ready() { return D()->is_ready(); }
+    int dec_is_ready() {
+        TScope ts(*this, 2);
+        return D()->is_ready();
+    }
     int dec_decode(std::vector<uint32_t>& nums, DecRef&) {
         std::vector<RecoveredPacket*> got;
-        const Result rc = D()->decode(got);
+        Result rc;
+        {
+            TScope ts(*this, 3);
+            rc = D()->decode(got);
+        }
         if (rc == kSuccess) {
             pend_dec.emplace_back();
             for (RecoveredPacket* rp : got) {
@@ -447,6 +490,10 @@ int main(int argc, char** argv) {
             (unsigned long long)s.acks, (unsigned long long)s.decode_calls,
             (unsigned long long)s.flush_encodes, (unsigned long long)s.missing_at_end);
     fclose(f);
+    if (getenv("CP_TIME"))
+        fprintf(stderr, "host us: encode %.1f ms / %llu, add_recovery %.1f ms / %llu, is_ready %.1f ms / %llu, decode %.1f ms / %llu\n",
+                h.t_ns[0] * 1e-6, (unsigned long long)h.t_n[0], h.t_ns[1] * 1e-6, (unsigned long long)h.t_n[1],
+                h.t_ns[2] * 1e-6, (unsigned long long)h.t_n[2], h.t_ns[3] * 1e-6, (unsigned long long)h.t_n[3]);
     fprintf(stderr, "programs=%llu ops=%llu instrs=%llu levels=%llu live_rows=%zu pipelined_pairs=%llu\n",
             (unsigned long long)h.programs, (unsigned long long)h.ops, (unsigned long long)h.instrs,
             (unsigned long long)h.levels, h.ctx.rows.live_rows(), (unsigned long long)h.pipelined_pairs);

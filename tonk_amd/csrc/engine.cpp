@@ -135,6 +135,7 @@ void ProgramBuilder::clear() {
     ops_.clear();
     instrs_.clear();
     levels_.clear();
+    pure_.clear();
     written_.clear();
     level_ops_.clear();
     level_items_.clear();
@@ -370,6 +371,7 @@ uint32_t ProgramBuilder::end_op(uint32_t min_level) {
     const uint32_t cls = (cur_pure_ && rows >= 48) ? 0u : cost >= 64 ? 1u : cost >= 32 ? 2u : cost >= 12 ? 3u : 4u;
     const uint32_t bucket = TAMD_COST_CLASSES * level + cls;
     levels_.push_back(bucket);
+    pure_.push_back(cur_pure_ ? 1 : 0);
     if (level_ops_.size() < TAMD_COST_CLASSES * (level + 1)) {
         level_ops_.resize(TAMD_COST_CLASSES * (level + 1), 0);
         level_items_.resize(TAMD_COST_CLASSES * (level + 1), 0);

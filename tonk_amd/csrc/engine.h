@@ -212,6 +212,7 @@ public:
         ops_.swap(o.ops_);
         instrs_.swap(o.instrs_);
         levels_.swap(o.levels_);
+        pure_.swap(o.pure_);
         written_.swap(o.written_);
         level_ops_.swap(o.level_ops_);
         level_items_.swap(o.level_items_);
@@ -225,6 +226,9 @@ public:
     const InstrVec& instrs() const { return instrs_; }
     // Per op: its bucket, TAMD_COST_CLASSES * level + cost class (0 = most expensive).
     const std::vector<uint32_t>& op_levels() const { return levels_; }
+    // Per op: 1 when it is a pure combine (ACC into acc_0, CONST/CAUCHY/DENSE runs, one final
+    // STORE + FOOTER) whose row batches several waves can split (partial sums reduced after).
+    const std::vector<uint8_t>& op_pure() const { return pure_; }
     const std::vector<RowId>& written_rows() const { return written_; }
     // Per bucket (see op_levels): op count and work-item count (slice_bytes() chunks).
     const std::vector<uint32_t>& level_ops() const { return level_ops_; }
@@ -238,6 +242,7 @@ private:
     std::vector<tamd_op> ops_;
     InstrVec instrs_;
     std::vector<uint32_t> levels_;
+    std::vector<uint8_t> pure_;
     std::vector<RowId> written_;
     std::vector<uint32_t> level_ops_, level_items_;
     uint32_t max_level_ = 0;

@@ -81,6 +81,16 @@ template <bool FULL>
 __device__ __forceinline__ uint32_t load_off(uint32_t o, uint32_t len) { return (FULL || o < len) ? o : 0u; }
 
 // row[len, len + 8) = footer, row[len + 8, cap) = 0 around acc (one lane's 8 bytes at offset o).
+// An 8-byte arena store; WT: write-through (an agent-scope relaxed atomic store, `sc1`), so the
+// row is visible to every CU and XCD once the storing wave has drained (the persistent C-ABI
+// executor's commands need no L2 write-back fence for the next command of the codec).
+template <bool WT>
+__device__ __forceinline__ void st_u64(uint8_t* p, u64 v) {
+    if constexpr (WT) __hip_atomic_store((u64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *(u64*)p = v;
+}
+
+template <bool WT = false>
 __device__ __forceinline__ void store_slice(uint8_t* __restrict__ arena, uint32_t row, uint32_t len, uint32_t cap,
                                             u64 footer, uint32_t o, u64 acc) {
     if (o >= cap) return;
@@ -96,7 +106,7 @@ __device__ __forceinline__ void store_slice(uint8_t* __restrict__ arena, uint32_
         const uint32_t sh = len - o;
         if (sh < 8u) fpart = footer << (8u * sh);
     }
-    *(u64*)(arena + (size_t)row * TAMD_ROW_UNIT + o) = (acc & keep) | fpart;
+    st_u64<WT>(arena + (size_t)row * TAMD_ROW_UNIT + o, (acc & keep) | fpart);
 }
 
 // LDS image of the device tables (device.cpp uploads the same layout):
@@ -246,12 +256,15 @@ __device__ __forceinline__ void lv_acc3(const LV<NH>& x, const PermT& c1, const 
         a2.h[i] ^= ((u64)mul_sel(hi, c2) << 32) | mul_sel(lo, c2);
     }
 }
-template <bool FULL, int NH>
+template <bool FULL, int NH, bool WT = false>
 __device__ __forceinline__ void lv_store_row(uint8_t* __restrict__ arena, uint32_t row, uint32_t len, uint32_t cap,
                                              u64 footer, uint32_t o, const LV<NH>& x, uint32_t ox = 0) {
     constexpr int NM = NH < 3 ? NH : 2;
     if (FULL) {
-        if constexpr (NH == 3) {
+        if constexpr (NH == 3 && WT) {
+            st_u64<true>(arena + (size_t)row * TAMD_ROW_UNIT + o, x.h[0]);
+            st_u64<true>(arena + (size_t)row * TAMD_ROW_UNIT + o + 8u, x.h[1]);
+        } else if constexpr (NH == 3) {
             u64x2 t;
             t.x = x.h[0];
             t.y = x.h[1];
@@ -261,9 +274,9 @@ __device__ __forceinline__ void lv_store_row(uint8_t* __restrict__ arena, uint32
         }
     } else {
 #pragma unroll
-        for (int i = 0; i < NM; ++i) store_slice(arena, row, len, cap, footer, o + 8u * i, x.h[i]);
+        for (int i = 0; i < NM; ++i) store_slice<WT>(arena, row, len, cap, footer, o + 8u * i, x.h[i]);
     }
-    if constexpr (NH == 3) store_slice(arena, row, len, cap, footer, ox, x.h[2]);
+    if constexpr (NH == 3) store_slice<WT>(arena, row, len, cap, footer, ox, x.h[2]);
 }
 
 // ACCR: a strided run of equally long rows (program.h).  TAMD_RBATCH row loads are issued
@@ -631,7 +644,7 @@ __device__ __forceinline__ LV<NH> run_item(const tamd_instr* __restrict__ instrs
                 if (c0 == 1u) x = a0; else if (c0) x = lv_mul<NH>(a0, perm_at(lds, c0 * 8u));
                 if (c1 == 1u) x ^= a1; else if (c1) x ^= lv_mul<NH>(a1, perm_at(lds, c1 * 8u));
                 if (c2 == 1u) x ^= a2; else if (c2) x ^= lv_mul<NH>(a2, perm_at(lds, c2 * 8u));
-                lv_store_row<FULL, NH>(arena, in[j].row, in[j].len, in[j].cap, 0, o, x, ox);
+                lv_store_row<FULL, NH, LDSI>(arena, in[j].row, in[j].len, in[j].cap, 0, o, x, ox);
             } else if (kind == TAMD_I_ACC3) {
                 const LV<NH> x = lv_keep<FULL, NH>(v[j], o, in[j].len, ox);
                 const PermT c1 = perm_at(lds, ((w >> 8) & 0xffu) * 8u), c2 = perm_at(lds, ((w >> 16) & 0xffu) * 8u);
@@ -644,7 +657,7 @@ __device__ __forceinline__ LV<NH> run_item(const tamd_instr* __restrict__ instrs
                 } else {
                     // the FOOTER word follows the STORE (possibly past this batch)
                     const tamd_instr f = fetch_instr<LDSI>(instrs, k + j + 1);
-                    lv_store_row<FULL, NH>(arena, in[j].row, in[j].len, in[j].cap, ((u64)f.len << 32) | f.row, o, x, ox);
+                    lv_store_row<FULL, NH, LDSI>(arena, in[j].row, in[j].len, in[j].cap, ((u64)f.len << 32) | f.row, o, x, ox);
                 }
             } else if (kind == TAMD_I_CLEAR) {
                 a0 = a1 = a2 = lv_zero<NH>();
@@ -818,7 +831,7 @@ __device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" :
 
 // Copy `len` bytes between host memory (16-B aligned) and an arena row, one wave: 16 B per lane
 // per chunk, four chunks in flight per lane, the tail (len mod 16) byte by byte.
-template <bool TO_HOST>
+template <bool TO_HOST, bool PLAIN = false>
 __device__ __forceinline__ void serve_xfer(uint8_t* __restrict__ arena, u64 host, uint32_t unit, uint32_t len,
                                            uint32_t lane) {
     uint8_t* a = arena + (size_t)unit * TAMD_ROW_UNIT;
@@ -834,13 +847,42 @@ __device__ __forceinline__ void serve_xfer(uint8_t* __restrict__ arena, u64 host
         const uint4 v1 = *(const uint4*)(src + 16u * min(c1, m));
         const uint4 v2 = *(const uint4*)(src + 16u * min(c2, m));
         const uint4 v3 = *(const uint4*)(src + 16u * min(c3, m));
-        if (c0 < n16) *(uint4*)(dst + 16u * c0) = v0;
-        if (c1 < n16) *(uint4*)(dst + 16u * c1) = v1;
-        if (c2 < n16) *(uint4*)(dst + 16u * c2) = v2;
-        if (c3 < n16) *(uint4*)(dst + 16u * c3) = v3;
+        // Arena rows: write-through (agent scope), visible to the codec's next command on any
+        // XCD; host memory: system-scope stores, written through to the host before the completion
+        // word (plain stores there can still sit in the L2 when it is seen: wrong packets)
+        const uint4 v[4] = {v0, v1, v2, v3};
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q)
+            if (c0 + 64u * q < n16) {
+                uint8_t* d = dst + 16u * (c0 + 64u * q);
+                const u64 lo = ((u64)v[q].y << 32) | v[q].x, hi = ((u64)v[q].w << 32) | v[q].z;
+                if constexpr (PLAIN) {
+                    *(uint4*)d = v[q];
+                } else if constexpr (TO_HOST) {
+                    st_sys((uint64_t*)d, lo);
+                    st_sys((uint64_t*)(d + 8), hi);
+                } else {
+                    st_u64<true>(d, lo);
+                    st_u64<true>(d + 8, hi);
+                }
+            }
     }
     const uint32_t tail = len & 15u;
-    if (lane < tail) dst[16u * n16 + lane] = src[16u * n16 + lane];
+    if (TO_HOST) {
+        // the last partial 8-byte words as whole words: the landing buffers are in 64-byte units
+        // (capi.cpp) and arena rows too, so the bytes past `len` stay inside both
+        const uint32_t w0 = 16u * n16, nw = (tail + 7u) / 8u;
+        if (lane < nw) st_sys((uint64_t*)(dst + w0 + 8u * lane), *(const u64*)(src + w0 + 8u * lane));
+    } else if (tail) {  // the last partial 8-byte words of the row, merged with the bytes already there
+        const uint32_t w0 = 16u * n16, nw = (tail + 7u) / 8u;
+        if (lane < nw) {
+            const uint32_t at = w0 + 8u * lane, nb = min(8u, len - at);
+            u64 x = 0;
+            for (uint32_t b = 0; b < nb; ++b) x |= (u64)src[at + b] << (8u * b);
+            if (nb < 8u) x |= *(const u64*)(dst + at) & ~byte_mask(nb);
+            st_u64<true>(dst + at, x);
+        }
+    }
 }
 
 __device__ __forceinline__ tamd_xfer lds_xfer(const uint8_t* base, uint32_t i) {
@@ -853,34 +895,35 @@ __device__ __forceinline__ tamd_xfer lds_xfer(const uint8_t* base, uint32_t i) {
 }
 
 extern "C" __global__ void __launch_bounds__(TAMD_SERVE_THREADS) tamd_serve(const tamd_serve_args a) {
-    uint64_t* ready = (uint64_t*)(a.dev + 1);
-    tamd_serve_entry* wl = (tamd_serve_entry*)(ready + a.wl_mask + 1);
+    tamd_serve_slot* wl = (tamd_serve_slot*)(a.dev + 1);
     if (blockIdx.x == 0) {
-        // ---- the dispatcher: one lane ----
-        if (threadIdx.x != 0) return;
+        // ---- the dispatcher: one wave ----
+        // Each poll reads slots t .. t + 9 (lane = 6 * slot + granule, lanes 60..63 idle) and
+        // hands on every complete slot from t on: its granules are copied unchanged into the
+        // work list with write-through stores (no fence: the tags are the flags).
+        if (threadIdx.x >= 64) return;
+        const uint32_t lane = threadIdx.x, j = lane / TAMD_SERVE_GRANULES, k = lane - TAMD_SERVE_GRANULES * j;
+        // (A/B, pad bit 1: one slot per poll)
+        const uint32_t width = (a.pad & 2u) ? 1u : 10u;
+        const bool mine = lane < width * TAMD_SERVE_GRANULES;
         u64 t = a.tail0;
         u64 last = __builtin_amdgcn_s_memrealtime();
-        st_sys(&a.host->dbg[0], last);
+        if (lane == 0) st_sys(&a.host->dbg[0], last);
         for (uint32_t polls = 0;; ++polls) {
-            if ((polls & 1023u) == 0) {
+            if ((polls & 1023u) == 0 && lane == 0) {
                 st_sys(&a.host->dbg[1], polls >> 10);
                 st_sys(&a.host->dbg[2], t);
             }
-            const tamd_serve_slot* s = a.ring + (t & a.ring_mask);
-            if (ld_sys(&s->seq) == t + 1) {
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the slot's fields after its seq
-                tamd_serve_entry e;
-                e.cmd = ld_sys(&s->cmd);
-                e.done = ld_sys(&s->done);
-                e.done_val = ld_sys(&s->done_val);
-                e.cmd_bytes = (uint32_t)ld_sys((const uint64_t*)&s->cmd_bytes);
-                e.pad = 0;
-                wl[t & a.wl_mask] = e;
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                vm_drain();
-                __hip_atomic_store(&ready[t & a.wl_mask], t + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                ++t;
-                st_sys(&a.host->consumed, t);
+            const u64 ti = t + (mine ? j : 0u);
+            const u64 gv = ld_sys(&a.ring[ti & a.ring_mask].g[mine ? k : 0u]);
+            const u64 okm = ballot(mine && (uint32_t)(gv >> 32) == (uint32_t)(ti + 1));
+            uint32_t n = 0;
+            while (n < width && ((okm >> (TAMD_SERVE_GRANULES * n)) & 0x3full) == 0x3full) ++n;
+            if (n) {
+                if (mine && j < n)
+                    __hip_atomic_store(&wl[ti & a.wl_mask].g[k], gv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                t += n;
+                if (lane == 0) st_sys(&a.host->consumed, t);
                 last = __builtin_amdgcn_s_memrealtime();
                 continue;
             }
@@ -889,13 +932,13 @@ extern "C" __global__ void __launch_bounds__(TAMD_SERVE_THREADS) tamd_serve(cons
         }
         // End: the workers drain what was published, then end; the host learns where the next
         // instance starts (exit_tail) before it learns that this one ended (exited_gen).
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         vm_drain();
-        __hip_atomic_store(&a.dev->quit, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        st_sys(&a.host->exit_tail, t);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-        vm_drain();
-        st_sys(&a.host->exited_gen, a.gen);
+        if (lane == 0) {
+            __hip_atomic_store(&a.dev->quit, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            st_sys(&a.host->exit_tail, t);
+            vm_drain();
+            st_sys(&a.host->exited_gen, a.gen);
+        }
         return;
     }
 
@@ -904,62 +947,81 @@ extern "C" __global__ void __launch_bounds__(TAMD_SERVE_THREADS) tamd_serve(cons
     constexpr uint32_t SLICE = 64u * 8u * NH, MAIN = 1024u;
     __shared__ __attribute__((aligned(16))) uint32_t lds_perm[TAMD_GF_DWORDS];
     __shared__ __attribute__((aligned(16))) uint4 cbuf[TAMD_SERVE_CMD_BYTES / 16];
-    __shared__ tamd_serve_entry sh_e;
-    __shared__ uint32_t sh_state, sh_item;
+    __shared__ u64 sh_cmd;
+    __shared__ uint32_t sh_state, sh_bytes, sh_item;
+    __shared__ LV<3> partial[TAMD_SERVE_WAVES][64];  // grouped levels: each wave's acc_0
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = uniform(tid >> 6);
     for (uint32_t i = tid; i < TAMD_GF_DWORDS / 4; i += TAMD_SERVE_THREADS)
         ((uint4*)lds_perm)[i] = ((const uint4*)a.gf)[i];
     const uint32_t laneb = lane * 16u, laneb_x = MAIN + lane * 8u;
     const uint8_t* cb = (const uint8_t*)cbuf;
-    // Lane 0 of wave 0 completes the previous command (its completion words) and claims the next
-    // one in ONE divergent region at the top of the loop, right before the barrier: a divergent
-    // region at the end of the body, before the back edge, was rotated by the compiler so that
-    // the other lanes of wave 0 looped through the barrier without lane 0 (a hang).
-    u64 prev_done = 0, prev_val = 0, prev_start = 0;
-    uint32_t prev_dbg = 0;
+    // Wave 0 completes the previous command (its completion words) and claims the next one in
+    // ONE wave-uniform region at the top of the loop, right before the barrier (a lane-divergent
+    // region before the back edge was rotated by the compiler so that the other lanes of wave 0
+    // looped through the barrier without lane 0: a hang).
+    u64 prev_done = 0, prev_start = 0;
+    u64 prev_t[4] = {0, 0, 0, 0};  // stamps: command in LDS, packets landed, program run, reads written
+    uint32_t prev_val = 0, prev_dbg = 0;
     for (;;) {
-        if (tid == 0) {
+        if (wave == 0) {
             if (prev_done) {
-                uint64_t* done = (uint64_t*)prev_done;
-                st_sys(done + 1, prev_start);
-                st_sys(done + 2, __builtin_amdgcn_s_memrealtime());
-                // everything the command wrote -- its rows, for the next command on any CU or XCD;
-                // its reads, for the host -- before its completion word
-                if (!(a.pad & 2u)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-                vm_drain();
-                st_sys(done, prev_val);
-                if (prev_dbg) st_sys(&a.host->dbg[3], 7);
+                // every wave drained its stores (rows write-through, reads to the host) before
+                // the barrier that ended the command: the completion word goes last
+                if (lane == 0) {
+                    uint64_t* done = (uint64_t*)prev_done;
+                    st_sys(done + 1, prev_start);
+                    st_sys(done + 2, __builtin_amdgcn_s_memrealtime());
+                    // the reads' lines and anything else of the command still in the L2 go to
+                    // memory before the completion word (pad bit 0: no fence, A/B)
+                    if (!(a.pad & 1u)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+                    vm_drain();
+                    st_sys(done + 3, prev_t[0]);
+                    st_sys(done + 4, prev_t[1]);
+                    st_sys(done + 5, prev_t[2]);
+                    st_sys(done + 6, prev_t[3]);
+                    st_sys(done, prev_val);
+                    if (prev_dbg) st_sys(&a.host->dbg[3], 7);
+                }
                 prev_done = 0;
             }
-            const u64 k = __hip_atomic_fetch_add(&a.dev->claim, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            u64 k = 0;
+            if (lane == 0) k = __hip_atomic_fetch_add(&a.dev->claim, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            k = ((u64)uniform((uint32_t)(rdl((uint32_t)(k >> 32), 0))) << 32) | uniform(rdl((uint32_t)k, 0));
             const u64 idx = a.tail0 + k;
-            const uint64_t* rp = &ready[idx & a.wl_mask];
-            if (idx == 0) {  // (diagnostics: the first command, the server's start-up probe)
+            const uint64_t* en = wl[idx & a.wl_mask].g;
+            const uint32_t tag = (uint32_t)(idx + 1);
+            if (idx == 0 && lane == 0) {  // (diagnostics: the first command, the server's start-up probe)
                 st_sys(&a.host->dbg[3], 1);
                 st_sys(&a.host->dbg[4], blockIdx.x);
             }
             uint32_t st = 0;
+            u64 gv = 0;
             for (;;) {
-                if (ld_agent(rp) == idx + 1) { st = 1; break; }
+                gv = ld_agent(en + min(lane, TAMD_SERVE_GRANULES - 1u));
+                if (ballot((uint32_t)(gv >> 32) != tag) == 0) { st = 1; break; }
                 if (ld_agent(&a.dev->quit)) {
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-                    st = ld_agent(rp) == idx + 1;
+                    gv = ld_agent(en + min(lane, TAMD_SERVE_GRANULES - 1u));
+                    st = ballot((uint32_t)(gv >> 32) != tag) == 0;
                     break;
                 }
                 __builtin_amdgcn_s_sleep(1);
             }
             if (st) {
-                // this CU's L1 and the host data the L2 may hold are refreshed before any load of
-                // the command, its packets or the codec's rows
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-                const tamd_serve_entry e = wl[idx & a.wl_mask];
-                sh_e = e;
-                prev_done = e.done;
-                prev_val = e.done_val;
+                const uint32_t v = (uint32_t)gv;
+                prev_done = ((u64)uniform(rdl(v, 3)) << 32) | uniform(rdl(v, 2));
+                prev_val = uniform(rdl(v, 4));
                 prev_start = __builtin_amdgcn_s_memrealtime();
                 prev_dbg = idx == 0;
+                if (lane == 0) {
+                    sh_cmd = ((u64)rdl(v, 1) << 32) | rdl(v, 0);
+                    sh_bytes = rdl(v, 5);
+                }
+                // this CU's L1 drops lines another CU may have rewritten since (the codec's rows);
+                // it completes while the command is copied (through uncached loads) and is waited
+                // for before the barrier below, ahead of every arena access
+                asm volatile("buffer_inv sc1" ::: "memory");
             }
-            sh_state = st ? (idx == 0 ? 2u : 1u) : 0u;
+            if (lane == 0) sh_state = st ? (idx == 0 ? 2u : 1u) : 0u;
         }
         __syncthreads();
         // (read through readfirstlane: a loop exit the compiler sees as divergent would put the
@@ -968,10 +1030,13 @@ extern "C" __global__ void __launch_bounds__(TAMD_SERVE_THREADS) tamd_serve(cons
         if (!state) break;
         const bool dbg = state == 2u && tid == 0;
         if (dbg) st_sys(&a.host->dbg[3], 2);
-        const u64 cmd_addr = ((u64)uniform((uint32_t)(sh_e.cmd >> 32)) << 32) | uniform((uint32_t)sh_e.cmd);
-        const uint32_t cmd_bytes = uniform(sh_e.cmd_bytes);
-        // 1. the command into LDS
-        {
+        const u64 cmd_addr = ((u64)uniform((uint32_t)(sh_cmd >> 32)) << 32) | uniform((uint32_t)sh_cmd);
+        const uint32_t cmd_bytes = uniform(sh_bytes);
+        // 1. the command into LDS (8-byte system-scope loads: they bypass the L1, whose invalidation
+        // runs meanwhile)
+        if (a.pad & 4u) {
+            vm_drain();
+            __syncthreads();
             const uint32_t n16 = (cmd_bytes + 15u) >> 4, m = n16 - 1u;
             const uint4* src = (const uint4*)cmd_addr;
             constexpr uint32_t T = TAMD_SERVE_THREADS;
@@ -983,25 +1048,120 @@ extern "C" __global__ void __launch_bounds__(TAMD_SERVE_THREADS) tamd_serve(cons
                 if (b + 2u * T < n16) cbuf[b + 2u * T] = v2;
                 if (b + 3u * T < n16) cbuf[b + 3u * T] = v3;
             }
+        } else {
+            const uint32_t n8 = (cmd_bytes + 7u) >> 3, m = n8 - 1u;
+            const uint64_t* src = (const uint64_t*)cmd_addr;
+            constexpr uint32_t T = TAMD_SERVE_THREADS;
+            u64* dst = (u64*)cbuf;
+            for (uint32_t b = tid; b < n8; b += 4u * T) {
+                const u64 v0 = ld_sys(src + min(b, m)), v1 = ld_sys(src + min(b + T, m)),
+                          v2 = ld_sys(src + min(b + 2u * T, m)), v3 = ld_sys(src + min(b + 3u * T, m));
+                dst[b] = v0;
+                if (b + T < n8) dst[b + T] = v1;
+                if (b + 2u * T < n8) dst[b + 2u * T] = v2;
+                if (b + 3u * T < n8) dst[b + 3u * T] = v3;
+            }
         }
+        vm_drain();  // (wave 0: its L1 invalidation too)
         __syncthreads();
+        prev_t[0] = __builtin_amdgcn_s_memrealtime();
         if (dbg) st_sys(&a.host->dbg[3], 3);
         const tamd_cmd* c = (const tamd_cmd*)cb;
         const uint32_t n_up = uniform(c->n_up), n_rd = uniform(c->n_rd), levels = uniform(c->levels);
         // 2. packets staged since the codec's last program land in their rows
-        for (uint32_t u = wave; u < n_up; u += TAMD_SERVE_WAVES) {
-            const tamd_xfer x = lds_xfer(cb + uniform(c->off_up), u);
-            serve_xfer<false>(a.arena, x.host, x.unit, x.len, lane);
+        const uint32_t up_chunks = uniform(c->up_chunks);
+        if (up_chunks) {
+            // one staging half: every thread copies 16-byte chunks of it, four loads in flight,
+            // each chunk to the packet it falls in (binary search over the uploads, in LDS);
+            // chunks in the alignment gaps between packets are dropped, a packet's last chunk
+            // may write bytes past its end inside its row (rows are whole 64-byte units)
+            const uint8_t* xs = cb + uniform(c->off_up);
+            const u64 base = lds_xfer(xs, 0).host;
+            constexpr uint32_t T = TAMD_SERVE_THREADS;
+            const uint32_t m = up_chunks - 1u;
+            for (uint32_t b = tid; b < up_chunks; b += 4u * T) {
+                uint4 v[4];
+#pragma unroll
+                for (uint32_t q = 0; q < 4; ++q) v[q] = *(const uint4*)(base + 16ull * min(b + q * T, m));
+#pragma unroll
+                for (uint32_t q = 0; q < 4; ++q) {
+                    const uint32_t ch = b + q * T;
+                    if (ch >= up_chunks) break;
+                    const u64 at = base + 16ull * ch;
+                    uint32_t lo = 0, hi = n_up;  // last upload whose host address is <= at
+                    while (hi - lo > 1u) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (((const tamd_xfer*)xs)[mid].host <= at) lo = mid; else hi = mid;
+                    }
+                    const tamd_xfer x = ((const tamd_xfer*)xs)[lo];
+                    const u64 off = at - x.host;
+                    if (off < x.len) {
+                        uint8_t* d = a.arena + (size_t)x.unit * TAMD_ROW_UNIT + off;
+                        st_u64<true>(d, ((u64)v[q].y << 32) | v[q].x);
+                        st_u64<true>(d + 8, ((u64)v[q].w << 32) | v[q].z);
+                    }
+                }
+            }
+        } else {
+            for (uint32_t u = wave; u < n_up; u += TAMD_SERVE_WAVES) {
+                const tamd_xfer x = lds_xfer(cb + uniform(c->off_up), u);
+                serve_xfer<false>(a.arena, x.host, x.unit, x.len, lane);
+            }
         }
         vm_drain();
         __syncthreads();
         if (dbg) st_sys(&a.host->dbg[3], 4);
+        prev_t[1] = __builtin_amdgcn_s_memrealtime();
         // 3. the program, level by level
         const tamd_instr* ins = (const tamd_instr*)(cb + uniform(c->off_instr));
         const uint4* ops = (const uint4*)(cb + uniform(c->off_ops));
         const uint2* items = (const uint2*)(cb + uniform(c->off_items));
         for (uint32_t l = 0; l < levels; ++l) {
-            const uint32_t b1 = uniform(c->level_base[l + 1]);
+            const uint32_t b0 = uniform(c->level_base[l]), b1 = uniform(c->level_base[l + 1]), n = b1 - b0;
+            if (n && 2u * n <= TAMD_SERVE_WAVES) {
+                // Few items: a group of G waves per item (G = 16, 8, 4, 2 for 1, 2, 3-4, 5-8 items).
+                // A pure combine's row batches are split over its group (every G-th batch per
+                // wave, run_item's shared mode) and the group's first wave sums the partial
+                // accumulators through LDS and stores the row; any other op runs on that wave alone.
+                // (A per-call program is one to three such levels of one to a few ops: a single
+                // wave walking a 50-row op was most of a command's time.)
+                const uint32_t G = TAMD_SERVE_WAVES >> (32u - __builtin_clz(n - 1u | 1u) - (n == 1u ? 1u : 0u));
+                const uint32_t grp = wave / G, rank = wave % G;
+                const bool active = grp < n;
+                uint32_t shared = 0, full = 0, first = 0, end = 0, o = 0, ox = 0;
+                LV<NH> x = lv_zero<NH>();
+                if (active) {
+                    const uint2 item = items[b0 + grp];
+                    const uint4 op = ops[uniform(item.x)];
+                    shared = uniform(item.y) >> 31;
+                    const uint32_t s0 = (uniform(item.y) & 0x7fffffffu) * SLICE;
+                    o = s0 + laneb;
+                    ox = s0 + laneb_x;
+                    first = uniform(op.x);
+                    end = first + uniform(op.y);
+                    full = s0 + MAIN <= uniform(op.w);
+                    if (shared || rank == 0) {
+                        const uint32_t nw = shared ? G : 1u, wid = shared ? rank : 0u;
+                        if (full)
+                            x = run_item<true, NH, 5, true>(ins, first, end, o, ox, laneb, a.arena, a.zrow, lds_perm, nw, wid);
+                        else
+                            x = run_item<false, NH, 5, true>(ins, first, end, o, ox, laneb, a.arena, a.zrow, lds_perm, nw, wid);
+                    }
+                }
+                partial[wave][lane] = x;
+                __syncthreads();
+                if (active && shared && rank == 0) {
+                    LV<NH> sum = x;
+                    for (uint32_t w = 1; w < G; ++w) sum ^= partial[wave + w][lane];
+                    const tamd_instr st = fetch_instr<true>(ins, end - 2u), f = fetch_instr<true>(ins, end - 1u);
+                    const u64 foot = ((u64)f.len << 32) | f.row;  // STORE (acc_0) + FOOTER end every pure op
+                    if (full) lv_store_row<true, NH, true>(a.arena, st.row, st.len, st.cap, foot, o, sum, ox);
+                    else lv_store_row<false, NH, true>(a.arena, st.row, st.len, st.cap, foot, o, sum, ox);
+                }
+                vm_drain();
+                __syncthreads();
+                continue;
+            }
             if (tid == 0) sh_item = c->level_base[l];
             __syncthreads();
             for (;;) {
@@ -1011,7 +1171,7 @@ extern "C" __global__ void __launch_bounds__(TAMD_SERVE_THREADS) tamd_serve(cons
                 if (it >= b1) break;
                 const uint2 item = items[it];
                 const uint4 op = ops[uniform(item.x)];
-                const uint32_t s0 = uniform(item.y) * SLICE;
+                const uint32_t s0 = (uniform(item.y) & 0x7fffffffu) * SLICE;
                 const uint32_t o = s0 + laneb, ox = s0 + laneb_x;
                 const uint32_t first = uniform(op.x), end = first + uniform(op.y);
                 if (s0 + MAIN <= uniform(op.w))
@@ -1023,14 +1183,20 @@ extern "C" __global__ void __launch_bounds__(TAMD_SERVE_THREADS) tamd_serve(cons
             __syncthreads();
         }
         if (dbg) st_sys(&a.host->dbg[3], 5);
+        prev_t[2] = __builtin_amdgcn_s_memrealtime();
         // 4. the reads into the caller's pinned buffer
         for (uint32_t r = wave; r < n_rd; r += TAMD_SERVE_WAVES) {
             const tamd_xfer x = lds_xfer(cb + uniform(c->off_rd), r);
-            serve_xfer<true>(a.arena, x.host, x.unit, x.len, lane);
+            // (plain stores into the host buffer, written back by the release fence ahead of the
+            // completion word: 8-byte system-scope stores, one fabric write each, made a
+            // recovery-packet read ~10x slower; pad bit 3 restores them for A/B)
+            if (a.pad & 8u) serve_xfer<true>(a.arena, x.host, x.unit, x.len, lane);
+            else serve_xfer<true, true>(a.arena, x.host, x.unit, x.len, lane);
         }
         vm_drain();
         __syncthreads();
         if (dbg) st_sys(&a.host->dbg[3], 6);
+        prev_t[3] = __builtin_amdgcn_s_memrealtime();
         // 5. completion: at the top of the next iteration (lane 0 of wave 0)
     }
 }

@@ -17,23 +17,26 @@
 #define TAMD_SERVE_CMD_BYTES (64u << 10)  /* LDS area one command fits in (else: launch path) */
 #define TAMD_SERVE_MAX_LEVELS 32u
 
-/* A host ring slot (coherent pinned memory, 64 B).  `seq` is stored last (release): index + 1
-   once the slot holds command `index`; the dispatcher copies the slot to the device work list
-   and advances `consumed`, after which the host may reuse the slot for index + ring size. */
-typedef struct tamd_serve_slot {
-    uint64_t seq;
-    uint64_t cmd;       /* host address of the command (tamd_cmd) */
-    uint64_t done;      /* host address of the completion word */
-    uint64_t done_val;  /* value stored there once the command has completed */
-    uint32_t cmd_bytes, pad0;
-    uint64_t pad[3];
+/* A command's descriptor is 6 tagged granules, each one 8-byte word {tag = low 32 bits of
+   index + 1, value}: 0/1 the command's host address (low/high half), 2/3 the completion word's,
+   4 the value the worker stores there (the tag), 5 the command's bytes.  The host writes them
+   into the ring slot with 8-byte stores in any order; the dispatcher copies them unchanged into
+   the device work list with write-through stores; a reader takes a descriptor once all six tags
+   match -- the data is the flag, no fence on either hand-off (MI355X_MICROARCH.md, R2). */
+#define TAMD_SERVE_GRANULES 6u
+typedef struct tamd_serve_slot {  /* host ring slot and device work-list entry, 64 B */
+    uint64_t g[TAMD_SERVE_GRANULES];
+    uint64_t pad[2];
 } tamd_serve_slot;
+static inline uint64_t tamd_granule(uint64_t index, uint32_t value) {
+    return ((uint64_t)(uint32_t)(index + 1) << 32) | value;
+}
 
 /* Host-side control words (coherent pinned memory), each on a line of its own. */
 typedef struct tamd_serve_host {
     uint64_t stop;        /* host: the dispatcher ends at its next poll (process exit) */
     uint64_t pad0[15];
-    uint64_t consumed;    /* dispatcher: ring indices below this one have been handed on */
+    uint64_t consumed;    /* dispatcher: ring slots below this index have been handed on */
     uint64_t pad1[15];
     uint64_t exit_tail;   /* dispatcher, when it ends: the first index it did not take ... */
     uint64_t exited_gen;  /* ... and then its instance's generation (release-stored after) */
@@ -44,20 +47,13 @@ typedef struct tamd_serve_host {
     uint64_t dbg[16];
 } tamd_serve_host;
 
-/* One command of the device work list (a copy of its ring slot). */
-typedef struct tamd_serve_entry {
-    uint64_t cmd, done, done_val;
-    uint32_t cmd_bytes, pad;
-} tamd_serve_entry;
-
 /* Device state of one kernel instance (hipMalloc; reset before each launch). */
 typedef struct tamd_serve_dev {
     uint64_t claim;       /* workers' next relative index (atomic add) */
     uint64_t pad0[15];
     uint64_t quit;        /* dispatcher: no further command comes in this instance */
     uint64_t pad1[15];
-    /* then: uint64_t ready[wl_size] (index + 1 once entry index is published), then
-       tamd_serve_entry wl[wl_size] */
+    /* then: tamd_serve_slot wl[wl_size], the work list */
 } tamd_serve_dev;
 
 /* A command (16-B aligned, host memory; copied whole into the worker's LDS). */
@@ -66,7 +62,10 @@ typedef struct tamd_cmd {
     uint32_t n_up, n_rd, levels;
     uint32_t off_up, off_rd, off_instr, off_ops;  /* byte offsets from the command's start */
     uint32_t off_items, n_items, n_instr, n_ops;
-    uint32_t level_base[TAMD_SERVE_MAX_LEVELS + 4]; /* item index where level l starts (levels + 1) */
+    uint32_t up_chunks;   /* > 0: the uploads' host bytes lie in increasing order within this many
+                             16-byte chunks from the first one's address (one staging half), which
+                             the worker's threads copy chunk by chunk, all in flight at once */
+    uint32_t level_base[TAMD_SERVE_MAX_LEVELS + 3]; /* item index where level l starts (levels + 1) */
 } tamd_cmd;
 
 /* A transfer between host memory and an arena row: upload (host -> row) or read (row -> host).

@@ -34,10 +34,11 @@ bool Server::init(Device& dev, unsigned workers, unsigned ring_size, double idle
     workers_ = workers ? workers : 1;
     idle_ticks_ = (uint64_t)(idle_ms * 1e5);  // s_memrealtime: 100 MHz
     if (const char* e = getenv("TONK_AMD_SERVE_DEBUG")) debug_ = (uint32_t)atoi(e);
+    stamps_ = getenv("TONK_AMD_CAPI_WATCH") != nullptr;
     ring_ = (tamd_serve_slot*)coherent_alloc((size_t)ring_size_ * sizeof(tamd_serve_slot));
     host_ = (volatile tamd_serve_host*)coherent_alloc(sizeof(tamd_serve_host));
     if (!ring_ || !host_) return false;
-    const size_t dbytes = sizeof(tamd_serve_dev) + (size_t)ring_size_ * (8 + sizeof(tamd_serve_entry));
+    const size_t dbytes = sizeof(tamd_serve_dev) + (size_t)ring_size_ * sizeof(tamd_serve_slot);
     if (hipMalloc((void**)&dstate_, dbytes) != hipSuccess) return false;
     int least = 0, greatest = 0;
     hipDeviceGetStreamPriorityRange(&least, &greatest);
@@ -84,7 +85,10 @@ bool Server::launch_locked(uint64_t tail0) {
     a.ring_mask = ring_size_ - 1;
     a.wl_mask = ring_size_ - 1;
     a.gen = gen_.load() + 1;
-    a.pad = debug_;
+    // (A/B bits of TONK_AMD_SERVE_DEBUG >> 2: 1 no release fence before the completion word,
+    // 2 the dispatcher polls one slot at a time, 4 commands copied with plain 16-byte loads,
+    // 8 reads stored with system-scope 8-byte stores)
+    a.pad = debug_ >> 2;
     // the instance's claim counter and quit flag start from zero (stream order: after the
     // previous instance has ended)
     if (hipMemsetAsync(dstate_, 0, sizeof(tamd_serve_dev), st) != hipSuccess) return false;
@@ -153,8 +157,17 @@ bool Server::build(CmdBuf& b, const std::vector<Device::HostCopy>& up, const Pro
     c->n_instr = n_instr;
     c->n_ops = n_ops;
     tamd_xfer* xu = (tamd_xfer*)(base + off_up);
-    for (size_t i = 0; i < up.size(); ++i)
+    uint64_t chunks = 0;
+    bool ordered = true;
+    for (size_t i = 0; i < up.size(); ++i) {
         xu[i] = tamd_xfer{(uint64_t)(uintptr_t)up[i].host, (uint32_t)(up[i].arena_off / 64), up[i].len};
+        chunks += (up[i].len + 15u) / 16u;
+        if (i && (uintptr_t)up[i].host < (uintptr_t)up[i - 1].host + up[i - 1].len) ordered = false;
+    }
+    if (!up.empty() && ordered) {
+        const uint64_t span = ((uintptr_t)up.back().host + up.back().len + 15u - (uintptr_t)up[0].host) / 16u;
+        if (span <= 2 * chunks + 64 && span < (1u << 24)) c->up_chunks = (uint32_t)span;
+    }
     tamd_xfer* xr = (tamd_xfer*)(base + off_rd);
     for (size_t i = 0; i < rd.size(); ++i)
         xr[i] = tamd_xfer{(uint64_t)(uintptr_t)rd[i].host, (uint32_t)(rd[i].arena_off / 64), rd[i].len};
@@ -181,6 +194,7 @@ bool Server::build(CmdBuf& b, const std::vector<Device::HostCopy>& up, const Pro
     uint32_t* hi = (uint32_t*)(base + off_items);
     const std::vector<tamd_op>& ops = pb->ops();
     const std::vector<uint32_t>& lv = pb->op_levels();
+    const std::vector<uint8_t>& pure = pb->op_pure();
     for (size_t i = 0; i < ops.size(); ++i) {
         const uint32_t k = lv[i];
         const uint32_t oi = op_fill[k]++;
@@ -188,9 +202,11 @@ bool Server::build(CmdBuf& b, const std::vector<Device::HostCopy>& up, const Pro
         const uint32_t slices = op_slices(ops[i].span);
         uint32_t ii = item_fill[k];
         item_fill[k] += slices;
+        // (bit 31 of the slice word: a pure combine, whose row batches a group of waves may split)
+        const uint32_t share = pure[i] ? 0x80000000u : 0u;
         for (uint32_t s = 0; s < slices; ++s, ++ii) {
             hi[2 * ii] = oi;
-            hi[2 * ii + 1] = s;
+            hi[2 * ii + 1] = s | share;
         }
     }
     return true;
@@ -207,20 +223,36 @@ void Server::post(CmdBuf& b) {
         }
         _mm_pause();
     }
-    s->cmd = (uint64_t)(uintptr_t)b.cmd();
-    s->done = (uint64_t)(uintptr_t)b.done();
-    s->done_val = idx + 1;
-    s->cmd_bytes = b.cmd()->bytes;
-    __atomic_store_n(&s->seq, idx + 1, __ATOMIC_RELEASE);
+    // six tagged granules, 8-byte stores (each one atomic): the dispatcher takes the slot once
+    // every tag is this command's
+    const uint64_t cmd = (uint64_t)(uintptr_t)b.cmd(), done = (uint64_t)(uintptr_t)b.done();
+    volatile uint64_t* g = s->g;
+    g[0] = tamd_granule(idx, (uint32_t)cmd);
+    g[1] = tamd_granule(idx, (uint32_t)(cmd >> 32));
+    g[2] = tamd_granule(idx, (uint32_t)done);
+    g[3] = tamd_granule(idx, (uint32_t)(done >> 32));
+    g[4] = tamd_granule(idx, (uint32_t)(idx + 1));
+    g[5] = tamd_granule(idx, b.cmd()->bytes);
     b.ticket = idx;
     b.busy = true;
+    if (stamps_) {
+        b.posted_us = now_us();
+        const tamd_cmd* c = b.cmd();
+        std::lock_guard<std::mutex> lk(stamp_mu_);
+        shape_[0] += c->levels;
+        shape_[1] += c->n_items;
+        shape_[2] += c->n_instr;
+        shape_[3] += c->n_up;
+        shape_[4] += c->bytes;
+        shape_n_++;
+    }
     posted.fetch_add(1, std::memory_order_relaxed);
     std::atomic_thread_fence(std::memory_order_seq_cst);
     if (host_->exited_gen == gen_.load()) ensure_running();
 }
 
 bool Server::wait(CmdBuf& b) {
-    const uint64_t want = b.ticket + 1;
+    const uint64_t want = (uint32_t)(b.ticket + 1);  // (the worker stores the 32-bit tag)
     volatile uint64_t* d = b.done();
     if (*d == want) {
         b.busy = false;
@@ -260,8 +292,37 @@ bool Server::wait(CmdBuf& b) {
     }
     std::atomic_thread_fence(std::memory_order_acquire);
     b.busy = false;
-    gpu_ns_sum += (d[2] - d[1]) * 10;
+    if (stamps_) {  // (watchdog: where a command's time goes, 100 MHz stamps -> ns)
+        const double wall = now_us() - b.posted_us;
+        std::lock_guard<std::mutex> lk(stamp_mu_);
+        phase_ns_[0] += (d[3] - d[1]) * 10;  // start -> command in LDS
+        phase_ns_[1] += (d[4] - d[3]) * 10;  // -> packets landed
+        phase_ns_[2] += (d[5] - d[4]) * 10;  // -> program run
+        phase_ns_[3] += (d[6] - d[5]) * 10;  // -> reads written
+        phase_ns_[4] += (d[2] - d[6]) * 10;  // -> completion stored (fence)
+        phase_ns_[5] += (uint64_t)(wall * 1e3) - (d[2] - d[1]) * 10;  // host wall outside the worker
+        phase_n_++;
+    }
+    gpu_ns_sum.fetch_add((d[2] - d[1]) * 10, std::memory_order_relaxed);
     return true;
+}
+
+std::string Server::phase_report() {
+    std::lock_guard<std::mutex> lk(stamp_mu_);
+    if (!phase_n_) return std::string();
+    char b[320];
+    const double n = (double)phase_n_ * 1e3;
+    snprintf(b, sizeof(b), "commands %llu, us each: copy %.2f land %.2f program %.2f reads %.2f fence+done %.2f; host wall outside the worker %.2f",
+             (unsigned long long)phase_n_, phase_ns_[0] / n, phase_ns_[1] / n, phase_ns_[2] / n, phase_ns_[3] / n,
+             phase_ns_[4] / n, phase_ns_[5] / n);
+    std::string r = b;
+    if (shape_n_) {
+        const double k = (double)shape_n_;
+        snprintf(b, sizeof(b), "; per command: levels %.2f items %.1f instrs %.1f packets landed %.1f bytes %.0f",
+                 shape_[0] / k, shape_[1] / k, shape_[2] / k, shape_[3] / k, shape_[4] / k);
+        r += b;
+    }
+    return r;
 }
 
 void Server::stop() {

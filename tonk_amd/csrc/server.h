@@ -14,6 +14,7 @@
 #include <atomic>
 #include <mutex>
 #include <stdint.h>
+#include <string>
 #include <vector>
 
 namespace tamd {
@@ -23,6 +24,7 @@ struct CmdBuf {
     uint8_t* mem = nullptr;
     size_t cap = 0;
     uint64_t ticket = 0;   // ring index of the command in flight from this buffer
+    double posted_us = 0;  // (watchdog stamps)
     bool busy = false;     // posted and not yet waited for
     static const size_t kHead = 128;
     volatile uint64_t* done_at = nullptr;  // completion words (null: the buffer's head)
@@ -49,10 +51,11 @@ public:
     bool wait(CmdBuf& b);
     bool settle(CmdBuf& b) { return b.busy ? wait(b) : true; }
     void stop();  // process exit: the executor ends and the stream drains (bounded wait)
+    std::string phase_report();  // (watchdog) mean time per command phase
 
     // counters for the C ABI's watchdog
     std::atomic<uint64_t> posted{0}, launches{0}, waits_slow{0};
-    uint64_t gpu_ns_sum = 0;  // (unsynchronised: diagnostics)
+    std::atomic<uint64_t> gpu_ns_sum{0};  // executor time of the commands waited for
 
 private:
     bool ok_ = false;
@@ -67,9 +70,13 @@ private:
     std::mutex launch_mu_;
     std::atomic<uint32_t> gen_{0};  // generation of the instance launched last
     void ensure_running();
-    uint32_t debug_ = 0;  // TONK_AMD_SERVE_DEBUG bits (diagnostics): 1 probe's completion words in
-                          // the server's own coherent page, 2 no release fence before them
+    uint32_t debug_ = 0;  // TONK_AMD_SERVE_DEBUG bits (diagnostics): 1 the probe's completion words in
+                          // the server's own coherent page, 4 a release fence before every completion word
     uint64_t* dbg_done_ = nullptr;
+    bool stamps_ = false;
+    std::mutex stamp_mu_;
+    uint64_t phase_ns_[6] = {0, 0, 0, 0, 0, 0}, phase_n_ = 0;
+    uint64_t shape_[5] = {0, 0, 0, 0, 0}, shape_n_ = 0;
     bool launch_locked(uint64_t tail0);
 };
 
