@@ -754,13 +754,16 @@ def main() -> int:
         if topo:
             lists = topo.split(";")
             cores = tonk_amd.cpu_share(lists, local_rank, lists[local_rank], os.environ.get("TONK_AMD_CPU_SLOT"))
-        bases = d.gather([float(stream_base(rank)), float(rank), float(local_rank)] + pad_cores(cores))
+        # a share smaller than the pool shrinks the pool to one worker per core (the session does
+        # the same, tamd_session_create): fewer workers, never two on one core
+        workers = min(host_threads(local_world), len(cores)) if cores else host_threads(local_world)
+        bases = d.gather([float(stream_base(rank)), float(rank), float(local_rank), float(workers)] + pad_cores(cores))
         nan = float("nan")
         per_rank = d.gather([float(rank), nan, nan, nan, nan, nan])  # (the same gather as a measured run)
         if rank == 0:
             print(json.dumps({"dry_run": True, "n_gpus": world, "streams_per_gpu": STREAMS_PER_GPU,
                               "ranks": [{"rank": int(v[1]), "local_rank": int(v[2]), "stream_base": int(v[0]),
-                                         "host_cores": unpad_cores(v[3:])} for v in bases],
+                                         "host_threads": int(v[3]), "host_cores": unpad_cores(v[4:])} for v in bases],
                               "per_gpu": per_gpu_entries(per_rank)}), file=line_out, flush=True)
         d.close()
         return 0
@@ -779,7 +782,8 @@ def main() -> int:
                             stream_base=stream_base(rank), threads=threads,
                             arena_bytes=(2 * pool * STREAMS_PER_GPU * 1344) + (4 << 30), input_pool=pool)
     sess.generate()
-    rank_cores = d.gather(pad_cores(sess.cpus()))
+    sess_cpus = sess.cpus()
+    rank_cores = d.gather(pad_cores(sess_cpus))
 
     for _ in range(a.warmup * PROGRAMS_PER_STEP):
         sess.step(ORIGINALS_PER_STEP)
@@ -852,7 +856,7 @@ def main() -> int:
             "workload": workload,
             "streams_per_gpu": STREAMS_PER_GPU, "originals_per_step": ORIGINALS_PER_STEP * PROGRAMS_PER_STEP,
             "originals_per_program": ORIGINALS_PER_STEP, "payload_bytes": PAYLOAD, "input_pool_per_stream": pool,
-            "loss": loss, "ack_every": ACK, "host_threads_per_gpu": threads,
+            "loss": loss, "ack_every": ACK, "host_threads_per_gpu": len(sess_cpus) or threads,
             "parallelism": f"streams sharded {STREAMS_PER_GPU}/GPU x {world} GPU, no collective",
             # each rank's pinned worker cores (its share of its GPU's NUMA node, tamd_cpu_share)
             "host_cores": [unpad_cores(v) for v in rank_cores],

@@ -127,3 +127,38 @@ def test_bench_dry_run_core_plan_disjoint():
     c0, c1 = (x["host_cores"] for x in j["ranks"])
     assert c0 == list(range(16)) and c1 == list(range(16, 32))
     assert not set(c0) & set(c1)
+
+
+# The same node with fewer usable cores: 48 per socket (the rest reserved), i.e. 12 per GPU.
+SMALL0 = ",".join(str(c) for c in range(48))
+SMALL1 = ",".join(str(c) for c in range(64, 112))
+SMALL = [SMALL0] * 4 + [SMALL1] * 4
+
+
+def test_cpu_share_fewer_cores_per_gpu():
+    """Twelve usable cores per GPU: every rank's share is 12 cores of its own socket, disjoint."""
+    import tonk_amd
+    shares = [tonk_amd.cpu_share(SMALL, d, SMALL[d]) for d in range(8)]
+    assert [len(s) for s in shares] == [12] * 8
+    flat = [c for s in shares for c in s]
+    assert len(flat) == len(set(flat)) == 96
+    assert all(set(s) <= (set(range(48)) if d < 4 else set(range(64, 112))) for d, s in enumerate(shares))
+
+
+def test_bench_dry_run_degrades_to_fewer_workers():
+    """`bench.py --gpus 2 --dry-run` on a node with 12 usable cores per GPU: each rank plans 12
+    workers (one per core of its share, never two on one core) instead of 16, and reports them."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
+    env["TONK_AMD_TOPOLOGY"] = ";".join(SMALL)
+    env["OMP_NUM_THREADS"] = "16"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dry-run"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    j = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    r0, r1 = j["ranks"]
+    assert r0["host_cores"] == list(range(12)) and r1["host_cores"] == list(range(12, 24))
+    # bench.host_threads: at most 16, and this process's CPUs split between the two ranks
+    pool = max(1, min(16, len(os.sched_getaffinity(0)) // 2))
+    assert r0["host_threads"] == r1["host_threads"] == min(pool, 12)

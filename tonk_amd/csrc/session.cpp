@@ -1166,7 +1166,16 @@ void* tamd_session_create(const tamd_session_params* p, char* err, size_t err_le
     // (the D2H gather right after a program needs all of its levels) and for A/B runs.  A
     // program stays in flight for as many launches as it has levels: 6 staging slots.
     const bool pipe = !p->stage_host && getenv("TONK_AMD_NO_PIPELINE") == nullptr;
-    const uint32_t nthreads = p->n_threads ? (p->n_threads < p->n_streams ? p->n_threads : p->n_streams) : 1;
+    uint32_t nthreads = p->n_threads ? (p->n_threads < p->n_streams ? p->n_threads : p->n_streams) : 1;
+    // The worker pool's cores: this GPU's share of its NUMA node (device_local_cpus).  A share
+    // smaller than the pool (a node with fewer usable cores per GPU than workers) shrinks the pool
+    // to one worker per core rather than putting two workers on one core: the rank's rate then
+    // degrades in proportion to its cores, and config.host_cores shows them.
+    std::vector<int> share;
+    if (nthreads > 1) {
+        share = device_local_cpus((int)p->device);
+        if (!share.empty() && share.size() < nthreads) nthreads = (uint32_t)share.size();
+    }
     // The free-running schedule (worker threads, pipelined levels): programs assembled in
     // parallel (Device::add_part) in 8 slots -- up to fr_ahead open, the rest in flight; otherwise
     // one laid-out program per step in 6 slots (TONK_AMD_PASSES=1 keeps the pass schedule).
@@ -1200,7 +1209,7 @@ void* tamd_session_create(const tamd_session_params* p, char* err, size_t err_le
     s->deferred = pipe && getenv("TONK_AMD_NO_DEFER") == nullptr;
     Session* raw = s.get();
     if (nthreads > 1 || s->fr_mode) {
-        raw->cpus = idle_cpus(device_local_cpus((int)p->device), nthreads);
+        raw->cpus = idle_cpus(share.empty() ? device_local_cpus((int)p->device) : share, nthreads);
         raw->threads_wanted = nthreads;
         for (uint32_t t = 0; t < nthreads; ++t) raw->threads.emplace_back([raw, t] { raw->pool_loop(t); });
     }
