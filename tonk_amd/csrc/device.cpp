@@ -36,6 +36,10 @@ extern "C" __global__ void tamd_verify_rows(const VerifyDescDev*, uint32_t, cons
 
 namespace tamd {
 
+namespace {
+int g_pin_device = -1;  // the device pinned slabs are mapped for (Device::init): bound before their HIP calls
+}
+
 // With the C ABI watchdog on (TONK_AMD_CAPI_WATCH), every runtime call through HIPCHK / HIPT
 // that blocks for 10 ms or more is named on stderr.
 static bool hip_watch() {
@@ -221,6 +225,7 @@ bool Device::init(int device, uint64_t arena_bytes) {
         return false;
     }
     device_ = device;
+    g_pin_device = device;
     // Persistent grid: exactly the workgroups that are resident at once (occupancy x CUs), so
     // every workgroup stages the GF tables once and no workgroup starts late (kernels.hip).
     int per_cu = 0;
@@ -1278,6 +1283,7 @@ std::vector<void*> g_spare_slabs;  // mapped and warmed ahead (host_prefill)
 // allocation has been seen to block for ~80 ms, which should not happen under the device lock.
 void* new_slab() {
     void* p = nullptr;
+    if (g_pin_device >= 0) hipSetDevice(g_pin_device);  // (a codec thread may not have bound it yet)
     const auto t0 = std::chrono::steady_clock::now();
     // (coherent: the persistent executor reads staged packets and commands, and writes results and
     // completion words, while the host works on the same pages -- server.h)
@@ -1303,15 +1309,24 @@ void Device::host_prefill(unsigned slabs) {
 }
 
 bool Device::host_reserve(size_t bytes) {
-    std::lock_guard<std::mutex> g(g_pin_mu);
-    // (one slab at a time: the current one is only replaced once used up)
-    if (g_slab && g_slab_used + bytes <= kPinSlab) return true;
     void* p = nullptr;
-    if (!g_spare_slabs.empty()) {
-        p = g_spare_slabs.back();
-        g_spare_slabs.pop_back();
-    } else if (!(p = new_slab())) {
-        return false;
+    {
+        std::lock_guard<std::mutex> g(g_pin_mu);
+        // (one slab at a time: the current one is only replaced once used up)
+        if (g_slab && g_slab_used + bytes <= kPinSlab) return true;
+        if (!g_spare_slabs.empty()) {
+            p = g_spare_slabs.back();
+            g_spare_slabs.pop_back();
+        }
+    }
+    // A new slab is mapped and warmed outside the mutex (hipHostMalloc and its copies can take
+    // tens of ms, which under the mutex would stall every codec allocating meanwhile), then
+    // published under it; a thread that lost the race parks its slab as a spare.
+    if (!p && !(p = new_slab())) return false;
+    std::lock_guard<std::mutex> g(g_pin_mu);
+    if (g_slab && g_slab_used + bytes <= kPinSlab) {
+        g_spare_slabs.push_back(p);
+        return true;
     }
     if (g_slab) {  // the rest of the old slab becomes free blocks
         for (unsigned c = 63; c >= 12; --c)
