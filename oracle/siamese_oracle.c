@@ -482,7 +482,9 @@ enum { R_LANE3 = 1, R_CAUCHY = 2, R_CONST = 3, R_MULTI = 4, R_DENSE = 5 };
            kind CAUCHY: acc_a ^= CauchyElement(p, col_k mod 64)*row_k, kind CONST: acc_a ^= row_k
            DENSE: then COEFS w0 = 10, o[0:32], o[32:48] | rx << 16: with b = (o >> 6*(col_k mod 8)) & 63
            and cx = CX(col_k), acc_0 ^= (b0 ^ b1 cx ^ b2 cx^2 ^ rx (b3 ^ b4 cx ^ b5 cx^2)) * row_k, the
-           lane-sum combination of a Siamese row (SiameseEncoder.cpp:1046-1098) packet by packet */
+           lane-sum combination of a Siamese row (SiameseEncoder.cpp:1046-1098) packet by packet;
+           with p = 2 or 3 targets: p COEFS words (cap = ADJ words | hi << 16), each followed by its
+           ADJ words, target t adding rows k < hi_t into acc_t (rows of nested sum ranges) */
 int oracle_run_program(uint8_t* arena, size_t arena_bytes,
                        const uint32_t* ops, unsigned n_ops,
                        const uint32_t* instrs, unsigned n_instrs)
@@ -533,7 +535,44 @@ int oracle_run_program(uint8_t* arena, size_t arena_bytes,
                     if (k + 2 >= count) { free(acc); return -15; }
                     tg = w + 8;
                     if ((tg[0] & 0xff) != (mode == R_MULTI ? I_TARGETS : I_COEFS)) { free(acc); return -16; }
-                    if (mode == R_DENSE && k + 2 + tg[3] >= count) { free(acc); return -18; }
+                    if (mode == R_DENSE && p < 2 && k + 2 + tg[3] >= count) { free(acc); return -18; }
+                }
+                if (mode == R_DENSE && p >= 2) {
+                    /* p targets: COEFS_t (cap = ADJ words | hi << 16) + its ADJ words each; target t
+                       takes rows e < hi_t into acc_t */
+                    const uint32_t* cw[3] = { NULL, NULL, NULL };
+                    uint32_t at = k + 2;
+                    if (p > 3) { free(acc); return -19; }
+                    for (uint32_t t = 0; t < p; ++t) {
+                        if (at >= count) { free(acc); return -20; }
+                        cw[t] = instrs + 4 * (size_t)(first + at);
+                        if ((cw[t][0] & 0xff) != I_COEFS) { free(acc); return -21; }
+                        at += 1 + (cw[t][3] & 0xffffu);
+                    }
+                    if (at > count) { free(acc); return -22; }
+                    for (uint32_t e = 0; e < n; ++e) {
+                        const size_t base = ((size_t)w[1] + (size_t)e * stride) * 64u;
+                        const unsigned col = (unsigned)(((uint64_t)col0 + (uint64_t)e * cstep) % 0x400000u);
+                        if (base + len > arena_bytes) { free(acc); return -13; }
+                        const uint8_t cx = oracle_column_value(col), cx2 = oracle_gf_sqr(cx);
+                        for (uint32_t t = 0; t < p; ++t) {
+                            if (e >= (cw[t][3] >> 16)) continue;
+                            const uint64_t ow = (uint64_t)cw[t][1] | ((uint64_t)(cw[t][2] & 0xffffu) << 32);
+                            const uint8_t rx = (uint8_t)(cw[t][2] >> 16);
+                            const unsigned b = (unsigned)(ow >> (6u * (col % 8u))) & 63u;
+                            const uint8_t sdir = (uint8_t)((b & 1u) ^ ((b & 2u) ? cx : 0u) ^ ((b & 4u) ? cx2 : 0u));
+                            const uint8_t tprod = (uint8_t)(((b >> 3) & 1u) ^ ((b & 16u) ? cx : 0u) ^ ((b & 32u) ? cx2 : 0u));
+                            uint8_t g = (uint8_t)(sdir ^ oracle_gf_mul(rx, tprod));
+                            for (uint32_t aw = 0; aw < (cw[t][3] & 0xffffu); ++aw)
+                                for (unsigned q = 0; q < 4; ++q) {
+                                    const uint32_t d = cw[t][4 + 4 * aw + q];
+                                    if ((d >> 16) == e) g ^= (uint8_t)(d >> 8);
+                                }
+                            if (g) oracle_muladd_mem(acc + (size_t)t * span, g, arena + base, len);
+                        }
+                    }
+                    k = at - 1;  /* the loop's ++k moves past the last ADJ word */
+                    continue;
                 }
                 for (uint32_t e = 0; e < n; ++e) {
                     const size_t base = ((size_t)w[1] + (size_t)e * stride) * 64u;

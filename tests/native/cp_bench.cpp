@@ -12,6 +12,7 @@
 #include <signal.h>
 #include <sys/time.h>
 #include <ucontext.h>
+#include <map>
 #include <memory>
 #include <malloc.h>
 #include <stdio.h>
@@ -132,6 +133,7 @@ static void dump_reads(Context& ctx) {
     const auto& ins = ctx.pb.instrs();
     const char* names[8] = {"acc", "lane3", "cauchy", "const", "multi", "dense", "cauchy_scaled", "acc3"};
     uint64_t rows[8] = {0}, bytes[8] = {0};
+    std::map<uint32_t, uint32_t> dense_rows;  // packet row -> DENSE runs reading it
     for (size_t k = 0; k < ins.size(); ++k) {
         const uint32_t kind = ins[k].w0 & 0xff;
         int m = -1;
@@ -144,11 +146,17 @@ static void dump_reads(Context& ctx) {
             n = ins[k].cap;
         }
         if (m < 0 || m > 7) continue;
+        if (m == TAMD_R_DENSE)
+            for (uint64_t j = 0; j < n; ++j) dense_rows[ins[k].row + j * ins[k + 1].row]++;
         rows[m] += n;
         bytes[m] += n * ins[k].len;
     }
     for (int m = 0; m < 8; ++m)
         if (rows[m]) fprintf(stderr, "reads %-14s rows %8llu  MB %8.2f\n", names[m], (unsigned long long)rows[m], bytes[m] / 1e6);
+    uint64_t hist[5] = {0, 0, 0, 0, 0};
+    for (const auto& kv : dense_rows) hist[kv.second < 4 ? kv.second : 4]++;
+    fprintf(stderr, "dense: %zu distinct packet rows; read by 1/2/3/4+ runs: %llu %llu %llu %llu\n", dense_rows.size(),
+            (unsigned long long)hist[1], (unsigned long long)hist[2], (unsigned long long)hist[3], (unsigned long long)hist[4]);
 }
 
 static void dump_levels(Context& ctx) {

@@ -33,6 +33,9 @@ static bool g_pipeline = false;
 static uint32_t g_expand = ~0u;  // expand=<terms>: the session's expansion limit
 static uint32_t g_backsub = ~0u;  // backsub=<unknowns>: back substitution over materialized rows
 static uint32_t g_split = 0;      // split=<packets>: the batched session's dense-range split
+static uint64_t g_rs[9];  // CP_READ_STATS totals
+static bool g_contig = false;  // contig=1: originals in rows reserved up front, in order, one range per
+                               // side and borrowed by the codecs (the batched session's layout)
 static uint32_t g_drain = 0;  // pipelined: complete every in-flight program after every g_drain-th (session record mode: 2)
 #include <map>
 #include <set>
@@ -173,7 +176,13 @@ struct Harness {
         arena.assign(g_arena_bytes, 0);
         enc = new Encoder(&ctx, row_bytes);
         dec = new Decoder(&ctx, row_bytes);
+        if (g_contig) {
+            const uint32_t cap = p.payload_max + 4;
+            for (int side = 0; side < 2; ++side)
+                for (uint32_t i = 0; i < p.n_originals; ++i) pre[side].push_back(ctx.alloc(cap));
+        }
     }
+    std::vector<RowId> pre[2];  // contig=1: the originals' rows of the encoder (0) and decoder (1)
     Encoder* E() {
         if (g_dirty) ctx.touch(enc);
         return enc;
@@ -189,10 +198,10 @@ struct Harness {
 
     uint8_t* at(RowId r) { return arena.data() + (size_t)ctx.rows.offset(r) * TAMD_ROW_UNIT; }
 
-    RowId write_original(uint32_t index, uint32_t len, uint32_t* framed, uint32_t* header) {
+    RowId write_original(uint32_t index, uint32_t len, uint32_t* framed, uint32_t* header, int side = 0) {
         uint8_t hdr[4];
         const uint32_t hb = put_length_header(len, hdr);
-        const RowId r = ctx.alloc(hb + len);
+        const RowId r = g_contig ? pre[side][index] : ctx.alloc(hb + len);
         if (r == kNoRow) return r;
         uint8_t* d = at(r);
         memset(d, 0, ctx.rows.cap_bytes(r));
@@ -236,6 +245,37 @@ struct Harness {
                 fprintf(stderr, "  op L%u c%u: %u instrs, %u rows (%u acc3, %u runs), %u stores, span %u\n",
                         lv[i] / TAMD_COST_CLASSES, lv[i] % TAMD_COST_CLASSES, o.count, rows, acc3, runs, stores, o.span);
             }
+        }
+        static const bool rstats = getenv("CP_READ_STATS") != nullptr;
+        if (rstats && !ops_v.empty()) {  // (diagnostics) rows read per run mode, and how many distinct
+            const auto& in = ctx.pb.instrs();
+            std::unordered_map<uint32_t, uint32_t> seen_dense, seen_all;
+            uint64_t reads[8] = {0, 0, 0, 0, 0, 0, 0, 0}, dense_ops = 0, dense_multi = 0;
+            std::vector<uint32_t> op_rows;
+            for (size_t i = 0; i < ops_v.size(); ++i) {
+                const tamd_op& o = ops_v[i];
+                bool has_dense = false;
+                for (uint32_t k = o.first; k < o.first + o.count; ++k) {
+                    const uint32_t kind = in[k].w0 & 0xff;
+                    if (kind == TAMD_I_ACC || kind == TAMD_I_ACC3) {
+                        reads[0]++;
+                        seen_all[in[k].row]++;
+                    } else if (kind == TAMD_I_ACCR) {
+                        const uint32_t mode = (in[k].w0 >> 8) & 0xff, stride = in[k + 1].row;
+                        for (uint32_t j = 0; j < in[k].cap; ++j) {
+                            reads[mode]++;
+                            seen_all[in[k].row + j * stride]++;
+                            if (mode == TAMD_R_DENSE) seen_dense[in[k].row + j * stride]++;
+                        }
+                        if (mode == TAMD_R_DENSE) has_dense = true;
+                    }
+                }
+                dense_ops += has_dense;
+            }
+            (void)dense_multi;
+            g_rs[0] += reads[0]; g_rs[1] += reads[TAMD_R_LANE3]; g_rs[2] += reads[TAMD_R_CAUCHY];
+            g_rs[3] += reads[TAMD_R_CONST]; g_rs[4] += reads[TAMD_R_MULTI]; g_rs[5] += reads[TAMD_R_DENSE];
+            g_rs[6] += seen_dense.size(); g_rs[7] += seen_all.size(); g_rs[8] += dense_ops;
         }
         if (!ops_v.empty()) {
             const int rc = oracle_run_program(arena.data(), arena.size(), sorted.data(),
@@ -292,8 +332,8 @@ struct Harness {
         uint32_t framed = 0, header = 0;
         const RowId r = write_original(index, len, &framed, &header);
         if (r == kNoRow) { error = "arena full"; return 5; }
-        const Result rc = E()->add(r, framed, header, len, nullptr, col);
-        if (rc != kSuccess) ctx.rows.free_deferred(r);
+        const Result rc = E()->add(r, framed, header, len, nullptr, col, g_contig);
+        if (rc != kSuccess && !g_contig) ctx.rows.free_deferred(r);
         if (batch && (index + 1) % batch == 0) flush();
         return rc;
     }
@@ -306,8 +346,9 @@ struct Harness {
             rows[j] = write_original(index + j, len, &framed, &header);
             if (rows[j] == kNoRow) { error = "arena full"; return false; }
         }
-        if (!E()->add_run(rows.data(), k, framed, header, len, false, col0)) {
-            for (RowId r : rows) ctx.rows.free_deferred(r);
+        if (!E()->add_run(rows.data(), k, framed, header, len, g_contig, col0)) {
+            if (!g_contig)
+                for (RowId r : rows) ctx.rows.free_deferred(r);
             return false;
         }
         if (batch && (index + k) / batch != index / batch) flush();
@@ -318,11 +359,12 @@ struct Harness {
         std::vector<RowId> rows(k);
         uint32_t framed = 0, header = 0;
         for (uint32_t j = 0; j < k; ++j) {
-            rows[j] = write_original(index + j, len, &framed, &header);
+            rows[j] = write_original(index + j, len, &framed, &header, 1);
             if (rows[j] == kNoRow) { error = "arena full"; return false; }
         }
-        if (!D()->add_run_inorder(col0, rows.data(), k, framed, header, len, false)) {
-            for (RowId r : rows) ctx.rows.free_deferred(r);
+        if (!D()->add_run_inorder(col0, rows.data(), k, framed, header, len, g_contig)) {
+            if (!g_contig)
+                for (RowId r : rows) ctx.rows.free_deferred(r);
             return false;
         }
         return true;
@@ -347,11 +389,11 @@ struct Harness {
     int enc_ack(const uint8_t* buf, uint32_t n, uint32_t* next) { return E()->acknowledge(buf, n, next); }
     int dec_add_original(uint32_t col, uint32_t index, uint32_t len) {
         uint32_t framed = 0, header = 0;
-        const RowId r = write_original(index, len, &framed, &header);
+        const RowId r = write_original(index, len, &framed, &header, 1);
         if (r == kNoRow) { error = "arena full"; return 5; }
         bool took = false;
-        const Result rc = D()->add_original(col, r, framed, header, len, nullptr, &took);
-        if (!took) ctx.rows.free_deferred(r);
+        const Result rc = D()->add_original(col, r, framed, header, len, nullptr, &took, g_contig);
+        if (!took && !g_contig) ctx.rows.free_deferred(r);
         return rc;
     }
     void recovery_lost(const RecRef& r) { ctx.rows.free_deferred(r.out.row); }
@@ -471,6 +513,7 @@ int main(int argc, char** argv) {
         else if (k == "expand") g_expand = (uint32_t)v;
         else if (k == "backsub") g_backsub = (uint32_t)v;
         else if (k == "split") g_split = (uint32_t)v;
+        else if (k == "contig") g_contig = v != 0;
         else if (parse_param(p, k, v)) {}
         else { fprintf(stderr, "bad key %s\n", k.c_str()); return 2; }
     }
@@ -497,6 +540,12 @@ int main(int argc, char** argv) {
     fprintf(stderr, "programs=%llu ops=%llu instrs=%llu levels=%llu live_rows=%zu pipelined_pairs=%llu\n",
             (unsigned long long)h.programs, (unsigned long long)h.ops, (unsigned long long)h.instrs,
             (unsigned long long)h.levels, h.ctx.rows.live_rows(), (unsigned long long)h.pipelined_pairs);
+    if (getenv("CP_READ_STATS"))
+        fprintf(stderr, "reads: acc %llu lane3 %llu cauchy %llu const %llu multi %llu dense %llu; distinct dense %llu, "
+                "distinct all %llu; ops with dense runs %llu\n",
+                (unsigned long long)g_rs[0], (unsigned long long)g_rs[1], (unsigned long long)g_rs[2],
+                (unsigned long long)g_rs[3], (unsigned long long)g_rs[4], (unsigned long long)g_rs[5],
+                (unsigned long long)g_rs[6], (unsigned long long)g_rs[7], (unsigned long long)g_rs[8]);
     if (!h.error.empty()) { fprintf(stderr, "error: %s\n", h.error.c_str()); return 6; }
     return 0;
 }

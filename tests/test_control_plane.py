@@ -28,7 +28,7 @@ SCENARIOS = ["c1_256_p3", "c2_4096_p1_ack64", "c2_4096_p1_noack", "c3_4096_p2_ac
              "rtx_restart_p1_ack4", "rtx_restart_p2_ack2"]
 MODES = [("sync", 0), ("batch", 1000), ("batch", 4096), ("sync-dirty", 0), ("batch-dirty", 1000),
          ("batch-pipe", 1000), ("batch-pipe", 4096), ("batch-pipedrain", 1000), ("batch-pipeexp", 512),
-         ("batch-pipesplit", 1000), ("sync-exp", 0)]
+         ("batch-pipesplit", 1000), ("sync-exp", 0), ("batch-pipecontig", 4096), ("batch-pipecontigsplit", 1000)]
 
 
 @pytest.fixture(scope="module")
@@ -56,11 +56,15 @@ def test_control_plane_matches_reference(harness, golden_index, tmp_path, name, 
     few = mode.endswith("exp")
     expand = 16 if few else 0xFFFFFFFF
     backsub = 2 if few else 0xFFFFFFFF
-    # the batched session splits direct dense ranges over 192 packets (Context::dense_split);
+    # the batched session splits direct dense ranges over 48 packets (Context::dense_split);
     # "-pipesplit" splits every range over 16, so most Siamese rows take the two-level form
-    split = 16 if mode.endswith("-pipesplit") else 192 if mode in ("batch-pipe", "batch-pipedrain") else 0
+    split = 16 if mode.endswith("split") else 48 if mode in ("batch-pipe", "batch-pipedrain", "batch-pipecontig") else 0
+    # "-pipecontig": every original in a row reserved up front, in order, borrowed by the codecs
+    # (the batched session's layout): windows are long segments, so Siamese rows read their sum
+    # ranges straight from the packets and consecutive ones are grouped (Encoder::defer_dense)
+    contig = int("contig" in mode)
     args = [harness, str(out), f"mode={base}", f"batch={batch}", f"dirty={dirty}", f"pipeline={pipe}",
-            f"drain={drain}", f"expand={expand}", f"backsub={backsub}", f"split={split}"] + sc["args"] + [
+            f"drain={drain}", f"expand={expand}", f"backsub={backsub}", f"split={split}", f"contig={contig}"] + sc["args"] + [
         f"seed_data={1000 + sid}", f"seed_loss={2000 + sid}"]
     r = subprocess.run(args, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
@@ -69,17 +73,19 @@ def test_control_plane_matches_reference(harness, golden_index, tmp_path, name, 
     assert got == want, first_diff(want, got)
 
 
+@pytest.mark.parametrize("contig", [0, 1])
 @pytest.mark.parametrize("batch_name,sid", [("cfg2_64x4096_p2_ack64", 0), ("cfg2_64x4096_p2_ack64", 37),
                                              ("cfg3_rank7_64x12288_p1_ack64", 448),
                                              ("cfg3_rank7_64x12288_p1_ack64", 511)])
-def test_control_plane_batch_streams(harness, golden_index, tmp_path, batch_name, sid):
+def test_control_plane_batch_streams(harness, golden_index, tmp_path, batch_name, sid, contig):
     """Streams of the multi-stream fixtures (BASELINE configs[2], the rank-7 shard of configs[3])
     through the control plane in the bench's batch mode, pipelined as the session launches it in
     record mode: transcript digest == reference's, no launch-order hazard."""
     import hashlib
     entry = golden_index["batches"][batch_name]
     out = tmp_path / "t.txt"
-    args = [harness, str(out), "mode=batch", "batch=4096", "dirty=0", "pipeline=1", "drain=2", "split=192"] + entry["args"] + [
+    args = [harness, str(out), "mode=batch", "batch=4096", "dirty=0", "pipeline=1", "drain=2", "split=48",
+            f"contig={contig}"] + entry["args"] + [
         f"seed_data={1000 + sid}", f"seed_loss={2000 + sid}"]
     r = subprocess.run(args, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]

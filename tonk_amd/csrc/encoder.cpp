@@ -70,6 +70,7 @@ StoredOriginal Encoder::view(uint32_t e) const {
 
 void Encoder::pre_flush() {
     emit_cauchy_group();
+    emit_dense_group();
     for (unsigned l = 0; l < kLanes; ++l) lanes_[l].sums.flush(ctx_->rows, ctx_->pb, ctx_->ex);
 }
 
@@ -787,104 +788,149 @@ void Encoder::add_dense(uint32_t row, uint32_t recovery_bytes, Sym& rec) {
 // packets of its sum range, so the row's dense part is one DENSE run per segment of that range
 // (program.h), each packet weighted by its lane's opcode combination -- no lane walk, snapshot
 // or carried sum.  Bytes are the same: a lane sum is its packets zero-padded to the longest, and
-// each packet is clipped to the recovery length as the sum would be.
-uint32_t Encoder::dense_direct_rows() const {
+// each packet is clipped to the recovery length as the sum would be.  The row's LDPC pair
+// columns (light_pairs) are folded into the runs' coefficients (ADJ words); a pair column no run
+// covers is read as a row of its own.
+//
+// Rows are queued (dgrp_) and emitted by emit_dense_group: rows of one sum range share its
+// packets, so up to three of them are one op per chunk, each packet loaded once for all.
+bool Encoder::defer_dense(uint32_t row, uint32_t recovery_bytes, const RecoveryOut& out) {
+    static const uint32_t max_group = getenv("TONK_AMD_NO_DENSE_GROUP") ? 1u : 3u;  // (A/B knob)
+    // A group's op is one work item per slice (one wave, or one workgroup in small launches), so
+    // its products per item are bounded as a lone row's are: packets per chunk x targets
+    static const uint32_t max_work = getenv("TONK_AMD_DENSE_WORK") ? (uint32_t)atoi(getenv("TONK_AMD_DENSE_WORK"))
+                                                                  : kDenseGroupWork;
     const uint32_t lo = sum_abs_start(), hi = base_ + count_;
-    uint32_t n = 0;
-    for (size_t i = seg_index_at(lo); i < segs_.size(); ++i) {
-        const Segment& sg = segs_[i];
-        if ((int32_t)(sg.first - hi) >= 0) break;
-        const uint32_t a = (int32_t)(sg.first - lo) > 0 ? sg.first : lo;
-        const uint32_t b = (int32_t)(sg.end() - hi) < 0 ? sg.end() : hi;
-        if ((int32_t)(b - a) > 0 && sg.bytes) n += b - a;
-    }
-    return n;
-}
-
-void Encoder::add_dense_direct(uint32_t row, uint32_t recovery_bytes, const std::vector<uint64_t>& pairs) {
-    uint64_t ops = 0;
-    for (unsigned l = 0; l < kLanes; ++l) ops |= (uint64_t)row_opcode(l, row) << (6 * l);
-    const uint8_t rx = row_value(row);
-    const uint32_t lo = sum_abs_start(), hi = base_ + count_;
-    ProgramBuilder& pb = ctx_->pb;
-    // A DENSE run over absolute elements [e0, e0 + k), with the pair columns that fall in it
-    // (pairs are sorted, runs come in element order: one cursor)
-    size_t pi = 0;
-    std::vector<uint32_t>& adj = adj_;
-    thread_local std::vector<uint64_t> loose;  // pair columns outside every run (read as rows)
-    loose.clear();
-    auto dense = [&](const Segment& sg, uint32_t j, uint32_t k, uint32_t len) {
-        const uint32_t e0 = sg.first + j;
-        adj.clear();
-        while (pi < pairs.size() && (int32_t)((uint32_t)(pairs[pi] >> 8) - e0) < 0) loose.push_back(pairs[pi++]);
-        while (pi < pairs.size() && (int32_t)((uint32_t)(pairs[pi] >> 8) - (e0 + k)) < 0) {
-            adj.push_back(((uint32_t)(pairs[pi] >> 8) - e0) << 16 | (uint32_t)(pairs[pi] & 0xffu) << 8);
-            ++pi;
-        }
-        pb.op_accr_dense(sg.off(j), sg.stride, k, len, col_add(sg.column0, j), ops, rx, adj.data(),
-                         (uint32_t)adj.size());
-    };
     const uint32_t split = ctx_->dense_split;
-    const uint32_t total = split ? dense_direct_rows() : 0;
-    if (split && total > split) {
-        // Partial sums of at most `split` packets each, closed before the row's own op: the
-        // caller's op (begun already, still empty) is set aside and reopened after them.
-        const uint32_t parts = (total + split - 1) / split, per = (total + parts - 1) / parts;
-        thread_local std::vector<RowId> partial;
-        partial.clear();
-        uint32_t left = 0;  // packets the current partial still takes
-        for (size_t i = seg_index_at(lo); i < segs_.size(); ++i) {
-            const Segment& sg = segs_[i];
-            if ((int32_t)(sg.first - hi) >= 0) break;
-            uint32_t a = (int32_t)(sg.first - lo) > 0 ? sg.first : lo;
-            const uint32_t b = (int32_t)(sg.end() - hi) < 0 ? sg.end() : hi;
-            if ((int32_t)(b - a) <= 0 || !sg.bytes) continue;
-            const uint32_t len = sg.bytes < recovery_bytes ? sg.bytes : recovery_bytes;
-            while (a != b) {
-                if (!left) {
-                    if (!partial.empty()) pb.finish_combine(partial.back(), recovery_bytes, nullptr, 0);
-                    const RowId t = ctx_->alloc_temp(recovery_bytes);
-                    if (t == kNoRow) { disabled_ = true; break; }
-                    partial.push_back(t);
-                    pb.begin_op();
-                    left = per;
-                }
-                const uint32_t k = std::min(b - a, left);
-                dense(sg, a - sg.first, k, len);
-                a += k;
-                left -= k;
-            }
-            if (disabled_) break;
-        }
-        if (!partial.empty()) pb.finish_combine(partial.back(), recovery_bytes, nullptr, 0);
-        pb.begin_op();  // the row's op again: the partials, then the caller's terms
-        for (RowId t : partial) pb.op_acc(t, 1, recovery_bytes);
-        add_loose_pairs(pairs, pi, loose);
-        sum_end_ = count_;
-        return;
-    }
+    const uint32_t rows = split && hi - lo > split ? split : hi - lo;
+    if (dgrp_n_ && (lo != dgrp_lo_ || recovery_bytes != dgrp_len_ || window_gen_ != dgrp_gen_ ||
+                    rows * (dgrp_n_ + 1) > max_work))
+        emit_dense_group();
+    // The range's runs (a superset of the queued rows' ranges: they share `lo` and end earlier)
+    std::vector<DenseRun>& runs = dgrp_runs_;
+    runs.clear();
     for (size_t i = seg_index_at(lo); i < segs_.size(); ++i) {
         const Segment& sg = segs_[i];
         if ((int32_t)(sg.first - hi) >= 0) break;
         const uint32_t a = (int32_t)(sg.first - lo) > 0 ? sg.first : lo;
         const uint32_t b = (int32_t)(sg.end() - hi) < 0 ? sg.end() : hi;
         if ((int32_t)(b - a) <= 0 || !sg.bytes) continue;
-        const uint32_t len = sg.bytes < recovery_bytes ? sg.bytes : recovery_bytes;
-        dense(sg, a - sg.first, b - a, len);
+        const uint32_t j = a - sg.first;
+        runs.push_back(DenseRun{sg.off(j), sg.stride, b - a, sg.bytes < recovery_bytes ? sg.bytes : recovery_bytes,
+                                col_add(sg.column0, j), a - lo});
     }
-    add_loose_pairs(pairs, pi, loose);
-    sum_end_ = count_;
+    if (!dgrp_n_) {
+        dgrp_lo_ = lo;
+        dgrp_len_ = recovery_bytes;
+        dgrp_gen_ = window_gen_;
+    }
+    DenseTarget& t = dgrp_[dgrp_n_];
+    t.row = out.row;
+    t.ops = 0;
+    for (unsigned l = 0; l < kLanes; ++l) t.ops |= (uint64_t)row_opcode(l, row) << (6 * l);
+    t.rx = row_value(row);
+    t.hi = hi - lo;
+    t.flen = out.footer_len;
+    memcpy(t.footer, out.footer, sizeof(t.footer));
+    // pair columns as (element - lo) << 8 | coefficient: those inside a run stay (ADJ words),
+    // the others are resolved to their rows now (the window may have moved on by emission)
+    t.pairs.clear();
+    t.loose.clear();
+    size_t ri = 0;
+    for (uint64_t pr : pairs_) {
+        const uint32_t e = (uint32_t)(pr >> 8), rel = e - lo;
+        while (ri < runs.size() && runs[ri].e0 + runs[ri].count <= rel) ++ri;
+        if (rel < t.hi && ri < runs.size() && runs[ri].e0 <= rel) {
+            t.pairs.push_back((uint64_t)rel << 8 | (pr & 0xffu));
+        } else {
+            const Segment& sg = seg_of(e - base_);
+            t.loose.push_back(Term{sg.row(e - sg.first), sg.bytes, (uint8_t)(pr & 0xffu)});
+        }
+    }
+    // partial sums: one per chunk of the range (none when it fits one)
+    const uint32_t chunks = split && t.hi > split ? (t.hi + split - 1) / split : 1u;
+    t.parts.clear();
+    for (uint32_t c = 1; chunks > 1 && c <= chunks; ++c) {
+        const RowId pr = ctx_->alloc_temp(recovery_bytes);
+        if (pr == kNoRow) return false;
+        t.parts.push_back(pr);
+    }
+    // the readers of the row see the level it will be written at (emission is within this program)
+    ctx_->rows.set_level(out.row, chunks > 1 ? 2 : 1);
+    if (++dgrp_n_ >= max_group) emit_dense_group();
+    return true;
 }
 
-// Pair columns no dense run covered (pairs[from..) and `loose`): plain row reads, as add_light.
-void Encoder::add_loose_pairs(const std::vector<uint64_t>& pairs, size_t from, const std::vector<uint64_t>& loose) {
-    auto one = [&](uint64_t p) {
-        const uint32_t e = (uint32_t)(p >> 8) - base_;
-        const Segment& sg = seg_of(e);
-        ctx_->pb.op_acc(sg.row(e + base_ - sg.first), (uint8_t)(p & 0xffu), sg.bytes);
-    };
-    for (uint64_t p : loose) one(p);
-    for (size_t i = from; i < pairs.size(); ++i) one(pairs[i]);
+void Encoder::emit_dense_group() {
+    const uint32_t n = dgrp_n_;
+    if (!n) return;
+    dgrp_n_ = 0;
+    ProgramBuilder& pb = ctx_->pb;
+    const uint32_t len = dgrp_len_, split = ctx_->dense_split;
+    const uint32_t total = dgrp_[n - 1].hi;  // the last (longest) range, relative to lo
+    const uint32_t step = split ? split : ~0u;
+    const uint32_t chunks = split && total > split ? (total + split - 1) / split : 1u;
+    const std::vector<DenseRun>& runs = dgrp_runs_;
+    size_t pc[3] = {0, 0, 0};  // per target: its next pair column
+    thread_local std::vector<uint32_t> adj[3];
+    size_t ri = 0;
+    for (uint32_t c = 0; c < chunks; ++c) {
+        const uint32_t c0 = c * step, c1 = total - c0 > step ? c0 + step : total;
+        uint32_t a0 = 0;  // targets a0 .. n-1 reach into this chunk (ranges are nested)
+        while (a0 < n && dgrp_[a0].hi <= c0) ++a0;
+        if (a0 == n) a0 = n - 1;  // (empty ranges: the stores still run)
+        const uint32_t nt = n - a0;
+        pb.begin_op();
+        for (; ri < runs.size() && runs[ri].e0 < c1; ++ri) {
+            const DenseRun& r = runs[ri];
+            const uint32_t pa = r.e0 > c0 ? r.e0 : c0, pe = r.e0 + r.count < c1 ? r.e0 + r.count : c1;
+            const uint32_t k = pe - pa;
+            ProgramBuilder::DenseCoefs tc[3];
+            for (uint32_t t = 0; t < nt; ++t) {
+                const DenseTarget& d = dgrp_[a0 + t];
+                const uint32_t h = d.hi > pa ? (d.hi - pa < k ? d.hi - pa : k) : 0u;
+                adj[t].clear();
+                while (pc[a0 + t] < d.pairs.size() && (uint32_t)(d.pairs[pc[a0 + t]] >> 8) < pa + h) {
+                    const uint64_t pr = d.pairs[pc[a0 + t]++];
+                    adj[t].push_back(((uint32_t)(pr >> 8) - pa) << 16 | (uint32_t)(pr & 0xffu) << 8);
+                }
+                tc[t] = ProgramBuilder::DenseCoefs{d.ops, d.rx, h, adj[t].data(), (uint32_t)adj[t].size()};
+            }
+            if (nt == 1) pb.op_accr_dense(r.off + (pa - r.e0) * r.stride, r.stride, k, r.len, col_add(r.col, pa - r.e0),
+                                          tc[0].ops, tc[0].rx, tc[0].adj, tc[0].nadj);
+            else pb.op_accr_dense_multi(r.off + (pa - r.e0) * r.stride, r.stride, k, r.len,
+                                        col_add(r.col, pa - r.e0), tc, nt);
+            if (pe < r.e0 + r.count) break;  // the run continues in the next chunk
+        }
+        // rows over one chunk are finished here (their loose pair columns included), the others
+        // store this chunk's partial sum
+        for (uint32_t t = 0; t < nt; ++t) {
+            const DenseTarget& d = dgrp_[a0 + t];
+            if (d.parts.empty())
+                for (const Term& x : d.loose) pb.op_acc(x.row, x.coef, x.len, t);
+        }
+        if (nt == 1) {
+            const DenseTarget& d = dgrp_[a0];
+            if (d.parts.empty()) pb.finish_combine(d.row, len, d.footer, d.flen);
+            else pb.finish_combine(d.parts[c], len, nullptr, 0);
+        } else {
+            for (uint32_t t = 0; t < nt; ++t) {
+                const DenseTarget& d = dgrp_[a0 + t];
+                if (d.parts.empty()) pb.op_store_shared(d.row, len, t, d.footer, d.flen);
+                else pb.op_store_shared(d.parts[c], len, t, nullptr, 0);
+            }
+            pb.end_op(1);
+        }
+    }
+    // rows over several chunks: their partial sums and loose pair columns (level 2)
+    for (uint32_t a = 0; a < n; ++a) {
+        const DenseTarget& d = dgrp_[a];
+        if (d.parts.empty()) continue;
+        pb.begin_op();
+        for (RowId p : d.parts) pb.op_acc(p, 1, len);
+        for (const Term& x : d.loose) pb.op_acc(x.row, x.coef, x.len);
+        pb.finish_combine(d.row, len, d.footer, d.flen);
+    }
 }
 
 // Encoder::AddLightColumns (SiameseEncoder.cpp:1100-1144).  The product half goes straight into
@@ -1000,11 +1046,8 @@ Result Encoder::encode(RecoveryOut& out) {
         out.data_len = recovery_bytes;
         out.row = ctx_->alloc(recovery_bytes + out.footer_len);
         if (out.row == kNoRow) { disabled_ = true; return kDisabled; }
-        ProgramBuilder& pb = ctx_->pb;
-        pb.begin_op();
-        add_dense_direct(row, recovery_bytes, pairs_);
-        pb.finish_combine(out.row, recovery_bytes, out.footer, out.footer_len);
-        if (disabled_) {  // a partial sum found no arena room: the row lacks dense runs, never emit it
+        if (!defer_dense(row, recovery_bytes, out)) {  // no arena room for its partial sums
+            disabled_ = true;
             ctx_->rows.free_deferred(out.row);
             out = RecoveryOut();
             return kDisabled;

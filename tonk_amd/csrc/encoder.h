@@ -79,9 +79,10 @@ struct Segment {
 class Encoder : public FlushClient {
 public:
     // Longer direct dense ranges are split (in contexts that ask for it, Context::dense_split):
-    // partial sums of at most this many packets, one pure combine each (level 1), added by the
-    // row's op (level 2), so no single work item walks hundreds of packets (a level's tail).
-    static const uint32_t kDenseSplit = 192;
+    // partial sums over chunks of this many packets from the range's start, one combine each
+    // (level 1), added by the row's op (level 2), so no single work item walks hundreds of
+    // packets (a level's tail).
+    static const uint32_t kDenseSplit = 48;
     Encoder(Context* ctx, uint32_t row_bytes, HostRelease release = nullptr, void* user = nullptr);
     ~Encoder();
 
@@ -232,17 +233,10 @@ private:
     Result generate_single(RecoveryOut& out);
     Result generate_cauchy(RecoveryOut& out);
     void add_dense(uint32_t row, uint32_t recovery_bytes, Sym& rec);
-    // (into the op under construction) the dense range's runs with the row's LDPC pair columns
-    // `pairs` (light_pairs) folded into their coefficients
-    void add_dense_direct(uint32_t row, uint32_t recovery_bytes, const std::vector<uint64_t>& pairs);
-    // Packets of the direct dense range (add_dense_direct's rows).
-    uint32_t dense_direct_rows() const;
     void add_light(uint32_t row, Sym& rec);
     // The same pair columns as (absolute element << 8 | coefficient), sorted by element.
     void light_pairs(uint32_t row, std::vector<uint64_t>& out);
-    void add_loose_pairs(const std::vector<uint64_t>& pairs, size_t from, const std::vector<uint64_t>& loose);
     std::vector<uint64_t> pairs_;
-    std::vector<uint32_t> adj_;
     Result emit(Sym& terms, uint32_t len, const RecoveryMeta& meta, RecoveryOut& out, bool distinct);
     Sym scratch_, rec_;
     struct Run { RowId row; uint32_t off, stride, count, len, col; };
@@ -264,13 +258,40 @@ private:
     // reads 27 % fewer window rows (cp_bench reads: 5998 -> 4366 per 4096 originals).
     static const uint32_t kGroupSpan = 160;
     // Siamese rows whose sum range is at most this many packets read it straight from the packets
-    // (add_dense_direct); longer ones through the running lane sums (TONK_AMD_DIRECT overrides).
+    // (defer_dense); longer ones through the running lane sums (TONK_AMD_DIRECT overrides).
     static const uint32_t kDirectMax = 512;
     static const uint32_t kDirectMinRun = 8;  // packets per run the direct reads need on average
     CauchyTarget grp_[3];
     uint32_t grp_n_ = 0, grp_gen_ = 0, window_gen_ = 0;
     std::vector<Run> grp_union_;
     void emit_cauchy_group();
+
+    // Up to three consecutive direct Siamese rows of one sum range are emitted together as one
+    // op per chunk (DENSE runs with targets, program.h).  Between two sum resets every row's range
+    // starts at the same element and ends at the window end of its encode, so the ranges are
+    // nested and the last row's runs are their union: each packet is read once for the group
+    // instead of once per row (a packet was read by ~4 rows on the headline workload).
+    struct DenseRun { uint32_t off, stride, count, len, col, e0; };  // e0: absolute first element
+    struct DenseTarget {
+        RowId row = kNoRow;
+        uint64_t ops = 0;            // lane opcodes, 6 bits each
+        uint32_t hi = 0, flen = 0;   // absolute end of the range; footer bytes
+        uint8_t rx = 0;
+        uint8_t footer[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        std::vector<uint64_t> pairs; // LDPC pair columns inside its runs: (element - lo) << 8 | coef
+        Sym loose;                   // the others, as rows
+        std::vector<RowId> parts;    // partial sums, one per chunk (ranges over one chunk: none)
+    };
+    // Packets x rows one group op may take per chunk (TONK_AMD_DENSE_WORK overrides): a chunk
+    // of 192 packets (kDenseSplit) is one row's work; its items are the level's longest.
+    static const uint32_t kDenseGroupWork = 144;
+    DenseTarget dgrp_[3];
+    uint32_t dgrp_n_ = 0, dgrp_lo_ = 0, dgrp_len_ = 0, dgrp_gen_ = 0;
+    std::vector<DenseRun> dgrp_runs_;  // the runs of [lo, hi) of the group's last row
+    // Queue `out.row` (allocated, footer set) with the group; false: no arena room for its
+    // partial sums (the codec is disabled).
+    bool defer_dense(uint32_t row, uint32_t recovery_bytes, const RecoveryOut& out);
+    void emit_dense_group();
 };
 
 uint64_t time_msec();

@@ -151,6 +151,7 @@ void ProgramBuilder::begin_op() {
     cur_full_ = ~0u;
     cur_runs_ = 0;
     cur_pure_ = true;
+    cur_multi_ = false;
     cur_level_in_ = 0;
     cur_written_begin_ = written_.size();
 }
@@ -251,6 +252,58 @@ void ProgramBuilder::op_accr_dense(uint32_t row0, uint32_t stride, uint32_t coun
     if (len > cur_span_) cur_span_ = len;
     if (len < cur_full_) cur_full_ = len;
     acc_bytes_ += (uint64_t)len * count;
+}
+
+void ProgramBuilder::op_accr_dense_multi(uint32_t row0, uint32_t stride, uint32_t count, uint32_t len,
+                                         uint32_t col0, const DenseCoefs* t, uint32_t nt) {
+    if (!len || !count || nt < 2 || nt > 3) return;
+    tamd_instr a, r;
+    a.w0 = tamd_w0(TAMD_I_ACCR, TAMD_R_DENSE, nt);
+    a.row = row0;
+    a.len = len;
+    a.cap = count;
+    r.w0 = TAMD_I_RANGE;
+    r.row = stride;
+    r.len = col0;
+    r.cap = 1;
+    instrs_.push_back(a);
+    instrs_.push_back(r);
+    for (uint32_t k = 0; k < nt; ++k) {
+        const uint32_t nwords = (t[k].nadj + 3) / 4;
+        tamd_instr g;
+        g.w0 = TAMD_I_COEFS;
+        g.row = (uint32_t)t[k].ops;
+        g.len = ((uint32_t)(t[k].ops >> 32) & 0xffffu) | (uint32_t)t[k].rx << 16;
+        g.cap = nwords | (t[k].hi < count ? t[k].hi : count) << 16;
+        instrs_.push_back(g);
+        for (uint32_t w = 0; w < nwords; ++w) {
+            uint32_t d[4] = {0, 0, 0, 0};
+            for (uint32_t q = 0; q < 4 && 4 * w + q < t[k].nadj; ++q) d[q] = t[k].adj[4 * w + q];
+            tamd_instr x;
+            x.w0 = (d[0] & ~0xffu) | TAMD_I_ADJ;
+            x.row = d[1];
+            x.len = d[2];
+            x.cap = d[3];
+            instrs_.push_back(x);
+        }
+    }
+    ++cur_runs_;
+    cur_multi_ = true;
+    if (len > cur_span_) cur_span_ = len;
+    if (len < cur_full_) cur_full_ = len;
+    acc_bytes_ += (uint64_t)len * count;
+}
+
+void ProgramBuilder::op_store_shared(RowId dst, uint32_t len, uint32_t acc, const uint8_t* footer,
+                                     uint32_t footer_len) {
+    const uint32_t cap = rows_->cap_bytes(dst);
+    push_store(instrs_, rows_->offset(dst), len, cap, footer, footer_len, acc);
+    if (acc) cur_multi_ = true;
+    if (cap > cur_span_) cur_span_ = cap;
+    if (len > cur_span_) cur_span_ = len;
+    if (len < cur_full_) cur_full_ = len;
+    written_.push_back(dst);
+    store_bytes_ += len + footer_len;
 }
 
 uint32_t ProgramBuilder::finish_combine(RowId dst, uint32_t len, const uint8_t* footer, uint32_t footer_len) {
@@ -371,7 +424,7 @@ uint32_t ProgramBuilder::end_op(uint32_t min_level) {
     const uint32_t cls = (cur_pure_ && rows >= 48) ? 0u : cost >= 64 ? 1u : cost >= 32 ? 2u : cost >= 12 ? 3u : 4u;
     const uint32_t bucket = TAMD_COST_CLASSES * level + cls;
     levels_.push_back(bucket);
-    pure_.push_back(cur_pure_ ? 1 : 0);
+    pure_.push_back(cur_pure_ ? (cur_multi_ ? 2 : 1) : 0);
     if (level_ops_.size() < TAMD_COST_CLASSES * (level + 1)) {
         level_ops_.resize(TAMD_COST_CLASSES * (level + 1), 0);
         level_items_.resize(TAMD_COST_CLASSES * (level + 1), 0);

@@ -185,6 +185,15 @@ public:
     // coefficient additions (ADJ words).
     void op_accr_dense(uint32_t row0, uint32_t stride, uint32_t count, uint32_t len, uint32_t col0, uint64_t ops,
                        uint8_t rx, const uint32_t* adj = nullptr, uint32_t nadj = 0);
+    // DENSE run for 2-3 rows at once (program.h): target t (COEFS word: lane opcodes `ops`, `rx`;
+    // rows i < hi of the run; ADJ additions adj[0..nadj)) accumulates into acc_t.  The op stays a
+    // shareable combine when it ends in op_store_shared stores only.
+    struct DenseCoefs { uint64_t ops; uint8_t rx; uint32_t hi; const uint32_t* adj; uint32_t nadj; };
+    void op_accr_dense_multi(uint32_t row0, uint32_t stride, uint32_t count, uint32_t len, uint32_t col0,
+                             const DenseCoefs* t, uint32_t nt);
+    // STORE (+FOOTER) of acc_a at the end of an op whose row batches waves may split: the executor
+    // reduces each stored accumulator across the waves (at most three stores, the op's last words).
+    void op_store_shared(RowId dst, uint32_t len, uint32_t acc, const uint8_t* footer, uint32_t footer_len);
     // Register a run of level-0 rows at offsets off0 + k * stride (k < count), columns col0 + k,
     // with per-row coefficients CauchyElement(p, column mod 64) (mode TAMD_R_CAUCHY) or 1
     // (TAMD_R_CONST), as one symbolic term (kRunFlag) of length len; combine() emits it as one
@@ -227,7 +236,9 @@ public:
     // Per op: its bucket, TAMD_COST_CLASSES * level + cost class (0 = most expensive).
     const std::vector<uint32_t>& op_levels() const { return levels_; }
     // Per op: 1 when it is a pure combine (ACC into acc_0, CONST/CAUCHY/DENSE runs, one final
-    // STORE + FOOTER) whose row batches several waves can split (partial sums reduced after).
+    // STORE + FOOTER) whose row batches several waves can split (partial sums reduced after);
+    // 2 when it is such a combine into up to three accumulators (multi-target DENSE runs, one
+    // STORE + FOOTER per accumulator).
     const std::vector<uint8_t>& op_pure() const { return pure_; }
     const std::vector<RowId>& written_rows() const { return written_; }
     // Per bucket (see op_levels): op count and work-item count (slice_bytes() chunks).
@@ -249,6 +260,7 @@ private:
     // op under construction
     uint32_t cur_first_ = 0, cur_span_ = 0, cur_level_in_ = 0, cur_full_ = ~0u, cur_runs_ = 0;
     bool cur_pure_ = true;  // only acc_0 sums and CONST/CAUCHY runs so far (see TAMD_COST_CLASSES)
+    bool cur_multi_ = false;  // (pure) multi-target DENSE runs: pure_ value 2
     struct RunRef { uint32_t mode, p, off0, stride, count, col0; };
     std::vector<RunRef> runs_;  // run terms of the pending program
     size_t cur_written_begin_ = 0;
@@ -489,7 +501,7 @@ struct Context {
     // extra level costs launches and saves no device bytes.
     uint32_t backsub_rows = ~0u;
     // Direct dense ranges longer than this are split into partial sums over two levels
-    // (Encoder::add_dense_direct; 0: never).  Only batched sessions split: there a long op is a
+    // (Encoder::defer_dense; 0: never).  Only batched sessions split: there a long op is a
     // launch's tail, while per-call programs (the C ABI) and single streams pay an extra level
     // launch in latency and already share a long op across a workgroup.
     uint32_t dense_split = 0;

@@ -279,6 +279,40 @@ __device__ __forceinline__ void lv_store_row(uint8_t* __restrict__ arena, uint32
     if constexpr (NH == 3) store_slice<WT>(arena, row, len, cap, footer, ox, x.h[2]);
 }
 
+// Rolling row loads over one wave's batches of a run: batch b (rows b*R .. b*R + R - 1) is
+// this wave's when (unit + b) mod nw == wid -- every batch when the wave runs the op alone, every
+// nw-th when nw waves share it.  The rows of the wave's next batch are loaded as soon as a half of
+// the current one has been combined, so a wave keeps 3-6 row loads in flight while it computes
+// instead of waiting a full memory round trip per batch.  body(i, v): row i's slice bytes.
+template <bool FULL, int NH, uint32_t R, class F>
+__device__ __forceinline__ void roll_rows(const uint8_t* rbase, size_t step, uint32_t lo, uint32_t lox,
+                                          uint32_t count, uint32_t o, uint32_t len, uint32_t ox, uint32_t& unit,
+                                          uint32_t nw, uint32_t wid, F&& body) {
+    const uint32_t nbat = (count + R - 1) / R;
+    const uint32_t b0 = (wid - unit) & (nw - 1u), jump = nw * R;
+    unit += nbat;
+    if (b0 >= nbat) return;
+    constexpr uint32_t H = R / 2;
+    LV<NH> d[R];
+    uint32_t e = b0 * R;
+#pragma unroll
+    for (uint32_t q = 0; q < R; ++q) d[q] = lv_load_at<NH>(rbase + (size_t)min(e + q, count - 1u) * step, lo, lox);
+    for (; e < count; e += jump) {
+        const bool more = e + jump < count;
+#pragma unroll
+        for (uint32_t h = 0; h < 2; ++h) {
+#pragma unroll
+            for (uint32_t q = h * H; q < (h ? R : H); ++q)
+                if (e + q < count) body(e + q, lv_keep<FULL, NH>(d[q], o, len, ox));
+            if (more) {
+#pragma unroll
+                for (uint32_t q = h * H; q < (h ? R : H); ++q)
+                    d[q] = lv_load_at<NH>(rbase + (size_t)min(e + jump + q, count - 1u) * step, lo, lox);
+            }
+        }
+    }
+}
+
 // ACCR: a strided run of equally long rows (program.h).  TAMD_RBATCH row loads are issued
 // together (the row index is clamped to the run, so no load is branched around); the per-row
 // table address stepping runs on the vector ALU: lane runs step the column value index
@@ -409,6 +443,62 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
 #undef TAMD_MULTI_TARGET
         unit += (count + TAMD_RBATCH - 1) / TAMD_RBATCH;
         return;
+    } else if (!LDSI && mode == TAMD_R_DENSE && p > 1u) {  // (not in tamd_serve: Server::build)
+        // p (2 or 3) Siamese rows of one encoder over nested sum ranges (program.h DENSE with
+        // targets): every packet of the run is loaded once and multiplied by each target's
+        // coefficient; target t takes rows i < hi_t into acc_t.  Coefficients as for one target
+        // (below), 64 rows at a time, the column value shared by the targets.
+        const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+        const uint8_t* sqr = (const uint8_t*)(lds + TAMD_LDS_INV + 64u);
+        // COEFS_t and its ADJ words: COEFS_0 is `tg`, the others follow the previous one's ADJ
+        const uint32_t n0 = tg.cap & 0xffffu;
+        const tamd_instr c1 = fetch_instr<LDSI>(adj, n0);
+        const uint32_t n1 = c1.cap & 0xffffu;
+        const tamd_instr c2 = p > 2u ? fetch_instr<LDSI>(adj, n0 + 1u + n1) : c1;
+        const uint32_t n2 = p > 2u ? c2.cap & 0xffffu : 0u;
+        const uint32_t* __restrict__ ad0 = (const uint32_t*)adj;
+        const uint32_t* __restrict__ ad1 = (const uint32_t*)(adj + n0 + 1u);
+        const uint32_t* __restrict__ ad2 = (const uint32_t*)(adj + n0 + n1 + 2u);
+        const uint32_t hi0 = tg.cap >> 16, hi1 = c1.cap >> 16, hi2 = p > 2u ? c2.cap >> 16 : 0u;
+        uint32_t cur0 = 0, cur1 = 0, cur2 = 0, gv0 = 0, gv1 = 0, gv2 = 0, gblk = ~0u;
+        // lane j's table indices for row 64 * gblk + j, one per target
+        auto block = [&](uint32_t i) __attribute__((always_inline)) {
+            gblk = i >> 6;
+            const uint32_t base = i & ~63u, mine = base + lane;
+            const uint32_t c = (col0 + mine * cstep) & (TAMD_COLUMN_PERIOD - 1u);
+            const uint32_t cx = 3u + (199u * (c % 253u)) % 253u, cx2 = sqr[cx], sh = 6u * (c & 7u);
+            // (the rx tables are read here, once per 64 rows, not kept across the rows)
+            auto one = [&](const tamd_instr& cw, const uint32_t* __restrict__ ad, uint32_t nadj,
+                           uint32_t& cur) __attribute__((always_inline)) -> uint32_t {
+                const PermT prx = perm_at(lds, ((cw.len >> 16) & 0xffu) * 8u);
+                const u64 opw = (u64)cw.row | ((u64)(cw.len & 0xffffu) << 32);
+                const uint32_t b = (uint32_t)(opw >> sh) & 63u;
+                const uint32_t sd = (b & 1u) ^ ((b & 2u) ? cx : 0u) ^ ((b & 4u) ? cx2 : 0u);
+                const uint32_t tp = ((b >> 3) & 1u) ^ ((b & 16u) ? cx : 0u) ^ ((b & 32u) ? cx2 : 0u);
+                uint32_t g = (sd ^ mul_sel(sel4(tp), prx)) & 0xffu;
+                for (; cur < 4u * nadj; ++cur) {
+                    const uint32_t d = LDSI ? uniform(ad[cur]) : ad[cur];
+                    if ((d >> 16) >= base + 64u) break;
+                    if ((d >> 16) == mine) g ^= (d >> 8) & 0xffu;
+                }
+                return g * 8u;
+            };
+            gv0 = one(tg, ad0, n0, cur0);
+            gv1 = one(c1, ad1, n1, cur1);
+            if (p > 2u) gv2 = one(c2, ad2, n2, cur2);
+        };
+        // row i (its slice bytes v) into every target whose range holds it, one product table
+        // live at a time
+        auto row = [&](uint32_t i, const LV<NH>& v) __attribute__((always_inline)) {
+            if ((i >> 6) != gblk) block(i);
+            const int l = (int)(i & 63u);
+            if (i < hi0) a0 ^= lv_mul<NH>(v, perm_at(lds, (uint32_t)__builtin_amdgcn_readlane((int)gv0, l)));
+            if (i < hi1) a1 ^= lv_mul<NH>(v, perm_at(lds, (uint32_t)__builtin_amdgcn_readlane((int)gv1, l)));
+            if (i < hi2) a2 ^= lv_mul<NH>(v, perm_at(lds, (uint32_t)__builtin_amdgcn_readlane((int)gv2, l)));
+        };
+        // (4-row batches: the three accumulators leave no registers for a fifth row in flight)
+        roll_rows<FULL, NH, 4>(rbase, step, lo, lox, count, o, len, ox, unit, nw, wid, row);
+        return;
     } else if (mode == TAMD_R_DENSE || (mode == TAMD_R_CAUCHY && (a.w0 >> 24) > 1u)) {
         // Rows with a per-row coefficient, then one product per byte:
         //  - DENSE: a Siamese row's dense part packet by packet (program.h); row k's coefficient
@@ -456,26 +546,11 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
             }
             return perm_at(lds, (uint32_t)__builtin_amdgcn_readlane((int)gv, (int)(i & 63u)));
         };
-        if (TAMD_ROLL && nw == 1u) {  // rolling loads, as for LANE3 runs
-            constexpr uint32_t H = TAMD_RBATCH / 2;
-            LV<NH> d[TAMD_RBATCH];
-#pragma unroll
-            for (uint32_t q = 0; q < TAMD_RBATCH; ++q) d[q] = TAMD_RUN_LD(min(q, count - 1u));
-            for (uint32_t e = 0; e < count; e += TAMD_RBATCH) {
-                const bool more = e + TAMD_RBATCH < count;
-#pragma unroll
-                for (uint32_t h = 0; h < 2; ++h) {
-#pragma unroll
-                    for (uint32_t q = h * H; q < (h ? TAMD_RBATCH : H); ++q)
-                        if (e + q < count) a0 ^= lv_mul<NH>(lv_keep<FULL, NH>(d[q], o, len, ox), row_tab(e + q));
-                    if (more) {
-#pragma unroll
-                        for (uint32_t q = h * H; q < (h ? TAMD_RBATCH : H); ++q)
-                            d[q] = TAMD_RUN_LD(min(e + TAMD_RBATCH + q, count - 1u));
-                    }
-                }
-            }
-            unit += (count + TAMD_RBATCH - 1) / TAMD_RBATCH;
+        if (TAMD_ROLL) {  // rolling loads over this wave's batches
+            roll_rows<FULL, NH, TAMD_RBATCH>(rbase, step, lo, lox, count, o, len, ox, unit, nw, wid,
+                                             [&](uint32_t i, const LV<NH>& v) __attribute__((always_inline)) {
+                                                 a0 ^= lv_mul<NH>(v, row_tab(i));
+                                             });
             return;
         }
         for (uint32_t e = 0; e < count; e += TAMD_RBATCH) {
@@ -492,30 +567,13 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
         uint32_t col = vgpr(col0);
         const uint32_t cs = vgpr(cstep), px = vgpr(p + 64u);
         const uint8_t* inv = (const uint8_t*)(lds + TAMD_LDS_INV);
-        if (TAMD_ROLL && nw == 1u) {  // rolling loads, as for LANE3 runs
-            constexpr uint32_t H = TAMD_RBATCH / 2;
-            LV<NH> d[TAMD_RBATCH];
-#pragma unroll
-            for (uint32_t q = 0; q < TAMD_RBATCH; ++q) d[q] = TAMD_RUN_LD(min(q, count - 1u));
-            for (uint32_t e = 0; e < count; e += TAMD_RBATCH) {
-                const bool more = e + TAMD_RBATCH < count;
-#pragma unroll
-                for (uint32_t h = 0; h < 2; ++h) {
-#pragma unroll
-                    for (uint32_t q = h * H; q < (h ? TAMD_RBATCH : H); ++q) {
-                        // the perm tables of inv((col mod 64) ^ (p + 64)), one LDS lookup
-                        const uint32_t ti = TAMD_LDS_CINV - 512u + (((col & 63u) ^ px) << 3);
-                        col += cs;
-                        if (e + q < count) a0 ^= lv_mul<NH>(lv_keep<FULL, NH>(d[q], o, len, ox), perm_at(lds, ti));
-                    }
-                    if (more) {
-#pragma unroll
-                        for (uint32_t q = h * H; q < (h ? TAMD_RBATCH : H); ++q)
-                            d[q] = TAMD_RUN_LD(min(e + TAMD_RBATCH + q, count - 1u));
-                    }
-                }
-            }
-            unit += (count + TAMD_RBATCH - 1) / TAMD_RBATCH;
+        if (TAMD_ROLL) {  // rolling loads over this wave's batches
+            roll_rows<FULL, NH, TAMD_RBATCH>(rbase, step, lo, lox, count, o, len, ox, unit, nw, wid,
+                                             [&](uint32_t i, const LV<NH>& v) __attribute__((always_inline)) {
+                                                 // the perm tables of inv((col mod 64) ^ (p + 64)), one LDS lookup
+                                                 const uint32_t ti = TAMD_LDS_CINV - 512u + ((((col + i * cs) & 63u) ^ px) << 3);
+                                                 a0 ^= lv_mul<NH>(v, perm_at(lds, ti));
+                                             });
             return;
         }
         for (uint32_t e = 0; e < count; e += TAMD_RBATCH) {
@@ -538,30 +596,13 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
     } else {
         const bool plain = p == 1u;
         const PermT cp = perm_at(lds, p * 8u);
-        if (TAMD_ROLL && nw == 1u) {
-            // rolling loads (as for LANE3 runs): the rows are summed as they arrive and the sum
-            // multiplied once (a parity row: p = 1, no multiply at all)
-            constexpr uint32_t H = TAMD_RBATCH / 2;
-            LV<NH> d[TAMD_RBATCH];
+        if (TAMD_ROLL) {
+            // rolling loads over this wave's batches: the rows are summed as they arrive and the
+            // sum multiplied once (a parity row: p = 1, no multiply at all)
             LV<NH> x = lv_zero<NH>();
-#pragma unroll
-            for (uint32_t q = 0; q < TAMD_RBATCH; ++q) d[q] = TAMD_RUN_LD(min(q, count - 1u));
-            for (uint32_t e = 0; e < count; e += TAMD_RBATCH) {
-                const bool more = e + TAMD_RBATCH < count;
-#pragma unroll
-                for (uint32_t h = 0; h < 2; ++h) {
-#pragma unroll
-                    for (uint32_t q = h * H; q < (h ? TAMD_RBATCH : H); ++q)
-                        if (e + q < count) x ^= lv_keep<FULL, NH>(d[q], o, len, ox);
-                    if (more) {
-#pragma unroll
-                        for (uint32_t q = h * H; q < (h ? TAMD_RBATCH : H); ++q)
-                            d[q] = TAMD_RUN_LD(min(e + TAMD_RBATCH + q, count - 1u));
-                    }
-                }
-            }
+            roll_rows<FULL, NH, TAMD_RBATCH>(rbase, step, lo, lox, count, o, len, ox, unit, nw, wid,
+                                             [&](uint32_t, const LV<NH>& v) __attribute__((always_inline)) { x ^= v; });
             a0 ^= plain ? x : lv_mul<NH>(x, cp);
-            unit += (count + TAMD_RBATCH - 1) / TAMD_RBATCH;
             return;
         }
         for (uint32_t e = 0; e < count; e += TAMD_RBATCH) {
@@ -590,7 +631,8 @@ template <bool FULL, int NH, uint32_t TAMD_BATCH, bool LDSI = false>
 __device__ __forceinline__ LV<NH> run_item(const tamd_instr* __restrict__ instrs, uint32_t first, uint32_t end,
                                            uint32_t o, uint32_t ox, uint32_t laneb, uint8_t* __restrict__ arena,
                                            const uint8_t* __restrict__ zrow, const uint32_t* __restrict__ lds,
-                                           uint32_t nw, uint32_t wid) {
+                                           uint32_t nw, uint32_t wid, LV<NH>* __restrict__ r1 = nullptr,
+                                           LV<NH>* __restrict__ r2 = nullptr) {
     LV<NH> a0 = lv_zero<NH>(), a1 = lv_zero<NH>(), a2 = lv_zero<NH>();  // the op's accumulators (program.h)
     uint32_t unit = 0;
     for (uint32_t k = first; k < end;) {
@@ -607,7 +649,14 @@ __device__ __forceinline__ LV<NH> run_item(const tamd_instr* __restrict__ instrs
             // COEFS.cap ADJ words)
             run_accr<FULL, NH, TAMD_BATCH, LDSI>(in[0], in[1], in[2], instrs + k + 3, o, ox, arena, lds, unit, nw, wid, a0,
                                            a1, a2);
-            const uint32_t rmode = (in[0].w0 >> 8) & 0xffu;
+            const uint32_t rmode = (in[0].w0 >> 8) & 0xffu, np = (in[0].w0 >> 16) & 0xffu;
+            if (rmode == TAMD_R_DENSE && np > 1u) {
+                // COEFS_t + its ADJ words for each of the np targets
+                uint32_t skip = 3u + (in[2].cap & 0xffffu);
+                for (uint32_t t = 1; t < np; ++t) skip += 1u + (fetch_instr<LDSI>(instrs, k + skip).cap & 0xffffu);
+                k += skip;
+                continue;
+            }
             k += rmode == TAMD_R_DENSE ? 3u + in[2].cap : rmode == TAMD_R_MULTI ? 3u : 2u;
             continue;
         }
@@ -664,6 +713,10 @@ __device__ __forceinline__ LV<NH> run_item(const tamd_instr* __restrict__ instrs
             }
         }
         k += nb;
+    }
+    if (r1) {  // (shared multi-target ops: the caller reduces acc_1 and acc_2 too)
+        *r1 = a1;
+        *r2 = a2;
     }
     return a0;
 }
@@ -726,19 +779,33 @@ __device__ __forceinline__ void exec_level(const tamd_segments& sg, const uint8_
         const uint32_t first = uniform(op.first), end = uniform(op.first + op.count);
         const bool full = s0 + MAIN <= uniform(op.full);
         const u64 t0 = stamps ? __builtin_amdgcn_s_memrealtime() : 0;
-        const LV<NH> x = full ? run_item<true, NH, B>(instrs, first, end, o, ox, laneb, arena, zrow, lds_perm, TAMD_WAVES_PER_WG, wave)
-                              : run_item<false, NH, B>(instrs, first, end, o, ox, laneb, arena, zrow, lds_perm, TAMD_WAVES_PER_WG, wave);
-        partial[wave][lane] = x;
-        __syncthreads();
+        LV<NH> x1, x2;
+        const LV<NH> x = full ? run_item<true, NH, B>(instrs, first, end, o, ox, laneb, arena, zrow, lds_perm, TAMD_WAVES_PER_WG, wave, &x1, &x2)
+                              : run_item<false, NH, B>(instrs, first, end, o, ox, laneb, arena, zrow, lds_perm, TAMD_WAVES_PER_WG, wave, &x1, &x2);
+        // The op ends with one STORE + FOOTER per accumulator it fills: one for a pure combine, up
+        // to three for a multi-target dense op; each is reduced through `partial` in turn.
+        uint32_t nst = 1;
+        while (nst < 3u && end >= first + 2u * (nst + 1u) && (instrs[end - 2u * (nst + 1u)].w0 & 0xffu) == TAMD_I_STORE) ++nst;
+        for (uint32_t s = 0; s < nst; ++s) {
+            const tamd_instr st = instrs[end - 2u * (nst - s)], f = instrs[end - 2u * (nst - s) + 1u];
+            const uint32_t acc = (st.w0 >> 16) & 0xffu;
+            if (s) __syncthreads();  // wave 0 has read the previous accumulator's partial sums
+            LV<NH> mine = x;
+            if (acc == 1u) mine = x1;
+            if (acc == 2u) mine = x2;
+            partial[wave][lane] = mine;
+            __syncthreads();
+            if (wave == 0) {
+                LV<NH> sum = partial[0][lane];
+                sum ^= partial[1][lane];
+                sum ^= partial[2][lane];
+                sum ^= partial[3][lane];
+                const u64 foot = ((u64)f.len << 32) | f.row;
+                if (full) lv_store_row<true, NH>(arena, st.row, st.len, st.cap, foot, o, sum, ox);
+                else lv_store_row<false, NH>(arena, st.row, st.len, st.cap, foot, o, sum, ox);
+            }
+        }
         if (wave == 0) {
-            LV<NH> sum = partial[0][lane];
-            sum ^= partial[1][lane];
-            sum ^= partial[2][lane];
-            sum ^= partial[3][lane];
-            const tamd_instr st = instrs[end - 2u], f = instrs[end - 1u];  // STORE (acc_0) + FOOTER
-            const u64 foot = ((u64)f.len << 32) | f.row;
-            if (full) lv_store_row<true, NH>(arena, st.row, st.len, st.cap, foot, o, sum, ox);
-            else lv_store_row<false, NH>(arena, st.row, st.len, st.cap, foot, o, sum, ox);
             if (stamps && lane == 0) {
                 __atomic_signal_fence(__ATOMIC_SEQ_CST);
                 stamps[3 * it] = t0;

@@ -172,6 +172,12 @@ bool Server::build(CmdBuf& b, const std::vector<Device::HostCopy>& up, const Pro
     for (size_t i = 0; i < rd.size(); ++i)
         xr[i] = tamd_xfer{(uint64_t)(uintptr_t)rd[i].host, (uint32_t)(rd[i].arena_off / 64), rd[i].len};
     if (!levels) return true;
+    // Multi-target DENSE runs are not built into the executor (its registers are at the limit);
+    // a program with one takes the launch path (per-call programs hold one encode each, so their
+    // rows are never grouped).
+    for (const tamd_instr& in : pb->instrs())
+        if ((in.w0 & 0xffu) == TAMD_I_ACCR && ((in.w0 >> 8) & 0xffu) == TAMD_R_DENSE && ((in.w0 >> 16) & 0xffu) > 1u)
+            return false;
     // The program as Device::begin / fill lay out one context's: ops grouped by bucket (level,
     // then cost class, most expensive first), each op's work items (op, slice) in that order.
     memcpy(base + off_instr, pb->instrs().data(), (size_t)n_instr * sizeof(tamd_instr));
@@ -203,7 +209,7 @@ bool Server::build(CmdBuf& b, const std::vector<Device::HostCopy>& up, const Pro
         uint32_t ii = item_fill[k];
         item_fill[k] += slices;
         // (bit 31 of the slice word: a pure combine, whose row batches a group of waves may split)
-        const uint32_t share = pure[i] ? 0x80000000u : 0u;
+        const uint32_t share = pure[i] == 1 ? 0x80000000u : 0u;  // (2: several accumulators, one wave)
         for (uint32_t s = 0; s < slices; ++s, ++ii) {
             hi[2 * ii] = oi;
             hi[2 * ii + 1] = s | share;
