@@ -581,6 +581,7 @@ uint64_t Device::close_program(int h, Part* const* parts, size_t n) {
     cur.levels = L;
     cur.level_items.assign(L, 0);
     cur.level_coop.assign(L, 0);
+    cur.class_items.assign(B, 0);
     cur.item_base.assign(L + 1, 0);
     // items of a level: cost class by cost class, each part's items of that class in part order
     uint64_t* items = (uint64_t*)slot.host;
@@ -601,6 +602,7 @@ uint64_t Device::close_program(int h, Part* const* parts, size_t n) {
             memcpy(items + at, p.items.data() + p.bucket_start[b], (size_t)c * 8);
             at += c;
             cur.level_items[l] += c;
+            cur.class_items[b] += c;
             if (b % TAMD_COST_CLASSES == 0) cur.level_coop[l] += c;
         }
     }
@@ -701,6 +703,7 @@ void Device::begin(Context* const* ctxs, size_t n, bool closed) {
     P.item_start.assign(n * B, 0);
     P.level_items.assign(L, 0);
     P.level_coop.assign(L, 0);
+    P.class_items.assign(B, 0);
     P.item_base.assign(L + 1, 0);
     P.instr_base.assign(n, 0);
     uint32_t op_at = 0, item_at = 0, instr_at = 0;
@@ -714,6 +717,7 @@ void Device::begin(Context* const* ctxs, size_t n, bool closed) {
                 op_at += pb.level_ops()[b];
                 item_at += pb.level_items()[b];
                 P.level_items[b / TAMD_COST_CLASSES] += pb.level_items()[b];
+                P.class_items[b] += pb.level_items()[b];
                 if (b % TAMD_COST_CLASSES == 0) P.level_coop[b / TAMD_COST_CLASSES] += pb.level_items()[b];
             }
         }
@@ -816,6 +820,7 @@ void Device::launch_step(Inflight* fresh, unsigned long long* stamps) {
         g.instrs = p.instrs;
         g.items = p.items + 8u * p.item_base[l];
         g.count = c;
+        for (uint32_t k = 0; k < TAMD_COST_CLASSES; ++k) g.cls[k] = p.class_items[TAMD_COST_CLASSES * l + k];
         cnt += c;
     };
     for (Inflight& p : progs_) add(p);
@@ -845,6 +850,10 @@ void Device::launch_step(Inflight* fresh, unsigned long long* stamps) {
         }
     }
     coop = seg_coop[0];
+    // Items class by class across the segments: the launch's long items (every level's class 0)
+    // are taken first (TONK_AMD_CLASS_MAJOR=0: segment by segment, A/B)
+    static const bool class_major = !getenv("TONK_AMD_CLASS_MAJOR") || atoi(getenv("TONK_AMD_CLASS_MAJOR")) != 0;
+    sg.flags = class_major ? 1u : 0u;
     hipStream_t st = (hipStream_t)stream_;
     uint32_t grid = (cnt + 3) / 4;
     if (grid > max_grid_) grid = max_grid_;
@@ -930,6 +939,7 @@ uint64_t Device::launch() {
     cur.level_items = P.level_items;
     cur.item_base = P.item_base;
     cur.level_coop = P.level_coop;
+    cur.class_items = P.class_items;
     cur.slot = &slot;
     return start_program(cur, P.n_instr, P.n_ops, P.n_items, P.total);
 }

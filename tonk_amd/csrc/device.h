@@ -294,6 +294,7 @@ private:
         std::vector<uint32_t> instr_base;          // per context
         std::vector<uint32_t> op_start, item_start; // [context * levels + level]
         std::vector<uint32_t> level_items, item_base, level_coop;  // level_coop: class-0 items (first)
+        std::vector<uint32_t> class_items;                       // per bucket (level, cost class)
         uint32_t levels = 0, buckets = 0;
         size_t n_instr = 0, n_ops = 0, n_items = 0, bytes_instr = 0, bytes_ops = 0, total = 0;
         Slot* slot = nullptr;
@@ -307,6 +308,7 @@ private:
         uint32_t ops = 0, instrs = 0, items = 0;  // offsets into prog_dev_
         uint32_t levels = 0, next = 1;
         std::vector<uint32_t> level_items, item_base, level_coop;
+        std::vector<uint32_t> class_items;  // per level and cost class (TAMD_COST_CLASSES * level + class)
         Slot* slot = nullptr;
         uint64_t ticket = 0;
         int verify = -1;  // index into vbatches_ (digested when the program completes)

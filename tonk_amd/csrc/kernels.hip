@@ -740,7 +740,10 @@ __device__ __forceinline__ void exec_level(const tamd_segments& sg, const uint8_
     __shared__ __attribute__((aligned(16))) uint32_t lds_perm[TAMD_GF_DWORDS];
     __shared__ LV<NH> partial[TAMD_WAVES_PER_WG][64];  // shared ops: the waves' acc_0
     __shared__ uint32_t claim, shared_claim, shared_item;
-    __shared__ tamd_segment lds_seg[TAMD_MAX_SEGMENTS + 1];  // + a sentinel (count ~0)
+    __shared__ tamd_segment lds_seg[TAMD_MAX_SEGMENTS];
+    // the launch's items in the order waves take them: blocks of (segment, cost class) items,
+    // class by class across the segments (flags bit 0) or segment by segment; + a sentinel
+    __shared__ uint4 lds_blk[TAMD_MAX_SEGMENTS * TAMD_COST_CLASSES + 1];  // {segment, first item, count, -}
     for (uint32_t i = threadIdx.x; i < TAMD_GF_DWORDS / 4; i += blockDim.x)
         ((uint4*)lds_perm)[i] = ((const uint4*)gf_perm)[i];
     if (threadIdx.x == 0) {
@@ -751,7 +754,26 @@ __device__ __forceinline__ void exec_level(const tamd_segments& sg, const uint8_
             lds_seg[k] = sg.s[k];
             if (k >= sg.n) lds_seg[k].count = 0;
         }
-        lds_seg[TAMD_MAX_SEGMENTS].count = ~0u;
+        // (.w: the segment's first item in segment order, where the stamps of an item go)
+        uint32_t nb = 0, base = 0;
+        if (sg.flags & 1u) {
+            uint32_t first[TAMD_MAX_SEGMENTS] = {0, 0, 0, 0, 0, 0};
+            for (uint32_t c = 0; c < TAMD_COST_CLASSES; ++c) {
+                base = 0;
+                for (uint32_t k = 0; k < sg.n; ++k) {
+                    const uint32_t m = lds_seg[k].cls[c];
+                    if (m) lds_blk[nb++] = make_uint4(k, first[k], m, base);
+                    first[k] += m;
+                    base += lds_seg[k].count;
+                }
+            }
+        } else {
+            for (uint32_t k = 0; k < sg.n; ++k) {
+                if (lds_seg[k].count) lds_blk[nb++] = make_uint4(k, 0, lds_seg[k].count, base);
+                base += lds_seg[k].count;
+            }
+        }
+        lds_blk[nb] = make_uint4(0, 0, ~0u, 0);
     }
     __syncthreads();
     const tamd_op* __restrict__ ops = (const tamd_op*)(pbase + sg.s[0].ops);
@@ -827,9 +849,12 @@ __device__ __forceinline__ void exec_level(const tamd_segments& sg, const uint8_
         if (lane == 0) k = atomicAdd(&claim, 1u);
         const uint32_t it = n_shared + blockIdx.x + uniform(__shfl(k, 0)) * gridDim.x;
         if (it >= n_all) break;
-        // the item's segment, from the LDS copy of the segment table (wave-uniform reads)
-        uint32_t seg = 0, rel = it;
-        while (rel >= lds_seg[seg].count) rel -= lds_seg[seg++].count;
+        // the item's segment and index there, from the LDS block table (wave-uniform reads)
+        uint32_t b = 0, rel = it;
+        while (rel >= lds_blk[b].z) rel -= lds_blk[b++].z;
+        const uint32_t seg = uniform(lds_blk[b].x);
+        rel += uniform(lds_blk[b].y);
+        const uint32_t at = uniform(lds_blk[b].w) + rel;  // (stamps)
         const tamd_segment sd = lds_seg[seg];
         const tamd_op* __restrict__ sops = (const tamd_op*)(pbase + uniform(sd.ops));
         const tamd_instr* __restrict__ ins = (const tamd_instr*)(pbase + uniform(sd.instrs));
@@ -846,9 +871,9 @@ __device__ __forceinline__ void exec_level(const tamd_segments& sg, const uint8_
         if (stamps && lane == 0) {  // profiling only (TONK_AMD_STAMPS): vector stores of 100 MHz stamps
             __atomic_signal_fence(__ATOMIC_SEQ_CST);
             const u64 t1 = __builtin_amdgcn_s_memrealtime();
-            stamps[3 * it] = t0;
-            stamps[3 * it + 1] = t1;
-            stamps[3 * it + 2] = ((u64)blockIdx.x << 32) | (threadIdx.x >> 6);
+            stamps[3 * at] = t0;
+            stamps[3 * at + 1] = t1;
+            stamps[3 * at + 2] = ((u64)blockIdx.x << 32) | (threadIdx.x >> 6);
         }
     }
 }

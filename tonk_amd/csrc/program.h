@@ -110,10 +110,13 @@ typedef struct tamd_op {
 typedef struct tamd_segment {
     uint32_t ops, instrs, items;  // offsets of the program's ops / instructions / this level's items
     uint32_t count;               // items ((op index, slice) uint32 pairs)
+    uint32_t cls[5];              // items per cost class (TAMD_COST_CLASSES), in that order
 } tamd_segment;
 typedef struct tamd_segments {
     tamd_segment s[TAMD_MAX_SEGMENTS];
-    uint32_t n, pad;
+    uint32_t n;
+    uint32_t flags;  // bit 0: items are taken class by class across the segments (the launch's
+                     // longest first), else segment by segment
 } tamd_segments;
 
 static inline uint32_t tamd_w0(uint32_t kind, uint32_t arg, uint32_t arg2 = 0) {
