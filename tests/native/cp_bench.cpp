@@ -153,6 +153,55 @@ static void dump_reads(Context& ctx) {
     }
     for (int m = 0; m < 8; ++m)
         if (rows[m]) fprintf(stderr, "reads %-14s rows %8llu  MB %8.2f\n", names[m], (unsigned long long)rows[m], bytes[m] / 1e6);
+    // scaled Cauchy runs (decoder elimination): rows read per op vs distinct rows per op
+    {
+        uint64_t runs = 0, rd = 0, distinct = 0, ops_multi = 0;
+        std::map<uint32_t, uint32_t> all;
+        const auto& ops = ctx.pb.ops();
+        for (const tamd_op& o : ops) {
+            std::map<uint32_t, uint32_t> seen;
+            uint32_t nr = 0;
+            for (uint32_t k = o.first; k < o.first + o.count; ++k) {
+                const uint32_t kind = ins[k].w0 & 0xff;
+                if (kind != TAMD_I_ACCR) continue;
+                const uint32_t mode = (ins[k].w0 >> 8) & 0xff;
+                if (mode != TAMD_R_CAUCHY || (ins[k].w0 >> 24) <= 1) continue;
+                ++nr;
+                for (uint32_t j = 0; j < ins[k].cap; ++j) seen[ins[k].row + j * ins[k + 1].row]++, all[ins[k].row + j * ins[k + 1].row]++;
+                rd += ins[k].cap;
+            }
+            runs += nr;
+            distinct += seen.size();
+            ops_multi += nr > 1;
+        }
+        fprintf(stderr, "scaled cauchy: runs %llu rows %llu distinct-per-op %llu distinct %zu ops with >1 run %llu\n",
+                (unsigned long long)runs, (unsigned long long)rd, (unsigned long long)distinct, all.size(),
+                (unsigned long long)ops_multi);
+        // every row any op reads, against the distinct rows
+        std::map<uint32_t, uint32_t> every;
+        uint64_t tot = 0;
+        for (size_t k = 0; k < ins.size(); ++k) {
+            const uint32_t kind = ins[k].w0 & 0xff;
+            if (kind == TAMD_I_ACC || kind == TAMD_I_ACC3) { every[ins[k].row]++; ++tot; }
+            else if (kind == TAMD_I_ACCR)
+                for (uint32_t j = 0; j < ins[k].cap; ++j) { every[ins[k].row + j * ins[k + 1].row]++; ++tot; }
+        }
+        fprintf(stderr, "all reads %llu distinct rows %zu\n", (unsigned long long)tot, every.size());
+        // rows read by each run mode, and by the encoder's MULTI and DENSE runs together
+        std::map<uint32_t, uint32_t> by_mode[8];
+        for (size_t k = 0; k < ins.size(); ++k)
+            if ((ins[k].w0 & 0xff) == TAMD_I_ACCR) {
+                const uint32_t mode = (ins[k].w0 >> 8) & 7;
+                for (uint32_t j = 0; j < ins[k].cap; ++j) by_mode[mode][ins[k].row + j * ins[k + 1].row]++;
+            }
+        size_t both = 0, md_reads = 0;
+        std::map<uint32_t, uint32_t> md;
+        for (int m : {TAMD_R_MULTI, TAMD_R_DENSE, TAMD_R_CAUCHY, TAMD_R_CONST})
+            for (const auto& kv : by_mode[m]) { md[kv.first] += kv.second; md_reads += kv.second; }
+        for (const auto& kv : by_mode[TAMD_R_MULTI]) both += by_mode[TAMD_R_DENSE].count(kv.first);
+        fprintf(stderr, "encoder-side runs (multi+dense+cauchy+const): reads %zu distinct %zu; rows in both multi and dense %zu\n",
+                md_reads, md.size(), both);
+    }
     uint64_t hist[5] = {0, 0, 0, 0, 0};
     for (const auto& kv : dense_rows) hist[kv.second < 4 ? kv.second : 4]++;
     fprintf(stderr, "dense: %zu distinct packet rows; read by 1/2/3/4+ runs: %llu %llu %llu %llu\n", dense_rows.size(),

@@ -583,28 +583,73 @@ uint64_t Device::close_program(int h, Part* const* parts, size_t n) {
     cur.level_coop.assign(L, 0);
     cur.class_items.assign(B, 0);
     cur.item_base.assign(L + 1, 0);
-    // items of a level: cost class by cost class, each part's items of that class in part order
+    // Items of a level: cost class by cost class.  Inside a class, part i (one context: a stream)
+    // has XCD affinity i mod 8: its items go to positions p with p mod 8 == i mod 8 as far as the
+    // counts allow, and the executor runs position p of a class block on a workgroup of XCD p mod 8
+    // (exec_level), so one stream's ops -- which read the same packets -- share that XCD's L2.
+    // (TONK_AMD_XCD_AFFINITY=0: parts in order, A/B.)
+    static const bool affinity = !getenv("TONK_AMD_XCD_AFFINITY") || atoi(getenv("TONK_AMD_XCD_AFFINITY")) != 0;
     uint64_t* items = (uint64_t*)slot.host;
     size_t at = 0;
     for (uint32_t b = 0; b < B && !failed_; ++b) {
         const uint32_t l = b / TAMD_COST_CLASSES;
         if (b % TAMD_COST_CLASSES == 0) cur.item_base[l] = (uint32_t)at;
+        size_t total = 0;
         for (size_t i = 0; i < n; ++i) {
             const Part& p = *parts[i];
-            if (b + 1 >= p.bucket_start.size()) continue;
-            const uint32_t c = p.bucket_start[b + 1] - p.bucket_start[b];
-            if (!c) continue;
-            if (at + c > asm_items_) {
-                error_ = "a program exceeds its work-item area";
-                failed_ = true;
-                break;
-            }
-            memcpy(items + at, p.items.data() + p.bucket_start[b], (size_t)c * 8);
-            at += c;
-            cur.level_items[l] += c;
-            cur.class_items[b] += c;
-            if (b % TAMD_COST_CLASSES == 0) cur.level_coop[l] += c;
+            if (b + 1 < p.bucket_start.size()) total += p.bucket_start[b + 1] - p.bucket_start[b];
         }
+        if (!total) continue;
+        if (at + total > asm_items_) {
+            error_ = "a program exceeds its work-item area";
+            failed_ = true;
+            break;
+        }
+        if (!affinity || n < 2) {
+            for (size_t i = 0; i < n; ++i) {
+                const Part& p = *parts[i];
+                if (b + 1 >= p.bucket_start.size()) continue;
+                const uint32_t c = p.bucket_start[b + 1] - p.bucket_start[b];
+                memcpy(items + at, p.items.data() + p.bucket_start[b], (size_t)c * 8);
+                at += c;
+            }
+        } else {
+            // per residue r: a cursor over the items of parts r, r + 8, ... (part, next item)
+            size_t part_of[8], next[8], left[8];
+            for (uint32_t r = 0; r < 8; ++r) {
+                part_of[r] = r;
+                next[r] = 0;
+                left[r] = 0;
+                for (size_t i = r; i < n; i += 8) {
+                    const Part& p = *parts[i];
+                    if (b + 1 < p.bucket_start.size()) left[r] += p.bucket_start[b + 1] - p.bucket_start[b];
+                }
+            }
+            auto take = [&](uint32_t r) -> uint64_t {
+                for (;;) {
+                    const Part& p = *parts[part_of[r]];
+                    const uint32_t c = b + 1 < p.bucket_start.size() ? p.bucket_start[b + 1] - p.bucket_start[b] : 0u;
+                    if (next[r] < c) {
+                        --left[r];
+                        return p.items[p.bucket_start[b] + next[r]++];
+                    }
+                    part_of[r] += 8;
+                    next[r] = 0;
+                }
+            };
+            for (size_t j = 0; j < total; ++j) {
+                uint32_t r = (uint32_t)(j & 7u);
+                if (!left[r]) {  // this residue's parts are done: the residue with most left
+                    for (uint32_t q = 0; q < 8; ++q)
+                        if (left[q] > left[r]) r = q;
+                }
+                items[at + j] = take(r);
+            }
+            at += total;
+        }
+        cur.level_items[l] += (uint32_t)total;
+        cur.class_items[b] += (uint32_t)total;
+        if (b % TAMD_COST_CLASSES == 0) cur.level_coop[l] += (uint32_t)total;
     }
     cur.item_base[L] = (uint32_t)at;
     if (at == 0 || failed_) {  // nothing to run: complete once everything before it is done
@@ -868,6 +913,16 @@ void Device::launch_step(Inflight* fresh, unsigned long long* stamps) {
     static const int share_mode = getenv("TONK_AMD_SHARE") ? atoi(getenv("TONK_AMD_SHARE")) : 0;  // A/B (profiling)
     const uint32_t shared = (share_mode == 1 || (share_mode == 0 && cnt < 2u * 4u * max_grid_)) ? coop : 0u;
     const ExecFn fn = (ExecFn)exec_kernel_;
+    // Profiling only: TONK_AMD_LAUNCH_STAMPS=<launch number> records per-item stamps of every
+    // segment of that launch (a pipelined one) into tonk_amd_launch_stamps.txt.
+    static const char* lstamp_env = getenv("TONK_AMD_LAUNCH_STAMPS");
+    unsigned long long* lstamps = nullptr;
+    if (lstamp_env && !stamps && (uint64_t)atoll(lstamp_env) == stats_.launches) {
+        if (hipMalloc((void**)&lstamps, (size_t)cnt * 24) == hipSuccess) {
+            hipMemsetAsync(lstamps, 0, (size_t)cnt * 24, st);
+            stamps = lstamps;
+        }
+    }
     // Timed: the events carry the dispatch's own start and end (hipExtLaunchKernelGGL), as a
     // kernel trace does; events recorded around the launch would add the dispatch latency.
     if (timing_)
@@ -878,6 +933,25 @@ void Device::launch_step(Inflight* fresh, unsigned long long* stamps) {
                            d_zero_, stamps));
     if (timing_) {
         timing_events_.push_back(std::make_pair((void*)e0, (void*)e1));
+    }
+    if (lstamps) {
+        std::vector<unsigned long long> h((size_t)cnt * 3);
+        hipMemcpyAsync(h.data(), lstamps, h.size() * 8, hipMemcpyDeviceToHost, st);
+        hipStreamSynchronize(st);
+        hipFree(lstamps);
+        if (FILE* f = fopen("tonk_amd_launch_stamps.txt", "w")) {
+            fprintf(f, "# seg level class t0 t1 block_wave (100 MHz ticks); shared items %u, grid %u\n", shared, grid);
+            size_t at = 0;
+            for (uint32_t k = 0; k < sg.n; ++k) {
+                uint32_t c = 0, left = sg.s[k].cls[0];
+                for (uint32_t i = 0; i < sg.s[k].count; ++i, ++at) {
+                    while (!left && c + 1 < TAMD_COST_CLASSES) left = sg.s[k].cls[++c];
+                    if (left) --left;
+                    fprintf(f, "%u %u %u %llu %llu %llu\n", k, seg_level[k], c, h[3 * at], h[3 * at + 1], h[3 * at + 2]);
+                }
+            }
+            fclose(f);
+        }
     }
     stats_.launches++;
 }

@@ -744,6 +744,8 @@ __device__ __forceinline__ void exec_level(const tamd_segments& sg, const uint8_
     // the launch's items in the order waves take them: blocks of (segment, cost class) items,
     // class by class across the segments (flags bit 0) or segment by segment; + a sentinel
     __shared__ uint4 lds_blk[TAMD_MAX_SEGMENTS * TAMD_COST_CLASSES + 1];  // {segment, first item, count, -}
+    // this workgroup's items of block b: positions r_b, r_b + G, ... (.x = r_b, .y = how many)
+    __shared__ uint2 lds_wg[TAMD_MAX_SEGMENTS * TAMD_COST_CLASSES + 1];
     for (uint32_t i = threadIdx.x; i < TAMD_GF_DWORDS / 4; i += blockDim.x)
         ((uint4*)lds_perm)[i] = ((const uint4*)gf_perm)[i];
     if (threadIdx.x == 0) {
@@ -774,6 +776,23 @@ __device__ __forceinline__ void exec_level(const tamd_segments& sg, const uint8_
             }
         }
         lds_blk[nb] = make_uint4(0, 0, ~0u, 0);
+        // Single-wave items (the shared ones, the first n_shared of the first block, excepted):
+        // workgroup g takes positions p = (g - o_b) mod G + m G of block b, o_b = the items before
+        // the block rounded down to a multiple of 8.  So position p runs on an XCD p mod 8 (g mod 8)
+        // -- the host lays out each class with every stream's items on one residue (XCD affinity,
+        // Device::close_program) -- and the rotation o_b spreads the blocks' remainders.
+        if (n_shared) {
+            lds_blk[0].y += n_shared;
+            lds_blk[0].z -= n_shared;
+        }
+        const uint32_t G = gridDim.x, g = blockIdx.x;
+        uint32_t before = 0;
+        for (uint32_t b = 0; b < nb; ++b) {
+            const uint32_t cnt = lds_blk[b].z, r = (g + G - (before & ~7u) % G) % G;
+            lds_wg[b] = make_uint2(r, cnt > r ? (cnt - 1u - r) / G + 1u : 0u);
+            before += cnt;
+        }
+        lds_wg[nb] = make_uint2(0, ~0u);
     }
     __syncthreads();
     const tamd_op* __restrict__ ops = (const tamd_op*)(pbase + sg.s[0].ops);
@@ -842,18 +861,16 @@ __device__ __forceinline__ void exec_level(const tamd_segments& sg, const uint8_
     // them (a stratified sample of the level: ordered by cost class, most expensive first); its
     // waves claim them one at a time through an LDS counter, so a wave that drew a long op does
     // not hold up the others.
-    uint32_t n_all = 0;
-    for (uint32_t k = 0; k < sg.n; ++k) n_all += sg.s[k].count;
     for (;;) {
         uint32_t k = 0;
         if (lane == 0) k = atomicAdd(&claim, 1u);
-        const uint32_t it = n_shared + blockIdx.x + uniform(__shfl(k, 0)) * gridDim.x;
-        if (it >= n_all) break;
-        // the item's segment and index there, from the LDS block table (wave-uniform reads)
-        uint32_t b = 0, rel = it;
-        while (rel >= lds_blk[b].z) rel -= lds_blk[b++].z;
+        k = uniform(__shfl(k, 0));
+        // this workgroup's k-th item: its block and position there (wave-uniform LDS reads)
+        uint32_t b = 0;
+        while (k >= lds_wg[b].y) k -= lds_wg[b++].y;
+        if (lds_wg[b].y == ~0u) break;
         const uint32_t seg = uniform(lds_blk[b].x);
-        rel += uniform(lds_blk[b].y);
+        const uint32_t rel = uniform(lds_blk[b].y) + uniform(lds_wg[b].x) + k * gridDim.x;
         const uint32_t at = uniform(lds_blk[b].w) + rel;  // (stamps)
         const tamd_segment sd = lds_seg[seg];
         const tamd_op* __restrict__ sops = (const tamd_op*)(pbase + uniform(sd.ops));
