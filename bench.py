@@ -78,11 +78,12 @@ import tonk_amd  # noqa: E402
 METRIC = "Siamese FEC encode+decode GiB/s (device-resident), 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0
 STREAMS_PER_GPU = 64
-ORIGINALS_PER_STEP = 4096   # per stream per device program (tamd_session_step)
+ORIGINALS_PER_STEP = int(os.environ.get("TONK_AMD_BENCH_PROGRAM", 4096))  # per stream per device program
+                                                                            # (tamd_session_step; env: A/B)
 # A bench step: 16 programs, 65536 originals per stream (round 5; 4 before): the driver's
 # `--steps 20` then times ~110 ms instead of ~28 ms.  The inputs are a pool of INPUT_POOL rows per
 # side per stream that original i reads as row i mod INPUT_POOL (tonk_amd.h input_pool).
-PROGRAMS_PER_STEP = 16
+PROGRAMS_PER_STEP = 65536 // ORIGINALS_PER_STEP
 INPUT_POOL = 65536
 LOSS = 0.01
 ACK = 64
@@ -834,9 +835,9 @@ def main() -> int:
     pmc = pmc_traffic(a.workload, a.steps, a.warmup) if (rank == 0 and world == 1 and not a.no_pmc) else None
     traffic = pmc.get("traffic_per_timed_launch") if pmc else None
     workload = {
-        "cfg3": "configs[3] per-GPU shard: 64 independent streams/GPU, 65536 originals per stream per step (16 programs), "
+        "cfg3": "configs[3] per-GPU shard: 64 independent streams/GPU, 65536 originals per stream per step " f"({PROGRAMS_PER_STEP} programs), "
                 "1300 B payloads, 1% uniform loss, f=2%, ack every 64",
-        "cfg2": "configs[2]: 64 independent streams/GPU, 65536 originals per stream per step (16 programs), 1300 B payloads, "
+        "cfg2": "configs[2]: 64 independent streams/GPU, 65536 originals per stream per step " f"({PROGRAMS_PER_STEP} programs), 1300 B payloads, "
                 "2% uniform loss, f=4%, ack every 64",
     }[a.workload]
     out = {
