@@ -29,7 +29,8 @@ thread_local uint64_t calls[kSlots];
 const char* const names[kSlots] = {"enc_add", "enc_encode", "enc_ack", "dec_add_orig", "dec_add_rec", "dec_decode",
     "dec_ack", "dec_is_ready", "gen_matrix", "ge", "elim", "lower_tri", "back_sub", "chain_flush", "sym_merge",
     "prepare_flush", "finish_flush", "release", "enc_dense", "enc_light", "enc_emit", "elim_sums", "elim_pairs",
-    "elim_fold", "enc_cauchy", "enc_remove", "elim_start", "lane_read", "lane_dyn", "combine", "fold_merge", "alloc"};
+    "elim_fold", "enc_cauchy", "enc_remove", "elim_start", "lane_read", "lane_dyn", "combine", "fold_merge", "alloc",
+    "x1", "x2", "x3", "x4"};
 } }
 #endif
 

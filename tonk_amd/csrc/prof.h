@@ -11,7 +11,8 @@ namespace prof {
 enum Slot {
     kEncAdd, kEncEncode, kEncAck, kDecAddOrig, kDecAddRec, kDecDecode, kDecAck, kDecIsReady,
     kGenMatrix, kGE, kElim, kLowerTri, kBackSub, kChainFlush, kSymMerge, kFlushAll, kFinish, kRelease,
-    kEncDense, kEncLight, kEncEmit, kElimSums, kElimPairs, kElimFold, kEncCauchy, kEncRemove, kElimStart, kLaneRead, kLaneDyn, kCombine, kFoldMerge, kAlloc, kSlots
+    kEncDense, kEncLight, kEncEmit, kElimSums, kElimPairs, kElimFold, kEncCauchy, kEncRemove, kElimStart, kLaneRead, kLaneDyn, kCombine, kFoldMerge, kAlloc,
+    kX1, kX2, kX3, kX4, kSlots  // kX*: ad-hoc probes
 };
 extern thread_local uint64_t cycles[kSlots];
 extern thread_local uint64_t calls[kSlots];
