@@ -37,6 +37,7 @@ const char* const names[kSlots] = {"enc_add", "enc_encode", "enc_ack", "dec_add_
 static int g_stub = 0;
 static int g_nobatch = 0;
 static int g_pipe = 1;
+static bool g_contig = true;  // contig=0: the codecs check run contiguity themselves (rows are allocated in order)
 static uint64_t g_step_clock = 1000;  // nobatch=1: single adds only (the runner's fallback path)  // stub=1: encoder calls return at once; stub=2: decoder calls too
 struct Null {
     struct RecRef { RecoveryOut out; };
@@ -46,6 +47,13 @@ struct Null {
     Decoder* dec;
     std::vector<RowId> enc_rows, dec_rows;
     uint64_t instrs = 0;
+    // (rows are allocated in order per side: each side's offsets are affine)
+    uint32_t pool = 0;  // rows per side; original i uses row i mod pool
+    uint64_t layout(const std::vector<RowId>& rows, uint32_t index, uint32_t k) const {
+        if (index % pool + k > pool) return 0;
+        const uint32_t o0 = ctx->rows.offset(rows[0]), stride = ctx->rows.offset(rows[1]) - o0;
+        return (uint64_t)(o0 + (index % pool) * stride) << 32 | stride;
+    }
     int enc_add(uint32_t index, uint32_t len, uint32_t* col) {
         const uint32_t hb = length_header_bytes(len);
         TAMD_PROF_SCOPE(kEncAdd);
@@ -56,13 +64,13 @@ struct Null {
         if (g_stub || g_nobatch) return false;
         const uint32_t hb = length_header_bytes(len);
         TAMD_PROF_SCOPE(kEncAdd);
-        return enc->add_run(&enc_rows[index], k, hb + len, hb, len, true, col0);
+        return enc->add_run(&enc_rows[index], k, hb + len, hb, len, true, col0, g_contig ? layout(enc_rows, index, k) : 0);
     }
     bool dec_add_run(uint32_t col0, uint32_t index, uint32_t k, uint32_t len) {
         if (g_stub > 1 || g_nobatch) return false;
         const uint32_t hb = length_header_bytes(len);
         TAMD_PROF_SCOPE(kDecAddOrig);
-        return dec->add_run_inorder(col0, &dec_rows[index], k, hb + len, hb, len, true);
+        return dec->add_run_inorder(col0, &dec_rows[index], k, hb + len, hb, len, true, g_contig ? layout(dec_rows, index, k) : 0);
     }
     int enc_encode(RecRef& r) { TAMD_PROF_SCOPE(kEncEncode); if (g_stub) return 2; return enc->encode(r.out); }
     int enc_ack(const uint8_t* b, uint32_t n, uint32_t* next) { TAMD_PROF_SCOPE(kEncAck); return enc->acknowledge(b, n, next); }
@@ -288,6 +296,7 @@ int main(int argc, char** argv) {
         if (k == "expand") { expand = (uint32_t)strtoul(eq + 1, nullptr, 0); continue; }
         if (k == "backsub") { backsub = (uint32_t)strtoul(eq + 1, nullptr, 0); continue; }
         if (k == "pipe") { g_pipe = atoi(eq + 1); continue; }
+        if (k == "contig") { g_contig = atoi(eq + 1) != 0; continue; }
         if (k == "reps") { reps = (uint32_t)atoi(eq + 1); continue; }  // level pipelining as the session runs it
         if (k == "prefault") {  // MB of heap faulted in and kept before the run (cold-start studies)
             const size_t mb = (size_t)atoi(eq + 1);
@@ -345,7 +354,7 @@ int main(int argc, char** argv) {
         ctx.dense_split = getenv("TONK_AMD_DENSE_SPLIT") ? (uint32_t)atoi(getenv("TONK_AMD_DENSE_SPLIT"))
                                                         : (streams > 4 ? Encoder::kDenseSplit : 0u);
         ctx.pipeline = g_pipe != 0;
-        ctx.rows.init(4ull * p.n_originals * 1344 + (256u << 20));
+        ctx.rows.init(4ull * std::min<uint32_t>(p.n_originals, 65536) * 1344 + (256u << 20));
         encs[s].reset(new Encoder(&ctx, 1344));
         encs[s]->set_clock(&g_step_clock);  // the session reads the clock once per step
         decs[s].reset(new Decoder(&ctx, 1344));
@@ -353,8 +362,13 @@ int main(int argc, char** argv) {
         be[s]->ctx = &ctx;
         be[s]->enc = encs[s].get();
         be[s]->dec = decs[s].get();
-        for (uint32_t i = 0; i < p.n_originals; ++i) be[s]->enc_rows.push_back(ctx.rows.alloc(1302));
-        for (uint32_t i = 0; i < p.n_originals; ++i) be[s]->dec_rows.push_back(ctx.rows.alloc(1302));
+        // (a pool of 65536 rows per side, as the bench's sessions: long runs fit in memory)
+        const uint32_t pool = std::min<uint32_t>(p.n_originals, 65536);
+        be[s]->pool = pool;
+        for (uint32_t i = 0; i < pool; ++i) be[s]->enc_rows.push_back(ctx.rows.alloc(1302));
+        for (uint32_t i = 0; i < pool; ++i) be[s]->dec_rows.push_back(ctx.rows.alloc(1302));
+        for (uint32_t i = pool; i < p.n_originals; ++i) be[s]->enc_rows.push_back(be[s]->enc_rows[i - pool]);
+        for (uint32_t i = pool; i < p.n_originals; ++i) be[s]->dec_rows.push_back(be[s]->dec_rows[i - pool]);
         run[s].reset(new wl::Runner<Null, NoTr>(ps[s], *be[s], tr));
         run[s]->pregenerate();
     }

@@ -88,16 +88,17 @@ void Decoder::release_segment(const Segment& s, uint32_t from, uint32_t n) {
 }
 
 void Decoder::append(uint32_t e0, const RowId* rows, uint32_t k, uint32_t framed_bytes, uint32_t header_bytes,
-                     uint8_t owned) {
+                     uint8_t owned, uint64_t layout) {
     const RowTable& rt = ctx_->rows;
     uint32_t e = e0, col = to_column(e0);
     // Fast path: the k packets are consecutive handles at one offset stride with no column wrap
     // inside (a stretch of a session's inputs): they continue the last segment or open one, and
     // only the elements' segment numbers are filled.
-    if (k >= 2 && col + k - 1 < kColumnPeriod && col != 0 && consecutive_handles(rows, k)) {
-        const uint32_t o0 = rt.offset(rows[0]), o1 = rt.offset(rows[1]);
+    if (k >= 2 && col + k - 1 < kColumnPeriod && col != 0 && (layout || consecutive_handles(rows, k))) {
+        const uint32_t o0 = layout ? (uint32_t)(layout >> 32) : rt.offset(rows[0]);
+        const uint32_t o1 = layout ? o0 + (uint32_t)layout : rt.offset(rows[1]);
         const uint32_t stride = o1 - o0;
-        if (o1 > o0 && rt.affine(rows[0], k, stride)) {
+        if (o1 > o0 && (layout || rt.affine(rows[0], k, stride))) {
             Segment* last = segs_.empty() ? nullptr : &segs_.back();
             const bool cont = last && last->end() == e0 + base_ && last->bytes == framed_bytes &&
                               last->header_bytes == header_bytes && last->owned == owned &&
@@ -319,7 +320,7 @@ Result Decoder::add_original(uint32_t packet_num, RowId row, uint32_t framed_byt
 // only stores the row, sets its got bit and moves NextExpected along (SiameseDecoder.cpp:
 // 1467-1536 restated for that case); is_ready() cannot succeed when no recovery is pending.
 bool Decoder::add_run_inorder(uint32_t col0, const RowId* rows, uint32_t k, uint32_t framed_bytes,
-                              uint32_t header_bytes, uint32_t payload_bytes, bool borrowed) {
+                              uint32_t header_bytes, uint32_t payload_bytes, bool borrowed, uint64_t layout) {
     if (disabled_ || has_recovered_ || !k) return false;
     const uint32_t e0 = to_element(col0);
     if (col_delta_negative(e0) || e0 < count_) return false;
@@ -329,7 +330,7 @@ bool Decoder::add_run_inorder(uint32_t col0, const RowId* rows, uint32_t k, uint
     // would repeat this answer without changing any state.
     if (head_ && (next_expected_ >= e0 || check_recovery_possible())) return false;
     grow_window(e0 + k);
-    append(e0, rows, k, framed_bytes, header_bytes, borrowed ? 0 : 1);
+    append(e0, rows, k, framed_bytes, header_bytes, borrowed ? 0 : 1, layout);
     for (uint32_t e = e0; e < e0 + k;) {  // got bits a subwindow at a time
         const uint32_t bit = e % kSubwindow;
         const uint32_t n = std::min(kSubwindow - bit, e0 + k - e);

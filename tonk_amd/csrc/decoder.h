@@ -43,7 +43,8 @@ public:
     // while no recovery packet is pending, when is_ready() cannot succeed after any of them.
     // Returns false, with nothing done, when that does not hold.
     bool add_run_inorder(uint32_t col0, const RowId* rows, uint32_t k, uint32_t framed_bytes,
-                         uint32_t header_bytes, uint32_t payload_bytes, bool borrowed);
+                         uint32_t header_bytes, uint32_t payload_bytes, bool borrowed,
+                         uint64_t layout = 0);
     Result is_ready();
     // siamese_decode: recovered packets are appended to `out` (increasing packet number).
     Result decode(std::vector<RecoveredPacket*>& out);
@@ -182,7 +183,8 @@ private:
     // Append received packets rows[0..k) (equally long, no host copy) as elements e0 .. e0 + k - 1
     // at the window end (beyond every segment), extending the last segment while they continue it.
     void append(uint32_t e0, const RowId* rows, uint32_t k, uint32_t framed_bytes, uint32_t header_bytes,
-                uint8_t owned);
+                uint8_t owned,
+                uint64_t layout = 0);
     void release_segment(const Segment& s, uint32_t from, uint32_t n);
     uint32_t next_lane_element(uint32_t element, uint32_t lane) const {
         uint32_t n = element - (element % kLanes) + lane;

@@ -75,7 +75,7 @@ void Encoder::pre_flush() {
 }
 
 void Encoder::append(const RowId* rows, uint32_t k, uint32_t framed_bytes, uint32_t header_bytes, uint8_t owned,
-                     void* host, uint32_t now) {
+                     void* host, uint32_t now, uint64_t layout) {
     const RowTable& rt = ctx_->rows;
     uint32_t e_abs = base_ + (uint32_t)win_.size();
     uint32_t col = next_column_;
@@ -86,10 +86,11 @@ void Encoder::append(const RowId* rows, uint32_t k, uint32_t framed_bytes, uint3
     // Fast path: the k packets are consecutive handles at one offset stride with no column wrap
     // inside (a stretch of a session's inputs): they continue the last segment or open one, and
     // only the element slots are filled.
-    if (k >= 2 && !host && col + k - 1 < kColumnPeriod && col != 0 && consecutive_handles(rows, k)) {
-        const uint32_t o0 = rt.offset(rows[0]), o1 = rt.offset(rows[1]);
+    if (k >= 2 && !host && col + k - 1 < kColumnPeriod && col != 0 && (layout || consecutive_handles(rows, k))) {
+        const uint32_t o0 = layout ? (uint32_t)(layout >> 32) : rt.offset(rows[0]);
+        const uint32_t o1 = layout ? o0 + (uint32_t)layout : rt.offset(rows[1]);
         const uint32_t stride = o1 - o0;
-        if (o1 > o0 && rt.affine(rows[0], k, stride)) {
+        if (o1 > o0 && (layout || rt.affine(rows[0], k, stride))) {
             Segment* last = segs_.empty() ? nullptr : &segs_.back();
             const bool cont = last && !last->host && last->row0 != kNoRow && last->end() == e_abs &&
                               last->bytes == framed_bytes && last->header_bytes == header_bytes &&
@@ -214,12 +215,13 @@ uint32_t Encoder::add_first(RowId row, uint32_t framed_bytes, uint32_t header_by
 
 // k consecutive add() calls that all succeed.
 bool Encoder::add_run(const RowId* rows, uint32_t k, uint32_t framed_bytes, uint32_t header_bytes,
-                      uint32_t payload_bytes, bool borrowed, uint32_t* first_col) {
+                      uint32_t payload_bytes, bool borrowed, uint32_t* first_col, uint64_t layout) {
     if (disabled_ || remaining_slots() < k || !k) return false;
     // the first add may start a window; the rest append to it (count_ > 0, element == count_)
     *first_col = add_first(rows[0], framed_bytes, header_bytes, payload_bytes, nullptr, borrowed);
     if (k == 1) return true;
-    append(rows + 1, k - 1, framed_bytes, header_bytes, borrowed ? 0 : 1, nullptr, (uint32_t)now_msec());
+    append(rows + 1, k - 1, framed_bytes, header_bytes, borrowed ? 0 : 1, nullptr, (uint32_t)now_msec(),
+           layout ? layout + ((layout & 0xffffffffull) << 32) : 0);  // (rows + 1: one stride on)
     count_ += k - 1;
     next_column_ = col_add(next_column_, k - 1);
     // every lane one of these columns fell on (all k - 1 have the same length)

@@ -96,8 +96,12 @@ public:
                void* host, uint32_t* packet_num, bool borrowed = false);
     // Batched add of k equally long packets (rows[0..k)): the window ends up exactly as after k
     // add() calls.  Returns false, with nothing done, when one of those calls would not succeed.
+    // `layout` (nonzero): the caller guarantees rows[j] == rows[0] + j at arena offsets
+    // layout >> 32 + j * (layout & 0xffffffff) (a stretch of a session's input rows), so neither
+    // is checked nor looked up.
     bool add_run(const RowId* rows, uint32_t k, uint32_t framed_bytes, uint32_t header_bytes,
-                 uint32_t payload_bytes, bool borrowed, uint32_t* first_col);
+                 uint32_t payload_bytes, bool borrowed, uint32_t* first_col,
+                 uint64_t layout = 0);
     // siamese_encoder_get / _retransmit: the packet as a value (row, lengths, column, host copy)
     Result get(uint32_t packet_num, StoredOriginal* out);
     void remove_before(uint32_t first_kept_column);
@@ -156,7 +160,8 @@ private:
     // Append k packets (rows[0..k), equally long) at the window end, extending the last segment
     // while the rows continue its strides; `now` is their send time.
     void append(const RowId* rows, uint32_t k, uint32_t framed_bytes, uint32_t header_bytes, uint8_t owned,
-                void* host, uint32_t now);
+                void* host, uint32_t now,
+                uint64_t layout = 0);
     void release_segment(const Segment& s, uint32_t from, uint32_t n);  // rows [from, from + n) of s
     void drop_all();                                // release every segment, empty window
     void drop_segments_below(uint32_t drop);        // release segments (parts) below absolute `drop`

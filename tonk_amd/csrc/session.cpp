@@ -204,6 +204,9 @@ struct Stream {
     std::unique_ptr<Encoder> enc;
     std::unique_ptr<Decoder> dec;
     std::vector<RowId> enc_rows, dec_rows;
+    uint32_t pool = 0;        // input rows per side (original i reads row i mod pool)
+    bool pool_affine = false; // each side's pool rows are consecutive handles at one arena stride:
+    uint32_t pool_off[2] = {0, 0}, pool_stride = 0;  // row i mod pool at pool_off[side] + (i mod pool) * stride
     std::vector<uint32_t> framed;
     std::vector<uint8_t> dec_row_used;
     SessTranscript tr;
@@ -228,16 +231,23 @@ struct Stream {
         }
         return r;
     }
+    // Input rows were allocated back to back per side (generate), so a run that does not wrap
+    // the input pool is consecutive handles at one stride: the codecs get its layout instead of
+    // checking and looking it up (the row table is cold).
+    uint64_t layout(int side, uint32_t index, uint32_t k) const {
+        if (!pool_affine || index % pool + k > pool) return 0;
+        return (uint64_t)(pool_off[side] + (index % pool) * pool_stride) << 32 | pool_stride;
+    }
     bool enc_add_run(uint32_t index, uint32_t k, uint32_t len, uint32_t* col0) {
         const uint32_t hb = length_header_bytes(len);
-        if (!enc->add_run(&enc_rows[index], k, hb + len, hb, len, true, col0)) return false;
+        if (!enc->add_run(&enc_rows[index], k, hb + len, hb, len, true, col0, layout(0, index, k))) return false;
         alg_bytes += (uint64_t)(hb + len) * k;
         payload_bytes += (uint64_t)len * k;
         return true;
     }
     bool dec_add_run(uint32_t col0, uint32_t index, uint32_t k, uint32_t len) {
         const uint32_t hb = length_header_bytes(len);
-        if (!dec->add_run_inorder(col0, &dec_rows[index], k, hb + len, hb, len, true)) return false;
+        if (!dec->add_run_inorder(col0, &dec_rows[index], k, hb + len, hb, len, true, layout(1, index, k))) return false;
         alg_bytes += (uint64_t)(hb + len) * k;
         return true;
     }
@@ -1306,6 +1316,16 @@ int tamd_session_generate(void* sp) {
             }
             std::vector<RowId>& rows = side ? st.dec_rows : st.enc_rows;
             for (uint32_t i = pool; i < n; ++i) rows[i] = rows[i - pool];
+        }
+        st.pool = pool;
+        st.pool_affine = pool >= 2;
+        for (int side = 0; side < 2 && st.pool_affine; ++side) {
+            const std::vector<RowId>& rows = side ? st.dec_rows : st.enc_rows;
+            const uint32_t o0 = st.ctx->rows.offset(rows[0]), stride = st.ctx->rows.offset(rows[1]) - o0;
+            st.pool_affine = consecutive_handles(rows.data(), pool) && stride > 0 &&
+                             st.ctx->rows.affine(rows[0], pool, stride) && (!side || stride == st.pool_stride);
+            st.pool_off[side] = o0;
+            st.pool_stride = stride;
         }
     });
     if (full) { s->error = "arena too small for the session inputs"; return -1; }
