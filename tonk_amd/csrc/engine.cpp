@@ -612,6 +612,7 @@ void LaneSums::reset(RowTable& rows) {
     n_ = 0;
     snaps_.clear();
     dyn_.clear();
+    drop_fold(rows);
     content_ = 0;
     bytes = 0;
 }
@@ -620,7 +621,50 @@ static inline bool same_coefs(const uint8_t* a, const uint8_t* b) {
     return a[0] == b[0] && a[1] == b[1] && a[2] == b[2];
 }
 
-void LaneSums::read(RowTable& rows, const ExpansionTable& ex, Sym& out, const uint8_t* c, uint32_t limit) {
+uint32_t LaneSums::dyn_fold_above() {
+    static const uint32_t v = getenv("TONK_AMD_DYN_FOLD") ? (uint32_t)atoi(getenv("TONK_AMD_DYN_FOLD")) : 4u;
+    return v;
+}
+
+// The dyn_ packets (and an earlier fold) into three rows, one combine each: every later read
+// names those three rows instead of every packet's expansion again.
+bool LaneSums::fold_dyn(RowTable& rows, ProgramBuilder& pb, const ExpansionTable& ex) {
+    uint32_t len = fold_len_;
+    for (const T& d : dyn_)
+        if (d.len > len) len = d.len;
+    RowId nf[3];
+    for (unsigned s = 0; s < 3; ++s) {
+        nf[s] = rows.alloc(len);
+        if (nf[s] == kNoRow) {
+            for (unsigned q = 0; q < s; ++q) rows.free_deferred(nf[q]);
+            return false;
+        }
+    }
+    thread_local Sym t;
+    for (unsigned s = 0; s < 3; ++s) {
+        t.clear();
+        if (fold_[s] != kNoRow) t.push_back(Term{fold_[s], fold_len_, 1});
+        for (const T& d : dyn_) ex.append(rows, d.row, d.len, sum_coef(s, column_value(d.col)), t);
+        sym_merge(t);
+        pb.combine(nf[s], t.data(), t.size(), len);
+    }
+    drop_fold(rows);
+    for (unsigned s = 0; s < 3; ++s) fold_[s] = nf[s];
+    fold_len_ = len;
+    dyn_.clear();
+    return true;
+}
+
+void LaneSums::drop_fold(RowTable& rows) {
+    for (unsigned s = 0; s < 3; ++s) {
+        rows.free_deferred(fold_[s]);
+        fold_[s] = kNoRow;
+    }
+    fold_len_ = 0;
+}
+
+void LaneSums::read(RowTable& rows, const ExpansionTable& ex, Sym& out, const uint8_t* c, uint32_t limit,
+                    ProgramBuilder* pb) {
     if (!limit || (!c[0] && !c[1] && !c[2])) return;
     TAMD_PROF_SCOPE(kLaneRead);
     const uint32_t clip = content_ < limit ? content_ : limit;
@@ -641,6 +685,13 @@ void LaneSums::read(RowTable& rows, const ExpansionTable& ex, Sym& out, const ui
             if (base_[s] != kNoRow && c[s]) out.push_back(Term{base_[s], clip, c[s]});
     }
     TAMD_PROF_SCOPE(kLaneDyn);
+    const uint32_t fold_at = dyn_fold_above();
+    // (only where expansions are limited -- the few-stream sessions and the C ABI, whose
+    // decoders pile up recovered packets at high loss; the batched sessions inline everything
+    // and a fold there costs a level for little: 1.05x the control time on the headline)
+    if (pb && fold_at && dyn_.size() >= fold_at && ex.expand_limit != ~0u) fold_dyn(rows, *pb, ex);
+    for (unsigned s = 0; s < 3; ++s)
+        if (fold_[s] != kNoRow && c[s]) out.push_back(Term{fold_[s], fold_len_ < limit ? fold_len_ : limit, c[s]});
     for (const T& d : dyn_) {
         const uint32_t l = d.len < limit ? d.len : limit;
         const uint8_t cx = column_value(d.col);
@@ -798,7 +849,8 @@ void LaneSums::flush(RowTable& rows, ProgramBuilder& pb, const ExpansionTable& e
     }
     n_closed_ = 0;
 
-    if (terms_.empty() && dyn_.empty()) {
+    const bool folded = fold_[0] != kNoRow;
+    if (terms_.empty() && dyn_.empty() && !folded) {
         // Nothing accumulated since the last flush: snapshots (if any) alias the bases.
         snaps_.clear();
         return;
@@ -817,11 +869,12 @@ void LaneSums::flush(RowTable& rows, ProgramBuilder& pb, const ExpansionTable& e
         state_is_new = true;
     }
 
-    if (!dyn_.empty()) {
+    if (!dyn_.empty() || folded) {
         // Fold contributions of rows produced by this program into the carried values.
         for (unsigned s = 0; s < 3; ++s) {
             Sym t;
             if (state[s] != kNoRow) t.push_back(Term{state[s], rows.cap_bytes(state[s]), 1});
+            if (fold_[s] != kNoRow) t.push_back(Term{fold_[s], fold_len_, 1});
             for (const T& d : dyn_) ex.append(rows, d.row, d.len, sum_coef(s, column_value(d.col)), t);
             sym_merge(t);
             const RowId carry = rows.alloc(content_);
@@ -840,6 +893,7 @@ void LaneSums::flush(RowTable& rows, ProgramBuilder& pb, const ExpansionTable& e
     n_ = 0;
     snaps_.clear();
     dyn_.clear();
+    drop_fold(rows);
 }
 
 void LaneSums::release(RowTable& rows) {
@@ -858,6 +912,7 @@ void LaneSums::release(RowTable& rows) {
     n_ = 0;
     snaps_.clear();
     dyn_.clear();
+    drop_fold(rows);
     content_ = bytes = 0;
 }
 

@@ -391,7 +391,10 @@ public:
         terms_.push_back(T{row, len, off, stride, count, column});
     }
     // Append c[0]*sum_0 + c[1]*sum_1 + c[2]*sum_2 (current values, clipped to `limit` bytes).
-    void read(RowTable& rows, const ExpansionTable& ex, Sym& out, const uint8_t* c, uint32_t limit);
+    // With `pb`, packets produced in this program that have piled up (dyn_, each read as its
+    // expansion by every read) are first folded into three rows (dyn_fold_above()).
+    void read(RowTable& rows, const ExpansionTable& ex, Sym& out, const uint8_t* c, uint32_t limit,
+              ProgramBuilder* pb = nullptr);
     // Emit the scan (and fix-up) ops for the pending program and rebase the sums.
     void flush(RowTable& rows, ProgramBuilder& pb, const ExpansionTable& ex);
     // Drop everything (codec destruction).
@@ -402,6 +405,8 @@ public:
     // a run of `count` lane packets: rows off + k*stride, columns col + 8k (count 1: a single row)
     struct T { RowId row; uint32_t len, off, stride, count, col; };
     static uint32_t chunk();  // longest packet walk of one scan op (see emit_scan)
+    // read() folds dyn_ once it holds this many packets (TONK_AMD_DYN_FOLD; 0: never)
+    static uint32_t dyn_fold_above();
     static uint32_t inline_max();  // segments this short are walked by the chain op (emit_scan)
     // Level of snapshot rows: chunk ops run at level 1, the chain op that stores the snapshots at
     // level 2 (a short scan is one op, also placed at level 2).  Readers are assigned levels when
@@ -424,6 +429,12 @@ private:
     std::vector<T> terms_;                      // level-0 packets accumulated since base_
     std::vector<Snap> snaps_;
     std::vector<T> dyn_;                        // packets produced in this program (level > 0)
+    // dyn_ packets folded away: fold_[s] = sum over them of coef_s(cx) * packet (this program's
+    // rows; read like base_, added into the carried values at flush)
+    RowId fold_[3] = {kNoRow, kNoRow, kNoRow};
+    uint32_t fold_len_ = 0;
+    bool fold_dyn(RowTable& rows, ProgramBuilder& pb, const ExpansionTable& ex);
+    void drop_fold(RowTable& rows);
     // closed epochs (reset while the program was pending) still owe their snapshots
     struct Closed { RowId base[3]; std::vector<T> terms; std::vector<Snap> snaps; };
     std::vector<Closed> closed_;  // [0, n_closed_) pending; the rest keep storage for reuse
