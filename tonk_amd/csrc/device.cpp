@@ -900,18 +900,19 @@ void Device::launch_step(Inflight* fresh, unsigned long long* stamps) {
     static const bool class_major = !getenv("TONK_AMD_CLASS_MAJOR") || atoi(getenv("TONK_AMD_CLASS_MAJOR")) != 0;
     sg.flags = class_major ? 1u : 0u;
     hipStream_t st = (hipStream_t)stream_;
-    uint32_t grid = (cnt + 3) / 4;
+    // Class-0 ops are shared by a workgroup only in launches too small to fill the chip twice
+    // over with single-wave items; in the big ones they run as ordinary (first) items.  Only the
+    // first segment's class-0 items (they lead it) can be shared.  A shared item gets a
+    // workgroup of its own, the single-wave items four to a workgroup beside them.
+    static const int share_mode = getenv("TONK_AMD_SHARE") ? atoi(getenv("TONK_AMD_SHARE")) : 0;  // A/B (profiling)
+    const uint32_t shared = (share_mode == 1 || (share_mode == 0 && cnt < 2u * 4u * max_grid_)) ? coop : 0u;
+    uint32_t grid = shared + (cnt - shared + 3) / 4;
     if (grid > max_grid_) grid = max_grid_;
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (timing_) {
         e0 = (hipEvent_t)timing_event();
         e1 = (hipEvent_t)timing_event();
     }
-    // Class-0 ops are shared by a workgroup only in launches too small to fill the chip twice
-    // over with single-wave items; in the big ones they run as ordinary (first) items.  Only the
-    // first segment's class-0 items (they lead it) can be shared.
-    static const int share_mode = getenv("TONK_AMD_SHARE") ? atoi(getenv("TONK_AMD_SHARE")) : 0;  // A/B (profiling)
-    const uint32_t shared = (share_mode == 1 || (share_mode == 0 && cnt < 2u * 4u * max_grid_)) ? coop : 0u;
     const ExecFn fn = (ExecFn)exec_kernel_;
     // Profiling only: TONK_AMD_LAUNCH_STAMPS=<launch number> records per-item stamps of every
     // segment of that launch (a pipelined one) into tonk_amd_launch_stamps.txt.

@@ -785,11 +785,15 @@ __device__ __forceinline__ void exec_level(const tamd_segments& sg, const uint8_
             lds_blk[0].y += n_shared;
             lds_blk[0].z -= n_shared;
         }
-        const uint32_t G = gridDim.x, g = blockIdx.x;
+        // (a small launch gives the shared items workgroups of their own, the first n_shared:
+        // the single-wave items then go to the others, none waiting behind a shared one)
+        const bool apart = n_shared && gridDim.x > n_shared;
+        const uint32_t G = apart ? gridDim.x - n_shared : gridDim.x, g = apart ? blockIdx.x - n_shared : blockIdx.x;
+        const bool none = apart && blockIdx.x < n_shared;
         uint32_t before = 0;
         for (uint32_t b = 0; b < nb; ++b) {
             const uint32_t cnt = lds_blk[b].z, r = (g + G - (before & ~7u) % G) % G;
-            lds_wg[b] = make_uint2(r, cnt > r ? (cnt - 1u - r) / G + 1u : 0u);
+            lds_wg[b] = make_uint2(r, !none && cnt > r ? (cnt - 1u - r) / G + 1u : 0u);
             before += cnt;
         }
         lds_wg[nb] = make_uint2(0, ~0u);
@@ -861,6 +865,7 @@ __device__ __forceinline__ void exec_level(const tamd_segments& sg, const uint8_
     // them (a stratified sample of the level: ordered by cost class, most expensive first); its
     // waves claim them one at a time through an LDS counter, so a wave that drew a long op does
     // not hold up the others.
+    const uint32_t wg_stride = n_shared && gridDim.x > n_shared ? gridDim.x - n_shared : gridDim.x;
     for (;;) {
         uint32_t k = 0;
         if (lane == 0) k = atomicAdd(&claim, 1u);
@@ -870,7 +875,7 @@ __device__ __forceinline__ void exec_level(const tamd_segments& sg, const uint8_
         while (k >= lds_wg[b].y) k -= lds_wg[b++].y;
         if (lds_wg[b].y == ~0u) break;
         const uint32_t seg = uniform(lds_blk[b].x);
-        const uint32_t rel = uniform(lds_blk[b].y) + uniform(lds_wg[b].x) + k * gridDim.x;
+        const uint32_t rel = uniform(lds_blk[b].y) + uniform(lds_wg[b].x) + k * wg_stride;
         const uint32_t at = uniform(lds_blk[b].w) + rel;  // (stamps)
         const tamd_segment sd = lds_seg[seg];
         const tamd_op* __restrict__ sops = (const tamd_op*)(pbase + uniform(sd.ops));
