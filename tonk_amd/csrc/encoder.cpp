@@ -217,22 +217,30 @@ uint32_t Encoder::add_first(RowId row, uint32_t framed_bytes, uint32_t header_by
 bool Encoder::add_run(const RowId* rows, uint32_t k, uint32_t framed_bytes, uint32_t header_bytes,
                       uint32_t payload_bytes, bool borrowed, uint32_t* first_col, uint64_t layout) {
     if (disabled_ || remaining_slots() < k || !k) return false;
-    // the first add may start a window; the rest append to it (count_ > 0, element == count_)
-    *first_col = add_first(rows[0], framed_bytes, header_bytes, payload_bytes, nullptr, borrowed);
-    if (k == 1) return true;
-    append(rows + 1, k - 1, framed_bytes, header_bytes, borrowed ? 0 : 1, nullptr, (uint32_t)now_msec(),
-           layout ? layout + ((layout & 0xffffffffull) << 32) : 0);  // (rows + 1: one stride on)
-    count_ += k - 1;
-    next_column_ = col_add(next_column_, k - 1);
-    // every lane one of these columns fell on (all k - 1 have the same length)
-    const uint32_t first = col_inc(*first_col);
-    for (uint32_t j = 0; j < k - 1 && j < kLanes; ++j) {
+    // A first add that starts a window goes alone; the rest (all k when the window is open)
+    // append at once (count_ > 0, element == count_).
+    uint32_t skip = 0;
+    if (count_ == 0) {
+        *first_col = add_first(rows[0], framed_bytes, header_bytes, payload_bytes, nullptr, borrowed);
+        if (k == 1) return true;
+        skip = 1;
+    } else {
+        *first_col = next_column_;
+    }
+    const uint32_t m = k - skip;
+    append(rows + skip, m, framed_bytes, header_bytes, borrowed ? 0 : 1, nullptr, (uint32_t)now_msec(),
+           layout && skip ? layout + ((layout & 0xffffffffull) << 32) : layout);  // (rows + 1: one stride on)
+    count_ += m;
+    const uint32_t first = next_column_;
+    next_column_ = col_add(next_column_, m);
+    // every lane one of these columns fell on (all m have the same length)
+    for (uint32_t j = 0; j < m && j < kLanes; ++j) {
         Lane& lane = lanes_[(first + j) % kLanes];
         if (lane.longest < framed_bytes) lane.longest = framed_bytes;
     }
     if (longest_ < framed_bytes) longest_ = framed_bytes;
-    stats_[0] += k - 1;
-    stats_[1] += (uint64_t)payload_bytes * (k - 1);
+    stats_[0] += m;
+    stats_[1] += (uint64_t)payload_bytes * m;
     return true;
 }
 
