@@ -716,6 +716,7 @@ SIAMESE_EXPORT int siamese_init_(int version) {
     if (const char* a = getenv("TONK_AMD_CAPI_SLOT_KB")) slot_kb = strtoull(a, nullptr, 10);
     if (const char* a = getenv("TONK_AMD_CAPI_OVERSIZE_KB")) big_kb = strtoull(a, nullptr, 10);
     g_rt->dev.set_program_slots(128, slot_kb << 10, big_kb << 10);
+    g_rt->dev.set_small_uploads(true);  // per-call programs are small
     if (!g_rt->dev.init_growable(device, arena_mb << 20, max_mb << 20)) {
         fprintf(stderr, "%s\n", g_rt->dev.error().c_str());
         return Siamese_Disabled;

@@ -25,6 +25,30 @@ struct ScatterDescDev { uint32_t row, len, src, pad; };
 extern "C" __global__ void tamd_scatter_rows(const ScatterDescDev*, uint32_t, const uint8_t*, uint8_t*);
 struct HostCopyDev { uint64_t host; uint32_t unit, len; };
 extern "C" __global__ void tamd_host_copy(const HostCopyDev*, uint32_t, uint8_t*, uint32_t);
+extern "C" __global__ void tamd_copy_in(const uint4*, uint4*, uint32_t, const uint4*, uint4*, uint32_t);
+namespace {
+// Program uploads below this many bytes go through tamd_copy_in (a launch whose threads read the
+// pinned bytes) instead of the DMA engine, on devices that asked for it (set_small_uploads: few
+// streams, the C ABI); TONK_AMD_SMALL_UPLOAD overrides the size (0: never, A/B).
+size_t small_upload() {
+    static const size_t v = getenv("TONK_AMD_SMALL_UPLOAD") ? (size_t)atoll(getenv("TONK_AMD_SMALL_UPLOAD")) : (256u << 10);
+    return v;
+}
+// Two host -> device ranges, by the copy kernel when small, else by DMA.
+void upload2(bool small_ok, void* d0, const void* h0, size_t b0, void* d1, const void* h1, size_t b1, hipStream_t st) {
+    if (small_ok && b0 + b1 < small_upload()) {
+        const uint32_t n0 = (uint32_t)((b0 + 15) / 16), n1 = (uint32_t)((b1 + 15) / 16);
+        const uint32_t blocks = std::min<uint32_t>(256u, (n0 + n1 + 255) / 256);
+        if (n0 + n1)
+            hipLaunchKernelGGL(tamd_copy_in, dim3(blocks), dim3(256), 0, st, (const uint4*)h0, (uint4*)d0, n0,
+                               (const uint4*)h1, (uint4*)d1, n1);
+        return;
+    }
+    if (b0) hipMemcpyAsync(d0, h0, b0, hipMemcpyHostToDevice, st);
+    if (b1) hipMemcpyAsync(d1, h1, b1, hipMemcpyHostToDevice, st);
+}
+}  // namespace
+size_t tamd::Device::small_upload_limit() { return small_upload(); }
 
 struct GenDescDev { uint32_t row, index, len, pad; unsigned long long seed; };
 struct DigestDescDev { uint32_t row, skip, len, pad; };
@@ -426,7 +450,13 @@ bool Device::alloc_slots(size_t cap) {
     slot_cap_ = 0;
     // one pinned and one device allocation, split into the slots
     if (hipMalloc((void**)&prog_dev_, dcap * slots_.size() + big) != hipSuccess) return false;
-    if (hipHostMalloc((void**)&prog_host_, hcap * slots_.size() + big, hipHostMallocDefault) != hipSuccess) return false;
+    // (coherent where small programs are read by the device's threads, tamd_copy_in: a slot is
+    // rewritten for later programs and no device cache may keep an older program's bytes.  Only
+    // there: the batched sessions' multi-MB programs go by DMA, and their host fill into
+    // coherent memory cost 2 % of the control time, 4 % of the headline)
+    if (hipHostMalloc((void**)&prog_host_, hcap * slots_.size() + big,
+                      small_uploads_ ? hipHostMallocMapped | hipHostMallocCoherent : hipHostMallocDefault) != hipSuccess)
+        return false;
     for (size_t k = 0; k < slots_.size(); ++k) {
         Slot& s = slots_[k];
         s.host = prog_host_ + k * hcap;
@@ -667,8 +697,8 @@ uint64_t Device::close_program(int h, Part* const* parts, size_t n) {
     const uint32_t recs = slot.bump.load(std::memory_order_relaxed);
     const size_t hrecs = recs < asm_host_recs_ ? recs : asm_host_recs_;
     const auto u0 = std::chrono::steady_clock::now();
-    HIPCHK(hipMemcpyAsync(slot.dev, slot.host, at * 8, hipMemcpyHostToDevice, st));
-    HIPCHK(hipMemcpyAsync(slot.dev + ibytes, slot.host + ibytes, hrecs * 16, hipMemcpyHostToDevice, st));
+    upload2(small_uploads_, slot.dev, slot.host, at * 8, slot.dev + ibytes, slot.host + ibytes, hrecs * 16, st);
+    HIPCHK(hipGetLastError());
     {
         std::lock_guard<std::mutex> g(spill_mu_);
         size_t keep = 0;
@@ -999,7 +1029,8 @@ uint64_t Device::launch() {
     hipStream_t st = (hipStream_t)stream_;
     Slot& slot = *P.slot;
     const auto u0 = std::chrono::steady_clock::now();
-    HIPCHK(hipMemcpyAsync(slot.dev, slot.host, P.total, hipMemcpyHostToDevice, st));
+    upload2(small_uploads_, slot.dev, slot.host, P.total, nullptr, nullptr, 0, st);
+    HIPCHK(hipGetLastError());
     const double up_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - u0).count();
     stats_.upload_enqueue_ms += up_ms;
     if (up_ms > 1.0 && getenv("TONK_AMD_TRACE_UPLOADS"))

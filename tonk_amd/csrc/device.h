@@ -130,6 +130,10 @@ public:
     // Parallel-assembly slots: `count` slots of `host_mb` MB pinned staging (the record area a
     // program can fill) and 4x that on the device, plus an item area; call before init.
     void set_assembly_slots(size_t count, size_t host_mb);
+    // Small programs (few-stream sessions, the C ABI) are uploaded by a copy kernel instead of DMA
+    // (its latency, not its rate, is what a single program waits for); call before init.
+    void set_small_uploads(bool on) { small_uploads_ = on && small_upload_limit() > 0; }
+    static size_t small_upload_limit();
     // Whether a program of `recs` records (instructions + ops) and `items` work items fits a slot;
     // ensure_assembly grows every slot to fit (drains the device first: no program may be open).
     bool assembly_fits(size_t recs, size_t items) const;
@@ -236,6 +240,7 @@ private:
     std::atomic<bool> growing_{false};
     uint32_t* d_gf_ = nullptr;
     uint8_t* d_zero_ = nullptr;
+    bool small_uploads_ = false;
     uint32_t max_grid_ = 256;
     const void* exec_kernel_ = nullptr;  // tamd_exec16
     // host staging

@@ -1424,6 +1424,20 @@ tamd_host_copy(const HostCopyDesc* __restrict__ d, uint32_t n, uint8_t* __restri
     for (uint32_t i = n16 * 16u + threadIdx.x; i < c.len; i += blockDim.x) dst[i] = src[i];
 }
 
+// A small program's upload (Device::close_program / run, below kSmallUpload bytes): two ranges of
+// pinned host memory into program memory, read over the link by the threads of one launch -- a
+// DMA-engine copy costs tens of microseconds of latency before the first level can start, which
+// a single stream or a per-call program waits out in full.
+extern "C" __global__ void __launch_bounds__(256)
+tamd_copy_in(const uint4* __restrict__ s0, uint4* __restrict__ d0, uint32_t n0, const uint4* __restrict__ s1,
+             uint4* __restrict__ d1, uint32_t n1) {
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n0 + n1; i += stride) {
+        if (i < n0) d0[i] = s0[i];
+        else d1[i - n0] = s1[i - n0];
+    }
+}
+
 // Digest of rows (FNV-1a 64 over `len` bytes starting `skip` bytes into the row): one thread
 // per row, for output verification after a timed run (not on the timed path).
 struct DigestDesc { uint32_t row, skip, len, pad; };

@@ -1202,6 +1202,7 @@ void* tamd_session_create(const tamd_session_params* p, char* err, size_t err_le
         const int v = atoi(a);
         s->fr_ahead = v < 1 ? 1u : v > (int)Session::kFrRing - 1 ? Session::kFrRing - 1 : (uint32_t)v;
     }
+    s->dev.set_small_uploads(p->n_streams <= 4);
     if (s->fr_mode) s->dev.set_assembly_slots(8, p->n_streams <= 4 ? 8 : 24);
     else {
         // (TONK_AMD_SLOTS: A/B knob for the slot count of the pass schedule)
