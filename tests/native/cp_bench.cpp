@@ -211,6 +211,30 @@ static void dump_reads(Context& ctx) {
         fprintf(stderr, "encoder-side runs (multi+dense+cauchy+const): reads %zu distinct %zu; rows in both multi and dense %zu\n",
                 md_reads, md.size(), both);
     }
+    // rows read by op kind: recovery rows (a STORE with a footer), lane scans (STOREC / ACC3 /
+    // LANE3), other (decoder rows, partial sums, temps)
+    {
+        uint64_t by[3] = {0, 0, 0}, nops[3] = {0, 0, 0};
+        for (const tamd_op& o : ctx.pb.ops()) {
+            uint64_t rd = 0;
+            int kind = 2;
+            for (uint32_t k = o.first; k < o.first + o.count; ++k) {
+                const uint32_t w = ins[k].w0, kk = w & 0xff;
+                if (kk == TAMD_I_ACC || kk == TAMD_I_ACC3) ++rd;
+                else if (kk == TAMD_I_ACCR) {
+                    rd += ins[k].cap;
+                    if (((w >> 8) & 0xff) == TAMD_R_LANE3) kind = 1;
+                }
+                if (kk == TAMD_I_STOREC || kk == TAMD_I_ACC3) kind = 1;
+                if (kk == TAMD_I_STORE && ((w >> 8) & 0xff) && kind != 1) kind = 0;
+            }
+            by[kind] += rd;
+            nops[kind]++;
+        }
+        fprintf(stderr, "reads by op kind: recovery rows %llu (%llu ops), lane scans %llu (%llu ops), other %llu (%llu ops)\n",
+                (unsigned long long)by[0], (unsigned long long)nops[0], (unsigned long long)by[1], (unsigned long long)nops[1],
+                (unsigned long long)by[2], (unsigned long long)nops[2]);
+    }
     uint64_t hist[5] = {0, 0, 0, 0, 0};
     for (const auto& kv : dense_rows) hist[kv.second < 4 ? kv.second : 4]++;
     fprintf(stderr, "dense: %zu distinct packet rows; read by 1/2/3/4+ runs: %llu %llu %llu %llu\n", dense_rows.size(),
