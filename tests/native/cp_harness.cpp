@@ -212,8 +212,52 @@ struct Harness {
         return r;
     }
 
+    // Within a program the device runs each level's ops together, in no order (levels run in
+    // order, which the oracle's level-by-level run checks through the outputs): no row one op of
+    // a level writes may be read or written by another op of the same level.
+    void check_levels() {
+        const auto& ops_v = ctx.pb.ops();
+        const auto& lv = ctx.pb.op_levels();
+        const auto& in = ctx.pb.instrs();
+        std::unordered_map<uint64_t, uint32_t> writer;  // (level, row) -> op that writes it
+        auto bad = [&](size_t i, uint32_t l, uint32_t x, uint32_t other) {
+            if (error.empty())
+                error = "program " + std::to_string(programs) + ": ops " + std::to_string(other) + " and " +
+                        std::to_string(i) + " of level " + std::to_string(l) + " both use row " + std::to_string(x) +
+                        ", one writing it";
+        };
+        std::vector<uint32_t> rd;
+        for (size_t i = 0; i < ops_v.size(); ++i) {
+            const uint32_t l = lv[i] / TAMD_COST_CLASSES;
+            for (uint32_t k = ops_v[i].first; k < ops_v[i].first + ops_v[i].count; ++k) {
+                const uint32_t kind = in[k].w0 & 0xff;
+                if (kind == TAMD_I_STORE || kind == TAMD_I_STOREC) {
+                    const uint64_t key = (uint64_t)l << 32 | in[k].row;
+                    const auto it = writer.find(key);
+                    if (it != writer.end() && it->second != i) bad(i, l, in[k].row, it->second);
+                    writer[key] = (uint32_t)i;
+                }
+            }
+        }
+        for (size_t i = 0; i < ops_v.size(); ++i) {
+            const uint32_t l = lv[i] / TAMD_COST_CLASSES;
+            rd.clear();
+            for (uint32_t k = ops_v[i].first; k < ops_v[i].first + ops_v[i].count; ++k) {
+                const uint32_t kind = in[k].w0 & 0xff;
+                if (kind == TAMD_I_ACC || kind == TAMD_I_ACC3) rd.push_back(in[k].row);
+                else if (kind == TAMD_I_ACCR)
+                    for (uint32_t q = 0; q < in[k].cap; ++q) rd.push_back(in[k].row + q * in[k + 1].row);
+            }
+            for (uint32_t x : rd) {
+                const auto it = writer.find((uint64_t)l << 32 | x);
+                if (it != writer.end() && it->second != i) bad(i, l, x, it->second);
+            }
+        }
+    }
+
     void flush() {
         ctx.prepare_flush();
+        check_levels();
         if (g_pipeline) check_pipeline();
         const auto& ops_v = ctx.pb.ops();
         const auto& lv = ctx.pb.op_levels();

@@ -63,6 +63,7 @@ def test_control_plane_matches_reference(harness, golden_index, tmp_path, name, 
     # (the batched session's layout): windows are long segments, so Siamese rows read their sum
     # ranges straight from the packets and consecutive ones are grouped (Encoder::defer_dense)
     contig = int("contig" in mode)
+    # (every mode also checks that no op of a level writes a row another op of that level uses)
     args = [harness, str(out), f"mode={base}", f"batch={batch}", f"dirty={dirty}", f"pipeline={pipe}",
             f"drain={drain}", f"expand={expand}", f"backsub={backsub}", f"split={split}", f"contig={contig}"] + sc["args"] + [
         f"seed_data={1000 + sid}", f"seed_loss={2000 + sid}"]
