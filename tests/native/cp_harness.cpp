@@ -10,6 +10,7 @@
 #include "../../tonk_amd/csrc/decoder.h"
 #include "../../tonk_amd/csrc/workload.h"
 #include "../../tonk_amd/csrc/transcript.h"
+#include "../../tonk_amd/csrc/prof.h"
 #include "../../oracle/siamese_oracle.h"
 
 #include <chrono>
@@ -33,6 +34,11 @@ static bool g_pipeline = false;
 static uint32_t g_expand = ~0u;  // expand=<terms>: the session's expansion limit
 static uint32_t g_backsub = ~0u;  // backsub=<unknowns>: back substitution over materialized rows
 static uint32_t g_split = 0;      // split=<packets>: the batched session's dense-range split
+// ahead=<K>: encode-ahead as the C ABI runs it (capi.cpp): from the second encode in a row (no
+// other encoder call between) up to K more encodes run ahead while Encoder::encode_is_quiet, and
+// are handed out by the next encode calls; any other encoder call first takes the rest back
+// (Encoder::rewind) and frees their rows.  The depth doubles from 1 while they are all used.
+static uint32_t g_ahead = 0;
 static uint64_t g_rs[9];  // CP_READ_STATS totals
 static bool g_contig = false;  // contig=1: originals in rows reserved up front, in order, one range per
                                // side and borrowed by the codecs (the batched session's layout)
@@ -40,6 +46,18 @@ static uint32_t g_drain = 0;  // pipelined: complete every in-flight program aft
 #include <map>
 #include <set>
 #include <unordered_map>
+
+#ifdef TAMD_PROF  // (_build/cp_harness_prof: cycles per control-plane phase at exit)
+namespace tamd { namespace prof {
+thread_local uint64_t cycles[kSlots];
+thread_local uint64_t calls[kSlots];
+const char* const names[kSlots] = {"enc_add", "enc_encode", "enc_ack", "dec_add_orig", "dec_add_rec", "dec_decode",
+    "dec_ack", "dec_is_ready", "gen_matrix", "ge", "elim", "lower_tri", "back_sub", "chain_flush", "sym_merge",
+    "prepare_flush", "finish_flush", "release", "enc_dense", "enc_light", "enc_emit", "elim_sums", "elim_pairs",
+    "elim_fold", "enc_cauchy", "enc_remove", "elim_start", "lane_read", "lane_dyn", "combine", "fold_merge", "alloc",
+    "x1", "x2", "x3", "x4"};
+} }
+#endif
 
 struct Harness {
     Params p;
@@ -373,6 +391,7 @@ struct Harness {
     struct DecRef { };
 
     int enc_add(uint32_t index, uint32_t len, uint32_t* col) {
+        cancel_ahead();
         uint32_t framed = 0, header = 0;
         const RowId r = write_original(index, len, &framed, &header);
         if (r == kNoRow) { error = "arena full"; return 5; }
@@ -384,6 +403,7 @@ struct Harness {
     // batched adds (the session's path), off with nobatch=1
     bool enc_add_run(uint32_t index, uint32_t k, uint32_t len, uint32_t* col0) {
         if (g_nobatch) return false;
+        cancel_ahead();
         std::vector<RowId> rows(k);
         uint32_t framed = 0, header = 0;
         for (uint32_t j = 0; j < k; ++j) {
@@ -426,11 +446,59 @@ struct Harness {
         TScope(Harness& hh, int kk) : h(hh), k(kk), t0(tnow()) {}
         ~TScope() { h.t_ns[k] += tnow() - t0; h.t_n[k]++; }
     };
+    std::vector<RecoveryOut> spec;
+    std::vector<Encoder::Mark> marks;  // marks[i]: the encoder before spec[i] was encoded
+    size_t spec_next = 0;
+    uint32_t depth = 1;
+    bool last_enc = false;
+    uint64_t ahead_used = 0, ahead_rewound = 0;
+    void cancel_ahead() {
+        if (spec_next < spec.size()) {
+            E()->rewind(marks[spec_next]);
+            for (size_t i = spec_next; i < spec.size(); ++i) ctx.rows.free_deferred(spec[i].row);
+            ahead_rewound += spec.size() - spec_next;
+            depth = 1;
+        }
+        spec.clear();
+        marks.clear();
+        spec_next = 0;
+        last_enc = false;
+    }
     int enc_encode(RecRef& r) {
         TScope ts(*this, 0);
-        return E()->encode(r.out);
+        if (g_ahead) {
+            if (spec_next < spec.size()) {
+                r.out = spec[spec_next++];
+                ++ahead_used;
+                return 0;
+            }
+            if (!spec.empty()) {
+                depth = depth * 2 < g_ahead ? depth * 2 : g_ahead;
+                spec.clear();
+                marks.clear();
+                spec_next = 0;
+            }
+        }
+        const int rc = E()->encode(r.out);
+        if (g_ahead && rc == kSuccess && last_enc) {
+            for (uint32_t k = 0; k < depth && E()->encode_is_quiet(); ++k) {
+                const Encoder::Mark m = E()->mark();
+                RecoveryOut o;
+                if (E()->encode(o) != kSuccess) {
+                    E()->rewind(m);
+                    break;
+                }
+                marks.push_back(m);
+                spec.push_back(o);
+            }
+        }
+        last_enc = rc == kSuccess;
+        return rc;
     }
-    int enc_ack(const uint8_t* buf, uint32_t n, uint32_t* next) { return E()->acknowledge(buf, n, next); }
+    int enc_ack(const uint8_t* buf, uint32_t n, uint32_t* next) {
+        cancel_ahead();
+        return E()->acknowledge(buf, n, next);
+    }
     int dec_add_original(uint32_t col, uint32_t index, uint32_t len) {
         uint32_t framed = 0, header = 0;
         const RowId r = write_original(index, len, &framed, &header, 1);
@@ -475,13 +543,18 @@ struct Harness {
         return rc;
     }
     int dec_ack(uint8_t* buf, uint32_t limit, uint32_t* used) { return D()->ack(buf, limit, used); }
-    void stats(uint64_t e[9], uint64_t d[11]) { E()->stats(e, 9); D()->stats(d, 11); }
+    void stats(uint64_t e[9], uint64_t d[11]) {
+        cancel_ahead();
+        E()->stats(e, 9);
+        D()->stats(d, 11);
+    }
     uint64_t vclock = 0;
     void set_time(uint64_t ms) {
         if (!vclock) enc->set_clock(&vclock);
         vclock = ms;
     }
     int enc_retransmit(uint32_t* num, uint32_t* bytes, const uint8_t** data) {
+        cancel_ahead();
         StoredOriginal ov;
         const StoredOriginal* o = &ov;
         const Result rc = E()->retransmit(&ov);
@@ -558,6 +631,7 @@ int main(int argc, char** argv) {
         else if (k == "backsub") g_backsub = (uint32_t)v;
         else if (k == "split") g_split = (uint32_t)v;
         else if (k == "contig") g_contig = v != 0;
+        else if (k == "ahead") g_ahead = (uint32_t)v;
         else if (parse_param(p, k, v)) {}
         else { fprintf(stderr, "bad key %s\n", k.c_str()); return 2; }
     }
@@ -584,6 +658,15 @@ int main(int argc, char** argv) {
     fprintf(stderr, "programs=%llu ops=%llu instrs=%llu levels=%llu live_rows=%zu pipelined_pairs=%llu\n",
             (unsigned long long)h.programs, (unsigned long long)h.ops, (unsigned long long)h.instrs,
             (unsigned long long)h.levels, h.ctx.rows.live_rows(), (unsigned long long)h.pipelined_pairs);
+#ifdef TAMD_PROF
+    for (int i = 0; i < prof::kSlots; ++i)
+        if (prof::calls[i])
+            fprintf(stderr, "%-14s calls %10llu  Mcyc %10.2f  cyc/call %10.0f\n", prof::names[i],
+                    (unsigned long long)prof::calls[i], prof::cycles[i] / 1e6, (double)prof::cycles[i] / prof::calls[i]);
+#endif
+    if (g_ahead)
+        fprintf(stderr, "ahead: used=%llu rewound=%llu\n", (unsigned long long)h.ahead_used,
+                (unsigned long long)h.ahead_rewound);
     if (getenv("CP_READ_STATS"))
         fprintf(stderr, "reads: acc %llu lane3 %llu cauchy %llu const %llu multi %llu dense %llu; distinct dense %llu, "
                 "distinct all %llu; ops with dense runs %llu\n",

@@ -64,8 +64,12 @@ def test_control_plane_matches_reference(harness, golden_index, tmp_path, name, 
     # ranges straight from the packets and consecutive ones are grouped (Encoder::defer_dense)
     contig = int("contig" in mode)
     # (every mode also checks that no op of a level writes a row another op of that level uses)
+    # "sync-exp" and "batch-dirty" also encode ahead as the C ABI does (Encoder::encode_is_quiet,
+    # rewind): up to 15 and 3 recovery packets
+    ahead = 15 if mode == "sync-exp" else 3 if mode == "batch-dirty" else 0
     args = [harness, str(out), f"mode={base}", f"batch={batch}", f"dirty={dirty}", f"pipeline={pipe}",
-            f"drain={drain}", f"expand={expand}", f"backsub={backsub}", f"split={split}", f"contig={contig}"] + sc["args"] + [
+            f"drain={drain}", f"expand={expand}", f"backsub={backsub}", f"split={split}", f"contig={contig}",
+            f"ahead={ahead}"] + sc["args"] + [
         f"seed_data={1000 + sid}", f"seed_loss={2000 + sid}"]
     r = subprocess.run(args, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]

@@ -404,8 +404,33 @@ struct Codec {
     ~Codec() { Device::host_free(pinned); }
 };
 
+// Encode-ahead.  A caller that encodes twice with no other call on the encoder between (the
+// end of a transfer: recovery packets until the receiver has everything, workload.h finish;
+// Tonk's flush of a quiet connection) is likely to encode again: from then on the same command
+// also encodes the next `depth` recovery packets while Encoder::encode_is_quiet (their encodes
+// change nothing but row counters and statistics), and reads them all back; the next calls
+// return them without a device round trip.  Any other call on the encoder first takes the
+// unused ones back (Encoder::rewind), so every result and statistic is the one a call-by-call
+// run gives.  The depth doubles (to TONK_AMD_CAPI_AHEAD, default 15; 0: off) while the packets
+// are all used and drops to 1 after a take-back.
 struct CEncoder : Codec {
     Encoder* enc = nullptr;
+    struct Ahead { size_t off; uint32_t total; };  // in `pinned`
+    std::vector<Ahead> ahead;
+    std::vector<Encoder::Mark> marks;  // marks[i]: the encoder before ahead[i] was encoded
+    size_t ahead_next = 0;
+    uint32_t depth = 1;
+    bool last_encode = false;  // the previous call on the encoder was a successful encode
+    void cancel_ahead() {
+        if (ahead_next < ahead.size()) {
+            enc->rewind(marks[ahead_next]);
+            depth = 1;
+        }
+        ahead.clear();
+        marks.clear();
+        ahead_next = 0;
+        last_encode = false;
+    }
 };
 
 void dump_encoders() {
@@ -814,6 +839,7 @@ SIAMESE_EXPORT SiameseResult siamese_encoder_add(SiameseEncoder encoder_t, Siame
     if (!e || !packet || !packet->Data || packet->DataBytes <= 0 || packet->DataBytes > SIAMESE_MAX_PACKET_BYTES)
         return Siamese_InvalidInput;
     API_CALL();
+    e->cancel_ahead();
     if (e->enc->disabled()) return Siamese_Disabled;
     if (e->enc->remaining_slots() <= 0) return Siamese_MaxPacketsReached;
     uint8_t* host = nullptr;
@@ -855,6 +881,7 @@ SIAMESE_EXPORT SiameseResult siamese_encoder_remove_before(SiameseEncoder encode
     CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
     if (!e || packetNum > SIAMESE_PACKET_NUM_MAX) return Siamese_InvalidInput;
     API_CALL();
+    e->cancel_ahead();
     e->enc->remove_before(packetNum);
     return Siamese_Success;
 }
@@ -864,6 +891,7 @@ SIAMESE_EXPORT SiameseResult siamese_encoder_ack(SiameseEncoder encoder_t, const
     CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
     if (!e || !buffer || bytes < 1 || !nextExpectedPacketNum) return Siamese_InvalidInput;
     API_CALL();
+    e->cancel_ahead();
     uint32_t next = 0;
     const Result r = e->enc->acknowledge((const uint8_t*)buffer, bytes, &next);
     if (r == kSuccess) *nextExpectedPacketNum = next;
@@ -874,6 +902,7 @@ SIAMESE_EXPORT SiameseResult siamese_encoder_retransmit(SiameseEncoder encoder_t
     CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
     if (!e || !original) return Siamese_InvalidInput;
     API_CALL();
+    e->cancel_ahead();
     original->Data = nullptr;
     original->DataBytes = 0;
     StoredOriginal ov;
@@ -890,28 +919,65 @@ SIAMESE_EXPORT SiameseResult siamese_encode(SiameseEncoder encoder_t, SiameseRec
     CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
     if (!e || !recovery) return Siamese_InvalidInput;
     API_CALL();
-    RecoveryOut out;
-    const Result r = e->enc->encode(out);
+    if (e->ahead_next < e->ahead.size()) {  // encoded ahead (CEncoder)
+        const CEncoder::Ahead& a = e->ahead[e->ahead_next++];
+        recovery->Data = e->pinned + a.off;
+        recovery->DataBytes = a.total;
+        return Siamese_Success;
+    }
+    static const uint32_t kAheadMax = getenv("TONK_AMD_CAPI_AHEAD") ? (uint32_t)atoi(getenv("TONK_AMD_CAPI_AHEAD")) : 15u;
+    if (!e->ahead.empty()) {  // all of them used
+        e->depth = 2 * e->depth < kAheadMax ? 2 * e->depth : kAheadMax;
+        e->ahead.clear();
+        e->marks.clear();
+        e->ahead_next = 0;
+    }
+    thread_local std::vector<RecoveryOut> outs;
+    outs.resize(1);
+    const Result r = e->enc->encode(outs[0]);
     if (r == kDisabled) report_disable("Encoder::encode");
     if (r != kSuccess) {
+        e->last_encode = false;
         if (r == kNeedMoreData) recovery->DataBytes = 0;
         return (SiameseResult)r;
     }
-    const uint32_t total = out.total();
-    bool ok = e->ensure_pinned(total);
-    // the program and the read of the recovery row behind it, waited for without a lock
+    if (kAheadMax && e->last_encode) {
+        for (uint32_t k = 0; k < e->depth && e->enc->encode_is_quiet(); ++k) {
+            const Encoder::Mark m = e->enc->mark();
+            RecoveryOut o;
+            if (e->enc->encode(o) != kSuccess) {
+                e->enc->rewind(m);
+                break;
+            }
+            e->marks.push_back(m);
+            outs.push_back(o);
+        }
+    }
+    e->last_encode = true;
+    size_t bytes = 0;
+    for (const RecoveryOut& o : outs) bytes += (o.total() + 63u) & ~(size_t)63;
+    bool ok = e->ensure_pinned(bytes);
+    // the program and the read of the recovery rows behind it, waited for without a lock
     if (ok) {
         thread_local std::vector<Device::HostCopy> rd;
-        rd.assign(1, Device::HostCopy{e->pinned, e->byte_offset(out.row), total});
+        rd.clear();
+        size_t at = 0;
+        for (size_t i = 0; i < outs.size(); ++i) {
+            rd.push_back(Device::HostCopy{e->pinned + at, e->byte_offset(outs[i].row), outs[i].total()});
+            if (i) e->ahead.push_back(CEncoder::Ahead{at, outs[i].total()});
+            at += (outs[i].total() + 63u) & ~(size_t)63;
+        }
         ok = run_and_read(*e, rd);
     }
-    e->ctx.rows.free_deferred(out.row);  // released once the codec's next program completes
+    for (const RecoveryOut& o : outs) e->ctx.rows.free_deferred(o.row);  // released once the codec's next program completes
     if (!ok) {
+        e->ahead.clear();
+        e->marks.clear();
         DISABLE(e->enc);
         return Siamese_Disabled;
     }
     recovery->Data = e->pinned;
-    recovery->DataBytes = total;
+    recovery->DataBytes = outs[0].total();
     return Siamese_Success;
 }
 
@@ -919,6 +985,7 @@ SIAMESE_EXPORT SiameseResult siamese_encoder_stats(SiameseEncoder encoder_t, uin
     CEncoder* e = reinterpret_cast<CEncoder*>(encoder_t);
     if (!e || !statsOut || statsCount <= 0) return Siamese_InvalidInput;
     API_CALL();
+    e->cancel_ahead();
     e->enc->stats(statsOut, statsCount);
     return Siamese_Success;
 }

@@ -995,6 +995,38 @@ void Encoder::light_pairs(uint32_t row, std::vector<uint64_t>& out) {
     }
 }
 
+// Short sum ranges (the usual case with acknowledgements: each Siamese row follows a sum reset)
+// are read straight from the packets; long ones through the running lane sums.
+bool Encoder::direct_sums() const {
+    static const uint32_t direct_max = getenv("TONK_AMD_DIRECT") ? (uint32_t)atoi(getenv("TONK_AMD_DIRECT"))
+                                                                  : kDirectMax;
+    static const int direct_mode = getenv("TONK_AMD_DIRECT_MODE") ? atoi(getenv("TONK_AMD_DIRECT_MODE")) : 0;
+    const uint32_t range = count_ + sum_erased_ - sum_start_;
+    const bool fresh = sum_end_ == sum_start_;
+    // Direct reads pay per run (a DENSE run's coefficient setup and first row loads); packets
+    // added one by one with host copies (the C ABI) are runs of one, where the lane sums' batched
+    // single-row reads are far cheaper: direct only while the range's runs average kDirectMinRun.
+    bool direct = range <= direct_max && (direct_mode == 0 || fresh || (direct_mode == 2 && range <= 128));
+    if (direct && range) direct = (segs_.size() - seg_index_at(sum_abs_start())) * kDirectMinRun <= range;
+    return direct;
+}
+
+// encode()'s branches without running them: the single packet and Cauchy / parity rows change
+// only row counters (and the sum end); a Siamese row also its sum end, unless its lane reads would
+// accumulate packets or snapshot a pending scan.
+bool Encoder::encode_is_quiet() const {
+    if (disabled_ || count_ <= 0 || first_unremoved_ >= kRemoveThreshold) return false;
+    const uint32_t un = unacked();
+    if (un == 1) return true;
+    const uint32_t ub = count_ - sum_start_ + sum_erased_;
+    if (sum_end_ <= sum_start_ || ub >= kMaxPackets) return un <= kCauchyThreshold;  // (else a sum reset)
+    if (un <= kSumResetThreshold || ub <= kCauchyThreshold) return true;
+    if (direct_sums()) return true;
+    for (unsigned l = 0; l < kLanes; ++l)
+        if ((int32_t)(base_ + count_ - lanes_[l].next_abs) > 0 || !lanes_[l].sums.idle()) return false;
+    return true;
+}
+
 // Encoder::Encode (SiameseEncoder.cpp:1146-1254)
 Result Encoder::encode(RecoveryOut& out) {
     out = RecoveryOut();
@@ -1020,18 +1052,7 @@ Result Encoder::encode(RecoveryOut& out) {
     const uint32_t recovery_bytes = longest_;
     Sym& rec = rec_;
     rec.clear();
-    // Short sum ranges (the usual case with acknowledgements: each Siamese row follows a sum
-    // reset) are read straight from the packets; long ones through the running lane sums.
-    static const uint32_t direct_max = getenv("TONK_AMD_DIRECT") ? (uint32_t)atoi(getenv("TONK_AMD_DIRECT"))
-                                                                  : kDirectMax;
-    static const int direct_mode = getenv("TONK_AMD_DIRECT_MODE") ? atoi(getenv("TONK_AMD_DIRECT_MODE")) : 0;
-    const uint32_t range = count_ + sum_erased_ - sum_start_;
-    const bool fresh = sum_end_ == sum_start_;
-    // Direct reads pay per run (a DENSE run's coefficient setup and first row loads); packets
-    // added one by one with host copies (the C ABI) are runs of one, where the lane sums' batched
-    // single-row reads are far cheaper: direct only while the range's runs average kDirectMinRun.
-    bool direct = range <= direct_max && (direct_mode == 0 || fresh || (direct_mode == 2 && range <= 128));
-    if (direct && range) direct = (segs_.size() - seg_index_at(sum_abs_start())) * kDirectMinRun <= range;
+    const bool direct = direct_sums();
     if (!direct) {
         TAMD_PROF_SCOPE(kEncDense);
         add_dense(row, recovery_bytes, rec);

@@ -111,6 +111,29 @@ public:
     // ctx->rows.free_deferred once nothing reads it).
     Result encode(RecoveryOut& out);
     void stats(uint64_t* out, unsigned n);
+    // Encode-ahead (the C ABI's encodes issued before the caller asks, capi.cpp): whether the
+    // next encode() would change no state but a Mark's fields -- no removal or sum reset due,
+    // and, for a Siamese row over the lane sums, nothing for them to accumulate or scan -- so that
+    // encodes run ahead of the caller are taken back exactly by rewind() when another call comes
+    // first.  (Rows those encodes allocated stay the caller's to free.)
+    struct Mark {
+        uint32_t next_row, next_parity_column, next_cauchy_row, sum_end;
+        uint64_t recoveries, recovery_bytes;
+        bool disabled;
+    };
+    bool encode_is_quiet() const;
+    Mark mark() const {
+        return Mark{next_row_, next_parity_column_, next_cauchy_row_, sum_end_, stats_[2], stats_[3], disabled_};
+    }
+    void rewind(const Mark& m) {
+        next_row_ = m.next_row;
+        next_parity_column_ = m.next_parity_column;
+        next_cauchy_row_ = m.next_cauchy_row;
+        sum_end_ = m.sum_end;
+        stats_[2] = m.recoveries;
+        stats_[3] = m.recovery_bytes;
+        disabled_ = m.disabled;
+    }
     // Millisecond clock of send times, RTO updates and retransmit decisions (GetTimeMsec in
     // SiameseEncoder.cpp:142, 595, 905).  Default: the monotonic clock; a batch driver may point
     // it at a per-step value or a virtual clock.
@@ -237,6 +260,7 @@ private:
 
     Result generate_single(RecoveryOut& out);
     Result generate_cauchy(RecoveryOut& out);
+    bool direct_sums() const;  // a Siamese row reads its sum range straight from the packets
     void add_dense(uint32_t row, uint32_t recovery_bytes, Sym& rec);
     void add_light(uint32_t row, Sym& rec);
     // The same pair columns as (absolute element << 8 | coefficient), sorted by element.

@@ -395,6 +395,8 @@ public:
     // expansion by every read) are first folded into three rows (dyn_fold_above()).
     void read(RowTable& rows, const ExpansionTable& ex, Sym& out, const uint8_t* c, uint32_t limit,
               ProgramBuilder* pb = nullptr);
+    // Nothing accumulated since the last flush: a read only names the carried rows.
+    bool idle() const { return terms_.empty() && dyn_.empty(); }
     // Emit the scan (and fix-up) ops for the pending program and rebase the sums.
     void flush(RowTable& rows, ProgramBuilder& pb, const ExpansionTable& ex);
     // Drop everything (codec destruction).
