@@ -528,6 +528,7 @@ void Decoder::remove_elements() {
     column_start_ = to_column(removed);
     next_expected_ -= removed;
 
+    ++list_gen_;
     for (Recovery* q = head_; q; q = q->next) {
         q->element_end -= removed;
         q->element_start -= removed;
@@ -545,13 +546,26 @@ void Decoder::list_insert(Recovery* rec, bool out_of_order) {
     Recovery* prev = tail_;
     Recovery* next = nullptr;
     const uint32_t rs = rec->meta.ColumnStart, re = rec->element_end;
-    for (; prev; next = prev, prev = prev->prev) {
-        const uint32_t ps = prev->meta.ColumnStart, pe = prev->element_end;
-        if (re >= pe) {
-            if (re > pe) break;
-            if (col_delta_negative(col_sub(rs, ps))) break;
+    if (ins_gen_ == list_gen_ && ins_end_ == re && ins_start_ == rs) {
+        // The walk from the tail passes every node it passed for the previous insertion, and that
+        // node too (an equal key continues the walk), and stops where that walk stopped: the
+        // packet goes right in front of it.  (The flush of a decoder far behind adds thousands of
+        // recovery packets with one key, each walk ~2,000 nodes long.)
+        next = ins_last_;
+        prev = ins_last_->prev;
+    } else {
+        for (; prev; next = prev, prev = prev->prev) {
+            const uint32_t ps = prev->meta.ColumnStart, pe = prev->element_end;
+            if (re >= pe) {
+                if (re > pe) break;
+                if (col_delta_negative(col_sub(rs, ps))) break;
+            }
         }
     }
+    ins_last_ = rec;
+    ins_end_ = re;
+    ins_start_ = rs;
+    ins_gen_ = ++list_gen_;
     rec->next = next;
     rec->prev = prev;
     if (prev) prev->next = rec; else head_ = rec;
@@ -566,6 +580,7 @@ void Decoder::list_insert(Recovery* rec, bool out_of_order) {
 
 // RecoveryPacketList::DeletePacketsBefore (:2637-2666)
 void Decoder::list_delete_before(uint32_t element) {
+    ++list_gen_;
     Recovery* r = head_;
     uint32_t deleted = 0;
     while (r) {
@@ -1028,14 +1043,25 @@ Result Decoder::decode(std::vector<RecoveredPacket*>& out) {
 
     Recovery* r = cr_.last;
     uint32_t next_check = cr_.next_check_start, rcount = cr_.recovery_count, lost = cr_.lost_count;
+    // The checked region (cr_) only moves after this loop, so every attempt after a failed one
+    // solves the same matrix again (GenerateMatrix reads CheckedRegion's counts, :2157-2165; the
+    // resumed elimination stops at the same pivot without changing anything) and fails the same
+    // way: those attempts are only counted (SolveFailCount), not repeated.  (A decoder far behind
+    // -- stream 56 of configs[2] -- walks ~2,000 recovery packets per call, each an attempt.)
+    bool failed = false;
     for (;;) {
         if (rcount >= lost) {
-            const Result res = decode_checked_region();
-            if (res == kSuccess) {
-                for (RecoveredPacket& p : recovered_) out.push_back(&p);
-                return kSuccess;
+            if (failed) {
+                stats_[8]++;
+            } else {
+                const Result res = decode_checked_region();
+                if (res == kSuccess) {
+                    for (RecoveredPacket& p : recovered_) out.push_back(&p);
+                    return kSuccess;
+                }
+                if (res != kNeedMoreData) return res;
+                failed = true;
             }
-            if (res != kNeedMoreData) return res;
         }
         if (!r->next) break;
         r = r->next;

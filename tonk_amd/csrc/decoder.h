@@ -122,6 +122,12 @@ private:
     // ---- RecoveryPacketList ----
     Recovery* head_ = nullptr;
     Recovery* tail_ = nullptr;
+    // list_insert's last insertion (node, its end and column start) and the list generation it
+    // left (list_gen_ counts every other change of the list or of its nodes' ends): a packet with
+    // the same key goes right in front of that node without the walk (list_insert).
+    Recovery* ins_last_ = nullptr;
+    uint32_t ins_end_ = 0, ins_start_ = 0;
+    uint64_t list_gen_ = 0, ins_gen_ = ~0ull;
     // Deleted packets stay readable until the checked region and matrix forget them: the
     // reference frees them into its pool allocator, where stale pointers still read the old
     // fields (RecoveryPacketList::DeletePacketsBefore, SiameseDecoder.cpp:2637-2666).
