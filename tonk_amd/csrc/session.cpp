@@ -976,8 +976,10 @@ struct Session {
         // (the other threads only run control planes, which touch no device state) instead of the
         // caller after the pass.  Record mode runs the same schedule (its digests are enqueued by
         // the launches themselves).
+        // A session without workers runs the same order: its one stream's previous program is
+        // filled and launched before this step's control plane, which then overlaps its levels.
         static const bool early_ok = getenv("TONK_AMD_LATE_LAUNCH") == nullptr;  // A/B switch
-        const bool early = fill && early_ok && !threads.empty();
+        const bool early = fill && early_ok;
         if (early) fills_left.store(streams.size(), std::memory_order_relaxed);
         run_all([this, originals, finish, rel, fill, early, &ms](size_t i, size_t ti) {
             const auto w0 = clk::now();
