@@ -426,6 +426,38 @@ LaneSums& Decoder::get_lane(uint32_t lane, uint32_t element_end) {
     return sum.sums;
 }
 
+// RemoveElements' walk over the recovery list (:1790-1830): the smallest element start, the
+// largest packet, the first sum row, and the first sum elements of the other sum rows that differ
+// from it (any of those outside the window disables the decoder).
+void Decoder::list_walk(ListWalk& w) const {
+    w.min_start = ~0u;
+    w.max_bytes = 0;
+    w.seen_sum = false;
+    w.target_start = w.target_count = 0;
+    w.min_fse = ~0u;
+    w.invalid = false;
+    for (const Recovery* r = head_; r; r = r->next) {
+        const uint32_t sc = r->meta.SumCount, cs = r->meta.ColumnStart;
+        if (sc > kCauchyThreshold) {
+            if (!w.seen_sum) {
+                w.target_start = cs;
+                w.target_count = sc;
+                w.target_end = r->element_end;
+                w.seen_sum = true;
+            } else if (cs != w.target_start || sc < w.target_count) {
+                const uint32_t fse = to_element(cs);
+                if (invalid_element(fse)) {
+                    w.invalid = true;
+                    return;
+                }
+                if (w.min_fse > fse) w.min_fse = fse;
+            }
+        }
+        if (w.min_start > r->element_start) w.min_start = r->element_start;
+        if (w.max_bytes < r->bytes) w.max_bytes = r->bytes;
+    }
+}
+
 // DecoderPacketWindow::RemoveElements (:1778-2033)
 void Decoder::remove_elements() {
     if (next_expected_ < kRemoveThreshold) return;
@@ -443,26 +475,21 @@ void Decoder::remove_elements() {
         initial_bytes = last_bytes_;
         if (m.SumCount > kCauchyThreshold) seen_sum = true;
     } else {
-        first_kept = r->element_start;
-        initial_bytes = r->bytes;
-        for (;;) {
-            const uint32_t sc = r->meta.SumCount, cs = r->meta.ColumnStart;
-            if (sc > kCauchyThreshold) {
-                if (!seen_sum) {
-                    target_start = cs;
-                    target_count = sc;
-                    seen_sum = true;
-                } else if (cs != target_start || sc < target_count) {
-                    const uint32_t fse = to_element(cs);
-                    if (invalid_element(fse)) { disabled_ = true; return; }
-                    if (first_kept > fse) first_kept = fse;
-                }
-            }
-            r = r->next;
-            if (!r) break;
-            if (first_kept > r->element_start) first_kept = r->element_start;
-            if (initial_bytes < r->bytes) initial_bytes = r->bytes;
+        // (the walk below, or what it found last time when neither the list nor the window moved:
+        // a decoder far behind holds thousands of recovery packets and calls this on every add)
+        if (!(walk_.valid && walk_.gen == list_gen_ && walk_.column_start == column_start_ && walk_.count == count_)) {
+            list_walk(walk_);
+            walk_.valid = true;
+            walk_.gen = list_gen_;
+            walk_.column_start = column_start_;
+            walk_.count = count_;
         }
+        if (walk_.invalid) { disabled_ = true; return; }
+        first_kept = walk_.min_start < walk_.min_fse ? walk_.min_start : walk_.min_fse;
+        initial_bytes = walk_.max_bytes;
+        seen_sum = walk_.seen_sum;
+        target_start = walk_.target_start;
+        target_count = walk_.target_count;
     }
     if (first_kept < kRemoveThreshold) return;
 
@@ -562,10 +589,36 @@ void Decoder::list_insert(Recovery* rec, bool out_of_order) {
             }
         }
     }
+    // remove_elements' walk over the list stays what it was, plus this packet, unless the packet
+    // can become the sum target in front of the current one: a sum row is the target when it is
+    // the first; one ending after the target's end goes behind it (the list is ordered by end)
+    // and counts its first sum element if it differs from the target; one with the target's start
+    // and count changes nothing wherever it goes.  Otherwise the next removal walks again.
+    const uint32_t sc = rec->meta.SumCount;
+    const bool is_sum = sc > kCauchyThreshold;
+    const bool same_target = is_sum && walk_.seen_sum && rs == walk_.target_start && sc == walk_.target_count;
+    const bool walk_kept = walk_.valid && walk_.gen == list_gen_ && walk_.column_start == column_start_ &&
+                           walk_.count == count_ &&
+                           (!is_sum || !walk_.seen_sum || same_target || re > walk_.target_end);
     ins_last_ = rec;
     ins_end_ = re;
     ins_start_ = rs;
     ins_gen_ = ++list_gen_;
+    if (walk_kept) {
+        if (is_sum && !walk_.seen_sum) {
+            walk_.seen_sum = true;
+            walk_.target_start = rs;
+            walk_.target_count = sc;
+            walk_.target_end = re;
+        } else if (is_sum && !same_target && (rs != walk_.target_start || sc < walk_.target_count)) {
+            const uint32_t fse = to_element(rs);
+            if (invalid_element(fse)) walk_.invalid = true;
+            else if (walk_.min_fse > fse) walk_.min_fse = fse;
+        }
+        if (walk_.min_start > rec->element_start) walk_.min_start = rec->element_start;
+        if (walk_.max_bytes < rec->bytes) walk_.max_bytes = rec->bytes;
+        walk_.gen = list_gen_;
+    }
     rec->next = next;
     rec->prev = prev;
     if (prev) prev->next = rec; else head_ = rec;

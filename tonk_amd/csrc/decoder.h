@@ -128,6 +128,20 @@ private:
     Recovery* ins_last_ = nullptr;
     uint32_t ins_end_ = 0, ins_start_ = 0;
     uint64_t list_gen_ = 0, ins_gen_ = ~0ull;
+    // What remove_elements' walk over the recovery list finds (RemoveElements, :1778-1830), kept
+    // for the list generation, window start and count it was taken at; list_insert carries it
+    // over an insertion that cannot change the walk's sum target or its participants.
+    struct ListWalk {
+        bool valid = false;
+        uint64_t gen = 0;
+        uint32_t column_start = 0, count = 0;
+        uint32_t min_start = 0, max_bytes = 0;      // every node's element start / bytes
+        bool seen_sum = false;                      // the first sum row (SumCount > Cauchy threshold)
+        uint32_t target_start = 0, target_count = 0, target_end = 0;  // (its element end)
+        uint32_t min_fse = ~0u;                     // other sum rows' first sum elements
+        bool invalid = false;                       // one of those is outside the window
+    } walk_;
+    void list_walk(ListWalk& w) const;
     // Deleted packets stay readable until the checked region and matrix forget them: the
     // reference frees them into its pool allocator, where stale pointers still read the old
     // fields (RecoveryPacketList::DeletePacketsBefore, SiameseDecoder.cpp:2637-2666).

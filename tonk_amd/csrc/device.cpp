@@ -270,6 +270,8 @@ bool Device::init(int device, uint64_t arena_bytes) {
         HIPCHK(hipMalloc((void**)&arena_, arena_bytes_));
     }
     HIPCHK(hipMemsetAsync(arena_, 0, arena_bytes_, s));
+    if (getenv("TONK_AMD_DEBUG_ALLOC"))  // (diagnostics: placement of the arena)
+        fprintf(stderr, "tonk_amd: arena %p, %llu bytes\n", (void*)arena_, (unsigned long long)arena_bytes_);
     if (!gf_init()) { error_ = "gf self test failed"; return false; }
     // kernels.hip TAMD_GF_DWORDS: perm tables, inv[256], sqr[256], then the lane table: for
     // i = 0..252 (column value cx = 3 + i) the perm dwords of cx and of cx^2, then the Cauchy table
