@@ -95,3 +95,36 @@ def test_control_plane_batch_streams(harness, golden_index, tmp_path, batch_name
     r = subprocess.run(args, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
     assert hashlib.sha256(out.read_bytes()).hexdigest() == entry["streams"][str(sid)]["sha256"]
+
+
+@pytest.mark.parametrize("family,streams", [("cfg2", range(48, 64)), ("cfg4", range(0, 3)), ("p5_ack32", range(0, 8))])
+def test_control_plane_vs_reference_build(harness, tmp_path, family, streams):
+    """Whole streams through the control plane against transcripts the reference codec compiled
+    from /root/reference (oracle/_ref/golden_gen, built by __graft_entry__.build) writes for the
+    same seeds: configs[2] streams 48-63 (stream 56 is the decoder far behind whose thousands of
+    failed solves Decoder::decode counts instead of repeating, with the list walks it caches), the
+    decoder-stress configs[4] and a 5 %-loss family, in the C ABI's per-call mode with
+    encode-ahead and in the batched session's mode."""
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle", "_ref", "golden_gen")
+    if not os.path.exists(exe):
+        pytest.skip("reference build absent (oracle/_ref)")
+    args = {
+        "cfg2": "n=4096 pmin=1300 pmax=1300 loss=85899345 ge=0 gb=0 bg=0 lossrec=1 fec=2621 ack=64 ackbytes=256 arq=0 flush=4096",
+        "cfg4": "n=65536 pmin=1300 pmax=1300 loss=0 ge=1 gb=56512727 bg=1073741824 lossrec=1 fec=6554 ack=256 ackbytes=256 arq=2048 flush=4096",
+        "p5_ack32": "n=4096 pmin=1300 pmax=1300 loss=214748364 ge=0 gb=0 bg=0 lossrec=1 fec=5243 ack=32 ackbytes=256 arq=0 flush=4096",
+    }[family].split()
+    first = min(streams)
+    ref = subprocess.run([exe, "transcripts", str(tmp_path / "r"), "threads=4", f"streams={max(streams) + 1 - first}",
+                          f"stream={first}"] + args, capture_output=True, text=True, timeout=600)
+    assert ref.returncode == 0, ref.stderr[-2000:]
+    modes = [["mode=sync", "dirty=1", "expand=16", "backsub=2", "ahead=15"],
+             ["mode=batch", "batch=4096", "pipeline=1", "drain=2", "split=48", "contig=1"]]
+    for s in streams:
+        want = (tmp_path / f"r{s}.txt").read_text()
+        for m in modes:
+            out = tmp_path / "o.txt"
+            r = subprocess.run([harness, str(out)] + m + args + [f"stream={s}", f"seed_data={1000 + s}",
+                                                                 f"seed_loss={2000 + s}"],
+                               capture_output=True, text=True, timeout=600)
+            assert r.returncode == 0, r.stderr[-2000:]
+            assert out.read_text() == want, f"stream {s} {m}: " + first_diff(want, out.read_text())

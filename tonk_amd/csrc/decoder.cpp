@@ -632,7 +632,15 @@ void Decoder::list_insert(Recovery* rec, bool out_of_order) {
 }
 
 // RecoveryPacketList::DeletePacketsBefore (:2637-2666)
+void Decoder::lazy_write() {
+    Recovery* r = lazy_from_;
+    for (uint32_t i = 0; i < lazy_n_ && r; ++i, r = r->next) r->lost_count = lazy_lost_;
+    lazy_n_ = 0;
+    lazy_from_ = nullptr;
+}
+
 void Decoder::list_delete_before(uint32_t element) {
+    if (lazy_n_) lazy_write();
     ++list_gen_;
     Recovery* r = head_;
     uint32_t deleted = 0;
@@ -656,6 +664,8 @@ void Decoder::list_delete_before(uint32_t element) {
 // CheckedRegionState::Reset (:2537-2548)
 void Decoder::checked_reset() {
     cr_ = Checked();
+    lazy_n_ = 0;  // (every loss count is written again before it is read)
+    lazy_from_ = nullptr;
     matrix_reset();
     for (Recovery* r : graveyard_) pool_.push_back(r);  // reused by add_recovery
     graveyard_.clear();
@@ -755,6 +765,7 @@ void Decoder::populate_rows(uint32_t old_rows, uint32_t new_rows) {
 
 // RecoveryMatrixState::GenerateMatrix (:2157-2383)
 bool Decoder::generate_matrix() {
+    if (lazy_n_) lazy_write();
     const uint32_t columns = cr_.lost_count;
     const uint32_t rows = cr_.recovery_count;
     uint32_t old_rows = (uint32_t)mrows_.size();
@@ -1117,6 +1128,19 @@ Result Decoder::decode(std::vector<RecoveredPacket*>& out) {
             }
         }
         if (!r->next) break;
+        if (failed && cr_.first == head_ && tail_->element_end <= next_check && !lazy_n_) {
+            // The rest of the walk after a failed solve, at once: the list is ordered by element
+            // end, so no later packet adds losses (its end is within next_check); each one counts
+            // a failed attempt and faces `lost` losses.  r is the rcount-th packet from the head.
+            const uint32_t rest = recovery_count_ - rcount;
+            stats_[8] += rest;
+            lazy_from_ = r->next;
+            lazy_n_ = rest;
+            lazy_lost_ = lost;
+            rcount += rest;
+            r = tail_;
+            break;
+        }
         r = r->next;
         ++rcount;
         uint32_t ee = r->element_end;

@@ -158,6 +158,12 @@ private:
         Recovery* last = nullptr;
         bool solve_failed = false;
     } cr_;
+    // Loss counts decode() has not written yet: `lazy_n_` packets from `lazy_from_` on all face
+    // `lazy_lost_` losses (decode's walk past a failed solve, Decoder::decode).  Written before
+    // anything reads them (generate_matrix) or the list drops packets; a reset forgets them.
+    Recovery* lazy_from_ = nullptr;
+    uint32_t lazy_n_ = 0, lazy_lost_ = 0;
+    void lazy_write();
 
     // ---- RecoveryMatrixState ----
     std::vector<MatRow> mrows_;
