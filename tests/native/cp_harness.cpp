@@ -39,6 +39,7 @@ static uint32_t g_split = 0;      // split=<packets>: the batched session's dens
 // are handed out by the next encode calls; any other encoder call first takes the rest back
 // (Encoder::rewind) and frees their rows.  The depth doubles from 1 while they are all used.
 static uint32_t g_ahead = 0;
+static bool g_short = false;  // short=1: Context::short_scans (the C ABI's lane-sum snapshot levels)
 static uint64_t g_rs[9];  // CP_READ_STATS totals
 static bool g_contig = false;  // contig=1: originals in rows reserved up front, in order, one range per
                                // side and borrowed by the codecs (the batched session's layout)
@@ -191,6 +192,7 @@ struct Harness {
         ctx.ex.expand_limit = g_expand;
         ctx.backsub_rows = g_backsub;
         ctx.dense_split = g_split;
+        ctx.short_scans = g_short;
         arena.assign(g_arena_bytes, 0);
         enc = new Encoder(&ctx, row_bytes);
         dec = new Decoder(&ctx, row_bytes);
@@ -632,6 +634,7 @@ int main(int argc, char** argv) {
         else if (k == "split") g_split = (uint32_t)v;
         else if (k == "contig") g_contig = v != 0;
         else if (k == "ahead") g_ahead = (uint32_t)v;
+        else if (k == "short") g_short = v != 0;
         else if (parse_param(p, k, v)) {}
         else { fprintf(stderr, "bad key %s\n", k.c_str()); return 2; }
     }

@@ -67,9 +67,11 @@ def test_control_plane_matches_reference(harness, golden_index, tmp_path, name, 
     # "sync-exp" and "batch-dirty" also encode ahead as the C ABI does (Encoder::encode_is_quiet,
     # rewind): up to 15 and 3 recovery packets
     ahead = 15 if mode == "sync-exp" else 3 if mode == "batch-dirty" else 0
+    # ... and "sync-exp" takes the C ABI's lane-sum snapshot levels (Context::short_scans)
+    short = int(mode == "sync-exp")
     args = [harness, str(out), f"mode={base}", f"batch={batch}", f"dirty={dirty}", f"pipeline={pipe}",
             f"drain={drain}", f"expand={expand}", f"backsub={backsub}", f"split={split}", f"contig={contig}",
-            f"ahead={ahead}"] + sc["args"] + [
+            f"ahead={ahead}", f"short={short}"] + sc["args"] + [
         f"seed_data={1000 + sid}", f"seed_loss={2000 + sid}"]
     r = subprocess.run(args, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
@@ -117,7 +119,7 @@ def test_control_plane_vs_reference_build(harness, tmp_path, family, streams):
     ref = subprocess.run([exe, "transcripts", str(tmp_path / "r"), "threads=4", f"streams={max(streams) + 1 - first}",
                           f"stream={first}"] + args, capture_output=True, text=True, timeout=600)
     assert ref.returncode == 0, ref.stderr[-2000:]
-    modes = [["mode=sync", "dirty=1", "expand=16", "backsub=2", "ahead=15"],
+    modes = [["mode=sync", "dirty=1", "expand=16", "backsub=2", "ahead=15", "short=1"],
              ["mode=batch", "batch=4096", "pipeline=1", "drain=2", "split=48", "contig=1"]]
     for s in streams:
         want = (tmp_path / f"r{s}.txt").read_text()

@@ -374,6 +374,8 @@ struct Codec {
         static const uint32_t ex = getenv("TONK_AMD_CAPI_EXPAND") ? (uint32_t)atoi(getenv("TONK_AMD_CAPI_EXPAND")) : 16u;
         ctx.backsub_rows = bs ? bs : ~0u;  // (0: never materialize / always inline)
         ctx.ex.expand_limit = ex ? ex : ~0u;
+        static const bool short_scans = !getenv("TONK_AMD_CAPI_SHORT_SCANS") || atoi(getenv("TONK_AMD_CAPI_SHORT_SCANS")) != 0;
+        ctx.short_scans = short_scans;  // (A/B: 0 restores the chain level)
         static std::atomic<unsigned> next{0};
         staging.stream = next.fetch_add(1) % g_rt->dev.stream_count();
     }

@@ -1251,7 +1251,7 @@ bool Decoder::eliminate_original_data() {
                 if (!n) continue;
                 uint8_t k[3];
                 opcode_coefs(op, rx, k);  // sums and RX * product sums in one read
-                c.read(ctx_->rows, ctx_->ex, buf, k, n, &ctx_->pb);
+                c.read(ctx_->rows, ctx_->ex, buf, k, n, &ctx_->pb, ctx_->short_scans);
             }
             }
             TAMD_PROF_SCOPE(kElimPairs);

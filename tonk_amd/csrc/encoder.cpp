@@ -789,7 +789,7 @@ void Encoder::add_dense(uint32_t row, uint32_t recovery_bytes, Sym& rec) {
         if (!n) continue;
         uint8_t k[3];
         opcode_coefs(op, rx, k);
-        c.read(ctx_->rows, ctx_->ex, rec, k, n);
+        c.read(ctx_->rows, ctx_->ex, rec, k, n, nullptr, ctx_->short_scans);
     }
     sum_end_ = count_;
 }

@@ -664,7 +664,7 @@ void LaneSums::drop_fold(RowTable& rows) {
 }
 
 void LaneSums::read(RowTable& rows, const ExpansionTable& ex, Sym& out, const uint8_t* c, uint32_t limit,
-                    ProgramBuilder* pb) {
+                    ProgramBuilder* pb, bool short_scan) {
     if (!limit || (!c[0] && !c[1] && !c[2])) return;
     TAMD_PROF_SCOPE(kLaneRead);
     const uint32_t clip = content_ < limit ? content_ : limit;
@@ -676,8 +676,10 @@ void LaneSums::read(RowTable& rows, const ExpansionTable& ex, Sym& out, const ui
         if (snap == kNoRow) {
             snap = rows.alloc(content_);
             if (snap == kNoRow) return;  // caller checks arena exhaustion via RowTable
-            rows.set_level(snap, snap_level(rows, base_));  // written by the scan's chain (or only) op
-            snaps_.push_back(Snap{snap, at, {c[0], c[1], c[2]}});
+            // written by the scan's chain (or only) op
+            const uint32_t level = short_scan && at <= chunk() ? snap_level(rows, base_, 1) : snap_level(rows, base_);
+            rows.set_level(snap, level);
+            snaps_.push_back(Snap{snap, at, {c[0], c[1], c[2]}, (uint8_t)level});
         }
         if (clip) out.push_back(Term{snap, clip, 1});
     } else if (clip) {
@@ -763,7 +765,12 @@ void LaneSums::emit_scan(RowTable& rows, ProgramBuilder& pb, const RowId* base, 
         }
     };
     const uint32_t kChunk = chunk();
-    if (n <= kChunk) {
+    // (a snapshot promised a lower level than the chain's -- LaneSums::read -- keeps the scan one op)
+    const uint32_t chain_level = snap_level(rows, base);
+    uint32_t level = chain_level;
+    for (const Snap& sn : snaps)
+        if (sn.level < level) level = sn.level;
+    if (n <= kChunk || level < chain_level) {
         pb.begin_op();
         for (unsigned s = 0; s < 3; ++s)
             if (base[s] != kNoRow) pb.op_acc(base[s], 1, rows.cap_bytes(base[s]), s);
@@ -779,7 +786,7 @@ void LaneSums::emit_scan(RowTable& rows, ProgramBuilder& pb, const RowId* base, 
         if (final_rows)
             for (unsigned s = 0; s < 3; ++s)
                 if (final_rows[s] != kNoRow) pb.op_storec(final_rows[s], rows.cap_bytes(final_rows[s]), unit[s]);
-        pb.end_op(snap_level(rows, base));
+        pb.end_op(level);
         return;
     }
 

@@ -393,8 +393,11 @@ public:
     // Append c[0]*sum_0 + c[1]*sum_1 + c[2]*sum_2 (current values, clipped to `limit` bytes).
     // With `pb`, packets produced in this program that have piled up (dyn_, each read as its
     // expansion by every read) are first folded into three rows (dyn_fold_above()).
+    // With `short_scan` (Context::short_scans), a snapshot taken while the scan is still one
+    // op's length is promised the scan op's own level (1 over level-0 bases) instead of the chain
+    // level, and the scan is then emitted as that one op.
     void read(RowTable& rows, const ExpansionTable& ex, Sym& out, const uint8_t* c, uint32_t limit,
-              ProgramBuilder* pb = nullptr);
+              ProgramBuilder* pb = nullptr, bool short_scan = false);
     // Nothing accumulated since the last flush: a read only names the carried rows.
     bool idle() const { return terms_.empty() && dyn_.empty(); }
     // Emit the scan (and fix-up) ops for the pending program and rebase the sums.
@@ -416,15 +419,14 @@ public:
     static const uint32_t kSnapLevel = 2;
     // Level of a scan's snapshot rows over carried values `base` (kSnapLevel, or above the
     // bases when they are still being written: rows of this program or inherited ones).
-    static uint32_t snap_level(const RowTable& rows, const RowId* base) {
-        uint32_t l = kSnapLevel;
+    static uint32_t snap_level(const RowTable& rows, const RowId* base, uint32_t l = kSnapLevel) {
         for (unsigned s = 0; s < 3; ++s)
             if (base[s] != kNoRow && rows.level(base[s]) + 1 > l) l = rows.level(base[s]) + 1;
         return l;
     }
 
 private:
-    struct Snap { RowId row; uint32_t after; uint8_t c[3]; };  // after = packets accumulated
+    struct Snap { RowId row; uint32_t after; uint8_t c[3]; uint8_t level; };  // after = packets accumulated
     uint32_t n_ = 0;                            // packets in terms_
     RowId base_[3] = {kNoRow, kNoRow, kNoRow};  // carried values from a previous flush (level 0)
     uint32_t content_ = 0;                      // bytes the accumulated content may occupy
@@ -518,6 +520,10 @@ struct Context {
     // launch's tail, while per-call programs (the C ABI) and single streams pay an extra level
     // launch in latency and already share a long op across a workgroup.
     uint32_t dense_split = 0;
+    // Lane-sum snapshots read while a scan is one op long take that op's level (LaneSums::read):
+    // per-call programs (the C ABI) flush right after their reads, so their scans stay short and
+    // a Siamese recovery row lands one level earlier.
+    bool short_scans = false;
     // Level pipelining (the session, Device::set_pipelined): every launch runs level 1 of the
     // newest program beside the next level of each older program still in flight, so level d
     // of a program runs with level 1 of the program d - 1 later.  A row written at level d is
