@@ -622,7 +622,7 @@ static inline bool same_coefs(const uint8_t* a, const uint8_t* b) {
 }
 
 uint32_t LaneSums::dyn_fold_above() {
-    static const uint32_t v = getenv("TONK_AMD_DYN_FOLD") ? (uint32_t)atoi(getenv("TONK_AMD_DYN_FOLD")) : 4u;
+    static const uint32_t v = getenv("TONK_AMD_DYN_FOLD") ? (uint32_t)atoi(getenv("TONK_AMD_DYN_FOLD")) : 2u;
     return v;
 }
 
