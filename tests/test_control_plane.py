@@ -67,8 +67,9 @@ def test_control_plane_matches_reference(harness, golden_index, tmp_path, name, 
     # "sync-exp" and "batch-dirty" also encode ahead as the C ABI does (Encoder::encode_is_quiet,
     # rewind): up to 15 and 3 recovery packets
     ahead = 15 if mode == "sync-exp" else 3 if mode == "batch-dirty" else 0
-    # ... and "sync-exp" takes the C ABI's lane-sum snapshot levels (Context::short_scans)
-    short = int(mode == "sync-exp")
+    # ... and "sync-exp" / "batch-pipeexp" take the C ABI's and the few-stream session's lane-sum
+    # snapshot levels (Context::short_scans)
+    short = int(mode in ("sync-exp", "batch-pipeexp"))
     args = [harness, str(out), f"mode={base}", f"batch={batch}", f"dirty={dirty}", f"pipeline={pipe}",
             f"drain={drain}", f"expand={expand}", f"backsub={backsub}", f"split={split}", f"contig={contig}",
             f"ahead={ahead}", f"short={short}"] + sc["args"] + [

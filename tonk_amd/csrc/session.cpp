@@ -1254,6 +1254,13 @@ void* tamd_session_create(const tamd_session_params* p, char* err, size_t err_le
         // (TONK_AMD_DENSE_SPLIT=<packets> overrides: A/B knob)
         static const char* split_env = getenv("TONK_AMD_DENSE_SPLIT");
         ctx->dense_split = split_env ? (uint32_t)atoi(split_env) : (p->n_streams <= 4 ? 0u : Encoder::kDenseSplit);
+        // Few-stream sessions also take the C ABI's lane scan levels (Context::short_scans): a
+        // snapshot read while its scan is one op long is promised level 1, which takes a level off
+        // configs[1]'s program (4 -> 3 launches, 17.4 -> 19.3 GiB/s; configs[4] 5.9 -> 6.2).
+        // Batched sessions keep the chain level: a promised snapshot makes its whole scan one op,
+        // a long item in a full-width launch.  TONK_AMD_SHORT_SCANS=0|1 overrides (A/B knob).
+        static const char* short_env = getenv("TONK_AMD_SHORT_SCANS");
+        ctx->short_scans = short_env ? atoi(short_env) != 0 : p->n_streams <= 4;
         std::unique_ptr<Stream> st(new Stream());
         st->ctx = ctx.get();
         wl::Params& q = st->p;
