@@ -1,5 +1,7 @@
 // engine.cpp -- see engine.h.
 #include "engine.h"
+
+#include <stdio.h>
 #include "prof.h"
 
 #include <stdlib.h>
@@ -419,9 +421,25 @@ uint32_t ProgramBuilder::end_op(uint32_t min_level) {
     ops_.push_back(op);
     // Cost class from the op's length in the executor's terms: instructions, and row loads
     // (an ACCR run is `count` rows); class 0 is the most expensive and starts first.
+    // (TONK_AMD_CLASS="rows_div,t1,t2,t3,rows0": A/B knob for the thresholds, default 2,64,32,12,48)
+    struct ClassCfg {
+        uint64_t div = 2, t1 = 64, t2 = 32, t3 = 12, r0 = 48;
+        ClassCfg() {
+            if (const char* e = getenv("TONK_AMD_CLASS")) {
+                unsigned long long v[5] = {div, t1, t2, t3, r0};
+                sscanf(e, "%llu,%llu,%llu,%llu,%llu", &v[0], &v[1], &v[2], &v[3], &v[4]);
+                div = v[0] ? v[0] : 2;
+                t1 = v[1];
+                t2 = v[2];
+                t3 = v[3];
+                r0 = v[4];
+            }
+        }
+    };
+    static const ClassCfg cc;
     const uint64_t rows = (acc_bytes_ - cur_acc_begin_) / 1024u;
-    const uint64_t cost = op.count + 4u * cur_runs_ + rows / 2u;
-    const uint32_t cls = (cur_pure_ && rows >= 48) ? 0u : cost >= 64 ? 1u : cost >= 32 ? 2u : cost >= 12 ? 3u : 4u;
+    const uint64_t cost = op.count + 4u * cur_runs_ + rows / cc.div;
+    const uint32_t cls = (cur_pure_ && rows >= cc.r0) ? 0u : cost >= cc.t1 ? 1u : cost >= cc.t2 ? 2u : cost >= cc.t3 ? 3u : 4u;
     const uint32_t bucket = TAMD_COST_CLASSES * level + cls;
     levels_.push_back(bucket);
     pure_.push_back(cur_pure_ ? (cur_multi_ ? 2 : 1) : 0);
