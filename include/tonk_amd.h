@@ -43,6 +43,9 @@ typedef struct tamd_session_params {
                                   i reads row i mod input_pool (the bench's long streams: the codecs'
                                   work does not depend on the payload bytes, as the reference
                                   timing leg's payload pool).  Ignored with record or stage_host. */
+    uint32_t hold_full;        /* 1: window-full behaviour of the workload (workload.h hold_full): the
+                                  sender asks siamese_encoder_is_ready before every add and a refused
+                                  add waits for an acknowledgement; single adds only */
 } tamd_session_params;
 
 /* Summary counters (tamd_session_summary indices). */

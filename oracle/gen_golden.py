@@ -57,7 +57,29 @@ def scenarios():
     # and the next RTT scan starts on placeholder elements (their send timestamps persist)
     s["rtx_restart_p1_ack4"] = (WorkloadParams(n=3000, loss=0.01, ack=4, rtx=2, rtx_msec=5), 0, True)
     s["rtx_restart_p2_ack2"] = (WorkloadParams(n=3000, loss=0.02, ack=2, rtx=1, rtx_msec=7), 0, True)
+    # the 16,000-packet window (siamese.h:163): no acknowledgements, the sender asks
+    # siamese_encoder_is_ready before every add and acks are forced by a refused add (workload.h
+    # hold_full; SiameseEncoder.cpp:91-96, siamese.cpp:80-93)
+    s["full_p1_noack"] = (WorkloadParams(n=50000, loss=0.01, ack=0, full=1), 0, True)
+    s["full_p3_noack"] = (WorkloadParams(n=50000, loss=0.03, ack=0, full=1), 0, True)
     return s
+
+
+def long_streams():
+    """name -> (WorkloadParams, stream id): streams past the 22-bit packet-number period
+    (SiameseCommon.h:102 kColumnPeriod = 0x400000): 4.3 M originals, so windows, Siamese sums,
+    Cauchy rows and LDPC pairs straddle column 0x3FFFFF -> 0.  With acks every 256 at 1 % loss a
+    window held open by an unrecovered loss straddles the wrap and the reference decoder disables
+    itself (every later call returns Siamese_Disabled; the encoder's window then fills up): the
+    engine must do exactly the same.  With no acks but the window-full behaviour (hold_full) the
+    16,000-packet window fills ~360 times, windows straddle the wrap and the decoder recovers
+    across it.  Digests only (the transcripts are 5-20 MB); 64-byte payloads for the CPU
+    control-plane tests, 1300-byte ones (the bench's) for the GPU."""
+    out = {}
+    for size in (64, 1300):
+        out[f"wrap_p1_ack256_{size}B"] = (WorkloadParams(n=4300000, payload=size, loss=0.01, ack=256), 0)
+        out[f"wrap_p1_full_{size}B"] = (WorkloadParams(n=4300000, payload=size, loss=0.01, ack=0, full=1), 0)
+    return out
 
 
 def batches():
@@ -117,6 +139,12 @@ def main() -> int:
                                           "summary": text.strip().splitlines()[-1]}
         index["batches"][name] = entry
         print(f"{name}: {count} streams from {base}")
+    index["long"] = {}
+    for name, (wp, sid) in long_streams().items():
+        text = run(wp, sid)
+        index["long"][name] = {"args": wp.args(), "stream": sid, "sha256": hashlib.sha256(text.encode()).hexdigest(),
+                               "lines": text.count("\n"), "summary": text.strip().splitlines()[-1]}
+        print(f"{name}: {index['long'][name]['lines']} lines")
     with open(os.path.join(OUT, "scenarios.json"), "w") as f:
         json.dump(index, f, indent=1, sort_keys=True)
     return 0

@@ -79,6 +79,7 @@ struct RefBackend {
     std::vector<uint32_t> lens;
     uint32_t stride = 0;
     uint64_t bad_recoveries = 0;
+    uint32_t top = 0;  // originals added (recovered packet numbers are 22-bit columns)
 
     // `pool` > 0 (timing only): payloads of the first `pool` indices, reused cyclically (original
     // i carries the bytes of i mod pool), so a long stream does not need its whole payload set in
@@ -120,8 +121,10 @@ struct RefBackend {
         ProfScope ps(P_ADD);
         const int rc = siamese_encoder_add(enc, &o);
         *col = o.PacketNum;
+        if (rc == 0) top = index + 1;
         return rc;
     }
+    int enc_is_ready() { return siamese_encoder_is_ready(enc); }
     int enc_encode(RecRef& r) {
         SiameseRecoveryPacket rp;
         rp.Data = nullptr;
@@ -168,7 +171,7 @@ struct RefBackend {
             for (unsigned k = 0; k < count; ++k) {
                 nums.push_back(pk[k].PacketNum);
                 out.data.emplace_back(pk[k].Data, pk[k].Data + pk[k].DataBytes);
-                const uint32_t idx = pk[k].PacketNum;
+                const uint32_t idx = index_of_column(pk[k].PacketNum, top);
                 if (idx >= p.n_originals || len_of(idx) != pk[k].DataBytes ||
                     memcmp(pay(idx), pk[k].Data, pk[k].DataBytes) != 0)
                     ++bad_recoveries;

@@ -74,6 +74,7 @@ struct Null {
     }
     int enc_encode(RecRef& r) { TAMD_PROF_SCOPE(kEncEncode); if (g_stub) return 2; return enc->encode(r.out); }
     int enc_ack(const uint8_t* b, uint32_t n, uint32_t* next) { TAMD_PROF_SCOPE(kEncAck); return enc->acknowledge(b, n, next); }
+    int enc_is_ready() { return enc->remaining_slots() <= 2 ? (int)kMaxPacketsReached : 0; }
     int dec_add_original(uint32_t col, uint32_t index, uint32_t len) {
         const uint32_t hb = length_header_bytes(len);
         TAMD_PROF_SCOPE(kDecAddOrig);

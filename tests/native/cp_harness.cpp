@@ -501,6 +501,7 @@ struct Harness {
         cancel_ahead();
         return E()->acknowledge(buf, n, next);
     }
+    int enc_is_ready() { return E()->remaining_slots() <= 2 ? (int)kMaxPacketsReached : 0; }
     int dec_add_original(uint32_t col, uint32_t index, uint32_t len) {
         uint32_t framed = 0, header = 0;
         const RowId r = write_original(index, len, &framed, &header, 1);

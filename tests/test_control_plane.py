@@ -131,3 +131,34 @@ def test_control_plane_vs_reference_build(harness, tmp_path, family, streams):
                                capture_output=True, text=True, timeout=600)
             assert r.returncode == 0, r.stderr[-2000:]
             assert out.read_text() == want, f"stream {s} {m}: " + first_diff(want, out.read_text())
+
+
+@pytest.mark.parametrize("name,mode", [
+    ("wrap_p1_ack256_64B", ["mode=sync", "dirty=1", "expand=16", "backsub=2", "ahead=15", "short=1"]),
+    ("wrap_p1_ack256_64B", ["mode=batch", "batch=4096", "pipeline=1", "drain=2", "split=48", "contig=1"]),
+    ("wrap_p1_full_64B", ["mode=sync", "dirty=1", "expand=16", "backsub=2", "ahead=15", "short=1"]),
+    ("full_p3_noack", ["mode=sync", "dirty=1", "expand=16", "backsub=2", "ahead=15", "short=1"]),
+    ("full_p1_noack", ["mode=sync", "dirty=0", "expand=4294967295", "backsub=4294967295"]),
+    ("full_p1_noack", ["mode=batch", "batch=4096", "pipeline=1", "drain=2", "split=48", "contig=1"]),
+    ("full_p1_noack", ["mode=batch", "batch=1000", "dirty=1", "ahead=3"])])
+def test_control_plane_long_streams(harness, golden_index, tmp_path, name, mode):
+    """The window-full fixtures (full_*: no acks, 50,000 originals, the 16,000-packet window fills
+    and a refused add waits for an acknowledgement, siamese.cpp:80-93, SiameseEncoder.cpp:91-96)
+    and 4.3 M originals, past the 22-bit packet-number period (SiameseCommon.h:102): windows,
+    Siamese sums, Cauchy rows and LDPC pairs straddle column 0x3FFFFF -> 0, in the C ABI's
+    per-call mode and the batched session's pipelined contiguous mode.  wrap_p1_ack256: the
+    reference decoder disables itself after the wrap and the encoder window fills up (the
+    engine must do the same); wrap_p1_full: no acks, the 16,000-packet window fills ~360 times
+    and recoveries continue across the wrap.  Transcript digest == the reference codec's.
+    (The batched mode of wrap_p1_full takes ~4 minutes on one core: run by hand, not here.)"""
+    import hashlib
+    e = golden_index["long"].get(name) or golden_index["scenarios"][name]
+    sid = e["stream"]
+    out = tmp_path / "t.txt"
+    r = subprocess.run([harness, str(out)] + mode + ["arena_mb=4096"] + e["args"] +
+                       [f"seed_data={1000 + sid}", f"seed_loss={2000 + sid}"],
+                       capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-2000:]
+    text = out.read_text()
+    assert text.splitlines()[-1] == e["summary"]
+    assert hashlib.sha256(text.encode()).hexdigest() == e["sha256"]

@@ -12,6 +12,7 @@ stats -- is compared with the golden transcript produced by the REFERENCE codec
 from __future__ import annotations
 
 import os
+import re
 import subprocess
 
 import pytest
@@ -24,11 +25,12 @@ SCEN_CAPI = ["c1_256_p3", "c2_4096_p1_ack64", "c2_4096_p1_noack", "c3_4096_p2_ac
              "var_1_1500_p2_ack32", "tiny_1_20_p5_ack16", "big_9000_p3_ack64", "hiloss_p20_arq",
              "norecloss_p5_arq", "single_p0", "burst8_p5", "c5_65536_ge5_b4",
              "rtx_p2_ack64", "rtx_p5_ack32", "rtx_p3_noack",
-             "rtx_restart_p1_ack4", "rtx_restart_p2_ack2"]
+             "rtx_restart_p1_ack4", "rtx_restart_p2_ack2", "full_p1_noack", "full_p3_noack"]
 SCEN_SESSION = ["c1_256_p3", "c2_4096_p1_ack64", "c2_4096_p1_noack", "c3_4096_p2_ack64_s1",
                 "c3_4096_p2_ack64_s63", "c4_4096_p1_ack64_s511", "var_1_1500_p2_ack32",
                 "tiny_1_20_p5_ack16", "big_9000_p3_ack64", "hiloss_p20_arq", "single_p0",
-                "burst8_p5", "c5_65536_ge5_b4", "rtx_p2_ack64", "rtx_p3_noack", "rtx_restart_p1_ack4"]
+                "burst8_p5", "c5_65536_ge5_b4", "rtx_p2_ack64", "rtx_p3_noack", "rtx_restart_p1_ack4",
+                "full_p1_noack", "full_p3_noack"]
 
 
 def _args(golden_index, name):
@@ -54,16 +56,16 @@ def test_capi_matches_reference(golden_index, name):
     assert got == want, first_diff(want, got)
 
 
-def _session_transcript(golden_index, name, threads=1, stage_host=False):
+def _session_transcript(golden_index, name, threads=1, stage_host=False, step=1000):
     import tonk_amd
-    sc = golden_index["scenarios"][name]
+    sc = golden_index["scenarios"].get(name) or golden_index["long"][name]
     wp = tonk_amd.WorkloadParams.from_args(sc["args"])
+    arena = max(1 << 30, 2 * wp.n * (wp.pmax + 64) + (2 << 30))
     s = tonk_amd.Session(wp, n_streams=1, stream_base=sc["stream"], threads=threads,
-                         arena_bytes=1 << 30, record=True, stage_host=stage_host)
+                         arena_bytes=arena, record=True, stage_host=stage_host)
     try:
         s.generate()
         n = wp.n
-        step = 1000
         done = 0
         while done < n:
             s.step(min(step, n - done))
@@ -233,3 +235,97 @@ def test_capi_arena_grows_past_many_chunks(golden_index, tmp_path):
     bad = [s for s in range(32)
            if hashlib.sha256(open(f"{prefix}{s}.txt", "rb").read()).hexdigest() != entry["streams"][str(s)]["sha256"]]
     assert not bad, f"streams differing from the reference: {bad}"
+
+
+def _capi_transcript(golden_index, name, env_extra, timeout=600):
+    exe = os.path.join(NATIVE, "_build", "capi_gen")
+    args, _ = _args(golden_index, name)
+    env = dict(os.environ, **env_extra)
+    out = subprocess.run([exe, "transcript", "/dev/stdout"] + args, capture_output=True, timeout=timeout, env=env)
+    assert out.returncode == 0, out.stderr.decode()[-2000:]
+    return out.stdout.decode(), out.stderr.decode()
+
+
+@pytest.mark.parametrize("name", ["c2_4096_p1_ack64", "hiloss_p20_arq", "rtx_restart_p1_ack4", "c5_65536_ge5_b4"])
+def test_capi_launch_path_matches_reference(golden_index, name):
+    """The C ABI with the persistent executor off (TONK_AMD_SERVE=0): every call takes the kernel
+    launch path that commands over 64 KB take with it on, and the transcript is the reference's."""
+    got, _ = _capi_transcript(golden_index, name, {"TONK_AMD_SERVE": "0"})
+    want = golden_text(name)
+    assert got == want, first_diff(want, got)
+
+
+@pytest.mark.parametrize("name", ["c2_4096_p1_noack", "norecloss_p5_arq", "rtx_p2_ack64"])
+def test_capi_no_encode_ahead_matches_reference(golden_index, name):
+    """Encode-ahead off (TONK_AMD_CAPI_AHEAD=0): one device round trip per siamese_encode."""
+    got, _ = _capi_transcript(golden_index, name, {"TONK_AMD_CAPI_AHEAD": "0"})
+    want = golden_text(name)
+    assert got == want, first_diff(want, got)
+
+
+def test_capi_executor_idle_exit_and_relaunch(golden_index):
+    """The persistent executor ends after 0.02 ms without a command (TONK_AMD_SERVE_IDLE_MS), so
+    it ends and is relaunched between the driver's calls over and over: the transcript is still
+    the reference's, and the watchdog shows more than one launch."""
+    name = "c3_4096_p2_ack64_s0"
+    got, err = _capi_transcript(golden_index, name, {"TONK_AMD_SERVE_IDLE_MS": "0.02", "TONK_AMD_CAPI_WATCH": "0.1"})
+    want = golden_text(name)
+    assert got == want, first_diff(want, got)
+    launches = [int(ln.split("launches=")[1].split()[0]) for ln in err.splitlines() if "server: posted=" in ln]
+    assert launches and max(launches) > 1, err[-2000:]
+
+
+def test_capi_dead_server_falls_back_and_never_reuses(golden_index, tmp_path):
+    """A command that times out (TONK_AMD_SERVE_TIMEOUT_US=1: the first wait does) kills the
+    persistent executor for the process: its codec is disabled and keeps its buffers and rows
+    (the command may still run), every later call takes the launch path.  Sixteen codec pairs on
+    eight threads, created and freed around the dead server: no wrong byte anywhere (the driver
+    memcmp-checks every recovered packet, exit 5), and every stream whose codecs were not the
+    ones caught in flight still matches the reference."""
+    import hashlib
+    exe = os.path.join(NATIVE, "_build", "capi_gen")
+    entry = golden_index["batches"]["cfg2_64x4096_p2_ack64"]
+    prefix = str(tmp_path / "s")
+    env = dict(os.environ, TONK_AMD_SERVE_TIMEOUT_US="1")
+    out = subprocess.run([exe, "transcripts", prefix, "threads=8", "streams=16", "stream=0"] + entry["args"],
+                         capture_output=True, timeout=600, env=env)
+    err = out.stderr.decode()
+    assert out.returncode == 0, err[-2000:]
+    assert "persistent executor is off" in err, err[-2000:]
+    good = 0
+    for s in range(16):
+        text = open(f"{prefix}{s}.txt", "rb").read()
+        if hashlib.sha256(text).hexdigest() == entry["streams"][str(s)]["sha256"]:
+            good += 1
+        else:  # a stream caught with a command in flight: disabled, never wrong bytes
+            assert re.search(rb"^[A-Z] 5\b", text, re.M), text[-400:]
+    assert good >= 8, f"only {good} of 16 streams match the reference after the server died"
+
+
+@pytest.mark.parametrize("name", ["wrap_p1_ack256_1300B", "wrap_p1_full_1300B"])
+def test_session_past_column_wrap(golden_index, name):
+    """4.3 M originals of 1300 bytes, past the 22-bit packet-number period (SiameseCommon.h:102):
+    windows, Siamese sums, Cauchy rows and LDPC pairs straddle column 0x3FFFFF -> 0 on the
+    device.  wrap_p1_ack256: the reference decoder disables itself after the wrap; wrap_p1_full:
+    no acks, the window fills ~360 times and recoveries continue across the wrap.  Every
+    recovery packet and recovered payload (digested on the device), ack and statistic: the
+    transcript's digest equals the reference codec's."""
+    e = golden_index["long"][name]
+    got, summ = _session_transcript(golden_index, name, step=4096)
+    assert sha256(got + e["summary"] + "\n") == e["sha256"], got.splitlines()[-1]
+    assert summ["disabled_codecs"] == (1 if "ack256" in name else 0)
+
+
+@pytest.mark.parametrize("name", ["wrap_p1_ack256_1300B", "wrap_p1_full_1300B"])
+def test_capi_past_column_wrap(golden_index, name):
+    """The same 4.3 M-original streams through the siamese.h C ABI (the reference's own driver
+    relinked against libtonk_amd.so): transcript digest == the reference codec's."""
+    e = golden_index["long"][name]
+    exe = os.path.join(NATIVE, "_build", "capi_gen")
+    sid = e["stream"]
+    out = subprocess.run([exe, "transcript", "/dev/stdout"] + e["args"] + [f"seed_data={1000 + sid}", f"seed_loss={2000 + sid}"],
+                         capture_output=True, timeout=900)
+    assert out.returncode == 0, out.stderr.decode()[-2000:]
+    text = out.stdout.decode()
+    assert text.splitlines()[-1] == e["summary"]
+    assert sha256(text) == e["sha256"]

@@ -79,7 +79,7 @@ class _SessionParams(ctypes.Structure):
         "loss_thresh", "ge_enable", "gb_thresh", "bg_thresh", "loss_on_recovery", "fec_rate_q16",
         "ack_every", "ack_bytes", "arq_lag", "flush_max", "record", "stage_host")] + [
             ("arena_bytes", ctypes.c_uint64), ("rtx_every", ctypes.c_uint32), ("rtx_msec", ctypes.c_uint32),
-            ("input_pool", ctypes.c_uint32)]
+            ("input_pool", ctypes.c_uint32), ("hold_full", ctypes.c_uint32)]
 
 
 SUMMARY_FIELDS = ["originals", "lost_originals", "recoveries", "lost_recoveries", "recovered", "arq",
@@ -110,11 +110,12 @@ class WorkloadParams:
     """Synthetic workload parameters (tonk_amd/csrc/workload.h Params)."""
 
     KEYS = ("n", "pmin", "pmax", "loss", "ge", "gb", "bg", "lossrec", "fec", "ack", "ackbytes", "arq", "flush")
-    # retransmission ticks under a virtual clock (workload.h); written to args() only when on
-    OPTIONAL = ("rtx", "rtxms")
+    # retransmission ticks under a virtual clock (workload.h) and the window-full behaviour; each
+    # written to args() only when on
+    OPTIONAL = ("rtx", "rtxms", "full")
 
     def __init__(self, n=4096, payload=1300, payload_max=None, loss=0.01, burst=None, fec=None, ack=64,
-                 ack_bytes=256, arq=0, flush=4096, loss_on_recovery=True, rtx=0, rtx_msec=1):
+                 ack_bytes=256, arq=0, flush=4096, loss_on_recovery=True, rtx=0, rtx_msec=1, full=0):
         self.n = n
         self.pmin = payload
         self.pmax = payload_max if payload_max is not None else payload
@@ -133,9 +134,10 @@ class WorkloadParams:
         self.lossrec = 1 if loss_on_recovery else 0
         self.rtx = rtx
         self.rtxms = rtx_msec
+        self.full = full
 
     def args(self) -> list[str]:
-        keys = self.KEYS + (self.OPTIONAL if self.rtx else ())
+        keys = self.KEYS + (("rtx", "rtxms") if self.rtx else ()) + (("full",) if self.full else ())
         return [f"{k}={getattr(self, k)}" for k in keys]
 
     @classmethod
@@ -181,6 +183,7 @@ class Session:
         p.stage_host = 3 if stage_host is True else int(stage_host or 0)
         p.rtx_every, p.rtx_msec = wp.rtx, wp.rtxms
         p.input_pool = input_pool
+        p.hold_full = wp.full
         self.n_streams = n_streams
         err = ctypes.create_string_buffer(512)
         self._h = lib().tamd_session_create(ctypes.byref(p), err, len(err))

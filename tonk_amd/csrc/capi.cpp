@@ -251,6 +251,10 @@ struct Staging {
     // The launch-free path: one command buffer per half.  A half that fills up goes out as an
     // upload-only command from its buffer; a program's command is built in the current half's.
     CmdBuf cmd[2];
+    // A command of this codec did not complete (the server timed out or died): it may still run,
+    // reading these halves and writing the codec's rows and pinned buffer, so none of them is
+    // ever freed or reused (the codec is disabled; Codec::~Codec leaks its segments too).
+    bool stalled = false;
 
     size_t need(size_t bytes, size_t n_desc) const { return ((bytes + 15) & ~(size_t)15) + n_desc * 16 + 16; }
     // The current half's packets as zero-copy sources of one batched host_copy (combined
@@ -269,7 +273,13 @@ struct Staging {
     bool settle_cmds() {
         bool ok = true;
         for (CmdBuf& b : cmd) ok = g_srv->settle(b) && ok;
+        if (!ok) stalled = true;
         return ok;
+    }
+    bool settle_cmd(int h) {
+        if (!g_srv || g_srv->settle(cmd[h])) return true;
+        stalled = true;
+        return false;
     }
     // Enqueue the current half (caller holds the device lock).
     void send_locked(Device& dev) {
@@ -310,18 +320,21 @@ struct Staging {
     }
     // Copy a packet into the staging for arena unit offset `row`.
     bool stage(uint32_t row, const uint8_t* data, uint32_t n) {
-        if (used && (used + n > kFlushBytes || need(used + n, descs.size() + 1) > cap) && g_srv) {
+        if (stalled) return false;
+        if (used && (used + n > kFlushBytes || need(used + n, descs.size() + 1) > cap) && g_srv && g_srv->live()) {
             // launch-free: the full half lands by an upload-only command; the other half is
-            // reused once its own command has completed
+            // reused once its own command -- and a launch-path copy from it -- has completed
             thread_local std::vector<Device::HostCopy> ups, none;
             ups.clear();
             peek_uploads(ups);
-            if (g_srv->settle(cmd[cur]) && Server::build(cmd[cur], ups, nullptr, none)) {
+            if (!settle_cmd(cur)) return false;
+            if (Server::build(cmd[cur], ups, nullptr, none)) {
                 g_srv->post(cmd[cur]);
                 descs.clear();
                 used = 0;
                 cur ^= 1;
-                if (!g_srv->settle(cmd[cur])) return false;
+                if (!settle_cmd(cur)) return false;
+                settle(sent[cur]);
             }
         }
         if (used && (used + n > kFlushBytes || need(used + n, descs.size() + 1) > cap)) {
@@ -334,6 +347,7 @@ struct Staging {
             }
             cur ^= 1;
             settle(sent[cur]);
+            if (!settle_cmd(cur)) return false;
         }
         if (need(used + n, descs.size() + 1) > cap) {  // (only while the half is empty)
             if (used) return false;
@@ -349,6 +363,7 @@ struct Staging {
         return true;
     }
     ~Staging() {
+        if (stalled) return;  // (kept for good: a command may still read or write them)
         for (uint8_t* h : half) Device::host_free(h);
         for (CmdBuf& b : cmd) Device::host_free(b.mem);
     }
@@ -383,6 +398,7 @@ struct Codec {
     // The pinned buffer holds at least n bytes (no copy can be landing in it: every read into it
     // was waited for before the call that issued it returned).
     bool ensure_pinned(size_t n) {
+        if (staging.stalled) return false;  // (a stalled command may still write the old one)
         if (n <= pinned_cap) return true;
         Device::host_free(pinned);
         pinned_cap = n < 4096 ? 4096 : n + n / 2;
@@ -393,7 +409,7 @@ struct Codec {
     // Before the codec's rows go back to the pool: nothing of its may still be in flight.
     bool used_launch = false;  // a program of this codec went through the launch path
     void quiesce() {
-        if (g_srv) staging.settle_cmds();
+        if (g_srv && !staging.settle_cmds()) return;  // stalled: ~Codec keeps everything
         if (g_srv && !used_launch && !staging.sent[0] && !staging.sent[1]) return;
         DevLock dl;
         g_rt->dev.synchronize();
@@ -403,7 +419,15 @@ struct Codec {
                 ev = nullptr;
             }
     }
-    ~Codec() { Device::host_free(pinned); }
+    ~Codec() {
+        if (staging.stalled) {
+            // a command that never completed may still write these rows and the pinned buffer:
+            // they never go back to the pool (a leak, bounded by one codec per stalled command)
+            ctx.rows.leak_segments();
+            return;
+        }
+        Device::host_free(pinned);
+    }
 };
 
 // Encode-ahead.  A caller that encodes twice with no other call on the encoder between (the
@@ -573,6 +597,7 @@ void launch_batch(std::vector<RunReq*>& b, unsigned stream) {
 bool run_and_read(Codec& c, const std::vector<Device::HostCopy>& reads) {
     Context& ctx = c.ctx;
     const int64_t t0 = g_watch ? now_ns() : 0;
+    if (c.staging.stalled) return false;
     ctx.prepare_flush();
     const int64_t t1 = g_watch ? now_ns() : 0;
     if (g_srv) {
@@ -594,7 +619,7 @@ bool run_and_read(Codec& c, const std::vector<Device::HostCopy>& reads) {
             ctx.finish_flush();
             return false;
         }
-        if (Server::build(b, ups, &ctx.pb, reads)) {
+        if (g_srv->live() && Server::build(b, ups, &ctx.pb, reads)) {
             sg.descs.clear();
             sg.used = 0;
             g_srv->post(b);
@@ -608,8 +633,12 @@ bool run_and_read(Codec& c, const std::vector<Device::HostCopy>& reads) {
                 g_wait_ns.fetch_add((uint64_t)(now_ns() - w0), std::memory_order_relaxed);
                 g_prepare_ns.fetch_add((uint64_t)(t1 - t0), std::memory_order_relaxed);
             }
+            if (!ok) {  // still in flight: nothing it may touch is released (Staging::stalled)
+                sg.stalled = true;
+                return false;
+            }
             ctx.rows.release_up_to(done);
-            return ok;
+            return true;
         }
         c.used_launch = true;
     }

@@ -138,6 +138,9 @@ public:
     }
     size_t live_rows() const { return live_; }
     uint64_t bytes_in_use() const { return (uint64_t)used_units_ * TAMD_ROW_UNIT; }
+    // Keep the segments on destruction instead of returning them to the source: device work that
+    // may still write them (a command that never completed) must not land in another codec's rows.
+    void leak_segments() { src_ = nullptr; segments_.clear(); }
 
 private:
     // per row handle (structure of arrays: offset lookups dominate)

@@ -61,12 +61,15 @@ bool Server::init(Device& dev, unsigned workers, unsigned ring_size, double idle
     if (!build(probe, none, nullptr, none)) return false;
     post(probe);
     const bool answered = wait(probe);
-    Device::host_free(probe.mem);
     if (!answered) {
+        // (the probe's buffer stays allocated: the executor may still write its completion words)
         fprintf(stderr, "tonk_amd: the persistent executor did not answer; using kernel launches\n");
         ok_ = false;
         return false;
     }
+    Device::host_free(probe.mem);
+    // (test hook: a short timeout makes a loaded command time out, to exercise the dead server)
+    if (const char* e = getenv("TONK_AMD_SERVE_TIMEOUT_US")) timeout_us_ = atof(e);
     return true;
 }
 
@@ -99,12 +102,18 @@ bool Server::launch_locked(uint64_t tail0) {
     return true;
 }
 
-void Server::ensure_running() {
+bool Server::ensure_running() {
     std::lock_guard<std::mutex> lk(launch_mu_);
-    if (host_->exited_gen != gen_.load()) return;  // the current instance runs (or a relaunch won)
+    if (dead_.load()) return false;
+    if (host_->exited_gen != gen_.load()) return true;  // the current instance runs (or a relaunch won)
     dev_->bind_thread();
     const uint64_t tail = host_->exit_tail;
-    if (!launch_locked(tail)) fprintf(stderr, "tonk_amd: relaunching the persistent executor failed\n");
+    if (launch_locked(tail)) return true;
+    // Nothing will consume the ring: later calls take the launch path, and the waits of commands
+    // already posted end at once (their codecs are disabled and keep their buffers).
+    fprintf(stderr, "tonk_amd: relaunching the persistent executor failed; using kernel launches\n");
+    dead_.store(true);
+    return false;
 }
 
 bool Server::build(CmdBuf& b, const std::vector<Device::HostCopy>& up, const ProgramBuilder* pb,
@@ -225,9 +234,15 @@ void Server::post(CmdBuf& b) {
     for (uint32_t spin = 0; idx >= host_->consumed + ring_size_; ++spin) {
         if ((spin & 255) == 255) {
             if (host_->exited_gen == gen_.load()) ensure_running();
+            if (dead_.load(std::memory_order_relaxed)) break;
             sched_yield();
         }
         _mm_pause();
+    }
+    if (idx >= host_->consumed + ring_size_) {  // dead server, slot still taken: never written
+        b.ticket = idx;
+        b.busy = true;
+        return;
     }
     // six tagged granules, 8-byte stores (each one atomic): the dispatcher takes the slot once
     // every tag is this command's
@@ -268,19 +283,25 @@ bool Server::wait(CmdBuf& b) {
     const double t0 = now_us();
     for (uint32_t spin = 1;; ++spin) {
         if (*d == want) break;
+        if (dead_.load(std::memory_order_relaxed)) return false;  // (b stays busy: never reused)
         if ((spin & 63) == 0) {
             const double t = now_us() - t0;
             // the executor ended on an idle spell without taking this command: start the next one
-            if (host_->exited_gen == gen_.load() && host_->exit_tail <= b.ticket) ensure_running();
-            if (t > 3e6) {
-                fprintf(stderr, "tonk_amd: command %llu not completed after 3 s (done word %llu); dispatcher: start %llu "
+            if (host_->exited_gen == gen_.load() && host_->exit_tail <= b.ticket && !ensure_running()) return false;
+            if (t > timeout_us_) {
+                // The command is still posted and may run later: the server goes dead (new
+                // commands take the launch path), and the caller keeps `b`, its codec's pinned
+                // buffers and rows for good (capi.cpp Codec::stalled).
+                dead_.store(true);
+                fprintf(stderr, "tonk_amd: command %llu not completed after %.0f us (done word %llu); dispatcher: start %llu "
                         "polls/1024 %llu waits for %llu; command 0: stage %llu block %llu; consumed %llu exited_gen %llu "
                         "(launched %u) exit_tail %llu\n",
-                        (unsigned long long)b.ticket, (unsigned long long)*d, (unsigned long long)host_->dbg[0],
+                        (unsigned long long)b.ticket, timeout_us_, (unsigned long long)*d, (unsigned long long)host_->dbg[0],
                         (unsigned long long)host_->dbg[1], (unsigned long long)host_->dbg[2],
                         (unsigned long long)host_->dbg[3], (unsigned long long)host_->dbg[4],
                         (unsigned long long)host_->consumed, (unsigned long long)host_->exited_gen, gen_.load(),
                         (unsigned long long)host_->exit_tail);
+                fprintf(stderr, "tonk_amd: the persistent executor is off; using kernel launches\n");
                 return false;
             }
             // a short spin, then give the core to other threads between polls (a Tonk process

@@ -40,13 +40,18 @@ public:
     // the C ABI keeps its launch path.
     bool init(Device& dev, unsigned workers, unsigned ring_size, double idle_ms);
     bool ok() const { return ok_; }
+    // Whether new commands may be posted.  False once a command timed out or a relaunch of the
+    // executor failed: later calls take the launch path, and commands already posted are only
+    // checked, never waited for again (wait() returns false at once for one not done).
+    bool live() const { return ok_ && !dead_.load(std::memory_order_relaxed); }
     // Build a command into `b` (grown as needed): `up` packets to land, the program of `pb`
     // (may be null or empty), `rd` rows to read back.  False when it does not fit the worker's
     // LDS (TAMD_SERVE_CMD_BYTES) or has too many levels: the caller takes the launch path.
     static bool build(CmdBuf& b, const std::vector<Device::HostCopy>& up, const ProgramBuilder* pb,
                       const std::vector<Device::HostCopy>& rd);
     // Post the command in `b` (after build); wait for it.  wait() returns false on a timeout
-    // (the executor stopped answering: the codec is disabled).
+    // (the executor stopped answering: the server goes dead, the codec is disabled and keeps
+    // the command's buffers and rows for good -- the command may still run later).
     void post(CmdBuf& b);
     bool wait(CmdBuf& b);
     bool settle(CmdBuf& b) { return b.busy ? wait(b) : true; }
@@ -69,7 +74,9 @@ private:
     std::atomic<uint64_t> head_{0};
     std::mutex launch_mu_;
     std::atomic<uint32_t> gen_{0};  // generation of the instance launched last
-    void ensure_running();
+    std::atomic<bool> dead_{false};
+    double timeout_us_ = 3e6;  // a command not completed after this long kills the server
+    bool ensure_running();      // false (and the server dead) when a relaunch failed
     uint32_t debug_ = 0;  // TONK_AMD_SERVE_DEBUG bits (diagnostics): 1 the probe's completion words in
                           // the server's own coherent page, 4 a release fence before every completion word
     uint64_t* dbg_done_ = nullptr;

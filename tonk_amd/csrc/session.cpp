@@ -260,6 +260,7 @@ struct Stream {
         return rc;
     }
     int enc_ack(const uint8_t* buf, uint32_t n, uint32_t* next) { return enc->acknowledge(buf, n, next); }
+    int enc_is_ready() { return enc->remaining_slots() <= 2 ? (int)kMaxPacketsReached : 0; }
     int dec_add_original(uint32_t col, uint32_t index, uint32_t len) {
         const uint32_t hb = length_header_bytes(len);
         bool took = false;
@@ -1280,6 +1281,7 @@ void* tamd_session_create(const tamd_session_params* p, char* err, size_t err_le
         q.flush_max = p->flush_max;
         q.rtx_every = p->rtx_every;
         q.rtx_msec = p->rtx_msec ? p->rtx_msec : 1;
+        q.hold_full = p->hold_full;
         q.batch_adds = getenv("TONK_AMD_SINGLE_ADDS") ? 0 : 1;  // A/B switch (profiling)
         q.seed_data = 1000 + q.stream_id;
         q.seed_loss = 2000 + q.stream_id;

@@ -64,8 +64,22 @@ struct Params {
     // original so RTO decisions are deterministic.  0: off (the codec's own clock is used).
     uint32_t rtx_every = 0, rtx_msec = 1;
     uint32_t batch_adds = 1;   // runs of quiet originals go to the backend as batched adds
+    // Window-full behaviour (siamese.cpp:80-93, SiameseEncoder.cpp:91-96): before every add the
+    // sender asks siamese_encoder_is_ready and logs a refusal ("W" line) but adds anyway (the
+    // two slots of slack); an add refused with MaxPacketsReached makes the receiver acknowledge
+    // (and, if that frees nothing, the sender flush a recovery packet) before the add is retried.
+    // Single adds only (the window's fill is the codec's, not the runner's, to know).
+    uint32_t hold_full = 0;
     uint64_t seed_data = 1000, seed_loss = 2000;
 };
+
+// Packet numbers are 22-bit columns (SiameseCommon.h:102 kColumnPeriod): the stream index of
+// column `col` when `top` originals have been added, the most recent one at or below top - 1
+// (recovered and retransmitted originals are always in the encoder's window, < 2^21 back).
+inline uint32_t index_of_column(uint32_t col, uint32_t top) {
+    const uint32_t last = top ? top - 1 : 0;
+    return last - ((last - col) & 0x3fffffu);
+}
 
 static const uint32_t kRtxPerTick = 4;
 static const uint64_t kVirtualClockStart = 1000;  // ms (send times are never 0)
@@ -89,6 +103,7 @@ inline bool parse_param(Params& p, const std::string& k, unsigned long long v) {
     else if (k == "flush") p.flush_max = (uint32_t)v;
     else if (k == "rtx") p.rtx_every = (uint32_t)v;
     else if (k == "rtxms") p.rtx_msec = (uint32_t)v;
+    else if (k == "full") p.hold_full = (uint32_t)v;
     else if (k == "seed_data") p.seed_data = v;
     else if (k == "seed_loss") p.seed_loss = v;
     else return false;
@@ -215,6 +230,7 @@ struct Summary {
 //   int  dec_ack(uint8_t* buf, uint32_t limit, uint32_t* used)
 //   void stats(uint64_t enc[9], uint64_t dec[11])
 //   void set_time(uint64_t msec)               -- virtual clock (retransmit scenarios only)
+//   int  enc_is_ready()                        -- siamese_encoder_is_ready (hold_full only)
 //   int  enc_retransmit(uint32_t* packetNum, uint32_t* bytes, const uint8_t** data)
 //                                              -- data may be null (the runner regenerates it)
 //   bool enc_add_run(uint32_t index, uint32_t k, uint32_t len, uint32_t* firstPacketNum)
@@ -254,7 +270,7 @@ public:
     // them) go to the backend as batched adds; the calls and results are those of single adds.
     void advance(uint32_t n) {
         const uint32_t end = std::min(p_.n_originals, next_ + n);
-        const bool batching = p_.batch_adds && !p_.rtx_every && p_.payload_min == p_.payload_max;
+        const bool batching = p_.batch_adds && !p_.rtx_every && !p_.hold_full && p_.payload_min == p_.payload_max;
         while (next_ < end) {
             int drawn = -1;  // loss draw of original next_ made by quiet_run (-1: not drawn)
             if (batching) {
@@ -283,9 +299,9 @@ public:
     void finish() {
         advance(p_.n_originals);
         for (uint32_t k = 0; k < p_.flush_max; ++k) {
-            bool complete = true;
-            for (uint32_t i = 0; i < p_.n_originals; ++i) if (!have_[i]) { complete = false; break; }
-            if (complete) break;
+            // (have_ only ever gains entries: the first missing index only moves up)
+            while (scan_ < p_.n_originals && have_[scan_]) ++scan_;
+            if (scan_ == p_.n_originals) break;
             ++s_.flush_encodes;
             send_recovery(false);
         }
@@ -305,6 +321,8 @@ private:
     std::vector<uint32_t> col_of_, pending_arq_;
     size_t arq_head_ = 0;
     uint32_t tokens_ = 0, next_ = 0;
+    uint32_t top_ = 0;   // originals added to the encoder (index_of_column)
+    uint32_t scan_ = 0;  // finish(): every index below is delivered or recovered
     uint32_t ack_countdown_ = 0;  // originals until the next acknowledgement
     uint32_t rtx_countdown_ = 0;  // originals until the next retransmission tick
     uint64_t now_ms_ = 0;         // virtual clock (rtx_every > 0)
@@ -313,17 +331,18 @@ private:
 
     // Retransmission tick (Tonk's PostRetransmit, TonkineseOutgoing.cpp:1079-1100): up to
     // kRtxPerTick originals chosen by the encoder's RTO logic, each sent through the channel.
-    // Packet numbers equal stream indices here (every add succeeds from column 0).
+    // Packet numbers are stream indices modulo the 22-bit column period.
     void retransmit_tick() {
         for (uint32_t k = 0; k < kRtxPerTick; ++k) {
             uint32_t num = 0, bytes = 0;
             const uint8_t* data = nullptr;
             const int rc = be_.enc_retransmit(&num, &bytes, &data);
             uint64_t h = 0;
+            const uint32_t idx = index_of_column(num, top_);
             if (rc == 0) {
-                if (!data && num < p_.n_originals) {
+                if (!data && idx < p_.n_originals) {
                     rtx_buf_.resize(bytes ? bytes : 1);
-                    payload_bytes(p_, num, rtx_buf_.data(), bytes);
+                    payload_bytes(p_, idx, rtx_buf_.data(), bytes);
                     data = rtx_buf_.data();
                 }
                 h = data ? fnv1a(data, bytes) : 0;
@@ -331,10 +350,10 @@ private:
             tr_.on_retransmit(rc, num, bytes, h);
             if (rc != 0) break;
             ++s_.retransmits;
-            if (ch_.lost() || num >= p_.n_originals) continue;
-            const int ro = be_.dec_add_original(num, num, bytes);
+            if (ch_.lost() || idx >= p_.n_originals) continue;
+            const int ro = be_.dec_add_original(num, idx, bytes);
             tr_.on_event('T', ro, num, 0);
-            if (!have_[num]) have_[num] = 1;
+            if (!have_[idx]) have_[idx] = 1;
             decode_loop();
         }
     }
@@ -348,7 +367,8 @@ private:
             tr_.on_decode(rc, nums_, dref);
             if (rc != 0) break;
             for (uint32_t c : nums_) {
-                if (c < p_.n_originals && !have_[c]) { have_[c] = 1; ++s_.recovered; }
+                const uint32_t i = index_of_column(c, top_);
+                if (i < p_.n_originals && !have_[i]) { have_[i] = 1; ++s_.recovered; }
             }
             if (nums_.empty()) break;
         }
@@ -399,6 +419,7 @@ private:
             for (uint32_t j = 0; j < k; ++j) one(i0 + j, 0);
             return;
         }
+        top_ = i0 + k;
         for (uint32_t j = 0; j < k; ++j) col_of_[i0 + j] = (col0 + j) & 0x3fffffu;
         s_.originals += k;
         if (be_.dec_add_run(col0, i0, k, len)) {
@@ -429,6 +450,7 @@ private:
             one(e, lost ? 1 : 0);
             return;
         }
+        top_ = e + 1;
         for (uint32_t j = 0; j <= k; ++j) col_of_[i0 + j] = (col0 + j) & 0x3fffffu;
         s_.originals += k + 1;
         const uint32_t kd = lost ? k : k + 1;  // delivered
@@ -451,6 +473,19 @@ private:
         events_after(e);
     }
 
+    // The decoder's acknowledgement, delivered to the encoder.
+    void exchange_ack() {
+        uint8_t buf[2048];
+        const uint32_t limit = p_.ack_bytes < sizeof(buf) ? p_.ack_bytes : (uint32_t)sizeof(buf);
+        uint32_t used = 0;
+        const int rd = be_.dec_ack(buf, limit, &used);
+        uint32_t next = 0;
+        int re = -1;
+        if (rd == 0 && used > 0) re = be_.enc_ack(buf, used, &next);
+        tr_.on_ack(rd, buf, used, re, next);
+        ++s_.acks;
+    }
+
     // One original: add, channel, recovery tokens, acknowledgement, retransmission, ARQ.
     // `drawn`: its loss draw when already made (0 delivered, 1 lost), -1 to draw here.
     void one(uint32_t i, int drawn = -1) {
@@ -460,8 +495,25 @@ private:
         }
         const uint32_t len = payload_length(p_, i);
         uint32_t col = 0;
-        const int ra = be_.enc_add(i, len, &col);
+        if (p_.hold_full) {
+            const int ready = be_.enc_is_ready();
+            tr_.on_event('W', ready, i, 0);
+        }
+        int ra = be_.enc_add(i, len, &col);
         tr_.on_event('a', ra, i, col);
+        // window full (hold_full): the receiver acknowledges, and if that frees no slot the
+        // sender flushes a recovery packet, until the add goes through (bounded)
+        for (uint32_t tries = 0; p_.hold_full && ra == 3 && tries < 64; ++tries) {
+            exchange_ack();
+            ra = be_.enc_add(i, len, &col);
+            tr_.on_event('a', ra, i, col);
+            if (ra == 3) send_recovery(false);
+        }
+        if (ra == 0) top_ = i + 1;
+        if (p_.hold_full && ra != 0) {  // never went out (the receiver does not expect it)
+            have_[i] = 1;
+            return;
+        }
         col_of_[i] = col;
         ++s_.originals;
         if (drawn >= 0 ? drawn != 0 : ch_.lost()) {
@@ -487,15 +539,7 @@ private:
 
         if (p_.ack_every && --ack_countdown_ == 0) {
             ack_countdown_ = p_.ack_every;
-            uint8_t buf[2048];
-            const uint32_t limit = p_.ack_bytes < sizeof(buf) ? p_.ack_bytes : (uint32_t)sizeof(buf);
-            uint32_t used = 0;
-            const int rd = be_.dec_ack(buf, limit, &used);
-            uint32_t next = 0;
-            int re = -1;
-            if (rd == 0 && used > 0) re = be_.enc_ack(buf, used, &next);
-            tr_.on_ack(rd, buf, used, re, next);
-            ++s_.acks;
+            exchange_ack();
         }
 
         if (p_.rtx_every && --rtx_countdown_ == 0) {
