@@ -484,7 +484,8 @@ enum { R_LANE3 = 1, R_CAUCHY = 2, R_CONST = 3, R_MULTI = 4, R_DENSE = 5 };
            and cx = CX(col_k), acc_0 ^= (b0 ^ b1 cx ^ b2 cx^2 ^ rx (b3 ^ b4 cx ^ b5 cx^2)) * row_k, the
            lane-sum combination of a Siamese row (SiameseEncoder.cpp:1046-1098) packet by packet;
            with p = 2 or 3 targets: p COEFS words (cap = ADJ words | hi << 16), each followed by its
-           ADJ words, target t adding rows k < hi_t into acc_t (rows of nested sum ranges) */
+           ADJ words, target t adding rows k < hi_t into acc_t (rows of nested sum ranges); one
+           target: w0 bits 24..31 = s > 1 scales every coefficient (decoder eliminations) */
 int oracle_run_program(uint8_t* arena, size_t arena_bytes,
                        const uint32_t* ops, unsigned n_ops,
                        const uint32_t* instrs, unsigned n_instrs)
@@ -604,6 +605,10 @@ int oracle_run_program(uint8_t* arena, size_t arena_bytes,
                                 const uint32_t d = tg[4 + 4 * w + q];
                                 if ((d >> 16) == e) g ^= (uint8_t)(d >> 8);
                             }
+                        /* w0 bits 24..31 (one target): scale s of every coefficient (0 or 1: none) --
+                           a decoder elimination run scaled by the solve */
+                        const uint8_t s = (uint8_t)(w[0] >> 24);
+                        if (s > 1) g = oracle_gf_mul(s, g);
                         if (g) oracle_muladd_mem(acc, g, row, len);
                     } else if (mode == R_MULTI) {
                         for (unsigned a = 0; a < 3; ++a) {

@@ -27,6 +27,7 @@ static uint64_t g_arena_bytes = 512ull << 20;
 // as the siamese.h C ABI runs it); every backend call touches its codec like capi.cpp does.
 static bool g_dirty = false;
 static bool g_nobatch = false;  // nobatch=1: the runner's single-add path only
+static int g_ddirect = -1;  // ddirect=0/1: decoder eliminations through the lanes / direct (default: the engine's)
 // pipeline=1: the session's pipelined launches (Device::launch_step: level 1 of a program beside
 // the next level of every older program in flight) are simulated and every launch is checked for
 // hazards (no segment reads or writes a row another writes) before the programs run in order.
@@ -193,6 +194,7 @@ struct Harness {
         ctx.backsub_rows = g_backsub;
         ctx.dense_split = g_split;
         ctx.short_scans = g_short;
+        if (g_ddirect >= 0) ctx.direct_elim = g_ddirect != 0;
         arena.assign(g_arena_bytes, 0);
         enc = new Encoder(&ctx, row_bytes);
         dec = new Decoder(&ctx, row_bytes);
@@ -636,6 +638,7 @@ int main(int argc, char** argv) {
         else if (k == "contig") g_contig = v != 0;
         else if (k == "ahead") g_ahead = (uint32_t)v;
         else if (k == "short") g_short = v != 0;
+        else if (k == "ddirect") g_ddirect = (int)v;
         else if (parse_param(p, k, v)) {}
         else { fprintf(stderr, "bad key %s\n", k.c_str()); return 2; }
     }

@@ -81,6 +81,24 @@ def test_control_plane_matches_reference(harness, golden_index, tmp_path, name, 
     assert got == want, first_diff(want, got)
 
 
+@pytest.mark.parametrize("mode", [["mode=batch", "batch=4096"], ["mode=batch", "batch=1000", "pipeline=1", "split=48", "contig=1"],
+                                  ["mode=sync", "dirty=1", "expand=16", "backsub=2"]])
+@pytest.mark.parametrize("name", ["c2_4096_p1_ack64", "c3_4096_p2_ack64_s63", "c5_65536_ge5_b4", "hiloss_p20_arq",
+                                  "burst8_p5", "big_9000_p3_ack64"])
+def test_control_plane_lane_eliminations(harness, golden_index, tmp_path, name, mode):
+    """The decoder's Siamese-row eliminations through its running lane sums only (ddirect=0), the
+    path rows with long or fragmented sum ranges take (the default reads short ranges of long
+    runs straight from the packets, Decoder::eliminate_direct): transcript == reference's."""
+    sc = golden_index["scenarios"][name]
+    sid = sc["stream"]
+    out = tmp_path / "t.txt"
+    r = subprocess.run([harness, str(out), "ddirect=0"] + mode + sc["args"] +
+                       [f"seed_data={1000 + sid}", f"seed_loss={2000 + sid}"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    want = golden_text(name)
+    assert out.read_text() == want, first_diff(want, out.read_text())
+
+
 @pytest.mark.parametrize("contig", [0, 1])
 @pytest.mark.parametrize("batch_name,sid", [("cfg2_64x4096_p2_ack64", 0), ("cfg2_64x4096_p2_ack64", 37),
                                              ("cfg3_rank7_64x12288_p1_ack64", 448),

@@ -1226,9 +1226,11 @@ bool Decoder::eliminate_original_data() {
             }
         } else {
             const uint32_t rbytes = rec->bytes;
+            uint32_t sum_elem = to_element(m.ColumnStart);
+            // (the sums' start is still in the window: no packet they would hold has been removed)
+            const bool sum_valid = !invalid_element(sum_elem);
             {
             TAMD_PROF_SCOPE(kElimStart);
-            uint32_t sum_elem = to_element(m.ColumnStart);
             if (m.ColumnStart != sum_column_start_ || m.SumCount < sum_column_count_) {
                 if (invalid_element(sum_elem)) return false;
                 reset_sums(sum_elem);
@@ -1239,6 +1241,17 @@ bool Decoder::eliminate_original_data() {
             }
             }
             sum_column_count_ = m.SumCount;
+            if (sum_valid && ctx_->direct_elim && eliminate_direct(rec, sum_elem, buf)) {
+                if (ctx_->oom) return false;
+                if (cr_.lost_count == 1) {
+                    if (buf.size() > kMergeAbove) sym_merge(buf);
+                    continue;
+                }
+                TAMD_PROF_SCOPE(kElimFold);
+                const RowId p = fold_low_levels(ctx_->rows, ctx_->pb, buf, 3, rec->bytes, row_bytes_);
+                if (p != kNoRow) ctx_->temps.push_back(p);
+                continue;
+            }
 
             const uint8_t rx = row_value(m.Row);
             {
@@ -1289,6 +1302,97 @@ bool Decoder::eliminate_original_data() {
         if (p != kNoRow) ctx_->temps.push_back(p);
     }
     return !disabled_ && !ctx_->oom;
+}
+
+// A Siamese row's elimination straight from the packets (the decoder's counterpart of the
+// encoder's direct dense ranges, Encoder::defer_dense).  The reference subtracts the lanes' running
+// sums over the row's sum range [sum_elem, ee) (SiameseDecoder.cpp:900-1028, GetSum :1680-1739)
+// and then its LDPC pairs (:1029-1047).  A lane sum holds every element of its lane in that range
+// that has data when it is read -- received, or recovered and plugged in (PlugSumHoles) -- each
+// zero-padded to the longest and read clipped to the row's length, so the same value is
+//   sum over known elements j in [sum_elem, ee) of coef(lane opcode of j, cx_j, RX) * clip(x_j),
+// one DENSE run term per run of received packets (coefficients computed on the device, the pairs
+// that land in the run folded in as ADJ additions) and one term per other known element.  Valid
+// while sum_elem is in the window: then no element the sums would hold has been removed (a
+// removal only ever cuts a prefix, and advances the lanes past it first).  The lane sums stay as
+// the reference leaves them (start_sums / reset_sums ran) but are not advanced here: a later
+// lane read accumulates from where they stand.  Returns false, with nothing appended, when the
+// range is long or broken into short runs (C ABI adds are one record each): the lanes are used.
+bool Decoder::eliminate_direct(Recovery* rec, uint32_t sum_elem, Sym& buf) {
+    const RecoveryMeta m = rec->meta;
+    const uint32_t es = rec->element_start, ee = rec->element_end;
+    if (ee <= sum_elem || ee - sum_elem > Encoder::kDirectMax || ee > count_) return false;
+    TAMD_PROF_SCOPE(kElimSums);
+    const uint32_t rbytes = rec->bytes;
+    // the range's records: runs of segment packets and single known elements
+    drun_.clear();
+    uint32_t singles = 0;
+    for (uint32_t j = sum_elem; j < ee;) {
+        const uint32_t id = seg_id(j);
+        if (id != kSingle) {
+            const Segment& sg = segs_[id - seg_base_];
+            const uint32_t k = j + base_ - sg.first;
+            const uint32_t stop = std::min(sg.end() - base_, ee);
+            if (sg.bytes) drun_.push_back(DirectRun{j, stop - j, sg.off(k), sg.stride, std::min(sg.bytes, rbytes),
+                                                    col_add(sg.column0, k), kNoRow});
+            j = stop;
+            continue;
+        }
+        const StoredOriginal& o = elem(j);
+        if (o.bytes > 0) {
+            drun_.push_back(DirectRun{j, 0, 0, 0, std::min(o.bytes, rbytes), to_column(j), o.row});
+            ++singles;
+        }
+        ++j;
+    }
+    if (drun_.size() * Encoder::kDirectMinRun > ee - sum_elem) {
+        drun_.clear();
+        return false;
+    }
+    // LDPC pairs (element << 8 | coefficient), sorted: those on a run's packets become its ADJ
+    // additions, the others are read as rows (only when the element has data)
+    const uint8_t rx = row_value(m.Row);
+    Pcg32 prng;
+    prng.seed(m.Row, m.LDPCCount);
+    const uint32_t pairs = (m.LDPCCount + kPairRate - 1) / kPairRate;
+    const FastMod ldpc_mod(m.LDPCCount);
+    dpairs_.resize(2 * (size_t)pairs);
+    for (uint32_t i = 0; i < pairs; ++i) {
+        dpairs_[2 * i] = (uint64_t)(es + ldpc_mod(prng.next())) << 8 | 1u;
+        dpairs_[2 * i + 1] = (uint64_t)(es + ldpc_mod(prng.next())) << 8 | rx;
+    }
+    std::sort(dpairs_.begin(), dpairs_.end());
+    uint64_t ops = 0;
+    uint8_t lk[kLanes][3];
+    for (unsigned l = 0; l < kLanes; ++l) {
+        const unsigned op = row_opcode(l, m.Row);
+        ops |= (uint64_t)op << (6 * l);
+        opcode_coefs(op, rx, lk[l]);
+    }
+    auto loose_pair = [&](uint64_t pr) {
+        RowId row;
+        uint32_t b;
+        if (packet((uint32_t)(pr >> 8), row, b)) read_original(row, b < rbytes ? b : rbytes, (uint8_t)pr, buf);
+    };
+    size_t pi = 0;
+    for (const DirectRun& r : drun_) {
+        while (pi < dpairs_.size() && (uint32_t)(dpairs_[pi] >> 8) < r.e0) loose_pair(dpairs_[pi++]);
+        if (!r.n) {  // a single known element: its dense coefficient on the host
+            const uint8_t* k = lk[r.col % kLanes];
+            const uint8_t cx = column_value(r.col);
+            const uint8_t c = (uint8_t)(k[0] ^ gf_mul(k[1], cx) ^ gf_mul(k[2], gf_sqr(cx)));
+            if (c) read_original(r.row, r.len, c, buf);
+            continue;
+        }
+        dadj_.clear();
+        for (; pi < dpairs_.size() && (uint32_t)(dpairs_[pi] >> 8) < r.e0 + r.n; ++pi)
+            dadj_.push_back(((uint32_t)(dpairs_[pi] >> 8) - r.e0) << 16 | (uint32_t)(dpairs_[pi] & 0xffu) << 8);
+        buf.push_back(ctx_->pb.dense_run_term(r.off, r.stride, r.n, r.col, ops, rx, dadj_.data(),
+                                              (uint32_t)dadj_.size(), r.len));
+    }
+    while (pi < dpairs_.size()) loose_pair(dpairs_[pi++]);
+    (void)singles;
+    return true;
 }
 
 // Decoder::MultiplyLowerTriangle (:1065-1104), in coefficient space.  The reference adds row

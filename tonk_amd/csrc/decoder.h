@@ -256,6 +256,11 @@ private:
     bool check_recovery_possible();
     Result decode_checked_region();
     bool eliminate_original_data();
+    bool eliminate_direct(Recovery* rec, uint32_t sum_elem, Sym& buf);
+    struct DirectRun { uint32_t e0, n, off, stride, len, col; RowId row; };  // n 0: a single element
+    std::vector<DirectRun> drun_;
+    std::vector<uint64_t> dpairs_;
+    std::vector<uint32_t> dadj_;
     bool multiply_lower_triangle();
     Result back_substitution();
     Result back_substitution_one();

@@ -83,6 +83,11 @@ public:
     // (level 1), added by the row's op (level 2), so no single work item walks hundreds of
     // packets (a level's tail).
     static const uint32_t kDenseSplit = 48;
+    // Siamese rows whose sum range is at most this many packets read it straight from the packets
+    // (defer_dense, and the decoder's Decoder::eliminate_direct); longer ones through the running
+    // lane sums (TONK_AMD_DIRECT overrides the encoder's).
+    static const uint32_t kDirectMax = 512;
+    static const uint32_t kDirectMinRun = 8;  // packets per run the direct reads need on average
     Encoder(Context* ctx, uint32_t row_bytes, HostRelease release = nullptr, void* user = nullptr);
     ~Encoder();
 
@@ -286,10 +291,6 @@ private:
     // (configs[2]) consecutive Cauchy windows of ~50 packets overlap by half, and grouping them
     // reads 27 % fewer window rows (cp_bench reads: 5998 -> 4366 per 4096 originals).
     static const uint32_t kGroupSpan = 160;
-    // Siamese rows whose sum range is at most this many packets read it straight from the packets
-    // (defer_dense); longer ones through the running lane sums (TONK_AMD_DIRECT overrides).
-    static const uint32_t kDirectMax = 512;
-    static const uint32_t kDirectMinRun = 8;  // packets per run the direct reads need on average
     CauchyTarget grp_[3];
     uint32_t grp_n_ = 0, grp_gen_ = 0, window_gen_ = 0;
     std::vector<Run> grp_union_;

@@ -142,6 +142,7 @@ void ProgramBuilder::clear() {
     level_ops_.clear();
     level_items_.clear();
     runs_.clear();
+    run_adj_.clear();
     max_level_ = 0;
     acc_bytes_ = store_bytes_ = 0;
 }
@@ -220,11 +221,11 @@ void ProgramBuilder::op_accr_multi(uint32_t row0, uint32_t stride, uint32_t coun
 }
 
 void ProgramBuilder::op_accr_dense(uint32_t row0, uint32_t stride, uint32_t count, uint32_t len, uint32_t col0,
-                                   uint64_t ops, uint8_t rx, const uint32_t* adj, uint32_t nadj) {
-    if (!len || !count) return;
+                                   uint64_t ops, uint8_t rx, const uint32_t* adj, uint32_t nadj, uint8_t scale) {
+    if (!len || !count || !scale) return;
     const uint32_t nwords = (nadj + 3) / 4;
     tamd_instr a, r, g;
-    a.w0 = tamd_w0(TAMD_I_ACCR, TAMD_R_DENSE, 0);
+    a.w0 = tamd_w0(TAMD_I_ACCR, TAMD_R_DENSE, 0) | (scale > 1 ? (uint32_t)scale << 24 : 0u);
     a.row = row0;
     a.len = len;
     a.cap = count;
@@ -492,10 +493,15 @@ uint32_t ProgramBuilder::combine(RowId dst, const Term* terms, size_t n, uint32_
         const Term& t = terms[i];
         if (!t.coef || !t.len || !is_run(t.row)) continue;
         const RunRef& r = runs_[t.row & ~kRunFlag];
+        --nrun;
+        if (r.mode == TAMD_R_DENSE) {  // (its scale rides in the ACCR word)
+            op_accr_dense(r.off0, r.stride, r.count, t.len, r.col0, r.ops, (uint8_t)r.p, run_adj_.data() + r.adj0,
+                          r.nadj, t.coef);
+            continue;
+        }
         // a CONST run's constant is the coefficient itself; a CAUCHY run carries it as its scale
         const uint32_t param = r.mode == TAMD_R_CONST ? gf_mul((uint8_t)r.p, t.coef) : r.p | (uint32_t)t.coef << 8;
         op_accr(r.mode, param, r.off0, r.stride, r.count, t.len, r.col0, 1);
-        --nrun;
     }
     const uint32_t cap = rows_->cap_bytes(dst);
     push_store(instrs_, rows_->offset(dst), len, cap, footer, footer_len);

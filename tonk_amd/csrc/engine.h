@@ -187,7 +187,7 @@ public:
     // the row's 8 lane opcodes, 6 bits each; adj[0..nadj) = (index in the run) << 16 | delta << 8
     // coefficient additions (ADJ words).
     void op_accr_dense(uint32_t row0, uint32_t stride, uint32_t count, uint32_t len, uint32_t col0, uint64_t ops,
-                       uint8_t rx, const uint32_t* adj = nullptr, uint32_t nadj = 0);
+                       uint8_t rx, const uint32_t* adj = nullptr, uint32_t nadj = 0, uint8_t scale = 1);
     // DENSE run for 2-3 rows at once (program.h): target t (COEFS word: lane opcodes `ops`, `rx`;
     // rows i < hi of the run; ADJ additions adj[0..nadj)) accumulates into acc_t.  The op stays a
     // shareable combine when it ends in op_store_shared stores only.
@@ -203,7 +203,18 @@ public:
     // ACCR run scaled by the term's coefficient.  Valid until clear().
     Term run_term(uint32_t mode, uint32_t p, uint32_t off0, uint32_t stride, uint32_t count, uint32_t col0,
                   uint32_t len) {
-        runs_.push_back(RunRef{mode, p, off0, stride, count, col0});
+        runs_.push_back(RunRef{mode, p, off0, stride, count, col0, 0, 0, 0});
+        return Term{kRunFlag | (uint32_t)(runs_.size() - 1), len, 1};
+    }
+    // The same for a Siamese row's dense part over a run of level-0 packets (TAMD_R_DENSE: lane
+    // opcodes `ops`, `rx`, coefficient additions adj[0..nadj) as op_accr_dense takes them): the
+    // decoder's elimination of received originals straight from the packets.  combine() emits it
+    // as one DENSE run scaled by the term's coefficient.
+    Term dense_run_term(uint32_t off0, uint32_t stride, uint32_t count, uint32_t col0, uint64_t ops, uint8_t rx,
+                        const uint32_t* adj, uint32_t nadj, uint32_t len) {
+        const uint32_t at = (uint32_t)run_adj_.size();
+        run_adj_.insert(run_adj_.end(), adj, adj + nadj);
+        runs_.push_back(RunRef{TAMD_R_DENSE, rx, off0, stride, count, col0, ops, at, nadj});
         return Term{kRunFlag | (uint32_t)(runs_.size() - 1), len, 1};
     }
     // STORE (+FOOTER) of acc_0 into dst and close the op (the tail of combine()).
@@ -264,8 +275,9 @@ private:
     uint32_t cur_first_ = 0, cur_span_ = 0, cur_level_in_ = 0, cur_full_ = ~0u, cur_runs_ = 0;
     bool cur_pure_ = true;  // only acc_0 sums and CONST/CAUCHY runs so far (see TAMD_COST_CLASSES)
     bool cur_multi_ = false;  // (pure) multi-target DENSE runs: pure_ value 2
-    struct RunRef { uint32_t mode, p, off0, stride, count, col0; };
+    struct RunRef { uint32_t mode, p, off0, stride, count, col0; uint64_t ops; uint32_t adj0, nadj; };
     std::vector<RunRef> runs_;  // run terms of the pending program
+    std::vector<uint32_t> run_adj_;  // ADJ words of DENSE run terms
     size_t cur_written_begin_ = 0;
     uint64_t acc_bytes_ = 0, store_bytes_ = 0, cur_acc_begin_ = 0;
 };
@@ -523,6 +535,14 @@ struct Context {
     // launch's tail, while per-call programs (the C ABI) and single streams pay an extra level
     // launch in latency and already share a long op across a workgroup.
     uint32_t dense_split = 0;
+    // Decoder eliminations of received originals from Siamese rows straight from the packets
+    // (Decoder::eliminate_direct) where the row's sum range is short and made of long runs, as the
+    // encoder's direct dense ranges; false: always through the decoder's lane sums.
+    bool direct_elim = default_direct_elim();
+    static bool default_direct_elim() {  // (TONK_AMD_DEC_DIRECT=0: A/B against the lanes)
+        static const bool on = !(getenv("TONK_AMD_DEC_DIRECT") && atoi(getenv("TONK_AMD_DEC_DIRECT")) == 0);
+        return on;
+    }
     // Lane-sum snapshots read while a scan is one op long take that op's level (LaneSums::read):
     // per-call programs (the C ABI) flush right after their reads, so their scans stay short and
     // a Siamese recovery row lands one level earlier.

@@ -511,6 +511,8 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
         // round trips of its own coefficient.
         const bool dense = mode == TAMD_R_DENSE;
         const u64 opw = (u64)tg.row | ((u64)(tg.len & 0xffffu) << 32);
+        // DENSE w0 bits 24..31: s > 1 scales every coefficient (a decoder's scaled elimination run)
+        const uint32_t dscale = dense ? a.w0 >> 24 : 0u;
         const PermT prx = perm_at(lds, (dense ? (tg.len >> 16) & 0xffu : a.w0 >> 24) * 8u);
         const uint8_t* sqr = (const uint8_t*)(lds + TAMD_LDS_INV + 64u);
         const uint8_t* inv = (const uint8_t*)(lds + TAMD_LDS_INV);
@@ -542,6 +544,7 @@ __device__ __forceinline__ void run_accr(const tamd_instr& a, const tamd_instr& 
                     if ((d >> 16) >= base + 64u) break;
                     if ((d >> 16) == mine) g ^= (d >> 8) & 0xffu;
                 }
+                if (dscale > 1u) g = mul_sel(sel4(g), perm_at(lds, dscale * 8u)) & 0xffu;
                 gv = g * 8u;
             }
             return perm_at(lds, (uint32_t)__builtin_amdgcn_readlane((int)gv, (int)(i & 63u)));

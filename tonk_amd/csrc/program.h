@@ -29,6 +29,8 @@
 //                 acc_0 ^= (b0 ^ b1*cx ^ b2*cx^2  ^  rx * (b3 ^ b4*cx ^ b5*cx^2)) * row_k
 //                 -- a Siamese row's dense part straight from the packets of its sum range: the
 //                 lane-sum combination the row reads (SiameseEncoder.cpp:1046-1098), without sums
+//                 One target: ACCR w0 bits 24..31 = s > 1 scales every row's coefficient (a decoder's
+//                 elimination of received originals from a Siamese row, scaled by its solve).
 //                 With p = 2 or 3 (ACCR w0 bits 16..23): p targets, each a COEFS word (cap = its
 //                 ADJ words | hi << 16) followed by its ADJ words; target t adds rows k < hi_t
 //                 into acc_t -- rows of nested sum ranges, each packet loaded once for all
