@@ -875,6 +875,11 @@ def main() -> int:
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": round(traffic, 1) if traffic else None,
             "traffic_over_alg": pmc.get("traffic_over_alg") if pmc else None,
+            # the same fraction on the bytes the counters saw move (traffic per timed launch of the
+            # PMC passes over this run's average launch): B_alg charges every received original
+            # to the decoder, which the executor partly reads from L2 / Infinity Cache instead
+            "frac_counters": (round(traffic / (kernel_ms * 1e-3 / launches) / 1e9 / HBM_PEAK_GBS, 4)
+                              if traffic and launches and kernel_ms else None),
             "pmc": pmc,
             "kernel": EXEC_KERNEL,
             "launches": launches,

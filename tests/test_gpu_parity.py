@@ -271,7 +271,8 @@ def test_capi_executor_idle_exit_and_relaunch(golden_index):
     got, err = _capi_transcript(golden_index, name, {"TONK_AMD_SERVE_IDLE_MS": "0.02", "TONK_AMD_CAPI_WATCH": "0.1"})
     want = golden_text(name)
     assert got == want, first_diff(want, got)
-    launches = [int(ln.split("launches=")[1].split()[0]) for ln in err.splitlines() if "server: posted=" in ln]
+    launches = [int(ln.split("launches=")[1].split()[0]) for ln in err.splitlines()
+                if "server: posted=" in ln or "executor stop:" in ln]
     assert launches and max(launches) > 1, err[-2000:]
 
 
@@ -329,3 +330,24 @@ def test_capi_past_column_wrap(golden_index, name):
     text = out.stdout.decode()
     assert text.splitlines()[-1] == e["summary"]
     assert sha256(text) == e["sha256"]
+
+
+def test_capi_ring_passes_a_stalled_post(golden_index, tmp_path):
+    """The executor's ring hands slots on out of order: a poster descheduled between taking its
+    ticket and writing its descriptor (test hook: command 100's poster sleeps 300 ms) holds up
+    only its own command.  Eight threads of codecs keep completing commands behind it, and
+    every stream's transcript still equals the reference codec's."""
+    import hashlib
+    exe = os.path.join(NATIVE, "_build", "capi_gen")
+    entry = golden_index["batches"]["cfg2_64x4096_p2_ack64"]
+    prefix = str(tmp_path / "s")
+    env = dict(os.environ, TONK_AMD_SERVE_STALL_POST_MS="300")
+    out = subprocess.run([exe, "transcripts", prefix, "threads=8", "streams=16", "stream=0"] + entry["args"],
+                         capture_output=True, timeout=600, env=env)
+    err = out.stderr.decode()
+    assert out.returncode == 0, err[-2000:]
+    m = re.search(r"(\d+) commands completed behind the stalled post", err)
+    assert m and int(m.group(1)) > 0, err[-2000:]
+    bad = [s for s in range(16)
+           if hashlib.sha256(open(f"{prefix}{s}.txt", "rb").read()).hexdigest() != entry["streams"][str(s)]["sha256"]]
+    assert not bad, f"streams differing from the reference: {bad}"

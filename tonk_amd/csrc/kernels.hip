@@ -1015,15 +1015,22 @@ extern "C" __global__ void __launch_bounds__(TAMD_SERVE_THREADS) tamd_serve(cons
     tamd_serve_slot* wl = (tamd_serve_slot*)(a.dev + 1);
     if (blockIdx.x == 0) {
         // ---- the dispatcher: one wave ----
-        // Each poll reads slots t .. t + 9 (lane = 6 * slot + granule, lanes 60..63 idle) and
-        // hands on every complete slot from t on: its granules are copied unchanged into the
-        // work list with write-through stores (no fence: the tags are the flags).
+        // Each poll reads ten slots (lane = 6 * slot + granule, lanes 60..63 idle) from t + scan,
+        // t being the first slot not yet handed on, and hands on every complete one among them, in
+        // any order: its granules are copied unchanged into the work list with write-through
+        // stores (no fence: the tags are the flags).  `ahead` marks the slots past t already
+        // handed on, so a poster descheduled between taking its ticket and writing its granules
+        // holds up only its own command: the ones behind it go on (the workers claim work-list
+        // indices in order but wait only on their own entry).  While every slot of the window
+        // but t is handed on, the next poll looks ten slots further (up to 60 past t).
         if (threadIdx.x >= 64) return;
         const uint32_t lane = threadIdx.x, j = lane / TAMD_SERVE_GRANULES, k = lane - TAMD_SERVE_GRANULES * j;
         // (A/B, pad bit 1: one slot per poll)
         const uint32_t width = (a.pad & 2u) ? 1u : 10u;
+        const uint32_t wmask = (1u << width) - 1u;
         const bool mine = lane < width * TAMD_SERVE_GRANULES;
-        u64 t = a.tail0;
+        u64 t = a.tail0, ahead = 0;  // ahead bit i: slot t + i handed on (bit 0 never set)
+        uint32_t scan = 0;
         u64 last = __builtin_amdgcn_s_memrealtime();
         if (lane == 0) st_sys(&a.host->dbg[0], last);
         for (uint32_t polls = 0;; ++polls) {
@@ -1031,20 +1038,37 @@ extern "C" __global__ void __launch_bounds__(TAMD_SERVE_THREADS) tamd_serve(cons
                 st_sys(&a.host->dbg[1], polls >> 10);
                 st_sys(&a.host->dbg[2], t);
             }
-            const u64 ti = t + (mine ? j : 0u);
+            const u64 ti = t + scan + (mine ? j : 0u);
             const u64 gv = ld_sys(&a.ring[ti & a.ring_mask].g[mine ? k : 0u]);
             const u64 okm = ballot(mine && (uint32_t)(gv >> 32) == (uint32_t)(ti + 1));
-            uint32_t n = 0;
-            while (n < width && ((okm >> (TAMD_SERVE_GRANULES * n)) & 0x3full) == 0x3full) ++n;
-            if (n) {
-                if (mine && j < n)
+            uint32_t comp = 0;
+            for (uint32_t n = 0; n < width; ++n)
+                if (((okm >> (TAMD_SERVE_GRANULES * n)) & 0x3full) == 0x3full) comp |= 1u << n;
+            const uint32_t done = (uint32_t)(ahead >> scan) & wmask;
+            const uint32_t fresh = comp & ~done;
+            if (fresh) {
+                if (mine && ((fresh >> j) & 1u))
                     __hip_atomic_store(&wl[ti & a.wl_mask].g[k], gv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ahead |= (u64)fresh << scan;
+                // t moves past the handed-on prefix
+                const uint32_t n = ~ahead ? (uint32_t)__builtin_ctzll(~ahead) : 64u;
+                ahead = n < 64u ? ahead >> n : 0ull;
                 t += n;
-                if (lane == 0) st_sys(&a.host->consumed, t);
+                if (lane == 0 && n) st_sys(&a.host->consumed, t);
                 last = __builtin_amdgcn_s_memrealtime();
+                scan = 0;
                 continue;
             }
-            if (__builtin_amdgcn_s_memrealtime() - last > a.idle_ticks || ld_sys(&a.host->stop)) break;
+            // nothing new here: while the window is handed on but for slot t, look further
+            const uint32_t open = ~done & wmask & (scan ? wmask : wmask & ~1u);
+            if (!open && scan + 2u * width <= 64u) {
+                scan += width;
+                continue;
+            }
+            scan = 0;
+            // (the instance never ends with commands past t handed on: the next one starts at t)
+            if (!ahead && (__builtin_amdgcn_s_memrealtime() - last > a.idle_ticks)) break;
+            if (ld_sys(&a.host->stop)) break;
             __builtin_amdgcn_s_sleep(2);
         }
         // End: the workers drain what was published, then end; the host learns where the next

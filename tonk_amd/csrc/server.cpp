@@ -34,6 +34,7 @@ bool Server::init(Device& dev, unsigned workers, unsigned ring_size, double idle
     workers_ = workers ? workers : 1;
     idle_ticks_ = (uint64_t)(idle_ms * 1e5);  // s_memrealtime: 100 MHz
     if (const char* e = getenv("TONK_AMD_SERVE_DEBUG")) debug_ = (uint32_t)atoi(e);
+    if (const char* e = getenv("TONK_AMD_SERVE_STALL_POST_MS")) stall_post_ms_ = (uint32_t)atoi(e);
     stamps_ = getenv("TONK_AMD_CAPI_WATCH") != nullptr;
     ring_ = (tamd_serve_slot*)coherent_alloc((size_t)ring_size_ * sizeof(tamd_serve_slot));
     host_ = (volatile tamd_serve_host*)coherent_alloc(sizeof(tamd_serve_host));
@@ -244,6 +245,11 @@ void Server::post(CmdBuf& b) {
         b.busy = true;
         return;
     }
+    const bool stall = stall_post_ms_ && idx == 100;
+    if (stall) {  // (test hook: a poster descheduled between its ticket and its descriptor)
+        stall_pending_.store(true);
+        std::this_thread::sleep_for(std::chrono::milliseconds(stall_post_ms_));
+    }
     // six tagged granules, 8-byte stores (each one atomic): the dispatcher takes the slot once
     // every tag is this command's
     const uint64_t cmd = (uint64_t)(uintptr_t)b.cmd(), done = (uint64_t)(uintptr_t)b.done();
@@ -254,6 +260,7 @@ void Server::post(CmdBuf& b) {
     g[3] = tamd_granule(idx, (uint32_t)(done >> 32));
     g[4] = tamd_granule(idx, (uint32_t)(idx + 1));
     g[5] = tamd_granule(idx, b.cmd()->bytes);
+    if (stall) stall_pending_.store(false);
     b.ticket = idx;
     b.busy = true;
     if (stamps_) {
@@ -331,6 +338,7 @@ bool Server::wait(CmdBuf& b) {
         phase_n_++;
     }
     gpu_ns_sum.fetch_add((d[2] - d[1]) * 10, std::memory_order_relaxed);
+    if (stall_post_ms_ && b.ticket > 100 && stall_pending_.load()) stall_passed_.fetch_add(1);
     return true;
 }
 
@@ -354,6 +362,12 @@ std::string Server::phase_report() {
 
 void Server::stop() {
     if (!ring_) return;
+    if (stall_post_ms_)
+        fprintf(stderr, "tonk_amd: %llu commands completed behind the stalled post\n",
+                (unsigned long long)stall_passed_.load());
+    if (stamps_)  // (watchdog: the executor's life at process exit)
+        fprintf(stderr, "tonk_amd: executor stop: posted=%llu launches=%llu\n", (unsigned long long)posted.load(),
+                (unsigned long long)launches.load());
     host_->stop = 1;
     std::atomic_thread_fence(std::memory_order_seq_cst);
     hipStream_t st = (hipStream_t)stream_;

@@ -80,6 +80,12 @@ private:
     uint32_t debug_ = 0;  // TONK_AMD_SERVE_DEBUG bits (diagnostics): 1 the probe's completion words in
                           // the server's own coherent page, 4 a release fence before every completion word
     uint64_t* dbg_done_ = nullptr;
+    // Test hook (TONK_AMD_SERVE_STALL_POST_MS): command 100's poster sleeps this long between
+    // taking its ticket and writing its descriptor; commands completed meanwhile behind it are
+    // counted and reported when the server stops (the ring hands slots on out of order).
+    uint32_t stall_post_ms_ = 0;
+    std::atomic<bool> stall_pending_{false};
+    std::atomic<uint64_t> stall_passed_{0};
     bool stamps_ = false;
     std::mutex stamp_mu_;
     uint64_t phase_ns_[6] = {0, 0, 0, 0, 0, 0}, phase_n_ = 0;
