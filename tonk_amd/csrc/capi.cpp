@@ -1172,7 +1172,7 @@ SIAMESE_EXPORT SiameseResult siamese_decode(SiameseDecoder decoder_t, SiameseOri
     std::vector<StoredOriginal*> outs;
     for (RecoveredPacket* rp : got) {
         StoredOriginal* o = nullptr;
-        if (d->dec->get(rp->packet_num, &o) != kSuccess || !o) { DISABLE(d->dec); return Siamese_Disabled; }
+        if (d->dec->get(rp->packet_num, &o, true) != kSuccess || !o) { DISABLE(d->dec); return Siamese_Disabled; }
         outs.push_back(o);
         if (!o->host) {
             rows.push_back(std::make_pair(o, rp->row));

@@ -1583,9 +1583,9 @@ void Decoder::set_recovered_length(uint32_t packet_num, uint32_t framed_bytes, u
 }
 
 // Decoder::Get (:71-123)
-Result Decoder::get(uint32_t packet_num, StoredOriginal** out) {
+Result Decoder::get(uint32_t packet_num, StoredOriginal** out, bool recovered_now) {
     *out = nullptr;
-    if (disabled_) return kDisabled;
+    if (disabled_ && !recovered_now) return kDisabled;
     const uint32_t e = to_element(packet_num);
     if (invalid_element(e)) return kNeedMoreData;
     const uint32_t id = seg_id(e);

@@ -48,7 +48,10 @@ public:
     Result is_ready();
     // siamese_decode: recovered packets are appended to `out` (increasing packet number).
     Result decode(std::vector<RecoveredPacket*>& out);
-    Result get(uint32_t packet_num, StoredOriginal** out);
+    // `recovered_now`: a packet the decode just returned, looked up even when that decode disabled
+    // the decoder on its way out (its removal step can, SiameseDecoder.cpp:1778-2033): the reference
+    // still hands those packets to the caller (siamese.cpp:257-270, Decoder::Decode).
+    Result get(uint32_t packet_num, StoredOriginal** out, bool recovered_now = false);
     Result ack(uint8_t* buffer, uint32_t limit, uint32_t* used);
     void stats(uint64_t* out, unsigned n);
 
