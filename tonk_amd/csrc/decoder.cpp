@@ -1374,6 +1374,21 @@ bool Decoder::eliminate_direct(Recovery* rec, uint32_t sum_elem, Sym& buf) {
         uint32_t b;
         if (packet((uint32_t)(pr >> 8), row, b)) read_original(row, b < rbytes ? b : rbytes, (uint8_t)pr, buf);
     };
+    // Batched sessions (Context::dense_split) cut the range into chunks of `split` elements from
+    // sum_elem, each one op that stores its partial sum (level 1, a shareable combine) and enters
+    // the row as one term: one work item never walks hundreds of packets (a launch's tail), as
+    // the encoder's chunked dense ranges.  Otherwise each run is one run term of the row.
+    const uint32_t split = ctx_->dense_split;
+    const bool chunked = split && ee - sum_elem > split;
+    ProgramBuilder& pb = ctx_->pb;
+    uint32_t chunk = ~0u;
+    RowId part = kNoRow;
+    auto close_chunk = [&]() {
+        if (part == kNoRow) return;
+        pb.finish_combine(part, rbytes, nullptr, 0);
+        buf.push_back(Term{part, rbytes, 1});
+        part = kNoRow;
+    };
     size_t pi = 0;
     for (const DirectRun& r : drun_) {
         while (pi < dpairs_.size() && (uint32_t)(dpairs_[pi] >> 8) < r.e0) loose_pair(dpairs_[pi++]);
@@ -1384,12 +1399,30 @@ bool Decoder::eliminate_direct(Recovery* rec, uint32_t sum_elem, Sym& buf) {
             if (c) read_original(r.row, r.len, c, buf);
             continue;
         }
-        dadj_.clear();
-        for (; pi < dpairs_.size() && (uint32_t)(dpairs_[pi] >> 8) < r.e0 + r.n; ++pi)
-            dadj_.push_back(((uint32_t)(dpairs_[pi] >> 8) - r.e0) << 16 | (uint32_t)(dpairs_[pi] & 0xffu) << 8);
-        buf.push_back(ctx_->pb.dense_run_term(r.off, r.stride, r.n, r.col, ops, rx, dadj_.data(),
-                                              (uint32_t)dadj_.size(), r.len));
+        for (uint32_t a = r.e0, end = r.e0 + r.n; a < end;) {
+            const uint32_t c = chunked ? (a - sum_elem) / split : 0u;
+            const uint32_t b = chunked ? std::min(end, sum_elem + (c + 1) * split) : end;
+            dadj_.clear();
+            for (; pi < dpairs_.size() && (uint32_t)(dpairs_[pi] >> 8) < b; ++pi)
+                dadj_.push_back(((uint32_t)(dpairs_[pi] >> 8) - a) << 16 | (uint32_t)(dpairs_[pi] & 0xffu) << 8);
+            const uint32_t off = r.off + (a - r.e0) * r.stride, col = col_add(r.col, a - r.e0);
+            if (!chunked) {
+                buf.push_back(pb.dense_run_term(off, r.stride, b - a, col, ops, rx, dadj_.data(),
+                                                (uint32_t)dadj_.size(), r.len));
+            } else {
+                if (c != chunk) {
+                    close_chunk();
+                    part = ctx_->alloc_temp(rbytes);
+                    if (part == kNoRow) return true;  // (ctx_->oom: the caller disables the decoder)
+                    chunk = c;
+                    pb.begin_op();
+                }
+                pb.op_accr_dense(off, r.stride, b - a, r.len, col, ops, rx, dadj_.data(), (uint32_t)dadj_.size());
+            }
+            a = b;
+        }
     }
+    close_chunk();
     while (pi < dpairs_.size()) loose_pair(dpairs_[pi++]);
     (void)singles;
     return true;
