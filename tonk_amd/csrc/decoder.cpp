@@ -297,8 +297,8 @@ Result Decoder::add_original(uint32_t packet_num, RowId row, uint32_t framed_byt
         o.host = host;
         o.run = 0;
         o.stride = 0;
-        if (o.owned || host) s->held++;
-        s->singles++;
+        if (o.owned || host) s->held |= 1ull << bit;
+        s->singles |= 1ull << bit;
     }
     *took = !borrowed;
     s->got_count++;
@@ -520,11 +520,11 @@ void Decoder::remove_elements() {
 
     for (uint32_t i = 0; i < first_kept_sub; ++i) {
         Subwindow* s = subs_[i];
-        if (s->held) {
-            for (unsigned k = 0; k < kSubwindow; ++k) drop_original(s->orig[k]);
-        } else if (s->singles) {
-            memset((void*)s->orig, 0, sizeof(s->orig));  // (nothing to release: borrowed rows)
-        }
+        // only the slots written since the last clear: those holding a row or host copy release
+        // it, every one is zeroed (borrowed rows need no release)
+        for (uint64_t m = s->held; m; m &= m - 1) drop_original(s->orig[__builtin_ctzll(m)]);
+        for (uint64_t m = s->singles | s->held; m; m &= m - 1)
+            memset((void*)&s->orig[__builtin_ctzll(m)], 0, sizeof(StoredOriginal));
         memset(s->seg, 0xff, sizeof(s->seg));
         s->got = 0;
         s->got_count = 0;
@@ -741,7 +741,7 @@ void Decoder::populate_columns(uint32_t old_cols, uint32_t new_cols) {
                 c.orig = &s->orig[bit];
                 c.cx = column_value(c.column);
                 c.orig->column = column;  // lost slot remembers its matrix column
-                s->singles++;
+                s->singles |= 1ull << bit;
                 if (++column >= new_cols) return;
             } while (++bit < kSubwindow);
         }
@@ -1023,8 +1023,8 @@ bool Decoder::add_single_recovery(RowId row, uint32_t data_bytes, const uint8_t*
     o.owned = 1;
     o.run = 0;
     o.stride = 0;
-    subs_[e / kSubwindow]->held++;
-    subs_[e / kSubwindow]->singles++;
+    subs_[e / kSubwindow]->held |= 1ull << (e % kSubwindow);
+    subs_[e / kSubwindow]->singles |= 1ull << (e % kSubwindow);
     *took = true;
 
     if (!has_recovered_) {
@@ -1577,8 +1577,11 @@ bool Decoder::store_recovered(uint32_t ci, Sym& value, uint32_t bytes, bool& ite
     o->owned = 1;
     o->run = 0;
     o->stride = 0;
-    subs_[to_element(o->column) / kSubwindow]->held++;
-    subs_[to_element(o->column) / kSubwindow]->singles++;
+    {
+        const uint32_t e = to_element(o->column);
+        subs_[e / kSubwindow]->held |= 1ull << (e % kSubwindow);
+        subs_[e / kSubwindow]->singles |= 1ull << (e % kSubwindow);
+    }
 
     RecoveredPacket& rp = recovered_[ci];
     rp.packet_num = o->column;

@@ -75,10 +75,10 @@ private:
     struct Subwindow {
         uint64_t got = 0;
         uint32_t got_count = 0;
-        // orig[] slots written with something to release (an owned row or a host copy) since the
-        // subwindow was last cleared; 0: clearing is a plain memset (empty slot = all zero)
-        uint32_t held = 0;
-        uint32_t singles = 0;  // orig[] slots written since the last clear (0: nothing to clear)
+        // bits: orig[] slots written with something to release (an owned row or a host copy) since
+        // the subwindow was last cleared (the others are cleared by zeroing; empty slot = all zero)
+        uint64_t held = 0;
+        uint64_t singles = 0;  // bits: orig[] slots written since the last clear (0: nothing to clear)
         uint32_t seg[kSubwindow];
         StoredOriginal orig[kSubwindow];
         Subwindow() { memset(seg, 0xff, sizeof(seg)); }

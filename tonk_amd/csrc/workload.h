@@ -420,14 +420,15 @@ private:
             return;
         }
         top_ = i0 + k;
-        for (uint32_t j = 0; j < k; ++j) col_of_[i0 + j] = (col0 + j) & 0x3fffffu;
+        // (col_of_ is read only for lost originals, by ARQ: delivered runs do not store theirs)
         s_.originals += k;
         if (be_.dec_add_run(col0, i0, k, len)) {
             memset(&have_[i0], 1, k);
         } else {
             for (uint32_t j = 0; j < k; ++j) {
-                const int ro = be_.dec_add_original(col_of_[i0 + j], i0 + j, len);
-                tr_.on_event('O', ro, col_of_[i0 + j], 0);
+                const uint32_t col = (col0 + j) & 0x3fffffu;
+                const int ro = be_.dec_add_original(col, i0 + j, len);
+                tr_.on_event('O', ro, col, 0);
                 have_[i0 + j] = 1;
                 decode_loop();
             }
@@ -451,15 +452,16 @@ private:
             return;
         }
         top_ = e + 1;
-        for (uint32_t j = 0; j <= k; ++j) col_of_[i0 + j] = (col0 + j) & 0x3fffffu;
+        col_of_[e] = (col0 + k) & 0x3fffffu;  // (ARQ reads the lost ones' only)
         s_.originals += k + 1;
         const uint32_t kd = lost ? k : k + 1;  // delivered
         if (be_.dec_add_run(col0, i0, kd, len)) {
             memset(&have_[i0], 1, kd);
         } else {
             for (uint32_t j = 0; j < kd; ++j) {
-                const int ro = be_.dec_add_original(col_of_[i0 + j], i0 + j, len);
-                tr_.on_event('O', ro, col_of_[i0 + j], 0);
+                const uint32_t col = (col0 + j) & 0x3fffffu;
+                const int ro = be_.dec_add_original(col, i0 + j, len);
+                tr_.on_event('O', ro, col, 0);
                 have_[i0 + j] = 1;
                 decode_loop();
             }
