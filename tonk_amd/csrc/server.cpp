@@ -15,6 +15,13 @@ extern "C" __global__ void tamd_serve(const tamd_serve_args);
 namespace tamd {
 
 namespace {
+std::atomic<int> g_spinners{0};  // callers spinning in Server::wait
+int spinners_max() {  // (TONK_AMD_SPINNERS overrides)
+    // (default: no cap in practice.  Capping at 8 kept Tonk's slow start-ups slow -- they are not
+    // the spinners' doing -- and cost the C ABI bench 16 % with its 16 calling threads)
+    static const int n = getenv("TONK_AMD_SPINNERS") ? atoi(getenv("TONK_AMD_SPINNERS")) : 1024;
+    return n;
+}
 double now_us() {
     return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -109,7 +116,14 @@ bool Server::ensure_running() {
     if (host_->exited_gen != gen_.load()) return true;  // the current instance runs (or a relaunch won)
     dev_->bind_thread();
     const uint64_t tail = host_->exit_tail;
-    if (launch_locked(tail)) return true;
+    const double t0 = now_us();
+    if (launch_locked(tail)) {
+        const double us = now_us() - t0;
+        if (stamps_ && us > 2000.0)  // (watchdog: a relaunch every waiting caller sits behind)
+            fprintf(stderr, "tonk_amd: slow executor relaunch: %.1f ms (launch %llu)\n", us * 1e-3,
+                    (unsigned long long)launches.load());
+        return true;
+    }
     // Nothing will consume the ring: later calls take the launch path, and the waits of commands
     // already posted end at once (their codecs are disabled and keep their buffers).
     fprintf(stderr, "tonk_amd: relaunching the persistent executor failed; using kernel launches\n");
@@ -288,9 +302,24 @@ bool Server::wait(CmdBuf& b) {
         return true;
     }
     const double t0 = now_us();
+    // At most spinners_max() callers spin (and yield) at a time; the others poll with short sleeps
+    // (TONK_AMD_SPINNERS: a bound on the CPU that waiting callers burn in processes with hundreds
+    // of calling threads on a few cores).
+    struct SpinSlot {
+        bool mine;
+        SpinSlot() : mine(g_spinners.fetch_add(1, std::memory_order_relaxed) < spinners_max()) {
+            if (!mine) g_spinners.fetch_sub(1, std::memory_order_relaxed);
+        }
+        ~SpinSlot() { if (mine) g_spinners.fetch_sub(1, std::memory_order_relaxed); }
+    } slot;
     for (uint32_t spin = 1;; ++spin) {
         if (*d == want) break;
         if (dead_.load(std::memory_order_relaxed)) return false;  // (b stays busy: never reused)
+        if (!slot.mine && (spin & 63) != 0) {
+            std::this_thread::sleep_for(std::chrono::microseconds(10));
+            spin |= 63;  // (every poll of a sleeper also takes the checks below)
+            continue;
+        }
         if ((spin & 63) == 0) {
             const double t = now_us() - t0;
             // the executor ended on an idle spell without taking this command: start the next one
