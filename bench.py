@@ -810,6 +810,7 @@ def main() -> int:
     d.barrier()
     sess.set_timing(False)
     kernel_ms, launches = sess.kernel_ms()
+    arena_base, arena_bytes = sess.arena()
     s1 = sess.summary()
     h1 = sess.host_ms()
     # per device program (a quarter of a bench step)
@@ -889,6 +890,8 @@ def main() -> int:
             # gap to alg_bytes is what L2 / Infinity Cache serve
             "op_trace_bytes_per_launch": round(op_trace / launches, 1) if launches else None,
             "device_busy_frac": round((kernel_ms / 1e3) / (t1 - t0), 4),
+            # (placement diagnostics: the executor's launch time differs between processes)
+            "arena": {"base": hex(arena_base), "bytes": arena_bytes, "base_mod_1g": arena_base % (1 << 30)},
             # (with several ranks this object is rank 0's executor; per_gpu holds every rank's)
             "scope": "rank 0" if world > 1 else "the one GPU",
         },

@@ -82,6 +82,8 @@ double tamd_session_kernel_ms(void* s, uint64_t* launches);
    Both: [6] wait for the staging slot        [7] H2D copy enqueue
    [8] longest single H2D enqueue             [9] staging-slot reallocations (count) */
 void  tamd_session_host_ms(void* s, double out[10]);
+/* The session's device arena: base address and mapped bytes (diagnostics: placement studies). */
+void  tamd_session_arena(void* s, uint64_t* base, uint64_t* bytes);
 /* Transcript of one stream in the oracle's text format (record mode). Returns bytes needed. */
 size_t tamd_session_transcript(void* s, uint32_t stream, char* buf, size_t cap);
 void  tamd_session_destroy(void* s);

@@ -63,6 +63,8 @@ def lib() -> ctypes.CDLL:
         L.tamd_session_destroy.argtypes = [vp]
         L.tamd_session_schedule.restype = ctypes.c_int
         L.tamd_session_schedule.argtypes = [vp]
+        L.tamd_session_arena.restype = None
+        L.tamd_session_arena.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]
         L.tamd_session_cpus.restype = ctypes.c_uint
         L.tamd_session_cpus.argtypes = [vp, ctypes.POINTER(ctypes.c_int), ctypes.c_uint]
         L.tamd_cpu_share.restype = ctypes.c_uint
@@ -214,6 +216,12 @@ class Session:
 
     def set_timing(self, on: bool) -> None:
         lib().tamd_session_set_timing(self._h, 1 if on else 0)
+
+    def arena(self) -> tuple[int, int]:
+        """(device base address, mapped bytes) of the session's arena (diagnostics)."""
+        base, n = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        lib().tamd_session_arena(self._h, ctypes.byref(base), ctypes.byref(n))
+        return int(base.value), int(n.value)
 
     def kernel_ms(self) -> tuple[float, int]:
         n = ctypes.c_uint64(0)

@@ -1472,6 +1472,12 @@ void tamd_session_host_ms(void* sp, double out[10]) {
     out[9] = (double)s->dev.stats().slot_reallocs;
 }
 
+void tamd_session_arena(void* sp, uint64_t* base, uint64_t* bytes) {
+    Session* s = (Session*)sp;
+    if (base) *base = (uint64_t)(uintptr_t)s->dev.arena();
+    if (bytes) *bytes = s->dev.arena_bytes();
+}
+
 void tamd_session_destroy(void* sp) { delete (Session*)sp; }
 
 const char* tamd_session_error(void* sp) {
