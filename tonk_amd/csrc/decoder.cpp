@@ -1378,7 +1378,8 @@ bool Decoder::eliminate_direct(Recovery* rec, uint32_t sum_elem, Sym& buf) {
     // sum_elem, each one op that stores its partial sum (level 1, a shareable combine) and enters
     // the row as one term: one work item never walks hundreds of packets (a launch's tail), as
     // the encoder's chunked dense ranges.  Otherwise each run is one run term of the row.
-    const uint32_t split = ctx_->dense_split;
+    static const int split_env = getenv("TONK_AMD_DEC_SPLIT") ? atoi(getenv("TONK_AMD_DEC_SPLIT")) : -1;  // (A/B)
+    const uint32_t split = split_env >= 0 && ctx_->dense_split ? (uint32_t)split_env : ctx_->dense_split;
     const bool chunked = split && ee - sum_elem > split;
     ProgramBuilder& pb = ctx_->pb;
     uint32_t chunk = ~0u;
