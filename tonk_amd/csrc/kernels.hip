@@ -1182,12 +1182,14 @@ extern "C" __global__ void __launch_bounds__(TAMD_SERVE_THREADS) tamd_serve(cons
         u64 pk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         if (upc) {
             const u64 upb = ((u64)uniform((uint32_t)(sh_upb >> 32)) << 32) | uniform((uint32_t)sh_upb);
+            // (only chunks that exist: each is a host read over PCIe)
 #pragma unroll
-            for (uint32_t q = 0; q < 4; ++q) {
-                const uint64_t* s8 = (const uint64_t*)(upb + 16ull * min(tid + q * TAMD_SERVE_THREADS, upc - 1u));
-                pk[2 * q] = ld_sys(s8);
-                pk[2 * q + 1] = ld_sys(s8 + 1);
-            }
+            for (uint32_t q = 0; q < 4; ++q)
+                if (tid + q * TAMD_SERVE_THREADS < upc) {
+                    const uint64_t* s8 = (const uint64_t*)(upb + 16ull * (tid + q * TAMD_SERVE_THREADS));
+                    pk[2 * q] = ld_sys(s8);
+                    pk[2 * q + 1] = ld_sys(s8 + 1);
+                }
         }
         // 1. the command into LDS (8-byte system-scope loads: they bypass the L1, whose invalidation
         // runs meanwhile)
