@@ -1178,7 +1178,7 @@ extern "C" __global__ void __launch_bounds__(TAMD_SERVE_THREADS) tamd_serve(cons
         // 0. the staged packets' first 4 x 1024 chunks start loading now, in the same round trip as
         // the command (8-byte system-scope loads, past the L1 being invalidated); they land in
         // their rows once the command -- which names the rows -- is in LDS (step 2)
-        const uint32_t upc = uniform(sh_upc);
+        const uint32_t upc = (a.pad & 16u) ? 0u : uniform(sh_upc);  // (pad bit 4: no early loads, A/B)
         u64 pk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
         if (upc) {
             const u64 upb = ((u64)uniform((uint32_t)(sh_upb >> 32)) << 32) | uniform((uint32_t)sh_upb);

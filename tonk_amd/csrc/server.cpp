@@ -98,7 +98,7 @@ bool Server::launch_locked(uint64_t tail0) {
     a.gen = gen_.load() + 1;
     // (A/B bits of TONK_AMD_SERVE_DEBUG >> 2: 1 no release fence before the completion word,
     // 2 the dispatcher polls one slot at a time, 4 commands copied with plain 16-byte loads,
-    // 8 reads stored with system-scope 8-byte stores)
+    // 8 reads stored with system-scope 8-byte stores, 16 the staged packets loaded only after the command)
     a.pad = debug_ >> 2;
     // the instance's claim counter and quit flag start from zero (stream order: after the
     // previous instance has ended)
@@ -399,8 +399,8 @@ void Server::stop() {
         fprintf(stderr, "tonk_amd: %llu commands completed behind the stalled post\n",
                 (unsigned long long)stall_passed_.load());
     if (stamps_)  // (watchdog: the executor's life at process exit)
-        fprintf(stderr, "tonk_amd: executor stop: posted=%llu launches=%llu\n", (unsigned long long)posted.load(),
-                (unsigned long long)launches.load());
+        fprintf(stderr, "tonk_amd: executor stop: posted=%llu launches=%llu; %s\n", (unsigned long long)posted.load(),
+                (unsigned long long)launches.load(), phase_report().c_str());
     host_->stop = 1;
     std::atomic_thread_fence(std::memory_order_seq_cst);
     hipStream_t st = (hipStream_t)stream_;
