@@ -1015,18 +1015,18 @@ extern "C" __global__ void __launch_bounds__(TAMD_SERVE_THREADS) tamd_serve(cons
     tamd_serve_slot* wl = (tamd_serve_slot*)(a.dev + 1);
     if (blockIdx.x == 0) {
         // ---- the dispatcher: one wave ----
-        // Each poll reads eight slots (lane = 8 * slot + granule) from t + scan,
+        // Each poll reads ten slots (lane = 6 * slot + granule, lanes 60..63 idle) from t + scan,
         // t being the first slot not yet handed on, and hands on every complete one among them, in
         // any order: its granules are copied unchanged into the work list with write-through
         // stores (no fence: the tags are the flags).  `ahead` marks the slots past t already
         // handed on, so a poster descheduled between taking its ticket and writing its granules
         // holds up only its own command: the ones behind it go on (the workers claim work-list
         // indices in order but wait only on their own entry).  While every slot of the window
-        // but t is handed on, the next poll looks eight slots further (up to 56 past t).
+        // but t is handed on, the next poll looks ten slots further (up to 60 past t).
         if (threadIdx.x >= 64) return;
         const uint32_t lane = threadIdx.x, j = lane / TAMD_SERVE_GRANULES, k = lane - TAMD_SERVE_GRANULES * j;
         // (A/B, pad bit 1: one slot per poll)
-        const uint32_t width = (a.pad & 2u) ? 1u : 64u / TAMD_SERVE_GRANULES;
+        const uint32_t width = (a.pad & 2u) ? 1u : 10u;
         const uint32_t wmask = (1u << width) - 1u;
         const bool mine = lane < width * TAMD_SERVE_GRANULES;
         u64 t = a.tail0, ahead = 0;  // ahead bit i: slot t + i handed on (bit 0 never set)
@@ -1043,7 +1043,7 @@ extern "C" __global__ void __launch_bounds__(TAMD_SERVE_THREADS) tamd_serve(cons
             const u64 okm = ballot(mine && (uint32_t)(gv >> 32) == (uint32_t)(ti + 1));
             uint32_t comp = 0;
             for (uint32_t n = 0; n < width; ++n)
-                if (((okm >> (TAMD_SERVE_GRANULES * n)) & 0xffull) == 0xffull) comp |= 1u << n;
+                if (((okm >> (TAMD_SERVE_GRANULES * n)) & 0x3full) == 0x3full) comp |= 1u << n;
             const uint32_t done = (uint32_t)(ahead >> scan) & wmask;
             const uint32_t fresh = comp & ~done;
             if (fresh) {
@@ -1088,8 +1088,8 @@ extern "C" __global__ void __launch_bounds__(TAMD_SERVE_THREADS) tamd_serve(cons
     constexpr uint32_t SLICE = 64u * 8u * NH, MAIN = 1024u;
     __shared__ __attribute__((aligned(16))) uint32_t lds_perm[TAMD_GF_DWORDS];
     __shared__ __attribute__((aligned(16))) uint4 cbuf[TAMD_SERVE_CMD_BYTES / 16];
-    __shared__ u64 sh_cmd, sh_upb;
-    __shared__ uint32_t sh_state, sh_bytes, sh_item, sh_upc;
+    __shared__ u64 sh_cmd;
+    __shared__ uint32_t sh_state, sh_bytes, sh_item;
     __shared__ LV<3> partial[TAMD_SERVE_WAVES][64];  // grouped levels: each wave's acc_0
     const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = uniform(tid >> 6);
     for (uint32_t i = tid; i < TAMD_GF_DWORDS / 4; i += TAMD_SERVE_THREADS)
@@ -1150,14 +1150,12 @@ extern "C" __global__ void __launch_bounds__(TAMD_SERVE_THREADS) tamd_serve(cons
             if (st) {
                 const uint32_t v = (uint32_t)gv;
                 prev_done = ((u64)uniform(rdl(v, 3)) << 32) | uniform(rdl(v, 2));
-                prev_val = tag;
+                prev_val = uniform(rdl(v, 4));
                 prev_start = __builtin_amdgcn_s_memrealtime();
                 prev_dbg = idx == 0;
                 if (lane == 0) {
                     sh_cmd = ((u64)rdl(v, 1) << 32) | rdl(v, 0);
                     sh_bytes = rdl(v, 5);
-                    sh_upc = rdl(v, 4);
-                    sh_upb = ((u64)rdl(v, 7) << 32) | rdl(v, 6);
                 }
                 // this CU's L1 drops lines another CU may have rewritten since (the codec's rows);
                 // it completes while the command is copied (through uncached loads) and is waited
@@ -1175,22 +1173,6 @@ extern "C" __global__ void __launch_bounds__(TAMD_SERVE_THREADS) tamd_serve(cons
         if (dbg) st_sys(&a.host->dbg[3], 2);
         const u64 cmd_addr = ((u64)uniform((uint32_t)(sh_cmd >> 32)) << 32) | uniform((uint32_t)sh_cmd);
         const uint32_t cmd_bytes = uniform(sh_bytes);
-        // 0. the staged packets' first 4 x 1024 chunks start loading now, in the same round trip as
-        // the command (8-byte system-scope loads, past the L1 being invalidated); they land in
-        // their rows once the command -- which names the rows -- is in LDS (step 2)
-        const uint32_t upc = (a.pad & 16u) ? 0u : uniform(sh_upc);  // (pad bit 4: no early loads, A/B)
-        u64 pk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (upc) {
-            const u64 upb = ((u64)uniform((uint32_t)(sh_upb >> 32)) << 32) | uniform((uint32_t)sh_upb);
-            // (only chunks that exist: each is a host read over PCIe)
-#pragma unroll
-            for (uint32_t q = 0; q < 4; ++q)
-                if (tid + q * TAMD_SERVE_THREADS < upc) {
-                    const uint64_t* s8 = (const uint64_t*)(upb + 16ull * (tid + q * TAMD_SERVE_THREADS));
-                    pk[2 * q] = ld_sys(s8);
-                    pk[2 * q + 1] = ld_sys(s8 + 1);
-                }
-        }
         // 1. the command into LDS (8-byte system-scope loads: they bypass the L1, whose invalidation
         // runs meanwhile)
         if (a.pad & 4u) {
@@ -1240,15 +1222,8 @@ extern "C" __global__ void __launch_bounds__(TAMD_SERVE_THREADS) tamd_serve(cons
             const uint32_t m = up_chunks - 1u;
             for (uint32_t b = tid; b < up_chunks; b += 4u * T) {
                 uint4 v[4];
-                if (b == tid && up_chunks == upc) {  // (loaded in step 0)
 #pragma unroll
-                    for (uint32_t q = 0; q < 4; ++q)
-                        v[q] = make_uint4((uint32_t)pk[2 * q], (uint32_t)(pk[2 * q] >> 32), (uint32_t)pk[2 * q + 1],
-                                          (uint32_t)(pk[2 * q + 1] >> 32));
-                } else {
-#pragma unroll
-                    for (uint32_t q = 0; q < 4; ++q) v[q] = *(const uint4*)(base + 16ull * min(b + q * T, m));
-                }
+                for (uint32_t q = 0; q < 4; ++q) v[q] = *(const uint4*)(base + 16ull * min(b + q * T, m));
 #pragma unroll
                 for (uint32_t q = 0; q < 4; ++q) {
                     const uint32_t ch = b + q * T;

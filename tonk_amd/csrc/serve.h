@@ -17,17 +17,16 @@
 #define TAMD_SERVE_CMD_BYTES (64u << 10)  /* LDS area one command fits in (else: launch path) */
 #define TAMD_SERVE_MAX_LEVELS 32u
 
-/* A command's descriptor is 8 tagged granules, each one 8-byte word {tag = low 32 bits of
-   index + 1, value}: 0/1 the command's host address (low/high half), 2/3 the completion word's
-   (the worker stores the tag there), 4 the command's up_chunks (tamd_cmd), 5 the command's bytes,
-   6/7 the host address of its first upload -- so a worker starts loading the staged packets in
-   the same round trip as the command itself.  The host writes them into the ring slot with
-   8-byte stores in any order; the dispatcher copies them unchanged into the device work list with
-   write-through stores; a reader takes a descriptor once all eight tags match -- the data is the
-   flag, no fence on either hand-off (MI355X_MICROARCH.md, R2). */
-#define TAMD_SERVE_GRANULES 8u
+/* A command's descriptor is 6 tagged granules, each one 8-byte word {tag = low 32 bits of
+   index + 1, value}: 0/1 the command's host address (low/high half), 2/3 the completion word's,
+   4 the value the worker stores there (the tag), 5 the command's bytes.  The host writes them
+   into the ring slot with 8-byte stores in any order; the dispatcher copies them unchanged into
+   the device work list with write-through stores; a reader takes a descriptor once all six tags
+   match -- the data is the flag, no fence on either hand-off (MI355X_MICROARCH.md, R2). */
+#define TAMD_SERVE_GRANULES 6u
 typedef struct tamd_serve_slot {  /* host ring slot and device work-list entry, 64 B */
     uint64_t g[TAMD_SERVE_GRANULES];
+    uint64_t pad[2];
 } tamd_serve_slot;
 static inline uint64_t tamd_granule(uint64_t index, uint32_t value) {
     return ((uint64_t)(uint32_t)(index + 1) << 32) | value;

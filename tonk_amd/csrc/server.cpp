@@ -98,7 +98,7 @@ bool Server::launch_locked(uint64_t tail0) {
     a.gen = gen_.load() + 1;
     // (A/B bits of TONK_AMD_SERVE_DEBUG >> 2: 1 no release fence before the completion word,
     // 2 the dispatcher polls one slot at a time, 4 commands copied with plain 16-byte loads,
-    // 8 reads stored with system-scope 8-byte stores, 16 the staged packets loaded only after the command)
+    // 8 reads stored with system-scope 8-byte stores)
     a.pad = debug_ >> 2;
     // the instance's claim counter and quit flag start from zero (stream order: after the
     // previous instance has ended)
@@ -267,17 +267,13 @@ void Server::post(CmdBuf& b) {
     // six tagged granules, 8-byte stores (each one atomic): the dispatcher takes the slot once
     // every tag is this command's
     const uint64_t cmd = (uint64_t)(uintptr_t)b.cmd(), done = (uint64_t)(uintptr_t)b.done();
-    const tamd_cmd* c = b.cmd();
-    const uint64_t up0 = c->up_chunks ? ((const tamd_xfer*)((const uint8_t*)c + c->off_up))[0].host : 0;
     volatile uint64_t* g = s->g;
     g[0] = tamd_granule(idx, (uint32_t)cmd);
     g[1] = tamd_granule(idx, (uint32_t)(cmd >> 32));
     g[2] = tamd_granule(idx, (uint32_t)done);
     g[3] = tamd_granule(idx, (uint32_t)(done >> 32));
-    g[4] = tamd_granule(idx, c->up_chunks);
-    g[5] = tamd_granule(idx, c->bytes);
-    g[6] = tamd_granule(idx, (uint32_t)up0);
-    g[7] = tamd_granule(idx, (uint32_t)(up0 >> 32));
+    g[4] = tamd_granule(idx, (uint32_t)(idx + 1));
+    g[5] = tamd_granule(idx, b.cmd()->bytes);
     if (stall) stall_pending_.store(false);
     b.ticket = idx;
     b.busy = true;
