@@ -271,8 +271,8 @@ def test_capi_executor_idle_exit_and_relaunch(golden_index):
     got, err = _capi_transcript(golden_index, name, {"TONK_AMD_SERVE_IDLE_MS": "0.02", "TONK_AMD_CAPI_WATCH": "0.1"})
     want = golden_text(name)
     assert got == want, first_diff(want, got)
-    launches = [int(ln.split("launches=")[1].split()[0]) for ln in err.splitlines()
-                if "server: posted=" in ln or "executor stop:" in ln]
+    launches = [int(m.group(1)) for ln in err.splitlines() if "server: posted=" in ln or "executor stop:" in ln
+                for m in [re.search(r"launches=(\d+)", ln)] if m]
     assert launches and max(launches) > 1, err[-2000:]
 
 
