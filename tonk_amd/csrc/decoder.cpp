@@ -1349,17 +1349,28 @@ bool Decoder::eliminate_direct(Recovery* rec, uint32_t sum_elem, Sym& buf) {
         drun_.clear();
         return false;
     }
-    // LDPC pairs (element << 8 | coefficient), sorted: those on a run's packets become its ADJ
-    // additions, the others are read as rows (only when the element has data)
+    // LDPC pairs (element << 8 | coefficient): those on a run's packets become its ADJ additions
+    // (sorted), the others are read as rows (only when the element has data).  The pairs span the
+    // row's whole unacknowledged window, mostly wider than the sum range: the ones outside it are
+    // read right away and only the rest are sorted.
     const uint8_t rx = row_value(m.Row);
+    auto loose_pair = [&](uint64_t pr) {
+        RowId row;
+        uint32_t b;
+        if (packet((uint32_t)(pr >> 8), row, b)) read_original(row, b < rbytes ? b : rbytes, (uint8_t)pr, buf);
+    };
     Pcg32 prng;
     prng.seed(m.Row, m.LDPCCount);
     const uint32_t pairs = (m.LDPCCount + kPairRate - 1) / kPairRate;
     const FastMod ldpc_mod(m.LDPCCount);
-    dpairs_.resize(2 * (size_t)pairs);
-    for (uint32_t i = 0; i < pairs; ++i) {
-        dpairs_[2 * i] = (uint64_t)(es + ldpc_mod(prng.next())) << 8 | 1u;
-        dpairs_[2 * i + 1] = (uint64_t)(es + ldpc_mod(prng.next())) << 8 | rx;
+    const uint32_t span0 = drun_.empty() ? 0u : drun_.front().e0;
+    const uint32_t span1 = drun_.empty() ? 0u : drun_.back().e0 + (drun_.back().n ? drun_.back().n : 1u);
+    dpairs_.clear();
+    for (uint32_t i = 0; i < 2 * pairs; ++i) {
+        const uint64_t pr = (uint64_t)(es + ldpc_mod(prng.next())) << 8 | (i & 1u ? rx : 1u);
+        const uint32_t e = (uint32_t)(pr >> 8);
+        if (e >= span0 && e < span1) dpairs_.push_back(pr);
+        else loose_pair(pr);
     }
     std::sort(dpairs_.begin(), dpairs_.end());
     uint64_t ops = 0;
@@ -1369,11 +1380,6 @@ bool Decoder::eliminate_direct(Recovery* rec, uint32_t sum_elem, Sym& buf) {
         ops |= (uint64_t)op << (6 * l);
         opcode_coefs(op, rx, lk[l]);
     }
-    auto loose_pair = [&](uint64_t pr) {
-        RowId row;
-        uint32_t b;
-        if (packet((uint32_t)(pr >> 8), row, b)) read_original(row, b < rbytes ? b : rbytes, (uint8_t)pr, buf);
-    };
     // Batched sessions (Context::dense_split) cut the range into chunks of `split` elements from
     // sum_elem, each one op that stores its partial sum (level 1, a shareable combine) and enters
     // the row as one term: one work item never walks hundreds of packets (a launch's tail), as
