@@ -702,7 +702,7 @@ def main() -> int:
                     help="BASELINE.json configs[] index: cfg3 (the headline, 64 streams per GPU), cfg2 (64 "
                          "streams, 2%% loss), cfg1 / cfg4 (one stream, start to finish)")
     ap.add_argument("--step", type=int, default=0,
-                    help="cfg1 / cfg4: originals per device program (default 4096 for cfg1, 512 for cfg4)")
+                    help="cfg1 / cfg4: originals per device program (default ORIGINALS_PER_STEP, 4096: the best of the 256..4096 sweep in profiles/r06_single_step_sweep.txt for both)")
     ap.add_argument("--dry-run", action="store_true",
                     help="form the ranks and print the shard plan without touching a GPU (tests)")
     a = ap.parse_args()

@@ -23,6 +23,8 @@ void ref_decomp_free(void* d);
 static uint32_t rng_state = 1;
 static bool g_huffman = true;
 static uint32_t g_minmatch = 4;
+static bool g_fitted = true;  // block-fitted sequence tables (tamd_seq_choose)
+static unsigned fitted_tables[3] = {0, 0, 0}, rle_tables[3] = {0, 0, 0};
 static unsigned huffman_blocks = 0;
 static uint64_t lit_bytes = 0, seq_bytes = 0, n_seqs = 0, lit_small = 0;
 static double est_fitted = 0;  // estimated bytes of the sequence streams with block-fitted tables
@@ -37,6 +39,7 @@ int main(int argc, char** argv) {
     rng_state = argc > 2 ? (uint32_t)atoi(argv[2]) : 1;
     g_huffman = argc > 3 ? atoi(argv[3]) != 0 : true;
     g_minmatch = argc > 4 ? (uint32_t)atoi(argv[4]) : 4;
+    g_fitted = argc > 5 ? atoi(argv[5]) != 0 : true;
     const unsigned kMax = 1300, kDict = 24000;
     uint8_t fse[TAMD_FSE_BYTES];
     tamd_fse_blob(fse);
@@ -168,12 +171,43 @@ int main(int argc, char** argv) {
                 w += lits;
             }
             const uint32_t hs = tamd_seq_header((uint32_t)lo.size(), h);
+            // the block's tables: codes packed as the kernel packs them
+            tamd_seq_tables tt;
+            std::vector<uint32_t> codes(lo.size());
+            for (size_t q = 0; q < lo.size(); ++q)
+                codes[q] = tamd_ll_code(lo[q] & 0xffffu) | (tamd_ml_code(lo[q] >> 16) << 8) |
+                           ((31u - (uint32_t)__builtin_clz(off[q] + 3u)) << 16);
+            uint32_t dl = 0;
+            if (g_fitted) {
+                dl = tamd_seq_choose(codes.data(), (uint32_t)codes.size(), fse, &tt);
+                h[hs - 1] = (uint8_t)tamd_modes_byte(tt.mode);
+                for (uint32_t k = 0; k < 3; ++k) {
+                    if (tt.mode[k] == TAMD_MODE_FSE) ++fitted_tables[k];
+                    if (tt.mode[k] == TAMD_MODE_RLE) ++rle_tables[k];
+                }
+            }
             memcpy(&out[w], h, hs);
             w += hs;
+            if (g_fitted) {
+                const uint32_t order[3] = {0u, 2u, 1u};  // descriptions: LL, OF, ML
+                for (uint32_t k : order) {
+                    memcpy(&out[w], tt.desc[k], tt.desc_len[k]);
+                    w += tt.desc_len[k];
+                }
+            }
             if (w < n - 1) {
-                const uint32_t nb = tamd_fse_sequences(lo.data(), off.data(), (uint32_t)lo.size(), fse, &out[w],
-                                                       n - 1 - w);
-                seq_bytes += nb + hs;
+                const uint32_t nb = tamd_fse_sequences_t(lo.data(), off.data(), (uint32_t)lo.size(), fse,
+                                                         g_fitted ? &tt : nullptr, &out[w], n - 1 - w);
+                if (!g_fitted) {  // the packed-map writer agrees with the table writer
+                    std::vector<uint8_t> alt(n);
+                    const uint32_t nb2 = tamd_fse_sequences(lo.data(), off.data(), (uint32_t)lo.size(), fse, alt.data(),
+                                                            n - 1 - w);
+                    if (nb2 != nb || memcmp(alt.data(), &out[w], nb) != 0) {
+                        printf("sequence writers differ at message %u\n", k);
+                        return 1;
+                    }
+                }
+                seq_bytes += nb + hs + dl;
                 {  // entropy of the three code streams per block + the same extra bits + ~8 B of table headers each
                     uint32_t hl[64] = {0}, hm[64] = {0}, ho[32] = {0};
                     double extra = 0;
@@ -217,6 +251,8 @@ int main(int argc, char** argv) {
     fprintf(stderr, "literal bytes %llu (in Huffman-able sections %llu), sequences %llu in %llu bytes\n",
             (unsigned long long)lit_bytes, (unsigned long long)lit_small, (unsigned long long)n_seqs,
             (unsigned long long)seq_bytes);
+    fprintf(stderr, "fitted tables LL/ML/OF %u/%u/%u, RLE %u/%u/%u\n", fitted_tables[0], fitted_tables[1],
+            fitted_tables[2], rle_tables[0], rle_tables[1], rle_tables[2]);
     printf("ok %u/%u compressed (%u with Huffman literals), %llu -> %llu bytes\n", compressed, n_msgs,
            huffman_blocks, (unsigned long long)total_in, (unsigned long long)total_out);
     return 0;

@@ -137,13 +137,18 @@ def test_reference_msgcodec_roundtrip():
 
 
 def test_block_writer_decodes_with_reference_zstd():
-    """The block writer shared by the kernel (lz.h) against the reference's zstd decoder."""
+    """The block writer shared by the kernel (lz.h) against the reference's zstd decoder: with
+    block-fitted / RLE sequence tables (tamd_seq_choose, the kernel's choice), and with the
+    predefined tables only (where the table writer must also equal the packed-map writer)."""
     ref_lib()
     _make(NATIVE, "_build/lz_check")
     exe = os.path.join(NATIVE, "_build", "lz_check")
     for seed in (1, 2, 3):
-        r = subprocess.run([exe, "300", str(seed)], capture_output=True, text=True, timeout=120)
-        assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout + r.stderr
+        for extra in ([], ["0", "4", "0"]):
+            r = subprocess.run([exe, "300", str(seed)] + extra, capture_output=True, text=True, timeout=120)
+            assert r.returncode == 0 and r.stdout.startswith("ok"), r.stdout + r.stderr
+            if not extra:
+                assert "fitted tables LL/ML/OF 0/0/0," not in r.stderr, r.stderr
 
 
 def test_compress_abi_exports_and_no_cpu_fallback():

@@ -212,9 +212,10 @@ void watch_loop(double period_s) {
                     st->ns.load() * 1e-6, h.c_str());
         }
         if (g_srv)
-            fprintf(stderr, "[tonk_amd capi]   server: posted=%llu launches=%llu slow_waits=%llu gpu_ms=%.1f\n",
+            fprintf(stderr, "[tonk_amd capi]   server: posted=%llu launches=%llu parked_waits=%llu slow_waits=%llu gpu_ms=%.1f\n",
                     (unsigned long long)g_srv->posted.load(), (unsigned long long)g_srv->launches.load(),
-                    (unsigned long long)g_srv->waits_slow.load(), g_srv->gpu_ns_sum.load() * 1e-6);
+                    (unsigned long long)g_srv->waits_parked.load(), (unsigned long long)g_srv->waits_slow.load(),
+                    g_srv->gpu_ns_sum.load() * 1e-6);
         if (g_srv) fprintf(stderr, "[tonk_amd capi]   server phases: %s\n", g_srv->phase_report().c_str());
         dump_encoders();
     }

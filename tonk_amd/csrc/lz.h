@@ -3,6 +3,7 @@
 // (RFC 8878 s3.1.1.3.2.1.1, the literal-length and match-length codes; offsets are coded as
 // Offset_Value = offset + 3, code = highbit(Offset_Value), value bits = the rest).
 #pragma once
+#include <math.h>
 #include <stdint.h>
 
 #define TAMD_LZ_MAX_MESSAGE 2048u  // messages up to this size are compressed entirely in LDS
@@ -67,7 +68,12 @@ uint32_t tamd_lz_scratch_bytes(uint32_t n) {
 #define TAMD_FSE_ML_E16 (36u * 64u)
 #define TAMD_FSE_OF_E16 (TAMD_FSE_ML_E16 + 53u * 64u)
 #define TAMD_FSE_E16_WORDS (TAMD_FSE_OF_E16 + 29u * 32u)
-#define TAMD_FSE_BYTES (TAMD_FSE_E16 + 2u * TAMD_FSE_E16_WORDS)
+// Symbol costs in 1/16 bit for choosing each block's table (tamd_seq_choose): the predefined
+// distributions' per symbol (64 bytes per table: LL, ML, OF; 0 past the last symbol), and a
+// block-fitted table's by normalized count 0..32.
+#define TAMD_FSE_PCOST (TAMD_FSE_E16 + 2u * TAMD_FSE_E16_WORDS)
+#define TAMD_FSE_FCOST (TAMD_FSE_PCOST + 3u * 64u)
+#define TAMD_FSE_BYTES (TAMD_FSE_FCOST + 64u)
 
 #ifdef __HIPCC__
 #define TAMD_HD __host__ __device__
@@ -246,6 +252,250 @@ TAMD_HD static inline uint32_t tamd_fse_sequences(const uint32_t* seq_lo, const 
     return over ? 0 : pos;
 }
 
+// ---- Block-fitted sequence tables (RFC 8878 s3.1.1.3.2.1.2: RLE_Mode, FSE_Compressed_Mode) -----
+// A block may replace each of the three predefined distributions by one fitted to its own codes:
+// RLE (every sequence has the same code: one byte, no state bits) or an FSE table described in
+// the block (s4.1.1, as zstd's FSE_readNCount reads it, entropy_common.c:61-155), which the
+// decoder builds as ZSTD_buildFSETable does (zstd_decompress.c:804-863, the spread of
+// tamd_build_fse).  Fitted tables here have accuracy log 5 (32 states, the format's minimum):
+// on Tonk-like messages (tens of sequences per block) a finer table never paid for its longer
+// description.  No table is ever "repeat" mode, so blocks still carry no entropy state.
+#define TAMD_FIT_LOG 5u
+#define TAMD_FIT_SIZE 32u
+#define TAMD_FIT_STEP 23u      // (32 >> 1) + (32 >> 3) + 3, FSE_TABLESTEP
+#define TAMD_FIT_STEP_INV 7u   // 23 * 7 = 1 (mod 32): the spread slot of state u is (u * 7) & 31
+#define TAMD_MODE_PREDEF 0u
+#define TAMD_MODE_RLE 1u
+#define TAMD_MODE_FSE 2u
+#define TAMD_FIT_DESC 48u      // description bytes per table (a 53-symbol table needs at most 45)
+
+// Normalized count of a symbol seen `count` of `total` times: the nearest share of the 32 states,
+// at least one for a present symbol.  The sum is brought to exactly 32 on the largest share
+// (lowest symbol on ties), which must stay >= 1 (else no fitted table).
+TAMD_HD static inline uint32_t tamd_fit_norm(uint32_t count, uint32_t total) {
+    if (!count) return 0;
+    const uint32_t n = (2u * TAMD_FIT_SIZE * count + total) / (2u * total);
+    return n ? n : 1u;
+}
+
+// One symbol's field in the table description (s4.1.1): the value count + 1 in a width set by
+// the states not yet given out ("remaining" = 33 - cum, cum = the counts of the symbols before
+// it); a zero count is followed by 2-bit repeat flags for the zero counts after it (3 = three
+// more and continue).  A zero inside such a run writes nothing itself.  `lead` = first symbol or
+// the previous one's count was not zero; `zeros_after` = zero counts following a zero.  Returns
+// the width in bits (<= 44) and the bits in *v (first bit = least significant).
+TAMD_HD static inline uint32_t tamd_ncount_item(uint32_t n, uint32_t cum, bool lead, uint32_t zeros_after,
+                                               uint64_t* v) {
+    *v = 0;
+    if (n == 0 && !lead) return 0;
+    const uint32_t R = TAMD_FIT_SIZE + 1u - cum;
+    const uint32_t hb = 31u - (uint32_t)__builtin_clz(R);
+    const uint32_t T = 1u << hb, nb = hb + 1u, mx = 2u * T - 1u - R;
+    uint32_t x = n + 1u;
+    if (x >= T) x += mx;
+    uint32_t w = nb - (x < mx ? 1u : 0u);
+    uint64_t val = x;
+    if (n == 0) {
+        const uint32_t q = zeros_after / 3u;
+        const uint64_t flags = ((1ull << (2u * q)) - 1ull) | ((uint64_t)(zeros_after % 3u) << (2u * q));
+        val |= flags << w;
+        w += 2u * q + 2u;
+    }
+    *v = val;
+    return w;
+}
+
+// The encoder's view of a fitted table (FSE_buildCTable_wksp, fse_compress.c:85-170, restated):
+// cum[s] = states of the symbols before s; state[cum[s] + k] = the k-th state (ascending) that
+// decodes s -- the one the decoder reaches with next-state value norm[s] + k.
+TAMD_HD static inline void tamd_fit_states(const uint8_t* norm, uint32_t nsym, uint8_t* cum, uint8_t* state) {
+    uint8_t sym[TAMD_FIT_SIZE];
+    uint8_t rank[64];
+    uint32_t c = 0, pos = 0;
+    for (uint32_t s = 0; s < nsym; ++s) {
+        cum[s] = (uint8_t)c;
+        rank[s] = 0;
+        c += norm[s];
+        for (uint32_t i = 0; i < norm[s]; ++i) {
+            sym[pos] = (uint8_t)s;
+            pos = (pos + TAMD_FIT_STEP) & (TAMD_FIT_SIZE - 1u);
+        }
+    }
+    for (uint32_t u = 0; u < TAMD_FIT_SIZE; ++u) {
+        const uint32_t s = sym[u];
+        state[cum[s] + rank[s]++] = (uint8_t)u;
+    }
+}
+
+// One step of a fitted table's state chain (FSE_encodeSymbol): the decoder must reach state `st`
+// after the symbol (norm n, cum c); returns the state that decodes it, *upd = the bits the decoder
+// reads to get from there to `st` | their number << 8.
+TAMD_HD static inline uint32_t tamd_fit_step(uint32_t n, uint32_t c, const uint8_t* state, uint32_t st, uint32_t* upd) {
+    const uint32_t S = TAMD_FIT_SIZE + st;
+    uint32_t nb = TAMD_FIT_LOG;
+    if (n > 1u) {
+        const uint32_t mbo = TAMD_FIT_LOG - (31u - (uint32_t)__builtin_clz(n - 1u));
+        nb = S >= (n << mbo) ? mbo : mbo - 1u;
+    }
+    *upd = (S & ((1u << nb) - 1u)) | (nb << 8);
+    return state[c + (S >> nb) - n];
+}
+
+// A block's three tables (index 0 literal lengths, 1 match lengths, 2 offsets, as the codes are
+// packed: LL | ML << 8 | OF << 16).
+typedef struct tamd_seq_tables {
+    uint32_t mode[3];       // TAMD_MODE_*
+    uint32_t desc_len[3];   // description bytes (RLE: 1, FSE: the NCount bytes)
+    uint8_t desc[3][TAMD_FIT_DESC];
+    uint8_t norm[3][64], cum[3][64], state[3][TAMD_FIT_SIZE];
+} tamd_seq_tables;
+
+// Choose each table for the codes of a block (sequential; the kernel computes the same choice a
+// lane per symbol): the cheapest of the predefined distribution, RLE when one code is used, and a
+// fitted table, by costs in 1/16 bit from the blob (state bits of every sequence + the initial
+// state + the description).  Returns the descriptions' total bytes.
+TAMD_HD static inline uint32_t tamd_seq_choose(const uint32_t* codes, uint32_t nseq, const uint8_t* blob,
+                                              tamd_seq_tables* t) {
+    uint32_t total = 0;
+    for (uint32_t k = 0; k < 3; ++k) {
+        const uint32_t nsym = k == 0 ? 36u : k == 1 ? 53u : 32u, plog = k == 2 ? 5u : 6u;
+        uint32_t count[64];
+        for (uint32_t s = 0; s < 64; ++s) count[s] = 0;
+        for (uint32_t q = 0; q < nseq; ++q) ++count[(codes[q] >> (8u * k)) & 0xffu];
+        uint32_t present = 0, last = 0, only = 0, sum = 0, big = 0;
+        uint64_t pre = 16u * plog;
+        for (uint32_t s = 0; s < nsym; ++s) {
+            pre += (uint64_t)count[s] * blob[TAMD_FSE_PCOST + 64u * k + s];
+            const uint32_t n = tamd_fit_norm(count[s], nseq);
+            t->norm[k][s] = (uint8_t)n;
+            sum += n;
+            if (n > t->norm[k][big]) big = s;
+            if (count[s]) {
+                ++present;
+                last = s;
+                only = s;
+            }
+        }
+        t->mode[k] = TAMD_MODE_PREDEF;
+        t->desc_len[k] = 0;
+        uint64_t best = pre;
+        if (present == 1 && 16u * 8u < best) {
+            t->mode[k] = TAMD_MODE_RLE;
+            t->desc_len[k] = 1;
+            t->desc[k][0] = (uint8_t)only;
+            best = 16u * 8u;
+        }
+        const int32_t fixed = (int32_t)t->norm[k][big] + (int32_t)TAMD_FIT_SIZE - (int32_t)sum;
+        if (present >= 2 && present <= TAMD_FIT_SIZE && fixed >= 1) {
+            t->norm[k][big] = (uint8_t)fixed;
+            uint64_t fit = 0, bits = 4;  // (4 bits: accuracy log - 5 = 0)
+            uint8_t d[TAMD_FIT_DESC];
+            for (uint32_t i = 0; i < TAMD_FIT_DESC; ++i) d[i] = 0;
+            uint32_t cum = 0;
+            for (uint32_t s = 0; s <= last; ++s) {
+                const uint32_t n = t->norm[k][s];
+                fit += (uint64_t)count[s] * blob[TAMD_FSE_FCOST + n];
+                uint32_t z = 0;
+                if (n == 0)
+                    while (s + 1u + z <= last && t->norm[k][s + 1u + z] == 0) ++z;
+                uint64_t v;
+                const uint32_t w = tamd_ncount_item(n, cum, s == 0 || t->norm[k][s - 1] != 0, z, &v);
+                for (uint32_t b = 0; b < w; ++b)
+                    if ((v >> b) & 1u) d[(bits + b) / 8u] |= (uint8_t)(1u << ((bits + b) % 8u));
+                bits += w;
+                cum += n;
+            }
+            fit += 16u * (TAMD_FIT_LOG + bits);
+            if (fit < best) {
+                t->mode[k] = TAMD_MODE_FSE;
+                t->desc_len[k] = (uint32_t)((bits + 7u) / 8u);
+                for (uint32_t i = 0; i < t->desc_len[k]; ++i) t->desc[k][i] = d[i];
+                tamd_fit_states(t->norm[k], last + 1u, t->cum[k], t->state[k]);
+            }
+        }
+        total += t->desc_len[k];
+    }
+    return total;
+}
+
+// The sequences section's modes byte (s3.1.1.3.2.1.2): LL << 6 | OF << 4 | ML << 2.
+TAMD_HD static inline uint32_t tamd_modes_byte(const uint32_t* mode) {
+    return (mode[0] << 6) | (mode[2] << 4) | (mode[1] << 2);
+}
+
+// tamd_fse_sequences with the block's tables: the descriptions are not written here (they follow
+// the modes byte: LL, OF, ML); `modes` null = all predefined.
+TAMD_HD static inline uint32_t tamd_fse_sequences_t(const uint32_t* seq_lo, const uint32_t* seq_off, uint32_t nseq,
+                                                   const uint8_t* tabs, const tamd_seq_tables* tt, uint8_t* out,
+                                                   uint32_t cap) {
+    uint64_t acc = 0;
+    uint32_t nbits = 0, pos = 0;
+    bool over = false;
+    auto add = [&](uint32_t v, uint32_t bits) {
+        if (!bits) return;
+        acc |= (uint64_t)(v & ((1u << bits) - 1u)) << nbits;
+        nbits += bits;
+        while (nbits >= 8) {
+            if (pos < cap) out[pos] = (uint8_t)acc;
+            else over = true;
+            ++pos;
+            acc >>= 8;
+            nbits -= 8;
+        }
+    };
+    const uint16_t* e16 = (const uint16_t*)(tabs + TAMD_FSE_E16);
+    const uint32_t e16_at[3] = {TAMD_FSE_LL_E16, TAMD_FSE_ML_E16, TAMD_FSE_OF_E16};
+    const uint32_t psize[3] = {64u, 64u, 32u};
+    uint32_t mode[3] = {0, 0, 0};
+    if (tt)
+        for (uint32_t k = 0; k < 3; ++k) mode[k] = tt->mode[k];
+    auto code_of = [&](uint32_t q, uint32_t k) {
+        if (k == 0) return tamd_ll_code(seq_lo[q] & 0xffffu);
+        if (k == 1) return tamd_ml_code(seq_lo[q] >> 16);
+        return 31u - (uint32_t)__builtin_clz(seq_off[q] + 3u);
+    };
+    // one step of table k into the symbol of sequence q, from the decoder's next state st
+    auto step = [&](uint32_t k, uint32_t q, uint32_t st, uint32_t* upd) -> uint32_t {
+        const uint32_t c = code_of(q, k);
+        if (mode[k] == TAMD_MODE_RLE) {
+            *upd = 0;
+            return 0;
+        }
+        if (mode[k] == TAMD_MODE_FSE) return tamd_fit_step(tt->norm[k][c], tt->cum[k][c], tt->state[k], st, upd);
+        const uint32_t e = e16[e16_at[k] + c * psize[k] + st];
+        *upd = (e >> 10) | (((e >> 6) & 15u) << 8);
+        return e & 63u;
+    };
+    const uint32_t init_bits[3] = {mode[0] == TAMD_MODE_PREDEF ? 6u : mode[0] == TAMD_MODE_FSE ? TAMD_FIT_LOG : 0u,
+                                   mode[1] == TAMD_MODE_PREDEF ? 6u : mode[1] == TAMD_MODE_FSE ? TAMD_FIT_LOG : 0u,
+                                   mode[2] == TAMD_MODE_PREDEF ? 5u : mode[2] == TAMD_MODE_FSE ? TAMD_FIT_LOG : 0u};
+    uint32_t s = nseq - 1, st[3], upd;
+    for (uint32_t k = 0; k < 3; ++k) st[k] = step(k, s, 0, &upd);
+    auto values = [&](uint32_t q) {
+        const uint32_t ll = seq_lo[q] & 0xffffu, ml = seq_lo[q] >> 16, off = seq_off[q] + 3u;
+        const uint32_t llc = tamd_ll_code(ll), mlc = tamd_ml_code(ml), ofc = 31u - (uint32_t)__builtin_clz(off);
+        add(ll - tamd_ll_base(llc), tamd_ll_bits(llc));
+        add(ml - tamd_ml_base(mlc), tamd_ml_bits(mlc));
+        add(off, ofc);
+    };
+    values(s);
+    while (s-- > 0) {
+        const uint32_t order[3] = {2u, 1u, 0u};  // offsets, match lengths, literal lengths
+        for (uint32_t i = 0; i < 3; ++i) {
+            const uint32_t k = order[i];
+            st[k] = step(k, s, st[k], &upd);
+            add(upd & 0xffu, upd >> 8);
+        }
+        values(s);
+    }
+    add(st[1], init_bits[1]);  // the initial states, read first by the decoder: LL, OF, ML
+    add(st[2], init_bits[2]);
+    add(st[0], init_bits[0]);
+    add(1, 1);  // end mark
+    if (nbits) add(0, 8 - nbits);
+    return over ? 0 : pos;
+}
+
 // Host: the FSE blob of the predefined distributions (RFC 8878 s3.1.1.3.2.2; zstd_internal.h
 // LL/ML/OF_defaultNorm).  Each decoding table is laid out as FSE_buildDTable does
 // (fse_decompress.c:93-148 restated: probability -1 symbols at the top, the others spread with
@@ -299,6 +549,15 @@ static inline void tamd_fse_blob(uint8_t* blob) {
     tamd_build_fse(ll, 36, 6, blob + TAMD_FSE_LL_ENC, blob + TAMD_FSE_LL_DEC, e16 + TAMD_FSE_LL_E16);
     tamd_build_fse(ml, 53, 6, blob + TAMD_FSE_ML_ENC, blob + TAMD_FSE_ML_DEC, e16 + TAMD_FSE_ML_E16);
     tamd_build_fse(of, 29, 5, blob + TAMD_FSE_OF_ENC, blob + TAMD_FSE_OF_DEC, e16 + TAMD_FSE_OF_E16);
+    // costs: log - log2(probability slots), a -1 symbol holding one slot
+    const struct { const int16_t* norm; uint32_t nsym, log; } t[3] = {{ll, 36, 6}, {ml, 53, 6}, {of, 29, 5}};
+    for (uint32_t k = 0; k < 3; ++k)
+        for (uint32_t s = 0; s < t[k].nsym; ++s) {
+            const double p = t[k].norm[s] > 0 ? (double)t[k].norm[s] : 1.0;
+            blob[TAMD_FSE_PCOST + 64 * k + s] = (uint8_t)(16.0 * ((double)t[k].log - log2(p)) + 0.5);
+        }
+    for (uint32_t n = 1; n <= TAMD_FIT_SIZE; ++n)
+        blob[TAMD_FSE_FCOST + n] = (uint8_t)(16.0 * ((double)TAMD_FIT_LOG - log2((double)n)) + 0.5);
 }
 
 // ---- Huffman-coded literals (RFC 8878 s3.1.1.3.1, s4.2) ----------------------------------------

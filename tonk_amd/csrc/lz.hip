@@ -7,8 +7,9 @@
 // bytes the decompressor will hold when it decodes the message: the current history segment and
 // the one before it (zstd keeps the previous contiguous segment as its external dictionary,
 // zstd_decompress.c ZSTD_checkContinuity).  The block uses raw literals and the predefined FSE
-// distributions for literal lengths, match lengths and offsets (no repeat offsets, so no state
-// carries from block to block).
+// distributions for literal lengths, match lengths and offsets, or per block the cheaper of an RLE
+// code or an FSE table fitted to the block's codes and described in it (round 6; no repeat
+// offsets or repeat tables, so no state carries from block to block).
 //
 // Per message: (1) candidate positions from a hash table of 8-byte keys in LDS (the window's positions
 // are inserted once per job, each message's after it is scanned, 64 at a time), (2) every lane
@@ -70,13 +71,42 @@ struct LzWave {
     __attribute__((aligned(16))) uint8_t mbuf[TAMD_LZ_MAX_MESSAGE + LZ_PROBE + 16];  // the message
     uint16_t seq_pos[LZ_MAX_SEQS];                            // where each sequence's literals start
     uint32_t sh_init[3], sh_bytes, sh_ok;
+    // the block's sequence tables (tamd_seq_choose, a lane per symbol): descriptions, and the
+    // fitted tables' normalized counts, state offsets and states (tamd_fit_states)
+    uint32_t fdesc[3][TAMD_FIT_DESC / 4];
+    uint8_t fnorm[3][64], fcum[3][64], fstate[3][TAMD_FIT_SIZE], gsym[TAMD_FIT_SIZE];
 };
+
+static __device__ __forceinline__ uint32_t lz_wave_sum(uint32_t x) {
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) x += __shfl_xor(x, d);
+    return x;
+}
+static __device__ __forceinline__ uint32_t lz_wave_max(uint32_t x) {
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_xor(x, d);
+        x = y > x ? y : x;
+    }
+    return x;
+}
+// exclusive prefix sum over the lanes
+static __device__ __forceinline__ uint32_t lz_wave_excl(uint32_t x, uint32_t lane) {
+    uint32_t v = x;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(v, d);
+        if (lane >= d) v += y;
+    }
+    return v - x;
+}
 
 
 // One message.  BIG: the message is read from the stream buffer and its per-sequence arrays live
 // in global scratch; otherwise all of it is in the wave's LDS.
 template <bool BIG>
-static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __restrict__ e16, const tamd_lz_msg m,
+static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __restrict__ e16,
+                                                  const uint8_t* __restrict__ fse, const tamd_lz_msg m,
                                                   const uint8_t* __restrict__ buf, uint32_t mask,
                                                   uint8_t* __restrict__ scratch, uint8_t* __restrict__ out,
                                                   uint32_t* __restrict__ written, uint32_t mi, uint32_t lane,
@@ -244,32 +274,127 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
     lits += last_lits;
     LZ_SYNC();
 
-    // (4) the sequence bit stream, as tamd_fse_sequences (lz.h) writes it, built in parallel:
-    // codes per sequence (all lanes), the three FSE state chains (lanes 0-2, one chain each,
-    // from the last sequence back), then every sequence's bit fields placed at their offsets
-    // (a prefix sum of the field widths in stream order: the last sequence first).
+    // (4) the sequence bit stream, as tamd_fse_sequences_t (lz.h) writes it, built in parallel:
+    // codes per sequence (all lanes), each table's choice (a lane per symbol), the three state
+    // chains (lanes 0-2, one chain each, from the last sequence back), then every sequence's bit
+    // fields placed at their offsets (a prefix sum of the field widths in stream order: the last
+    // sequence first).
     uint32_t lh = 0, shb = 0;
     const uint32_t lits_word = tamd_lits_header_word(lits, &lh);
-    const uint32_t seq_word = tamd_seq_header_word(nseq, &shb);
+    uint32_t seq_word = tamd_seq_header_word(nseq, &shb);
     const uint32_t limit = n - 1u < m.cap ? n - 1u : m.cap;  // smaller than the message, fits
-    const uint32_t head = lh + lits + shb;
+    uint32_t head = lh + lits + shb;
     bool ok = head < limit && nseq > 0;
     uint32_t total = 0;
+    uint32_t mode[3] = {TAMD_MODE_PREDEF, TAMD_MODE_PREDEF, TAMD_MODE_PREDEF}, dlen[3] = {0, 0, 0};
     if (ok) {
-        for (uint32_t sq = lane; sq < nseq; sq += 64)
-            code[sq] = tamd_ll_code(seq_lo[sq] & 0xffffu) | (tamd_ml_code(seq_lo[sq] >> 16) << 8) |
-                       ((31u - (uint32_t)__builtin_clz(seq_off[sq] + 3u)) << 16);
+        uint32_t* hist = L.bitw;  // (3 x 64 counts; the bit stream's words are zeroed after)
+        for (uint32_t k = lane; k < 3u * 64u; k += 64) hist[k] = 0;
+        if (lane < 3u * TAMD_FIT_DESC / 4u) (&L.fdesc[0][0])[lane] = 0;
         LZ_SYNC();
+        for (uint32_t sq = lane; sq < nseq; sq += 64) {
+            const uint32_t cd = tamd_ll_code(seq_lo[sq] & 0xffffu) | (tamd_ml_code(seq_lo[sq] >> 16) << 8) |
+                                ((31u - (uint32_t)__builtin_clz(seq_off[sq] + 3u)) << 16);
+            code[sq] = cd;
+            atomicAdd(&hist[cd & 0xffu], 1u);
+            atomicAdd(&hist[64u + ((cd >> 8) & 0xffu)], 1u);
+            atomicAdd(&hist[128u + (cd >> 16)], 1u);
+        }
+        LZ_SYNC();
+        // each table's mode (tamd_seq_choose restated a lane per symbol)
+        for (uint32_t k = 0; k < 3; ++k) {
+            const uint32_t nsym = k == 0 ? 36u : k == 1 ? 53u : 32u, plog = k == 2 ? 5u : 6u;
+            const uint32_t cnt = lane < nsym ? hist[64u * k + lane] : 0u;
+            uint32_t nrm = tamd_fit_norm(cnt, nseq);
+            const uint64_t pres = __ballot(cnt != 0);
+            const uint32_t present = (uint32_t)__builtin_popcountll(pres), last = 63u - (uint32_t)__builtin_clzll(pres);
+            const uint32_t pre = lz_wave_sum(cnt * fse[TAMD_FSE_PCOST + 64u * k + lane]) + 16u * plog;
+            const uint32_t sum = lz_wave_sum(nrm);
+            const uint32_t key = lz_wave_max((nrm << 8) | (63u - lane));
+            const uint32_t big = 63u - (key & 0xffu);
+            const int32_t fixed = (int32_t)(key >> 8) + (int32_t)TAMD_FIT_SIZE - (int32_t)sum;
+            uint32_t md = TAMD_MODE_PREDEF, best = pre, dl = 0;
+            if (present == 1u && 16u * 8u < best) {
+                md = TAMD_MODE_RLE;
+                best = 16u * 8u;
+                dl = 1;
+            }
+            if (present >= 2u && present <= TAMD_FIT_SIZE && fixed >= 1) {
+                if (lane == big) nrm = (uint32_t)fixed;
+                const uint32_t cum = lz_wave_excl(nrm, lane);
+                const uint32_t prev = __shfl_up(nrm, 1);
+                const bool lead = lane == 0 || prev != 0;
+                const uint64_t above = __ballot(nrm != 0) & ~((2ull << lane) - 1ull);
+                const uint32_t z = nrm == 0 && above ? (uint32_t)__builtin_ctzll(above) - lane - 1u : 0u;
+                uint64_t v = 0;
+                const uint32_t w = lane <= last ? tamd_ncount_item(nrm, cum, lead, z, &v) : 0u;
+                const uint32_t wsum = lz_wave_sum(w);
+                const uint32_t fit = lz_wave_sum(cnt * fse[TAMD_FSE_FCOST + nrm]) + 16u * (TAMD_FIT_LOG + 4u + wsum);
+                if (fit < best) {
+                    md = TAMD_MODE_FSE;
+                    dl = (4u + wsum + 7u) / 8u;
+                    // the description's bits, then the encoder's states (tamd_fit_states)
+                    const uint32_t at = 4u + lz_wave_excl(w, lane);
+                    if (w) {
+                        uint32_t* d = L.fdesc[k];
+                        const uint32_t w0 = at / 32u, sh = at % 32u;
+                        atomicOr(&d[w0], (uint32_t)(v << sh));
+                        if (sh + w > 32u) atomicOr(&d[w0 + 1], (uint32_t)(v >> (32u - sh)));
+                        if (sh + w > 64u) atomicOr(&d[w0 + 2], (uint32_t)(v >> (64u - sh)));
+                    }
+                    L.fnorm[k][lane] = (uint8_t)nrm;
+                    L.fcum[k][lane] = (uint8_t)cum;
+                    for (uint32_t i = 0; i < nrm; ++i) L.gsym[cum + i] = (uint8_t)lane;
+                    LZ_SYNC();
+                    // state u decodes the symbol spread to slot u: occurrence g = u * 7 (mod 32);
+                    // its rank among that symbol's states is the number of smaller u with it
+                    const bool in = lane < TAMD_FIT_SIZE;
+                    const uint32_t sym = in ? L.gsym[(lane * TAMD_FIT_STEP_INV) & (TAMD_FIT_SIZE - 1u)] : 0u;
+                    uint64_t same = __ballot(in);
+#pragma unroll
+                    for (uint32_t b = 0; b < 6; ++b) {
+                        const uint64_t bb = __ballot(in && ((sym >> b) & 1u));
+                        same &= ((sym >> b) & 1u) ? bb : ~bb;
+                    }
+                    const uint32_t rank = (uint32_t)__builtin_popcountll(same & ((1ull << lane) - 1ull));
+                    if (in) L.fstate[k][L.fcum[k][sym] + rank] = (uint8_t)lane;
+                }
+            }
+            if (md == TAMD_MODE_RLE && lane == 0) L.fdesc[k][0] = 63u - __builtin_clzll(pres);
+            mode[k] = md;
+            dlen[k] = dl;
+        }
+        LZ_SYNC();
+        seq_word |= tamd_modes_byte(mode) << (8u * (shb - 1u));
+        head += dlen[0] + dlen[1] + dlen[2];
+        ok = head < limit;
+    }
+    if (ok) {
         if (lane < 3) {
             const uint32_t shift = 8u * lane, size = lane == 2 ? 32u : 64u;
+            const uint32_t md = lane == 0 ? mode[0] : lane == 1 ? mode[1] : mode[2];
             const uint16_t* enc = e16 + (lane == 0 ? TAMD_FSE_LL_E16 : lane == 1 ? TAMD_FSE_ML_E16 : TAMD_FSE_OF_E16);
             uint16_t* u_out = upd + S * lane;
-            uint32_t st = enc[((code[nseq - 1] >> shift) & 0xffu) * size] & 63u;
-            for (uint32_t sq = nseq - 1; sq-- > 0;) {
-                const uint32_t e = enc[((code[sq] >> shift) & 0xffu) * size + st];
-                u_out[sq] = (uint16_t)((e >> 10) | (((e >> 6) & 15u) << 8));
-                st = e & 63u;
-            }
+            uint32_t st = 0;
+            if (md == TAMD_MODE_FSE) {
+                const uint8_t* nm = L.fnorm[lane];
+                const uint8_t* cm = L.fcum[lane];
+                const uint8_t* sv = L.fstate[lane];
+                uint32_t u, c = (code[nseq - 1] >> shift) & 0xffu;
+                st = tamd_fit_step(nm[c], cm[c], sv, 0, &u);
+                for (uint32_t sq = nseq - 1; sq-- > 0;) {
+                    c = (code[sq] >> shift) & 0xffu;
+                    st = tamd_fit_step(nm[c], cm[c], sv, st, &u);
+                    u_out[sq] = (uint16_t)u;
+                }
+            } else if (md == TAMD_MODE_PREDEF) {
+                st = enc[((code[nseq - 1] >> shift) & 0xffu) * size] & 63u;
+                for (uint32_t sq = nseq - 1; sq-- > 0;) {
+                    const uint32_t e = enc[((code[sq] >> shift) & 0xffu) * size + st];
+                    u_out[sq] = (uint16_t)((e >> 10) | (((e >> 6) & 15u) << 8));
+                    st = e & 63u;
+                }
+            }  // (RLE: no state bits)
             L.sh_init[lane] = st;
         }
         // zero the bit buffer words the stream can use
@@ -290,7 +415,9 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
                     nbits += nb;
                 };
                 if (sq != nseq - 1u) {
-                    const uint32_t o = upd[2u * S + sq], ml_u = upd[S + sq], l_u = upd[sq];
+                    const uint32_t o = mode[2] != TAMD_MODE_RLE ? upd[2u * S + sq] : 0u;
+                    const uint32_t ml_u = mode[1] != TAMD_MODE_RLE ? upd[S + sq] : 0u;
+                    const uint32_t l_u = mode[0] != TAMD_MODE_RLE ? upd[sq] : 0u;
                     put(o & 0xffu, o >> 8);
                     put(ml_u & 0xffu, ml_u >> 8);
                     put(l_u & 0xffu, l_u >> 8);
@@ -316,15 +443,20 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
         }
         LZ_SYNC();
         // the initial states (ML, OF, LL: the decoder reads LL first) and the end mark
-        const uint64_t tail = (uint64_t)L.sh_init[1] | ((uint64_t)L.sh_init[2] << 6) | ((uint64_t)L.sh_init[0] << 11) |
-                              (1ull << 17);
-        const uint32_t bits_total = carry + 18u;
+        auto init_w = [&](uint32_t k) {
+            return mode[k] == TAMD_MODE_PREDEF ? (k == 2 ? 5u : 6u) : mode[k] == TAMD_MODE_FSE ? TAMD_FIT_LOG : 0u;
+        };
+        const uint32_t w_ml = init_w(1), w_of = init_w(2), w_ll = init_w(0);
+        const uint64_t tail = (uint64_t)L.sh_init[1] | ((uint64_t)L.sh_init[2] << w_ml) |
+                              ((uint64_t)L.sh_init[0] << (w_ml + w_of)) | (1ull << (w_ml + w_of + w_ll));
+        const uint32_t tail_bits = w_ml + w_of + w_ll + 1u;
+        const uint32_t bits_total = carry + tail_bits;
         total = head + (bits_total + 7u) / 8u;
         ok = total <= limit;
         if (ok && lane == 0) {
             const uint32_t w0 = carry / 32u, sh = carry % 32u;
             bitw[w0] |= (uint32_t)(tail << sh);
-            if (sh + 18u > 32u) bitw[w0 + 1] |= (uint32_t)(tail >> (32u - sh));
+            if (sh + tail_bits > 32u) bitw[w0 + 1] |= (uint32_t)(tail >> (32u - sh));
         }
     }
     if (lane == 0) {
@@ -366,6 +498,14 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
         const uint32_t hs = shb;
         if (lane < hs) o[w + lane] = (uint8_t)(seq_word >> (8u * lane));
         w += hs;
+        // the tables' descriptions: literal lengths, offsets, match lengths
+        const uint32_t order[3] = {0u, 2u, 1u};
+#pragma unroll
+        for (uint32_t i = 0; i < 3; ++i) {
+            const uint32_t k = order[i];
+            if (lane < dlen[k]) o[w + lane] = ((const uint8_t*)L.fdesc[k])[lane];
+            w += dlen[k];
+        }
         const uint32_t nb = L.sh_bytes - w;
         const uint8_t* bits = (const uint8_t*)bitw;
         for (uint32_t k = lane; k < nb; k += 64) o[w + k] = bits[k];
@@ -441,8 +581,8 @@ tamd_lz_compress(const tamd_lz_job* __restrict__ jobs, uint32_t n_jobs, const ta
             LZ_SYNC();
             continue;
         }
-        if (big) lz_message<true>(L, e16, m, buf, mask, scratch, out, written, mi, lane, ph, t_ph, prof != nullptr);
-        else lz_message<false>(L, e16, m, buf, mask, scratch, out, written, mi, lane, ph, t_ph, prof != nullptr);
+        if (big) lz_message<true>(L, e16, fse, m, buf, mask, scratch, out, written, mi, lane, ph, t_ph, prof != nullptr);
+        else lz_message<false>(L, e16, fse, m, buf, mask, scratch, out, written, mi, lane, ph, t_ph, prof != nullptr);
     }
     if (prof && lane == 0)
 #pragma unroll

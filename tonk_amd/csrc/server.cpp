@@ -9,6 +9,10 @@
 #include <string.h>
 #include <thread>
 #include <immintrin.h>
+#include <linux/futex.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+#include <time.h>
 
 extern "C" __global__ void tamd_serve(const tamd_serve_args);
 
@@ -22,6 +26,11 @@ int spinners_max() {  // (TONK_AMD_SPINNERS overrides)
     static const int n = getenv("TONK_AMD_SPINNERS") ? atoi(getenv("TONK_AMD_SPINNERS")) : 1024;
     return n;
 }
+long futex_wait(std::atomic<uint32_t>* w, uint32_t expect, long timeout_ns) {
+    timespec ts{timeout_ns / 1000000000L, timeout_ns % 1000000000L};
+    return syscall(SYS_futex, (uint32_t*)w, FUTEX_WAIT_PRIVATE, expect, &ts, nullptr, 0);
+}
+void futex_wake(std::atomic<uint32_t>* w) { syscall(SYS_futex, (uint32_t*)w, FUTEX_WAKE_PRIVATE, 1, nullptr, nullptr, 0); }
 double now_us() {
     return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
@@ -42,6 +51,8 @@ bool Server::init(Device& dev, unsigned workers, unsigned ring_size, double idle
     idle_ticks_ = (uint64_t)(idle_ms * 1e5);  // s_memrealtime: 100 MHz
     if (const char* e = getenv("TONK_AMD_SERVE_DEBUG")) debug_ = (uint32_t)atoi(e);
     if (const char* e = getenv("TONK_AMD_SERVE_STALL_POST_MS")) stall_post_ms_ = (uint32_t)atoi(e);
+    if (const char* e = getenv("TONK_AMD_WAIT_SPIN_US")) spin_us_ = atof(e);
+    if (const char* e = getenv("TONK_AMD_WAIT_PARK")) park_ = atoi(e) != 0;
     stamps_ = getenv("TONK_AMD_CAPI_WATCH") != nullptr;
     ring_ = (tamd_serve_slot*)coherent_alloc((size_t)ring_size_ * sizeof(tamd_serve_slot));
     host_ = (volatile tamd_serve_host*)coherent_alloc(sizeof(tamd_serve_host));
@@ -302,6 +313,7 @@ bool Server::wait(CmdBuf& b) {
         return true;
     }
     const double t0 = now_us();
+    if (park_) return wait_parked(b, t0);
     // At most spinners_max() callers spin (and yield) at a time; the others poll with short sleeps
     // (TONK_AMD_SPINNERS: a bound on the CPU that waiting callers burn in processes with hundreds
     // of calling threads on a few cores).
@@ -353,6 +365,12 @@ bool Server::wait(CmdBuf& b) {
         }
         _mm_pause();
     }
+    return completed(b);
+}
+
+// The command in `b` is done (its completion word seen).
+bool Server::completed(CmdBuf& b) {
+    volatile uint64_t* d = b.done();
     std::atomic_thread_fence(std::memory_order_acquire);
     b.busy = false;
     if (stamps_) {  // (watchdog: where a command's time goes, 100 MHz stamps -> ns)
@@ -369,6 +387,113 @@ bool Server::wait(CmdBuf& b) {
     gpu_ns_sum.fetch_add((d[2] - d[1]) * 10, std::memory_order_relaxed);
     if (stall_post_ms_ && b.ticket > 100 && stall_pending_.load()) stall_passed_.fetch_add(1);
     return true;
+}
+
+// Spin on the completion word for spin_us_, then park (server.h Parked): the poller wakes the caller
+// when the word is written; the caller also wakes every millisecond to check the executor's life
+// (idle exit, timeout, dead server) as the spinning loop does.
+bool Server::wait_parked(CmdBuf& b, double t0) {
+    const uint64_t want = (uint32_t)(b.ticket + 1);
+    volatile uint64_t* d = b.done();
+    Parked p;
+    p.done = d;
+    p.want = want;
+    p.ticket = b.ticket;
+    bool parked = false;
+    for (uint32_t spin = 1;; ++spin) {
+        if (*d == want) break;
+        if (dead_.load(std::memory_order_relaxed)) {
+            if (parked) unpark(p);
+            return false;  // (b stays busy: never reused)
+        }
+        if (parked) {
+            if (!p.woken.load(std::memory_order_acquire)) futex_wait(&p.woken, 0, 1000000L);
+            if (p.woken.load(std::memory_order_acquire)) break;
+        } else if ((spin & 63) != 0) {
+            _mm_pause();
+            continue;
+        }
+        const double t = now_us() - t0;
+        if (host_->exited_gen == gen_.load() && host_->exit_tail <= b.ticket && !ensure_running()) {
+            if (parked) unpark(p);
+            return false;
+        }
+        if (t > timeout_us_) {
+            if (parked) unpark(p);
+            dead_.store(true);
+            fprintf(stderr, "tonk_amd: command %llu not completed after %.0f us (done word %llu); dispatcher: start %llu "
+                    "polls/1024 %llu waits for %llu; command 0: stage %llu block %llu; consumed %llu exited_gen %llu "
+                    "(launched %u) exit_tail %llu\n",
+                    (unsigned long long)b.ticket, timeout_us_, (unsigned long long)*d, (unsigned long long)host_->dbg[0],
+                    (unsigned long long)host_->dbg[1], (unsigned long long)host_->dbg[2],
+                    (unsigned long long)host_->dbg[3], (unsigned long long)host_->dbg[4],
+                    (unsigned long long)host_->consumed, (unsigned long long)host_->exited_gen, gen_.load(),
+                    (unsigned long long)host_->exit_tail);
+            fprintf(stderr, "tonk_amd: the persistent executor is off; using kernel launches\n");
+            return false;
+        }
+        if (!parked && t > spin_us_) {
+            std::call_once(poller_once_, [this] { poller_ = std::thread([this] { poller_loop(); }); });
+            {
+                std::lock_guard<std::mutex> lk(park_mu_);
+                parked_.push_back(&p);
+            }
+            park_seq_.fetch_add(1, std::memory_order_release);
+            futex_wake(&park_seq_);
+            waits_parked.fetch_add(1, std::memory_order_relaxed);
+            parked = true;
+        }
+    }
+    if (parked) {
+        unpark(p);
+        if (now_us() - t0 > 2000.0) waits_slow.fetch_add(1, std::memory_order_relaxed);
+    }
+    return completed(b);
+}
+
+// Off the poller's list (a no-op when the poller took it): after this the poller no longer
+// touches `p` (it wakes under the same lock).
+void Server::unpark(Parked& p) {
+    std::lock_guard<std::mutex> lk(park_mu_);
+    for (size_t i = 0; i < parked_.size(); ++i)
+        if (parked_[i] == &p) {
+            parked_[i] = parked_.back();
+            parked_.pop_back();
+            break;
+        }
+}
+
+// The poller: while callers are parked, rescan their completion words (about every microsecond)
+// and wake the done ones; with none parked, sleep on park_seq_.  It also relaunches the executor
+// when it ended on an idle spell with parked commands still unconsumed.
+void Server::poller_loop() {
+    while (!poller_stop_.load(std::memory_order_relaxed)) {
+        const uint32_t seq = park_seq_.load(std::memory_order_acquire);
+        size_t left;
+        uint64_t low_ticket = ~0ull;
+        {
+            std::lock_guard<std::mutex> lk(park_mu_);
+            for (size_t i = 0; i < parked_.size();) {
+                Parked* p = parked_[i];
+                if (*p->done == p->want) {
+                    p->woken.store(1, std::memory_order_release);
+                    futex_wake(&p->woken);
+                    parked_[i] = parked_.back();
+                    parked_.pop_back();
+                } else {
+                    if (p->ticket < low_ticket) low_ticket = p->ticket;
+                    ++i;
+                }
+            }
+            left = parked_.size();
+        }
+        if (!left) {
+            futex_wait(&park_seq_, seq, 10000000L);
+            continue;
+        }
+        if (host_->exited_gen == gen_.load() && host_->exit_tail <= low_ticket) ensure_running();
+        for (int i = 0; i < 64; ++i) _mm_pause();
+    }
 }
 
 std::string Server::phase_report() {
@@ -397,6 +522,12 @@ void Server::stop() {
     if (stamps_)  // (watchdog: the executor's life at process exit)
         fprintf(stderr, "tonk_amd: executor stop: posted=%llu launches=%llu; %s\n", (unsigned long long)posted.load(),
                 (unsigned long long)launches.load(), phase_report().c_str());
+    if (poller_.joinable()) {
+        poller_stop_.store(true);
+        park_seq_.fetch_add(1);
+        futex_wake(&park_seq_);
+        poller_.join();
+    }
     host_->stop = 1;
     std::atomic_thread_fence(std::memory_order_seq_cst);
     hipStream_t st = (hipStream_t)stream_;

@@ -13,6 +13,7 @@
 
 #include <atomic>
 #include <mutex>
+#include <thread>
 #include <stdint.h>
 #include <string>
 #include <vector>
@@ -59,7 +60,7 @@ public:
     std::string phase_report();  // (watchdog) mean time per command phase
 
     // counters for the C ABI's watchdog
-    std::atomic<uint64_t> posted{0}, launches{0}, waits_slow{0};
+    std::atomic<uint64_t> posted{0}, launches{0}, waits_slow{0}, waits_parked{0};
     std::atomic<uint64_t> gpu_ns_sum{0};  // executor time of the commands waited for
 
 private:
@@ -91,6 +92,29 @@ private:
     uint64_t phase_ns_[6] = {0, 0, 0, 0, 0, 0}, phase_n_ = 0;
     uint64_t shape_[5] = {0, 0, 0, 0, 0}, shape_n_ = 0;
     bool launch_locked(uint64_t tail0);
+
+    // Completion waits that outlast a short spin are parked: the caller sleeps on a futex word and
+    // one poller thread watches the completion words of every parked caller, waking each when its
+    // command is done.  A Tonk process has hundreds of calling threads on a CPU quota of a few
+    // cores: waiters that poll (yield or short sleeps) burn that quota as a group, and a burst of
+    // them starves the threads that post and consume (a start-up that never recovers speed).
+    struct Parked {
+        volatile uint64_t* done;
+        uint64_t want, ticket;
+        std::atomic<uint32_t> woken{0};
+    };
+    std::mutex park_mu_;
+    std::vector<Parked*> parked_;
+    std::atomic<uint32_t> park_seq_{0};  // futex word of the poller while nothing is parked
+    std::thread poller_;
+    std::once_flag poller_once_;
+    std::atomic<bool> poller_stop_{false};
+    double spin_us_ = 30.0;  // TONK_AMD_WAIT_SPIN_US: spin this long before parking
+    bool park_ = true;       // TONK_AMD_WAIT_PARK=0: the round-5 yield/sleep polling (A/B)
+    void poller_loop();
+    void unpark(Parked& p);
+    bool wait_parked(CmdBuf& b, double t0);
+    bool completed(CmdBuf& b);
 };
 
 }  // namespace tamd
