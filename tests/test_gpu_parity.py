@@ -263,6 +263,24 @@ def test_capi_no_encode_ahead_matches_reference(golden_index, name):
     assert got == want, first_diff(want, got)
 
 
+@pytest.mark.parametrize("env", [{"TONK_AMD_WAIT_PARK": "0"}, {"TONK_AMD_WAIT_SPIN_US": "0"}])
+def test_capi_wait_modes_match_reference(golden_index, env):
+    """Completion waits: the round-5 polling waits (TONK_AMD_WAIT_PARK=0), and every wait parked at
+    once (TONK_AMD_WAIT_SPIN_US=0: the poller thread wakes each caller), eight codec pairs on four
+    threads: every stream's transcript is the reference's."""
+    import hashlib
+    exe = os.path.join(NATIVE, "_build", "capi_gen")
+    entry = golden_index["batches"]["cfg2_64x4096_p2_ack64"]
+    prefix = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"waitmode_{os.getpid()}_")
+    out = subprocess.run([exe, "transcripts", prefix, "threads=4", "streams=8", "stream=0"] + entry["args"],
+                         capture_output=True, timeout=600, env=dict(os.environ, **env))
+    assert out.returncode == 0, out.stderr.decode()[-2000:]
+    for s in range(8):
+        text = open(f"{prefix}{s}.txt", "rb").read()
+        os.remove(f"{prefix}{s}.txt")
+        assert hashlib.sha256(text).hexdigest() == entry["streams"][str(s)]["sha256"], f"stream {s}"
+
+
 def test_capi_executor_idle_exit_and_relaunch(golden_index):
     """The persistent executor ends after 0.02 ms without a command (TONK_AMD_SERVE_IDLE_MS), so
     it ends and is relaunched between the driver's calls over and over: the transcript is still

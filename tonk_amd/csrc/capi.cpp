@@ -108,6 +108,10 @@ struct Runtime {
 };
 // The launch-free path (server.h): null when off (TONK_AMD_SERVE=0) or when it failed its checks.
 Server* g_srv = nullptr;
+// The codecs' staging halves and command buffers in device memory the host writes through the
+// PCIe BAR (Device::bar_alloc): the executor then copies commands and lands packets at HBM
+// latency instead of pulling them across PCIe.  TONK_AMD_CAPI_BAR=0: pinned host memory.
+bool g_bar = false;
 
 struct DevLock {
     std::unique_lock<std::mutex> lk;
@@ -256,6 +260,7 @@ struct Staging {
     // reading these halves and writing the codec's rows and pinned buffer, so none of them is
     // ever freed or reused (the codec is disabled; Codec::~Codec leaks its segments too).
     bool stalled = false;
+    bool bar = false;  // halves in BAR-written device memory (g_bar)
 
     size_t need(size_t bytes, size_t n_desc) const { return ((bytes + 15) & ~(size_t)15) + n_desc * 16 + 16; }
     // The current half's packets as zero-copy sources of one batched host_copy (combined
@@ -311,12 +316,13 @@ struct Staging {
         settle(sent[1]);
         if (g_srv && !settle_cmds()) return false;
         for (uint8_t*& h : half) {
-            Device::host_free(h);
+            if (bar) Device::bar_free(h);
+            else Device::host_free(h);
             h = nullptr;
         }
         cap = want < (256u << 10) ? (256u << 10) : want;
         for (uint8_t*& h : half)
-            if (!(h = (uint8_t*)Device::host_alloc(cap))) { cap = 0; return false; }
+            if (!(h = (uint8_t*)(bar ? Device::bar_alloc(cap) : Device::host_alloc(cap)))) { cap = 0; return false; }
         return true;
     }
     // Copy a packet into the staging for arena unit offset `row`.
@@ -365,8 +371,11 @@ struct Staging {
     }
     ~Staging() {
         if (stalled) return;  // (kept for good: a command may still read or write them)
-        for (uint8_t* h : half) Device::host_free(h);
-        for (CmdBuf& b : cmd) Device::host_free(b.mem);
+        for (uint8_t* h : half) {
+            if (bar) Device::bar_free(h);
+            else Device::host_free(h);
+        }
+        for (CmdBuf& b : cmd) b.release();
     }
 };
 
@@ -394,6 +403,8 @@ struct Codec {
         ctx.short_scans = short_scans;  // (A/B: 0 restores the chain level)
         static std::atomic<unsigned> next{0};
         staging.stream = next.fetch_add(1) % g_rt->dev.stream_count();
+        staging.bar = g_bar;
+        staging.cmd[0].bar = staging.cmd[1].bar = g_bar;
     }
     uint64_t byte_offset(RowId r) const { return (uint64_t)ctx.rows.offset(r) * TAMD_ROW_UNIT; }
     // The pinned buffer holds at least n bytes (no copy can be landing in it: every read into it
@@ -816,6 +827,11 @@ SIAMESE_EXPORT int siamese_init_(int version) {
             } else {
                 g_srv = srv;
                 atexit([] { if (g_srv) g_srv->stop(); });
+                if (!(getenv("TONK_AMD_CAPI_BAR") && atoi(getenv("TONK_AMD_CAPI_BAR")) == 0)) {
+                    void* p = Device::bar_alloc(4096);  // (maps the first slab now)
+                    g_bar = p != nullptr;
+                    Device::bar_free(p);
+                }
             }
         } else {
             srv->stop();

@@ -39,6 +39,8 @@ const uint8_t* device_fse(int device) {
     if ((size_t)device < g_tables.fse.size() && g_tables.fse[device]) return g_tables.fse[device];
     std::vector<uint8_t> blob(TAMD_FSE_BYTES, 0);
     tamd_fse_blob(blob.data());
+    // (TONK_AMD_LZ_FIT=0: the predefined sequence tables only, as before round 6 -- A/B knob)
+    if (getenv("TONK_AMD_LZ_FIT") && atoi(getenv("TONK_AMD_LZ_FIT")) == 0) blob[TAMD_FSE_FLAGS] |= TAMD_FSE_PREDEFINED_ONLY;
     uint8_t* d = nullptr;
     if (hipSetDevice(device) != hipSuccess || hipMalloc((void**)&d, TAMD_FSE_BYTES) != hipSuccess) return nullptr;
     if (hipMemcpy(d, blob.data(), TAMD_FSE_BYTES, hipMemcpyHostToDevice) != hipSuccess) {

@@ -1251,7 +1251,8 @@ void Device::scatter_upload(uint8_t* src, size_t bytes, const ScatterIn* d, uint
         if (!sc_per_stream_.empty()) sc_per_stream_[cur_stream_] = std::make_pair(sc_dev_, sc_cap_);
     }
     // (the landing area is reused batch after batch: copies and scatters are stream ordered)
-    HIPCHK(hipMemcpyAsync(sc_dev_, src, total, hipMemcpyHostToDevice, st));
+    // (hipMemcpyDefault: the C ABI's staging may be BAR-written device memory)
+    HIPCHK(hipMemcpyAsync(sc_dev_, src, total, hipMemcpyDefault, st));
     HIPT(hipLaunchKernelGGL(tamd_scatter_rows, dim3(n), dim3(64), 0, st, (const ScatterDescDev*)(sc_dev_ + at), n,
                        (const uint8_t*)sc_dev_, arena_));
     HIPCHK(hipGetLastError());
@@ -1388,119 +1389,143 @@ bool Device::event_wait(void* ev) {
 // closing) would stall every other codec's work behind it; and on some hosts every hipHostMalloc
 // takes 10+ ms while blocking other HIP calls -- hundreds of codecs starting together (a Tonk test
 // opening 100 connections) then spent seconds in allocations.  host_reserve() maps slabs up front.
+// The same pool kind serves device memory the host writes through the PCIe BAR (bar_alloc):
+// fine-grained device allocations, which the host stores into directly (write-combined) and the
+// executor reads at HBM latency instead of across PCIe.
 namespace {
 const size_t kPinSlab = 64u << 20;
-std::mutex g_pin_mu;
-std::vector<void*> g_pin_free[64];
-std::unordered_map<void*, unsigned> g_pin_class;
-uint8_t* g_slab = nullptr;  // the slab blocks are cut from
-size_t g_slab_used = kPinSlab;
-std::vector<void*> g_spare_slabs;  // mapped and warmed ahead (host_prefill)
 
-// A new slab, and one small copy out of it and back: the first transfer touching a new pinned
-// allocation has been seen to block for ~80 ms, which should not happen under the device lock.
-void* new_slab() {
-    void* p = nullptr;
-    if (g_pin_device >= 0) hipSetDevice(g_pin_device);  // (a codec thread may not have bound it yet)
-    const auto t0 = std::chrono::steady_clock::now();
-    // (coherent: the persistent executor reads staged packets and commands, and writes results and
-    // completion words, while the host works on the same pages -- server.h)
-    if (hipHostMalloc(&p, kPinSlab, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return nullptr;
-    static uint8_t* d = nullptr;
-    if (!d && hipMalloc((void**)&d, 4096) != hipSuccess) d = nullptr;
-    if (d) {
-        memset(p, 0, 4096);
-        hipMemcpy(d, p, 4096, hipMemcpyHostToDevice);
-        hipMemcpy(p, d, 4096, hipMemcpyDeviceToHost);
-    }
-    report_slow("pinned slab", t0, kPinSlab >> 20, 0);
-    return p;
-}
-}  // namespace
+struct SlabPool {
+    bool bar = false;  // device memory (BAR-writable) instead of pinned host memory
+    std::mutex mu;
+    std::vector<void*> free_[64];
+    std::unordered_map<void*, unsigned> cls;
+    uint8_t* slab = nullptr;  // the slab blocks are cut from
+    size_t used = kPinSlab;
+    std::vector<void*> spare;  // mapped and warmed ahead (prefill)
 
-void Device::host_prefill(unsigned slabs) {
-    std::vector<void*> got;
-    for (unsigned i = 0; i < slabs; ++i)
-        if (void* p = new_slab()) got.push_back(p);
-    std::lock_guard<std::mutex> g(g_pin_mu);
-    g_spare_slabs.insert(g_spare_slabs.end(), got.begin(), got.end());
-}
-
-bool Device::host_reserve(size_t bytes) {
-    void* p = nullptr;
-    {
-        std::lock_guard<std::mutex> g(g_pin_mu);
-        // (one slab at a time: the current one is only replaced once used up)
-        if (g_slab && g_slab_used + bytes <= kPinSlab) return true;
-        if (!g_spare_slabs.empty()) {
-            p = g_spare_slabs.back();
-            g_spare_slabs.pop_back();
-        }
-    }
-    // A new slab is mapped and warmed outside the mutex (hipHostMalloc and its copies can take
-    // tens of ms, which under the mutex would stall every codec allocating meanwhile), then
-    // published under it; a thread that lost the race parks its slab as a spare.
-    if (!p && !(p = new_slab())) return false;
-    std::lock_guard<std::mutex> g(g_pin_mu);
-    if (g_slab && g_slab_used + bytes <= kPinSlab) {
-        g_spare_slabs.push_back(p);
-        return true;
-    }
-    if (g_slab) {  // the rest of the old slab becomes free blocks
-        for (unsigned c = 63; c >= 12; --c)
-            while (g_slab_used + ((size_t)1 << c) <= kPinSlab) {
-                void* b = g_slab + g_slab_used;
-                g_pin_class[b] = c;
-                g_pin_free[c].push_back(b);
-                g_slab_used += (size_t)1 << c;
-            }
-    }
-    g_slab = (uint8_t*)p;
-    g_slab_used = 0;
-    return true;
-}
-
-void* Device::host_alloc(size_t n) {
-    unsigned c = 12;
-    while (((size_t)1 << c) < n) ++c;
-    const size_t sz = (size_t)1 << c;
-    {
-        std::lock_guard<std::mutex> g(g_pin_mu);
-        if (!g_pin_free[c].empty()) {
-            void* p = g_pin_free[c].back();
-            g_pin_free[c].pop_back();
-            return p;
-        }
-    }
-    if (sz > kPinSlab / 4) {  // (large blocks: their own allocation)
+    void* raw(size_t n) {
         void* p = nullptr;
+        if (g_pin_device >= 0) hipSetDevice(g_pin_device);  // (a codec thread may not have bound it yet)
+        if (bar) return hipExtMallocWithFlags(&p, n, hipDeviceMallocFinegrained) == hipSuccess ? p : nullptr;
+        // (coherent: the persistent executor reads staged packets and commands, and writes results
+        // and completion words, while the host works on the same pages -- server.h)
+        return hipHostMalloc(&p, n, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess ? p : nullptr;
+    }
+    // A new slab, and one small copy out of it and back: the first transfer touching a new pinned
+    // allocation has been seen to block for ~80 ms, which should not happen under the device lock.
+    void* new_slab() {
         const auto t0 = std::chrono::steady_clock::now();
-        if (hipHostMalloc(&p, sz, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) return nullptr;
-        report_slow("pinned allocation", t0, sz >> 10, 0);
-        std::lock_guard<std::mutex> g(g_pin_mu);
-        g_pin_class[p] = c;
+        void* p = raw(kPinSlab);
+        if (!p) return nullptr;
+        static uint8_t* d = nullptr;
+        if (!d && hipMalloc((void**)&d, 4096) != hipSuccess) d = nullptr;
+        if (d && !bar) {
+            memset(p, 0, 4096);
+            hipMemcpy(d, p, 4096, hipMemcpyHostToDevice);
+            hipMemcpy(p, d, 4096, hipMemcpyDeviceToHost);
+        }
+        report_slow(bar ? "BAR slab" : "pinned slab", t0, kPinSlab >> 20, 0);
         return p;
     }
-    for (;;) {
+    void prefill(unsigned slabs) {
+        std::vector<void*> got;
+        for (unsigned i = 0; i < slabs; ++i)
+            if (void* p = new_slab()) got.push_back(p);
+        std::lock_guard<std::mutex> g(mu);
+        spare.insert(spare.end(), got.begin(), got.end());
+    }
+    bool reserve(size_t bytes) {
+        void* p = nullptr;
         {
-            std::lock_guard<std::mutex> g(g_pin_mu);
-            if (g_slab && g_slab_used + sz <= kPinSlab) {  // (4 KB aligned: every size is a multiple)
-                void* p = g_slab + g_slab_used;
-                g_slab_used += sz;
-                g_pin_class[p] = c;
+            std::lock_guard<std::mutex> g(mu);
+            // (one slab at a time: the current one is only replaced once used up)
+            if (slab && used + bytes <= kPinSlab) return true;
+            if (!spare.empty()) {
+                p = spare.back();
+                spare.pop_back();
+            }
+        }
+        // A new slab is mapped and warmed outside the mutex (the allocation and its copies can take
+        // tens of ms, which under the mutex would stall every codec allocating meanwhile), then
+        // published under it; a thread that lost the race parks its slab as a spare.
+        if (!p && !(p = new_slab())) return false;
+        std::lock_guard<std::mutex> g(mu);
+        if (slab && used + bytes <= kPinSlab) {
+            spare.push_back(p);
+            return true;
+        }
+        if (slab) {  // the rest of the old slab becomes free blocks
+            for (unsigned c = 63; c >= 12; --c)
+                while (used + ((size_t)1 << c) <= kPinSlab) {
+                    void* b = slab + used;
+                    cls[b] = c;
+                    free_[c].push_back(b);
+                    used += (size_t)1 << c;
+                }
+        }
+        slab = (uint8_t*)p;
+        used = 0;
+        return true;
+    }
+    void* alloc(size_t n) {
+        unsigned c = 12;
+        while (((size_t)1 << c) < n) ++c;
+        const size_t sz = (size_t)1 << c;
+        {
+            std::lock_guard<std::mutex> g(mu);
+            if (!free_[c].empty()) {
+                void* p = free_[c].back();
+                free_[c].pop_back();
                 return p;
             }
         }
-        if (!host_reserve(sz)) return nullptr;
+        if (sz > kPinSlab / 4) {  // (large blocks: their own allocation)
+            const auto t0 = std::chrono::steady_clock::now();
+            void* p = raw(sz);
+            if (!p) return nullptr;
+            report_slow(bar ? "BAR allocation" : "pinned allocation", t0, sz >> 10, 0);
+            std::lock_guard<std::mutex> g(mu);
+            cls[p] = c;
+            return p;
+        }
+        for (;;) {
+            {
+                std::lock_guard<std::mutex> g(mu);
+                if (slab && used + sz <= kPinSlab) {  // (4 KB aligned: every size is a multiple)
+                    void* p = slab + used;
+                    used += sz;
+                    cls[p] = c;
+                    return p;
+                }
+            }
+            if (!reserve(sz)) return nullptr;
+        }
     }
+    void release(void* p) {
+        if (!p) return;
+        std::lock_guard<std::mutex> g(mu);
+        auto it = cls.find(p);
+        if (it != cls.end()) free_[it->second].push_back(p);
+    }
+};
+SlabPool g_pin;
+SlabPool& bar_pool() {
+    static SlabPool* p = [] {
+        SlabPool* q = new SlabPool();
+        q->bar = true;
+        return q;
+    }();
+    return *p;
 }
+}  // namespace
 
-void Device::host_free(void* p) {
-    if (!p) return;
-    std::lock_guard<std::mutex> g(g_pin_mu);
-    auto it = g_pin_class.find(p);
-    if (it != g_pin_class.end()) g_pin_free[it->second].push_back(p);
-}
+void Device::host_prefill(unsigned slabs) { g_pin.prefill(slabs); }
+bool Device::host_reserve(size_t bytes) { return g_pin.reserve(bytes); }
+void* Device::host_alloc(size_t n) { return g_pin.alloc(n); }
+void Device::host_free(void* p) { g_pin.release(p); }
+void* Device::bar_alloc(size_t n) { return bar_pool().alloc(n); }
+void Device::bar_free(void* p) { bar_pool().release(p); }
 
 bool Device::enable_staging() {
     if (h2d_stream_) return true;

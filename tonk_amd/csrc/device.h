@@ -187,6 +187,11 @@ public:
     static bool host_reserve(size_t n);  // map a pinned slab now if fewer than n bytes are left in it
     static void host_prefill(unsigned slabs);  // map (and warm) that many 64 MB slabs ahead of use
     static void host_free(void* p);
+    // Device memory the host writes directly (fine-grained, through the PCIe BAR; pooled as the
+    // pinned blocks): the C ABI's staging and commands when TONK_AMD_CAPI_BAR is on.  The host must
+    // only store into it (a host load is an uncached PCIe round trip).
+    static void* bar_alloc(size_t n);
+    static void bar_free(void* p);
 
     // Bench helpers (kernels.hip).
     struct GenDesc { uint32_t row, index, len, pad; uint64_t seed; };

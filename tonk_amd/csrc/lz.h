@@ -73,6 +73,8 @@ uint32_t tamd_lz_scratch_bytes(uint32_t n) {
 // block-fitted table's by normalized count 0..32.
 #define TAMD_FSE_PCOST (TAMD_FSE_E16 + 2u * TAMD_FSE_E16_WORDS)
 #define TAMD_FSE_FCOST (TAMD_FSE_PCOST + 3u * 64u)
+#define TAMD_FSE_FLAGS (TAMD_FSE_FCOST + 63u)  // (an unused cost slot)
+#define TAMD_FSE_PREDEFINED_ONLY 1u              // flag: every block keeps the predefined tables
 #define TAMD_FSE_BYTES (TAMD_FSE_FCOST + 64u)
 
 #ifdef __HIPCC__
@@ -268,6 +270,7 @@ TAMD_HD static inline uint32_t tamd_fse_sequences(const uint32_t* seq_lo, const 
 #define TAMD_MODE_RLE 1u
 #define TAMD_MODE_FSE 2u
 #define TAMD_FIT_DESC 48u      // description bytes per table (a 53-symbol table needs at most 45)
+#define TAMD_FIT_MIN_SEQS 8u   // fewer sequences: no fitted table (its description never pays)
 
 // Normalized count of a symbol seen `count` of `total` times: the nearest share of the 32 states,
 // at least one for a present symbol.  The sum is brought to exactly 32 on the largest share
@@ -386,7 +389,7 @@ TAMD_HD static inline uint32_t tamd_seq_choose(const uint32_t* codes, uint32_t n
             best = 16u * 8u;
         }
         const int32_t fixed = (int32_t)t->norm[k][big] + (int32_t)TAMD_FIT_SIZE - (int32_t)sum;
-        if (present >= 2 && present <= TAMD_FIT_SIZE && fixed >= 1) {
+        if (present >= 2 && present <= TAMD_FIT_SIZE && nseq >= TAMD_FIT_MIN_SEQS && fixed >= 1) {
             t->norm[k][big] = (uint8_t)fixed;
             uint64_t fit = 0, bits = 4;  // (4 bits: accuracy log - 5 = 0)
             uint8_t d[TAMD_FIT_DESC];

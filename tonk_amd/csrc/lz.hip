@@ -74,31 +74,22 @@ struct LzWave {
     // the block's sequence tables (tamd_seq_choose, a lane per symbol): descriptions, and the
     // fitted tables' normalized counts, state offsets and states (tamd_fit_states)
     uint32_t fdesc[3][TAMD_FIT_DESC / 4];
+    uint32_t fstarts[3];  // bit g: some symbol's share of the 32 states starts at occurrence g
     uint8_t fnorm[3][64], fcum[3][64], fstate[3][TAMD_FIT_SIZE], gsym[TAMD_FIT_SIZE];
 };
 
-static __device__ __forceinline__ uint32_t lz_wave_sum(uint32_t x) {
+// Wave sums (DPP row shifts: a few instructions) and exclusive prefix sums of B-bit values, a bit
+// plane at a time (one ballot and a lane's mbcnt per bit).
+static __device__ __forceinline__ uint32_t lz_wave_sum(uint32_t x) { return __reduce_add_sync(~0ull, x); }
+template <uint32_t B>
+static __device__ __forceinline__ uint32_t lz_wave_excl(uint32_t x) {  // sum over the lanes below
+    uint32_t s = 0;
 #pragma unroll
-    for (uint32_t d = 1; d < 64; d <<= 1) x += __shfl_xor(x, d);
-    return x;
-}
-static __device__ __forceinline__ uint32_t lz_wave_max(uint32_t x) {
-#pragma unroll
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_xor(x, d);
-        x = y > x ? y : x;
+    for (uint32_t b = 0; b < B; ++b) {
+        const uint64_t m = __ballot((x >> b) & 1u);
+        s += __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) << b;
     }
-    return x;
-}
-// exclusive prefix sum over the lanes
-static __device__ __forceinline__ uint32_t lz_wave_excl(uint32_t x, uint32_t lane) {
-    uint32_t v = x;
-#pragma unroll
-    for (uint32_t d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(v, d);
-        if (lane >= d) v += y;
-    }
-    return v - x;
+    return s;
 }
 
 
@@ -291,6 +282,7 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
         uint32_t* hist = L.bitw;  // (3 x 64 counts; the bit stream's words are zeroed after)
         for (uint32_t k = lane; k < 3u * 64u; k += 64) hist[k] = 0;
         if (lane < 3u * TAMD_FIT_DESC / 4u) (&L.fdesc[0][0])[lane] = 0;
+        if (lane < 3u) L.fstarts[lane] = 0;
         LZ_SYNC();
         for (uint32_t sq = lane; sq < nseq; sq += 64) {
             const uint32_t cd = tamd_ll_code(seq_lo[sq] & 0xffffu) | (tamd_ml_code(seq_lo[sq] >> 16) << 8) |
@@ -302,6 +294,7 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
         }
         LZ_SYNC();
         // each table's mode (tamd_seq_choose restated a lane per symbol)
+        const bool fit_on = !(fse[TAMD_FSE_FLAGS] & TAMD_FSE_PREDEFINED_ONLY);
         for (uint32_t k = 0; k < 3; ++k) {
             const uint32_t nsym = k == 0 ? 36u : k == 1 ? 53u : 32u, plog = k == 2 ? 5u : 6u;
             const uint32_t cnt = lane < nsym ? hist[64u * k + lane] : 0u;
@@ -309,22 +302,29 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
             const uint64_t pres = __ballot(cnt != 0);
             const uint32_t present = (uint32_t)__builtin_popcountll(pres), last = 63u - (uint32_t)__builtin_clzll(pres);
             const uint32_t pre = lz_wave_sum(cnt * fse[TAMD_FSE_PCOST + 64u * k + lane]) + 16u * plog;
-            const uint32_t sum = lz_wave_sum(nrm);
-            const uint32_t key = lz_wave_max((nrm << 8) | (63u - lane));
-            const uint32_t big = 63u - (key & 0xffu);
-            const int32_t fixed = (int32_t)(key >> 8) + (int32_t)TAMD_FIT_SIZE - (int32_t)sum;
             uint32_t md = TAMD_MODE_PREDEF, best = pre, dl = 0;
-            if (present == 1u && 16u * 8u < best) {
+            if (present == 1u && 16u * 8u < best && fit_on) {
                 md = TAMD_MODE_RLE;
                 best = 16u * 8u;
                 dl = 1;
             }
-            if (present >= 2u && present <= TAMD_FIT_SIZE && fixed >= 1) {
+            if (present >= 2u && present <= TAMD_FIT_SIZE && nseq >= TAMD_FIT_MIN_SEQS && fit_on) {
+                const uint32_t sum = lz_wave_sum(nrm);
+                // the largest share, lowest symbol on ties: bit planes from the top
+                uint64_t cand = pres;
+#pragma unroll
+                for (uint32_t b = 6; b-- > 0;) {
+                    const uint64_t m = cand & __ballot((nrm >> b) & 1u);
+                    if (m) cand = m;
+                }
+                const uint32_t big = (uint32_t)__builtin_ctzll(cand);
+                const int32_t fixed = (int32_t)__builtin_amdgcn_readlane((int)nrm, (int)big) + (int32_t)TAMD_FIT_SIZE - (int32_t)sum;
+                if (fixed >= 1) {
                 if (lane == big) nrm = (uint32_t)fixed;
-                const uint32_t cum = lz_wave_excl(nrm, lane);
-                const uint32_t prev = __shfl_up(nrm, 1);
-                const bool lead = lane == 0 || prev != 0;
-                const uint64_t above = __ballot(nrm != 0) & ~((2ull << lane) - 1ull);
+                const uint32_t cum = lz_wave_excl<6>(nrm);
+                const uint64_t nz = __ballot(nrm != 0);
+                const bool lead = lane == 0 || ((nz >> (lane - 1u)) & 1ull) != 0;
+                const uint64_t above = nz & ~((2ull << lane) - 1ull);
                 const uint32_t z = nrm == 0 && above ? (uint32_t)__builtin_ctzll(above) - lane - 1u : 0u;
                 uint64_t v = 0;
                 const uint32_t w = lane <= last ? tamd_ncount_item(nrm, cum, lead, z, &v) : 0u;
@@ -334,7 +334,7 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
                     md = TAMD_MODE_FSE;
                     dl = (4u + wsum + 7u) / 8u;
                     // the description's bits, then the encoder's states (tamd_fit_states)
-                    const uint32_t at = 4u + lz_wave_excl(w, lane);
+                    const uint32_t at = 4u + lz_wave_excl<6>(w);
                     if (w) {
                         uint32_t* d = L.fdesc[k];
                         const uint32_t w0 = at / 32u, sh = at % 32u;
@@ -344,12 +344,18 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
                     }
                     L.fnorm[k][lane] = (uint8_t)nrm;
                     L.fcum[k][lane] = (uint8_t)cum;
-                    for (uint32_t i = 0; i < nrm; ++i) L.gsym[cum + i] = (uint8_t)lane;
+                    // occurrence g belongs to the symbol whose share starts at the last start <= g
+                    if (nrm) {
+                        L.gsym[cum] = (uint8_t)lane;
+                        atomicOr(&L.fstarts[k], 1u << cum);
+                    }
                     LZ_SYNC();
+                    const uint32_t starts = L.fstarts[k];
                     // state u decodes the symbol spread to slot u: occurrence g = u * 7 (mod 32);
                     // its rank among that symbol's states is the number of smaller u with it
                     const bool in = lane < TAMD_FIT_SIZE;
-                    const uint32_t sym = in ? L.gsym[(lane * TAMD_FIT_STEP_INV) & (TAMD_FIT_SIZE - 1u)] : 0u;
+                    const uint32_t g = (lane * TAMD_FIT_STEP_INV) & (TAMD_FIT_SIZE - 1u);
+                    const uint32_t sym = in ? L.gsym[31u - (uint32_t)__builtin_clz(starts & ((2u << g) - 1u))] : 0u;
                     uint64_t same = __ballot(in);
 #pragma unroll
                     for (uint32_t b = 0; b < 6; ++b) {
@@ -358,6 +364,7 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
                     }
                     const uint32_t rank = (uint32_t)__builtin_popcountll(same & ((1ull << lane) - 1ull));
                     if (in) L.fstate[k][L.fcum[k][sym] + rank] = (uint8_t)lane;
+                }
                 }
             }
             if (md == TAMD_MODE_RLE && lane == 0) L.fdesc[k][0] = 63u - __builtin_clzll(pres);

@@ -52,6 +52,8 @@ bool Server::init(Device& dev, unsigned workers, unsigned ring_size, double idle
     if (const char* e = getenv("TONK_AMD_SERVE_DEBUG")) debug_ = (uint32_t)atoi(e);
     if (const char* e = getenv("TONK_AMD_SERVE_STALL_POST_MS")) stall_post_ms_ = (uint32_t)atoi(e);
     if (const char* e = getenv("TONK_AMD_WAIT_SPIN_US")) spin_us_ = atof(e);
+    if (const char* e = getenv("TONK_AMD_WAIT_YIELD_US")) yield_us_ = atof(e);
+    if (yield_us_ < spin_us_) yield_us_ = spin_us_;
     if (const char* e = getenv("TONK_AMD_WAIT_PARK")) park_ = atoi(e) != 0;
     stamps_ = getenv("TONK_AMD_CAPI_WATCH") != nullptr;
     ring_ = (tamd_serve_slot*)coherent_alloc((size_t)ring_size_ * sizeof(tamd_serve_slot));
@@ -86,7 +88,7 @@ bool Server::init(Device& dev, unsigned workers, unsigned ring_size, double idle
         ok_ = false;
         return false;
     }
-    Device::host_free(probe.mem);
+    probe.release();
     // (test hook: a short timeout makes a loaded command time out, to exercise the dead server)
     if (const char* e = getenv("TONK_AMD_SERVE_TIMEOUT_US")) timeout_us_ = atof(e);
     return true;
@@ -166,16 +168,27 @@ bool Server::build(CmdBuf& b, const std::vector<Device::HostCopy>& up, const Pro
     const uint32_t bytes = (off_items + 8u * n_items + 15u) & ~15u;
     if ((size_t)bytes + 256 > TAMD_SERVE_CMD_BYTES) return false;
     if (CmdBuf::kHead + bytes > b.cap) {
-        Device::host_free(b.mem);
+        if (b.bar) Device::bar_free(b.mem);
+        else Device::host_free(b.mem);
         b.cap = 4096;
         while (b.cap < CmdBuf::kHead + bytes) b.cap <<= 1;
-        b.mem = (uint8_t*)Device::host_alloc(b.cap);
-        if (!b.mem) {
+        b.mem = (uint8_t*)(b.bar ? Device::bar_alloc(b.cap) : Device::host_alloc(b.cap));
+        if (b.bar && !b.head) {
+            b.head = (uint8_t*)Device::host_alloc(4096);
+            if (b.head) memset(b.head, 0, CmdBuf::kHead);
+            b.done_at = (volatile uint64_t*)b.head;
+        }
+        if (!b.mem || (b.bar && !b.head)) {
             b.cap = 0;
             return false;
         }
-        memset(b.mem, 0, CmdBuf::kHead);
+        if (!b.bar) memset(b.mem, 0, CmdBuf::kHead);
     }
+    b.bytes = bytes;
+    b.shape[0] = levels;
+    b.shape[1] = n_items;
+    b.shape[2] = n_instr;
+    b.shape[3] = (uint32_t)up.size();
     uint8_t* base = (uint8_t*)b.cmd();
     tamd_cmd* c = b.cmd();
     memset(c, 0, sizeof(tamd_cmd));
@@ -278,25 +291,27 @@ void Server::post(CmdBuf& b) {
     // six tagged granules, 8-byte stores (each one atomic): the dispatcher takes the slot once
     // every tag is this command's
     const uint64_t cmd = (uint64_t)(uintptr_t)b.cmd(), done = (uint64_t)(uintptr_t)b.done();
+    // the command and the packets it lands, when they were written through the BAR
+    // (write-combined), leave the CPU before its descriptor does (PCIe keeps posted writes in order)
+    _mm_sfence();
     volatile uint64_t* g = s->g;
     g[0] = tamd_granule(idx, (uint32_t)cmd);
     g[1] = tamd_granule(idx, (uint32_t)(cmd >> 32));
     g[2] = tamd_granule(idx, (uint32_t)done);
     g[3] = tamd_granule(idx, (uint32_t)(done >> 32));
     g[4] = tamd_granule(idx, (uint32_t)(idx + 1));
-    g[5] = tamd_granule(idx, b.cmd()->bytes);
+    g[5] = tamd_granule(idx, b.bytes);
     if (stall) stall_pending_.store(false);
     b.ticket = idx;
     b.busy = true;
     if (stamps_) {
         b.posted_us = now_us();
-        const tamd_cmd* c = b.cmd();
         std::lock_guard<std::mutex> lk(stamp_mu_);
-        shape_[0] += c->levels;
-        shape_[1] += c->n_items;
-        shape_[2] += c->n_instr;
-        shape_[3] += c->n_up;
-        shape_[4] += c->bytes;
+        shape_[0] += b.shape[0];
+        shape_[1] += b.shape[1];
+        shape_[2] += b.shape[2];
+        shape_[3] += b.shape[3];
+        shape_[4] += b.bytes;
         shape_n_++;
     }
     posted.fetch_add(1, std::memory_order_relaxed);
@@ -389,7 +404,8 @@ bool Server::completed(CmdBuf& b) {
     return true;
 }
 
-// Spin on the completion word for spin_us_, then park (server.h Parked): the poller wakes the caller
+// Spin on the completion word for spin_us_, spin and yield up to yield_us_ (a command that lands
+// just after the spin costs no wake-up), then park (server.h Parked): the poller wakes the caller
 // when the word is written; the caller also wakes every millisecond to check the executor's life
 // (idle exit, timeout, dead server) as the spinning loop does.
 bool Server::wait_parked(CmdBuf& b, double t0) {
@@ -432,7 +448,11 @@ bool Server::wait_parked(CmdBuf& b, double t0) {
             fprintf(stderr, "tonk_amd: the persistent executor is off; using kernel launches\n");
             return false;
         }
-        if (!parked && t > spin_us_) {
+        if (!parked && t > spin_us_ && t <= yield_us_) {
+            sched_yield();
+            continue;
+        }
+        if (!parked && t > yield_us_) {
             std::call_once(poller_once_, [this] { poller_ = std::thread([this] { poller_loop(); }); });
             {
                 std::lock_guard<std::mutex> lk(park_mu_);

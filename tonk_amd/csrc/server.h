@@ -21,16 +21,35 @@
 namespace tamd {
 
 // A codec's command buffer: [0, 128) completion words (done, start, end), then the command.
+// With `bar` the buffer is device memory the host writes through the PCIe BAR (Device::bar_alloc:
+// the executor copies the command at HBM latency); its completion words, which the host polls,
+// then live in a pinned block of their own (`head`).  The host never reads a BAR buffer.
 struct CmdBuf {
     uint8_t* mem = nullptr;
     size_t cap = 0;
     uint64_t ticket = 0;   // ring index of the command in flight from this buffer
     double posted_us = 0;  // (watchdog stamps)
     bool busy = false;     // posted and not yet waited for
+    bool bar = false;
+    uint8_t* head = nullptr;  // (bar) pinned completion words
+    uint32_t bytes = 0;       // the command's size (Server::build)
+    uint32_t shape[4] = {0, 0, 0, 0};  // levels, items, instructions, uploads (watchdog stamps)
     static const size_t kHead = 128;
     volatile uint64_t* done_at = nullptr;  // completion words (null: the buffer's head)
     volatile uint64_t* done() const { return done_at ? done_at : (volatile uint64_t*)mem; }
     tamd_cmd* cmd() const { return (tamd_cmd*)(mem + kHead); }
+    void release() {  // (the command must be complete)
+        if (bar) {
+            Device::bar_free(mem);
+            Device::host_free(head);
+            head = nullptr;
+            done_at = nullptr;
+        } else {
+            Device::host_free(mem);
+        }
+        mem = nullptr;
+        cap = 0;
+    }
 };
 
 class Server {
@@ -109,7 +128,8 @@ private:
     std::thread poller_;
     std::once_flag poller_once_;
     std::atomic<bool> poller_stop_{false};
-    double spin_us_ = 30.0;  // TONK_AMD_WAIT_SPIN_US: spin this long before parking
+    double spin_us_ = 30.0;   // TONK_AMD_WAIT_SPIN_US: spin this long,
+    double yield_us_ = 150.0; // TONK_AMD_WAIT_YIELD_US: then spin and yield up to this long, then park
     bool park_ = true;       // TONK_AMD_WAIT_PARK=0: the round-5 yield/sleep polling (A/B)
     void poller_loop();
     void unpark(Parked& p);
