@@ -110,8 +110,10 @@ struct Runtime {
 Server* g_srv = nullptr;
 // The codecs' staging halves and command buffers in device memory the host writes through the
 // PCIe BAR (Device::bar_alloc): the executor then copies commands and lands packets at HBM
-// latency instead of pulling them across PCIe.  TONK_AMD_CAPI_BAR=0: pinned host memory.
-bool g_bar = false;
+// latency instead of pulling them across PCIe.  TONK_AMD_CAPI_BAR: a mask of what goes there
+// (1 staging halves, 2 command buffers, 4 the executor's ring -- server.cpp; default 7; 0: all in
+// pinned host memory).
+unsigned g_bar = 0;
 
 struct DevLock {
     std::unique_lock<std::mutex> lk;
@@ -403,8 +405,8 @@ struct Codec {
         ctx.short_scans = short_scans;  // (A/B: 0 restores the chain level)
         static std::atomic<unsigned> next{0};
         staging.stream = next.fetch_add(1) % g_rt->dev.stream_count();
-        staging.bar = g_bar;
-        staging.cmd[0].bar = staging.cmd[1].bar = g_bar;
+        staging.bar = (g_bar & 1u) != 0;
+        staging.cmd[0].bar = staging.cmd[1].bar = (g_bar & 2u) != 0;
     }
     uint64_t byte_offset(RowId r) const { return (uint64_t)ctx.rows.offset(r) * TAMD_ROW_UNIT; }
     // The pinned buffer holds at least n bytes (no copy can be landing in it: every read into it
@@ -827,9 +829,10 @@ SIAMESE_EXPORT int siamese_init_(int version) {
             } else {
                 g_srv = srv;
                 atexit([] { if (g_srv) g_srv->stop(); });
-                if (!(getenv("TONK_AMD_CAPI_BAR") && atoi(getenv("TONK_AMD_CAPI_BAR")) == 0)) {
+                const unsigned want = getenv("TONK_AMD_CAPI_BAR") ? (unsigned)atoi(getenv("TONK_AMD_CAPI_BAR")) : 7u;
+                if (want & 3u) {
                     void* p = Device::bar_alloc(4096);  // (maps the first slab now)
-                    g_bar = p != nullptr;
+                    g_bar = p ? want : 0u;
                     Device::bar_free(p);
                 }
             }

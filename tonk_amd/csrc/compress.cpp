@@ -478,7 +478,7 @@ extern "C" int tamd_compress_batch(const void* dev_data, uint64_t stride, uint32
     // profiling only: TONK_AMD_LZ_PROF=1 prints the phase totals of the launch (lz.hip LZ_PHASE)
     static const bool prof_on = getenv("TONK_AMD_LZ_PROF") != nullptr;
     unsigned long long* d_prof = nullptr;
-    if (ok && prof_on) ok = hipMalloc((void**)&d_prof, jobs.size() * 5 * 8) == hipSuccess;
+    if (ok && prof_on) ok = hipMalloc((void**)&d_prof, jobs.size() * TAMD_LZ_PHASES * 8) == hipSuccess;
     if (ok) {
         const uint32_t nj = (uint32_t)jobs.size();
         hipExtLaunchKernelGGL(tamd_lz_compress, dim3((nj + kLzJobsPerGroup - 1) / kLzJobsPerGroup),
@@ -487,15 +487,15 @@ extern "C" int tamd_compress_batch(const void* dev_data, uint64_t stride, uint32
         ok = hipGetLastError() == hipSuccess;
     }
     if (ok && d_prof) {
-        std::vector<unsigned long long> h(jobs.size() * 5);
+        std::vector<unsigned long long> h(jobs.size() * TAMD_LZ_PHASES);
         ok = hipMemcpyAsync(h.data(), d_prof, h.size() * 8, hipMemcpyDeviceToHost, st) == hipSuccess &&
              hipStreamSynchronize(st) == hipSuccess;
-        double t[5] = {0, 0, 0, 0, 0};
+        double t[TAMD_LZ_PHASES] = {0, 0, 0, 0, 0, 0, 0, 0};
         for (size_t j = 0; j < jobs.size(); ++j)
-            for (int k = 0; k < 5; ++k) t[k] += (double)h[5 * j + k];
-        fprintf(stderr, "lz phases (us per job): window %.1f probe %.1f parse %.1f fse %.1f out %.1f\n",
-                t[0] / jobs.size() / 100.0, t[1] / jobs.size() / 100.0, t[2] / jobs.size() / 100.0,
-                t[3] / jobs.size() / 100.0, t[4] / jobs.size() / 100.0);
+            for (uint32_t k = 0; k < TAMD_LZ_PHASES; ++k) t[k] += (double)h[TAMD_LZ_PHASES * j + k];
+        const double q = 100.0 * (double)jobs.size();
+        fprintf(stderr, "lz phases (us per job): window %.1f probe %.1f parse %.1f codes+tables %.1f chains %.1f "
+                "stream %.1f out %.1f\n", t[0] / q, t[1] / q, t[2] / q, t[5] / q, t[6] / q, t[3] / q, t[4] / q);
         hipFree(d_prof);
     }
     ok = ok && hipMemcpyAsync(written_host, d_written, total * 4, hipMemcpyDeviceToHost, st) == hipSuccess;

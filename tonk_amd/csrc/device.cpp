@@ -2,6 +2,7 @@
 #include "device.h"
 
 #include <hip/hip_runtime.h>
+#include <immintrin.h>
 #include <hip/hip_ext.h>
 #include <algorithm>
 #include <chrono>
@@ -1251,7 +1252,9 @@ void Device::scatter_upload(uint8_t* src, size_t bytes, const ScatterIn* d, uint
         if (!sc_per_stream_.empty()) sc_per_stream_[cur_stream_] = std::make_pair(sc_dev_, sc_cap_);
     }
     // (the landing area is reused batch after batch: copies and scatters are stream ordered)
-    // (hipMemcpyDefault: the C ABI's staging may be BAR-written device memory)
+    // (hipMemcpyDefault: the C ABI's staging may be BAR-written device memory, whose
+    // write-combined stores -- packets and the descriptors above -- must be out before the copy)
+    _mm_sfence();
     HIPCHK(hipMemcpyAsync(sc_dev_, src, total, hipMemcpyDefault, st));
     HIPT(hipLaunchKernelGGL(tamd_scatter_rows, dim3(n), dim3(64), 0, st, (const ScatterDescDev*)(sc_dev_ + at), n,
                        (const uint8_t*)sc_dev_, arena_));
@@ -1309,6 +1312,7 @@ void Device::flush_host_reads() {
 
 void Device::host_copy(const HostCopy* d, uint32_t n, bool to_host) {
     if (!n) return;
+    _mm_sfence();  // (sources the host wrote through the BAR, write-combined: out before the launch)
     flush_uploads();
     hipStream_t st = (hipStream_t)stream_;
     // a descriptor buffer whose previous launch has read it: the next one in turn that is free,

@@ -12,6 +12,7 @@
 #define TAMD_LZ_WINDOW 32768u      // history bytes inserted into a job's hash table
 #define TAMD_LZ_RING 65536u        // per-compressor device ring of the stream's bytes (the drop-in)
 #define TAMD_LZ_MIRROR 64u         // the ring's first bytes repeated after it (wide loads at its end)
+#define TAMD_LZ_PHASES 8u          // (profiling: 100 MHz ticks per job and phase, TONK_AMD_LZ_PROF)
 
 // The drop-in's staging: message bytes land in their compressor's ring (one workgroup each).
 typedef struct tamd_lz_scatter {

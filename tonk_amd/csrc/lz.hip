@@ -75,7 +75,7 @@ struct LzWave {
     // fitted tables' normalized counts, state offsets and states (tamd_fit_states)
     uint32_t fdesc[3][TAMD_FIT_DESC / 4];
     uint32_t fstarts[3];  // bit g: some symbol's share of the 32 states starts at occurrence g
-    uint8_t fnorm[3][64], fcum[3][64], fstate[3][TAMD_FIT_SIZE], gsym[TAMD_FIT_SIZE];
+    uint8_t fnorm[3][64], fcum[3][64], fstate[3][TAMD_FIT_SIZE], gsym[3][TAMD_FIT_SIZE];
 };
 
 // Wave sums (DPP row shifts: a few instructions) and exclusive prefix sums of B-bit values, a bit
@@ -293,69 +293,104 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
             atomicAdd(&hist[128u + (cd >> 16)], 1u);
         }
         LZ_SYNC();
-        // each table's mode (tamd_seq_choose restated a lane per symbol)
+        // each table's mode (tamd_seq_choose restated a lane per symbol), the three tables side by
+        // side: their chains of wave operations are independent, so each one's latency hides the
+        // others' (one wave per SIMD here)
         const bool fit_on = !(fse[TAMD_FSE_FLAGS] & TAMD_FSE_PREDEFINED_ONLY);
+        uint32_t cnt[3], nrm[3], present[3], last[3], best[3], cum[3] = {0, 0, 0}, w[3] = {0, 0, 0};
+        uint64_t pres[3], v[3] = {0, 0, 0};
+        bool cand[3];
+#pragma unroll
         for (uint32_t k = 0; k < 3; ++k) {
             const uint32_t nsym = k == 0 ? 36u : k == 1 ? 53u : 32u, plog = k == 2 ? 5u : 6u;
-            const uint32_t cnt = lane < nsym ? hist[64u * k + lane] : 0u;
-            uint32_t nrm = tamd_fit_norm(cnt, nseq);
-            const uint64_t pres = __ballot(cnt != 0);
-            const uint32_t present = (uint32_t)__builtin_popcountll(pres), last = 63u - (uint32_t)__builtin_clzll(pres);
-            const uint32_t pre = lz_wave_sum(cnt * fse[TAMD_FSE_PCOST + 64u * k + lane]) + 16u * plog;
-            uint32_t md = TAMD_MODE_PREDEF, best = pre, dl = 0;
-            if (present == 1u && 16u * 8u < best && fit_on) {
-                md = TAMD_MODE_RLE;
-                best = 16u * 8u;
-                dl = 1;
+            cnt[k] = lane < nsym ? hist[64u * k + lane] : 0u;
+            nrm[k] = tamd_fit_norm(cnt[k], nseq);
+            pres[k] = __ballot(cnt[k] != 0);
+            present[k] = (uint32_t)__builtin_popcountll(pres[k]);
+            last[k] = 63u - (uint32_t)__builtin_clzll(pres[k]);
+            best[k] = lz_wave_sum(cnt[k] * fse[TAMD_FSE_PCOST + 64u * k + lane]) + 16u * plog;
+            if (present[k] == 1u && 16u * 8u < best[k] && fit_on) {
+                mode[k] = TAMD_MODE_RLE;
+                best[k] = 16u * 8u;
+                dlen[k] = 1;
             }
-            if (present >= 2u && present <= TAMD_FIT_SIZE && nseq >= TAMD_FIT_MIN_SEQS && fit_on) {
-                const uint32_t sum = lz_wave_sum(nrm);
-                // the largest share, lowest symbol on ties: bit planes from the top
-                uint64_t cand = pres;
+            cand[k] = present[k] >= 2u && present[k] <= TAMD_FIT_SIZE && nseq >= TAMD_FIT_MIN_SEQS && fit_on;
+        }
+        if (cand[0] || cand[1] || cand[2]) {
+            uint32_t sum[3], big[3];
+            uint64_t top[3];
 #pragma unroll
-                for (uint32_t b = 6; b-- > 0;) {
-                    const uint64_t m = cand & __ballot((nrm >> b) & 1u);
-                    if (m) cand = m;
+            for (uint32_t k = 0; k < 3; ++k) {
+                sum[k] = lz_wave_sum(nrm[k]);
+                top[k] = pres[k];
+            }
+            // the largest share, lowest symbol on ties: bit planes from the top
+#pragma unroll
+            for (uint32_t b = 6; b-- > 0;)
+#pragma unroll
+                for (uint32_t k = 0; k < 3; ++k) {
+                    const uint64_t m = top[k] & __ballot((nrm[k] >> b) & 1u);
+                    if (m) top[k] = m;
                 }
-                const uint32_t big = (uint32_t)__builtin_ctzll(cand);
-                const int32_t fixed = (int32_t)__builtin_amdgcn_readlane((int)nrm, (int)big) + (int32_t)TAMD_FIT_SIZE - (int32_t)sum;
-                if (fixed >= 1) {
-                if (lane == big) nrm = (uint32_t)fixed;
-                const uint32_t cum = lz_wave_excl<6>(nrm);
-                const uint64_t nz = __ballot(nrm != 0);
+#pragma unroll
+            for (uint32_t k = 0; k < 3; ++k) {
+                big[k] = (uint32_t)__builtin_ctzll(top[k]);
+                const int32_t fixed = (int32_t)__builtin_amdgcn_readlane((int)nrm[k], (int)big[k]) + (int32_t)TAMD_FIT_SIZE - (int32_t)sum[k];
+                cand[k] = cand[k] && fixed >= 1;
+                if (cand[k] && lane == big[k]) nrm[k] = (uint32_t)fixed;
+            }
+            uint32_t wsum[3], fit[3];
+#pragma unroll
+            for (uint32_t k = 0; k < 3; ++k) {
+                cum[k] = lz_wave_excl<6>(nrm[k]);
+                const uint64_t nz = __ballot(nrm[k] != 0);
                 const bool lead = lane == 0 || ((nz >> (lane - 1u)) & 1ull) != 0;
                 const uint64_t above = nz & ~((2ull << lane) - 1ull);
-                const uint32_t z = nrm == 0 && above ? (uint32_t)__builtin_ctzll(above) - lane - 1u : 0u;
-                uint64_t v = 0;
-                const uint32_t w = lane <= last ? tamd_ncount_item(nrm, cum, lead, z, &v) : 0u;
-                const uint32_t wsum = lz_wave_sum(w);
-                const uint32_t fit = lz_wave_sum(cnt * fse[TAMD_FSE_FCOST + nrm]) + 16u * (TAMD_FIT_LOG + 4u + wsum);
-                if (fit < best) {
-                    md = TAMD_MODE_FSE;
-                    dl = (4u + wsum + 7u) / 8u;
-                    // the description's bits, then the encoder's states (tamd_fit_states)
-                    const uint32_t at = 4u + lz_wave_excl<6>(w);
-                    if (w) {
-                        uint32_t* d = L.fdesc[k];
-                        const uint32_t w0 = at / 32u, sh = at % 32u;
-                        atomicOr(&d[w0], (uint32_t)(v << sh));
-                        if (sh + w > 32u) atomicOr(&d[w0 + 1], (uint32_t)(v >> (32u - sh)));
-                        if (sh + w > 64u) atomicOr(&d[w0 + 2], (uint32_t)(v >> (64u - sh)));
-                    }
-                    L.fnorm[k][lane] = (uint8_t)nrm;
-                    L.fcum[k][lane] = (uint8_t)cum;
-                    // occurrence g belongs to the symbol whose share starts at the last start <= g
-                    if (nrm) {
-                        L.gsym[cum] = (uint8_t)lane;
-                        atomicOr(&L.fstarts[k], 1u << cum);
-                    }
-                    LZ_SYNC();
+                const uint32_t z = nrm[k] == 0 && above ? (uint32_t)__builtin_ctzll(above) - lane - 1u : 0u;
+                w[k] = cand[k] && lane <= last[k] ? tamd_ncount_item(nrm[k], cum[k], lead, z, &v[k]) : 0u;
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < 3; ++k) {
+                wsum[k] = lz_wave_sum(w[k]);
+                fit[k] = lz_wave_sum(cnt[k] * fse[TAMD_FSE_FCOST + nrm[k]]) + 16u * (TAMD_FIT_LOG + 4u + wsum[k]);
+                if (cand[k] && fit[k] < best[k]) {
+                    mode[k] = TAMD_MODE_FSE;
+                    dlen[k] = (4u + wsum[k] + 7u) / 8u;
+                }
+            }
+            // the fitted tables' descriptions, then the encoder's states (tamd_fit_states)
+            bool any = false;
+#pragma unroll
+            for (uint32_t k = 0; k < 3; ++k) {
+                if (mode[k] != TAMD_MODE_FSE) continue;
+                any = true;
+                const uint32_t at = 4u + lz_wave_excl<6>(w[k]);
+                if (w[k]) {
+                    uint32_t* d = L.fdesc[k];
+                    const uint32_t w0 = at / 32u, sh = at % 32u;
+                    atomicOr(&d[w0], (uint32_t)(v[k] << sh));
+                    if (sh + w[k] > 32u) atomicOr(&d[w0 + 1], (uint32_t)(v[k] >> (32u - sh)));
+                    if (sh + w[k] > 64u) atomicOr(&d[w0 + 2], (uint32_t)(v[k] >> (64u - sh)));
+                }
+                L.fnorm[k][lane] = (uint8_t)nrm[k];
+                L.fcum[k][lane] = (uint8_t)cum[k];
+                // occurrence g belongs to the symbol whose share starts at the last start <= g
+                if (nrm[k]) {
+                    L.gsym[k][cum[k]] = (uint8_t)lane;
+                    atomicOr(&L.fstarts[k], 1u << cum[k]);
+                }
+            }
+            if (any) {
+                LZ_SYNC();
+                // state u decodes the symbol spread to slot u: occurrence g = u * 7 (mod 32); its
+                // rank among that symbol's states is the number of smaller u with it
+                const bool in = lane < TAMD_FIT_SIZE;
+                const uint32_t g = (lane * TAMD_FIT_STEP_INV) & (TAMD_FIT_SIZE - 1u);
+#pragma unroll
+                for (uint32_t k = 0; k < 3; ++k) {
+                    if (mode[k] != TAMD_MODE_FSE) continue;
                     const uint32_t starts = L.fstarts[k];
-                    // state u decodes the symbol spread to slot u: occurrence g = u * 7 (mod 32);
-                    // its rank among that symbol's states is the number of smaller u with it
-                    const bool in = lane < TAMD_FIT_SIZE;
-                    const uint32_t g = (lane * TAMD_FIT_STEP_INV) & (TAMD_FIT_SIZE - 1u);
-                    const uint32_t sym = in ? L.gsym[31u - (uint32_t)__builtin_clz(starts & ((2u << g) - 1u))] : 0u;
+                    const uint32_t sym = in ? L.gsym[k][31u - (uint32_t)__builtin_clz(starts & ((2u << g) - 1u))] : 0u;
                     uint64_t same = __ballot(in);
 #pragma unroll
                     for (uint32_t b = 0; b < 6; ++b) {
@@ -365,18 +400,32 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
                     const uint32_t rank = (uint32_t)__builtin_popcountll(same & ((1ull << lane) - 1ull));
                     if (in) L.fstate[k][L.fcum[k][sym] + rank] = (uint8_t)lane;
                 }
-                }
             }
-            if (md == TAMD_MODE_RLE && lane == 0) L.fdesc[k][0] = 63u - __builtin_clzll(pres);
-            mode[k] = md;
-            dlen[k] = dl;
         }
+        if (lane == 0)
+#pragma unroll
+            for (uint32_t k = 0; k < 3; ++k)
+                if (mode[k] == TAMD_MODE_RLE) L.fdesc[k][0] = 63u - __builtin_clzll(pres[k]);
         LZ_SYNC();
         seq_word |= tamd_modes_byte(mode) << (8u * (shb - 1u));
         head += dlen[0] + dlen[1] + dlen[2];
         ok = head < limit;
     }
+    LZ_PHASE(5)
     if (ok) {
+        if (mode[0] == TAMD_MODE_FSE || mode[1] == TAMD_MODE_FSE || mode[2] == TAMD_MODE_FSE) {
+            // the fitted tables' share | offset << 6 of every sequence's code, in its update slot
+            for (uint32_t sq = lane; sq + 1u < nseq; sq += 64) {
+                const uint32_t cd = code[sq];
+#pragma unroll
+                for (uint32_t t = 0; t < 3; ++t)
+                    if (mode[t] == TAMD_MODE_FSE) {
+                        const uint32_t c = (cd >> (8u * t)) & 0xffu;
+                        upd[S * t + sq] = (uint16_t)(L.fnorm[t][c] | (uint32_t)L.fcum[t][c] << 6);
+                    }
+            }
+            LZ_SYNC();
+        }
         if (lane < 3) {
             const uint32_t shift = 8u * lane, size = lane == 2 ? 32u : 64u;
             const uint32_t md = lane == 0 ? mode[0] : lane == 1 ? mode[1] : mode[2];
@@ -387,11 +436,15 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
                 const uint8_t* nm = L.fnorm[lane];
                 const uint8_t* cm = L.fcum[lane];
                 const uint8_t* sv = L.fstate[lane];
-                uint32_t u, c = (code[nseq - 1] >> shift) & 0xffu;
+                uint32_t u;
+                const uint32_t c = (code[nseq - 1] >> shift) & 0xffu;
                 st = tamd_fit_step(nm[c], cm[c], sv, 0, &u);
+                // (each step's symbol share and offset were put in its update slot beforehand: the
+                // only load that waits for the previous step is the state's)
+#pragma unroll 4
                 for (uint32_t sq = nseq - 1; sq-- > 0;) {
-                    c = (code[sq] >> shift) & 0xffu;
-                    st = tamd_fit_step(nm[c], cm[c], sv, st, &u);
+                    const uint32_t inf = u_out[sq];
+                    st = tamd_fit_step(inf & 63u, inf >> 6, sv, st, &u);
                     u_out[sq] = (uint16_t)u;
                 }
             } else if (md == TAMD_MODE_PREDEF) {
@@ -404,6 +457,7 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
             }  // (RLE: no state bits)
             L.sh_init[lane] = st;
         }
+        LZ_PHASE(6)
         // zero the bit buffer words the stream can use
         const uint32_t cap_words = (limit - head + 3u) / 4u + 1u;
         const uint32_t wcap = cap_words < bw_cap ? cap_words : bw_cap;
@@ -538,7 +592,7 @@ tamd_lz_compress(const tamd_lz_job* __restrict__ jobs, uint32_t n_jobs, const ta
     LzWave& L = W[wave];
     const tamd_lz_job job = jobs[ji];
     // profiling only (TONK_AMD_LZ_PROF): per job, 100 MHz ticks spent in each phase
-    unsigned long long ph[5] = {0, 0, 0, 0, 0}, t_ph = prof ? __builtin_amdgcn_s_memrealtime() : 0;
+    unsigned long long ph[TAMD_LZ_PHASES] = {0, 0, 0, 0, 0, 0, 0, 0}, t_ph = prof ? __builtin_amdgcn_s_memrealtime() : 0;
     const uint8_t* __restrict__ buf = job.buf;
     const uint32_t mask = job.mask;
     for (uint32_t i = lane; i < LZ_HASH; i += 64) L.htab[i] = 0;
@@ -593,7 +647,7 @@ tamd_lz_compress(const tamd_lz_job* __restrict__ jobs, uint32_t n_jobs, const ta
     }
     if (prof && lane == 0)
 #pragma unroll
-        for (uint32_t k = 0; k < 5; ++k) prof[5 * ji + k] = ph[k];
+        for (uint32_t k = 0; k < TAMD_LZ_PHASES; ++k) prof[TAMD_LZ_PHASES * ji + k] = ph[k];
 }
 
 // The per-message drop-in's staging (compress.cpp): each message of a combined batch is copied

@@ -56,7 +56,17 @@ bool Server::init(Device& dev, unsigned workers, unsigned ring_size, double idle
     if (yield_us_ < spin_us_) yield_us_ = spin_us_;
     if (const char* e = getenv("TONK_AMD_WAIT_PARK")) park_ = atoi(e) != 0;
     stamps_ = getenv("TONK_AMD_CAPI_WATCH") != nullptr;
-    ring_ = (tamd_serve_slot*)coherent_alloc((size_t)ring_size_ * sizeof(tamd_serve_slot));
+    // The ring in device memory the host writes through the BAR (the dispatcher then polls HBM,
+    // not host memory across PCIe), unless TONK_AMD_CAPI_BAR leaves out bit 4 or that memory is
+    // unavailable.
+    const size_t ring_bytes = (size_t)ring_size_ * sizeof(tamd_serve_slot);
+    if ((getenv("TONK_AMD_CAPI_BAR") ? (atoi(getenv("TONK_AMD_CAPI_BAR")) & 4) != 0 : true) &&
+        (ring_ = (tamd_serve_slot*)Device::bar_alloc(ring_bytes))) {
+        for (size_t i = 0; i < ring_bytes / 8; ++i) ((volatile uint64_t*)ring_)[i] = 0;
+        _mm_sfence();
+    } else {
+        ring_ = (tamd_serve_slot*)coherent_alloc(ring_bytes);
+    }
     host_ = (volatile tamd_serve_host*)coherent_alloc(sizeof(tamd_serve_host));
     if (!ring_ || !host_) return false;
     const size_t dbytes = sizeof(tamd_serve_dev) + (size_t)ring_size_ * sizeof(tamd_serve_slot);
