@@ -111,8 +111,9 @@ Server* g_srv = nullptr;
 // The codecs' staging halves and command buffers in device memory the host writes through the
 // PCIe BAR (Device::bar_alloc): the executor then copies commands and lands packets at HBM
 // latency instead of pulling them across PCIe.  TONK_AMD_CAPI_BAR: a mask of what goes there
-// (1 staging halves, 2 command buffers, 4 the executor's ring -- server.cpp; default 7; 0: all in
-// pinned host memory).
+// (1 staging halves, 2 command buffers, 4 the executor's ring -- server.cpp; 0: all in pinned
+// host memory).  Default 6: staging in BAR memory makes every add a PCIe write on the caller's
+// thread, which cost more than the faster landing saved (profiles/r06m_capi_bar_placement.txt).
 unsigned g_bar = 0;
 
 struct DevLock {
@@ -829,7 +830,7 @@ SIAMESE_EXPORT int siamese_init_(int version) {
             } else {
                 g_srv = srv;
                 atexit([] { if (g_srv) g_srv->stop(); });
-                const unsigned want = getenv("TONK_AMD_CAPI_BAR") ? (unsigned)atoi(getenv("TONK_AMD_CAPI_BAR")) : 7u;
+                const unsigned want = getenv("TONK_AMD_CAPI_BAR") ? (unsigned)atoi(getenv("TONK_AMD_CAPI_BAR")) : 6u;
                 if (want & 3u) {
                     void* p = Device::bar_alloc(4096);  // (maps the first slab now)
                     g_bar = p ? want : 0u;
