@@ -334,15 +334,20 @@ TAMD_HD static inline void tamd_fit_states(const uint8_t* norm, uint32_t nsym, u
 // One step of a fitted table's state chain (FSE_encodeSymbol): the decoder must reach state `st`
 // after the symbol (norm n, cum c); returns the state that decodes it, *upd = the bits the decoder
 // reads to get from there to `st` | their number << 8.
-TAMD_HD static inline uint32_t tamd_fit_step(uint32_t n, uint32_t c, const uint8_t* state, uint32_t st, uint32_t* upd) {
+// (the most bits a step out of one of the symbol's states reads: the accuracy log for a single
+// state, else log - highbit(n - 1); a state value S below n << mbo reads one bit fewer)
+TAMD_HD static inline uint32_t tamd_fit_mbo(uint32_t n) {
+    return n > 1u ? TAMD_FIT_LOG - (31u - (uint32_t)__builtin_clz(n - 1u)) : TAMD_FIT_LOG;
+}
+TAMD_HD static inline uint32_t tamd_fit_step_m(uint32_t n, uint32_t c, uint32_t mbo, const uint8_t* state, uint32_t st,
+                                              uint32_t* upd) {
     const uint32_t S = TAMD_FIT_SIZE + st;
-    uint32_t nb = TAMD_FIT_LOG;
-    if (n > 1u) {
-        const uint32_t mbo = TAMD_FIT_LOG - (31u - (uint32_t)__builtin_clz(n - 1u));
-        nb = S >= (n << mbo) ? mbo : mbo - 1u;
-    }
+    const uint32_t nb = S >= (n << mbo) ? mbo : mbo - 1u;
     *upd = (S & ((1u << nb) - 1u)) | (nb << 8);
     return state[c + (S >> nb) - n];
+}
+TAMD_HD static inline uint32_t tamd_fit_step(uint32_t n, uint32_t c, const uint8_t* state, uint32_t st, uint32_t* upd) {
+    return tamd_fit_step_m(n, c, tamd_fit_mbo(n), state, st, upd);
 }
 
 // A block's three tables (index 0 literal lengths, 1 match lengths, 2 offsets, as the codes are

@@ -34,6 +34,8 @@
 // LZ_MAX_SEQS halfwords).
 #define LZ_CH (LZ_MAX_SEQS + 3u * LZ_MAX_SEQS / 2u)
 #define LZ_WAVES 2  // jobs per workgroup: the waves share the FSE maps (2 workgroups per CU)
+#define LZ_COST_BYTES (TAMD_FSE_BYTES - TAMD_FSE_PCOST)  // costs and flags, in LDS after the maps
+static_assert(TAMD_FSE_PCOST == TAMD_FSE_E16 + 2u * TAMD_FSE_E16_WORDS && LZ_COST_BYTES % 4u == 0u, "blob layout");
 
 // Byte loads of a stream: `buf` at linear position p & mask.  Multi-byte loads are unaligned
 // global loads; the buffers carry readable slack past their end (a linear stream: 32 bytes past
@@ -296,7 +298,8 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
         // each table's mode (tamd_seq_choose restated a lane per symbol), the three tables side by
         // side: their chains of wave operations are independent, so each one's latency hides the
         // others' (one wave per SIMD here)
-        const bool fit_on = !(fse[TAMD_FSE_FLAGS] & TAMD_FSE_PREDEFINED_ONLY);
+        const uint8_t* costs = (const uint8_t*)(e16 + TAMD_FSE_E16_WORDS);  // (LDS: the blob from TAMD_FSE_PCOST)
+        const bool fit_on = !(costs[TAMD_FSE_FLAGS - TAMD_FSE_PCOST] & TAMD_FSE_PREDEFINED_ONLY);
         uint32_t cnt[3], nrm[3], present[3], last[3], best[3], cum[3] = {0, 0, 0}, w[3] = {0, 0, 0};
         uint64_t pres[3], v[3] = {0, 0, 0};
         bool cand[3];
@@ -308,7 +311,7 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
             pres[k] = __ballot(cnt[k] != 0);
             present[k] = (uint32_t)__builtin_popcountll(pres[k]);
             last[k] = 63u - (uint32_t)__builtin_clzll(pres[k]);
-            best[k] = lz_wave_sum(cnt[k] * fse[TAMD_FSE_PCOST + 64u * k + lane]) + 16u * plog;
+            best[k] = lz_wave_sum(cnt[k] * costs[64u * k + lane]) + 16u * plog;
             if (present[k] == 1u && 16u * 8u < best[k] && fit_on) {
                 mode[k] = TAMD_MODE_RLE;
                 best[k] = 16u * 8u;
@@ -352,7 +355,8 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
 #pragma unroll
             for (uint32_t k = 0; k < 3; ++k) {
                 wsum[k] = lz_wave_sum(w[k]);
-                fit[k] = lz_wave_sum(cnt[k] * fse[TAMD_FSE_FCOST + nrm[k]]) + 16u * (TAMD_FIT_LOG + 4u + wsum[k]);
+                fit[k] = lz_wave_sum(cnt[k] * costs[TAMD_FSE_FCOST - TAMD_FSE_PCOST + nrm[k]]) +
+                         16u * (TAMD_FIT_LOG + 4u + wsum[k]);
                 if (cand[k] && fit[k] < best[k]) {
                     mode[k] = TAMD_MODE_FSE;
                     dlen[k] = (4u + wsum[k] + 7u) / 8u;
@@ -414,14 +418,16 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
     LZ_PHASE(5)
     if (ok) {
         if (mode[0] == TAMD_MODE_FSE || mode[1] == TAMD_MODE_FSE || mode[2] == TAMD_MODE_FSE) {
-            // the fitted tables' share | offset << 6 of every sequence's code, in its update slot
+            // the fitted tables' share | offset << 6 | step bits << 11 of every sequence's code, in
+            // its update slot
             for (uint32_t sq = lane; sq + 1u < nseq; sq += 64) {
                 const uint32_t cd = code[sq];
 #pragma unroll
                 for (uint32_t t = 0; t < 3; ++t)
                     if (mode[t] == TAMD_MODE_FSE) {
                         const uint32_t c = (cd >> (8u * t)) & 0xffu;
-                        upd[S * t + sq] = (uint16_t)(L.fnorm[t][c] | (uint32_t)L.fcum[t][c] << 6);
+                        const uint32_t nn = L.fnorm[t][c];
+                        upd[S * t + sq] = (uint16_t)(nn | (uint32_t)L.fcum[t][c] << 6 | tamd_fit_mbo(nn) << 11);
                     }
             }
             LZ_SYNC();
@@ -444,7 +450,7 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
 #pragma unroll 4
                 for (uint32_t sq = nseq - 1; sq-- > 0;) {
                     const uint32_t inf = u_out[sq];
-                    st = tamd_fit_step(inf & 63u, inf >> 6, sv, st, &u);
+                    st = tamd_fit_step_m(inf & 63u, (inf >> 6) & 31u, inf >> 11, sv, st, &u);
                     u_out[sq] = (uint16_t)u;
                 }
             } else if (md == TAMD_MODE_PREDEF) {
@@ -581,8 +587,10 @@ tamd_lz_compress(const tamd_lz_job* __restrict__ jobs, uint32_t n_jobs, const ta
                  const uint8_t* __restrict__ fse, uint8_t* __restrict__ out, uint32_t* __restrict__ written,
                  uint8_t* __restrict__ scratch, unsigned long long* __restrict__ prof) {
     __shared__ LzWave W[LZ_WAVES];
-    __shared__ uint16_t e16[TAMD_FSE_E16_WORDS];  // FSE encode maps with decode info (lz.h)
-    for (uint32_t i = threadIdx.x; i < TAMD_FSE_E16_WORDS / 2; i += blockDim.x)
+    // FSE encode maps with decode info, then the table costs and flags (lz.h: the blob from
+    // TAMD_FSE_E16 to its end, contiguous)
+    __shared__ uint16_t e16[TAMD_FSE_E16_WORDS + LZ_COST_BYTES / 2];
+    for (uint32_t i = threadIdx.x; i < (TAMD_FSE_E16_WORDS + LZ_COST_BYTES / 2) / 2; i += blockDim.x)
         ((uint32_t*)e16)[i] = ((const uint32_t*)(fse + TAMD_FSE_E16))[i];
     __syncthreads();  // (the only workgroup barrier: from here on the waves are independent)
     const uint32_t lane = threadIdx.x & 63u;
