@@ -17,7 +17,7 @@
 extern "C" __global__ void tamd_lz_compress(const tamd_lz_job*, uint32_t, const tamd_lz_msg*, const uint8_t*,
                                             uint8_t*, uint32_t*, uint8_t*, unsigned long long*);
 // (lz.hip: two jobs per 128-thread workgroup)
-static const uint32_t kLzJobsPerGroup = 2;
+static const uint32_t kLzJobsPerGroup = TAMD_LZ_WAVES;
 extern "C" __global__ void tamd_lz_scatter_ring(const tamd_lz_scatter*, const uint8_t*);
 
 namespace tamd {

@@ -6,7 +6,8 @@
 #include <math.h>
 #include <stdint.h>
 
-#define TAMD_LZ_MAX_MESSAGE 2048u  // messages up to this size are compressed entirely in LDS
+#define TAMD_LZ_MAX_MESSAGE 1536u  // messages up to this size are compressed entirely in LDS
+#define TAMD_LZ_WAVES 8u           // jobs (waves) per workgroup of tamd_lz_compress: 2 waves per SIMD
 #define TAMD_LZ_MAX_BLOCK 131071u  // larger ones (up to zstd's block limit, 128 KB) use global scratch
 #define TAMD_LZ_NO_SCRATCH 0xffffffffu
 #define TAMD_LZ_WINDOW 32768u      // history bytes inserted into a job's hash table
@@ -41,16 +42,16 @@ static inline
 __host__ __device__
 #endif
 uint32_t tamd_lz_big_seqs(uint32_t n) { return n / 4u + 1u; }
-// Scratch of a message above TAMD_LZ_MAX_MESSAGE (lz.hip lz_message<true>): sequences, offsets,
-// literal starts, codes (4 x S words), the bit stream ((n + 64) / 4 + 4 words) and three chains
-// of state updates (3 x S halfwords).
+// Scratch of a message above TAMD_LZ_MAX_MESSAGE (lz.hip lz_message<true>): sequences and offsets
+// (2 x S words), the bit stream ((n + 64) / 4 + 4 words) and three chains of state updates
+// (3 x S halfwords).
 static inline
 #ifdef __HIPCC__
 __host__ __device__
 #endif
 uint32_t tamd_lz_scratch_bytes(uint32_t n) {
     const uint32_t S = tamd_lz_big_seqs(n);
-    return (16u * S + 4u * ((n + 64u) / 4u + 4u) + 6u * S + 15u) & ~15u;
+    return (8u * S + 4u * ((n + 64u) / 4u + 4u) + 6u * S + 15u) & ~15u;
 }
 
 // FSE tables of the predefined distributions, one blob:

@@ -11,8 +11,10 @@
 // code or an FSE table fitted to the block's codes and described in it (round 6; no repeat
 // offsets or repeat tables, so no state carries from block to block).
 //
-// Per message: (1) candidate positions from a hash table of 8-byte keys in LDS (the window's positions
-// are inserted once per job, each message's after it is scanned, 64 at a time), (2) every lane
+// Eight waves per workgroup (two per SIMD: a wave's LDS is 17.5 KB, the FSE maps are shared).
+// Per message: (1) candidate positions from a hash table of 8-byte keys in LDS (16-bit positions
+// relative to the job's base; the window's positions are inserted once per job, each message's
+// after it is scanned, 64 at a time), (2) every lane
 // extends its own candidate, (3) a ballot-driven greedy parse, (4) lane 0 writes the backward
 // FSE bit stream of the sequences into LDS, (5) the wave copies header, literals and bit stream
 // to the output when the block is smaller than the message (else written = 0, as
@@ -22,18 +24,22 @@
 
 #include "lz.h"
 
-#include <type_traits>
-
-#define LZ_HASH_LOG 12
+#define LZ_HASH_LOG 12  // 4K entries of 16 bits: 8 KB per wave, so that 8 waves (2 per SIMD) fit a CU
+#ifndef LZ_WINDOW_LANE16
+#define LZ_WINDOW_LANE16 1
+#endif
+#define LZ_REL_MAX 65535u  // job-relative positions (+ 1) the table can hold
 #define LZ_HASH (1u << LZ_HASH_LOG)
 #define LZ_MIN_MATCH 4u
+#ifndef LZ_PROBE
 #define LZ_PROBE 16u  // bytes a lane compares per candidate; a chosen match is extended by the wave
+#endif
 #define LZ_MAX_SEQS (TAMD_LZ_MAX_MESSAGE / LZ_MIN_MATCH)
 // Candidates are found and parsed LZ_CH positions at a time; after the parse the same words
-// hold the sequences' codes (LZ_MAX_SEQS words) and the three state-update chains (3 x
-// LZ_MAX_SEQS halfwords).
-#define LZ_CH (LZ_MAX_SEQS + 3u * LZ_MAX_SEQS / 2u)
-#define LZ_WAVES 2  // jobs per workgroup: the waves share the FSE maps (2 workgroups per CU)
+// hold the three state-update chains (3 x LZ_MAX_SEQS halfwords).  A sequence's codes are
+// recomputed from its lengths and offset wherever they are needed instead of being stored.
+#define LZ_CH (3u * LZ_MAX_SEQS / 2u)
+#define LZ_WAVES TAMD_LZ_WAVES  // jobs per workgroup: the waves share the FSE maps (1 workgroup per CU)
 #define LZ_COST_BYTES (TAMD_FSE_BYTES - TAMD_FSE_PCOST)  // costs and flags, in LDS after the maps
 static_assert(TAMD_FSE_PCOST == TAMD_FSE_E16 + 2u * TAMD_FSE_E16_WORDS && LZ_COST_BYTES % 4u == 0u, "blob layout");
 
@@ -65,13 +71,12 @@ static __device__ __forceinline__ uint32_t lz_hash(uint64_t w) {
 
 // One wave's LDS.
 struct LzWave {
-    uint32_t htab[LZ_HASH];                                   // (position + 1), 0 = empty
+    uint16_t htab[LZ_HASH];  // (position - job base + 1), 0 = empty
     uint32_t mword[LZ_CH];  // per chunk position: the match there, length | distance << 16
     uint32_t seq_lo[LZ_MAX_SEQS];                             // literal length | match length << 16
     uint32_t seq_off[LZ_MAX_SEQS];                            // offset
     uint32_t bitw[(TAMD_LZ_MAX_MESSAGE + 64) / 4];            // backward FSE bit stream
     __attribute__((aligned(16))) uint8_t mbuf[TAMD_LZ_MAX_MESSAGE + LZ_PROBE + 16];  // the message
-    uint16_t seq_pos[LZ_MAX_SEQS];                            // where each sequence's literals start
     uint32_t sh_init[3], sh_bytes, sh_ok;
     // the block's sequence tables (tamd_seq_choose, a lane per symbol): descriptions, and the
     // fitted tables' normalized counts, state offsets and states (tamd_fit_states)
@@ -79,6 +84,28 @@ struct LzWave {
     uint32_t fstarts[3];  // bit g: some symbol's share of the 32 states starts at occurrence g
     uint8_t fnorm[3][64], fcum[3][64], fstate[3][TAMD_FIT_SIZE], gsym[3][TAMD_FIT_SIZE];
 };
+
+// The hash table keeps each bucket's most recent position, relative to the job's base (lz_rebase).
+// Positions enter it in increasing order, 64 consecutive ones per store (the window, each
+// message's scan), so a later store is always more recent; lanes of one store that share a bucket
+// leave one of theirs (LDS resolves same-address lanes in a fixed order: the output does not
+// vary from run to run, and its ratio equals that of a version that re-stored until the largest
+// stayed, profiles/r06q_lz_occupancy_ab.txt).
+static __device__ __forceinline__ void lz_insert(uint16_t* htab, bool ins, uint32_t h, uint32_t rel) {
+    if (ins) htab[h] = (uint16_t)rel;
+}
+
+// Moves the job's base forward to `to` (> base): entries keep their positions, the ones before
+// `to` become empty.  Only jobs that span more than LZ_REL_MAX bytes (large messages) need it.
+static __device__ __noinline__ void lz_rebase(uint16_t* htab, uint32_t& base, uint32_t to, uint32_t lane) {
+    const uint32_t d = to - base;
+    for (uint32_t k = lane; k < LZ_HASH; k += 64) {
+        const uint32_t e = htab[k];
+        htab[k] = (uint16_t)(e > d ? e - d : 0u);
+    }
+    LZ_SYNC();
+    base = to;
+}
 
 // Wave sums (DPP row shifts: a few instructions) and exclusive prefix sums of B-bit values, a bit
 // plane at a time (one ballot and a lane's mbcnt per bit).
@@ -102,7 +129,7 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
                                                   const uint8_t* __restrict__ fse, const tamd_lz_msg m,
                                                   const uint8_t* __restrict__ buf, uint32_t mask,
                                                   uint8_t* __restrict__ scratch, uint8_t* __restrict__ out,
-                                                  uint32_t* __restrict__ written, uint32_t mi, uint32_t lane,
+                                                  uint32_t* __restrict__ written, uint32_t mi, uint32_t lane, uint32_t& jb,
                                                   unsigned long long* ph, unsigned long long& t_ph, bool prof) {
 #define LZ_PHASE(k)                                                          \
     if (prof) {                                                              \
@@ -112,30 +139,30 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
     }
     const uint32_t n = m.len;
     const uint32_t S = BIG ? tamd_lz_big_seqs(n) : LZ_MAX_SEQS;
-    uint32_t *seq_lo, *seq_off, *code, *bitw;
+    uint32_t *seq_lo, *seq_off, *bitw;
     uint16_t* upd;
-    typedef typename std::conditional<BIG, uint32_t, uint16_t>::type pos_t;
-    pos_t* seq_pos;
     uint32_t bw_cap;  // bit-stream words
     if constexpr (BIG) {
         uint32_t* w = (uint32_t*)(scratch + m.scratch);
         seq_lo = w;
         seq_off = w + S;
-        seq_pos = w + 2 * S;
-        code = w + 3 * S;
-        bitw = w + 4 * S;
+        bitw = w + 2 * S;
         bw_cap = (n + 64u) / 4u;
         upd = (uint16_t*)(bitw + bw_cap + 4u);
     } else {
         seq_lo = L.seq_lo;
         seq_off = L.seq_off;
-        seq_pos = L.seq_pos;
-        code = L.mword;                        // (free after the parse)
-        upd = (uint16_t*)(L.mword + LZ_MAX_SEQS);
+        upd = (uint16_t*)L.mword;  // (free after the parse)
         bitw = L.bitw;
         bw_cap = (TAMD_LZ_MAX_MESSAGE + 64u) / 4u;
     }
     const uint8_t* mb = L.mbuf;
+    // the literal-length, match-length and offset codes of sequence sq (bytes 0, 1, 2)
+    auto seq_code = [&](uint32_t sq) -> uint32_t {
+        const uint32_t lo = seq_lo[sq];
+        return tamd_ll_code(lo & 0xffffu) | (tamd_ml_code(lo >> 16) << 8) |
+               ((31u - (uint32_t)__builtin_clz(seq_off[sq] + 3u)) << 16);
+    };
     // the message's bytes at offset i (LDS copy, or the stream buffer for BIG messages)
     auto msg_dword = [&](uint32_t i) -> uint64_t {
         if constexpr (BIG) return lz_dword(buf, mask, m.pos + i);
@@ -161,9 +188,12 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
     // window moves only when p leaves it.  Sequences collect in registers (lane j keeps sequence
     // j of each group of 64) and are stored a group at a time.
     uint32_t p = 0, lit_start = 0, nseq = 0, lits = 0;
-    uint32_t my_lo = 0, my_off = 0, my_pos = 0;
+    uint32_t my_lo = 0, my_off = 0;
     for (uint32_t c0 = 0; c0 < n; c0 += LZ_CH) {
         const uint32_t cend = n - c0 < LZ_CH ? n : c0 + LZ_CH;
+        // (the chunk's positions must fit the table: a job past 64 KB moves its base up to the
+        // last TAMD_LZ_WINDOW bytes before the chunk)
+        if (m.pos + cend - jb >= LZ_REL_MAX) lz_rebase(L.htab, jb, m.pos + c0 - TAMD_LZ_WINDOW, lane);
         for (uint32_t c = c0; c < cend; c += 64) {
             const uint32_t i = c + lane;
             uint32_t len = 0, src = 0;
@@ -171,7 +201,7 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
                 const uint32_t pp = m.pos + i;
                 const uint32_t e = L.htab[lz_hash(msg_dword(i))];
                 if (e) {
-                    src = e - 1;
+                    src = jb + e - 1;
                     if (src >= m.win && src < pp) {
                         const uint32_t lim = n - i < LZ_PROBE ? n - i : LZ_PROBE;
                         // the probe's loads all go out together
@@ -190,7 +220,10 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
             }
             if (i < cend) L.mword[i - c0] = len ? len | ((m.pos + i - src) << 16) : 0u;
             LZ_SYNC();
-            if (i + 3 < n && i < cend) atomicMax(&L.htab[lz_hash(msg_dword(i))], m.pos + i + 1);
+            const bool ins = i + 3 < n && i < cend;
+            uint32_t h = 0;
+            if (ins) h = lz_hash(msg_dword(i));
+            lz_insert(L.htab, ins, h, m.pos + i + 1 - jb);
             LZ_SYNC();
         }
         LZ_PHASE(1)
@@ -236,14 +269,12 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
                 if (lane == (nseq & 63u)) {
                     my_lo = (at - lit_start) | (ml << 16);
                     my_off = dist;
-                    my_pos = lit_start;
                 }
                 lits += at - lit_start;
                 ++nseq;
                 if ((nseq & 63u) == 0) {
                     seq_lo[nseq - 64 + lane] = my_lo;
                     seq_off[nseq - 64 + lane] = my_off;
-                    seq_pos[nseq - 64 + lane] = (pos_t)my_pos;
                 }
                 p = __builtin_amdgcn_readfirstlane(at + ml);
                 lit_start = p;
@@ -261,7 +292,6 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
         const uint32_t g = nseq & ~63u;
         seq_lo[g + lane] = my_lo;
         seq_off[g + lane] = my_off;
-        seq_pos[g + lane] = (pos_t)my_pos;
     }
     const uint32_t last_lits = n - lit_start;  // literals after the last sequence
     lits += last_lits;
@@ -287,9 +317,7 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
         if (lane < 3u) L.fstarts[lane] = 0;
         LZ_SYNC();
         for (uint32_t sq = lane; sq < nseq; sq += 64) {
-            const uint32_t cd = tamd_ll_code(seq_lo[sq] & 0xffffu) | (tamd_ml_code(seq_lo[sq] >> 16) << 8) |
-                                ((31u - (uint32_t)__builtin_clz(seq_off[sq] + 3u)) << 16);
-            code[sq] = cd;
+            const uint32_t cd = seq_code(sq);
             atomicAdd(&hist[cd & 0xffu], 1u);
             atomicAdd(&hist[64u + ((cd >> 8) & 0xffu)], 1u);
             atomicAdd(&hist[128u + (cd >> 16)], 1u);
@@ -417,34 +445,33 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
     }
     LZ_PHASE(5)
     if (ok) {
-        if (mode[0] == TAMD_MODE_FSE || mode[1] == TAMD_MODE_FSE || mode[2] == TAMD_MODE_FSE) {
-            // the fitted tables' share | offset << 6 | step bits << 11 of every sequence's code, in
-            // its update slot
-            for (uint32_t sq = lane; sq + 1u < nseq; sq += 64) {
-                const uint32_t cd = code[sq];
+        // every sequence's code in its update slot of each table's chain: for a predefined table the
+        // code itself, for a fitted one its share | offset << 6 | step bits << 11
+        for (uint32_t sq = lane; sq < nseq; sq += 64) {
+            const uint32_t cd = seq_code(sq);
 #pragma unroll
-                for (uint32_t t = 0; t < 3; ++t)
-                    if (mode[t] == TAMD_MODE_FSE) {
-                        const uint32_t c = (cd >> (8u * t)) & 0xffu;
-                        const uint32_t nn = L.fnorm[t][c];
-                        upd[S * t + sq] = (uint16_t)(nn | (uint32_t)L.fcum[t][c] << 6 | tamd_fit_mbo(nn) << 11);
-                    }
+            for (uint32_t t = 0; t < 3; ++t) {
+                const uint32_t c = (cd >> (8u * t)) & 0xffu;
+                if (mode[t] == TAMD_MODE_FSE) {
+                    const uint32_t nn = L.fnorm[t][c];
+                    upd[S * t + sq] = (uint16_t)(nn | (uint32_t)L.fcum[t][c] << 6 | tamd_fit_mbo(nn) << 11);
+                } else if (mode[t] == TAMD_MODE_PREDEF) {
+                    upd[S * t + sq] = (uint16_t)c;
+                }
             }
-            LZ_SYNC();
         }
+        LZ_SYNC();
         if (lane < 3) {
-            const uint32_t shift = 8u * lane, size = lane == 2 ? 32u : 64u;
+            const uint32_t size = lane == 2 ? 32u : 64u;
             const uint32_t md = lane == 0 ? mode[0] : lane == 1 ? mode[1] : mode[2];
             const uint16_t* enc = e16 + (lane == 0 ? TAMD_FSE_LL_E16 : lane == 1 ? TAMD_FSE_ML_E16 : TAMD_FSE_OF_E16);
             uint16_t* u_out = upd + S * lane;
             uint32_t st = 0;
             if (md == TAMD_MODE_FSE) {
-                const uint8_t* nm = L.fnorm[lane];
-                const uint8_t* cm = L.fcum[lane];
                 const uint8_t* sv = L.fstate[lane];
                 uint32_t u;
-                const uint32_t c = (code[nseq - 1] >> shift) & 0xffu;
-                st = tamd_fit_step(nm[c], cm[c], sv, 0, &u);
+                const uint32_t inf0 = u_out[nseq - 1];
+                st = tamd_fit_step_m(inf0 & 63u, (inf0 >> 6) & 31u, inf0 >> 11, sv, 0, &u);
                 // (each step's symbol share and offset were put in its update slot beforehand: the
                 // only load that waits for the previous step is the state's)
 #pragma unroll 4
@@ -454,9 +481,9 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
                     u_out[sq] = (uint16_t)u;
                 }
             } else if (md == TAMD_MODE_PREDEF) {
-                st = enc[((code[nseq - 1] >> shift) & 0xffu) * size] & 63u;
+                st = enc[u_out[nseq - 1] * size] & 63u;
                 for (uint32_t sq = nseq - 1; sq-- > 0;) {
-                    const uint32_t e = enc[((code[sq] >> shift) & 0xffu) * size + st];
+                    const uint32_t e = enc[u_out[sq] * size + st];
                     u_out[sq] = (uint16_t)((e >> 10) | (((e >> 6) & 15u) << 8));
                     st = e & 63u;
                 }
@@ -476,7 +503,7 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
             uint32_t nbits = 0;
             if (r < nseq) {
                 const uint32_t sq = nseq - 1u - r;
-                const uint32_t cd = code[sq], llc = cd & 0xffu, mlc = (cd >> 8) & 0xffu, ofc = cd >> 16;
+                const uint32_t cd = seq_code(sq), llc = cd & 0xffu, mlc = (cd >> 8) & 0xffu, ofc = cd >> 16;
                 auto put = [&](uint32_t val, uint32_t nb) {
                     v |= (uint64_t)(val & ((1u << nb) - 1u)) << nbits;
                     nbits += nb;
@@ -539,27 +566,32 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
         uint32_t w = lh;
         if (lane < w) o[lane] = (uint8_t)(lits_word >> (8u * lane));
         // literals: lane j copies the literal run of sequences j, j + 64, ... (and the final run)
-        // to its place, found by a wave prefix sum of the run lengths
-        uint32_t carry = 0;
+        // to its place, found by a wave prefix sum of the run lengths; where it starts in the
+        // message, by a prefix sum of the sequences' spans (literals + match)
+        uint32_t carry = 0, mcarry = 0;
         for (uint32_t base = 0; base <= nseq; base += 64) {
             const uint32_t sq = base + lane;
-            uint32_t ll = 0, from = 0;
+            uint32_t ll = 0, span = 0;
             if (sq < nseq) {
-                ll = seq_lo[sq] & 0xffffu;
-                from = seq_pos[sq];
+                const uint32_t lo = seq_lo[sq];
+                ll = lo & 0xffffu;
+                span = ll + (lo >> 16);
             } else if (sq == nseq) {
                 ll = last_lits;
-                from = n - last_lits;
             }
-            uint32_t x = ll;
+            uint32_t x = ll, y = span;
 #pragma unroll
             for (uint32_t d = 1; d < 64; d <<= 1) {
-                const uint32_t y = __shfl_up(x, d);
-                if (lane >= d) x += y;
+                const uint32_t xu = __shfl_up(x, d), yu = __shfl_up(y, d);
+                if (lane >= d) {
+                    x += xu;
+                    y += yu;
+                }
             }
-            const uint32_t at = w + carry + x - ll;
+            const uint32_t at = w + carry + x - ll, from = mcarry + y - span;
             for (uint32_t k = 0; k < ll; ++k) o[at + k] = msg_byte(from + k);
             carry += __shfl(x, 63);
+            mcarry += __shfl(y, 63);
         }
         w += lits;
         const uint32_t hs = shb;
@@ -603,6 +635,7 @@ tamd_lz_compress(const tamd_lz_job* __restrict__ jobs, uint32_t n_jobs, const ta
     unsigned long long ph[TAMD_LZ_PHASES] = {0, 0, 0, 0, 0, 0, 0, 0}, t_ph = prof ? __builtin_amdgcn_s_memrealtime() : 0;
     const uint8_t* __restrict__ buf = job.buf;
     const uint32_t mask = job.mask;
+    uint32_t jb = 0;  // the job's base position: table entries are relative to it
     for (uint32_t i = lane; i < LZ_HASH; i += 64) L.htab[i] = 0;
     LZ_SYNC();
 
@@ -611,23 +644,46 @@ tamd_lz_compress(const tamd_lz_job* __restrict__ jobs, uint32_t n_jobs, const ta
         const tamd_lz_msg m0 = msgs[job.first];
         uint32_t w0 = m0.win;
         if (m0.pos - w0 > TAMD_LZ_WINDOW) w0 = m0.pos - TAMD_LZ_WINDOW;
-        // 16 consecutive positions per lane: 24 bytes loaded once, 16 keys from registers
+        jb = w0;
+#if LZ_WINDOW_LANE16
+        // 16 consecutive positions per lane: 24 bytes loaded once, 16 keys from registers (one
+        // load per 64 positions, per lane, made the window phase 3x longer); inside a block of 1024
+        // positions a bucket may keep an older one of its positions
         for (uint32_t q = w0; q < m0.pos; q += 1024) {
             const uint32_t p0 = q + 16u * lane;
+            uint64_t a = 0, b = 0, c = 0;
             if (p0 < m0.pos) {
-                const uint64_t a = lz_dword(buf, mask, p0), b = lz_dword(buf, mask, p0 + 8),
-                               c = lz_dword(buf, mask, p0 + 16);
+                a = lz_dword(buf, mask, p0);
+                b = lz_dword(buf, mask, p0 + 8);
+                c = lz_dword(buf, mask, p0 + 16);
+            }
 #pragma unroll
-                for (uint32_t k = 0; k < 16; ++k) {
-                    uint64_t w;
-                    if (k == 0) w = a;
-                    else if (k < 8) w = (a >> (8 * k)) | (b << (64 - 8 * k));
-                    else if (k == 8) w = b;
-                    else w = (b >> (8 * (k - 8))) | (c << (64 - 8 * (k - 8)));
-                    if (p0 + k < m0.pos) atomicMax(&L.htab[lz_hash(w)], p0 + k + 1);
-                }
+            for (uint32_t k = 0; k < 16; ++k) {
+                uint64_t w;
+                if (k == 0) w = a;
+                else if (k < 8) w = (a >> (8 * k)) | (b << (64 - 8 * k));
+                else if (k == 8) w = b;
+                else w = (b >> (8 * (k - 8))) | (c << (64 - 8 * (k - 8)));
+                lz_insert(L.htab, p0 + k < m0.pos, lz_hash(w), p0 + k + 1 - jb);
             }
         }
+#else
+        // 64 consecutive positions per store (in increasing order), the keys of eight stores
+        // loaded at once
+        for (uint32_t q = w0; q < m0.pos; q += 512) {
+            uint64_t w[8];
+#pragma unroll
+            for (uint32_t k = 0; k < 8; ++k) {
+                const uint32_t p = q + 64u * k + lane;
+                w[k] = p < m0.pos ? lz_dword(buf, mask, p) : 0ull;
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < 8; ++k) {
+                const uint32_t p = q + 64u * k + lane;
+                lz_insert(L.htab, p < m0.pos, lz_hash(w[k]), p + 1 - jb);
+            }
+        }
+#endif
         LZ_SYNC();
     }
     if (prof) {
@@ -644,14 +700,18 @@ tamd_lz_compress(const tamd_lz_job* __restrict__ jobs, uint32_t n_jobs, const ta
             // (outside the kernel's bounds: stored uncompressed; its positions still enter the table)
             if (lane == 0) written[mi] = 0;
             for (uint32_t q = m.pos; q + 3 < m.pos + n; q += 64) {
+                if (q + 64u - jb >= LZ_REL_MAX) lz_rebase(L.htab, jb, q - TAMD_LZ_WINDOW, lane);
                 const uint32_t pp = q + lane;
-                if (pp + 3 < m.pos + n) atomicMax(&L.htab[lz_hash(lz_dword(buf, mask, pp))], pp + 1);
+                const bool ins = pp + 3 < m.pos + n;
+                uint32_t h = 0;
+                if (ins) h = lz_hash(lz_dword(buf, mask, pp));
+                lz_insert(L.htab, ins, h, pp + 1 - jb);
             }
             LZ_SYNC();
             continue;
         }
-        if (big) lz_message<true>(L, e16, fse, m, buf, mask, scratch, out, written, mi, lane, ph, t_ph, prof != nullptr);
-        else lz_message<false>(L, e16, fse, m, buf, mask, scratch, out, written, mi, lane, ph, t_ph, prof != nullptr);
+        if (big) lz_message<true>(L, e16, fse, m, buf, mask, scratch, out, written, mi, lane, jb, ph, t_ph, prof != nullptr);
+        else lz_message<false>(L, e16, fse, m, buf, mask, scratch, out, written, mi, lane, jb, ph, t_ph, prof != nullptr);
     }
     if (prof && lane == 0)
 #pragma unroll
