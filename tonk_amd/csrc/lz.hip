@@ -28,7 +28,13 @@
 #ifndef LZ_WINDOW_LANE16
 #define LZ_WINDOW_LANE16 1
 #endif
-#define LZ_REL_MAX 65535u  // job-relative positions (+ 1) the table can hold
+#define LZ_REL_MAX 65535u
+#ifndef LZ_NO_EXTEND
+#define LZ_NO_EXTEND 0  // (measurement only: matches stop at the probe's LZ_PROBE bytes)
+#endif
+#ifndef LZ_PROBE_BATCH
+#define LZ_PROBE_BATCH 3u  // groups of 64 positions whose candidate loads go out together
+#endif  // job-relative positions (+ 1) the table can hold
 #define LZ_HASH (1u << LZ_HASH_LOG)
 #define LZ_MIN_MATCH 4u
 #ifndef LZ_PROBE
@@ -194,38 +200,52 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
         // (the chunk's positions must fit the table: a job past 64 KB moves its base up to the
         // last TAMD_LZ_WINDOW bytes before the chunk)
         if (m.pos + cend - jb >= LZ_REL_MAX) lz_rebase(L.htab, jb, m.pos + c0 - TAMD_LZ_WINDOW, lane);
-        for (uint32_t c = c0; c < cend; c += 64) {
-            const uint32_t i = c + lane;
-            uint32_t len = 0, src = 0;
-            if (i + LZ_MIN_MATCH <= n) {
-                const uint32_t pp = m.pos + i;
-                const uint32_t e = L.htab[lz_hash(msg_dword(i))];
-                if (e) {
-                    src = jb + e - 1;
-                    if (src >= m.win && src < pp) {
-                        const uint32_t lim = n - i < LZ_PROBE ? n - i : LZ_PROBE;
-                        // the probe's loads all go out together
-                        uint64_t xs[LZ_PROBE / 8];
+        // LZ_PROBE_BATCH groups of 64 positions at a time: the table is read and written group
+        // after group in LDS order (group g's lookups see groups < g, not g itself), and only then
+        // do the candidates' loads go out, every group's together.  Lanes without a candidate load
+        // from the message start and drop the result (no exec-masked loads).
+        for (uint32_t c = c0; c < cend; c += 64u * LZ_PROBE_BATCH) {
+            uint64_t key[LZ_PROBE_BATCH];
 #pragma unroll
-                        for (uint32_t k = 0; k < LZ_PROBE / 8; ++k)  // (no load past the message)
-                            xs[k] = 8 * k < lim ? lz_dword(buf, mask, src + 8 * k) ^ msg_dword(i + 8 * k) : 0ull;
-                        len = LZ_PROBE;
-#pragma unroll
-                        for (uint32_t k = LZ_PROBE / 8; k-- > 0;)
-                            if (xs[k]) len = 8 * k + ((uint32_t)__builtin_ctzll(xs[k]) >> 3);
-                        if (len > lim) len = lim;
-                        if (len < LZ_MIN_MATCH) len = 0;
-                    }
-                }
+            for (uint32_t b = 0; b < LZ_PROBE_BATCH; ++b) {
+                const uint32_t i = c + 64u * b + lane;
+                key[b] = 0;
+                if (i < cend && i + LZ_MIN_MATCH <= n) key[b] = msg_dword(i);
             }
-            if (i < cend) L.mword[i - c0] = len ? len | ((m.pos + i - src) << 16) : 0u;
-            LZ_SYNC();
-            const bool ins = i + 3 < n && i < cend;
-            uint32_t h = 0;
-            if (ins) h = lz_hash(msg_dword(i));
-            lz_insert(L.htab, ins, h, m.pos + i + 1 - jb);
-            LZ_SYNC();
+            uint32_t src[LZ_PROBE_BATCH];
+#pragma unroll
+            for (uint32_t b = 0; b < LZ_PROBE_BATCH; ++b) {
+                const uint32_t i = c + 64u * b + lane;
+                const bool look = i < cend && i + LZ_MIN_MATCH <= n;  // (= i + 3 < n: inserted too)
+                const uint32_t h = lz_hash(key[b]);
+                uint32_t e = 0;
+                if (look) e = L.htab[h];
+                lz_insert(L.htab, look, h, m.pos + i + 1 - jb);
+                src[b] = e ? jb + e - 1 : 0u;
+            }
+#pragma unroll
+            for (uint32_t b = 0; b < LZ_PROBE_BATCH; ++b) {
+                const uint32_t i = c + 64u * b + lane;
+                const bool cand = i < cend && i + LZ_MIN_MATCH <= n && src[b] && src[b] >= m.win && src[b] < m.pos + i;
+                const uint32_t lim = cand ? (n - i < LZ_PROBE ? n - i : LZ_PROBE) : 0u;
+                const uint32_t s0 = cand ? src[b] : m.pos;
+                uint64_t xs[LZ_PROBE / 8];
+#pragma unroll
+                for (uint32_t k = 0; k < LZ_PROBE / 8; ++k) {  // (no load past the message)
+                    const bool in = 8 * k < lim;
+                    xs[k] = lz_dword(buf, mask, s0 + (in ? 8 * k : 0u)) ^ msg_dword(in ? i + 8 * k : 0u);
+                    if (!in) xs[k] = 0;
+                }
+                uint32_t len = LZ_PROBE;
+#pragma unroll
+                for (uint32_t k = LZ_PROBE / 8; k-- > 0;)
+                    if (xs[k]) len = 8 * k + ((uint32_t)__builtin_ctzll(xs[k]) >> 3);
+                if (len > lim) len = lim;
+                if (len < LZ_MIN_MATCH) len = 0;
+                if (i < cend) L.mword[i - c0] = len ? len | ((m.pos + i - src[b]) << 16) : 0u;
+            }
         }
+        LZ_SYNC();
         LZ_PHASE(1)
         if (p < cend) {
             uint32_t wb = p > c0 ? p : c0;  // (positions in [p, c0) were scanned with the last chunk)
@@ -244,7 +264,7 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
                 const uint32_t word = (uint32_t)__builtin_amdgcn_readlane((int)mine, (int)first);
                 const uint32_t dist = word >> 16;
                 uint32_t ml = word & 0xffffu;
-                if (ml == LZ_PROBE && at + ml < n) {
+                if (!LZ_NO_EXTEND && ml == LZ_PROBE && at + ml < n) {
                     // the probe matched in full: the wave extends the match 512 bytes per step
                     const uint32_t q = m.pos + at;
                     for (;;) {
