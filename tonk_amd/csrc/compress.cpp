@@ -495,7 +495,8 @@ extern "C" int tamd_compress_batch(const void* dev_data, uint64_t stride, uint32
             for (uint32_t k = 0; k < TAMD_LZ_PHASES; ++k) t[k] += (double)h[TAMD_LZ_PHASES * j + k];
         const double q = 100.0 * (double)jobs.size();
         fprintf(stderr, "lz phases (us per job): window %.1f probe %.1f parse %.1f codes+tables %.1f chains %.1f "
-                "stream %.1f out %.1f\n", t[0] / q, t[1] / q, t[2] / q, t[5] / q, t[6] / q, t[3] / q, t[4] / q);
+                "stream %.1f out %.1f; sequences per job %.1f\n", t[0] / q, t[1] / q, t[2] / q, t[5] / q, t[6] / q,
+                t[3] / q, t[4] / q, t[7] / (double)jobs.size());
         hipFree(d_prof);
     }
     ok = ok && hipMemcpyAsync(written_host, d_written, total * 4, hipMemcpyDeviceToHost, st) == hipSuccess;

@@ -250,13 +250,18 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
         if (p < cend) {
             uint32_t wb = p > c0 ? p : c0;  // (positions in [p, c0) were scanned with the last chunk)
             uint32_t mine = wb + lane < cend ? L.mword[wb + lane - c0] : 0u;
+            // the window's positions with a match, once per window: a step only masks off the
+            // positions below p (scalar work)
+            uint64_t mm = __ballot((mine & 0xffffu) != 0);
             for (;;) {
-                const uint64_t b = __ballot((mine & 0xffffu) != 0 && wb + lane >= p);
+                const uint32_t sh = p > wb ? p - wb : 0u;
+                const uint64_t b = sh < 64u ? mm & (~0ull << sh) : 0ull;
                 if (!b) {
                     wb = __builtin_amdgcn_readfirstlane(wb + 64);
                     if (wb >= cend) break;
                     if (p < wb) p = wb;
                     mine = wb + lane < cend ? L.mword[wb + lane - c0] : 0u;
+                    mm = __ballot((mine & 0xffffu) != 0);
                     continue;
                 }
                 const uint32_t first = (uint32_t)__builtin_ctzll(b);
@@ -286,10 +291,9 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
                     if (ml > n - at) ml = n - at;
                     ml = __builtin_amdgcn_readfirstlane(ml);
                 }
-                if (lane == (nseq & 63u)) {
-                    my_lo = (at - lit_start) | (ml << 16);
-                    my_off = dist;
-                }
+                const bool slot = lane == (nseq & 63u);  // (selects, no branch)
+                my_lo = slot ? (at - lit_start) | (ml << 16) : my_lo;
+                my_off = slot ? dist : my_off;
                 lits += at - lit_start;
                 ++nseq;
                 if ((nseq & 63u) == 0) {
@@ -302,6 +306,7 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
                 if (p >= wb + 64) {
                     wb = p;
                     mine = wb + lane < cend ? L.mword[wb + lane - c0] : 0u;
+                    mm = __ballot((mine & 0xffffu) != 0);
                 }
             }
         }
@@ -313,6 +318,7 @@ static __device__ __forceinline__ void lz_message(LzWave& L, const uint16_t* __r
         seq_lo[g + lane] = my_lo;
         seq_off[g + lane] = my_off;
     }
+    if (prof) ph[7] += nseq;  // (profiling: sequences, not ticks)
     const uint32_t last_lits = n - lit_start;  // literals after the last sequence
     lits += last_lits;
     LZ_SYNC();
