@@ -103,7 +103,7 @@ static __device__ __forceinline__ void lz_insert(uint16_t* htab, bool ins, uint3
 
 // Moves the job's base forward to `to` (> base): entries keep their positions, the ones before
 // `to` become empty.  Only jobs that span more than LZ_REL_MAX bytes (large messages) need it.
-static __device__ __noinline__ void lz_rebase(uint16_t* htab, uint32_t& base, uint32_t to, uint32_t lane) {
+static __device__ __forceinline__ void lz_rebase(uint16_t* htab, uint32_t& base, uint32_t to, uint32_t lane) {
     const uint32_t d = to - base;
     for (uint32_t k = lane; k < LZ_HASH; k += 64) {
         const uint32_t e = htab[k];
