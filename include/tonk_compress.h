@@ -37,7 +37,7 @@ void  tamd_compressor_destroy(void* c);
    empty) and applies MessageCompressor's Allocate(max)/Commit ring rule.  Outputs: message
    (s, k) compressed at dev_out + (s * n_msgs + k) * max_bytes, written_host[s * n_msgs + k]
    (0: send uncompressed).  msgs_per_job consecutive messages of a stream share one wave's hash
-   table.  *kernel_ms (optional) = the compression kernel's duration.  Returns 0 or negative. */
+   table (0: chosen so that the jobs fill the device's wave slots once).  *kernel_ms (optional) = the compression kernel's duration.  Returns 0 or negative. */
 int   tamd_compress_batch(const void* dev_data, uint64_t stride, uint32_t n_streams, uint32_t n_msgs,
                           const uint32_t* lens, uint32_t max_bytes, void* dev_out, uint32_t* written_host,
                           uint32_t msgs_per_job, float* kernel_ms);

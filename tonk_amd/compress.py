@@ -64,7 +64,7 @@ class MessageCompressor:
 
 
 def compress_batch(dev_data: int, stride: int, n_streams: int, n_msgs: int, lens, max_bytes: int, dev_out: int,
-                   msgs_per_job: int = 16):
+                   msgs_per_job: int = 0):
     """Compress every message of `n_streams` fresh streams (device pointers from the caller, e.g.
     torch tensors' data_ptr()).  `lens`: uint32 per message (any sequence; a contiguous numpy
     uint32 array is passed without a copy).  Returns (written bytes per message as a numpy array,
@@ -83,7 +83,7 @@ def compress_batch(dev_data: int, stride: int, n_streams: int, n_msgs: int, lens
 
 
 def compress_batch_host(data, stride: int, n_streams: int, n_msgs: int, lens, max_bytes: int,
-                        msgs_per_job: int = 16) -> tuple[bytes, list[int], float]:
+                        msgs_per_job: int = 0) -> tuple[bytes, list[int], float]:
     """compress_batch from a host buffer (bytes-like of n_streams * stride): returns (the output
     slots, max_bytes per message; written per message; kernel ms)."""
     total = n_streams * n_msgs

@@ -388,10 +388,18 @@ extern "C" int tamd_compress_batch(const void* dev_data, uint64_t stride, uint32
         max_bytes > kDictBytes)
         return -1;
     if (stride > 0xffffffffull) return -1;  // linear positions are 32-bit per stream
-    if (!msgs_per_job) msgs_per_job = 16;
     int dev = 0;
     if (!device_ok()) return -3;
     hipGetDevice(&dev);
+    if (!msgs_per_job) {
+        // auto: the fewest messages per job that keep every stream's jobs within one job per wave
+        // slot (CUs x TAMD_LZ_WAVES): one round of jobs, each seeding its window once
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+        const uint32_t slots = (uint32_t)cus * TAMD_LZ_WAVES;
+        const uint32_t per_stream = slots / n_streams ? slots / n_streams : 1u;
+        msgs_per_job = (n_msgs + per_stream - 1) / per_stream;
+    }
     const uint8_t* fse = device_fse(dev);
     if (!fse) return -3;
     const uint64_t total = (uint64_t)n_streams * n_msgs;
