@@ -285,9 +285,12 @@ def test_gpu_compressor_edge_cases(max_bytes):
 
 
 @pytest.mark.gpu
-def test_gpu_compress_batch_large_messages():
+@pytest.mark.parametrize("per_job", [4, 0])
+def test_gpu_compress_batch_large_messages(per_job):
     """The batch API with messages of 64 B .. 24,000 B (the history size) mixed in one launch:
-    the large ones go through global scratch; every stream restored by the reference."""
+    the large ones go through global scratch, jobs longer than 64 KB move their hash table's base;
+    per_job 0: the library's job size (one round of jobs over the wave slots: here one message
+    per job); every stream restored by the reference."""
     from tonk_amd.compress import compress_batch_host
     L = ref_lib()
     max_bytes, n_streams, n_msgs = 24000, 4, 24
@@ -311,7 +314,7 @@ def test_gpu_compress_batch_large_messages():
         blob = b"".join(ms)
         host[s, :len(blob)] = np.frombuffer(blob, dtype=np.uint8)
         lens += [len(m) for m in ms]
-    raw, written, _ = compress_batch_host(host.tobytes(), stride, n_streams, n_msgs, lens, max_bytes, msgs_per_job=4)
+    raw, written, _ = compress_batch_host(host.tobytes(), stride, n_streams, n_msgs, lens, max_bytes, msgs_per_job=per_job)
     out_h = np.frombuffer(raw, dtype=np.uint8)
     big = 0
     for s, msgs in enumerate(streams):
