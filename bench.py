@@ -78,9 +78,12 @@ import tonk_amd  # noqa: E402
 METRIC = "Siamese FEC encode+decode GiB/s (device-resident), 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0
 STREAMS_PER_GPU = 64
-ORIGINALS_PER_STEP = int(os.environ.get("TONK_AMD_BENCH_PROGRAM", 4096))  # per stream per device program
+ORIGINALS_PER_STEP = int(os.environ.get("TONK_AMD_BENCH_PROGRAM", 8192))  # per stream per device program
                                                                             # (tamd_session_step; env: A/B)
-# A bench step: 16 programs, 65536 originals per stream (round 5; 4 before): the driver's
+# (8192 since late round 6, 4096 before: the same host work per original, and launches twice as
+# long drain relatively less -- frac 0.594 -> 0.635 at the same GiB/s, profiles/r06v_program_size.txt)
+SINGLE_PROGRAM = 4096  # cfg1 / cfg4 (profiles/r06_single_step_sweep.txt)
+# A bench step: 8 programs, 65536 originals per stream (round 5: 16 of 4096; 4 before): the driver's
 # `--steps 20` then times ~110 ms instead of ~28 ms.  The inputs are a pool of INPUT_POOL rows per
 # side per stream that original i reads as row i mod INPUT_POOL (tonk_amd.h input_pool).
 PROGRAMS_PER_STEP = 65536 // ORIGINALS_PER_STEP
@@ -323,7 +326,7 @@ BATCHED = {
     # BASELINE.json configs[3] (the headline): 512 streams sharded 64/GPU, 1% loss
     "cfg3": dict(loss=0.01),
     # BASELINE.json configs[2]: 64 streams x 4096 originals, 2% loss, batched on one GPU
-    # (4096 originals per stream per step)
+    # (the headline's schedule: programs of ORIGINALS_PER_STEP originals per stream)
     "cfg2": dict(loss=0.02),
 }
 
@@ -702,7 +705,7 @@ def main() -> int:
                     help="BASELINE.json configs[] index: cfg3 (the headline, 64 streams per GPU), cfg2 (64 "
                          "streams, 2%% loss), cfg1 / cfg4 (one stream, start to finish)")
     ap.add_argument("--step", type=int, default=0,
-                    help="cfg1 / cfg4: originals per device program (default ORIGINALS_PER_STEP, 4096: the best of the 256..4096 sweep in profiles/r06_single_step_sweep.txt for both)")
+                    help="cfg1 / cfg4: originals per device program (default SINGLE_PROGRAM, 4096: the best of the 256..4096 sweep in profiles/r06_single_step_sweep.txt for both)")
     ap.add_argument("--dry-run", action="store_true",
                     help="form the ranks and print the shard plan without touching a GPU (tests)")
     a = ap.parse_args()
@@ -745,7 +748,7 @@ def main() -> int:
         if world > 1:
             print("bench.py: single-stream workloads run on one GPU (replicas only)", file=sys.stderr)
             return 2
-        step = a.step or ORIGINALS_PER_STEP
+        step = a.step or SINGLE_PROGRAM
         print(json.dumps(single_stream(a.workload, local_rank, step)), flush=True)
         return 0
 
